@@ -1,0 +1,564 @@
+/*
+ * nk_oracle.c -- TEST INFRASTRUCTURE ONLY (the parity oracle and the CPU baseline).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this
+ * library, and only as the checker / the timed CPU comparison.  The product path
+ * (newtonkrylov.jl_amd/, libnkhip.so) never links, loads or falls back to it.
+ *
+ * What it is: a plain-C (OpenMP) restatement of the reference's hot path
+ *   - Ariadne's inexact Newton driver       src/Ariadne.jl:288-372
+ *   - Eisenstat-Walker / Fixed forcing       src/Ariadne.jl:185-217
+ *   - the exact Jacobian-vector product      src/Ariadne.jl:48-57 (Enzyme Forward; here the
+ *     hand-derived tangent of each residual), plus the FD operator of BASELINE.json's north star
+ *   - Krylov.jl 0.10 gmres!/cg! (third-party, NOT present in /root/reference; pinned only by
+ *     compat "0.10.1" in Project.toml:8,14 -- restated from its published algorithm, see
+ *     SURVEY.md Appendix A.  Iterates and iteration counts are therefore "parity unpinned"
+ *     against the reference; tests pin this oracle with the reference's own known answers
+ *     (test/runtests.jl) and with independent numpy/scipy goldens in tests/golden/.)
+ *   - residuals: 1D Bratu examples/bratu.jl:14-24, 2D heat + G_Euler!
+ *     examples/heat_2D.jl:28-62 + examples/implicit.jl:8-13, and their build-defined
+ *     generalisations 2D Bratu and 3D heat.
+ *
+ * Layout: dense interior arrays, x fastest: idx = (k*ny + j)*nx + i (the same memory order as
+ * the reference's column-major u[i,j]).  Zero-Dirichlet boundaries are applied by predication
+ * (the reference writes zeros into ghost cells with bc_zero!, heat_2D.jl:28-38).
+ *
+ * Floating point: compiled with -ffp-contract=off so every stencil expression rounds exactly as
+ * written (the reference's evaluation order, Julia does not contract).  BLAS-1 axpy uses fma()
+ * explicitly (OpenBLAS daxpy, which Krylov.jl calls for dense vectors, is FMA based); the device
+ * kernels use the same convention, so elementwise ops agree bit for bit.  Reductions are
+ * deterministic (fixed chunking, independent of the thread count).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <float.h>
+#include <omp.h>
+
+enum { OC_BRATU1D = 1, OC_BRATU2D = 2, OC_HEAT2D_EULER = 3, OC_HEAT3D_EULER = 4 };
+enum { OC_JV_EXACT = 0, OC_JV_FD = 1 };
+enum { OC_FORCING_NONE = 0, OC_FORCING_FIXED = 1, OC_FORCING_EW = 2 };
+enum { OC_ALGO_GMRES = 0, OC_ALGO_CG = 1 };
+
+typedef struct {
+    int32_t kind;
+    int32_t bc;             /* 0 = zero Dirichlet */
+    int64_t nx, ny, nz;
+    double hx, hy, hz;
+    double lambda;          /* Bratu */
+    double a, dt;           /* heat diffusivity and time step */
+    const double* un;       /* heat: u_n (borrowed) */
+} oc_problem;
+
+typedef struct {
+    int32_t memory;         /* Krylov workspace memory (default 20) */
+    int32_t restart;        /* bool */
+    int32_t reorthogonalization;
+    int32_t itmax;          /* 0 => 2n */
+    double atol, rtol;
+} oc_krylov_opts;
+
+typedef struct {
+    int64_t niter;
+    int32_t solved, inconsistent, breakdown, status;
+    int64_t n_matvec;       /* mul!(J) calls incl. restart residuals */
+} oc_krylov_stats;
+
+typedef struct {
+    double tol_rel, tol_abs;
+    int32_t max_niter;
+    int32_t forcing;        /* OC_FORCING_* */
+    double eta_fixed, eta_max, gamma;
+    int32_t algo;           /* OC_ALGO_* */
+    int32_t jv_mode;        /* OC_JV_* */
+    oc_krylov_opts krylov;
+    int32_t rtol_user;      /* krylov_kwargs carries rtol: it wins over the forcing (Ariadne.jl:330-333) */
+} oc_newton_opts;
+
+typedef struct {
+    int64_t outer_iterations, inner_iterations;
+    double n_res;
+    int32_t solved;
+    int64_t n_matvec, n_residual;
+    double tol;
+} oc_newton_stats;
+
+static inline int64_t oc_n(const oc_problem* P) { return P->nx * P->ny * P->nz; }
+
+/* ------------------------------------------------------------------ BLAS-1 (Krylov k* primitives) */
+#define OC_CHUNK 8192
+
+double oc_dot(int64_t n, const double* x, const double* y) {
+    int64_t nch = (n + OC_CHUNK - 1) / OC_CHUNK;
+    double* part = (double*)malloc(sizeof(double) * (size_t)(nch > 0 ? nch : 1));
+#pragma omp parallel for schedule(static)
+    for (int64_t c = 0; c < nch; ++c) {
+        int64_t lo = c * OC_CHUNK, hi = lo + OC_CHUNK < n ? lo + OC_CHUNK : n;
+        double s = 0.0;
+        for (int64_t i = lo; i < hi; ++i) s = fma(x[i], y[i], s);
+        part[c] = s;
+    }
+    double s = 0.0;
+    for (int64_t c = 0; c < nch; ++c) s += part[c];
+    free(part);
+    return s;
+}
+double oc_norm(int64_t n, const double* x) { return sqrt(oc_dot(n, x, x)); }
+
+void oc_axpy(int64_t n, double s, const double* x, double* y) {   /* y += s x      (kaxpy!)  */
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) y[i] = fma(s, x[i], y[i]);
+}
+void oc_axpby(int64_t n, double s, const double* x, double t, double* y) { /* y = s x + t y (kaxpby!) */
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) y[i] = fma(t, y[i], s * x[i]);
+}
+void oc_scal(int64_t n, double s, double* x) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) x[i] = s * x[i];
+}
+void oc_copy(int64_t n, double* y, const double* x) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) y[i] = x[i];
+}
+void oc_fill(int64_t n, double* x, double v) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) x[i] = v;
+}
+void oc_divcopy(int64_t n, double* y, const double* x, double s) { /* y = x / s (kdivcopy!) */
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) y[i] = x[i] / s;
+}
+void oc_ref(int64_t n, double* x, double* y, double c, double s) { /* Givens on vectors (kref!) */
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+        double xi = x[i], yi = y[i];
+        x[i] = c * xi + s * yi;
+        y[i] = s * xi - c * yi;
+    }
+}
+
+/* ------------------------------------------------------------------ residuals */
+/* ((p - 2c) + m) / (h*h): Julia's (u[i+1] - 2u[i] + u[i-1]) / Δx^2 (bratu.jl:19, heat_2D.jl:65) */
+static inline double lap1(double c, double p, double m, double h) { return ((p - 2.0 * c) + m) / (h * h); }
+
+#define AT(arr, i, j, k) ((arr)[((int64_t)(k) * ny + (j)) * nx + (i)])
+
+/* value of w at (i,j,k) with zero Dirichlet outside, where w = u (+ eps*v when v != NULL) */
+static inline double wval(const double* u, const double* v, double eps, int64_t nx, int64_t ny, int64_t nz,
+                          int64_t i, int64_t j, int64_t k) {
+    if (i < 0 || i >= nx || j < 0 || j >= ny || k < 0 || k >= nz) return 0.0;
+    double x = AT(u, i, j, k);
+    if (v) x = x + eps * AT(v, i, j, k);
+    return x;
+}
+
+/* F(w) at one point, w = u + eps*v (v==NULL: w = u) */
+static inline double point_residual(const oc_problem* P, const double* u, const double* v, double eps,
+                                    int64_t i, int64_t j, int64_t k) {
+    const int64_t nx = P->nx, ny = P->ny, nz = P->nz;
+    double c = wval(u, v, eps, nx, ny, nz, i, j, k);
+    switch (P->kind) {
+    case OC_BRATU1D: {
+        double l = wval(u, v, eps, nx, ny, nz, i - 1, j, k), r = wval(u, v, eps, nx, ny, nz, i + 1, j, k);
+        return lap1(c, r, l, P->hx) + P->lambda * exp(c);
+    }
+    case OC_BRATU2D: {
+        double e = wval(u, v, eps, nx, ny, nz, i + 1, j, k), w = wval(u, v, eps, nx, ny, nz, i - 1, j, k);
+        double n = wval(u, v, eps, nx, ny, nz, i, j + 1, k), s = wval(u, v, eps, nx, ny, nz, i, j - 1, k);
+        return (lap1(c, e, w, P->hx) + lap1(c, n, s, P->hy)) + P->lambda * exp(c);
+    }
+    case OC_HEAT2D_EULER: {
+        double e = wval(u, v, eps, nx, ny, nz, i + 1, j, k), w = wval(u, v, eps, nx, ny, nz, i - 1, j, k);
+        double n = wval(u, v, eps, nx, ny, nz, i, j + 1, k), s = wval(u, v, eps, nx, ny, nz, i, j - 1, k);
+        double du = P->a * (lap1(c, e, w, P->hx) + lap1(c, n, s, P->hy));
+        return (AT(P->un, i, j, k) + P->dt * du) - c;
+    }
+    case OC_HEAT3D_EULER: {
+        double e = wval(u, v, eps, nx, ny, nz, i + 1, j, k), w = wval(u, v, eps, nx, ny, nz, i - 1, j, k);
+        double n = wval(u, v, eps, nx, ny, nz, i, j + 1, k), s = wval(u, v, eps, nx, ny, nz, i, j - 1, k);
+        double t = wval(u, v, eps, nx, ny, nz, i, j, k + 1), b = wval(u, v, eps, nx, ny, nz, i, j, k - 1);
+        double du = P->a * ((lap1(c, e, w, P->hx) + lap1(c, n, s, P->hy)) + lap1(c, t, b, P->hz));
+        return (AT(P->un, i, j, k) + P->dt * du) - c;
+    }
+    }
+    return NAN;
+}
+
+void oc_residual(const oc_problem* P, double* res, const double* u) {
+    const int64_t nx = P->nx, ny = P->ny, nz = P->nz;
+#pragma omp parallel for collapse(2) schedule(static)
+    for (int64_t k = 0; k < nz; ++k)
+        for (int64_t j = 0; j < ny; ++j)
+            for (int64_t i = 0; i < nx; ++i) AT(res, i, j, k) = point_residual(P, u, NULL, 0.0, i, j, k);
+}
+
+/* exact JVP: the forward-mode tangent Enzyme computes for each residual (Ariadne.jl:48-57) */
+void oc_jv_exact(const oc_problem* P, double* out, const double* u, const double* v) {
+    const int64_t nx = P->nx, ny = P->ny, nz = P->nz;
+#pragma omp parallel for collapse(2) schedule(static)
+    for (int64_t k = 0; k < nz; ++k)
+        for (int64_t j = 0; j < ny; ++j)
+            for (int64_t i = 0; i < nx; ++i) {
+                double c = AT(v, i, j, k), r;
+                double e = wval(v, NULL, 0, nx, ny, nz, i + 1, j, k), w = wval(v, NULL, 0, nx, ny, nz, i - 1, j, k);
+                switch (P->kind) {
+                case OC_BRATU1D:
+                    r = lap1(c, e, w, P->hx) + P->lambda * (exp(AT(u, i, j, k)) * c);
+                    break;
+                case OC_BRATU2D: {
+                    double n = wval(v, NULL, 0, nx, ny, nz, i, j + 1, k), s = wval(v, NULL, 0, nx, ny, nz, i, j - 1, k);
+                    r = (lap1(c, e, w, P->hx) + lap1(c, n, s, P->hy)) + P->lambda * (exp(AT(u, i, j, k)) * c);
+                    break;
+                }
+                case OC_HEAT2D_EULER: {
+                    double n = wval(v, NULL, 0, nx, ny, nz, i, j + 1, k), s = wval(v, NULL, 0, nx, ny, nz, i, j - 1, k);
+                    r = P->dt * (P->a * (lap1(c, e, w, P->hx) + lap1(c, n, s, P->hy))) - c;
+                    break;
+                }
+                default: {
+                    double n = wval(v, NULL, 0, nx, ny, nz, i, j + 1, k), s = wval(v, NULL, 0, nx, ny, nz, i, j - 1, k);
+                    double t = wval(v, NULL, 0, nx, ny, nz, i, j, k + 1), b = wval(v, NULL, 0, nx, ny, nz, i, j, k - 1);
+                    r = P->dt * (P->a * ((lap1(c, e, w, P->hx) + lap1(c, n, s, P->hy)) + lap1(c, t, b, P->hz))) - c;
+                }
+                }
+                AT(out, i, j, k) = r;
+            }
+}
+
+/* FD JVP (BASELINE.json north star): out = (F(u + eps v) - F0) / eps */
+void oc_jv_fd(const oc_problem* P, double* out, const double* u, const double* v, const double* F0, double eps) {
+    const int64_t nx = P->nx, ny = P->ny, nz = P->nz;
+#pragma omp parallel for collapse(2) schedule(static)
+    for (int64_t k = 0; k < nz; ++k)
+        for (int64_t j = 0; j < ny; ++j)
+            for (int64_t i = 0; i < nx; ++i)
+                AT(out, i, j, k) = (point_residual(P, u, v, eps, i, j, k) - AT(F0, i, j, k)) / eps;
+}
+
+/* eps = sqrt(eps_mach) * max(1, ||u||) / ||v||  (SURVEY.md §6 probe; ||v|| := 1 for Arnoldi basis vectors) */
+double oc_fd_eps(double unorm, double vnorm) { return sqrt(DBL_EPSILON) * fmax(1.0, unorm) / vnorm; }
+
+typedef struct {
+    const oc_problem* P;
+    int mode;
+    const double* u;
+    const double* F0;
+    double unorm;
+    int64_t n_matvec;
+} oc_op;
+
+static void op_apply(oc_op* A, double* out, const double* v, double vnorm) {
+    A->n_matvec++;
+    if (A->mode == OC_JV_EXACT) {
+        oc_jv_exact(A->P, out, A->u, v);
+    } else {
+        if (vnorm < 0) vnorm = oc_norm(oc_n(A->P), v);
+        if (vnorm == 0.0) { oc_fill(oc_n(A->P), out, 0.0); return; }
+        oc_jv_fd(A->P, out, A->u, v, A->F0, oc_fd_eps(A->unorm, vnorm));
+    }
+}
+
+/* ------------------------------------------------------------------ Krylov.jl sym_givens (real) */
+static inline double sgn(double x) { return (x > 0) - (x < 0); }
+void oc_sym_givens(double a, double b, double* c, double* s, double* rho) {
+    if (b == 0.0) {
+        *c = (a == 0.0) ? 1.0 : sgn(a);
+        *s = 0.0;
+        *rho = fabs(a);
+    } else if (a == 0.0) {
+        *c = 0.0;
+        *s = sgn(b);
+        *rho = fabs(b);
+    } else if (fabs(b) > fabs(a)) {
+        double t = a / b;
+        *s = sgn(b) / sqrt(1.0 + t * t);
+        *c = *s * t;
+        *rho = b / *s;
+    } else {
+        double t = b / a;
+        *c = sgn(a) / sqrt(1.0 + t * t);
+        *s = *c * t;
+        *rho = a / *c;
+    }
+}
+
+/* ------------------------------------------------------------------ GMRES (Krylov.jl 0.10 gmres!, M = N = I) */
+static void* xrealloc(void* p, size_t sz) { void* q = realloc(p, sz); if (!q) abort(); return q; }
+
+int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_krylov_stats* st,
+             double* hist, int64_t hist_cap, int64_t* hist_len) {
+    const int64_t n = oc_n(A->P);
+    int mem = o->memory > 0 ? o->memory : 20;
+    const int restart = o->restart, reorth = o->reorthogonalization;
+    int64_t itmax = o->itmax;
+    int64_t nh = 0;
+    const int64_t nmv0 = A->n_matvec;
+#define PUSH_HIST(v) do { if (hist && nh < hist_cap) hist[nh] = (v); nh++; } while (0)
+
+    double* w = (double*)malloc(sizeof(double) * n);
+    double* xr = restart ? (double*)malloc(sizeof(double) * n) : x;
+    int vcap = mem;
+    double** V = (double**)calloc((size_t)vcap, sizeof(double*));
+    for (int i = 0; i < vcap; ++i) V[i] = (double*)malloc(sizeof(double) * n);
+    int cap = mem;  /* capacity of c, s, z (z has cap entries) and R (cap(cap+1)/2) */
+    double* c = (double*)calloc((size_t)cap, sizeof(double));
+    double* s = (double*)calloc((size_t)cap, sizeof(double));
+    double* z = (double*)calloc((size_t)cap, sizeof(double));
+    double* R = (double*)calloc((size_t)cap * (cap + 1) / 2, sizeof(double));
+
+    oc_fill(n, x, 0.0);
+    oc_copy(n, w, b); /* r0 = b - A*0 */
+    double beta = oc_norm(n, w);
+    double rNorm = beta;
+    PUSH_HIST(rNorm);
+    const double eps_ = o->atol + o->rtol * rNorm;
+    st->inconsistent = 0; st->breakdown = 0;
+    if (beta == 0.0) {
+        st->niter = 0; st->solved = 1; st->status = 1;
+        goto done;
+    }
+    {
+        int npass = 0;
+        int64_t iter = 0, inner_iter = 0;
+        if (itmax == 0) itmax = 2 * n;
+        int64_t inner_itmax = itmax;
+        const double btol = pow(DBL_EPSILON, 0.75);
+        int breakdown = 0, inconsistent = 0;
+        int solved = rNorm <= eps_;
+        int tired = iter >= itmax;
+        while (!(solved || tired || breakdown)) {
+            int64_t nr = 0;
+            memset(c, 0, sizeof(double) * cap); memset(s, 0, sizeof(double) * cap);
+            memset(z, 0, sizeof(double) * cap); memset(R, 0, sizeof(double) * (size_t)cap * (cap + 1) / 2);
+            if (restart) {
+                oc_fill(n, xr, 0.0);
+                if (npass >= 1) {
+                    op_apply(A, w, x, -1.0);
+                    oc_axpby(n, 1.0, b, -1.0, w);
+                }
+            }
+            beta = oc_norm(n, w);
+            z[0] = beta;
+            oc_divcopy(n, V[0], w, beta);
+            npass++;
+            inner_iter = 0;
+            int inner_tired = 0;
+            while (!(solved || inner_tired || breakdown)) {
+                inner_iter++;
+                const int k = (int)inner_iter;
+                if (k + 1 > cap) { /* unrestarted GMRES grows its workspace beyond `memory` */
+                    int ncap = cap * 2;
+                    c = (double*)xrealloc(c, sizeof(double) * ncap); memset(c + cap, 0, sizeof(double) * (ncap - cap));
+                    s = (double*)xrealloc(s, sizeof(double) * ncap); memset(s + cap, 0, sizeof(double) * (ncap - cap));
+                    z = (double*)xrealloc(z, sizeof(double) * ncap); memset(z + cap, 0, sizeof(double) * (ncap - cap));
+                    size_t oR = (size_t)cap * (cap + 1) / 2, nR = (size_t)ncap * (ncap + 1) / 2;
+                    R = (double*)xrealloc(R, sizeof(double) * nR); memset(R + oR, 0, sizeof(double) * (nR - oR));
+                    cap = ncap;
+                }
+                op_apply(A, w, V[k - 1], 1.0);
+                for (int i = 1; i <= k; ++i) {
+                    R[nr + i - 1] = oc_dot(n, V[i - 1], w);
+                    oc_axpy(n, -R[nr + i - 1], V[i - 1], w);
+                }
+                if (reorth) {
+                    for (int i = 1; i <= k; ++i) {
+                        double htmp = oc_dot(n, V[i - 1], w);
+                        R[nr + i - 1] += htmp;
+                        oc_axpy(n, -htmp, V[i - 1], w);
+                    }
+                }
+                double Hbis = oc_norm(n, w);
+                for (int i = 1; i <= k - 1; ++i) {
+                    double Rtmp = c[i - 1] * R[nr + i - 1] + s[i - 1] * R[nr + i];
+                    R[nr + i] = s[i - 1] * R[nr + i - 1] - c[i - 1] * R[nr + i];
+                    R[nr + i - 1] = Rtmp;
+                }
+                oc_sym_givens(R[nr + k - 1], Hbis, &c[k - 1], &s[k - 1], &R[nr + k - 1]);
+                double zeta = s[k - 1] * z[k - 1];
+                z[k - 1] = c[k - 1] * z[k - 1];
+                rNorm = fabs(zeta);
+                PUSH_HIST(rNorm);
+                nr += k;
+                int mach = (rNorm + 1.0 <= 1.0);
+                solved = (rNorm <= eps_) || mach;
+                breakdown = Hbis <= btol;
+                inner_tired = restart ? (inner_iter >= (mem < inner_itmax ? mem : inner_itmax)) : (inner_iter >= inner_itmax);
+                if (!(solved || inner_tired || breakdown)) {
+                    if (k >= vcap) {
+                        int nv = vcap * 2;
+                        V = (double**)xrealloc(V, sizeof(double*) * nv);
+                        for (int i = vcap; i < nv; ++i) V[i] = (double*)malloc(sizeof(double) * n);
+                        vcap = nv;
+                    }
+                    oc_divcopy(n, V[k], w, Hbis);
+                    z[k] = zeta; /* cap >= k+1 guaranteed by the growth above */
+                }
+            }
+            /* back substitution R y = z, y stored in z */
+            const int kk = (int)inner_iter;
+            for (int i = kk; i >= 1; --i) {
+                int64_t pos = nr + i - kk;
+                for (int j = kk; j >= i + 1; --j) {
+                    z[i - 1] = z[i - 1] - R[pos - 1] * z[j - 1];
+                    pos = pos - j + 1;
+                }
+                if (fabs(R[pos - 1]) <= btol) { z[i - 1] = 0.0; inconsistent = 1; }
+                else z[i - 1] = z[i - 1] / R[pos - 1];
+            }
+            for (int i = 1; i <= kk; ++i) oc_axpy(n, z[i - 1], V[i - 1], xr);
+            if (restart) oc_axpy(n, 1.0, xr, x);
+            iter += inner_iter;
+            inner_itmax = itmax - iter;
+            tired = iter >= itmax;
+        }
+        st->niter = iter;
+        st->solved = solved;
+        st->inconsistent = inconsistent;
+        st->breakdown = breakdown;
+        st->status = solved ? 1 : (tired ? 2 : (breakdown ? 3 : 0));
+    }
+done:
+    st->n_matvec = A->n_matvec - nmv0;
+    if (hist_len) *hist_len = nh;
+    free(w);
+    if (restart) free(xr);
+    for (int i = 0; i < vcap; ++i) free(V[i]);
+    free(V); free(c); free(s); free(z); free(R);
+    return 0;
+#undef PUSH_HIST
+}
+
+/* ------------------------------------------------------------------ CG (Krylov.jl 0.10 cg!, M = I, radius = 0, linesearch = false) */
+int oc_cg(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_krylov_stats* st,
+          double* hist, int64_t hist_cap, int64_t* hist_len) {
+    const int64_t n = oc_n(A->P);
+    int64_t nh = 0;
+    const int64_t nmv0 = A->n_matvec;
+#define PUSH_HIST(v) do { if (hist && nh < hist_cap) hist[nh] = (v); nh++; } while (0)
+    double* r = (double*)malloc(sizeof(double) * n);
+    double* p = (double*)malloc(sizeof(double) * n);
+    double* Ap = (double*)malloc(sizeof(double) * n);
+    oc_fill(n, x, 0.0);
+    oc_copy(n, r, b);
+    oc_copy(n, p, r);
+    double gamma = oc_dot(n, r, r);
+    double rNorm = sqrt(gamma);
+    PUSH_HIST(rNorm);
+    st->inconsistent = 0; st->breakdown = 0;
+    if (gamma == 0.0) {
+        st->niter = 0; st->solved = 1; st->status = 1;
+    } else {
+        int64_t iter = 0, itmax = o->itmax == 0 ? 2 * n : o->itmax;
+        double pNorm2 = gamma;
+        const double eps_ = o->atol + o->rtol * rNorm;
+        int solved = rNorm <= eps_, tired = iter >= itmax, zero_curvature = 0, inconsistent = 0;
+        while (!(solved || tired || zero_curvature)) {
+            op_apply(A, Ap, p, -1.0);
+            double pAp = oc_dot(n, p, Ap);
+            if (pAp <= DBL_EPSILON * pNorm2) {
+                if (fabs(pAp) <= DBL_EPSILON * pNorm2) { zero_curvature = 1; inconsistent = 1; }
+            }
+            if (zero_curvature) continue;
+            double alpha = gamma / pAp;
+            oc_axpy(n, alpha, p, x);
+            oc_axpy(n, -alpha, Ap, r);
+            double gamma_next = oc_dot(n, r, r);
+            rNorm = sqrt(gamma_next);
+            PUSH_HIST(rNorm);
+            int mach = (rNorm + 1.0 <= 1.0);
+            solved = (rNorm <= eps_) || mach;
+            if (!solved) {
+                double beta = gamma_next / gamma;
+                pNorm2 = gamma_next + beta * beta * pNorm2;
+                gamma = gamma_next;
+                oc_axpby(n, 1.0, r, beta, p);
+            }
+            iter++;
+            tired = iter >= itmax;
+        }
+        st->niter = iter; st->solved = solved; st->inconsistent = inconsistent;
+        st->status = solved ? 1 : (tired ? 2 : (zero_curvature ? 4 : 0));
+    }
+    st->n_matvec = A->n_matvec - nmv0;
+    if (hist_len) *hist_len = nh;
+    free(r); free(p); free(Ap);
+    return 0;
+#undef PUSH_HIST
+}
+
+/* ------------------------------------------------------------------ forcing (Ariadne.jl:185-217) */
+double oc_ew_forcing(double eta_max, double gamma, double eta, double tol, double n_res, double n_res_prior) {
+    double eta_res = gamma * (n_res * n_res) / (n_res_prior * n_res_prior);
+    double eta_safe;
+    /* `F.γ * η^2 <= 1 // 10` compares against the exact rational 1/10: for a double x that is x < 0.1 */
+    if (gamma * (eta * eta) < 0.1) eta_safe = fmin(eta_max, eta_res);
+    else eta_safe = fmin(eta_max, fmax(eta_res, gamma * (eta * eta)));
+    return fmin(eta_max, fmax(eta_safe, 0.5 * tol / n_res));
+}
+
+/* ------------------------------------------------------------------ Newton driver (Ariadne.jl:288-372) */
+int oc_newton_krylov(const oc_problem* P, double* u, const oc_newton_opts* o, oc_newton_stats* st,
+                     double* nres_hist, int64_t hist_cap, int64_t* inner_hist) {
+    const int64_t n = oc_n(P);
+    double* res = (double*)malloc(sizeof(double) * n);
+    double* d = (double*)malloc(sizeof(double) * n);
+    oc_op A = {P, o->jv_mode, u, res, 0.0, 0};
+    int64_t nres_count = 0;
+    oc_residual(P, res, u);
+    nres_count++;
+    double n_res = oc_norm(n, res);
+    int64_t nh = 0;
+    if (nres_hist && nh < hist_cap) nres_hist[nh] = n_res;
+    nh++;
+    const double tol = o->tol_rel * n_res + o->tol_abs;
+    double eta = 0.0;
+    if (o->forcing == OC_FORCING_FIXED) eta = o->eta_fixed;
+    else if (o->forcing == OC_FORCING_EW) eta = o->eta_max;
+    int64_t outer = 0, inner = 0;
+    while (n_res > tol && outer <= o->max_niter) {
+        oc_krylov_opts ko = o->krylov;
+        if (!o->rtol_user) ko.rtol = (o->forcing != OC_FORCING_NONE) ? eta : sqrt(DBL_EPSILON);
+        oc_krylov_stats ks;
+        memset(&ks, 0, sizeof ks);
+        if (o->jv_mode == OC_JV_FD) A.unorm = oc_norm(n, u);
+        /* b = copy(res) (Ariadne.jl:338): res is not overwritten by our operator, so pass it directly */
+        if (o->algo == OC_ALGO_CG) oc_cg(&A, res, d, &ko, &ks, NULL, 0, NULL);
+        else oc_gmres(&A, res, d, &ko, &ks, NULL, 0, NULL);
+        oc_axpy(n, -1.0, d, u); /* u .-= 1 .* d */
+        double n_prior = n_res;
+        oc_residual(P, res, u);
+        nres_count++;
+        n_res = oc_norm(n, res);
+        if (isinf(n_res) || isnan(n_res)) break;
+        if (o->forcing == OC_FORCING_EW) eta = oc_ew_forcing(o->eta_max, o->gamma, eta, tol, n_res, n_prior);
+        outer += 1;
+        inner += ks.niter;
+        if (nres_hist && nh < hist_cap) nres_hist[nh] = n_res;
+        if (inner_hist && nh - 1 < hist_cap) inner_hist[nh - 1] = ks.niter;
+        nh++;
+    }
+    st->outer_iterations = outer;
+    st->inner_iterations = inner;
+    st->n_res = n_res;
+    st->solved = n_res <= tol;
+    st->n_matvec = A.n_matvec;
+    st->n_residual = nres_count;
+    st->tol = tol;
+    free(res); free(d);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ entry points used by the Python wrapper */
+int oc_krylov_solve(const oc_problem* P, int jv_mode, int algo, const double* u, const double* F0,
+                    const double* b, double* x, const oc_krylov_opts* o, oc_krylov_stats* st,
+                    double* hist, int64_t hist_cap, int64_t* hist_len) {
+    oc_op A = {P, jv_mode, u, F0, 0.0, 0};
+    if (jv_mode == OC_JV_FD) A.unorm = oc_norm(oc_n(P), u);
+    if (algo == OC_ALGO_CG) return oc_cg(&A, b, x, o, st, hist, hist_cap, hist_len);
+    return oc_gmres(&A, b, x, o, st, hist, hist_cap, hist_len);
+}
+
+void oc_set_threads(int t) { if (t > 0) omp_set_num_threads(t); }
+int oc_get_threads(void) { return omp_get_max_threads(); }

@@ -1,0 +1,299 @@
+"""ctypes front-end of the C oracle (oracle/nk_oracle.c).
+
+TEST INFRASTRUCTURE ONLY.  Only tests/, ``__graft_entry__.smoke()`` and bench.py's
+``cpu_baseline`` leg may import this module -- as the checker / the timed CPU baseline,
+never as the thing measured or shipped.  The product package (newtonkrylov.jl_amd/)
+never imports it and has no CPU fallback.
+
+Each function restates the reference (file:line in nk_oracle.c); parity of the
+Krylov.jl part (third-party, absent from /root/reference) is pinned only through the
+reference's known answers and the numpy/scipy goldens in tests/golden/.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+import subprocess
+from dataclasses import dataclass, field
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libnkoracle.so")
+
+BRATU1D, BRATU2D, HEAT2D_EULER, HEAT3D_EULER = 1, 2, 3, 4
+JV_EXACT, JV_FD = 0, 1
+FORCING_NONE, FORCING_FIXED, FORCING_EW = 0, 1, 2
+ALGO_GMRES, ALGO_CG = 0, 1
+SQRT_EPS = math.sqrt(np.finfo(np.float64).eps)
+
+
+class _Problem(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("bc", C.c_int32),
+                ("nx", C.c_int64), ("ny", C.c_int64), ("nz", C.c_int64),
+                ("hx", C.c_double), ("hy", C.c_double), ("hz", C.c_double),
+                ("lam", C.c_double), ("a", C.c_double), ("dt", C.c_double),
+                ("un", C.POINTER(C.c_double))]
+
+
+class _KrylovOpts(C.Structure):
+    _fields_ = [("memory", C.c_int32), ("restart", C.c_int32), ("reorthogonalization", C.c_int32),
+                ("itmax", C.c_int32), ("atol", C.c_double), ("rtol", C.c_double)]
+
+
+class _KrylovStats(C.Structure):
+    _fields_ = [("niter", C.c_int64), ("solved", C.c_int32), ("inconsistent", C.c_int32),
+                ("breakdown", C.c_int32), ("status", C.c_int32), ("n_matvec", C.c_int64)]
+
+
+class _NewtonOpts(C.Structure):
+    _fields_ = [("tol_rel", C.c_double), ("tol_abs", C.c_double), ("max_niter", C.c_int32),
+                ("forcing", C.c_int32), ("eta_fixed", C.c_double), ("eta_max", C.c_double),
+                ("gamma", C.c_double), ("algo", C.c_int32), ("jv_mode", C.c_int32),
+                ("krylov", _KrylovOpts), ("rtol_user", C.c_int32)]
+
+
+class _NewtonStats(C.Structure):
+    _fields_ = [("outer_iterations", C.c_int64), ("inner_iterations", C.c_int64), ("n_res", C.c_double),
+                ("solved", C.c_int32), ("n_matvec", C.c_int64), ("n_residual", C.c_int64), ("tol", C.c_double)]
+
+
+_lib = None
+
+
+def build() -> str:
+    """Compile the oracle with its Makefile (gcc is part of the image)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(HERE, "nk_oracle.c")):
+            build()
+        L = C.CDLL(LIB_PATH)
+        D, I64, P = C.c_double, C.c_int64, C.POINTER(C.c_double)
+        L.oc_dot.restype = D
+        L.oc_dot.argtypes = [I64, P, P]
+        L.oc_norm.restype = D
+        L.oc_norm.argtypes = [I64, P]
+        L.oc_fd_eps.restype = D
+        L.oc_fd_eps.argtypes = [D, D]
+        L.oc_ew_forcing.restype = D
+        L.oc_ew_forcing.argtypes = [D, D, D, D, D, D]
+        L.oc_residual.argtypes = [C.POINTER(_Problem), P, P]
+        L.oc_jv_exact.argtypes = [C.POINTER(_Problem), P, P, P]
+        L.oc_jv_fd.argtypes = [C.POINTER(_Problem), P, P, P, P, D]
+        L.oc_krylov_solve.argtypes = [C.POINTER(_Problem), C.c_int, C.c_int, P, P, P, P,
+                                      C.POINTER(_KrylovOpts), C.POINTER(_KrylovStats), P, I64, C.POINTER(I64)]
+        L.oc_newton_krylov.argtypes = [C.POINTER(_Problem), P, C.POINTER(_NewtonOpts), C.POINTER(_NewtonStats),
+                                       P, I64, C.POINTER(I64)]
+        L.oc_sym_givens.argtypes = [D, D, P, P, P]
+        L.oc_set_threads.argtypes = [C.c_int]
+        L.oc_get_threads.restype = C.c_int
+        for name in ("oc_axpy",):
+            getattr(L, name).argtypes = [I64, D, P, P]
+        L.oc_axpby.argtypes = [I64, D, P, D, P]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+@dataclass
+class Problem:
+    """Grid problem: kind + interior dims (x fastest) + parameters (see nk_oracle.c)."""
+    kind: int
+    nx: int
+    ny: int = 1
+    nz: int = 1
+    hx: float = 1.0
+    hy: float = 1.0
+    hz: float = 1.0
+    lam: float = 0.0
+    a: float = 0.0
+    dt: float = 0.0
+    un: np.ndarray | None = field(default=None, repr=False)
+
+    @property
+    def n(self) -> int:
+        return self.nx * self.ny * self.nz
+
+    @property
+    def shape(self):
+        return {1: (self.nx,), 2: (self.ny, self.nx), 3: (self.nz, self.ny, self.nx)}[self.dim]
+
+    @property
+    def dim(self) -> int:
+        return 1 if self.kind == BRATU1D else (3 if self.kind == HEAT3D_EULER else 2)
+
+    def _c(self) -> _Problem:
+        s = _Problem(self.kind, 0, self.nx, self.ny, self.nz, self.hx, self.hy, self.hz, self.lam, self.a, self.dt, None)
+        if self.un is not None:
+            self._un_keep = np.ascontiguousarray(self.un, dtype=np.float64).reshape(-1)
+            assert self._un_keep.size == self.n
+            s.un = _p(self._un_keep)
+        return s
+
+
+# -- problem constructors (parameters of the reference examples / SURVEY.md §8d) -------------------
+LAMBDA_BRATU = 3.51382  # examples/bratu.jl:41
+
+
+def bratu1d(N: int, lam: float = LAMBDA_BRATU) -> Problem:
+    dx = 1.0 / (N + 1)  # bratu.jl:42
+    return Problem(BRATU1D, N, hx=dx, lam=lam)
+
+
+def bratu2d(nx: int, ny: int | None = None, lam: float = LAMBDA_BRATU) -> Problem:
+    ny = nx if ny is None else ny
+    return Problem(BRATU2D, nx, ny, hx=1.0 / (nx + 1), hy=1.0 / (ny + 1), lam=lam)
+
+
+def heat_dt_2d(hx, hy, a):
+    return hx ** 2 * hy ** 2 / (2.0 * a * (hx ** 2 + hy ** 2))  # heat_2D.jl:72
+
+
+def heat2d_euler(nx: int, ny: int | None = None, a: float = 0.01, dt: float | None = None, un=None) -> Problem:
+    ny = nx if ny is None else ny
+    hx, hy = 1.0 / (nx + 1), 1.0 / (ny + 1)
+    dt = heat_dt_2d(hx, hy, a) if dt is None else dt
+    return Problem(HEAT2D_EULER, nx, ny, hx=hx, hy=hy, a=a, dt=dt, un=un)
+
+
+def heat_dt_3d(hx, hy, hz, a):
+    return 1.0 / (2.0 * a * (1.0 / hx ** 2 + 1.0 / hy ** 2 + 1.0 / hz ** 2))
+
+
+def heat3d_euler(nx: int, ny=None, nz=None, a: float = 0.01, dt=None, un=None) -> Problem:
+    ny = nx if ny is None else ny
+    nz = nx if nz is None else nz
+    hx, hy, hz = 1.0 / (nx + 1), 1.0 / (ny + 1), 1.0 / (nz + 1)
+    dt = heat_dt_3d(hx, hy, hz, a) if dt is None else dt
+    return Problem(HEAT3D_EULER, nx, ny, nz, hx=hx, hy=hy, hz=hz, a=a, dt=dt, un=un)
+
+
+def sin_ic(P: Problem) -> np.ndarray:
+    """u0 = sin(pi x) [sin(pi y) [sin(pi z)]] on the interior nodes h, 2h, ... (bratu.jl:45-46)."""
+    xs = [np.arange(1, m + 1) * h for m, h in ((P.nx, P.hx), (P.ny, P.hy), (P.nz, P.hz))][: P.dim]
+    out = np.sin(np.pi * xs[0])
+    if P.dim >= 2:
+        out = np.sin(np.pi * xs[1])[:, None] * out[None, :]
+    if P.dim == 3:
+        out = np.sin(np.pi * xs[2])[:, None, None] * out[None, :, :]
+    return np.ascontiguousarray(out, dtype=np.float64)
+
+
+# -- kernels -------------------------------------------------------------------------------------
+def residual(P: Problem, u: np.ndarray) -> np.ndarray:
+    u = np.ascontiguousarray(u, dtype=np.float64)
+    res = np.empty_like(u)
+    cp = P._c()
+    lib().oc_residual(C.byref(cp), _p(res), _p(u))
+    return res
+
+
+def jv_exact(P: Problem, u, v) -> np.ndarray:
+    u = np.ascontiguousarray(u, dtype=np.float64)
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    out = np.empty_like(u)
+    cp = P._c()
+    lib().oc_jv_exact(C.byref(cp), _p(out), _p(u), _p(v))
+    return out
+
+
+def fd_eps(unorm: float, vnorm: float) -> float:
+    return lib().oc_fd_eps(unorm, vnorm)
+
+
+def jv_fd(P: Problem, u, v, F0=None, eps: float | None = None) -> np.ndarray:
+    u = np.ascontiguousarray(u, dtype=np.float64)
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    F0 = residual(P, u) if F0 is None else np.ascontiguousarray(F0, dtype=np.float64)
+    if eps is None:
+        eps = fd_eps(norm(u), norm(v))
+    out = np.empty_like(u)
+    cp = P._c()
+    lib().oc_jv_fd(C.byref(cp), _p(out), _p(u), _p(v), _p(F0), eps)
+    return out
+
+
+def dot(x, y) -> float:
+    x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
+    y = np.ascontiguousarray(y, dtype=np.float64).reshape(-1)
+    return lib().oc_dot(x.size, _p(x), _p(y))
+
+
+def norm(x) -> float:
+    x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
+    return lib().oc_norm(x.size, _p(x))
+
+
+def sym_givens(a: float, b: float):
+    c, s, r = C.c_double(), C.c_double(), C.c_double()
+    lib().oc_sym_givens(a, b, C.byref(c), C.byref(s), C.byref(r))
+    return c.value, s.value, r.value
+
+
+def ew_forcing(eta, tol, n_res, n_res_prior, eta_max=0.999, gamma=0.9):
+    return lib().oc_ew_forcing(eta_max, gamma, eta, tol, n_res, n_res_prior)
+
+
+def set_threads(t: int):
+    lib().oc_set_threads(int(t))
+
+
+def get_threads() -> int:
+    return lib().oc_get_threads()
+
+
+def krylov_solve(P: Problem, u, b, *, algo="gmres", jv="exact", F0=None, memory=20, restart=False,
+                 reorthogonalization=False, itmax=0, atol=SQRT_EPS, rtol=SQRT_EPS, history=True):
+    """One Krylov.jl-style solve of J(u) x = b; returns (x, stats dict, residual-norm history)."""
+    u = np.ascontiguousarray(u, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    if jv == "fd" and F0 is None:
+        F0 = residual(P, u)
+    F0 = np.ascontiguousarray(F0 if F0 is not None else u, dtype=np.float64)
+    x = np.empty_like(u)
+    o = _KrylovOpts(memory, int(restart), int(reorthogonalization), itmax, atol, rtol)
+    st = _KrylovStats()
+    cap = (itmax if itmax else 2 * P.n) + 16 if history else 0
+    cap = min(cap, 1 << 22)
+    hist = np.zeros(max(cap, 1))
+    hl = C.c_int64(0)
+    cp = P._c()
+    lib().oc_krylov_solve(C.byref(cp), JV_FD if jv == "fd" else JV_EXACT, ALGO_CG if algo == "cg" else ALGO_GMRES,
+                          _p(u), _p(F0), _p(b), _p(x), C.byref(o), C.byref(st), _p(hist), cap, C.byref(hl))
+    stats = dict(niter=st.niter, solved=bool(st.solved), inconsistent=bool(st.inconsistent),
+                 breakdown=bool(st.breakdown), status=st.status, n_matvec=st.n_matvec)
+    return x, stats, hist[: min(hl.value, cap)].copy()
+
+
+def newton_krylov(P: Problem, u0, *, tol_rel=1e-6, tol_abs=1e-12, max_niter=50, forcing="ew", eta=0.1,
+                  eta_max=0.999, gamma=0.9, algo="gmres", jv="exact", memory=20, restart=False,
+                  reorthogonalization=False, itmax=0, atol=SQRT_EPS, rtol=None):
+    """Ariadne newton_krylov! restated (src/Ariadne.jl:288-372). rtol given => krylov_kwargs rtol wins."""
+    u = np.array(u0, dtype=np.float64, order="C", copy=True)
+    fk = {"none": FORCING_NONE, None: FORCING_NONE, "fixed": FORCING_FIXED, "ew": FORCING_EW}[forcing]
+    ko = _KrylovOpts(memory, int(restart), int(reorthogonalization), itmax, atol, 0.0 if rtol is None else rtol)
+    o = _NewtonOpts(tol_rel, tol_abs, max_niter, fk, eta, eta_max, gamma,
+                    ALGO_CG if algo == "cg" else ALGO_GMRES, JV_FD if jv == "fd" else JV_EXACT, ko,
+                    0 if rtol is None else 1)
+    st = _NewtonStats()
+    cap = max_niter + 4
+    hist = np.zeros(cap)
+    inner = np.zeros(cap, dtype=np.int64)
+    cp = P._c()
+    lib().oc_newton_krylov(C.byref(cp), _p(u), C.byref(o), C.byref(st), _p(hist), cap,
+                           inner.ctypes.data_as(C.POINTER(C.c_int64)))
+    k = st.outer_iterations
+    stats = dict(outer_iterations=st.outer_iterations, inner_iterations=st.inner_iterations, n_res=st.n_res,
+                 solved=bool(st.solved), n_matvec=st.n_matvec, n_residual=st.n_residual, tol=st.tol,
+                 n_res_history=hist[: k + 1].copy(), inner_history=inner[:k].copy())
+    return u, stats

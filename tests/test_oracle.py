@@ -1,0 +1,256 @@
+"""Pin the CPU oracle before trusting it (CPU only).
+
+1. the reference's own known answers (test/runtests.jl) through the dual-number restatement;
+2. the C oracle's residuals / JVPs against the independent numpy goldens (tests/golden/);
+3. the two restatements of the Krylov.jl + Ariadne loop (C and Python) against each other;
+4. whole Newton solves against sparse-direct roots, the analytic 1D Bratu solution
+   (examples/bratu.jl:33-37) and the exact implicit-Euler decay of the heat eigenvector.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle import ariadne_ref as ar
+from oracle import oracle as oc
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(np.asarray(a) - np.asarray(b))) / max(1e-300, np.max(np.abs(b))))
+
+
+# ----------------------------------------------------------------------------- runtests.jl known answers
+def kelley_F_(res, x, _):
+    res[0] = x[0] ** 2 + x[1] ** 2 - 2
+    res[1] = ar.dexp(x[0] - 1) + x[1] ** 2 - 2
+
+
+def kelley_F(x, p):
+    res = np.zeros(2, dtype=object) if x.dtype == object else np.zeros(2)
+    kelley_F_(res, x, p)
+    return res
+
+
+@pytest.fixture(scope="module")
+def kelley(golden_dir):
+    with open(os.path.join(golden_dir, "kelley2x2.json")) as f:
+        return json.load(f)
+
+
+def test_kelley_jvp_exact(kelley):
+    # runtests.jl:36-38: mul!(out, J, [1,0]) == [6.0, 7.38905609893065] (exact equality)
+    _, out = ar.jvp(kelley_F_, np.array(kelley["x_jvp"]), np.array([1.0, 0.0]))
+    assert list(out) == kelley["jvp_e1"]
+
+
+def test_kelley_vjp_and_collect(kelley):
+    x = np.array(kelley["x_jvp"])
+    assert list(ar.vjp(kelley_F_, x, [1.0, 0.0])) == kelley["vjp_e1"]      # runtests.jl:40-42
+    J = ar.collect(kelley_F_, x)
+    assert np.array_equal(J, np.array(kelley["jacobian"]))                  # runtests.jl:44-46
+    assert np.array_equal(ar.collect(kelley_F_, x).T, J.T)                  # runtests.jl:54
+    v = np.random.default_rng(0).random(2)
+    assert np.allclose(ar.jvp(kelley_F_, x, v)[1], J @ v)                   # runtests.jl:48-52
+
+
+def test_kelley_newton_solved(kelley):
+    for x0 in kelley["starts_inplace"]:                                     # runtests.jl:15-18
+        x, st = ar.newton_krylov_(kelley_F_, np.array(x0))
+        assert st["solved"]
+        assert np.allclose(x, kelley["root"], atol=1e-5)
+    for x0 in kelley["starts_outofplace"]:                                  # runtests.jl:20-23
+        x, st = ar.newton_krylov(kelley_F, np.array(x0))
+        assert st["solved"]
+
+
+# ----------------------------------------------------------------------------- forcing / givens
+def test_eisenstat_walker_matches_c():
+    ew = ar.EisenstatWalker()
+    rng = np.random.default_rng(5)
+    for _ in range(200):
+        eta, tol = rng.uniform(0, 1), 10 ** rng.uniform(-12, -2)
+        n_prior = 10 ** rng.uniform(-6, 2)
+        n = n_prior * rng.uniform(0.01, 1.2)
+        assert ew(eta, tol, n, n_prior) == oc.ew_forcing(eta, tol, n, n_prior)
+
+
+def test_eisenstat_walker_rational_threshold():
+    # γη² exactly equal to the double 0.1 is NOT <= 1//10 (the double 0.1 exceeds 1/10):
+    ew = ar.EisenstatWalker(eta_max=0.999, gamma=1.0)
+    eta = math.sqrt(0.1)
+    g_eta2 = 1.0 * eta ** 2
+    n_res, n_prior, tol = 1e-3, 1.0, 1e-12
+    expect = (min(0.999, max(0.9 * 0 + n_res ** 2 / n_prior ** 2, g_eta2)) if g_eta2 >= 0.1
+              else min(0.999, n_res ** 2 / n_prior ** 2))
+    assert ew(eta, tol, n_res, n_prior) == max(expect, 0.5 * tol / n_res)
+
+
+def test_sym_givens():
+    for a, b in [(3.0, 4.0), (-2.0, 0.5), (0.0, 0.0), (0.0, -3.0), (1.5, 0.0), (1e-300, 1e300)]:
+        c, s, r = oc.sym_givens(a, b)
+        assert (c, s, r) == ar.sym_givens(a, b)
+        assert abs(c * a + s * b - r) <= 1e-14 * max(1.0, abs(r))
+        if a != 0 or b != 0:
+            assert abs(s * a - c * b) <= 1e-14 * max(abs(a), abs(b))
+
+
+# ----------------------------------------------------------------------------- kernels vs numpy goldens
+def test_bratu1d_kernels(golden_dir):
+    g = np.load(os.path.join(golden_dir, "bratu1d_n1000.npz"))
+    P = oc.bratu1d(1000)
+    assert P.hx == g["dx"]
+    assert np.array_equal(oc.sin_ic(P), np.sin(g["x"] * np.pi)) or _rel(oc.sin_ic(P), g["u0"]) < 1e-15
+    u0 = g["u0"]
+    assert _rel(oc.residual(P, u0), g["F0"]) < 1e-14
+    assert _rel(oc.jv_exact(P, u0, g["v"]), g["Jv"]) < 1e-14
+    # FD operator approximates the exact JVP to ~sqrt(eps)
+    assert _rel(oc.jv_fd(P, u0, g["v"]), g["Jv"]) < 1e-6
+
+
+def test_bratu2d_kernels(golden_dir):
+    g = np.load(os.path.join(golden_dir, "bratu2d_64.npz"))
+    P = oc.bratu2d(64)
+    assert _rel(oc.sin_ic(P), g["u0"]) < 1e-15
+    assert _rel(oc.residual(P, g["u0"]), g["F0"]) < 1e-14
+    assert _rel(oc.jv_exact(P, g["u0"], g["v"]), g["Jv"]) < 1e-14
+    assert _rel(oc.jv_fd(P, g["u0"], g["v"]), g["Jv"]) < 1e-6
+
+
+def test_heat2d_kernels(golden_dir):
+    g = np.load(os.path.join(golden_dir, "heat2d_40.npz"))
+    P = oc.heat2d_euler(40, un=g["u0"])
+    assert P.dt == g["dt"]
+    assert _rel(oc.residual(P, g["u0"]), g["G0"]) < 1e-13
+    assert _rel(oc.jv_exact(P, g["u0"], g["v"]), g["Jv"]) < 1e-14
+    assert _rel(oc.jv_fd(P, g["u0"], g["v"]), g["Jv"]) < 1e-6
+
+
+def test_heat3d_kernels(golden_dir):
+    g = np.load(os.path.join(golden_dir, "heat3d_12.npz"))
+    P = oc.heat3d_euler(12, un=g["un"])
+    assert abs(P.dt - g["dt"]) <= 1e-15 * g["dt"]
+    assert _rel(oc.residual(P, g["u"]), g["G"]) < 1e-13
+    assert _rel(oc.jv_exact(P, g["u"], g["v"]), g["Jv"]) < 1e-14
+
+
+# ----------------------------------------------------------------------------- Krylov: C vs Python restatement
+@pytest.mark.parametrize("restart,memory,reorth", [(False, 20, False), (True, 10, False), (True, 8, True)])
+def test_gmres_c_matches_python(restart, memory, reorth):
+    P = oc.bratu2d(12)
+    u = oc.sin_ic(P)
+    b = oc.residual(P, u)
+    kw = dict(memory=memory, restart=restart, reorthogonalization=reorth, atol=1e-12, rtol=1e-10, itmax=120)
+    x_c, st_c, h_c = oc.krylov_solve(P, u, b, **kw)
+    A = lambda v: oc.jv_exact(P, u, v.reshape(P.shape)).ravel()
+    x_p, st_p, h_p = ar.gmres(A, b.ravel(), **kw)
+    assert st_c["niter"] == st_p.niter and st_c["solved"] == st_p.solved
+    # first cycle agrees to rounding; restart residuals amplify rounding at the 1e-8 level later on
+    assert np.allclose(h_c[: memory + 1], h_p[: memory + 1], rtol=1e-8, atol=0)
+    # rounding differences (different dot order) grow once the residual nears the rounding floor
+    h_p = np.asarray(h_p)
+    m = h_p > 1e-6 * h_p[0]
+    assert np.allclose(h_c[m], h_p[m], rtol=1e-5, atol=0)
+    assert _rel(x_c.ravel(), x_p) < 1e-8
+    nmv = st_p.niter + (0 if not restart else (st_p.niter - 1) // memory)
+    assert st_c["n_matvec"] == nmv
+
+
+def test_cg_c_matches_python():
+    P = oc.bratu1d(200)
+    u = oc.sin_ic(P)
+    b = oc.residual(P, u)
+    x_c, st_c, h_c = oc.krylov_solve(P, u, b, algo="cg", atol=1e-12, rtol=1e-10)
+    A = lambda v: oc.jv_exact(P, u, v)
+    x_p, st_p, h_p = ar.cg(A, b.copy(), atol=1e-12, rtol=1e-10)
+    assert st_c["niter"] == st_p.niter
+    assert _rel(x_c, x_p) < 1e-6
+
+
+def test_gmres_solves_linear_system():
+    P = oc.bratu2d(16)
+    u = oc.sin_ic(P)
+    b = oc.residual(P, u)
+    x, st, _ = oc.krylov_solve(P, u, b, atol=0.0, rtol=1e-12, itmax=0)
+    assert st["solved"]
+    assert oc.norm(oc.jv_exact(P, u, x) - b) <= 1e-10 * oc.norm(b)
+
+
+# ----------------------------------------------------------------------------- whole Newton solves
+def test_newton_bratu1d_cg_matches_root(golden_dir):
+    """examples/bratu.jl:59-63 (algo = :cg) at BASELINE config 1 (N = 1000)."""
+    g = np.load(os.path.join(golden_dir, "bratu1d_n1000.npz"))
+    P = oc.bratu1d(1000)
+    u, st = oc.newton_krylov(P, g["u0"], algo="cg")
+    assert st["solved"]
+    assert st["n_res"] <= st["tol"]
+    # discretisation error vs the analytic solution (SURVEY.md §6 probe: 2.6e-4)
+    assert np.max(np.abs(u - g["true_sol"])) < 3e-4
+    # the discrete root (sparse-direct Newton): cond(J) ~ 1.75e8 => fp64 fixes u only to ~1e-6 here
+    assert np.max(np.abs(u - g["ustar"])) < 1e-4
+
+
+def test_newton_bratu1d_forcing_variants():
+    # bratu.jl:92-108: Fixed(0.1) and forcing = nothing (N = 1000; smaller grids stagnate near the fold)
+    P = oc.bratu1d(1000)
+    u0 = oc.sin_ic(P)
+    for forcing in ("ew", "fixed", "none"):
+        u, st = oc.newton_krylov(P, u0, algo="cg", forcing=forcing)
+        assert st["solved"], forcing
+
+
+def test_newton_bratu2d_gmres30_matches_root(golden_dir):
+    g = np.load(os.path.join(golden_dir, "bratu2d_64.npz"))
+    P = oc.bratu2d(64)
+    u, st = oc.newton_krylov(P, g["u0"], memory=30, restart=True, tol_rel=1e-10)
+    assert st["solved"]
+    assert _rel(u, g["ustar"]) < 1e-8
+
+
+def test_newton_bratu2d_fd_matches_exact():
+    P = oc.bratu2d(32)
+    u0 = oc.sin_ic(P)
+    # tol_rel = 1e-9 keeps tol above Krylov's default atol = sqrt(eps) floor
+    ue, se = oc.newton_krylov(P, u0, memory=30, restart=True, tol_rel=1e-9, jv="exact")
+    uf, sf = oc.newton_krylov(P, u0, memory=30, restart=True, tol_rel=1e-9, jv="fd")
+    assert se["solved"] and sf["solved"]
+    assert _rel(uf, ue) < 1e-8
+    assert se["outer_iterations"] == sf["outer_iterations"]
+
+
+def test_newton_matches_python_restatement():
+    P = oc.bratu2d(10)
+    u0 = oc.sin_ic(P)
+    u_c, st_c = oc.newton_krylov(P, u0, memory=20, restart=True)
+
+    h = P.hx
+
+    def F_(res, u, p):  # 2D Bratu written elementwise so the dual numbers differentiate it
+        U = u.reshape(P.shape)
+        R = res.reshape(P.shape)
+        for j in range(P.ny):
+            for i in range(P.nx):
+                e = U[j, i + 1] if i + 1 < P.nx else 0.0
+                w = U[j, i - 1] if i > 0 else 0.0
+                n = U[j + 1, i] if j + 1 < P.ny else 0.0
+                s = U[j - 1, i] if j > 0 else 0.0
+                c = U[j, i]
+                R[j, i] = ((e - 2.0 * c) + w) / (h * h) + ((n - 2.0 * c) + s) / (h * h) + oc.LAMBDA_BRATU * ar.dexp(c)
+
+    u_p, st_p = ar.newton_krylov_(F_, u0.ravel(), krylov_kwargs=dict(restart=True), memory=20)
+    assert st_c["outer_iterations"] == st_p["outer_iterations"]
+    assert st_c["inner_iterations"] == st_p["inner_iterations"]
+    assert _rel(u_c.ravel(), u_p) < 1e-9
+
+
+def test_heat2d_reference_ic_one_step(golden_dir):
+    """Reference IC is the discrete Laplacian's eigenvector: one implicit Euler step (tol_abs=6e-6,
+    implicit.jl:67-70) must reproduce the exact decay with a single Krylov iteration."""
+    g = np.load(os.path.join(golden_dir, "heat2d_40.npz"))
+    P = oc.heat2d_euler(40, un=g["u0"])
+    u, st = oc.newton_krylov(P, g["u0"], tol_abs=6e-6)
+    assert st["solved"]
+    assert st["inner_iterations"] == 1
+    assert np.max(np.abs(u - g["u1"])) < 1e-10
+    assert np.max(np.abs(u - g["decay"] * g["u0"])) < 1e-10
