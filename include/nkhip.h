@@ -1,0 +1,157 @@
+/*
+ * nkhip.h -- C ABI of libnkhip.so, the MI355X-native JFNK inner loop.
+ *
+ * Plain pointers and sizes only (no C++ or torch types).  Every entry point replaces one
+ * call the reference makes on its hot path; the reference interface is cited per group.
+ * A Julia shim binds these with `ccall`; the Python host mirror in
+ * newtonkrylov.jl_amd/ binds them with ctypes.
+ *
+ * Conventions
+ *  - Return value: 0 = ok; < 0 = error (NK_E_*; HIP / RCCL errors are mapped, the message is in
+ *    nk_last_error(ctx)).  No C++ exception crosses the ABI.
+ *  - All device work of a context runs in stream order on the context's single HIP stream.
+ *    Functions that return host scalars (nk_dot, nk_norm, nk_residual_norm, solver stats)
+ *    synchronise that stream, as Krylov.jl's kdot/knorm return host scalars.
+ *  - Vectors are device pointers to the INTERIOR of a grid function allocated by nk_vec_alloc:
+ *    the allocation carries one ghost plane before and after the interior along the slowest
+ *    axis (zero = physical Dirichlet boundary; written by the halo exchange when distributed).
+ *    BLAS-1 primitives touch the n interior entries only.
+ */
+#ifndef NKHIP_H
+#define NKHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- error codes */
+#define NK_OK 0
+#define NK_E_HIP (-1)
+#define NK_E_ARG (-2)
+#define NK_E_NOMEM (-3)
+#define NK_E_RCCL (-4)
+#define NK_E_STATE (-5)
+
+/* ---------------------------------------------------------------- problem kinds */
+#define NK_BRATU1D 1       /* examples/bratu.jl:14-24  bratu!(res, y, (Δx, λ))                         */
+#define NK_BRATU2D 2       /* build-defined 2D generalisation                       */
+#define NK_HEAT2D_EULER 3  /* examples/implicit.jl:8-13 G_Euler! ∘ examples/heat_2D.jl:45-62 diffusion! */
+#define NK_HEAT3D_EULER 4  /* build-defined 3D generalisation                      */
+
+#define NK_BC_ZERO 0       /* bc_zero!, examples/heat_2D.jl:28-38 */
+
+#define NK_JV_EXACT 0      /* exact JVP == Enzyme Forward in mul!(out, J, v), src/Ariadne.jl:48-57 */
+#define NK_JV_FD 1         /* (F(u + eps v) - F(u)) / eps, BASELINE.json north star                */
+
+#define NK_ALGO_GMRES 0    /* krylov_workspace(:gmres, …), src/Ariadne.jl:317-318 */
+#define NK_ALGO_CG 1       /* krylov_workspace(:cg, …)    (examples/bratu.jl:59-63) */
+
+typedef struct nk_ctx nk_ctx;
+typedef struct nk_workspace nk_workspace;
+
+/* F!(res, u, p) of one problem on this rank's slab.  Dimensions are LOCAL interior extents;
+ * spacings are global (h = 1/(N_global + 1)).  x is the fastest axis (the reference's
+ * column-major first index). */
+typedef struct nk_problem {
+    int32_t kind;           /* NK_BRATU1D … NK_HEAT3D_EULER */
+    int32_t bc;             /* NK_BC_ZERO */
+    int64_t nx, ny, nz;     /* local interior extents (ny = nz = 1 in 1D, nz = 1 in 2D) */
+    double hx, hy, hz;      /* grid spacings */
+    double lambda;          /* Bratu λ */
+    double a, dt;           /* heat diffusivity and time step Δt */
+    const double* un;       /* heat: device interior pointer to u_n (borrowed for the call) */
+} nk_problem;
+
+/* ---------------------------------------------------------------- context / memory */
+int nk_device_count(int* count);
+int nk_ctx_create(int device, nk_ctx** out);
+int nk_ctx_destroy(nk_ctx* ctx);
+const char* nk_last_error(nk_ctx* ctx);
+int nk_sync(nk_ctx* ctx);
+
+/* similar(u) / zero(u) for a grid function of `p`'s local grid: zero-filled incl. ghost planes. */
+int nk_vec_alloc(nk_ctx* ctx, const nk_problem* p, double** out);
+int nk_vec_free(nk_ctx* ctx, double* v);
+int nk_memcpy_h2d(nk_ctx* ctx, double* dst, const double* src, int64_t n);
+int nk_memcpy_d2h(nk_ctx* ctx, double* dst, const double* src, int64_t n);
+
+/* ---------------------------------------------------------------- residual and Jacobian operator */
+/* F!(res, u, p): Ariadne calls it at src/Ariadne.jl:302 and :349. */
+int nk_residual(nk_ctx* ctx, const nk_problem* p, double* res, const double* u);
+/* F!(res, u, p); n_res = norm(res)  fused into one pass (src/Ariadne.jl:302-303, :349-350). */
+int nk_residual_norm(nk_ctx* ctx, const nk_problem* p, double* res, const double* u, double* n_res);
+/* mul!(out, J::JacobianOperator, v) (src/Ariadne.jl:48-57).  mode NK_JV_EXACT: the tangent of F!
+ * (u, v read; F0 unused).  NK_JV_FD: (F(u + eps v) - F0)/eps with F0 = F(u); eps <= 0 selects
+ * eps = sqrt(eps_mach) * max(1, ||u||) / ||v||.  Unlike Enzyme, `res` is not rewritten. */
+int nk_jv(nk_ctx* ctx, const nk_problem* p, double* out, const double* u, const double* v,
+          const double* F0, int32_t mode, double eps);
+
+/* ---------------------------------------------------------------- Krylov vector primitives
+ * Krylov.kdot/knorm/kscal!/kaxpy!/kaxpby!/kcopy!/kfill!/kdivcopy!/kref! -- the overload points
+ * examples/halovector.jl:51-147 demonstrates for a custom vector type.  n = interior length. */
+int nk_dot(nk_ctx* ctx, int64_t n, const double* x, const double* y, double* out);
+int nk_norm(nk_ctx* ctx, int64_t n, const double* x, double* out);
+int nk_scal(nk_ctx* ctx, int64_t n, double s, double* x);                              /* x = s x       */
+int nk_axpy(nk_ctx* ctx, int64_t n, double s, const double* x, double* y);             /* y = s x + y   */
+int nk_axpby(nk_ctx* ctx, int64_t n, double s, const double* x, double t, double* y);  /* y = s x + t y */
+int nk_copy(nk_ctx* ctx, int64_t n, double* y, const double* x);                       /* y = x         */
+int nk_fill(nk_ctx* ctx, int64_t n, double* x, double v);                              /* x .= v        */
+int nk_divcopy(nk_ctx* ctx, int64_t n, double* y, const double* x, double s);          /* y = x / s     */
+int nk_ref(nk_ctx* ctx, int64_t n, double* x, double* y, double c, double s);          /* Givens        */
+
+/* ---------------------------------------------------------------- device-resident Krylov solves
+ * krylov_workspace(algo, KrylovConstructor(res)) + krylov_solve!(workspace, J, b; kwargs...)
+ * (src/Ariadne.jl:317-318, :338), restating Krylov.jl 0.10 gmres!/cg! with M = N = I.  The
+ * Arnoldi basis, Hessenberg column and every reduction stay on the device; the host syncs once
+ * per Arnoldi step (Givens update + stopping test), not once per kdot. */
+typedef struct nk_krylov_opts {
+    int32_t restart;              /* gmres: restart = true  (Krylov kwarg)            */
+    int32_t reorthogonalization;  /* gmres: double MGS      (heat_2D.jl:131)          */
+    int32_t itmax;                /* 0 => 2n                                          */
+    int32_t jv_mode;              /* NK_JV_EXACT / NK_JV_FD                           */
+    double atol, rtol;            /* Krylov stopping: ||r|| <= atol + rtol ||b||      */
+} nk_krylov_opts;
+
+typedef struct nk_krylov_stats {
+    int64_t niter;                /* workspace.stats.niter (Arnoldi / CG iterations)  */
+    int32_t solved, inconsistent, breakdown, status; /* status 1 solved 2 tired 3 breakdown 4 zero curvature */
+    int64_t n_matvec;             /* mul!(J) calls incl. restart residuals            */
+} nk_krylov_stats;
+
+/* memory = Krylov workspace memory (GMRES restart length; default 20 like Krylov.jl). */
+int nk_workspace_create(nk_ctx* ctx, int32_t algo, const nk_problem* p, int32_t memory, nk_workspace** out);
+int nk_workspace_destroy(nk_workspace* ws);
+double* nk_workspace_x(nk_workspace* ws);  /* workspace.x (device interior pointer) */
+/* Solve J(u) x = b; F0 = F(u) (FD mode only).  hist (optional, host) receives the residual-norm
+ * estimates (Krylov `history`); *hist_len the number produced (may exceed hist_cap). */
+int nk_krylov_solve(nk_workspace* ws, const nk_problem* p, const double* u, const double* F0, const double* b,
+                    const nk_krylov_opts* opts, nk_krylov_stats* stats, double* hist, int64_t hist_cap,
+                    int64_t* hist_len);
+
+/* ---------------------------------------------------------------- multi-GPU (one process per GPU)
+ * Slab decomposition along the slowest axis; rank r's lower/upper neighbours are r-1 / r+1.
+ * After nk_dist_init every residual / Jv exchanges ghost planes (RCCL send/recv over xGMI) and
+ * every dot / norm is all-reduced (RCCL). */
+int nk_dist_unique_id(char out[128]);
+int nk_dist_init(nk_ctx* ctx, int32_t rank, int32_t nranks, const char id[128]);
+int nk_dist_allreduce_sum(nk_ctx* ctx, double* dev_buf, int64_t count);
+int nk_halo_exchange(nk_ctx* ctx, const nk_problem* p, double* v);
+
+/* ---------------------------------------------------------------- profiling (HIP events, per kernel class) */
+#define NK_PROF_NAME 32
+typedef struct nk_prof_entry {
+    char name[NK_PROF_NAME];
+    int64_t launches;
+    double total_ms;       /* sum of per-launch event durations                            */
+    double bytes;          /* algorithmic bytes (compulsory HBM traffic) summed over launches */
+} nk_prof_entry;
+int nk_prof_enable(nk_ctx* ctx, int32_t on);
+int nk_prof_reset(nk_ctx* ctx);
+int nk_prof_read(nk_ctx* ctx, nk_prof_entry* out, int32_t cap, int32_t* count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NKHIP_H */

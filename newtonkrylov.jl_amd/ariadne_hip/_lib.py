@@ -1,0 +1,121 @@
+"""ctypes binding of libnkhip.so (include/nkhip.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no GPU is visible,
+every compute entry point raises.  (Only loading the library and reading its symbol table
+works without a GPU -- that is what the CPU test-suite checks.)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libnkhip.so")
+HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "nkhip.h")
+
+NK_OK = 0
+NK_BRATU1D, NK_BRATU2D, NK_HEAT2D_EULER, NK_HEAT3D_EULER = 1, 2, 3, 4
+NK_BC_ZERO = 0
+NK_JV_EXACT, NK_JV_FD = 0, 1
+NK_ALGO_GMRES, NK_ALGO_CG = 0, 1
+
+_ERRORS = {-1: "HIP error", -2: "invalid argument", -3: "out of device memory", -4: "RCCL error", -5: "bad state"}
+
+
+class NKError(RuntimeError):
+    pass
+
+
+class nk_problem(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("bc", C.c_int32),
+                ("nx", C.c_int64), ("ny", C.c_int64), ("nz", C.c_int64),
+                ("hx", C.c_double), ("hy", C.c_double), ("hz", C.c_double),
+                ("lam", C.c_double), ("a", C.c_double), ("dt", C.c_double),
+                ("un", C.c_void_p)]
+
+
+class nk_krylov_opts(C.Structure):
+    _fields_ = [("restart", C.c_int32), ("reorthogonalization", C.c_int32), ("itmax", C.c_int32),
+                ("jv_mode", C.c_int32), ("atol", C.c_double), ("rtol", C.c_double)]
+
+
+class nk_krylov_stats(C.Structure):
+    _fields_ = [("niter", C.c_int64), ("solved", C.c_int32), ("inconsistent", C.c_int32),
+                ("breakdown", C.c_int32), ("status", C.c_int32), ("n_matvec", C.c_int64)]
+
+
+class nk_prof_entry(C.Structure):
+    _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("total_ms", C.c_double), ("bytes", C.c_double)]
+
+
+# name -> (restype, argtypes); mirrors include/nkhip.h one to one
+_VP, _I32, _I64, _D, _PD = C.c_void_p, C.c_int32, C.c_int64, C.c_double, C.POINTER(C.c_double)
+_PP = C.POINTER(nk_problem)
+SIGNATURES = {
+    "nk_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "nk_ctx_create": (C.c_int, [C.c_int, C.POINTER(_VP)]),
+    "nk_ctx_destroy": (C.c_int, [_VP]),
+    "nk_last_error": (C.c_char_p, [_VP]),
+    "nk_sync": (C.c_int, [_VP]),
+    "nk_vec_alloc": (C.c_int, [_VP, _PP, C.POINTER(_VP)]),
+    "nk_vec_free": (C.c_int, [_VP, _VP]),
+    "nk_memcpy_h2d": (C.c_int, [_VP, _VP, _VP, _I64]),
+    "nk_memcpy_d2h": (C.c_int, [_VP, _VP, _VP, _I64]),
+    "nk_residual": (C.c_int, [_VP, _PP, _VP, _VP]),
+    "nk_residual_norm": (C.c_int, [_VP, _PP, _VP, _VP, _PD]),
+    "nk_jv": (C.c_int, [_VP, _PP, _VP, _VP, _VP, _VP, _I32, _D]),
+    "nk_dot": (C.c_int, [_VP, _I64, _VP, _VP, _PD]),
+    "nk_norm": (C.c_int, [_VP, _I64, _VP, _PD]),
+    "nk_scal": (C.c_int, [_VP, _I64, _D, _VP]),
+    "nk_axpy": (C.c_int, [_VP, _I64, _D, _VP, _VP]),
+    "nk_axpby": (C.c_int, [_VP, _I64, _D, _VP, _D, _VP]),
+    "nk_copy": (C.c_int, [_VP, _I64, _VP, _VP]),
+    "nk_fill": (C.c_int, [_VP, _I64, _VP, _D]),
+    "nk_divcopy": (C.c_int, [_VP, _I64, _VP, _VP, _D]),
+    "nk_ref": (C.c_int, [_VP, _I64, _VP, _VP, _D, _D]),
+    "nk_workspace_create": (C.c_int, [_VP, _I32, _PP, _I32, C.POINTER(_VP)]),
+    "nk_workspace_destroy": (C.c_int, [_VP]),
+    "nk_workspace_x": (_VP, [_VP]),
+    "nk_krylov_solve": (C.c_int, [_VP, _PP, _VP, _VP, _VP, C.POINTER(nk_krylov_opts), C.POINTER(nk_krylov_stats),
+                                  _PD, _I64, C.POINTER(_I64)]),
+    "nk_dist_unique_id": (C.c_int, [C.c_char_p]),
+    "nk_dist_init": (C.c_int, [_VP, _I32, _I32, C.c_char_p]),
+    "nk_dist_allreduce_sum": (C.c_int, [_VP, _VP, _I64]),
+    "nk_halo_exchange": (C.c_int, [_VP, _PP, _VP]),
+    "nk_prof_enable": (C.c_int, [_VP, _I32]),
+    "nk_prof_reset": (C.c_int, [_VP]),
+    "nk_prof_read": (C.c_int, [_VP, C.POINTER(nk_prof_entry), _I32, C.POINTER(_I32)]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libnkhip.so (built in-tree by __graft_entry__.build() / `make -C newtonkrylov.jl_amd`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NKError(f"libnkhip.so not built ({LIB_PATH}); run `make -C newtonkrylov.jl_amd` -- "
+                          "there is no CPU fallback")
+        lib = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(lib, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, ctx=None, what: str = ""):
+    if rc != NK_OK:
+        msg = ""
+        if ctx is not None:
+            m = load().nk_last_error(ctx)
+            msg = m.decode() if m else ""
+        raise NKError(f"{what}: {_ERRORS.get(rc, rc)} {msg}".strip())
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    rc = load().nk_device_count(C.byref(n))
+    return n.value if rc == NK_OK else 0

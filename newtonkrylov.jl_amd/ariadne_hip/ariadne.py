@@ -1,0 +1,193 @@
+"""Host mirror of Ariadne's public API (src/Ariadne.jl) on the HIP path.
+
+Same names (Julia `!` -> trailing `_`), same keyword arguments and defaults, same control flow
+and the same error behaviour (non-finite residual -> log + break, `solved = n_res <= tol`).
+The Newton loop is host code, as in the reference; every O(n) operation it triggers runs in
+libnkhip.so: the residual stencil, the fused Jv kernel and the device-resident Krylov solve.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import logging
+import math
+import time
+from dataclasses import dataclass
+from typing import NamedTuple
+
+from . import _lib
+from ._lib import load
+from .device import DeviceArray
+from .krylov import KrylovConstructor, kaxpy_, krylov_solve_, krylov_workspace
+from .problems import DeviceResidual
+
+log = logging.getLogger("ariadne_hip")
+
+
+# ----------------------------------------------------------------------------- forcing (Ariadne.jl:180-217)
+class Forcing:
+    """Forcing term η of the inexact Newton condition ‖F′(u)d + F(u)‖ <= η ‖F(u)‖."""
+
+
+@dataclass(frozen=True)
+class Fixed(Forcing):
+    """Fixed(η = 0.1) -- src/Ariadne.jl:185-192."""
+    eta: float = 0.1
+
+    def __call__(self, *args):
+        return self.eta
+
+    def initial(self):
+        return self.eta
+
+
+@dataclass(frozen=True)
+class EisenstatWalker(Forcing):
+    """EisenstatWalker(η_max = 0.999, γ = 0.9) -- src/Ariadne.jl:197-217."""
+    eta_max: float = 0.999
+    gamma: float = 0.9
+
+    def __call__(self, eta, tol, n_res, n_res_prior):
+        eta_res = self.gamma * n_res ** 2 / n_res_prior ** 2
+        # Eq 3.6; `γ η^2 <= 1 // 10` is an exact rational comparison, i.e. `< 0.1` for a double
+        if self.gamma * eta ** 2 < 0.1:
+            eta_safe = min(self.eta_max, eta_res)
+        else:
+            eta_safe = min(self.eta_max, max(eta_res, self.gamma * eta ** 2))
+        return min(self.eta_max, max(eta_safe, 0.5 * tol / n_res))  # Eq 3.5
+
+    def initial(self):
+        return self.eta_max
+
+
+# ----------------------------------------------------------------------------- Jacobian operator
+class JacobianOperator:
+    """JacobianOperator(F!, res, u, p) -- src/Ariadne.jl:34-46.
+
+    Holds (F, res, u, p) by reference like the reference.  `mul_(out, J, v)` is the device Jv:
+    jv="exact" is the dual-number tangent of F (the value Enzyme's forward mode computes in the
+    reference's mul!), jv="fd" the north-star operator (F(u + ε v) - F(u)) / ε with F(u) = res.
+    """
+
+    def __init__(self, f: DeviceResidual, res: DeviceArray, u: DeviceArray, p=None, jv: str = "exact"):
+        if not isinstance(f, DeviceResidual):
+            raise TypeError("the HIP JacobianOperator needs a device residual (ariadne_hip.problems); "
+                            "generic Python callables have no kernel")
+        if jv not in ("exact", "fd"):
+            raise ValueError("jv must be 'exact' or 'fd'")
+        self.f, self.res, self.u, self.p = f, res, u, p
+        self.jv = jv
+
+    @property
+    def jv_mode(self) -> int:
+        return _lib.NK_JV_FD if self.jv == "fd" else _lib.NK_JV_EXACT
+
+    def problem(self) -> _lib.nk_problem:
+        return self.f.problem(self.u, self.p)
+
+    @property
+    def size(self):
+        return (len(self.res), len(self.u))
+
+    @property
+    def eltype(self):
+        return float
+
+    def __len__(self):
+        return self.size[0] * self.size[1]
+
+
+def mul_(out: DeviceArray, J: JacobianOperator, v: DeviceArray, eps: float = 0.0):
+    """mul!(out, J, v) (src/Ariadne.jl:48-57).  Unlike Enzyme it does not rewrite J.res."""
+    prob = J.problem()
+    F0 = J.res.ptr if J.jv_mode == _lib.NK_JV_FD else None
+    out.ctx.check(load().nk_jv(out.ctx.handle, C.byref(prob), out.ptr, J.u.ptr, v.ptr, F0, J.jv_mode, float(eps)),
+                  "mul!(out, J, v)")
+    return None
+
+
+# ----------------------------------------------------------------------------- Newton-Krylov
+class Stats(NamedTuple):
+    """Stats(outer_iterations, inner_iterations, n_res) -- src/Ariadne.jl:265-276."""
+    outer_iterations: int
+    inner_iterations: int
+    n_res: float
+
+    def update(self, inner_iterations: int, n_res: float) -> "Stats":
+        return Stats(self.outer_iterations + 1, self.inner_iterations + inner_iterations, n_res)
+
+
+class Result(NamedTuple):
+    """(; solved, stats, t) -- src/Ariadne.jl:370-371."""
+    solved: bool
+    stats: Stats
+    t: float
+
+
+def newton_krylov_(F_: DeviceResidual, u: DeviceArray, p=None, res: DeviceArray | None = None, *,
+                   tol_rel: float = 1.0e-6, tol_abs: float = 1.0e-12, max_niter: int = 50,
+                   forcing: Forcing | None = EisenstatWalker(), verbose: int = 0, algo: str = "gmres",
+                   M=None, N=None, krylov_kwargs: dict | None = None, callback=None, memory: int = 20,
+                   jv: str = "exact", workspace=None):
+    """newton_krylov!(F!, u, p, res; kwargs...) -- src/Ariadne.jl:288-372 (and the 3-arg form :259-263).
+
+    Additions of the HIP path: `memory` (Krylov workspace memory = GMRES restart length),
+    `jv` ("exact" | "fd") and `workspace` (re-use a Krylov workspace across calls -- the
+    reference's own TODO at :316); everything else keeps the reference's meaning and default.
+    """
+    if M is not None or N is not None:
+        raise NotImplementedError("preconditioner factories M/N are out of scope for the HIP path (SURVEY.md §2 C15)")
+    callback = callback or (lambda *a: None)
+    krylov_kwargs = dict(krylov_kwargs or {})
+    t0 = time.perf_counter_ns()
+    if res is None:
+        res = u.zero()  # similar(u₀); Enzyme.make_zero!(res)   (:260-261)
+    n = len(u)
+    n_res = F_.residual_norm(res, u, p)  # F!(res, u, p); n_res = norm(res)   (:302-303)
+    callback(u, res, n_res)
+
+    tol = tol_rel * n_res + tol_abs
+    eta = forcing.initial() if forcing is not None else None
+    if verbose > 0:
+        log.info("Jacobian-Free Newton-Krylov algo=%s res0=%g tol=%g tol_rel=%g tol_abs=%g eta=%s",
+                 algo, n_res, tol, tol_rel, tol_abs, eta)
+
+    J = JacobianOperator(F_, res, u, p, jv=jv)
+    own_ws = workspace is None
+    if own_ws:
+        workspace = krylov_workspace(algo, KrylovConstructor(res, memory=memory))
+    elif workspace.algo != str(algo).lstrip(":"):
+        raise ValueError("workspace algo does not match `algo`")
+
+    stats = Stats(0, 0, n_res)
+    while n_res > tol and stats.outer_iterations <= max_niter:
+        kwargs = dict(krylov_kwargs)
+        if forcing is not None:
+            kwargs = {"rtol": eta, **kwargs}  # user krylov_kwargs win (:330-333)
+        # Solve J d = F(u).  The reference passes copy(res) because Enzyme rewrites res inside
+        # mul!; the device operator never writes res, so res itself is the right-hand side.
+        krylov_solve_(workspace, J, res, **kwargs)
+        d = workspace.x
+        kaxpy_(n, -1.0, d, u)  # u .-= 1 .* d  (Newton step s = 1, :341-344)
+        n_res_prior = n_res
+        n_res = F_.residual_norm(res, u, p)
+        callback(u, res, n_res)
+        if math.isinf(n_res) or math.isnan(n_res):
+            log.error("Inner solver blew up: %s", stats)
+            break
+        if forcing is not None:
+            eta = forcing(eta, tol, n_res, n_res_prior)
+        if verbose > 0 and workspace.stats.niter == 0 and forcing is not None:
+            log.info("Inexact Newton thinks our step is good enough eta=%g %s", eta, stats)
+        stats = stats.update(workspace.stats.niter, n_res)
+        if verbose > 0:
+            log.info("Newton iter=%g eta=%s %s", n_res, eta, stats)
+    t = (time.perf_counter_ns() - t0) / 1.0e9
+    if own_ws:
+        workspace.free()
+    return u, Result(n_res <= tol, stats, t)
+
+
+def newton_krylov(F: DeviceResidual, u0: DeviceArray, p=None, **kwargs):
+    """newton_krylov(F, u₀, p; kwargs...) -- out-of-place form (src/Ariadne.jl:245-248).
+    The device residual computes in place; u₀ is not modified."""
+    return newton_krylov_(F, u0.copy(), p, **kwargs)

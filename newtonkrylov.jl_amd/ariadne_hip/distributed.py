@@ -1,0 +1,38 @@
+"""Multi-GPU setup: one process per GPU, slab decomposition, RCCL inside libnkhip.so.
+
+torch.distributed (gloo) is only the control plane here: it broadcasts RCCL's unique id from
+rank 0; the data path (ghost planes, inner products) is RCCL over xGMI on the library's stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from ._lib import NKError, load
+from .device import Context, Grid
+
+
+def dist_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    if load().nk_dist_unique_id(buf) != 0:
+        raise NKError("ncclGetUniqueId failed")
+    return buf.raw
+
+
+def slab(global_xyz, rank: int, nranks: int) -> Grid:
+    """Split the slowest axis into `nranks` contiguous slabs (sizes differ by at most one plane)."""
+    g = tuple(int(d) for d in global_xyz)
+    nslow = g[-1]
+    if nslow < nranks:
+        raise ValueError("fewer planes than ranks")
+    base, extra = divmod(nslow, nranks)
+    sizes = [base + (1 if r < extra else 0) for r in range(nranks)]
+    off = sum(sizes[:rank])
+    return Grid(g[:-1] + (sizes[rank],), g, off)
+
+
+def init_distributed(ctx: Context, rank: int, nranks: int, broadcast_object) -> None:
+    """Create the RCCL communicator of `ctx`; `broadcast_object(obj, src)` returns rank 0's object
+    (e.g. built on torch.distributed.broadcast_object_list)."""
+    uid = dist_unique_id() if rank == 0 else None
+    uid = broadcast_object(uid, 0)
+    ctx.init_distributed(rank, nranks, uid)

@@ -1,0 +1,164 @@
+"""Krylov.jl's plug-in surface on device vectors.
+
+* vector primitives `kdot, knorm, kscal_, kaxpy_, kaxpby_, kcopy_, kfill_, kdivcopy_, kref_`:
+  the overload points `examples/halovector.jl:51-147` implements for HaloVector -- here each is
+  one HIP kernel (dot/norm return host scalars, as in Krylov.jl);
+* `KrylovConstructor`, `krylov_workspace`, `krylov_solve_`: what Ariadne calls at
+  src/Ariadne.jl:317-318 and :338.  The solve runs the device-resident GMRES / CG of
+  libnkhip.so (nk_krylov_solve), a restatement of Krylov.jl 0.10.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import load
+from .device import DeviceArray
+
+SQRT_EPS = math.sqrt(np.finfo(np.float64).eps)
+
+
+def _h(x: DeviceArray):
+    return x.ctx.handle
+
+
+# -------------------------------------------------------------------------- vector primitives
+def kdot(n: int, x: DeviceArray, y: DeviceArray) -> float:
+    out = C.c_double()
+    x.ctx.check(load().nk_dot(_h(x), n, x.ptr, y.ptr, C.byref(out)), "kdot")
+    return out.value
+
+
+def knorm(n: int, x: DeviceArray) -> float:
+    out = C.c_double()
+    x.ctx.check(load().nk_norm(_h(x), n, x.ptr, C.byref(out)), "knorm")
+    return out.value
+
+
+def kscal_(n: int, s: float, x: DeviceArray):
+    x.ctx.check(load().nk_scal(_h(x), n, float(s), x.ptr), "kscal!")
+    return x
+
+
+def kaxpy_(n: int, s: float, x: DeviceArray, y: DeviceArray):
+    y.ctx.check(load().nk_axpy(_h(y), n, float(s), x.ptr, y.ptr), "kaxpy!")
+    return y
+
+
+def kaxpby_(n: int, s: float, x: DeviceArray, t: float, y: DeviceArray):
+    y.ctx.check(load().nk_axpby(_h(y), n, float(s), x.ptr, float(t), y.ptr), "kaxpby!")
+    return y
+
+
+def kcopy_(n: int, y: DeviceArray, x: DeviceArray):
+    y.ctx.check(load().nk_copy(_h(y), n, y.ptr, x.ptr), "kcopy!")
+    return y
+
+
+def kfill_(x: DeviceArray, val: float):
+    x.ctx.check(load().nk_fill(_h(x), x.n, x.ptr, float(val)), "kfill!")
+    return x
+
+
+def kdivcopy_(n: int, y: DeviceArray, x: DeviceArray, s: float):
+    y.ctx.check(load().nk_divcopy(_h(y), n, y.ptr, x.ptr, float(s)), "kdivcopy!")
+    return y
+
+
+def kref_(n: int, x: DeviceArray, y: DeviceArray, c: float, s: float):
+    x.ctx.check(load().nk_ref(_h(x), n, x.ptr, y.ptr, float(c), float(s)), "kref!")
+    return x, y
+
+
+# -------------------------------------------------------------------------- workspace / solve
+@dataclass
+class KrylovConstructor:
+    """KrylovConstructor(res) (src/Ariadne.jl:317): workspace vectors follow `similar(res)`.
+
+    `memory` is Krylov.jl's workspace argument (default 20).  Ariadne cannot forward it
+    (SURVEY.md §8a A1); the host mirror exposes it so GMRES(30) (BASELINE config 2) is expressible.
+    """
+    vm: DeviceArray
+    memory: int = 20
+
+
+@dataclass
+class KrylovStats:
+    niter: int = 0
+    solved: bool = False
+    inconsistent: bool = False
+    status: str = "unknown"
+    n_matvec: int = 0
+    residuals: list = field(default_factory=list)
+
+
+_STATUS = {0: "unknown", 1: "solution good enough given atol and rtol", 2: "maximum number of iterations exceeded",
+           3: "breakdown", 4: "zero curvature detected"}
+_ALGOS = {"gmres": _lib.NK_ALGO_GMRES, "cg": _lib.NK_ALGO_CG}
+
+
+class KrylovWorkspace:
+    """krylov_workspace(algo, kc): device basis + x, allocated once and reused every Newton step."""
+
+    def __init__(self, algo: str, kc: KrylovConstructor):
+        if algo not in _ALGOS:
+            raise NotImplementedError(f"algo = :{algo} -- the HIP path implements :gmres and :cg "
+                                      "(other Krylov methods are out of scope, SURVEY.md §2 C16)")
+        self.algo = algo
+        self.memory = int(kc.memory)
+        self.ctx = kc.vm.ctx
+        self.grid = kc.vm.grid
+        gp = self.grid.geometry_problem()
+        h = C.c_void_p()
+        self.ctx.check(load().nk_workspace_create(self.ctx.handle, _ALGOS[algo], C.byref(gp), self.memory, C.byref(h)),
+                       "krylov_workspace")
+        self.handle = h
+        self.x = DeviceArray(self.grid, self.ctx, _ptr=load().nk_workspace_x(h))
+        self.stats = KrylovStats()
+
+    def free(self):
+        if getattr(self, "handle", None) and self.ctx.handle:
+            load().nk_workspace_destroy(self.handle)
+        self.handle = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def krylov_workspace(algo, kc: KrylovConstructor) -> KrylovWorkspace:
+    return KrylovWorkspace(str(algo).lstrip(":"), kc)
+
+
+def krylov_solve_(ws: KrylovWorkspace, J, b: DeviceArray, *, restart=False, reorthogonalization=False,
+                  atol=SQRT_EPS, rtol=SQRT_EPS, itmax=0, history=False, verbose=0, M=None, N=None, ldiv=False,
+                  **unknown):
+    """krylov_solve!(workspace, J, b; kwargs...) for a JacobianOperator J on device vectors."""
+    if unknown:
+        raise TypeError(f"unsupported Krylov keyword(s): {sorted(unknown)}")
+    if M is not None or N is not None:
+        raise NotImplementedError("preconditioners M/N are out of scope for the HIP path (SURVEY.md §2 C15)")
+    if ws.algo == "cg" and (restart or reorthogonalization):
+        raise TypeError("restart / reorthogonalization are GMRES keywords")
+    prob = J.problem()
+    opts = _lib.nk_krylov_opts(int(bool(restart)), int(bool(reorthogonalization)), int(itmax), J.jv_mode,
+                               float(atol), float(rtol))
+    st = _lib.nk_krylov_stats()
+    cap = ((int(itmax) or 4096) + 64) if history else 0
+    hist = (C.c_double * max(cap, 1))()
+    hl = C.c_int64(0)
+    F0 = J.res.ptr if J.jv_mode == _lib.NK_JV_FD else None
+    ws.ctx.check(load().nk_krylov_solve(ws.handle, C.byref(prob), J.u.ptr, F0, b.ptr, C.byref(opts), C.byref(st),
+                                        hist, cap, C.byref(hl)), "krylov_solve!")
+    ws.stats = KrylovStats(niter=int(st.niter), solved=bool(st.solved), inconsistent=bool(st.inconsistent),
+                           status=_STATUS.get(st.status, "unknown"), n_matvec=int(st.n_matvec),
+                           residuals=list(hist[: min(hl.value, cap)]) if history else [])
+    if verbose:
+        print(f"{ws.algo.upper()}: niter={ws.stats.niter} status={ws.stats.status}")
+    return ws

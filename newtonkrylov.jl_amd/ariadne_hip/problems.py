@@ -1,0 +1,105 @@
+"""Device residuals: the `F!(res, u, p)` callbacks of the reference examples, as HIP stencils.
+
+A `DeviceResidual` is called exactly like the reference's residual functions, with the same
+parameter tuples, but it launches a hand-written gfx950 kernel (nk_residual) instead of a Julia
+loop, and `JacobianOperator` maps it to the matching fused Jv kernel (nk_jv) instead of Enzyme.
+
+| object        | reference                                             | p                                   |
+|---------------|-------------------------------------------------------|-------------------------------------|
+| `bratu_`      | `bratu!(res, y, (Δx, λ))`  examples/bratu.jl:14-24    | `(dx, lam)`                          |
+| `bratu2d_`    | 2D generalisation                  | `(dx, dy, lam)`                      |
+| `heat2d_euler_` | `G_Euler!` ∘ `diffusion!` implicit.jl:8-13 + heat_2D.jl:45-62 | `(u_n, dt, du, (a, dx, dy, bc_zero_), t)` |
+| `heat3d_euler_` | 3D generalisation                | `(u_n, dt, du, (a, dx, dy, dz, bc_zero_), t)` |
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from . import _lib
+from ._lib import load
+from .device import DeviceArray
+
+
+def bc_zero_(u):
+    """`bc_zero!` (heat_2D.jl:28-38): zero ghost cells.  DeviceArray ghosts are zero by
+    construction (or hold the neighbour slab's plane), so this is a marker, not an action."""
+    return None
+
+
+class DeviceResidual:
+    """F!(res, u, p) backed by a HIP stencil kernel."""
+
+    kind: int
+    name: str
+
+    def problem(self, u: DeviceArray, p) -> _lib.nk_problem:
+        raise NotImplementedError
+
+    def __call__(self, res: DeviceArray, u: DeviceArray, p=None):
+        prob = self.problem(u, p)
+        u.ctx.check(load().nk_residual(u.ctx.handle, C.byref(prob), res.ptr, u.ptr), f"{self.name}")
+        return None
+
+    def residual_norm(self, res: DeviceArray, u: DeviceArray, p=None) -> float:
+        """F!(res, u, p); norm(res) as one fused pass (src/Ariadne.jl:302-303, :349-350)."""
+        prob = self.problem(u, p)
+        out = C.c_double()
+        u.ctx.check(load().nk_residual_norm(u.ctx.handle, C.byref(prob), res.ptr, u.ptr, C.byref(out)), self.name)
+        return out.value
+
+    def __repr__(self):
+        return self.name
+
+
+class _Bratu1D(DeviceResidual):
+    kind, name = _lib.NK_BRATU1D, "bratu!"
+
+    def problem(self, u, p):
+        dx, lam = p
+        if u.grid.dim != 1:
+            raise ValueError("bratu! is the 1D problem")
+        nx, ny, nz = u.grid.nxyz
+        return _lib.nk_problem(self.kind, 0, nx, 1, 1, float(dx), 1.0, 1.0, float(lam), 0.0, 0.0, None)
+
+
+class _Bratu2D(DeviceResidual):
+    kind, name = _lib.NK_BRATU2D, "bratu2d!"
+
+    def problem(self, u, p):
+        dx, dy, lam = p
+        if u.grid.dim != 2:
+            raise ValueError("bratu2d! needs a 2D grid")
+        nx, ny, _ = u.grid.nxyz
+        return _lib.nk_problem(self.kind, 0, nx, ny, 1, float(dx), float(dy), 1.0, float(lam), 0.0, 0.0, None)
+
+
+class _HeatEuler(DeviceResidual):
+    """F!(res, u, (uₙ, Δt, du, p, t)) = G_Euler!(res, uₙ, Δt, diffusion!, du, u, p, t)."""
+
+    def __init__(self, dim: int):
+        self.dim = dim
+        self.kind = _lib.NK_HEAT2D_EULER if dim == 2 else _lib.NK_HEAT3D_EULER
+        self.name = f"G_Euler!∘diffusion{dim}d!"
+
+    def problem(self, u, p):
+        un, dt, _du, fp, _t = p
+        if u.grid.dim != self.dim:
+            raise ValueError(f"{self.name} needs a {self.dim}D grid")
+        if self.dim == 2:
+            a, dx, dy, bc = fp
+            dz = 1.0
+        else:
+            a, dx, dy, dz, bc = fp
+        if bc is not bc_zero_:
+            raise NotImplementedError("only bc_zero! is implemented on the device (periodic BC: SURVEY.md §8f)")
+        if not isinstance(un, DeviceArray) or un.grid != u.grid:
+            raise ValueError("u_n must be a DeviceArray on u's grid")
+        nx, ny, nz = u.grid.nxyz
+        return _lib.nk_problem(self.kind, 0, nx, ny, nz, float(dx), float(dy), float(dz), 0.0, float(a), float(dt),
+                               un.ptr)
+
+
+bratu_ = _Bratu1D()
+bratu2d_ = _Bratu2D()
+heat2d_euler_ = _HeatEuler(2)
+heat3d_euler_ = _HeatEuler(3)

@@ -1,0 +1,341 @@
+// nk_core.cpp -- context, device memory, profiling and the C-ABI wrappers of the residual,
+// Jacobian operator and Krylov vector primitives (include/nkhip.h).
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+
+#include "nk_internal.hpp"
+
+namespace nk {
+
+int fail(nk_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+int geometry(nk_ctx* c, const nk_problem* p, Geo* g) {
+    if (!p) return fail(c, NK_E_ARG, "null problem");
+    if (p->nx < 1 || p->ny < 1 || p->nz < 1) return fail(c, NK_E_ARG, "grid extents must be >= 1");
+    switch (p->kind) {
+    case NK_BRATU1D:
+        if (p->ny != 1 || p->nz != 1) return fail(c, NK_E_ARG, "1D problem needs ny = nz = 1");
+        g->dim = 1; g->plane = 1; g->nplanes = p->nx;
+        break;
+    case NK_BRATU2D:
+    case NK_HEAT2D_EULER:
+        if (p->nz != 1) return fail(c, NK_E_ARG, "2D problem needs nz = 1");
+        g->dim = 2; g->plane = p->nx; g->nplanes = p->ny;
+        break;
+    case NK_HEAT3D_EULER:
+        g->dim = 3; g->plane = p->nx * p->ny; g->nplanes = p->nz;
+        break;
+    default:
+        return fail(c, NK_E_ARG, "unknown problem kind");
+    }
+    if (p->bc != NK_BC_ZERO) return fail(c, NK_E_ARG, "only zero-Dirichlet boundaries are implemented");
+    if ((p->kind == NK_HEAT2D_EULER || p->kind == NK_HEAT3D_EULER) && !p->un)
+        return fail(c, NK_E_ARG, "heat problem needs u_n");
+    g->n = p->nx * p->ny * p->nz;
+    g->front = (g->plane + 31) / 32 * 32;
+    return NK_OK;
+}
+
+double* red_slot(nk_ctx* c) {
+    double* s = c->red + (size_t)c->red_next * kRedCap;
+    c->red_next = (c->red_next + 1) % kRedSlots;
+    return s;
+}
+
+int finish_reduction(nk_ctx* c, Red* r) {
+    if (c->nranks <= 1) return NK_OK;
+    // collapse this rank's partials to one scalar, then sum the scalars over ranks (RCCL)
+    double* dst = red_slot(c);
+    NK_TRY(launch_finalize(c, *r, dst, 0));
+    NK_TRY(allreduce_scalar(c, dst, 1));
+    r->ptr = dst;
+    r->len = 1;
+    return NK_OK;
+}
+
+// ---------------------------------------------------------------- profiling
+int kid(nk_ctx* c, const char* name) {
+    auto it = c->kid_of.find(name);
+    if (it != c->kid_of.end()) return it->second;
+    const int k = (int)c->kid_names.size();
+    c->kid_of[name] = k;
+    c->kid_names.push_back(name);
+    c->acc.emplace_back();
+    return k;
+}
+
+static int get_event(nk_ctx* c, hipEvent_t* e) {
+    if (!c->ev_pool.empty()) {
+        *e = c->ev_pool.back();
+        c->ev_pool.pop_back();
+        return NK_OK;
+    }
+    NK_HIP(c, hipEventCreate(e));
+    return NK_OK;
+}
+
+int prof_begin(nk_ctx* c, hipEvent_t* a) {
+    NK_TRY(get_event(c, a));
+    NK_HIP(c, hipEventRecord(*a, c->stream));
+    return NK_OK;
+}
+
+int prof_end(nk_ctx* c, int k, hipEvent_t a, double bytes) {
+    hipEvent_t b;
+    NK_TRY(get_event(c, &b));
+    NK_HIP(c, hipEventRecord(b, c->stream));
+    c->pending.push_back({k, a, b, bytes});
+    if (c->pending.size() > 8192) prof_drain(c, false);
+    return NK_OK;
+}
+
+void prof_drain(nk_ctx* c, bool blocking) {
+    size_t done = 0;
+    for (; done < c->pending.size(); ++done) {
+        ProfPending& p = c->pending[done];
+        if (blocking) {
+            (void)hipEventSynchronize(p.b);
+        } else if (hipEventQuery(p.b) != hipSuccess) {
+            break;
+        }
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, p.a, p.b);
+        c->acc[p.kid].launches += 1;
+        c->acc[p.kid].ms += ms;
+        c->acc[p.kid].bytes += p.bytes;
+        c->ev_pool.push_back(p.a);
+        c->ev_pool.push_back(p.b);
+    }
+    c->pending.erase(c->pending.begin(), c->pending.begin() + done);
+}
+
+}  // namespace nk
+
+using namespace nk;
+
+// =====================================================================================  C ABI
+extern "C" {
+
+int nk_device_count(int* count) {
+    if (!count) return NK_E_ARG;
+    hipError_t e = hipGetDeviceCount(count);
+    if (e != hipSuccess) {
+        *count = 0;
+        return NK_E_HIP;
+    }
+    return NK_OK;
+}
+
+int nk_ctx_create(int device, nk_ctx** out) {
+    if (!out) return NK_E_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return NK_E_HIP;
+    if (device < 0 || device >= ndev) return NK_E_ARG;
+    nk_ctx* c = new nk_ctx();
+    c->device = device;
+    auto bail = [&](int code) {
+        delete c;
+        return code;
+    };
+    if (hipSetDevice(device) != hipSuccess) return bail(NK_E_HIP);
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bail(NK_E_HIP);
+    if (hipMalloc(&c->red, sizeof(double) * (size_t)kRedSlots * kRedCap) != hipSuccess) return bail(NK_E_NOMEM);
+    if (hipMalloc(&c->scal, sizeof(double) * kScalCap) != hipSuccess) return bail(NK_E_NOMEM);
+    if (hipHostMalloc(&c->hpin, sizeof(double) * kScalCap, hipHostMallocDefault) != hipSuccess) return bail(NK_E_NOMEM);
+    if (hipMemset(c->red, 0, sizeof(double) * (size_t)kRedSlots * kRedCap) != hipSuccess) return bail(NK_E_HIP);
+    if (hipMemset(c->scal, 0, sizeof(double) * kScalCap) != hipSuccess) return bail(NK_E_HIP);
+    *out = c;
+    return NK_OK;
+}
+
+int nk_dist_free(nk_ctx* ctx);  // nk_dist.cpp
+
+int nk_ctx_destroy(nk_ctx* c) {
+    if (!c) return NK_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    nk_dist_free(c);
+    for (auto& kv : c->allocs) (void)hipFree(kv.second);
+    for (auto& p : c->pending) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    (void)hipFree(c->red);
+    (void)hipFree(c->scal);
+    (void)hipHostFree(c->hpin);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return NK_OK;
+}
+
+const char* nk_last_error(nk_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int nk_sync(nk_ctx* c) {
+    if (!c) return NK_E_ARG;
+    NK_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->prof) prof_drain(c, false);
+    return NK_OK;
+}
+
+int nk_vec_alloc(nk_ctx* c, const nk_problem* p, double** out) {
+    if (!c || !out) return NK_E_ARG;
+    Geo g;
+    NK_TRY(geometry(c, p, &g));
+    const size_t total = (size_t)(g.front + g.n + g.plane + 32);
+    void* base = nullptr;
+    if (hipMalloc(&base, total * sizeof(double)) != hipSuccess) return fail(c, NK_E_NOMEM, "hipMalloc failed (vector)");
+    NK_HIP(c, hipMemsetAsync(base, 0, total * sizeof(double), c->stream));
+    NK_HIP(c, hipStreamSynchronize(c->stream));
+    double* interior = static_cast<double*>(base) + g.front;
+    c->allocs[interior] = base;
+    *out = interior;
+    return NK_OK;
+}
+
+int nk_vec_free(nk_ctx* c, double* v) {
+    if (!c) return NK_E_ARG;
+    auto it = c->allocs.find(v);
+    if (it == c->allocs.end()) return fail(c, NK_E_ARG, "nk_vec_free: not a vector of this context");
+    NK_HIP(c, hipStreamSynchronize(c->stream));
+    NK_HIP(c, hipFree(it->second));
+    c->allocs.erase(it);
+    return NK_OK;
+}
+
+int nk_memcpy_h2d(nk_ctx* c, double* dst, const double* src, int64_t n) {
+    if (!c || n < 0) return NK_E_ARG;
+    NK_HIP(c, hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    NK_HIP(c, hipStreamSynchronize(c->stream));
+    return NK_OK;
+}
+
+int nk_memcpy_d2h(nk_ctx* c, double* dst, const double* src, int64_t n) {
+    if (!c || n < 0) return NK_E_ARG;
+    NK_HIP(c, hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    NK_HIP(c, hipStreamSynchronize(c->stream));
+    return NK_OK;
+}
+
+// ---------------------------------------------------------------- residual / Jv
+int nk_residual(nk_ctx* c, const nk_problem* p, double* res, const double* u) {
+    if (!c || !res || !u) return NK_E_ARG;
+    NK_TRY(halo_exchange(c, p, u));
+    StencilIn in{p, MODE_RES, EPI_NONE, res, u, nullptr, nullptr, nullptr, 0.0};
+    Red r{};
+    return launch_stencil(c, in, &r);
+}
+
+int nk_residual_norm(nk_ctx* c, const nk_problem* p, double* res, const double* u, double* n_res) {
+    if (!c || !res || !u || !n_res) return NK_E_ARG;
+    NK_TRY(halo_exchange(c, p, u));
+    StencilIn in{p, MODE_RES, EPI_SUMSQ, res, u, nullptr, nullptr, nullptr, 0.0};
+    Red r{};
+    NK_TRY(launch_stencil(c, in, &r));
+    NK_TRY(finish_reduction(c, &r));
+    NK_TRY(launch_finalize(c, r, c->scal, 1));
+    NK_HIP(c, hipMemcpyAsync(c->hpin, c->scal, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    NK_TRY(nk_sync(c));
+    *n_res = c->hpin[0];
+    return NK_OK;
+}
+
+int nk_jv(nk_ctx* c, const nk_problem* p, double* out, const double* u, const double* v, const double* F0, int32_t mode,
+          double eps) {
+    if (!c || !out || !u || !v) return NK_E_ARG;
+    if (mode != NK_JV_EXACT && mode != NK_JV_FD) return fail(c, NK_E_ARG, "bad Jv mode");
+    Geo g;
+    NK_TRY(geometry(c, p, &g));
+    if (mode == NK_JV_FD) {
+        if (!F0) return fail(c, NK_E_ARG, "FD Jv needs F0 = F(u)");
+        if (eps <= 0.0) {
+            double un = 0.0, vn = 0.0;
+            NK_TRY(nk_norm(c, g.n, u, &un));
+            NK_TRY(nk_norm(c, g.n, v, &vn));
+            if (vn == 0.0) return launch_fill(c, g.n, out, 0.0);
+            eps = std::sqrt(DBL_EPSILON) * std::fmax(1.0, un) / vn;
+        }
+    }
+    NK_TRY(halo_exchange(c, p, u));
+    NK_TRY(halo_exchange(c, p, v));
+    StencilIn in{p, mode == NK_JV_FD ? MODE_JFD : MODE_JEXACT, EPI_NONE, out, u, v, F0, nullptr, eps};
+    Red r{};
+    return launch_stencil(c, in, &r);
+}
+
+// ---------------------------------------------------------------- Krylov vector primitives
+static int scalar_result(nk_ctx* c, Red r, int sqrt_it, double* out) {
+    NK_TRY(finish_reduction(c, &r));
+    NK_TRY(launch_finalize(c, r, c->scal, sqrt_it));
+    NK_HIP(c, hipMemcpyAsync(c->hpin, c->scal, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    NK_TRY(nk_sync(c));
+    *out = c->hpin[0];
+    return NK_OK;
+}
+
+int nk_dot(nk_ctx* c, int64_t n, const double* x, const double* y, double* out) {
+    if (!c || !out || n < 0) return NK_E_ARG;
+    Red r{};
+    NK_TRY(launch_dot(c, n, x, y, &r));
+    return scalar_result(c, r, 0, out);
+}
+
+int nk_norm(nk_ctx* c, int64_t n, const double* x, double* out) {
+    if (!c || !out || n < 0) return NK_E_ARG;
+    Red r{};
+    NK_TRY(launch_sumsq(c, n, x, &r));
+    return scalar_result(c, r, 1, out);
+}
+
+int nk_scal(nk_ctx* c, int64_t n, double s, double* x) { return c ? launch_scal(c, n, s, x) : NK_E_ARG; }
+int nk_axpy(nk_ctx* c, int64_t n, double s, const double* x, double* y) { return c ? launch_axpy(c, n, s, x, y) : NK_E_ARG; }
+int nk_axpby(nk_ctx* c, int64_t n, double s, const double* x, double t, double* y) {
+    return c ? launch_axpby(c, n, s, x, t, y) : NK_E_ARG;
+}
+int nk_copy(nk_ctx* c, int64_t n, double* y, const double* x) { return c ? launch_copy(c, n, y, x) : NK_E_ARG; }
+int nk_fill(nk_ctx* c, int64_t n, double* x, double v) { return c ? launch_fill(c, n, x, v) : NK_E_ARG; }
+int nk_divcopy(nk_ctx* c, int64_t n, double* y, const double* x, double s) { return c ? launch_divcopy(c, n, y, x, s) : NK_E_ARG; }
+int nk_ref(nk_ctx* c, int64_t n, double* x, double* y, double cc, double ss) { return c ? launch_ref(c, n, x, y, cc, ss) : NK_E_ARG; }
+
+// ---------------------------------------------------------------- profiling
+int nk_prof_enable(nk_ctx* c, int32_t on) {
+    if (!c) return NK_E_ARG;
+    if (!on && c->prof) prof_drain(c, true);
+    c->prof = on != 0;
+    return NK_OK;
+}
+
+int nk_prof_reset(nk_ctx* c) {
+    if (!c) return NK_E_ARG;
+    prof_drain(c, true);
+    for (auto& a : c->acc) a = ProfAcc();
+    return NK_OK;
+}
+
+int nk_prof_read(nk_ctx* c, nk_prof_entry* out, int32_t cap, int32_t* count) {
+    if (!c || !count) return NK_E_ARG;
+    prof_drain(c, true);
+    int m = 0;
+    for (size_t k = 0; k < c->kid_names.size(); ++k) {
+        if (c->acc[k].launches == 0) continue;
+        if (out && m < cap) {
+            std::memset(out[m].name, 0, NK_PROF_NAME);
+            std::strncpy(out[m].name, c->kid_names[k].c_str(), NK_PROF_NAME - 1);
+            out[m].launches = c->acc[k].launches;
+            out[m].total_ms = c->acc[k].ms;
+            out[m].bytes = c->acc[k].bytes;
+        }
+        ++m;
+    }
+    *count = m;
+    return NK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,161 @@
+// nk_internal.hpp -- shared definitions of libnkhip.so (context, launch/profiling helpers,
+// kernel-launcher prototypes).  Not part of the public ABI (that is include/nkhip.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "nkhip.h"
+
+namespace nk {
+
+constexpr int kBlock = 256;          // threads per block for every streaming kernel (4 waves of 64)
+constexpr int kMaxRedBlocks = 2048;  // partial sums per reduction (8 blocks per CU on 256 CUs)
+constexpr int kRedSlots = 4;         // ring of partial-sum slots
+constexpr int kRedCap = 16384;       // doubles per slot (a stencil launch may have more blocks)
+constexpr int kScalCap = 8192;       // device scalar area (Hessenberg column, y, norms)
+constexpr int kMaxUpdateVecs = 32;   // basis vectors folded per x-update launch
+
+enum Mode { MODE_RES = 0, MODE_JEXACT = 1, MODE_JFD = 2 };
+enum Epi { EPI_NONE = 0, EPI_SUMSQ = 1, EPI_DOT = 2, EPI_RESID = 3 };
+
+struct ProfPending {
+    int kid;
+    hipEvent_t a, b;
+    double bytes;
+};
+struct ProfAcc {
+    int64_t launches = 0;
+    double ms = 0.0, bytes = 0.0;
+};
+
+struct Comm;  // RCCL state (nk_dist.cpp)
+
+}  // namespace nk
+
+struct nk_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::unordered_map<double*, void*> allocs;  // interior pointer -> allocation base
+    double* red = nullptr;                      // kRedSlots * kRedCap partial sums
+    double* scal = nullptr;                     // kScalCap device scalars
+    double* hpin = nullptr;                     // kScalCap pinned host scalars
+    int red_next = 0;
+    // profiling
+    bool prof = false;
+    std::vector<nk::ProfPending> pending;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::string> kid_names;
+    std::map<std::string, int> kid_of;
+    std::vector<nk::ProfAcc> acc;
+    // distribution
+    int rank = 0, nranks = 1;
+    nk::Comm* comm = nullptr;
+};
+
+namespace nk {
+
+// ---------------------------------------------------------------- errors
+int fail(nk_ctx* c, int code, const std::string& msg);
+#define NK_HIP(c, expr)                                                                         \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return ::nk::fail((c), NK_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+#define NK_TRY(expr)             \
+    do {                         \
+        int r_ = (expr);         \
+        if (r_ != NK_OK) return r_; \
+    } while (0)
+
+// ---------------------------------------------------------------- grid geometry
+struct Geo {
+    int dim;          // 1, 2, 3
+    int64_t n;        // interior points
+    int64_t plane;    // ghost-plane size along the slowest axis (1, nx, nx*ny)
+    int64_t nplanes;  // interior planes along the slowest axis
+    int64_t front;    // doubles before the interior (>= plane, multiple of 32 => 256-B aligned interior)
+};
+int geometry(nk_ctx* c, const nk_problem* p, Geo* g);
+
+// ---------------------------------------------------------------- profiling helpers
+int kid(nk_ctx* c, const char* name);
+int prof_begin(nk_ctx* c, hipEvent_t* a);
+int prof_end(nk_ctx* c, int k, hipEvent_t a, double bytes);
+void prof_drain(nk_ctx* c, bool blocking);
+
+// run `launch()` (which enqueues one kernel on c->stream) under optional event timing
+template <typename F>
+int launch(nk_ctx* c, const char* name, double bytes, F&& f) {
+    hipEvent_t a = nullptr;
+    if (c->prof) NK_TRY(prof_begin(c, &a));
+    f();
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(c, NK_E_HIP, std::string("launch ") + name + ": " + hipGetErrorString(e));
+    if (c->prof) NK_TRY(prof_end(c, kid(c, name), a, bytes));
+    return NK_OK;
+}
+
+// ---------------------------------------------------------------- reductions
+// A reduction result lives either as `len` partial sums (single rank) or, after finish_reduction
+// on several ranks, as one all-reduced scalar.  Consumers sum `len` doubles at `ptr` in a fixed
+// order, so every block (and every run) sees the bit-identical value.
+struct Red {
+    const double* ptr;
+    int len;
+};
+double* red_slot(nk_ctx* c);                 // next partial-sum slot of the ring
+int finish_reduction(nk_ctx* c, Red* r);     // multi-rank: collapse + RCCL all-reduce
+int red_blocks(int64_t n);                   // grid size of streaming reductions
+
+// ---------------------------------------------------------------- kernel launchers (nk_kernels.hip)
+struct StencilIn {
+    const nk_problem* p;
+    int mode;          // Mode
+    int epi;           // Epi
+    double* out;
+    const double* u;
+    const double* v;
+    const double* F0;
+    const double* aux; // EPI_DOT: dot partner; EPI_RESID: b (out = b - J v)
+    double eps;
+};
+// returns the partial sums (when epi != EPI_NONE) in *red
+int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red);
+
+int launch_dot(nk_ctx* c, int64_t n, const double* x, const double* y, Red* red);
+int launch_sumsq(nk_ctx* c, int64_t n, const double* x, Red* red);
+int launch_finalize(nk_ctx* c, Red r, double* dst, int sqrt_it);  // dst[0] = sum (or sqrt(sum))
+int launch_axpy(nk_ctx* c, int64_t n, double s, const double* x, double* y);
+int launch_axpby(nk_ctx* c, int64_t n, double s, const double* x, double t, double* y);
+int launch_scal(nk_ctx* c, int64_t n, double s, double* x);
+int launch_copy(nk_ctx* c, int64_t n, double* y, const double* x);
+int launch_fill(nk_ctx* c, int64_t n, double* x, double v);
+int launch_divcopy(nk_ctx* c, int64_t n, double* y, const double* x, double s);
+int launch_ref(nk_ctx* c, int64_t n, double* x, double* y, double cc, double ss);
+// one fused modified-Gram-Schmidt pass: h = Σ in; q -= h vi; partials of <vnext, q> (or <q,q>
+// when vnext == nullptr).  Block 0 stores h at h_out.
+int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const double* vnext, Red in,
+                    double* h_out, Red* out);
+// xr = Σ_i y_i V_i (fma chain from 0 in i order, y on device); then x = x + xr (restart) or
+// x = xr; optional partial sums of ||x||^2.
+int launch_update_x(nk_ctx* c, int64_t n, double* x, double* xr, const double* const* V, int k,
+                    const double* y_dev, int restart, Red* xnorm);
+// CG pieces: x += a p ; r -= a Ap ; partial <r,r>   and   p = r + b p
+int launch_cg_update(nk_ctx* c, int64_t n, double alpha, double* x, double* r, const double* p,
+                     const double* Ap, Red* rr);
+int launch_cg_direction(nk_ctx* c, int64_t n, double beta, double* p, const double* r);
+
+// ---------------------------------------------------------------- distribution (nk_dist.cpp)
+int halo_exchange(nk_ctx* c, const nk_problem* p, const double* v);
+int allreduce_scalar(nk_ctx* c, double* dev, int64_t count);
+
+}  // namespace nk

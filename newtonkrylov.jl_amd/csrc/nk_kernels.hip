@@ -1,0 +1,764 @@
+// nk_kernels.hip -- the hand-written gfx950 kernels of the JFNK inner loop and their launchers.
+//
+// Every kernel here is HBM-bound (fp64, ~1 flop/B): no MFMA.  Design rules applied:
+//  * 256-thread blocks (4 waves of 64), 16-B (double2) loads/stores wherever the row length is
+//    even, grid-stride streaming for BLAS-1 with a fixed grid so reductions are deterministic.
+//  * Stencils march along the slowest axis keeping three planes of the stencil field in
+//    registers (one HBM read per input per point); x-neighbours come from the neighbouring
+//    lane by cross-lane shuffle, only the two wave-edge lanes load their outer column.
+//  * XCD-aware tile order: the 8 XCDs each take a contiguous band of tiles, so the halo rows
+//    two vertically adjacent tiles share are read on the same XCD.
+//  * Reductions never use atomics: each block writes one partial; the NEXT kernel (or the
+//    finaliser) sums the partials in a fixed order -- run-to-run bit reproducible.
+//  * -ffp-contract=off: stencil expressions round exactly as the reference writes them
+//    (((p - 2c) + m) / (h*h), bratu.jl:19, heat_2D.jl:65).  axpy-type updates use fma()
+//    explicitly (the oracle uses the same convention), so elementwise results are bit-identical
+//    to the CPU oracle; only exp (ocml vs glibc, <= 1 ulp) and reduction order differ.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "nk_internal.hpp"
+
+namespace nk {
+namespace {
+
+// ------------------------------------------------------------------------------ reductions
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;  // lane 0's value is used: a fixed association order
+}
+
+// sum over the 256 threads; valid in thread 0
+__device__ __forceinline__ double block_sum(double v, double* sh) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) sh[w] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (threadIdx.x == 0) r = ((sh[0] + sh[1]) + sh[2]) + sh[3];
+    return r;
+}
+
+// fixed-order sum of in[0..len), broadcast to the whole block
+__device__ __forceinline__ double reduce_input(const double* __restrict__ in, int len, double* sh) {
+    if (threadIdx.x < 64) {
+        double t = 0.0;
+        for (int m = threadIdx.x; m < len; m += 64) t += in[m];
+        t = wave_sum(t);
+        if (threadIdx.x == 0) sh[4] = t;
+    }
+    __syncthreads();
+    return sh[4];
+}
+
+__device__ __forceinline__ double lap(double c, double p, double m, double h2) { return ((p - 2.0 * c) + m) / h2; }
+
+struct KArgs {
+    double* out;
+    const double* u;
+    const double* v;
+    const double* F0;
+    const double* un;
+    const double* aux;
+    double* part;
+    int64_t nx, ny, nz;
+    double hx2, hy2, hz2, lam, a, dt, eps;
+    int tiles_x, tiles_y, rows;
+};
+
+template <int MODE>
+__device__ __forceinline__ double fieldval(const KArgs& A, int64_t o) {
+    if (MODE == MODE_RES) return A.u[o];
+    if (MODE == MODE_JEXACT) return A.v[o];
+    return A.u[o] + A.eps * A.v[o];  // w = u + eps v
+}
+
+template <int MODE, int VEC>
+__device__ __forceinline__ void fieldvec(const KArgs& A, int64_t o, double* f) {
+    if (VEC == 2) {
+        if (MODE == MODE_RES) {
+            const double2 q = *reinterpret_cast<const double2*>(A.u + o);
+            f[0] = q.x; f[1] = q.y;
+        } else if (MODE == MODE_JEXACT) {
+            const double2 q = *reinterpret_cast<const double2*>(A.v + o);
+            f[0] = q.x; f[1] = q.y;
+        } else {
+            const double2 qu = *reinterpret_cast<const double2*>(A.u + o);
+            const double2 qv = *reinterpret_cast<const double2*>(A.v + o);
+            f[0] = qu.x + A.eps * qv.x;
+            f[1] = qu.y + A.eps * qv.y;
+        }
+    } else {
+        f[0] = fieldval<MODE>(A, o);
+    }
+}
+
+template <int VEC>
+__device__ __forceinline__ void loadvec(const double* __restrict__ p, int64_t o, double* f) {
+    if (VEC == 2) {
+        const double2 q = *reinterpret_cast<const double2*>(p + o);
+        f[0] = q.x; f[1] = q.y;
+    } else {
+        f[0] = p[o];
+    }
+}
+
+template <int VEC>
+__device__ __forceinline__ void storevec(double* __restrict__ p, int64_t o, const double* f) {
+    if (VEC == 2) {
+        *reinterpret_cast<double2*>(p + o) = make_double2(f[0], f[1]);
+    } else {
+        p[o] = f[0];
+    }
+}
+
+// residual / JVP value at one point from the stencil field (c + neighbours) and centre data.
+// lsum = Laplacian-like sum in the reference's association order.
+template <int KIND, int MODE>
+__device__ __forceinline__ double point_value(const KArgs& A, double c, double lsum, double uc, double unc, double f0c) {
+    if (KIND == NK_BRATU1D || KIND == NK_BRATU2D) {
+        if (MODE == MODE_JEXACT) return lsum + A.lam * (exp(uc) * c);  // Enzyme tangent of λ exp(u)
+        const double r = lsum + A.lam * exp(c);
+        return MODE == MODE_JFD ? (r - f0c) / A.eps : r;
+    } else {  // implicit Euler: res = (u_n + dt f(u)) - u  (implicit.jl:8-13)
+        if (MODE == MODE_JEXACT) return A.dt * (A.a * lsum) - c;
+        const double r = (unc + A.dt * (A.a * lsum)) - c;
+        return MODE == MODE_JFD ? (r - f0c) / A.eps : r;
+    }
+}
+
+template <int EPI>
+__device__ __forceinline__ double epilogue(double& val, double ax, double acc) {
+    if (EPI == EPI_SUMSQ) return fma(val, val, acc);
+    if (EPI == EPI_DOT) return fma(ax, val, acc);
+    if (EPI == EPI_RESID) {
+        val = ax - val;  // w = b - A x  (kaxpby!(n, 1, b, -1, w))
+        return fma(val, val, acc);
+    }
+    return acc;
+}
+
+// ------------------------------------------------------------------------------ 1D stencil
+template <int MODE, int EPI>
+__global__ __launch_bounds__(kBlock) void k_st1d(KArgs A) {
+    __shared__ double sh[8];
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    double acc = 0.0;
+    if (i < A.nx) {
+        // ghost cells at -1 and nx exist (zero Dirichlet) -- examples/bratu.jl:17-18
+        const double c = fieldval<MODE>(A, i), l = fieldval<MODE>(A, i - 1), r = fieldval<MODE>(A, i + 1);
+        const double uc = (MODE == MODE_JEXACT) ? A.u[i] : 0.0;
+        const double f0 = (MODE == MODE_JFD) ? A.F0[i] : 0.0;
+        double val = point_value<NK_BRATU1D, MODE>(A, c, lap(c, r, l, A.hx2), uc, 0.0, f0);
+        const double ax = (EPI == EPI_DOT || EPI == EPI_RESID) ? A.aux[i] : 0.0;
+        acc = epilogue<EPI>(val, ax, acc);
+        A.out[i] = val;
+    }
+    if (EPI != EPI_NONE) {
+        const double s = block_sum(acc, sh);
+        if (threadIdx.x == 0) A.part[blockIdx.x] = s;
+    }
+}
+
+// ------------------------------------------------------------------------------ 2D stencil
+// Block = 256 threads x VEC columns (one row segment), marching A.rows rows in y.
+template <int KIND, int MODE, int EPI, int VEC>
+__global__ __launch_bounds__(kBlock) void k_st2d(KArgs A) {
+    __shared__ double sh[8];
+    const int lane = threadIdx.x & 63;
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int t = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;  // XCD-contiguous tile bands
+    const int tx = t % A.tiles_x, ty = t / A.tiles_x;
+    const int64_t nx = A.nx, ny = A.ny;
+    const int64_t x0 = (int64_t)tx * (kBlock * VEC) + (int64_t)threadIdx.x * VEC;
+    const bool act = x0 < nx;
+    const int64_t y0 = (int64_t)ty * A.rows;
+    const int64_t y1 = y0 + A.rows < ny ? y0 + A.rows : ny;
+
+    double fm[VEC], fc[VEC], fp[VEC];
+    double elc = 0.0, erc = 0.0, elp = 0.0, erp = 0.0;
+    double acc = 0.0;
+
+    auto load_row = [&](int64_t j, double* f) {
+        if (act) {
+            fieldvec<MODE, VEC>(A, j * nx + x0, f);
+        } else {
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) f[k] = 0.0;
+        }
+    };
+    auto load_edges = [&](int64_t j, double& el, double& er) {
+        if (lane == 0 && x0 - 1 >= 0 && x0 - 1 < nx) el = fieldval<MODE>(A, j * nx + x0 - 1);
+        if (lane == 63 && x0 + VEC < nx) er = fieldval<MODE>(A, j * nx + x0 + VEC);
+    };
+
+    if (y0 < ny) {
+        load_row(y0 - 1, fm);  // row -1 is the ghost plane (zero, or the lower neighbour's row)
+        load_row(y0, fc);
+        load_edges(y0, elc, erc);
+        for (int64_t j = y0; j < y1; ++j) {
+            load_row(j + 1, fp);  // row ny is the upper ghost plane
+            elp = 0.0; erp = 0.0;
+            if (j + 1 < ny) load_edges(j + 1, elp, erp);
+            double uc[VEC], unc[VEC], f0c[VEC], ax[VEC];
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) uc[k] = unc[k] = f0c[k] = ax[k] = 0.0;
+            const int64_t o = j * nx + x0;
+            if (act) {
+                if (MODE == MODE_JEXACT && KIND == NK_BRATU2D) loadvec<VEC>(A.u, o, uc);
+                if (KIND == NK_HEAT2D_EULER && MODE != MODE_JEXACT) loadvec<VEC>(A.un, o, unc);
+                if (MODE == MODE_JFD) loadvec<VEC>(A.F0, o, f0c);
+                if (EPI == EPI_DOT || EPI == EPI_RESID) loadvec<VEC>(A.aux, o, ax);
+            }
+            double lft = __shfl_up(fc[VEC - 1], 1, 64);
+            double rgt = __shfl_down(fc[0], 1, 64);
+            if (lane == 0) lft = elc;
+            if (lane == 63) rgt = erc;
+            if (act) {
+                double val[VEC];
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    const double w = (k == 0) ? lft : fc[k - 1];
+                    const double e = (k == VEC - 1) ? rgt : fc[k + 1];
+                    const double c = fc[k];
+                    const double lsum = lap(c, e, w, A.hx2) + lap(c, fp[k], fm[k], A.hy2);
+                    val[k] = point_value<KIND, MODE>(A, c, lsum, uc[k], unc[k], f0c[k]);
+                    acc = epilogue<EPI>(val[k], ax[k], acc);
+                }
+                storevec<VEC>(A.out, o, val);
+            }
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) { fm[k] = fc[k]; fc[k] = fp[k]; }
+            elc = elp; erc = erp;
+        }
+    }
+    if (EPI != EPI_NONE) {
+        const double s = block_sum(acc, sh);
+        if (threadIdx.x == 0) A.part[blockIdx.x] = s;
+    }
+}
+
+// ------------------------------------------------------------------------------ 3D stencil
+// Block = 4 waves = 4 rows (y) x 64*VEC columns, marching A.rows planes in z.
+template <int KIND, int MODE, int EPI, int VEC>
+__global__ __launch_bounds__(kBlock) void k_st3d(KArgs A) {
+    __shared__ double sh[8];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int t = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;
+    const int tpl = A.tiles_x * A.tiles_y;
+    const int tz = t / tpl, txy = t % tpl;
+    const int ty = txy / A.tiles_x, tx = txy % A.tiles_x;
+    const int64_t nx = A.nx, ny = A.ny, nz = A.nz, pl = nx * ny;
+    const int64_t x0 = (int64_t)tx * (64 * VEC) + (int64_t)lane * VEC;
+    const int64_t j = (int64_t)ty * 4 + wv;
+    const bool act = x0 < nx && j < ny;
+    const int64_t z0 = (int64_t)tz * A.rows;
+    const int64_t z1 = z0 + A.rows < nz ? z0 + A.rows : nz;
+
+    double fm[VEC], fc[VEC], fp[VEC];
+    double elc = 0.0, erc = 0.0, elp = 0.0, erp = 0.0;
+    double acc = 0.0;
+    auto load_row = [&](int64_t k, int64_t jj, double* f) {
+        if (x0 < nx && jj >= 0 && jj < ny) {
+            fieldvec<MODE, VEC>(A, k * pl + jj * nx + x0, f);
+        } else {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) f[q] = 0.0;
+        }
+    };
+    auto load_edges = [&](int64_t k, double& el, double& er) {
+        if (j < ny) {
+            if (lane == 0 && x0 - 1 >= 0 && x0 - 1 < nx) el = fieldval<MODE>(A, k * pl + j * nx + x0 - 1);
+            if (lane == 63 && x0 + VEC < nx) er = fieldval<MODE>(A, k * pl + j * nx + x0 + VEC);
+        }
+    };
+    if (z0 < nz) {
+        load_row(z0 - 1, j, fm);  // plane -1: ghost plane
+        load_row(z0, j, fc);
+        load_edges(z0, elc, erc);
+        for (int64_t k = z0; k < z1; ++k) {
+            load_row(k + 1, j, fp);  // plane nz: ghost plane
+            elp = 0.0; erp = 0.0;
+            if (k + 1 < nz) load_edges(k + 1, elp, erp);
+            double fn[VEC], fs[VEC];
+            load_row(k, j + 1, fn);
+            load_row(k, j - 1, fs);
+            double unc[VEC], f0c[VEC], ax[VEC];
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) unc[q] = f0c[q] = ax[q] = 0.0;
+            const int64_t o = k * pl + j * nx + x0;
+            if (act) {
+                if (MODE != MODE_JEXACT) loadvec<VEC>(A.un, o, unc);
+                if (MODE == MODE_JFD) loadvec<VEC>(A.F0, o, f0c);
+                if (EPI == EPI_DOT || EPI == EPI_RESID) loadvec<VEC>(A.aux, o, ax);
+            }
+            double lft = __shfl_up(fc[VEC - 1], 1, 64);
+            double rgt = __shfl_down(fc[0], 1, 64);
+            if (lane == 0) lft = elc;
+            if (lane == 63) rgt = erc;
+            if (act) {
+                double val[VEC];
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) {
+                    const double w = (q == 0) ? lft : fc[q - 1];
+                    const double e = (q == VEC - 1) ? rgt : fc[q + 1];
+                    const double c = fc[q];
+                    const double lsum = (lap(c, e, w, A.hx2) + lap(c, fn[q], fs[q], A.hy2)) + lap(c, fp[q], fm[q], A.hz2);
+                    val[q] = point_value<KIND, MODE>(A, c, lsum, 0.0, unc[q], f0c[q]);
+                    acc = epilogue<EPI>(val[q], ax[q], acc);
+                }
+                storevec<VEC>(A.out, o, val);
+            }
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) { fm[q] = fc[q]; fc[q] = fp[q]; }
+            elc = elp; erc = erp;
+        }
+    }
+    if (EPI != EPI_NONE) {
+        const double s = block_sum(acc, sh);
+        if (threadIdx.x == 0) A.part[blockIdx.x] = s;
+    }
+}
+
+// ------------------------------------------------------------------------------ BLAS-1
+#define NK_GRID_STRIDE2(i)                                                   \
+    const int64_t n2_ = n >> 1;                                              \
+    const int64_t st_ = (int64_t)gridDim.x * kBlock;                         \
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n2_; i += st_)
+#define NK_TAIL (((n & 1) != 0) && blockIdx.x == 0 && threadIdx.x == 0)
+
+__global__ __launch_bounds__(kBlock) void k_dot(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
+                                               double* __restrict__ part) {
+    __shared__ double sh[8];
+    const double2* x2 = reinterpret_cast<const double2*>(x);
+    const double2* y2 = reinterpret_cast<const double2*>(y);
+    double acc = 0.0;
+    NK_GRID_STRIDE2(i) {
+        const double2 a = x2[i], b = y2[i];
+        acc = fma(a.x, b.x, acc);
+        acc = fma(a.y, b.y, acc);
+    }
+    if (NK_TAIL) acc = fma(x[n - 1], y[n - 1], acc);
+    const double s = block_sum(acc, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(kBlock) void k_sumsq(int64_t n, const double* __restrict__ x, double* __restrict__ part) {
+    __shared__ double sh[8];
+    const double2* x2 = reinterpret_cast<const double2*>(x);
+    double acc = 0.0;
+    NK_GRID_STRIDE2(i) {
+        const double2 a = x2[i];
+        acc = fma(a.x, a.x, acc);
+        acc = fma(a.y, a.y, acc);
+    }
+    if (NK_TAIL) acc = fma(x[n - 1], x[n - 1], acc);
+    const double s = block_sum(acc, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(64) void k_finalize(const double* __restrict__ in, int len, double* __restrict__ dst, int sqrt_it) {
+    double t = 0.0;
+    for (int m = threadIdx.x; m < len; m += 64) t += in[m];
+    t = wave_sum(t);
+    if (threadIdx.x == 0) dst[0] = sqrt_it ? sqrt(t) : t;
+}
+
+__global__ __launch_bounds__(kBlock) void k_axpy(int64_t n, double s, const double* __restrict__ x, double* __restrict__ y) {
+    const double2* x2 = reinterpret_cast<const double2*>(x);
+    double2* y2 = reinterpret_cast<double2*>(y);
+    NK_GRID_STRIDE2(i) {
+        const double2 a = x2[i];
+        double2 b = y2[i];
+        b.x = fma(s, a.x, b.x);
+        b.y = fma(s, a.y, b.y);
+        y2[i] = b;
+    }
+    if (NK_TAIL) y[n - 1] = fma(s, x[n - 1], y[n - 1]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_axpby(int64_t n, double s, const double* __restrict__ x, double t,
+                                                 double* __restrict__ y) {
+    const double2* x2 = reinterpret_cast<const double2*>(x);
+    double2* y2 = reinterpret_cast<double2*>(y);
+    NK_GRID_STRIDE2(i) {
+        const double2 a = x2[i];
+        double2 b = y2[i];
+        b.x = fma(t, b.x, s * a.x);
+        b.y = fma(t, b.y, s * a.y);
+        y2[i] = b;
+    }
+    if (NK_TAIL) y[n - 1] = fma(t, y[n - 1], s * x[n - 1]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_scal(int64_t n, double s, double* __restrict__ x) {
+    double2* x2 = reinterpret_cast<double2*>(x);
+    NK_GRID_STRIDE2(i) {
+        double2 a = x2[i];
+        a.x = s * a.x;
+        a.y = s * a.y;
+        x2[i] = a;
+    }
+    if (NK_TAIL) x[n - 1] = s * x[n - 1];
+}
+
+__global__ __launch_bounds__(kBlock) void k_copy(int64_t n, double* __restrict__ y, const double* __restrict__ x) {
+    const double2* x2 = reinterpret_cast<const double2*>(x);
+    double2* y2 = reinterpret_cast<double2*>(y);
+    NK_GRID_STRIDE2(i) { y2[i] = x2[i]; }
+    if (NK_TAIL) y[n - 1] = x[n - 1];
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill(int64_t n, double* __restrict__ x, double v) {
+    double2* x2 = reinterpret_cast<double2*>(x);
+    NK_GRID_STRIDE2(i) { x2[i] = make_double2(v, v); }
+    if (NK_TAIL) x[n - 1] = v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_divcopy(int64_t n, double* __restrict__ y, const double* __restrict__ x, double s) {
+    const double2* x2 = reinterpret_cast<const double2*>(x);
+    double2* y2 = reinterpret_cast<double2*>(y);
+    NK_GRID_STRIDE2(i) {
+        const double2 a = x2[i];
+        y2[i] = make_double2(a.x / s, a.y / s);
+    }
+    if (NK_TAIL) y[n - 1] = x[n - 1] / s;
+}
+
+__global__ __launch_bounds__(kBlock) void k_ref(int64_t n, double* __restrict__ x, double* __restrict__ y, double c, double s) {
+    double2* x2 = reinterpret_cast<double2*>(x);
+    double2* y2 = reinterpret_cast<double2*>(y);
+    NK_GRID_STRIDE2(i) {
+        const double2 a = x2[i], b = y2[i];
+        x2[i] = make_double2(c * a.x + s * b.x, c * a.y + s * b.y);
+        y2[i] = make_double2(s * a.x - c * b.x, s * a.y - c * b.y);
+    }
+    if (NK_TAIL) {
+        const double a = x[n - 1], b = y[n - 1];
+        x[n - 1] = c * a + s * b;
+        y[n - 1] = s * a - c * b;
+    }
+}
+
+// One fused MGS pass (Krylov.jl gmres! inner loop):
+//   h = <V_i, q>   (reduced from the previous kernel's partials, fixed order)
+//   q = q - h V_i  (kaxpy!(n, -h, V_i, q) == fma(-h, V_i, q))
+//   partials of <V_{i+1}, q>  (or <q, q> on the last pass: h_{k+1,k} = ||q||)
+// 32 B/point (24 on the last pass) instead of the 40 B of separate kdot + kaxpy!.
+template <bool HAS_NEXT>
+__global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restrict__ q, const double* __restrict__ vi,
+                                                    const double* __restrict__ vnext, const double* __restrict__ red_in,
+                                                    int red_len, double* __restrict__ h_out, double* __restrict__ part) {
+    __shared__ double sh[8];
+    const double h = reduce_input(red_in, red_len, sh);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *h_out = h;
+    const double mh = -h;
+    double2* q2 = reinterpret_cast<double2*>(q);
+    const double2* v2 = reinterpret_cast<const double2*>(vi);
+    const double2* w2 = reinterpret_cast<const double2*>(vnext);
+    double acc = 0.0;
+    NK_GRID_STRIDE2(i) {
+        double2 a = q2[i];
+        const double2 b = v2[i];
+        a.x = fma(mh, b.x, a.x);
+        a.y = fma(mh, b.y, a.y);
+        q2[i] = a;
+        if (HAS_NEXT) {
+            const double2 c = w2[i];
+            acc = fma(c.x, a.x, acc);
+            acc = fma(c.y, a.y, acc);
+        } else {
+            acc = fma(a.x, a.x, acc);
+            acc = fma(a.y, a.y, acc);
+        }
+    }
+    if (NK_TAIL) {
+        const double a = fma(mh, vi[n - 1], q[n - 1]);
+        q[n - 1] = a;
+        acc = HAS_NEXT ? fma(vnext[n - 1], a, acc) : fma(a, a, acc);
+    }
+    const double s = block_sum(acc, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+struct UpdArgs {
+    const double* V[kMaxUpdateVecs];
+    double* x;
+    double* xr;
+    const double* y;
+    double* part;
+    int64_t n;
+    int k, first, last, restart;
+};
+
+// xr = Σ y_i V_i (the kaxpy! chain of gmres!, from xr = 0); on the last chunk x = x + xr
+// (restart) or x = xr; optional partials of ||x||^2.
+__global__ __launch_bounds__(kBlock) void k_update_x(UpdArgs A) {
+    __shared__ double sh[8];
+    const int64_t n = A.n;
+    double yv[kMaxUpdateVecs];
+#pragma unroll
+    for (int m = 0; m < kMaxUpdateVecs; ++m) yv[m] = m < A.k ? A.y[m] : 0.0;
+    double acc = 0.0;
+    const int64_t st = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += st) {
+        double t = A.first ? 0.0 : A.xr[i];
+#pragma unroll
+        for (int m = 0; m < kMaxUpdateVecs; ++m)  // compile-time indices keep yv in registers
+            if (m < A.k) t = fma(yv[m], A.V[m][i], t);
+        if (A.last) {
+            const double xv = A.restart ? fma(1.0, t, A.x[i]) : t;
+            A.x[i] = xv;
+            acc = fma(xv, xv, acc);
+        } else {
+            A.xr[i] = t;
+        }
+    }
+    if (A.part) {
+        const double s = block_sum(acc, sh);
+        if (threadIdx.x == 0) A.part[blockIdx.x] = s;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_cg_update(int64_t n, double alpha, double* __restrict__ x, double* __restrict__ r,
+                                                     const double* __restrict__ p, const double* __restrict__ Ap,
+                                                     double* __restrict__ part) {
+    __shared__ double sh[8];
+    double acc = 0.0;
+    const double ma = -alpha;
+    const int64_t st = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += st) {
+        x[i] = fma(alpha, p[i], x[i]);
+        const double rv = fma(ma, Ap[i], r[i]);
+        r[i] = rv;
+        acc = fma(rv, rv, acc);
+    }
+    const double s = block_sum(acc, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(kBlock) void k_cg_direction(int64_t n, double beta, double* __restrict__ p, const double* __restrict__ r) {
+    const int64_t st = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += st) p[i] = fma(beta, p[i], 1.0 * r[i]);
+}
+
+// ------------------------------------------------------------------------------ stencil dispatch
+template <int KIND, int MODE, int EPI>
+void go_stencil(const KArgs& A, int dim, int vec, int grid, hipStream_t s) {
+    if (dim == 1) {
+        if (KIND == NK_BRATU1D) hipLaunchKernelGGL((k_st1d<MODE, EPI>), dim3(grid), dim3(kBlock), 0, s, A);
+    } else if (dim == 2) {
+        if (KIND == NK_BRATU2D || KIND == NK_HEAT2D_EULER) {
+            if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
+            else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1>), dim3(grid), dim3(kBlock), 0, s, A);
+        }
+    } else {
+        if (KIND == NK_HEAT3D_EULER) {
+            if (vec == 2) hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
+            else hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 1>), dim3(grid), dim3(kBlock), 0, s, A);
+        }
+    }
+}
+
+template <int KIND, int MODE>
+void go_stencil_epi(const KArgs& A, int epi, int dim, int vec, int grid, hipStream_t s) {
+    switch (epi) {
+    case EPI_NONE: go_stencil<KIND, MODE, EPI_NONE>(A, dim, vec, grid, s); break;
+    case EPI_SUMSQ: go_stencil<KIND, MODE, EPI_SUMSQ>(A, dim, vec, grid, s); break;
+    case EPI_DOT: go_stencil<KIND, MODE, EPI_DOT>(A, dim, vec, grid, s); break;
+    default: go_stencil<KIND, MODE, EPI_RESID>(A, dim, vec, grid, s); break;
+    }
+}
+
+template <int KIND>
+void go_stencil_mode(const KArgs& A, int mode, int epi, int dim, int vec, int grid, hipStream_t s) {
+    switch (mode) {
+    case MODE_RES: go_stencil_epi<KIND, MODE_RES>(A, epi, dim, vec, grid, s); break;
+    case MODE_JEXACT: go_stencil_epi<KIND, MODE_JEXACT>(A, epi, dim, vec, grid, s); break;
+    default: go_stencil_epi<KIND, MODE_JFD>(A, epi, dim, vec, grid, s); break;
+    }
+}
+
+int env_int(const char* name, int dflt) {
+    const char* s = getenv(name);
+    return (s && *s) ? atoi(s) : dflt;
+}
+
+}  // namespace
+
+int red_blocks(int64_t n) {
+    static const int cap = env_int("NK_RED_BLOCKS", kMaxRedBlocks);
+    int64_t g = (n + 2LL * kBlock * 4 - 1) / (2LL * kBlock * 4);  // >= 4 double2 per thread
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red) {
+    const nk_problem* p = in.p;
+    Geo g;
+    NK_TRY(geometry(c, p, &g));
+    KArgs A{};
+    A.out = in.out; A.u = in.u; A.v = in.v; A.F0 = in.F0; A.un = p->un; A.aux = in.aux;
+    A.nx = p->nx; A.ny = p->ny; A.nz = p->nz;
+    A.hx2 = p->hx * p->hx; A.hy2 = p->hy * p->hy; A.hz2 = p->hz * p->hz;
+    A.lam = p->lambda; A.a = p->a; A.dt = p->dt; A.eps = in.eps;
+    int vec = 1, grid = 1;
+    if (g.dim == 1) {
+        grid = (int)((p->nx + kBlock - 1) / kBlock);
+    } else if (g.dim == 2) {
+        vec = (p->nx % 2 == 0) ? 2 : 1;
+        A.tiles_x = (int)((p->nx + kBlock * vec - 1) / (kBlock * vec));
+        static const int target = env_int("NK_ST_BLOCKS", 2048);
+        int64_t rows = (p->ny * A.tiles_x + target - 1) / target;
+        static const int min_rows = env_int("NK_ST_MINROWS", 8);
+        if (rows < min_rows) rows = min_rows;
+        if (rows > p->ny) rows = p->ny;
+        A.rows = (int)rows;
+        A.tiles_y = (int)((p->ny + rows - 1) / rows);
+        grid = A.tiles_x * A.tiles_y;
+    } else {
+        vec = (p->nx % 2 == 0) ? 2 : 1;
+        A.tiles_x = (int)((p->nx + 64 * vec - 1) / (64 * vec));
+        A.tiles_y = (int)((p->ny + 3) / 4);
+        static const int target = env_int("NK_ST_BLOCKS", 2048);
+        int64_t planes = ((int64_t)p->nz * A.tiles_x * A.tiles_y + target - 1) / target;
+        static const int min_planes = env_int("NK_ST_MINPLANES", 8);
+        if (planes < min_planes) planes = min_planes;
+        if (planes > p->nz) planes = p->nz;
+        A.rows = (int)planes;
+        grid = A.tiles_x * A.tiles_y * (int)((p->nz + planes - 1) / planes);
+    }
+    if (in.epi != EPI_NONE) {
+        if (grid > kRedCap) return fail(c, NK_E_ARG, "stencil grid exceeds reduction capacity");
+        A.part = red_slot(c);
+        red->ptr = A.part;
+        red->len = grid;
+    }
+    // algorithmic (compulsory) bytes per launch
+    const bool heat = p->kind == NK_HEAT2D_EULER || p->kind == NK_HEAT3D_EULER;
+    int words = 1;  // out
+    if (in.mode == MODE_RES) words += 1 + (heat ? 1 : 0);
+    else if (in.mode == MODE_JEXACT) words += 1 + (heat ? 0 : 1);
+    else words += 3 + (heat ? 1 : 0);
+    if (in.epi == EPI_DOT || in.epi == EPI_RESID) words += 1;
+    const double bytes = 8.0 * words * (double)g.n;
+    static const char* names[3][4] = {
+        {"residual", "residual_norm", "residual_dot", "residual_resid"},
+        {"jv_exact", "jv_exact_sumsq", "jv_exact_dot", "jv_exact_resid"},
+        {"jv_fd", "jv_fd_sumsq", "jv_fd_dot", "jv_fd_resid"}};
+    const int kind = p->kind, dim = g.dim, mode = in.mode, epi = in.epi;
+    hipStream_t s = c->stream;
+    return launch(c, names[mode][epi], bytes, [&] {
+        switch (kind) {
+        case NK_BRATU1D: go_stencil_mode<NK_BRATU1D>(A, mode, epi, dim, vec, grid, s); break;
+        case NK_BRATU2D: go_stencil_mode<NK_BRATU2D>(A, mode, epi, dim, vec, grid, s); break;
+        case NK_HEAT2D_EULER: go_stencil_mode<NK_HEAT2D_EULER>(A, mode, epi, dim, vec, grid, s); break;
+        default: go_stencil_mode<NK_HEAT3D_EULER>(A, mode, epi, dim, vec, grid, s); break;
+        }
+    });
+}
+
+int launch_dot(nk_ctx* c, int64_t n, const double* x, const double* y, Red* red) {
+    const int g = red_blocks(n);
+    double* part = red_slot(c);
+    red->ptr = part;
+    red->len = g;
+    return launch(c, "dot", 16.0 * n, [&] { hipLaunchKernelGGL(k_dot, dim3(g), dim3(kBlock), 0, c->stream, n, x, y, part); });
+}
+
+int launch_sumsq(nk_ctx* c, int64_t n, const double* x, Red* red) {
+    const int g = red_blocks(n);
+    double* part = red_slot(c);
+    red->ptr = part;
+    red->len = g;
+    return launch(c, "norm", 8.0 * n, [&] { hipLaunchKernelGGL(k_sumsq, dim3(g), dim3(kBlock), 0, c->stream, n, x, part); });
+}
+
+int launch_finalize(nk_ctx* c, Red r, double* dst, int sqrt_it) {
+    return launch(c, "finalize", 0.0, [&] { hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, c->stream, r.ptr, r.len, dst, sqrt_it); });
+}
+
+#define NK_STREAM_LAUNCH(name, bytes_per, kern, ...)                                              \
+    const int g = red_blocks(n);                                                                   \
+    return launch(c, name, (bytes_per) * (double)n,                                                \
+                  [&] { hipLaunchKernelGGL(kern, dim3(g), dim3(kBlock), 0, c->stream, __VA_ARGS__); })
+
+int launch_axpy(nk_ctx* c, int64_t n, double s, const double* x, double* y) { NK_STREAM_LAUNCH("axpy", 24.0, k_axpy, n, s, x, y); }
+int launch_axpby(nk_ctx* c, int64_t n, double s, const double* x, double t, double* y) {
+    NK_STREAM_LAUNCH("axpby", 24.0, k_axpby, n, s, x, t, y);
+}
+int launch_scal(nk_ctx* c, int64_t n, double s, double* x) { NK_STREAM_LAUNCH("scal", 16.0, k_scal, n, s, x); }
+int launch_copy(nk_ctx* c, int64_t n, double* y, const double* x) { NK_STREAM_LAUNCH("copy", 16.0, k_copy, n, y, x); }
+int launch_fill(nk_ctx* c, int64_t n, double* x, double v) { NK_STREAM_LAUNCH("fill", 8.0, k_fill, n, x, v); }
+int launch_divcopy(nk_ctx* c, int64_t n, double* y, const double* x, double s) {
+    NK_STREAM_LAUNCH("divcopy", 16.0, k_divcopy, n, y, x, s);
+}
+int launch_ref(nk_ctx* c, int64_t n, double* x, double* y, double cc, double ss) { NK_STREAM_LAUNCH("ref", 32.0, k_ref, n, x, y, cc, ss); }
+
+int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const double* vnext, Red in, double* h_out, Red* out) {
+    const int g = red_blocks(n);
+    double* part = red_slot(c);
+    out->ptr = part;
+    out->len = g;
+    if (vnext)
+        return launch(c, "mgs_pass", 32.0 * n, [&] {
+            hipLaunchKernelGGL(k_mgs_pass<true>, dim3(g), dim3(kBlock), 0, c->stream, n, q, vi, vnext, in.ptr, in.len, h_out, part);
+        });
+    return launch(c, "mgs_pass_last", 24.0 * n, [&] {
+        hipLaunchKernelGGL(k_mgs_pass<false>, dim3(g), dim3(kBlock), 0, c->stream, n, q, vi, vnext, in.ptr, in.len, h_out, part);
+    });
+}
+
+int launch_update_x(nk_ctx* c, int64_t n, double* x, double* xr, const double* const* V, int k, const double* y_dev,
+                    int restart, Red* xnorm) {
+    const int g = red_blocks(n);
+    int done = 0;
+    if (k == 0) {  // nothing to add: x unchanged (restart) or x = 0
+        if (!restart) NK_TRY(launch_fill(c, n, x, 0.0));
+        if (xnorm) return launch_sumsq(c, n, x, xnorm);
+        return NK_OK;
+    }
+    while (done < k) {
+        UpdArgs A{};
+        const int m = (k - done) < kMaxUpdateVecs ? (k - done) : kMaxUpdateVecs;
+        for (int i = 0; i < m; ++i) A.V[i] = V[done + i];
+        A.x = x; A.xr = xr; A.y = y_dev + done; A.n = n; A.k = m;
+        A.first = done == 0;
+        A.last = done + m == k;
+        A.restart = restart;
+        A.part = nullptr;
+        if (A.last && xnorm) {
+            A.part = red_slot(c);
+            xnorm->ptr = A.part;
+            xnorm->len = g;
+        }
+        // every chunk reads m basis vectors and (after the first) xr; the last writes x (reading it on restart)
+        const double bytes = 8.0 * n * (m + (A.first ? 0 : 1) + (A.last ? (restart ? 2 : 1) : 1));
+        NK_TRY(launch(c, "update_x", bytes, [&] {
+            hipLaunchKernelGGL(k_update_x, dim3(g), dim3(kBlock), 0, c->stream, A);
+        }));
+        done += m;
+    }
+    return NK_OK;
+}
+
+int launch_cg_update(nk_ctx* c, int64_t n, double alpha, double* x, double* r, const double* p, const double* Ap, Red* rr) {
+    const int g = red_blocks(n);
+    double* part = red_slot(c);
+    rr->ptr = part;
+    rr->len = g;
+    return launch(c, "cg_update", 48.0 * n, [&] {
+        hipLaunchKernelGGL(k_cg_update, dim3(g), dim3(kBlock), 0, c->stream, n, alpha, x, r, p, Ap, part);
+    });
+}
+
+int launch_cg_direction(nk_ctx* c, int64_t n, double beta, double* p, const double* r) {
+    NK_STREAM_LAUNCH("cg_direction", 24.0, k_cg_direction, n, beta, p, r);
+}
+
+}  // namespace nk

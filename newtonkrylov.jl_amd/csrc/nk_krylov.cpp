@@ -1,0 +1,453 @@
+// nk_krylov.cpp -- device-resident Krylov.jl 0.10 gmres!/cg! (M = N = I) for the Jacobian operator.
+//
+// Restates krylov_workspace(algo, KrylovConstructor(res)) + krylov_solve!(workspace, J, b; kwargs)
+// as called by Ariadne (src/Ariadne.jl:317-318, :338, :340, :367) -- SURVEY.md Appendix A.
+// Krylov.jl itself is third-party and absent from /root/reference; the same restatement lives in
+// oracle/nk_oracle.c (oc_gmres / oc_cg) and the tests check this driver against it.
+//
+// What moves to the device compared with Krylov.jl's generic loop:
+//  * the Arnoldi basis V, q (= w), x, and every reduction;
+//  * each Arnoldi step is: one fused Jv kernel (also emits the partials of <V_1, q>), k fused
+//    MGS passes (q -= h_i V_i and partials of <V_{i+1}, q>; the last pass emits ||q||^2 partials),
+//    one 64-thread finaliser, ONE device->host copy of the Hessenberg column and one sync.
+//    Krylov.jl's schedule would sync 2k+1 times (every kdot/knorm returns a host scalar).
+//  * the per-cycle kfill!(V[i], 0) of Krylov.jl is dropped: every V[i] read in a cycle is
+//    overwritten first, so the zeroing is dead work (no observable difference).
+// The Givens rotations, the least-squares back-substitution and all stopping tests run on the
+// host on the same scalars, in the same order as Krylov.jl.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <vector>
+
+#include "nk_internal.hpp"
+
+struct nk_workspace {
+    nk_ctx* c = nullptr;
+    int algo = NK_ALGO_GMRES;
+    nk_problem prob{};
+    int mem = 20;
+    int64_t n = 0;
+    double* x = nullptr;
+    double* w = nullptr;   // gmres: q (= w); cg: Ap
+    double* xr = nullptr;  // gmres restart: Δx (chunked x update);  cg: r
+    double* p = nullptr;   // cg: search direction
+    std::vector<double*> V;
+    double* hdev = nullptr;  // device Hessenberg column (2*cap + 2 doubles)
+    double* ydev = nullptr;  // device y (cap doubles)
+    double* hpin = nullptr;  // pinned host mirror of hdev
+    double* ypin = nullptr;  // pinned host y
+    int cap = 0;             // capacity of hdev / ydev / pinned buffers (in basis vectors)
+};
+
+namespace nk {
+namespace {
+
+int ws_scalars(nk_workspace* ws, int need) {
+    if (need <= ws->cap) return NK_OK;
+    nk_ctx* c = ws->c;
+    int cap = ws->cap ? ws->cap : 64;
+    while (cap < need) cap *= 2;
+    NK_HIP(c, hipStreamSynchronize(c->stream));
+    if (ws->hdev) (void)hipFree(ws->hdev);
+    if (ws->ydev) (void)hipFree(ws->ydev);
+    if (ws->hpin) (void)hipHostFree(ws->hpin);
+    if (ws->ypin) (void)hipHostFree(ws->ypin);
+    ws->hdev = ws->ydev = ws->hpin = ws->ypin = nullptr;
+    NK_HIP(c, hipMalloc(&ws->hdev, sizeof(double) * (2 * (size_t)cap + 2)));
+    NK_HIP(c, hipMalloc(&ws->ydev, sizeof(double) * (size_t)cap));
+    NK_HIP(c, hipHostMalloc(&ws->hpin, sizeof(double) * (2 * (size_t)cap + 2), hipHostMallocDefault));
+    NK_HIP(c, hipHostMalloc(&ws->ypin, sizeof(double) * (size_t)cap, hipHostMallocDefault));
+    ws->cap = cap;
+    return NK_OK;
+}
+
+int ws_basis(nk_workspace* ws, int need) {
+    while ((int)ws->V.size() < need) {
+        double* v = nullptr;
+        NK_TRY(nk_vec_alloc(ws->c, &ws->prob, &v));
+        ws->V.push_back(v);
+    }
+    return NK_OK;
+}
+
+inline double sgn(double x) { return (double)((x > 0) - (x < 0)); }
+
+// Krylov.jl sym_givens (real case)
+void sym_givens(double a, double b, double* c, double* s, double* rho) {
+    if (b == 0.0) {
+        *c = (a == 0.0) ? 1.0 : sgn(a);
+        *s = 0.0;
+        *rho = std::fabs(a);
+    } else if (a == 0.0) {
+        *c = 0.0;
+        *s = sgn(b);
+        *rho = std::fabs(b);
+    } else if (std::fabs(b) > std::fabs(a)) {
+        const double t = a / b;
+        *s = sgn(b) / std::sqrt(1.0 + t * t);
+        *c = *s * t;
+        *rho = b / *s;
+    } else {
+        const double t = b / a;
+        *c = sgn(a) / std::sqrt(1.0 + t * t);
+        *s = *c * t;
+        *rho = a / *c;
+    }
+}
+
+// reduce `r` to one host scalar (optionally sqrt) through the context's pinned scratch
+int host_scalar(nk_ctx* c, Red r, int sqrt_it, double* out) {
+    NK_TRY(finish_reduction(c, &r));
+    NK_TRY(launch_finalize(c, r, c->scal, sqrt_it));
+    NK_HIP(c, hipMemcpyAsync(c->hpin, c->scal, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    NK_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->prof) prof_drain(c, false);
+    *out = c->hpin[0];
+    return NK_OK;
+}
+
+struct Op {
+    nk_ctx* c;
+    const nk_problem* p;
+    int mode;  // NK_JV_*
+    const double* u;
+    const double* F0;
+    double unorm;
+    int64_t n_matvec = 0;
+
+    // out = J v  (+ epilogue).  vnorm: ||v|| for the FD step (1 for Arnoldi basis vectors).
+    int apply(double* out, const double* v, double vnorm, int epi, const double* aux, Red* red) {
+        ++n_matvec;
+        double eps = 0.0;
+        if (mode == NK_JV_FD) {
+            if (vnorm == 0.0) {  // J 0 = 0
+                NK_TRY(launch_fill(c, ws_n(), out, 0.0));
+                if (epi == EPI_RESID) NK_TRY(launch_copy(c, ws_n(), out, aux));
+                if (epi != EPI_NONE) {
+                    if (epi == EPI_DOT) return launch_dot(c, ws_n(), aux, out, red);
+                    return launch_sumsq(c, ws_n(), out, red);
+                }
+                return NK_OK;
+            }
+            eps = std::sqrt(DBL_EPSILON) * std::fmax(1.0, unorm) / vnorm;
+        }
+        NK_TRY(halo_exchange(c, p, v));
+        StencilIn in{p, mode == NK_JV_FD ? MODE_JFD : MODE_JEXACT, epi, out, u, v, F0, aux, eps};
+        return launch_stencil(c, in, red);
+    }
+    int64_t ws_n() const { return p->nx * p->ny * p->nz; }
+};
+
+#define PUSH_HIST(v)                                   \
+    do {                                               \
+        if (hist && nh < hist_cap) hist[nh] = (v);     \
+        ++nh;                                          \
+    } while (0)
+
+int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const nk_krylov_opts* o, nk_krylov_stats* st,
+          double* hist, int64_t hist_cap, int64_t* hist_len) {
+    nk_ctx* c = ws->c;
+    const int64_t n = ws->n;
+    const int mem = ws->mem;
+    const int restart = o->restart, reorth = o->reorthogonalization;
+    int64_t itmax = o->itmax;
+    int64_t nh = 0;
+    double* x = ws->x;
+    double* w = ws->w;
+
+    // host Krylov state (same layout as Krylov.jl: R column-packed)
+    int hcap = mem;
+    std::vector<double> cs(hcap), sn(hcap), z(hcap + 1), R((size_t)hcap * (hcap + 1) / 2);
+
+    NK_TRY(ws_basis(ws, mem));
+    NK_TRY(ws_scalars(ws, mem + 1));
+    NK_TRY(launch_fill(c, n, x, 0.0));  // x .= 0 ; r0 = b - A*0 = b
+    Red rb{};
+    NK_TRY(launch_sumsq(c, n, b, &rb));
+    double beta = 0.0;
+    NK_TRY(host_scalar(c, rb, 1, &beta));
+    double rNorm = beta;
+    PUSH_HIST(rNorm);
+    const double eps_ = o->atol + o->rtol * rNorm;
+    st->inconsistent = 0;
+    st->breakdown = 0;
+    if (beta == 0.0) {
+        st->niter = 0;
+        st->solved = 1;
+        st->status = 1;
+        if (hist_len) *hist_len = nh;
+        return NK_OK;
+    }
+    int npass = 0;
+    int64_t iter = 0, inner_iter = 0;
+    if (itmax == 0) itmax = 2 * n;
+    int64_t inner_itmax = itmax;
+    const double btol = std::pow(DBL_EPSILON, 0.75);
+    bool breakdown = false, inconsistent = false;
+    bool solved = rNorm <= eps_;
+    bool tired = iter >= itmax;
+    double xnorm = 0.0;  // ||x|| for the FD restart residual (from the fused x update)
+    while (!(solved || tired || breakdown)) {
+        int64_t nr = 0;
+        std::fill(cs.begin(), cs.end(), 0.0);
+        std::fill(sn.begin(), sn.end(), 0.0);
+        std::fill(z.begin(), z.end(), 0.0);
+        std::fill(R.begin(), R.end(), 0.0);
+        const double* src = b;
+        if (restart && npass >= 1) {
+            Red rr{};
+            NK_TRY(A.apply(w, x, xnorm, EPI_RESID, b, &rr));  // w = b - A x, fused ||w||^2 partials
+            NK_TRY(host_scalar(c, rr, 1, &beta));
+            src = w;
+        }
+        z[0] = beta;
+        NK_TRY(launch_divcopy(c, n, ws->V[0], src, beta));  // V1 = r0 / beta
+        npass++;
+        inner_iter = 0;
+        bool inner_tired = false;
+        while (!(solved || inner_tired || breakdown)) {
+            inner_iter++;
+            const int k = (int)inner_iter;
+            if (k + 1 > hcap) {  // unrestarted GMRES grows beyond `memory`
+                int nc = hcap * 2;
+                cs.resize(nc, 0.0);
+                sn.resize(nc, 0.0);
+                z.resize(nc + 1, 0.0);
+                R.resize((size_t)nc * (nc + 1) / 2, 0.0);
+                hcap = nc;
+            }
+            const int npasses = reorth ? 2 * k : k;
+            NK_TRY(ws_scalars(ws, npasses + 1));
+            // q = A V_k, fused with the partials of <V_1, q>
+            Red red{};
+            NK_TRY(A.apply(w, ws->V[k - 1], 1.0, EPI_DOT, ws->V[0], &red));
+            for (int t = 0; t < npasses; ++t) {
+                const double* vi = ws->V[t % k];
+                const double* vnext = (t + 1 < npasses) ? ws->V[(t + 1) % k] : nullptr;
+                NK_TRY(finish_reduction(c, &red));
+                Red nxt{};
+                NK_TRY(launch_mgs_pass(c, n, w, vi, vnext, red, ws->hdev + t, &nxt));
+                red = nxt;
+            }
+            NK_TRY(finish_reduction(c, &red));
+            NK_TRY(launch_finalize(c, red, ws->hdev + npasses, 1));  // h_{k+1,k} = ||q||
+            NK_HIP(c, hipMemcpyAsync(ws->hpin, ws->hdev, sizeof(double) * (npasses + 1), hipMemcpyDeviceToHost, c->stream));
+            NK_HIP(c, hipStreamSynchronize(c->stream));
+            if (c->prof) prof_drain(c, false);
+            for (int i = 0; i < k; ++i) R[nr + i] = ws->hpin[i];
+            if (reorth)
+                for (int i = 0; i < k; ++i) R[nr + i] += ws->hpin[k + i];
+            const double Hbis = ws->hpin[npasses];
+            for (int i = 1; i <= k - 1; ++i) {
+                const double Rtmp = cs[i - 1] * R[nr + i - 1] + sn[i - 1] * R[nr + i];
+                R[nr + i] = sn[i - 1] * R[nr + i - 1] - cs[i - 1] * R[nr + i];
+                R[nr + i - 1] = Rtmp;
+            }
+            sym_givens(R[nr + k - 1], Hbis, &cs[k - 1], &sn[k - 1], &R[nr + k - 1]);
+            const double zeta = sn[k - 1] * z[k - 1];
+            z[k - 1] = cs[k - 1] * z[k - 1];
+            rNorm = std::fabs(zeta);
+            PUSH_HIST(rNorm);
+            nr += k;
+            const bool mach = (rNorm + 1.0 <= 1.0);
+            solved = (rNorm <= eps_) || mach;
+            breakdown = Hbis <= btol;
+            inner_tired = restart ? (inner_iter >= std::min<int64_t>(mem, inner_itmax)) : (inner_iter >= inner_itmax);
+            if (!(solved || inner_tired || breakdown)) {
+                NK_TRY(ws_basis(ws, k + 1));
+                NK_TRY(launch_divcopy(c, n, ws->V[k], w, Hbis));  // V_{k+1} = q / h_{k+1,k}
+                z[k] = zeta;
+            }
+        }
+        // back substitution R y = z (Krylov.jl, y stored in z)
+        const int kk = (int)inner_iter;
+        for (int i = kk; i >= 1; --i) {
+            int64_t pos = nr + i - kk;
+            for (int j = kk; j >= i + 1; --j) {
+                z[i - 1] = z[i - 1] - R[pos - 1] * z[j - 1];
+                pos = pos - j + 1;
+            }
+            if (std::fabs(R[pos - 1]) <= btol) {
+                z[i - 1] = 0.0;
+                inconsistent = true;
+            } else {
+                z[i - 1] = z[i - 1] / R[pos - 1];
+            }
+        }
+        NK_TRY(ws_scalars(ws, kk + 1));
+        for (int i = 0; i < kk; ++i) ws->ypin[i] = z[i];
+        NK_HIP(c, hipMemcpyAsync(ws->ydev, ws->ypin, sizeof(double) * kk, hipMemcpyHostToDevice, c->stream));
+        iter += inner_iter;
+        inner_itmax = itmax - iter;
+        tired = iter >= itmax;
+        const bool need_xnorm = restart && A.mode == NK_JV_FD && !(solved || tired || breakdown);
+        Red xr{};
+        NK_TRY(launch_update_x(c, n, x, ws->xr, ws->V.data(), kk, ws->ydev, restart, need_xnorm ? &xr : nullptr));
+        if (need_xnorm) NK_TRY(host_scalar(c, xr, 1, &xnorm));
+        else {
+            NK_HIP(c, hipStreamSynchronize(c->stream));  // ypin may be rewritten next cycle
+        }
+    }
+    st->niter = iter;
+    st->solved = solved;
+    st->inconsistent = inconsistent;
+    st->breakdown = breakdown;
+    st->status = solved ? 1 : (tired ? 2 : (breakdown ? 3 : 0));
+    if (hist_len) *hist_len = nh;
+    return NK_OK;
+}
+
+int cg(nk_workspace* ws, Op& A, const double* b, const nk_krylov_opts* o, nk_krylov_stats* st, double* hist,
+       int64_t hist_cap, int64_t* hist_len) {
+    nk_ctx* c = ws->c;
+    const int64_t n = ws->n;
+    int64_t nh = 0;
+    double *x = ws->x, *r = ws->xr, *p = ws->p, *Ap = ws->w;
+    NK_TRY(launch_fill(c, n, x, 0.0));
+    NK_TRY(launch_copy(c, n, r, b));
+    NK_TRY(launch_copy(c, n, p, r));
+    Red rg{};
+    NK_TRY(launch_sumsq(c, n, r, &rg));
+    double gamma = 0.0;
+    NK_TRY(host_scalar(c, rg, 0, &gamma));
+    double rNorm = std::sqrt(gamma);
+    PUSH_HIST(rNorm);
+    st->inconsistent = 0;
+    st->breakdown = 0;
+    if (gamma == 0.0) {
+        st->niter = 0;
+        st->solved = 1;
+        st->status = 1;
+        if (hist_len) *hist_len = nh;
+        return NK_OK;
+    }
+    int64_t iter = 0, itmax = o->itmax == 0 ? 2 * n : o->itmax;
+    double pNorm2 = gamma;
+    const double eps_ = o->atol + o->rtol * rNorm;
+    bool solved = rNorm <= eps_, tired = iter >= itmax, zero_curvature = false, inconsistent = false;
+    while (!(solved || tired || zero_curvature)) {
+        double pnorm = 1.0;
+        if (A.mode == NK_JV_FD) {
+            Red rp{};
+            NK_TRY(launch_sumsq(c, n, p, &rp));
+            NK_TRY(host_scalar(c, rp, 1, &pnorm));
+        }
+        Red rpa{};
+        NK_TRY(A.apply(Ap, p, pnorm, EPI_DOT, p, &rpa));  // Ap and the partials of <p, Ap>
+        double pAp = 0.0;
+        NK_TRY(host_scalar(c, rpa, 0, &pAp));
+        if (pAp <= DBL_EPSILON * pNorm2) {
+            if (std::fabs(pAp) <= DBL_EPSILON * pNorm2) {
+                zero_curvature = true;
+                inconsistent = true;
+            }
+        }
+        if (zero_curvature) continue;
+        const double alpha = gamma / pAp;
+        Red rn{};
+        NK_TRY(launch_cg_update(c, n, alpha, x, r, p, Ap, &rn));  // x += a p ; r -= a Ap ; <r,r>
+        double gamma_next = 0.0;
+        NK_TRY(host_scalar(c, rn, 0, &gamma_next));
+        rNorm = std::sqrt(gamma_next);
+        PUSH_HIST(rNorm);
+        const bool mach = (rNorm + 1.0 <= 1.0);
+        solved = (rNorm <= eps_) || mach;
+        if (!solved) {
+            const double beta = gamma_next / gamma;
+            pNorm2 = gamma_next + beta * beta * pNorm2;
+            gamma = gamma_next;
+            NK_TRY(launch_cg_direction(c, n, beta, p, r));  // p = r + beta p
+        }
+        iter++;
+        tired = iter >= itmax;
+    }
+    NK_HIP(c, hipStreamSynchronize(c->stream));
+    st->niter = iter;
+    st->solved = solved;
+    st->inconsistent = inconsistent;
+    st->status = solved ? 1 : (tired ? 2 : (zero_curvature ? 4 : 0));
+    if (hist_len) *hist_len = nh;
+    return NK_OK;
+}
+
+}  // namespace
+}  // namespace nk
+
+using namespace nk;
+
+extern "C" {
+
+int nk_workspace_create(nk_ctx* c, int32_t algo, const nk_problem* p, int32_t memory, nk_workspace** out) {
+    if (!c || !p || !out) return NK_E_ARG;
+    if (algo != NK_ALGO_GMRES && algo != NK_ALGO_CG) return fail(c, NK_E_ARG, "unsupported Krylov algorithm");
+    Geo g;
+    NK_TRY(geometry(c, p, &g));
+    nk_workspace* ws = new nk_workspace();
+    ws->c = c;
+    ws->algo = algo;
+    ws->prob = *p;
+    ws->prob.un = p->un ? p->un : reinterpret_cast<const double*>(1);  // geometry only
+    ws->mem = memory > 0 ? memory : 20;
+    ws->n = g.n;
+    int rc = NK_OK;
+    if ((rc = nk_vec_alloc(c, &ws->prob, &ws->x)) != NK_OK || (rc = nk_vec_alloc(c, &ws->prob, &ws->w)) != NK_OK ||
+        (rc = nk_vec_alloc(c, &ws->prob, &ws->xr)) != NK_OK) {
+        nk_workspace_destroy(ws);
+        return rc;
+    }
+    if (algo == NK_ALGO_CG) {
+        if ((rc = nk_vec_alloc(c, &ws->prob, &ws->p)) != NK_OK) {
+            nk_workspace_destroy(ws);
+            return rc;
+        }
+    } else {
+        if ((rc = ws_basis(ws, ws->mem)) != NK_OK || (rc = ws_scalars(ws, ws->mem + 1)) != NK_OK) {
+            nk_workspace_destroy(ws);
+            return rc;
+        }
+    }
+    *out = ws;
+    return NK_OK;
+}
+
+int nk_workspace_destroy(nk_workspace* ws) {
+    if (!ws) return NK_OK;
+    nk_ctx* c = ws->c;
+    for (double* v : ws->V) nk_vec_free(c, v);
+    for (double* v : {ws->x, ws->w, ws->xr, ws->p})
+        if (v) nk_vec_free(c, v);
+    if (ws->hdev) (void)hipFree(ws->hdev);
+    if (ws->ydev) (void)hipFree(ws->ydev);
+    if (ws->hpin) (void)hipHostFree(ws->hpin);
+    if (ws->ypin) (void)hipHostFree(ws->ypin);
+    delete ws;
+    return NK_OK;
+}
+
+double* nk_workspace_x(nk_workspace* ws) { return ws ? ws->x : nullptr; }
+
+int nk_krylov_solve(nk_workspace* ws, const nk_problem* p, const double* u, const double* F0, const double* b,
+                    const nk_krylov_opts* o, nk_krylov_stats* st, double* hist, int64_t hist_cap, int64_t* hist_len) {
+    if (!ws || !p || !u || !b || !o || !st) return NK_E_ARG;
+    nk_ctx* c = ws->c;
+    Geo g;
+    NK_TRY(geometry(c, p, &g));
+    if (g.n != ws->n) return fail(c, NK_E_ARG, "problem size does not match the workspace");
+    if (o->jv_mode == NK_JV_FD && !F0) return fail(c, NK_E_ARG, "FD Jv needs F0 = F(u)");
+    *st = nk_krylov_stats{};
+    Op A{c, p, o->jv_mode, u, F0, 0.0};
+    NK_TRY(halo_exchange(c, p, u));  // u is constant during the solve: one exchange
+    if (o->jv_mode == NK_JV_FD) {
+        Red ru{};
+        NK_TRY(launch_sumsq(c, ws->n, u, &ru));
+        NK_TRY(host_scalar(c, ru, 1, &A.unorm));
+    }
+    int rc = (ws->algo == NK_ALGO_CG) ? cg(ws, A, b, o, st, hist, hist_cap, hist_len)
+                                      : gmres(ws, p, A, b, o, st, hist, hist_cap, hist_len);
+    st->n_matvec = A.n_matvec;
+    return rc;
+}
+
+}  // extern "C"

@@ -297,3 +297,23 @@ def newton_krylov(P: Problem, u0, *, tol_rel=1e-6, tol_abs=1e-12, max_niter=50, 
                  solved=bool(st.solved), n_matvec=st.n_matvec, n_residual=st.n_residual, tol=st.tol,
                  n_res_history=hist[: k + 1].copy(), inner_history=inner[:k].copy())
     return u, stats
+
+
+def _blas1(name, *args):
+    getattr(lib(), name)(*args)
+
+
+def axpy(s, x, y):
+    """y + s x with fma (Krylov kaxpy! on dense vectors); returns a new array."""
+    x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
+    y = np.array(y, dtype=np.float64).reshape(-1)
+    lib().oc_axpy(x.size, float(s), _p(x), _p(y))
+    return y
+
+
+def axpby(s, x, t, y):
+    """s x + t y as fma(t, y, s*x) (Krylov kaxpby!); returns a new array."""
+    x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
+    y = np.array(y, dtype=np.float64).reshape(-1)
+    lib().oc_axpby(x.size, float(s), _p(x), float(t), _p(y))
+    return y

@@ -1,0 +1,95 @@
+"""CPU-only checks of the product boundary: libnkhip.so loads, exports every symbol the public
+header declares, and the host mirror fails loudly without a GPU (no CPU fallback)."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import _nkpath  # noqa: F401
+import ariadne_hip as ah
+from ariadne_hip import _lib
+from oracle import oracle as oc
+
+HEADER = _lib.HEADER
+
+
+def header_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|double\*|const char\*)\s+(nk_\w+)\s*\(", src, re.M)))
+
+
+def test_library_built_in_tree():
+    assert os.path.exists(_lib.LIB_PATH), "run __graft_entry__.build()"
+    assert _lib.LIB_PATH.startswith(os.path.dirname(os.path.dirname(__file__)))
+
+
+def test_every_header_symbol_exported_and_bound():
+    lib = ah.load()
+    names = header_functions()
+    assert len(names) >= 30
+    for name in names:
+        assert hasattr(lib, name), f"{name} declared in include/nkhip.h but not exported"
+        assert name in _lib.SIGNATURES, f"{name} has no ctypes signature"
+    assert set(_lib.SIGNATURES) == set(names)
+
+
+def test_header_structs_match_ctypes():
+    src = open(HEADER).read()
+    body = re.search(r"typedef struct nk_problem \{(.*?)\} nk_problem;", src, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    fields = re.findall(r"\b(\w+);", body.replace(",", ";"))
+    # names differ only where Python reserves the word (lambda -> lam)
+    want = [f if f != "lambda" else "lam" for f in fields]
+    got = [f[0] for f in _lib.nk_problem._fields_]
+    assert got == want
+
+
+def test_no_gpu_fails_loudly():
+    if _lib.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(ah.NKError):
+        ah.Context(0)
+
+
+def test_forcing_mirror_matches_oracle():
+    ew = ah.EisenstatWalker()
+    rng = np.random.default_rng(7)
+    for _ in range(100):
+        eta, tol = rng.uniform(0, 1), 10 ** rng.uniform(-12, -2)
+        prior = 10 ** rng.uniform(-6, 2)
+        n = prior * rng.uniform(0.01, 1.2)
+        assert ew(eta, tol, n, prior) == oc.ew_forcing(eta, tol, n, prior)
+    assert ah.Fixed().initial() == 0.1 and ah.Fixed(0.3)(1, 2, 3, 4) == 0.3
+    assert ew.initial() == 0.999
+
+
+def test_stats_update():
+    s = ah.Stats(0, 0, 1.0).update(7, 0.5).update(3, 0.25)
+    assert s == ah.Stats(2, 10, 0.25)
+
+
+def test_slab_partition():
+    for n, r in [(4096, 8), (37, 4), (9, 3), (5, 5)]:
+        grids = [ah.slab((16, n), k, r) for k in range(r)]
+        assert sum(g.shape_xyz[-1] for g in grids) == n
+        assert [g.offset for g in grids] == list(np.cumsum([0] + [g.shape_xyz[-1] for g in grids])[:-1])
+        assert all(g.global_xyz == (16, n) for g in grids)
+    with pytest.raises(ValueError):
+        ah.slab((4, 2), 0, 3)
+
+
+def test_grid_shapes():
+    g = ah.Grid.full(7, 5)
+    assert g.np_shape == (5, 7) and g.n == 35 and g.nxyz == (7, 5, 1)
+    g3 = ah.Grid.full(4, 3, 2)
+    assert g3.np_shape == (2, 3, 4) and g3.dim == 3
+
+
+def test_unsupported_algo_and_generic_residual_rejected():
+    with pytest.raises(NotImplementedError):
+        ah.krylov.KrylovWorkspace("bicgstab", ah.KrylovConstructor.__new__(ah.KrylovConstructor))
+    with pytest.raises(TypeError):
+        ah.JacobianOperator(lambda r, u, p: None, None, None)
+    with pytest.raises(NotImplementedError):
+        ah.G_Midpoint_.bind(ah.diffusion_)

@@ -1,0 +1,345 @@
+"""GPU parity tests: the HIP path (through libnkhip.so's C ABI) against the CPU oracle and the goldens.
+
+Tolerances (stated per test):
+  * heat residual / JVP: no transcendental -> bit-identical to the oracle (both -ffp-contract=off,
+    same association order).
+  * Bratu residual / JVP: identical except `exp` (ocml vs glibc, <= 1 ulp): |diff| <= 4 ulp of
+    lambda * max(exp(u)) (absolute), i.e. ~1e-15 relative.
+  * BLAS-1 elementwise ops: bit-identical (same fma convention); dot/norm: 1e-13 relative
+    (different, but fixed, summation order).
+  * Krylov / Newton: equal iteration counts; residual histories 1e-8 relative over the first cycle;
+    converged solutions to the stated solver tolerance.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import _nkpath  # noqa: F401
+import ariadne_hip as ah
+from oracle import oracle as oc
+
+pytestmark = pytest.mark.gpu
+
+ULP = np.finfo(np.float64).eps
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = ah.Context(0)
+    ah.set_default_context(c)
+    yield c
+    c.sync()
+
+
+def dev(a, grid=None):
+    return ah.DeviceArray.from_numpy(a, grid)
+
+
+def params(P):
+    if P.kind == oc.BRATU1D:
+        return ah.bratu_, (P.hx, P.lam)
+    if P.kind == oc.BRATU2D:
+        return ah.bratu2d_, (P.hx, P.hy, P.lam)
+    un = dev(P.un)
+    if P.kind == oc.HEAT2D_EULER:
+        return ah.heat2d_euler_, (un, P.dt, None, (P.a, P.hx, P.hy, ah.bc_zero_), 0.0)
+    return ah.heat3d_euler_, (un, P.dt, None, (P.a, P.hx, P.hy, P.hz, ah.bc_zero_), 0.0)
+
+
+def bratu_atol(P, u):
+    return 4 * ULP * P.lam * float(np.exp(np.max(u)))
+
+
+def problems():
+    rng = np.random.default_rng(11)
+    out = []
+    for P in (oc.bratu1d(1000), oc.bratu1d(7), oc.bratu2d(64), oc.bratu2d(63, 37), oc.bratu2d(1000, 5),
+              oc.bratu2d(1, 1), oc.bratu2d(3, 1), oc.bratu2d(1, 6), oc.bratu2d(130, 9)):
+        out.append((P, oc.sin_ic(P) + 0.05 * rng.standard_normal(P.shape)))
+    for shape in ((40, 40), (130, 67), (33, 5), (1, 1)):
+        un = rng.standard_normal(shape[::-1])
+        P = oc.heat2d_euler(*shape, un=un)
+        out.append((P, un + 0.01 * rng.standard_normal(un.shape)))
+    for shape in ((12, 12, 12), (33, 17, 9), (8, 5, 20), (2, 3, 1)):
+        un = rng.standard_normal(shape[::-1])
+        P = oc.heat3d_euler(*shape, un=un)
+        out.append((P, un + 0.01 * rng.standard_normal(un.shape)))
+    return out
+
+
+PROBLEMS = problems()
+IDS = [f"k{P.kind}-{P.nx}x{P.ny}x{P.nz}" for P, _ in PROBLEMS]
+
+
+def compare(P, got, ref, u):
+    if P.kind in (oc.HEAT2D_EULER, oc.HEAT3D_EULER):
+        assert np.array_equal(got, ref), f"max diff {np.max(np.abs(got - ref))}"
+    else:
+        assert np.max(np.abs(got - ref)) <= bratu_atol(P, u), np.max(np.abs(got - ref))
+
+
+@pytest.mark.parametrize("P,u", PROBLEMS, ids=IDS)
+def test_residual_parity(ctx, P, u):
+    F, p = params(P)
+    ud = dev(u)
+    res = ud.zero()
+    F(res, ud, p)
+    compare(P, res.to_numpy(), oc.residual(P, u), u)
+    nrm = F.residual_norm(res, ud, p)
+    assert abs(nrm - oc.norm(oc.residual(P, u))) <= 1e-13 * nrm + 1e-300
+
+
+@pytest.mark.parametrize("P,u", PROBLEMS, ids=IDS)
+def test_jv_exact_parity(ctx, P, u):
+    F, p = params(P)
+    v = np.random.default_rng(3).standard_normal(u.shape)
+    ud, vd = dev(u), dev(v)
+    res, out = ud.zero(), ud.zero()
+    ah.mul_(out, ah.JacobianOperator(F, res, ud, p, jv="exact"), vd)
+    ref = oc.jv_exact(P, u, v)
+    if P.kind in (oc.HEAT2D_EULER, oc.HEAT3D_EULER):
+        assert np.array_equal(out.to_numpy(), ref)
+    else:
+        assert np.max(np.abs(out.to_numpy() - ref)) <= 4 * ULP * P.lam * np.max(np.exp(u) * np.abs(v)) + 1e-300
+
+
+@pytest.mark.parametrize("P,u", PROBLEMS, ids=IDS)
+def test_jv_fd_parity(ctx, P, u):
+    F, p = params(P)
+    v = np.random.default_rng(4).standard_normal(u.shape)
+    ud, vd = dev(u), dev(v)
+    res, out = ud.zero(), ud.zero()
+    F(res, ud, p)
+    F0 = res.to_numpy()  # same F0 on both sides: only F(u + eps v) is recomputed
+    eps = oc.fd_eps(oc.norm(u), oc.norm(v))
+    ah.mul_(out, ah.JacobianOperator(F, res, ud, p, jv="fd"), vd, eps=eps)
+    ref = oc.jv_fd(P, u, v, F0, eps)
+    if P.kind in (oc.HEAT2D_EULER, oc.HEAT3D_EULER):
+        assert np.array_equal(out.to_numpy(), ref)
+    else:
+        # exp of u + eps v differs by <= 1 ulp; the difference quotient divides that by eps
+        assert np.max(np.abs(out.to_numpy() - ref)) <= bratu_atol(P, u) / eps * 2
+    # and the FD operator approximates the exact JVP
+    exact = oc.jv_exact(P, u, v)
+    assert np.max(np.abs(out.to_numpy() - exact)) <= 1e-5 * np.max(np.abs(exact))
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 1000, 4097, 1 << 20])
+def test_blas1_parity(ctx, n):
+    rng = np.random.default_rng(n)
+    x, y = rng.standard_normal(n), rng.standard_normal(n)
+    g = ah.Grid.full(n)
+    xd, yd = dev(x, g), dev(y, g)
+    assert abs(ah.kdot(n, xd, yd) - np.dot(x, y)) <= 1e-13 * np.sqrt(n) * np.linalg.norm(x) * np.linalg.norm(y)
+    assert abs(ah.knorm(n, xd) - np.linalg.norm(x)) <= 1e-13 * np.linalg.norm(x)
+    s, t = 0.37, -1.25
+    assert np.array_equal(ah.kaxpy_(n, s, xd, yd.copy()).to_numpy(), oc.axpy(s, x, y))
+    assert np.array_equal(ah.kaxpby_(n, s, xd, t, yd.copy()).to_numpy(), oc.axpby(s, x, t, y))
+    assert np.array_equal(ah.kscal_(n, s, xd.copy()).to_numpy(), s * x)
+    assert np.array_equal(ah.kdivcopy_(n, yd.copy(), xd, 3.0).to_numpy(), x / 3.0)
+    assert np.array_equal(ah.kcopy_(n, yd.copy(), xd).to_numpy(), x)
+    assert np.array_equal(ah.kfill_(xd.copy(), 2.5).to_numpy(), np.full(n, 2.5))
+    a, b = ah.kref_(n, xd.copy(), yd.copy(), 0.6, 0.8)
+    assert np.array_equal(a.to_numpy(), 0.6 * x + 0.8 * y)
+    assert np.array_equal(b.to_numpy(), 0.8 * x - 0.6 * y)
+
+
+def test_dot_deterministic(ctx):
+    n = 3_000_001
+    rng = np.random.default_rng(5)
+    x, y = rng.standard_normal(n), rng.standard_normal(n)
+    g = ah.Grid.full(n)
+    xd, yd = dev(x, g), dev(y, g)
+    vals = {ah.kdot(n, xd, yd) for _ in range(5)}
+    assert len(vals) == 1
+
+
+# ----------------------------------------------------------------------------- Krylov solves
+def device_solve(P, u, b, **kw):
+    F, p = params(P)
+    ud, bd = dev(u), dev(b)
+    res = ud.zero()
+    F(res, ud, p)
+    algo = kw.pop("algo", "gmres")
+    jv = kw.pop("jv", "exact")
+    memory = kw.pop("memory", 20)
+    ws = ah.krylov_workspace(algo, ah.KrylovConstructor(res, memory=memory))
+    J = ah.JacobianOperator(F, res, ud, p, jv=jv)
+    ah.krylov_solve_(ws, J, bd, history=True, **kw)
+    return ws.x.to_numpy(), ws.stats, res.to_numpy()
+
+
+@pytest.mark.parametrize("restart,memory,reorth,jv", [(False, 20, False, "exact"), (True, 10, False, "exact"),
+                                                      (True, 8, True, "exact"), (True, 10, False, "fd")])
+def test_gmres_matches_oracle(ctx, restart, memory, reorth, jv):
+    P = oc.bratu2d(24)
+    u = oc.sin_ic(P)
+    b = oc.residual(P, u)
+    kw = dict(restart=restart, reorthogonalization=reorth, atol=1e-12, rtol=1e-9, itmax=150)
+    x, st, F0 = device_solve(P, u, b, memory=memory, jv=jv, **kw)
+    xo, sto, ho = oc.krylov_solve(P, u, b, jv=jv, F0=F0, memory=memory, **kw)
+    assert st.niter == sto["niter"] and st.solved == sto["solved"]
+    assert st.n_matvec == sto["n_matvec"]
+    h = np.array(st.residuals)
+    assert np.allclose(h[: memory + 1], ho[: memory + 1], rtol=1e-8, atol=0)
+    m = ho > 1e-6 * ho[0]
+    assert np.allclose(h[m], ho[m], rtol=1e-5)
+    assert np.max(np.abs(x - xo)) <= 1e-7 * np.max(np.abs(xo))
+
+
+def test_cg_matches_oracle(ctx):
+    P = oc.bratu1d(300)
+    u = oc.sin_ic(P)
+    b = oc.residual(P, u)
+    x, st, _ = device_solve(P, u, b, algo="cg", atol=1e-12, rtol=1e-10)
+    xo, sto, ho = oc.krylov_solve(P, u, b, algo="cg", atol=1e-12, rtol=1e-10)
+    assert st.niter == sto["niter"]
+    m = ho > 1e-6 * ho[0]
+    assert np.allclose(np.array(st.residuals)[m], ho[m], rtol=1e-6)
+    assert np.max(np.abs(x - xo)) <= 1e-6 * np.max(np.abs(xo))
+
+
+def test_gmres_deterministic(ctx):
+    P = oc.bratu2d(48)
+    u = oc.sin_ic(P)
+    b = oc.residual(P, u)
+    xs = [device_solve(P, u, b, restart=True, memory=10, itmax=40, atol=0.0, rtol=0.0)[0] for _ in range(2)]
+    assert np.array_equal(xs[0], xs[1])
+
+
+# ----------------------------------------------------------------------------- Newton (Ariadne)
+def test_newton_bratu1d_cg_config1(ctx, golden_dir):
+    """BASELINE config 1: examples/bratu.jl:59-63 (N = 1000, algo = :cg) -- solved, same stats as the oracle."""
+    g = np.load(os.path.join(golden_dir, "bratu1d_n1000.npz"))
+    P = oc.bratu1d(1000)
+    u = dev(g["u0"])
+    u, r = ah.newton_krylov_(ah.bratu_, u, (P.hx, P.lam), u.similar(), algo="cg")
+    uo, so = oc.newton_krylov(P, g["u0"], algo="cg")
+    assert r.solved and so["solved"]
+    assert r.stats.outer_iterations == so["outer_iterations"]
+    assert abs(r.stats.inner_iterations - so["inner_iterations"]) <= 0.02 * so["inner_iterations"]
+    assert np.max(np.abs(u.to_numpy() - g["true_sol"])) < 3e-4
+
+
+def test_newton_bratu2d_gmres30_golden(ctx, golden_dir):
+    g = np.load(os.path.join(golden_dir, "bratu2d_64.npz"))
+    P = oc.bratu2d(64)
+    u = dev(g["u0"])
+    kw = dict(restart=True)
+    u, r = ah.newton_krylov_(ah.bratu2d_, u, (P.hx, P.hy, P.lam), memory=30, tol_rel=1e-10, krylov_kwargs=kw)
+    uo, so = oc.newton_krylov(P, g["u0"], memory=30, restart=True, tol_rel=1e-10)
+    assert r.solved
+    assert r.stats.outer_iterations == so["outer_iterations"]
+    assert r.stats.inner_iterations == so["inner_iterations"]
+    assert np.max(np.abs(u.to_numpy() - g["ustar"])) <= 1e-8 * np.max(np.abs(g["ustar"]))
+    # north-star parity statement: same ||F(u)|| as the CPU path on the same final iterate
+    Fo = oc.norm(oc.residual(P, u.to_numpy()))
+    assert abs(Fo - r.stats.n_res) <= 1e-10 * Fo
+
+
+def test_newton_fd_vs_exact(ctx):
+    P = oc.bratu2d(32)
+    u0 = oc.sin_ic(P)
+    p = (P.hx, P.hy, P.lam)
+    kw = dict(restart=True)
+    ue, re_ = ah.newton_krylov_(ah.bratu2d_, dev(u0), p, memory=30, tol_rel=1e-9, krylov_kwargs=kw, jv="exact")
+    uf, rf = ah.newton_krylov_(ah.bratu2d_, dev(u0), p, memory=30, tol_rel=1e-9, krylov_kwargs=kw, jv="fd")
+    uo, so = oc.newton_krylov(P, u0, memory=30, restart=True, tol_rel=1e-9, jv="fd")
+    assert re_.solved and rf.solved
+    assert rf.stats.outer_iterations == so["outer_iterations"]
+    assert np.max(np.abs(uf.to_numpy() - ue.to_numpy())) <= 1e-8 * np.max(np.abs(ue.to_numpy()))
+
+
+def test_newton_forcing_variants_and_outofplace(ctx):
+    P = oc.bratu2d(32)
+    u0 = oc.sin_ic(P)
+    p = (P.hx, P.hy, P.lam)
+    for forcing, name in ((ah.Fixed(0.1), "fixed"), (None, "none"), (ah.EisenstatWalker(), "ew")):
+        u, r = ah.newton_krylov_(ah.bratu2d_, dev(u0), p, memory=30, forcing=forcing, krylov_kwargs=dict(restart=True))
+        uo, so = oc.newton_krylov(P, u0, memory=30, restart=True, forcing=name)
+        assert r.solved and so["solved"]
+        assert r.stats.outer_iterations == so["outer_iterations"]
+    ud = dev(u0)
+    u2, r2 = ah.newton_krylov(ah.bratu2d_, ud, p, memory=30, krylov_kwargs=dict(restart=True))
+    assert r2.solved and np.array_equal(ud.to_numpy(), u0)  # out-of-place leaves u0 alone
+
+
+def test_heat2d_reference_ic_step(ctx, golden_dir):
+    """heat_2D.jl IC = Laplacian eigenvector: one implicit Euler step is an exact decay, 1 Krylov iteration."""
+    g = np.load(os.path.join(golden_dir, "heat2d_40.npz"))
+    un = dev(g["u0"])
+    u = un.copy()
+    p = (un, float(g["dt"]), None, (float(g["a"]), float(g["dx"]), float(g["dx"]), ah.bc_zero_), 0.0)
+    u, r = ah.newton_krylov_(ah.heat2d_euler_, u, p, tol_abs=6e-6)
+    assert r.solved and r.stats.inner_iterations == 1
+    assert np.max(np.abs(u.to_numpy() - g["u1"])) < 1e-10
+
+
+def test_heat2d_solve_timestepping(ctx):
+    """implicit.jl `solve` with G_Euler! on a noisy IC: per-step Newton/Krylov counts equal the oracle's."""
+    N = 64
+    rng = np.random.default_rng(0)
+    P = oc.heat2d_euler(N)
+    u0 = oc.sin_ic(P) + 0.1 * rng.uniform(-1, 1, (N, N))
+    ts = [i * P.dt for i in range(4)]
+    un = dev(u0)
+    results = []
+    ah.solve(ah.G_Euler_, ah.diffusion_, un, (P.a, P.hx, P.hy, ah.bc_zero_), P.dt, ts, stats_out=results)
+    cur = u0.copy()
+    for r in results:
+        Q = oc.heat2d_euler(N, un=cur)
+        cur, so = oc.newton_krylov(Q, cur, tol_abs=6e-6)
+        assert r.solved and so["solved"]
+        assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
+    assert np.max(np.abs(un.to_numpy() - cur)) <= 1e-10
+
+
+def test_heat3d_newton(ctx, golden_dir):
+    g = np.load(os.path.join(golden_dir, "heat3d_12.npz"))
+    P = oc.heat3d_euler(12, un=g["un"])
+    F, p = params(P)
+    u, r = ah.newton_krylov_(F, dev(g["u"]), p, tol_abs=6e-6)
+    uo, so = oc.newton_krylov(P, g["u"], tol_abs=6e-6)
+    assert r.solved and (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
+    assert np.max(np.abs(u.to_numpy() - uo)) <= 1e-12
+
+
+# ----------------------------------------------------------------------------- BASELINE size (4096^2)
+def test_bratu2d_4096_full_size(ctx):
+    """Config 2 size: kernels vs the oracle, exact-JVP linearity, and the first GMRES(30) steps."""
+    n = 4096
+    P = oc.bratu2d(n)
+    u = oc.sin_ic(P)
+    v = np.random.default_rng(9).standard_normal(u.shape)
+    F, p = params(P)
+    ud, vd = dev(u), dev(v)
+    res, out, out2 = ud.zero(), ud.zero(), ud.zero()
+    F(res, ud, p)
+    F0 = oc.residual(P, u)
+    assert np.max(np.abs(res.to_numpy() - F0)) <= bratu_atol(P, u)
+    J = ah.JacobianOperator(F, res, ud, p, jv="exact")
+    ah.mul_(out, J, vd)
+    assert np.max(np.abs(out.to_numpy() - oc.jv_exact(P, u, v))) <= 4 * ULP * P.lam * np.max(np.exp(u) * np.abs(v))
+    # linearity is exact in binary floating point for a power-of-two scale
+    ah.kscal_(len(vd), 2.0, vd)
+    ah.mul_(out2, J, vd)
+    assert np.array_equal(out2.to_numpy(), 2.0 * out.to_numpy())
+    # 12 Arnoldi steps of the FD GMRES(30) against the oracle
+    kw = dict(restart=True, atol=0.0, rtol=0.0, itmax=12)
+    x, st, F0d = device_solve(P, u, F0, memory=30, jv="fd", **kw)
+    xo, sto, ho = oc.krylov_solve(P, u, F0, jv="fd", F0=F0d, memory=30, **kw)
+    assert st.niter == sto["niter"] == 12
+    assert np.allclose(np.array(st.residuals), ho, rtol=1e-8)
+    assert np.max(np.abs(x - xo)) <= 1e-8 * np.max(np.abs(xo))
+
+
+def test_errors_are_reported(ctx):
+    u = dev(np.zeros((4, 4)))
+    bad = ah.ariadne.JacobianOperator(ah.bratu2d_, u.zero(), u, (0.1, 0.1, 1.0))
+    with pytest.raises(ValueError):
+        ah.bratu_(u.zero(), u, (0.1, 1.0))  # 1D residual on a 2D grid
+    ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(dev(np.zeros((5, 5)))))
+    with pytest.raises(ah.NKError):
+        ah.krylov_solve_(ws, bad, u)  # size mismatch with the workspace
