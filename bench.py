@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--itmax", type=int, default=300)
     ap.add_argument("--jv", choices=["fd", "exact"], default="fd")
     ap.add_argument("--no-prof", action="store_true", help="do not time kernels with HIP events")
+    ap.add_argument("--prof-every", type=int, default=16,
+                    help="time every k-th launch of each kernel class (HIP events; k > 1 keeps their cost out)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-itmax", type=int, default=30, help="Arnoldi steps in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os.cpu_count())")
@@ -116,7 +118,7 @@ def main():
     barrier()
     if not args.no_prof:
         ctx.prof_reset()
-        ctx.prof_enable(True)
+        ctx.prof_enable(args.prof_every)
     barrier()
     t0 = time.perf_counter()
     matvecs = 0
@@ -135,13 +137,15 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     prof = ctx.prof_read() if not args.no_prof else {}
-    ctx.prof_enable(False)
+    ctx.prof_enable(0)
 
-    total_bytes = sum(v["bytes"] for v in prof.values())
-    kernels = {k: dict(launches=v["launches"], avg_us=1e3 * v["ms"] / max(1, v["launches"]),
+    # algorithmic bytes of every launch (timed launches carry bytes; scale by launches / timed)
+    total_bytes = sum(v["bytes"] / max(1, v["timed"]) * v["launches"] for v in prof.values())
+    kernels = {k: dict(launches=v["launches"], timed=v["timed"], avg_us=1e3 * v["ms"] / max(1, v["timed"]),
                        gbs=(v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["ms"] > 0 else None,
-                       share=v["ms"] / max(1e-30, sum(x["ms"] for x in prof.values())))
-               for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"])}
+                       share=v["ms"] / max(1, v["timed"]) * v["launches"]
+                       / max(1e-30, sum(x["ms"] / max(1, x["timed"]) * x["launches"] for x in prof.values())))
+               for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"] / max(1, kv[1]["timed"]) * kv[1]["launches"])}
 
     def roof(name):
         v = prof.get(name)
@@ -150,7 +154,8 @@ def main():
         ach = v["bytes"] / (v["ms"] * 1e-3) / 1e9
         return {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                "bytes_per_launch": v["bytes"] / v["launches"], "avg_us": 1e3 * v["ms"] / v["launches"]}
+                "bytes_per_launch": v["bytes"] / v["timed"], "avg_us": 1e3 * v["ms"] / v["timed"],
+                "timed_launches": v["timed"]}
 
     dominant = next(iter(kernels), None)
     jv_kernel = "jv_fd_dot" if args.jv == "fd" else "jv_exact_dot"

@@ -143,11 +143,14 @@ int nk_halo_exchange(nk_ctx* ctx, const nk_problem* p, double* v);
 #define NK_PROF_NAME 32
 typedef struct nk_prof_entry {
     char name[NK_PROF_NAME];
-    int64_t launches;
-    double total_ms;       /* sum of per-launch event durations                            */
-    double bytes;          /* algorithmic bytes (compulsory HBM traffic) summed over launches */
+    int64_t launches;      /* all launches of this kernel class while profiling was on        */
+    int64_t timed;         /* launches bracketed by HIP events (every `every`-th one)          */
+    double total_ms;       /* sum of the timed launches' event durations                      */
+    double bytes;          /* algorithmic bytes (compulsory HBM traffic) of the timed launches */
 } nk_prof_entry;
-int nk_prof_enable(nk_ctx* ctx, int32_t on);
+/* every = 0: off; every = k > 0: time every k-th launch of each kernel class with a pair of HIP
+ * events on the context stream (k > 1 keeps the event overhead out of the timed region). */
+int nk_prof_enable(nk_ctx* ctx, int32_t every);
 int nk_prof_reset(nk_ctx* ctx);
 int nk_prof_read(nk_ctx* ctx, nk_prof_entry* out, int32_t cap, int32_t* count);
 

@@ -59,8 +59,9 @@ class Context:
         self.rank, self.nranks = rank, nranks
 
     # -- profiling ---------------------------------------------------------------------------
-    def prof_enable(self, on: bool = True):
-        self.check(load().nk_prof_enable(self.handle, int(on)), "nk_prof_enable")
+    def prof_enable(self, every: int = 1):
+        """Time every `every`-th launch of each kernel class with HIP events (0 = off)."""
+        self.check(load().nk_prof_enable(self.handle, int(every)), "nk_prof_enable")
 
     def prof_reset(self):
         self.check(load().nk_prof_reset(self.handle), "nk_prof_reset")
@@ -70,7 +71,8 @@ class Context:
         buf = (_lib.nk_prof_entry * cap)()
         cnt = C.c_int32(0)
         self.check(load().nk_prof_read(self.handle, buf, cap, C.byref(cnt)), "nk_prof_read")
-        return {buf[i].name.decode(): dict(launches=buf[i].launches, ms=buf[i].total_ms, bytes=buf[i].bytes)
+        return {buf[i].name.decode(): dict(launches=buf[i].launches, timed=buf[i].timed, ms=buf[i].total_ms,
+                                           bytes=buf[i].bytes)
                 for i in range(min(cnt.value, cap))}
 
 

@@ -106,7 +106,7 @@ void prof_drain(nk_ctx* c, bool blocking) {
         }
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, p.a, p.b);
-        c->acc[p.kid].launches += 1;
+        c->acc[p.kid].timed += 1;
         c->acc[p.kid].ms += ms;
         c->acc[p.kid].bytes += p.bytes;
         c->ev_pool.push_back(p.a);
@@ -305,10 +305,11 @@ int nk_divcopy(nk_ctx* c, int64_t n, double* y, const double* x, double s) { ret
 int nk_ref(nk_ctx* c, int64_t n, double* x, double* y, double cc, double ss) { return c ? launch_ref(c, n, x, y, cc, ss) : NK_E_ARG; }
 
 // ---------------------------------------------------------------- profiling
-int nk_prof_enable(nk_ctx* c, int32_t on) {
-    if (!c) return NK_E_ARG;
-    if (!on && c->prof) prof_drain(c, true);
-    c->prof = on != 0;
+int nk_prof_enable(nk_ctx* c, int32_t every) {
+    if (!c || every < 0) return NK_E_ARG;
+    if (!every && c->prof) prof_drain(c, true);
+    c->prof = every != 0;
+    c->prof_every = every > 0 ? every : 1;
     return NK_OK;
 }
 
@@ -329,6 +330,7 @@ int nk_prof_read(nk_ctx* c, nk_prof_entry* out, int32_t cap, int32_t* count) {
             std::memset(out[m].name, 0, NK_PROF_NAME);
             std::strncpy(out[m].name, c->kid_names[k].c_str(), NK_PROF_NAME - 1);
             out[m].launches = c->acc[k].launches;
+            out[m].timed = c->acc[k].timed;
             out[m].total_ms = c->acc[k].ms;
             out[m].bytes = c->acc[k].bytes;
         }

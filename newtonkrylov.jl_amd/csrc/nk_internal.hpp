@@ -21,6 +21,8 @@ constexpr int kRedSlots = 4;         // ring of partial-sum slots
 constexpr int kRedCap = 16384;       // doubles per slot (a stencil launch may have more blocks)
 constexpr int kScalCap = 8192;       // device scalar area (Hessenberg column, y, norms)
 constexpr int kMaxUpdateVecs = 32;   // basis vectors folded per x-update launch
+constexpr int kMgsUnroll = 2;        // independent 16-B loads per stream in flight per thread (MGS pass)
+constexpr bool kMgsNT = false;       // non-temporal loads of V_i in the MGS pass
 
 enum Mode { MODE_RES = 0, MODE_JEXACT = 1, MODE_JFD = 2 };
 enum Epi { EPI_NONE = 0, EPI_SUMSQ = 1, EPI_DOT = 2, EPI_RESID = 3 };
@@ -31,7 +33,7 @@ struct ProfPending {
     double bytes;
 };
 struct ProfAcc {
-    int64_t launches = 0;
+    int64_t launches = 0, timed = 0;
     double ms = 0.0, bytes = 0.0;
 };
 
@@ -50,6 +52,7 @@ struct nk_ctx {
     int red_next = 0;
     // profiling
     bool prof = false;
+    int prof_every = 1;
     std::vector<nk::ProfPending> pending;
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::string> kid_names;
@@ -96,11 +99,17 @@ void prof_drain(nk_ctx* c, bool blocking);
 template <typename F>
 int launch(nk_ctx* c, const char* name, double bytes, F&& f) {
     hipEvent_t a = nullptr;
-    if (c->prof) NK_TRY(prof_begin(c, &a));
+    int k = -1;
+    bool timed = false;
+    if (c->prof) {
+        k = kid(c, name);
+        timed = (c->acc[k].launches++ % c->prof_every) == 0;
+        if (timed) NK_TRY(prof_begin(c, &a));
+    }
     f();
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(c, NK_E_HIP, std::string("launch ") + name + ": " + hipGetErrorString(e));
-    if (c->prof) NK_TRY(prof_end(c, kid(c, name), a, bytes));
+    if (timed) NK_TRY(prof_end(c, k, a, bytes));
     return NK_OK;
 }
 

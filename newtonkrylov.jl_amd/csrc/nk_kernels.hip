@@ -162,6 +162,66 @@ __global__ __launch_bounds__(kBlock) void k_st1d(KArgs A) {
     }
 }
 
+// ------------------------------------------------------------------------------ row fragments
+// VEC consecutive x-points of one row, held by value (no address taken -> stays in VGPRs).
+template <int VEC>
+struct Row {
+    double v[VEC];
+};
+
+template <int MODE, int VEC>
+__device__ __forceinline__ Row<VEC> field_row(const KArgs& A, int64_t o, bool ok) {
+    Row<VEC> r;
+    if (ok) {
+        if constexpr (VEC == 2) {
+            if constexpr (MODE == MODE_RES) {
+                const double2 q = *reinterpret_cast<const double2*>(A.u + o);
+                r.v[0] = q.x; r.v[1] = q.y;
+            } else if constexpr (MODE == MODE_JEXACT) {
+                const double2 q = *reinterpret_cast<const double2*>(A.v + o);
+                r.v[0] = q.x; r.v[1] = q.y;
+            } else {
+                const double2 qu = *reinterpret_cast<const double2*>(A.u + o);
+                const double2 qv = *reinterpret_cast<const double2*>(A.v + o);
+                r.v[0] = qu.x + A.eps * qv.x;  // w = u + eps v
+                r.v[1] = qu.y + A.eps * qv.y;
+            }
+        } else {
+            r.v[0] = fieldval<MODE>(A, o);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) r.v[k] = 0.0;
+    }
+    return r;
+}
+
+template <int VEC>
+__device__ __forceinline__ Row<VEC> data_row(const double* __restrict__ p, int64_t o, bool ok) {
+    Row<VEC> r;
+    if (ok) {
+        if constexpr (VEC == 2) {
+            const double2 q = *reinterpret_cast<const double2*>(p + o);
+            r.v[0] = q.x; r.v[1] = q.y;
+        } else {
+            r.v[0] = p[o];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) r.v[k] = 0.0;
+    }
+    return r;
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_row(double* __restrict__ p, int64_t o, const Row<VEC>& r) {
+    if constexpr (VEC == 2) {
+        *reinterpret_cast<double2*>(p + o) = make_double2(r.v[0], r.v[1]);
+    } else {
+        p[o] = r.v[0];
+    }
+}
+
 // ------------------------------------------------------------------------------ 2D stencil
 // Block = 256 threads x VEC columns (one row segment), marching A.rows rows in y.
 template <int KIND, int MODE, int EPI, int VEC>
@@ -174,67 +234,53 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A) {
     const int64_t nx = A.nx, ny = A.ny;
     const int64_t x0 = (int64_t)tx * (kBlock * VEC) + (int64_t)threadIdx.x * VEC;
     const bool act = x0 < nx;
+    const bool left_lane = lane == 0 && x0 >= 1 && x0 - 1 < nx;  // wave-edge lanes load their outer column
+    const bool right_lane = lane == 63 && x0 + VEC < nx;
     const int64_t y0 = (int64_t)ty * A.rows;
     const int64_t y1 = y0 + A.rows < ny ? y0 + A.rows : ny;
-
-    double fm[VEC], fc[VEC], fp[VEC];
-    double elc = 0.0, erc = 0.0, elp = 0.0, erp = 0.0;
     double acc = 0.0;
-
-    auto load_row = [&](int64_t j, double* f) {
-        if (act) {
-            fieldvec<MODE, VEC>(A, j * nx + x0, f);
-        } else {
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) f[k] = 0.0;
-        }
-    };
-    auto load_edges = [&](int64_t j, double& el, double& er) {
-        if (lane == 0 && x0 - 1 >= 0 && x0 - 1 < nx) el = fieldval<MODE>(A, j * nx + x0 - 1);
-        if (lane == 63 && x0 + VEC < nx) er = fieldval<MODE>(A, j * nx + x0 + VEC);
-    };
-
     if (y0 < ny) {
-        load_row(y0 - 1, fm);  // row -1 is the ghost plane (zero, or the lower neighbour's row)
-        load_row(y0, fc);
-        load_edges(y0, elc, erc);
+        // row -1 / row ny are the ghost planes (zero, or the neighbouring slab's boundary row)
+        Row<VEC> fm = field_row<MODE, VEC>(A, (y0 - 1) * nx + x0, act);
+        Row<VEC> fc = field_row<MODE, VEC>(A, y0 * nx + x0, act);
+        double elc = left_lane ? fieldval<MODE>(A, y0 * nx + x0 - 1) : 0.0;
+        double erc = right_lane ? fieldval<MODE>(A, y0 * nx + x0 + VEC) : 0.0;
         for (int64_t j = y0; j < y1; ++j) {
-            load_row(j + 1, fp);  // row ny is the upper ghost plane
-            elp = 0.0; erp = 0.0;
-            if (j + 1 < ny) load_edges(j + 1, elp, erp);
-            double uc[VEC], unc[VEC], f0c[VEC], ax[VEC];
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) uc[k] = unc[k] = f0c[k] = ax[k] = 0.0;
             const int64_t o = j * nx + x0;
-            if (act) {
-                if (MODE == MODE_JEXACT && KIND == NK_BRATU2D) loadvec<VEC>(A.u, o, uc);
-                if (KIND == NK_HEAT2D_EULER && MODE != MODE_JEXACT) loadvec<VEC>(A.un, o, unc);
-                if (MODE == MODE_JFD) loadvec<VEC>(A.F0, o, f0c);
-                if (EPI == EPI_DOT || EPI == EPI_RESID) loadvec<VEC>(A.aux, o, ax);
-            }
-            double lft = __shfl_up(fc[VEC - 1], 1, 64);
-            double rgt = __shfl_down(fc[0], 1, 64);
+            const Row<VEC> fp = field_row<MODE, VEC>(A, o + nx, act);
+            const bool nxt = j + 1 < ny;
+            const double elp = (left_lane && nxt) ? fieldval<MODE>(A, o + nx - 1) : 0.0;
+            const double erp = (right_lane && nxt) ? fieldval<MODE>(A, o + nx + VEC) : 0.0;
+            Row<VEC> uc{}, unc{}, f0c{}, ax{};
+            if constexpr (MODE == MODE_JEXACT && KIND == NK_BRATU2D) uc = data_row<VEC>(A.u, o, act);
+            if constexpr (KIND == NK_HEAT2D_EULER && MODE != MODE_JEXACT) unc = data_row<VEC>(A.un, o, act);
+            if constexpr (MODE == MODE_JFD) f0c = data_row<VEC>(A.F0, o, act);
+            if constexpr (EPI == EPI_DOT || EPI == EPI_RESID) ax = data_row<VEC>(A.aux, o, act);
+            double lft = __shfl_up(fc.v[VEC - 1], 1, 64);
+            double rgt = __shfl_down(fc.v[0], 1, 64);
             if (lane == 0) lft = elc;
             if (lane == 63) rgt = erc;
             if (act) {
-                double val[VEC];
+                Row<VEC> val;
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) {
-                    const double w = (k == 0) ? lft : fc[k - 1];
-                    const double e = (k == VEC - 1) ? rgt : fc[k + 1];
-                    const double c = fc[k];
-                    const double lsum = lap(c, e, w, A.hx2) + lap(c, fp[k], fm[k], A.hy2);
-                    val[k] = point_value<KIND, MODE>(A, c, lsum, uc[k], unc[k], f0c[k]);
-                    acc = epilogue<EPI>(val[k], ax[k], acc);
+                    const double w = (k == 0) ? lft : fc.v[k == 0 ? 0 : k - 1];
+                    const double e = (k == VEC - 1) ? rgt : fc.v[k == VEC - 1 ? k : k + 1];
+                    const double c = fc.v[k];
+                    const double lsum = lap(c, e, w, A.hx2) + lap(c, fp.v[k], fm.v[k], A.hy2);
+                    double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unc.v[k], f0c.v[k]);
+                    acc = epilogue<EPI>(r, ax.v[k], acc);
+                    val.v[k] = r;
                 }
-                storevec<VEC>(A.out, o, val);
+                store_row<VEC>(A.out, o, val);
             }
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) { fm[k] = fc[k]; fc[k] = fp[k]; }
-            elc = elp; erc = erp;
+            fm = fc;
+            fc = fp;
+            elc = elp;
+            erc = erp;
         }
     }
-    if (EPI != EPI_NONE) {
+    if constexpr (EPI != EPI_NONE) {
         const double s = block_sum(acc, sh);
         if (threadIdx.x == 0) A.part[blockIdx.x] = s;
     }
@@ -256,69 +302,55 @@ __global__ __launch_bounds__(kBlock) void k_st3d(KArgs A) {
     const int64_t x0 = (int64_t)tx * (64 * VEC) + (int64_t)lane * VEC;
     const int64_t j = (int64_t)ty * 4 + wv;
     const bool act = x0 < nx && j < ny;
+    const bool has_n = act && j + 1 < ny, has_s = act && j >= 1;
+    const bool left_lane = lane == 0 && j < ny && x0 >= 1 && x0 - 1 < nx;
+    const bool right_lane = lane == 63 && j < ny && x0 + VEC < nx;
     const int64_t z0 = (int64_t)tz * A.rows;
     const int64_t z1 = z0 + A.rows < nz ? z0 + A.rows : nz;
-
-    double fm[VEC], fc[VEC], fp[VEC];
-    double elc = 0.0, erc = 0.0, elp = 0.0, erp = 0.0;
     double acc = 0.0;
-    auto load_row = [&](int64_t k, int64_t jj, double* f) {
-        if (x0 < nx && jj >= 0 && jj < ny) {
-            fieldvec<MODE, VEC>(A, k * pl + jj * nx + x0, f);
-        } else {
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) f[q] = 0.0;
-        }
-    };
-    auto load_edges = [&](int64_t k, double& el, double& er) {
-        if (j < ny) {
-            if (lane == 0 && x0 - 1 >= 0 && x0 - 1 < nx) el = fieldval<MODE>(A, k * pl + j * nx + x0 - 1);
-            if (lane == 63 && x0 + VEC < nx) er = fieldval<MODE>(A, k * pl + j * nx + x0 + VEC);
-        }
-    };
     if (z0 < nz) {
-        load_row(z0 - 1, j, fm);  // plane -1: ghost plane
-        load_row(z0, j, fc);
-        load_edges(z0, elc, erc);
+        const int64_t oj = j * nx + x0;
+        Row<VEC> fm = field_row<MODE, VEC>(A, (z0 - 1) * pl + oj, act);  // plane -1: ghost plane
+        Row<VEC> fc = field_row<MODE, VEC>(A, z0 * pl + oj, act);
+        double elc = left_lane ? fieldval<MODE>(A, z0 * pl + oj - 1) : 0.0;
+        double erc = right_lane ? fieldval<MODE>(A, z0 * pl + oj + VEC) : 0.0;
         for (int64_t k = z0; k < z1; ++k) {
-            load_row(k + 1, j, fp);  // plane nz: ghost plane
-            elp = 0.0; erp = 0.0;
-            if (k + 1 < nz) load_edges(k + 1, elp, erp);
-            double fn[VEC], fs[VEC];
-            load_row(k, j + 1, fn);
-            load_row(k, j - 1, fs);
-            double unc[VEC], f0c[VEC], ax[VEC];
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) unc[q] = f0c[q] = ax[q] = 0.0;
-            const int64_t o = k * pl + j * nx + x0;
-            if (act) {
-                if (MODE != MODE_JEXACT) loadvec<VEC>(A.un, o, unc);
-                if (MODE == MODE_JFD) loadvec<VEC>(A.F0, o, f0c);
-                if (EPI == EPI_DOT || EPI == EPI_RESID) loadvec<VEC>(A.aux, o, ax);
-            }
-            double lft = __shfl_up(fc[VEC - 1], 1, 64);
-            double rgt = __shfl_down(fc[0], 1, 64);
+            const int64_t o = k * pl + oj;
+            const Row<VEC> fp = field_row<MODE, VEC>(A, o + pl, act);  // plane nz: ghost plane
+            const bool nxt = k + 1 < nz;
+            const double elp = (left_lane && nxt) ? fieldval<MODE>(A, o + pl - 1) : 0.0;
+            const double erp = (right_lane && nxt) ? fieldval<MODE>(A, o + pl + VEC) : 0.0;
+            const Row<VEC> fn = field_row<MODE, VEC>(A, o + nx, has_n);
+            const Row<VEC> fs = field_row<MODE, VEC>(A, o - nx, has_s);
+            Row<VEC> unc{}, f0c{}, ax{};
+            if constexpr (MODE != MODE_JEXACT) unc = data_row<VEC>(A.un, o, act);
+            if constexpr (MODE == MODE_JFD) f0c = data_row<VEC>(A.F0, o, act);
+            if constexpr (EPI == EPI_DOT || EPI == EPI_RESID) ax = data_row<VEC>(A.aux, o, act);
+            double lft = __shfl_up(fc.v[VEC - 1], 1, 64);
+            double rgt = __shfl_down(fc.v[0], 1, 64);
             if (lane == 0) lft = elc;
             if (lane == 63) rgt = erc;
             if (act) {
-                double val[VEC];
+                Row<VEC> val;
 #pragma unroll
                 for (int q = 0; q < VEC; ++q) {
-                    const double w = (q == 0) ? lft : fc[q - 1];
-                    const double e = (q == VEC - 1) ? rgt : fc[q + 1];
-                    const double c = fc[q];
-                    const double lsum = (lap(c, e, w, A.hx2) + lap(c, fn[q], fs[q], A.hy2)) + lap(c, fp[q], fm[q], A.hz2);
-                    val[q] = point_value<KIND, MODE>(A, c, lsum, 0.0, unc[q], f0c[q]);
-                    acc = epilogue<EPI>(val[q], ax[q], acc);
+                    const double w = (q == 0) ? lft : fc.v[q == 0 ? 0 : q - 1];
+                    const double e = (q == VEC - 1) ? rgt : fc.v[q == VEC - 1 ? q : q + 1];
+                    const double c = fc.v[q];
+                    const double lsum = (lap(c, e, w, A.hx2) + lap(c, fn.v[q], fs.v[q], A.hy2)) + lap(c, fp.v[q], fm.v[q], A.hz2);
+                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unc.v[q], f0c.v[q]);
+                    acc = epilogue<EPI>(r, ax.v[q], acc);
+                    val.v[q] = r;
                 }
-                storevec<VEC>(A.out, o, val);
+                store_row<VEC>(A.out, o, val);
             }
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) { fm[q] = fc[q]; fc[q] = fp[q]; }
-            elc = elp; erc = erp;
+            fm = fc;
+            fc = fp;
+            elc = elp;
+            erc = erp;
         }
     }
-    if (EPI != EPI_NONE) {
+    if constexpr (EPI != EPI_NONE) {
         const double s = block_sum(acc, sh);
         if (threadIdx.x == 0) A.part[blockIdx.x] = s;
     }
@@ -449,7 +481,22 @@ __global__ __launch_bounds__(kBlock) void k_ref(int64_t n, double* __restrict__ 
 //   q = q - h V_i  (kaxpy!(n, -h, V_i, q) == fma(-h, V_i, q))
 //   partials of <V_{i+1}, q>  (or <q, q> on the last pass: h_{k+1,k} = ||q||)
 // 32 B/point (24 on the last pass) instead of the 40 B of separate kdot + kaxpy!.
-template <bool HAS_NEXT>
+// U independent 16-B loads per stream are issued before any use (memory-level parallelism);
+// NT marks the loads/stores non-temporal (streams that are not re-read soon).
+typedef double dx2 __attribute__((ext_vector_type(2)));
+
+template <bool NT>
+__device__ __forceinline__ dx2 ld2(const dx2* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st2(dx2* p, dx2 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <bool HAS_NEXT, int U, bool NT>
 __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restrict__ q, const double* __restrict__ vi,
                                                     const double* __restrict__ vnext, const double* __restrict__ red_in,
                                                     int red_len, double* __restrict__ h_out, double* __restrict__ part) {
@@ -457,18 +504,43 @@ __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restri
     const double h = reduce_input(red_in, red_len, sh);
     if (blockIdx.x == 0 && threadIdx.x == 0) *h_out = h;
     const double mh = -h;
-    double2* q2 = reinterpret_cast<double2*>(q);
-    const double2* v2 = reinterpret_cast<const double2*>(vi);
-    const double2* w2 = reinterpret_cast<const double2*>(vnext);
+    dx2* q2 = reinterpret_cast<dx2*>(q);
+    const dx2* v2 = reinterpret_cast<const dx2*>(vi);
+    const dx2* w2 = reinterpret_cast<const dx2*>(vnext);
+    const int64_t n2 = n >> 1;
+    const int64_t st = (int64_t)gridDim.x * kBlock;
     double acc = 0.0;
-    NK_GRID_STRIDE2(i) {
-        double2 a = q2[i];
-        const double2 b = v2[i];
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (; i + (U - 1) * st < n2; i += U * st) {
+        dx2 a[U], bv[U], cv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            a[u] = ld2<false>(q2 + i + u * st);
+            bv[u] = ld2<NT>(v2 + i + u * st);
+            if constexpr (HAS_NEXT) cv[u] = ld2<false>(w2 + i + u * st);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            a[u].x = fma(mh, bv[u].x, a[u].x);
+            a[u].y = fma(mh, bv[u].y, a[u].y);
+            st2<false>(q2 + i + u * st, a[u]);
+            if constexpr (HAS_NEXT) {
+                acc = fma(cv[u].x, a[u].x, acc);
+                acc = fma(cv[u].y, a[u].y, acc);
+            } else {
+                acc = fma(a[u].x, a[u].x, acc);
+                acc = fma(a[u].y, a[u].y, acc);
+            }
+        }
+    }
+    for (; i < n2; i += st) {
+        dx2 a = q2[i];
+        const dx2 b = v2[i];
         a.x = fma(mh, b.x, a.x);
         a.y = fma(mh, b.y, a.y);
         q2[i] = a;
-        if (HAS_NEXT) {
-            const double2 c = w2[i];
+        if constexpr (HAS_NEXT) {
+            const dx2 c = w2[i];
             acc = fma(c.x, a.x, acc);
             acc = fma(c.y, a.y, acc);
         } else {
@@ -548,38 +620,34 @@ __global__ __launch_bounds__(kBlock) void k_cg_direction(int64_t n, double beta,
 
 // ------------------------------------------------------------------------------ stencil dispatch
 template <int KIND, int MODE, int EPI>
-void go_stencil(const KArgs& A, int dim, int vec, int grid, hipStream_t s) {
-    if (dim == 1) {
-        if (KIND == NK_BRATU1D) hipLaunchKernelGGL((k_st1d<MODE, EPI>), dim3(grid), dim3(kBlock), 0, s, A);
-    } else if (dim == 2) {
-        if (KIND == NK_BRATU2D || KIND == NK_HEAT2D_EULER) {
-            if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
-            else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1>), dim3(grid), dim3(kBlock), 0, s, A);
-        }
+void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s) {
+    if constexpr (KIND == NK_BRATU1D) {
+        hipLaunchKernelGGL((k_st1d<MODE, EPI>), dim3(grid), dim3(kBlock), 0, s, A);
+    } else if constexpr (KIND == NK_BRATU2D || KIND == NK_HEAT2D_EULER) {
+        if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
+        else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1>), dim3(grid), dim3(kBlock), 0, s, A);
     } else {
-        if (KIND == NK_HEAT3D_EULER) {
-            if (vec == 2) hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
-            else hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 1>), dim3(grid), dim3(kBlock), 0, s, A);
-        }
+        if (vec == 2) hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
+        else hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 1>), dim3(grid), dim3(kBlock), 0, s, A);
     }
 }
 
 template <int KIND, int MODE>
-void go_stencil_epi(const KArgs& A, int epi, int dim, int vec, int grid, hipStream_t s) {
+void go_stencil_epi(const KArgs& A, int epi, int vec, int grid, hipStream_t s) {
     switch (epi) {
-    case EPI_NONE: go_stencil<KIND, MODE, EPI_NONE>(A, dim, vec, grid, s); break;
-    case EPI_SUMSQ: go_stencil<KIND, MODE, EPI_SUMSQ>(A, dim, vec, grid, s); break;
-    case EPI_DOT: go_stencil<KIND, MODE, EPI_DOT>(A, dim, vec, grid, s); break;
-    default: go_stencil<KIND, MODE, EPI_RESID>(A, dim, vec, grid, s); break;
+    case EPI_NONE: go_stencil<KIND, MODE, EPI_NONE>(A, vec, grid, s); break;
+    case EPI_SUMSQ: go_stencil<KIND, MODE, EPI_SUMSQ>(A, vec, grid, s); break;
+    case EPI_DOT: go_stencil<KIND, MODE, EPI_DOT>(A, vec, grid, s); break;
+    default: go_stencil<KIND, MODE, EPI_RESID>(A, vec, grid, s); break;
     }
 }
 
 template <int KIND>
-void go_stencil_mode(const KArgs& A, int mode, int epi, int dim, int vec, int grid, hipStream_t s) {
+void go_stencil_mode(const KArgs& A, int mode, int epi, int vec, int grid, hipStream_t s) {
     switch (mode) {
-    case MODE_RES: go_stencil_epi<KIND, MODE_RES>(A, epi, dim, vec, grid, s); break;
-    case MODE_JEXACT: go_stencil_epi<KIND, MODE_JEXACT>(A, epi, dim, vec, grid, s); break;
-    default: go_stencil_epi<KIND, MODE_JFD>(A, epi, dim, vec, grid, s); break;
+    case MODE_RES: go_stencil_epi<KIND, MODE_RES>(A, epi, vec, grid, s); break;
+    case MODE_JEXACT: go_stencil_epi<KIND, MODE_JEXACT>(A, epi, vec, grid, s); break;
+    default: go_stencil_epi<KIND, MODE_JFD>(A, epi, vec, grid, s); break;
     }
 }
 
@@ -651,14 +719,14 @@ int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red) {
         {"residual", "residual_norm", "residual_dot", "residual_resid"},
         {"jv_exact", "jv_exact_sumsq", "jv_exact_dot", "jv_exact_resid"},
         {"jv_fd", "jv_fd_sumsq", "jv_fd_dot", "jv_fd_resid"}};
-    const int kind = p->kind, dim = g.dim, mode = in.mode, epi = in.epi;
+    const int kind = p->kind, mode = in.mode, epi = in.epi;
     hipStream_t s = c->stream;
     return launch(c, names[mode][epi], bytes, [&] {
         switch (kind) {
-        case NK_BRATU1D: go_stencil_mode<NK_BRATU1D>(A, mode, epi, dim, vec, grid, s); break;
-        case NK_BRATU2D: go_stencil_mode<NK_BRATU2D>(A, mode, epi, dim, vec, grid, s); break;
-        case NK_HEAT2D_EULER: go_stencil_mode<NK_HEAT2D_EULER>(A, mode, epi, dim, vec, grid, s); break;
-        default: go_stencil_mode<NK_HEAT3D_EULER>(A, mode, epi, dim, vec, grid, s); break;
+        case NK_BRATU1D: go_stencil_mode<NK_BRATU1D>(A, mode, epi, vec, grid, s); break;
+        case NK_BRATU2D: go_stencil_mode<NK_BRATU2D>(A, mode, epi, vec, grid, s); break;
+        case NK_HEAT2D_EULER: go_stencil_mode<NK_HEAT2D_EULER>(A, mode, epi, vec, grid, s); break;
+        default: go_stencil_mode<NK_HEAT3D_EULER>(A, mode, epi, vec, grid, s); break;
         }
     });
 }
@@ -707,10 +775,12 @@ int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const dou
     out->len = g;
     if (vnext)
         return launch(c, "mgs_pass", 32.0 * n, [&] {
-            hipLaunchKernelGGL(k_mgs_pass<true>, dim3(g), dim3(kBlock), 0, c->stream, n, q, vi, vnext, in.ptr, in.len, h_out, part);
+            hipLaunchKernelGGL((k_mgs_pass<true, kMgsUnroll, kMgsNT>), dim3(g), dim3(kBlock), 0, c->stream, n, q, vi, vnext,
+                               in.ptr, in.len, h_out, part);
         });
     return launch(c, "mgs_pass_last", 24.0 * n, [&] {
-        hipLaunchKernelGGL(k_mgs_pass<false>, dim3(g), dim3(kBlock), 0, c->stream, n, q, vi, vnext, in.ptr, in.len, h_out, part);
+        hipLaunchKernelGGL((k_mgs_pass<false, kMgsUnroll, kMgsNT>), dim3(g), dim3(kBlock), 0, c->stream, n, q, vi, vnext,
+                           in.ptr, in.len, h_out, part);
     });
 }
 
@@ -761,4 +831,84 @@ int launch_cg_direction(nk_ctx* c, int64_t n, double beta, double* p, const doub
     NK_STREAM_LAUNCH("cg_direction", 24.0, k_cg_direction, n, beta, p, r);
 }
 
+// ------------------------------------------------------------------------------ variant bench hook
+// Times kernel variants in ONE process (interleaved A/B, MI355X_MICROARCH methodology rule 24).
+// Not part of the public ABI (exported as nkb_*; used by tools/kbench.py only).
+namespace {
+template <bool HAS_NEXT, int U, bool NT>
+void mgs_variant(nk_ctx* c, int g, int64_t n, double* q, const double* vi, const double* vn, const double* red,
+                 double* h, double* part) {
+    hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, U, NT>), dim3(g), dim3(kBlock), 0, c->stream, n, q, vi, vn, red, 1, h, part);
+}
+}  // namespace
+
 }  // namespace nk
+
+extern "C" int nkb_mgs(nk_ctx* c, int64_t n, int variant, int grid, int reps, double* us_out) {
+    using namespace nk;
+    if (!c || n < 2 || reps < 1 || !us_out) return NK_E_ARG;
+    double *q = nullptr, *v = nullptr, *w = nullptr;
+    NK_HIP(c, hipMalloc(&q, sizeof(double) * n));
+    NK_HIP(c, hipMalloc(&v, sizeof(double) * n));
+    NK_HIP(c, hipMalloc(&w, sizeof(double) * n));
+    NK_HIP(c, hipMemsetAsync(q, 0, sizeof(double) * n, c->stream));
+    NK_HIP(c, hipMemsetAsync(v, 0, sizeof(double) * n, c->stream));
+    NK_HIP(c, hipMemsetAsync(w, 0, sizeof(double) * n, c->stream));
+    const int g = grid > 0 ? grid : red_blocks(n);
+    double* part = red_slot(c);
+    double* red = c->scal;
+    hipEvent_t a, b;
+    NK_HIP(c, hipEventCreate(&a));
+    NK_HIP(c, hipEventCreate(&b));
+    auto run = [&] {
+        switch (variant) {
+        case 0: mgs_variant<true, 1, false>(c, g, n, q, v, w, red, red + 1, part); break;
+        case 1: mgs_variant<true, 2, false>(c, g, n, q, v, w, red, red + 1, part); break;
+        case 2: mgs_variant<true, 4, false>(c, g, n, q, v, w, red, red + 1, part); break;
+        case 3: mgs_variant<true, 2, true>(c, g, n, q, v, w, red, red + 1, part); break;
+        case 4: mgs_variant<true, 4, true>(c, g, n, q, v, w, red, red + 1, part); break;
+        case 5: mgs_variant<false, 2, false>(c, g, n, q, v, w, red, red + 1, part); break;
+        default: mgs_variant<true, 8, false>(c, g, n, q, v, w, red, red + 1, part); break;
+        }
+    };
+    run();
+    NK_HIP(c, hipEventRecord(a, c->stream));
+    for (int r = 0; r < reps; ++r) run();
+    NK_HIP(c, hipEventRecord(b, c->stream));
+    NK_HIP(c, hipEventSynchronize(b));
+    float ms = 0.f;
+    NK_HIP(c, hipEventElapsedTime(&ms, a, b));
+    *us_out = 1e3 * ms / reps;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    (void)hipFree(q);
+    (void)hipFree(v);
+    (void)hipFree(w);
+    return NK_OK;
+}
+
+// plain streaming copy (y = x, 16 B per lane) as the achievable-bandwidth calibration point
+extern "C" int nkb_copy(nk_ctx* c, int64_t n, int reps, double* us_out) {
+    using namespace nk;
+    if (!c || n < 2 || reps < 1 || !us_out) return NK_E_ARG;
+    double *x = nullptr, *y = nullptr;
+    NK_HIP(c, hipMalloc(&x, sizeof(double) * n));
+    NK_HIP(c, hipMalloc(&y, sizeof(double) * n));
+    NK_HIP(c, hipMemsetAsync(x, 0, sizeof(double) * n, c->stream));
+    hipEvent_t a, b;
+    NK_HIP(c, hipEventCreate(&a));
+    NK_HIP(c, hipEventCreate(&b));
+    NK_TRY(launch_copy(c, n, y, x));
+    NK_HIP(c, hipEventRecord(a, c->stream));
+    for (int r = 0; r < reps; ++r) NK_TRY(launch_copy(c, n, y, x));
+    NK_HIP(c, hipEventRecord(b, c->stream));
+    NK_HIP(c, hipEventSynchronize(b));
+    float ms = 0.f;
+    NK_HIP(c, hipEventElapsedTime(&ms, a, b));
+    *us_out = 1e3 * ms / reps;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    (void)hipFree(x);
+    (void)hipFree(y);
+    return NK_OK;
+}
