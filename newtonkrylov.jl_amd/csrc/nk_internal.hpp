@@ -21,8 +21,7 @@ constexpr int kRedSlots = 4;         // ring of partial-sum slots
 constexpr int kRedCap = 16384;       // doubles per slot (a stencil launch may have more blocks)
 constexpr int kScalCap = 8192;       // device scalar area (Hessenberg column, y, norms)
 constexpr int kMaxUpdateVecs = 32;   // basis vectors folded per x-update launch
-constexpr int kMgsUnroll = 2;        // independent 16-B loads per stream in flight per thread (MGS pass)
-constexpr bool kMgsNT = false;       // non-temporal loads of V_i in the MGS pass
+constexpr int kMgsVariant = 1;       // MGS-pass variant (unroll x non-temporal V_i), see mgs_dispatch
 
 enum Mode { MODE_RES = 0, MODE_JEXACT = 1, MODE_JFD = 2 };
 enum Epi { EPI_NONE = 0, EPI_SUMSQ = 1, EPI_DOT = 2, EPI_RESID = 3 };
@@ -153,7 +152,7 @@ int launch_ref(nk_ctx* c, int64_t n, double* x, double* y, double cc, double ss)
 // one fused modified-Gram-Schmidt pass: h = Σ in; q -= h vi; partials of <vnext, q> (or <q,q>
 // when vnext == nullptr).  Block 0 stores h at h_out.
 int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const double* vnext, Red in,
-                    double* h_out, Red* out);
+                    double* h_out, Red* out, int rev);
 // xr = Σ_i y_i V_i (fma chain from 0 in i order, y on device); then x = x + xr (restart) or
 // x = xr; optional partial sums of ||x||^2.
 int launch_update_x(nk_ctx* c, int64_t n, double* x, double* xr, const double* const* V, int k,

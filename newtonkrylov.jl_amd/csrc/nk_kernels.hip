@@ -41,14 +41,21 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
     return r;
 }
 
-// fixed-order sum of in[0..len), broadcast to the whole block
+// fixed-order sum of in[0..len), broadcast to the whole block.  All 256 threads load (8
+// independent loads in flight each), so a block pays ~one L2 round trip, not 32 dependent ones.
 __device__ __forceinline__ double reduce_input(const double* __restrict__ in, int len, double* sh) {
-    if (threadIdx.x < 64) {
-        double t = 0.0;
-        for (int m = threadIdx.x; m < len; m += 64) t += in[m];
-        t = wave_sum(t);
-        if (threadIdx.x == 0) sh[4] = t;
+    double t = 0.0;
+    int m = threadIdx.x;
+    for (; m + 7 * kBlock < len; m += 8 * kBlock) {
+        double a[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) a[r] = in[m + r * kBlock];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) t += a[r];
     }
+    for (; m < len; m += kBlock) t += in[m];
+    t = block_sum(t, sh);
+    if (threadIdx.x == 0) sh[4] = t;
     __syncthreads();
     return sh[4];
 }
@@ -66,7 +73,15 @@ struct KArgs {
     int64_t nx, ny, nz;
     double hx2, hy2, hz2, lam, a, dt, eps;
     int tiles_x, tiles_y, rows;
+    int fast;            // 1: multiply by reciprocals instead of dividing (measurement variant, not bit-faithful)
+    double ihx2, ihy2, ihz2, ieps;
 };
+
+// ((p - 2c) + m) / h^2 exactly as the reference writes it; `fast` multiplies by 1/h^2 instead
+__device__ __forceinline__ double lapk(const KArgs& A, double c, double p, double m, double h2, double ih2) {
+    const double s = (p - 2.0 * c) + m;
+    return (A.fast & 1) ? s * ih2 : s / h2;
+}
 
 template <int MODE>
 __device__ __forceinline__ double fieldval(const KArgs& A, int64_t o) {
@@ -121,11 +136,11 @@ __device__ __forceinline__ double point_value(const KArgs& A, double c, double l
     if (KIND == NK_BRATU1D || KIND == NK_BRATU2D) {
         if (MODE == MODE_JEXACT) return lsum + A.lam * (exp(uc) * c);  // Enzyme tangent of λ exp(u)
         const double r = lsum + A.lam * exp(c);
-        return MODE == MODE_JFD ? (r - f0c) / A.eps : r;
+        return MODE == MODE_JFD ? ((A.fast & 1) ? (r - f0c) * A.ieps : (r - f0c) / A.eps) : r;
     } else {  // implicit Euler: res = (u_n + dt f(u)) - u  (implicit.jl:8-13)
         if (MODE == MODE_JEXACT) return A.dt * (A.a * lsum) - c;
         const double r = (unc + A.dt * (A.a * lsum)) - c;
-        return MODE == MODE_JFD ? (r - f0c) / A.eps : r;
+        return MODE == MODE_JFD ? ((A.fast & 1) ? (r - f0c) * A.ieps : (r - f0c) / A.eps) : r;
     }
 }
 
@@ -173,18 +188,21 @@ template <int MODE, int VEC>
 __device__ __forceinline__ Row<VEC> field_row(const KArgs& A, int64_t o, bool ok) {
     Row<VEC> r;
     if (ok) {
-        if constexpr (VEC == 2) {
-            if constexpr (MODE == MODE_RES) {
-                const double2 q = *reinterpret_cast<const double2*>(A.u + o);
-                r.v[0] = q.x; r.v[1] = q.y;
-            } else if constexpr (MODE == MODE_JEXACT) {
-                const double2 q = *reinterpret_cast<const double2*>(A.v + o);
-                r.v[0] = q.x; r.v[1] = q.y;
-            } else {
-                const double2 qu = *reinterpret_cast<const double2*>(A.u + o);
-                const double2 qv = *reinterpret_cast<const double2*>(A.v + o);
-                r.v[0] = qu.x + A.eps * qv.x;  // w = u + eps v
-                r.v[1] = qu.y + A.eps * qv.y;
+        if constexpr (VEC % 2 == 0) {
+#pragma unroll
+            for (int h = 0; h < VEC; h += 2) {
+                if constexpr (MODE == MODE_RES) {
+                    const double2 q = *reinterpret_cast<const double2*>(A.u + o + h);
+                    r.v[h] = q.x; r.v[h + 1] = q.y;
+                } else if constexpr (MODE == MODE_JEXACT) {
+                    const double2 q = *reinterpret_cast<const double2*>(A.v + o + h);
+                    r.v[h] = q.x; r.v[h + 1] = q.y;
+                } else {
+                    const double2 qu = *reinterpret_cast<const double2*>(A.u + o + h);
+                    const double2 qv = *reinterpret_cast<const double2*>(A.v + o + h);
+                    r.v[h] = qu.x + A.eps * qv.x;  // w = u + eps v
+                    r.v[h + 1] = qu.y + A.eps * qv.y;
+                }
             }
         } else {
             r.v[0] = fieldval<MODE>(A, o);
@@ -200,9 +218,12 @@ template <int VEC>
 __device__ __forceinline__ Row<VEC> data_row(const double* __restrict__ p, int64_t o, bool ok) {
     Row<VEC> r;
     if (ok) {
-        if constexpr (VEC == 2) {
-            const double2 q = *reinterpret_cast<const double2*>(p + o);
-            r.v[0] = q.x; r.v[1] = q.y;
+        if constexpr (VEC % 2 == 0) {
+#pragma unroll
+            for (int h = 0; h < VEC; h += 2) {
+                const double2 q = *reinterpret_cast<const double2*>(p + o + h);
+                r.v[h] = q.x; r.v[h + 1] = q.y;
+            }
         } else {
             r.v[0] = p[o];
         }
@@ -215,15 +236,18 @@ __device__ __forceinline__ Row<VEC> data_row(const double* __restrict__ p, int64
 
 template <int VEC>
 __device__ __forceinline__ void store_row(double* __restrict__ p, int64_t o, const Row<VEC>& r) {
-    if constexpr (VEC == 2) {
-        *reinterpret_cast<double2*>(p + o) = make_double2(r.v[0], r.v[1]);
+    if constexpr (VEC % 2 == 0) {
+#pragma unroll
+        for (int h = 0; h < VEC; h += 2) *reinterpret_cast<double2*>(p + o + h) = make_double2(r.v[h], r.v[h + 1]);
     } else {
         p[o] = r.v[0];
     }
 }
 
 // ------------------------------------------------------------------------------ 2D stencil
-// Block = 256 threads x VEC columns (one row segment), marching A.rows rows in y.
+// Block = 256 threads x VEC columns (one row segment), marching A.rows rows in y.  Software
+// pipeline: while row j is computed, the stencil field of row j+2 and the centre operands of
+// row j+1 are in flight, so no iteration waits on a load it issued itself.
 template <int KIND, int MODE, int EPI, int VEC>
 __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A) {
     __shared__ double sh[8];
@@ -234,28 +258,49 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A) {
     const int64_t nx = A.nx, ny = A.ny;
     const int64_t x0 = (int64_t)tx * (kBlock * VEC) + (int64_t)threadIdx.x * VEC;
     const bool act = x0 < nx;
-    const bool left_lane = lane == 0 && x0 >= 1 && x0 - 1 < nx;  // wave-edge lanes load their outer column
-    const bool right_lane = lane == 63 && x0 + VEC < nx;
+    const bool probe = (A.fast & 2) != 0;  // cost probe (bench hook only): skip the edge loads
+    const bool left_lane = !probe && lane == 0 && x0 >= 1 && x0 - 1 < nx;  // wave-edge lanes load their outer column
+    const bool right_lane = !probe && lane == 63 && x0 + VEC < nx;
     const int64_t y0 = (int64_t)ty * A.rows;
     const int64_t y1 = y0 + A.rows < ny ? y0 + A.rows : ny;
+    constexpr bool kU = MODE == MODE_JEXACT && KIND == NK_BRATU2D;
+    constexpr bool kUn = KIND == NK_HEAT2D_EULER && MODE != MODE_JEXACT;
+    constexpr bool kF0 = MODE == MODE_JFD;
+    constexpr bool kAx = EPI == EPI_DOT || EPI == EPI_RESID;
     double acc = 0.0;
     if (y0 < ny) {
-        // row -1 / row ny are the ghost planes (zero, or the neighbouring slab's boundary row)
+        // rows y0-1 .. y0+1 (row -1 / row ny are the ghost planes: zero, or the neighbour slab's row)
         Row<VEC> fm = field_row<MODE, VEC>(A, (y0 - 1) * nx + x0, act);
         Row<VEC> fc = field_row<MODE, VEC>(A, y0 * nx + x0, act);
+        Row<VEC> fp = field_row<MODE, VEC>(A, (y0 + 1) * nx + x0, act);
         double elc = left_lane ? fieldval<MODE>(A, y0 * nx + x0 - 1) : 0.0;
         double erc = right_lane ? fieldval<MODE>(A, y0 * nx + x0 + VEC) : 0.0;
+        const bool has1 = y0 + 1 < ny;
+        double elp = (left_lane && has1) ? fieldval<MODE>(A, (y0 + 1) * nx + x0 - 1) : 0.0;
+        double erp = (right_lane && has1) ? fieldval<MODE>(A, (y0 + 1) * nx + x0 + VEC) : 0.0;
+        Row<VEC> uc{}, unc{}, f0c{}, ax{};
+        {
+            const int64_t o = y0 * nx + x0;
+            if constexpr (kU) uc = data_row<VEC>(A.u, o, act);
+            if constexpr (kUn) unc = data_row<VEC>(A.un, o, act);
+            if constexpr (kF0) f0c = data_row<VEC>(A.F0, o, act);
+            if constexpr (kAx) ax = data_row<VEC>(A.aux, o, act);
+        }
         for (int64_t j = y0; j < y1; ++j) {
             const int64_t o = j * nx + x0;
-            const Row<VEC> fp = field_row<MODE, VEC>(A, o + nx, act);
-            const bool nxt = j + 1 < ny;
-            const double elp = (left_lane && nxt) ? fieldval<MODE>(A, o + nx - 1) : 0.0;
-            const double erp = (right_lane && nxt) ? fieldval<MODE>(A, o + nx + VEC) : 0.0;
-            Row<VEC> uc{}, unc{}, f0c{}, ax{};
-            if constexpr (MODE == MODE_JEXACT && KIND == NK_BRATU2D) uc = data_row<VEC>(A.u, o, act);
-            if constexpr (KIND == NK_HEAT2D_EULER && MODE != MODE_JEXACT) unc = data_row<VEC>(A.un, o, act);
-            if constexpr (MODE == MODE_JFD) f0c = data_row<VEC>(A.F0, o, act);
-            if constexpr (EPI == EPI_DOT || EPI == EPI_RESID) ax = data_row<VEC>(A.aux, o, act);
+            // ---- issue: stencil field of row j+2, centre operands of row j+1
+            const bool f2 = act && j + 1 < y1;  // row j+2 is needed only if row j+1 is computed here
+            const Row<VEC> fpp = field_row<MODE, VEC>(A, o + 2 * nx, f2);
+            const bool e2 = j + 2 < ny && j + 1 < y1;
+            const double elpp = (left_lane && e2) ? fieldval<MODE>(A, o + 2 * nx - 1) : 0.0;
+            const double erpp = (right_lane && e2) ? fieldval<MODE>(A, o + 2 * nx + VEC) : 0.0;
+            const bool pre = act && j + 1 < y1;
+            Row<VEC> ucn{}, uncn{}, f0cn{}, axn{};
+            if constexpr (kU) ucn = data_row<VEC>(A.u, o + nx, pre);
+            if constexpr (kUn) uncn = data_row<VEC>(A.un, o + nx, pre);
+            if constexpr (kF0) f0cn = data_row<VEC>(A.F0, o + nx, pre);
+            if constexpr (kAx) axn = data_row<VEC>(A.aux, o + nx, pre);
+            // ---- compute row j from registers loaded in earlier iterations
             double lft = __shfl_up(fc.v[VEC - 1], 1, 64);
             double rgt = __shfl_down(fc.v[0], 1, 64);
             if (lane == 0) lft = elc;
@@ -267,7 +312,7 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A) {
                     const double w = (k == 0) ? lft : fc.v[k == 0 ? 0 : k - 1];
                     const double e = (k == VEC - 1) ? rgt : fc.v[k == VEC - 1 ? k : k + 1];
                     const double c = fc.v[k];
-                    const double lsum = lap(c, e, w, A.hx2) + lap(c, fp.v[k], fm.v[k], A.hy2);
+                    const double lsum = lapk(A, c, e, w, A.hx2, A.ihx2) + lapk(A, c, fp.v[k], fm.v[k], A.hy2, A.ihy2);
                     double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unc.v[k], f0c.v[k]);
                     acc = epilogue<EPI>(r, ax.v[k], acc);
                     val.v[k] = r;
@@ -276,8 +321,15 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A) {
             }
             fm = fc;
             fc = fp;
+            fp = fpp;
             elc = elp;
             erc = erp;
+            elp = elpp;
+            erp = erpp;
+            uc = ucn;
+            unc = uncn;
+            f0c = f0cn;
+            ax = axn;
         }
     }
     if constexpr (EPI != EPI_NONE) {
@@ -337,7 +389,8 @@ __global__ __launch_bounds__(kBlock) void k_st3d(KArgs A) {
                     const double w = (q == 0) ? lft : fc.v[q == 0 ? 0 : q - 1];
                     const double e = (q == VEC - 1) ? rgt : fc.v[q == VEC - 1 ? q : q + 1];
                     const double c = fc.v[q];
-                    const double lsum = (lap(c, e, w, A.hx2) + lap(c, fn.v[q], fs.v[q], A.hy2)) + lap(c, fp.v[q], fm.v[q], A.hz2);
+                    const double lsum = (lapk(A, c, e, w, A.hx2, A.ihx2) + lapk(A, c, fn.v[q], fs.v[q], A.hy2, A.ihy2)) +
+                                        lapk(A, c, fp.v[q], fm.v[q], A.hz2, A.ihz2);
                     double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unc.v[q], f0c.v[q]);
                     acc = epilogue<EPI>(r, ax.v[q], acc);
                     val.v[q] = r;
@@ -393,10 +446,9 @@ __global__ __launch_bounds__(kBlock) void k_sumsq(int64_t n, const double* __res
     if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
-__global__ __launch_bounds__(64) void k_finalize(const double* __restrict__ in, int len, double* __restrict__ dst, int sqrt_it) {
-    double t = 0.0;
-    for (int m = threadIdx.x; m < len; m += 64) t += in[m];
-    t = wave_sum(t);
+__global__ __launch_bounds__(kBlock) void k_finalize(const double* __restrict__ in, int len, double* __restrict__ dst, int sqrt_it) {
+    __shared__ double sh[8];
+    const double t = reduce_input(in, len, sh);
     if (threadIdx.x == 0) dst[0] = sqrt_it ? sqrt(t) : t;
 }
 
@@ -496,34 +548,53 @@ __device__ __forceinline__ void st2(dx2* p, dx2 v) {
     else *p = v;
 }
 
+// rev = 1 sweeps the vectors from the end: consecutive passes alternate direction so each pass
+// starts on the lines the previous pass touched last (still in the 256 MB Infinity Cache).
 template <bool HAS_NEXT, int U, bool NT>
 __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restrict__ q, const double* __restrict__ vi,
                                                     const double* __restrict__ vnext, const double* __restrict__ red_in,
-                                                    int red_len, double* __restrict__ h_out, double* __restrict__ part) {
+                                                    int red_len, double* __restrict__ h_out, double* __restrict__ part,
+                                                    int rev) {
     __shared__ double sh[8];
-    const double h = reduce_input(red_in, red_len, sh);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *h_out = h;
-    const double mh = -h;
     dx2* q2 = reinterpret_cast<dx2*>(q);
     const dx2* v2 = reinterpret_cast<const dx2*>(vi);
     const dx2* w2 = reinterpret_cast<const dx2*>(vnext);
     const int64_t n2 = n >> 1;
     const int64_t st = (int64_t)gridDim.x * kBlock;
-    double acc = 0.0;
+    const int64_t base = rev ? n2 - 1 : 0, sgn = rev ? -1 : 1;
     int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    for (; i + (U - 1) * st < n2; i += U * st) {
-        dx2 a[U], bv[U], cv[U];
+    // prologue: the first U stream loads go out before the partial-sum reduction, so h's L2 round
+    // trip overlaps with HBM latency instead of preceding it
+    dx2 a[U], bv[U], cv[U];
+    bool have = i + (U - 1) * st < n2;
+    if (have) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            a[u] = ld2<false>(q2 + i + u * st);
-            bv[u] = ld2<NT>(v2 + i + u * st);
-            if constexpr (HAS_NEXT) cv[u] = ld2<false>(w2 + i + u * st);
+            const int64_t e = base + sgn * (i + u * st);
+            a[u] = ld2<false>(q2 + e);
+            bv[u] = ld2<NT>(v2 + e);
+            if constexpr (HAS_NEXT) cv[u] = ld2<false>(w2 + e);
+        }
+    }
+    const double h = reduce_input(red_in, red_len, sh);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *h_out = h;
+    const double mh = -h;
+    double acc = 0.0;
+    for (; have; i += U * st, have = i + (U - 1) * st < n2) {
+        if (i != (int64_t)blockIdx.x * kBlock + threadIdx.x) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t e = base + sgn * (i + u * st);
+                a[u] = ld2<false>(q2 + e);
+                bv[u] = ld2<NT>(v2 + e);
+                if constexpr (HAS_NEXT) cv[u] = ld2<false>(w2 + e);
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             a[u].x = fma(mh, bv[u].x, a[u].x);
             a[u].y = fma(mh, bv[u].y, a[u].y);
-            st2<false>(q2 + i + u * st, a[u]);
+            st2<false>(q2 + base + sgn * (i + u * st), a[u]);
             if constexpr (HAS_NEXT) {
                 acc = fma(cv[u].x, a[u].x, acc);
                 acc = fma(cv[u].y, a[u].y, acc);
@@ -534,13 +605,14 @@ __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restri
         }
     }
     for (; i < n2; i += st) {
-        dx2 a = q2[i];
-        const dx2 b = v2[i];
+        const int64_t e = base + sgn * i;
+        dx2 a = q2[e];
+        const dx2 b = ld2<NT>(v2 + e);
         a.x = fma(mh, b.x, a.x);
         a.y = fma(mh, b.y, a.y);
-        q2[i] = a;
+        q2[e] = a;
         if constexpr (HAS_NEXT) {
-            const dx2 c = w2[i];
+            const dx2 c = w2[e];
             acc = fma(c.x, a.x, acc);
             acc = fma(c.y, a.y, acc);
         } else {
@@ -568,7 +640,7 @@ struct UpdArgs {
 };
 
 // xr = Σ y_i V_i (the kaxpy! chain of gmres!, from xr = 0); on the last chunk x = x + xr
-// (restart) or x = xr; optional partials of ||x||^2.
+// (restart) or x = xr; optional partials of ||x||^2.  16-B accesses; V loads non-temporal.
 __global__ __launch_bounds__(kBlock) void k_update_x(UpdArgs A) {
     __shared__ double sh[8];
     const int64_t n = A.n;
@@ -577,10 +649,35 @@ __global__ __launch_bounds__(kBlock) void k_update_x(UpdArgs A) {
     for (int m = 0; m < kMaxUpdateVecs; ++m) yv[m] = m < A.k ? A.y[m] : 0.0;
     double acc = 0.0;
     const int64_t st = (int64_t)gridDim.x * kBlock;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += st) {
-        double t = A.first ? 0.0 : A.xr[i];
+    const int64_t n2 = n >> 1;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n2; i += st) {
+        dx2 t = A.first ? dx2{0.0, 0.0} : reinterpret_cast<const dx2*>(A.xr)[i];
 #pragma unroll
         for (int m = 0; m < kMaxUpdateVecs; ++m)  // compile-time indices keep yv in registers
+            if (m < A.k) {
+                const dx2 v = __builtin_nontemporal_load(reinterpret_cast<const dx2*>(A.V[m]) + i);
+                t.x = fma(yv[m], v.x, t.x);
+                t.y = fma(yv[m], v.y, t.y);
+            }
+        if (A.last) {
+            dx2 xv = t;
+            if (A.restart) {
+                const dx2 x0 = reinterpret_cast<const dx2*>(A.x)[i];
+                xv.x = fma(1.0, t.x, x0.x);
+                xv.y = fma(1.0, t.y, x0.y);
+            }
+            reinterpret_cast<dx2*>(A.x)[i] = xv;
+            acc = fma(xv.x, xv.x, acc);
+            acc = fma(xv.y, xv.y, acc);
+        } else {
+            reinterpret_cast<dx2*>(A.xr)[i] = t;
+        }
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+        const int64_t i = n - 1;
+        double t = A.first ? 0.0 : A.xr[i];
+#pragma unroll
+        for (int m = 0; m < kMaxUpdateVecs; ++m)
             if (m < A.k) t = fma(yv[m], A.V[m][i], t);
         if (A.last) {
             const double xv = A.restart ? fma(1.0, t, A.x[i]) : t;
@@ -624,7 +721,8 @@ void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s) {
     if constexpr (KIND == NK_BRATU1D) {
         hipLaunchKernelGGL((k_st1d<MODE, EPI>), dim3(grid), dim3(kBlock), 0, s, A);
     } else if constexpr (KIND == NK_BRATU2D || KIND == NK_HEAT2D_EULER) {
-        if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
+        if (vec == 4) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 4>), dim3(grid), dim3(kBlock), 0, s, A);
+        else if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
         else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1>), dim3(grid), dim3(kBlock), 0, s, A);
     } else {
         if (vec == 2) hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
@@ -666,7 +764,14 @@ int red_blocks(int64_t n) {
     return (int)g;
 }
 
-int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red) {
+namespace {
+int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_override, int fast);
+}
+
+int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red) { return launch_stencil_ex(c, in, red, 0, 0); }
+
+namespace {
+int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_override, int fast) {
     const nk_problem* p = in.p;
     Geo g;
     NK_TRY(geometry(c, p, &g));
@@ -675,16 +780,21 @@ int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red) {
     A.nx = p->nx; A.ny = p->ny; A.nz = p->nz;
     A.hx2 = p->hx * p->hx; A.hy2 = p->hy * p->hy; A.hz2 = p->hz * p->hz;
     A.lam = p->lambda; A.a = p->a; A.dt = p->dt; A.eps = in.eps;
+    A.fast = fast;
+    A.ihx2 = 1.0 / A.hx2; A.ihy2 = 1.0 / A.hy2; A.ihz2 = 1.0 / A.hz2; A.ieps = in.eps != 0.0 ? 1.0 / in.eps : 0.0;
     int vec = 1, grid = 1;
     if (g.dim == 1) {
         grid = (int)((p->nx + kBlock - 1) / kBlock);
     } else if (g.dim == 2) {
+        static const int vec_pref = env_int("NK_ST_VEC", 2);
         vec = (p->nx % 2 == 0) ? 2 : 1;
+        if (((fast & 4) || vec_pref == 4) && p->nx % 4 == 0) vec = 4;
         A.tiles_x = (int)((p->nx + kBlock * vec - 1) / (kBlock * vec));
         static const int target = env_int("NK_ST_BLOCKS", 2048);
         int64_t rows = (p->ny * A.tiles_x + target - 1) / target;
         static const int min_rows = env_int("NK_ST_MINROWS", 8);
         if (rows < min_rows) rows = min_rows;
+        if (rows_override > 0) rows = rows_override;
         if (rows > p->ny) rows = p->ny;
         A.rows = (int)rows;
         A.tiles_y = (int)((p->ny + rows - 1) / rows);
@@ -697,6 +807,7 @@ int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red) {
         int64_t planes = ((int64_t)p->nz * A.tiles_x * A.tiles_y + target - 1) / target;
         static const int min_planes = env_int("NK_ST_MINPLANES", 8);
         if (planes < min_planes) planes = min_planes;
+        if (rows_override > 0) planes = rows_override;
         if (planes > p->nz) planes = p->nz;
         A.rows = (int)planes;
         grid = A.tiles_x * A.tiles_y * (int)((p->nz + planes - 1) / planes);
@@ -730,6 +841,7 @@ int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red) {
         }
     });
 }
+}  // namespace
 
 int launch_dot(nk_ctx* c, int64_t n, const double* x, const double* y, Red* red) {
     const int g = red_blocks(n);
@@ -748,7 +860,7 @@ int launch_sumsq(nk_ctx* c, int64_t n, const double* x, Red* red) {
 }
 
 int launch_finalize(nk_ctx* c, Red r, double* dst, int sqrt_it) {
-    return launch(c, "finalize", 0.0, [&] { hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, c->stream, r.ptr, r.len, dst, sqrt_it); });
+    return launch(c, "finalize", 0.0, [&] { hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, c->stream, r.ptr, r.len, dst, sqrt_it); });
 }
 
 #define NK_STREAM_LAUNCH(name, bytes_per, kern, ...)                                              \
@@ -768,19 +880,33 @@ int launch_divcopy(nk_ctx* c, int64_t n, double* y, const double* x, double s) {
 }
 int launch_ref(nk_ctx* c, int64_t n, double* x, double* y, double cc, double ss) { NK_STREAM_LAUNCH("ref", 32.0, k_ref, n, x, y, cc, ss); }
 
-int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const double* vnext, Red in, double* h_out, Red* out) {
+namespace {
+template <bool HAS_NEXT>
+void mgs_dispatch(int variant, int g, hipStream_t s, int64_t n, double* q, const double* vi, const double* vn,
+                  const double* red, int len, double* h, double* part, int rev) {
+    switch (variant) {  // unroll depth x non-temporal V_i loads (tools/kbench.py measures them)
+    case 0: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, false>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
+    case 1: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
+    case 2: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
+    case 3: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 8, false>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
+    default: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 8, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
+    }
+}
+}  // namespace
+
+int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const double* vnext, Red in, double* h_out, Red* out,
+                    int rev) {
+    static const int variant = env_int("NK_MGS_VARIANT", kMgsVariant);
     const int g = red_blocks(n);
     double* part = red_slot(c);
     out->ptr = part;
     out->len = g;
     if (vnext)
         return launch(c, "mgs_pass", 32.0 * n, [&] {
-            hipLaunchKernelGGL((k_mgs_pass<true, kMgsUnroll, kMgsNT>), dim3(g), dim3(kBlock), 0, c->stream, n, q, vi, vnext,
-                               in.ptr, in.len, h_out, part);
+            mgs_dispatch<true>(variant, g, c->stream, n, q, vi, vnext, in.ptr, in.len, h_out, part, rev);
         });
     return launch(c, "mgs_pass_last", 24.0 * n, [&] {
-        hipLaunchKernelGGL((k_mgs_pass<false, kMgsUnroll, kMgsNT>), dim3(g), dim3(kBlock), 0, c->stream, n, q, vi, vnext,
-                           in.ptr, in.len, h_out, part);
+        mgs_dispatch<false>(variant, g, c->stream, n, q, vi, vnext, in.ptr, in.len, h_out, part, rev);
     });
 }
 
@@ -834,46 +960,65 @@ int launch_cg_direction(nk_ctx* c, int64_t n, double beta, double* p, const doub
 // ------------------------------------------------------------------------------ variant bench hook
 // Times kernel variants in ONE process (interleaved A/B, MI355X_MICROARCH methodology rule 24).
 // Not part of the public ABI (exported as nkb_*; used by tools/kbench.py only).
-namespace {
-template <bool HAS_NEXT, int U, bool NT>
-void mgs_variant(nk_ctx* c, int g, int64_t n, double* q, const double* vi, const double* vn, const double* red,
-                 double* h, double* part) {
-    hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, U, NT>), dim3(g), dim3(kBlock), 0, c->stream, n, q, vi, vn, red, 1, h, part);
-}
-}  // namespace
-
 }  // namespace nk
 
-extern "C" int nkb_mgs(nk_ctx* c, int64_t n, int variant, int grid, int reps, double* us_out) {
+// One Arnoldi step's MGS sweep at basis size k, as GMRES runs it: passes i = 1..k read q, V_i,
+// V_{i+1} (the last one q, V_k) over a real basis of k+1 distinct vectors.  alt = alternate the
+// sweep direction pass to pass.  Returns the average microseconds per pass.
+extern "C" int nkb_mgs_seq(nk_ctx* c, int64_t n, int k, int variant, int alt, int reps, double* us_out) {
     using namespace nk;
-    if (!c || n < 2 || reps < 1 || !us_out) return NK_E_ARG;
-    double *q = nullptr, *v = nullptr, *w = nullptr;
-    NK_HIP(c, hipMalloc(&q, sizeof(double) * n));
-    NK_HIP(c, hipMalloc(&v, sizeof(double) * n));
-    NK_HIP(c, hipMalloc(&w, sizeof(double) * n));
-    NK_HIP(c, hipMemsetAsync(q, 0, sizeof(double) * n, c->stream));
-    NK_HIP(c, hipMemsetAsync(v, 0, sizeof(double) * n, c->stream));
-    NK_HIP(c, hipMemsetAsync(w, 0, sizeof(double) * n, c->stream));
-    const int g = grid > 0 ? grid : red_blocks(n);
-    double* part = red_slot(c);
-    double* red = c->scal;
+    if (!c || n < 2 || k < 1 || reps < 1 || !us_out) return NK_E_ARG;
+    std::vector<double*> V(k + 2, nullptr);
+    for (auto& p : V) {
+        NK_HIP(c, hipMalloc(&p, sizeof(double) * n));
+        NK_HIP(c, hipMemsetAsync(p, 0, sizeof(double) * n, c->stream));
+    }
+    double* q = V[k + 1];
+    const int g = red_blocks(n);
+    double* parts[2] = {red_slot(c), red_slot(c)};  // ping-pong partials, as in the solver
+    double* hs = c->scal;
     hipEvent_t a, b;
     NK_HIP(c, hipEventCreate(&a));
     NK_HIP(c, hipEventCreate(&b));
-    auto run = [&] {
-        switch (variant) {
-        case 0: mgs_variant<true, 1, false>(c, g, n, q, v, w, red, red + 1, part); break;
-        case 1: mgs_variant<true, 2, false>(c, g, n, q, v, w, red, red + 1, part); break;
-        case 2: mgs_variant<true, 4, false>(c, g, n, q, v, w, red, red + 1, part); break;
-        case 3: mgs_variant<true, 2, true>(c, g, n, q, v, w, red, red + 1, part); break;
-        case 4: mgs_variant<true, 4, true>(c, g, n, q, v, w, red, red + 1, part); break;
-        case 5: mgs_variant<false, 2, false>(c, g, n, q, v, w, red, red + 1, part); break;
-        default: mgs_variant<true, 8, false>(c, g, n, q, v, w, red, red + 1, part); break;
+    auto sweep = [&] {
+        for (int i = 0; i < k; ++i) {
+            const int rev = alt ? (i & 1) : 0;
+            const double* in = parts[i & 1];
+            double* out = parts[(i + 1) & 1];
+            if (i + 1 < k) mgs_dispatch<true>(variant, g, c->stream, n, q, V[i], V[i + 1], in, g, hs + 1, out, rev);
+            else mgs_dispatch<false>(variant, g, c->stream, n, q, V[i], nullptr, in, g, hs + 1, out, rev);
         }
     };
-    run();
+    sweep();
     NK_HIP(c, hipEventRecord(a, c->stream));
-    for (int r = 0; r < reps; ++r) run();
+    for (int r = 0; r < reps; ++r) sweep();
+    NK_HIP(c, hipEventRecord(b, c->stream));
+    NK_HIP(c, hipEventSynchronize(b));
+    float ms = 0.f;
+    NK_HIP(c, hipEventElapsedTime(&ms, a, b));
+    *us_out = 1e3 * ms / ((double)reps * k);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    for (auto p : V) (void)hipFree(p);
+    return NK_OK;
+}
+
+// 2D Bratu stencil variants: mode (0 res, 1 exact, 2 fd), epi, rows per tile, fast reciprocals.
+extern "C" int nkb_stencil(nk_ctx* c, int64_t nx, int64_t ny, int mode, int epi, int rows, int fast, int reps,
+                           double* us_out) {
+    using namespace nk;
+    if (!c || nx < 2 || ny < 2 || reps < 1 || !us_out) return NK_E_ARG;
+    nk_problem p{NK_BRATU2D, NK_BC_ZERO, nx, ny, 1, 1.0 / (nx + 1), 1.0 / (ny + 1), 1.0, 3.51382, 0.0, 0.0, nullptr};
+    double *u = nullptr, *v = nullptr, *F0 = nullptr, *aux = nullptr, *out = nullptr;
+    for (double** q : {&u, &v, &F0, &aux, &out}) NK_TRY(nk_vec_alloc(c, &p, q));
+    StencilIn in{&p, mode, epi, out, u, v, F0, aux, 1e-6};
+    Red r{};
+    hipEvent_t a, b;
+    NK_HIP(c, hipEventCreate(&a));
+    NK_HIP(c, hipEventCreate(&b));
+    NK_TRY(launch_stencil_ex(c, in, &r, rows, fast));
+    NK_HIP(c, hipEventRecord(a, c->stream));
+    for (int k = 0; k < reps; ++k) NK_TRY(launch_stencil_ex(c, in, &r, rows, fast));
     NK_HIP(c, hipEventRecord(b, c->stream));
     NK_HIP(c, hipEventSynchronize(b));
     float ms = 0.f;
@@ -881,9 +1026,7 @@ extern "C" int nkb_mgs(nk_ctx* c, int64_t n, int variant, int grid, int reps, do
     *us_out = 1e3 * ms / reps;
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
-    (void)hipFree(q);
-    (void)hipFree(v);
-    (void)hipFree(w);
+    for (double* q : {u, v, F0, aux, out}) nk_vec_free(c, q);
     return NK_OK;
 }
 

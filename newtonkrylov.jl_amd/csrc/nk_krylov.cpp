@@ -189,6 +189,10 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
     bool solved = rNorm <= eps_;
     bool tired = iter >= itmax;
     double xnorm = 0.0;  // ||x|| for the FD restart residual (from the fused x update)
+    static const int mgs_alt = [] {
+        const char* e = getenv("NK_MGS_ALT");
+        return (e && *e) ? atoi(e) : 0;  // alternating sweeps: no gain once V_i is loaded non-temporally
+    }();
     while (!(solved || tired || breakdown)) {
         int64_t nr = 0;
         std::fill(cs.begin(), cs.end(), 0.0);
@@ -228,7 +232,7 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
                 const double* vnext = (t + 1 < npasses) ? ws->V[(t + 1) % k] : nullptr;
                 NK_TRY(finish_reduction(c, &red));
                 Red nxt{};
-                NK_TRY(launch_mgs_pass(c, n, w, vi, vnext, red, ws->hdev + t, &nxt));
+                NK_TRY(launch_mgs_pass(c, n, w, vi, vnext, red, ws->hdev + t, &nxt, mgs_alt ? (t & 1) : 0));
                 red = nxt;
             }
             NK_TRY(finish_reduction(c, &red));

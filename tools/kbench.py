@@ -17,16 +17,25 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=4096 * 4096)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--what", default="mgs,stencil")
 args = ap.parse_args()
 
 ctx = ah.Context(0)
 lib = ah.load()
-lib.nkb_mgs.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]
+lib.nkb_mgs_seq.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]
 lib.nkb_copy.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.POINTER(C.c_double)]
+lib.nkb_stencil.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                            C.POINTER(C.c_double)]
 n = args.n
+side = int(round(n ** 0.5))
 
-MGS = {0: "U1", 1: "U2", 2: "U4", 3: "U2+nt(V_i)", 4: "U4+nt(V_i)", 5: "U2 last-pass", 6: "U8"}
-configs = [("copy", None, None)] + [("mgs", v, g) for v in MGS for g in (1024, 2048, 4096)]
+MGS = {0: "U2", 1: "U2+nt(V_i)", 2: "U4+nt(V_i)", 3: "U8", 4: "U8+nt(V_i)"}
+configs = [("copy", None, None, None)]
+if "mgs" in args.what:
+    configs += [("mgs", v, 0, k) for k in (16, 30) for v in MGS]
+ST = {(2, 2): ("jv_fd_dot", 40.0), (1, 2): ("jv_exact_dot", 32.0), (0, 1): ("residual_norm", 16.0)}
+if "stencil" in args.what:
+    configs += [("st", mode_epi, rows, fast) for mode_epi in ST for rows in (8, 16, 32) for fast in (0, 2, 4, 6)]
 res = {c: [] for c in configs}
 for _ in range(args.rounds):
     for cfg in configs:
@@ -34,13 +43,23 @@ for _ in range(args.rounds):
         if cfg[0] == "copy":
             rc = lib.nkb_copy(ctx.handle, n, args.reps, C.byref(us))
             nbytes = 16.0 * n
+        elif cfg[0] == "st":
+            (mode, epi), rows, fast = cfg[1], cfg[2], cfg[3]
+            rc = lib.nkb_stencil(ctx.handle, side, side, mode, epi, rows, fast, args.reps, C.byref(us))
+            nbytes = ST[cfg[1]][1] * side * side
         else:
-            rc = lib.nkb_mgs(ctx.handle, n, cfg[1], cfg[2], args.reps, C.byref(us))
-            nbytes = (32.0 if cfg[1] != 5 else 24.0) * n
+            _, v, alt, k = cfg
+            rc = lib.nkb_mgs_seq(ctx.handle, n, k, v, alt, 2, C.byref(us))
+            nbytes = (32.0 * (k - 1) + 24.0) / k * n  # average algorithmic bytes per pass
         assert rc == 0, rc
         res[cfg].append((us.value, nbytes / (us.value * 1e-6) / 1e9))
 for cfg, v in res.items():
     us = statistics.median(x[0] for x in v)
     gbs = statistics.median(x[1] for x in v)
-    name = "copy (16 B/pt)" if cfg[0] == "copy" else f"mgs {MGS[cfg[1]]:>14s} grid={cfg[2]}"
-    print(f"{name:40s} {us:9.2f} us  {gbs:8.1f} GB/s  ({gbs / 8000 * 100:5.1f}% of 8 TB/s)")
+    if cfg[0] == "copy":
+        name = "copy (16 B/pt, 2 buffers)"
+    elif cfg[0] == "st":
+        name = f"{ST[cfg[1]][0]:>14s} rows={cfg[2]:2d} fast={cfg[3]}"
+    else:
+        name = f"mgs k={cfg[3]:2d} {MGS[cfg[1]]:>11s} alt={cfg[2]}"
+    print(f"{name:40s} {us:9.2f} us/pass  {gbs:8.1f} GB/s  ({gbs / 8000 * 100:5.1f}% of 8 TB/s)")
