@@ -31,6 +31,10 @@ import _nkpath  # noqa: F401
 import ariadne_hip as ah
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+ROOT = os.path.dirname(os.path.abspath(__file__))
+# bench kernel class -> rocprofv3 kernel name prefix (for the PMC traffic of profiles/*/pmc_traffic.json)
+PMC_NAME = {"mgs_pass": "nk::k_mgs_pass<true,", "mgs_pass_last": "nk::k_mgs_pass<false,",
+            "jv_fd_dot": "nk::k_st2d<2, 2, 2,", "jv_exact_dot": "nk::k_st2d<2, 1, 2,", "divcopy": "nk::k_divcopy"}
 LAMBDA = 3.51382       # examples/bratu.jl:41
 
 
@@ -49,6 +53,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-itmax", type=int, default=30, help="Arnoldi steps in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os.cpu_count())")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"),
+                    help="per-kernel HBM traffic from separate rocprofv3 --pmc passes (tools/pmc_traffic.py)")
     return ap.parse_args()
 
 
@@ -147,13 +153,28 @@ def main():
                        / max(1e-30, sum(x["ms"] / max(1, x["timed"]) * x["launches"] for x in prof.values())))
                for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"] / max(1, kv[1]["timed"]) * kv[1]["launches"])}
 
+    pmc = {}
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            pmc = json.load(f)
+
+    def traffic(name):
+        """PMC HBM bytes per launch of this kernel class as a rate over the same launch duration."""
+        pre = PMC_NAME.get(name)
+        hit = [v for k, v in pmc.items() if pre and k.startswith(pre)]
+        return hit[0]["traffic_bytes"] if hit else None
+
     def roof(name):
         v = prof.get(name)
         if not v or v["ms"] <= 0:
             return None
         ach = v["bytes"] / (v["ms"] * 1e-3) / 1e9
+        tb = traffic(name)
         return {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": round(tb / (v["ms"] / v["timed"] * 1e-3) / 1e9, 1) if tb else None,
+                "traffic_bytes_per_launch": tb,
+                "traffic_source": os.path.relpath(args.traffic_json, ROOT) if tb else None,
                 "bytes_per_launch": v["bytes"] / v["timed"], "avg_us": 1e3 * v["ms"] / v["timed"],
                 "timed_launches": v["timed"]}
 

@@ -49,7 +49,7 @@ double* red_slot(nk_ctx* c) {
 }
 
 int finish_reduction(nk_ctx* c, Red* r) {
-    if (c->nranks <= 1) return NK_OK;
+    if (!c->comm) return NK_OK;
     // collapse this rank's partials to one scalar, then sum the scalars over ranks (RCCL)
     double* dst = red_slot(c);
     NK_TRY(launch_finalize(c, *r, dst, 0));

@@ -22,29 +22,36 @@ static int rccl_fail(nk_ctx* c, ncclResult_t r, const char* what) {
 }
 
 int halo_exchange(nk_ctx* c, const nk_problem* p, const double* v) {
-    if (c->nranks <= 1) return NK_OK;
+    if (!c->comm) return NK_OK;
     Geo g;
     NK_TRY(geometry(c, p, &g));
     double* vv = const_cast<double*>(v);  // only the ghost planes are written
     const size_t pl = (size_t)g.plane;
     const int up = c->rank + 1, dn = c->rank - 1;
     ncclComm_t comm = c->comm->comm;
-    return launch(c, "halo", 16.0 * pl * ((dn >= 0) + (up < c->nranks)), [&] {
-        ncclGroupStart();
-        if (dn >= 0) {
-            ncclSend(vv, pl, ncclFloat64, dn, comm, c->stream);
-            ncclRecv(vv - pl, pl, ncclFloat64, dn, comm, c->stream);
+    if (dn < 0 && up >= c->nranks) return NK_OK;  // a lone slab has only physical boundaries
+    ncclResult_t r = ncclSuccess;
+    auto chk = [&r](ncclResult_t x) {
+        if (r == ncclSuccess) r = x;
+    };
+    NK_TRY(launch(c, "halo", 16.0 * pl * ((dn >= 0) + (up < c->nranks)), [&] {
+        chk(ncclGroupStart());
+        if (dn >= 0) {  // my first interior plane -> lower neighbour's upper ghost; its last -> my lower ghost
+            chk(ncclSend(vv, pl, ncclFloat64, dn, comm, c->stream));
+            chk(ncclRecv(vv - pl, pl, ncclFloat64, dn, comm, c->stream));
         }
         if (up < c->nranks) {
-            ncclSend(vv + (size_t)(g.nplanes - 1) * pl, pl, ncclFloat64, up, comm, c->stream);
-            ncclRecv(vv + (size_t)g.nplanes * pl, pl, ncclFloat64, up, comm, c->stream);
+            chk(ncclSend(vv + (size_t)(g.nplanes - 1) * pl, pl, ncclFloat64, up, comm, c->stream));
+            chk(ncclRecv(vv + (size_t)g.nplanes * pl, pl, ncclFloat64, up, comm, c->stream));
         }
-        ncclGroupEnd();
-    });
+        chk(ncclGroupEnd());
+    }));
+    if (r != ncclSuccess) return rccl_fail(c, r, "halo send/recv");
+    return NK_OK;
 }
 
 int allreduce_scalar(nk_ctx* c, double* dev, int64_t count) {
-    if (c->nranks <= 1) return NK_OK;
+    if (!c->comm) return NK_OK;
     ncclResult_t r = ncclSuccess;
     NK_TRY(launch(c, "allreduce", 0.0, [&] {
         r = ncclAllReduce(dev, dev, (size_t)count, ncclFloat64, ncclSum, c->comm->comm, c->stream);
@@ -71,7 +78,8 @@ int nk_dist_unique_id(char out[128]) {
 int nk_dist_init(nk_ctx* c, int32_t rank, int32_t nranks, const char id[128]) {
     if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return NK_E_ARG;
     if (c->comm) return fail(c, NK_E_STATE, "context already distributed");
-    if (nranks == 1) {
+    const char* force = getenv("NK_DIST_FORCE");  // 1-rank communicator: exercises the RCCL path on one GPU
+    if (nranks == 1 && !(force && *force == '1')) {
         c->rank = 0;
         c->nranks = 1;
         return NK_OK;

@@ -139,13 +139,18 @@ class KrylovStats:
     status: str = "unknown"
 
 
-def gmres(A, b, *, memory=20, restart=False, reorthogonalization=False, atol=SQRT_EPS, rtol=SQRT_EPS, itmax=0):
-    """Krylov.jl gmres! with M = N = I. A: callable v -> A v."""
-    n = b.size
-    x = np.zeros(n)
-    xr = np.zeros(n) if restart else x
+def gmres(A, b, *, memory=20, restart=False, reorthogonalization=False, atol=SQRT_EPS, rtol=SQRT_EPS, itmax=0,
+          dot=None, n=None):
+    """Krylov.jl gmres! with M = N = I. A: callable v -> A v.
+
+    `dot` (default numpy) lets a caller supply a distributed inner product (all-reduced over
+    ranks) and `n` the global length -- the multi-rank protocol test uses both."""
+    dot = dot or (lambda x, y: float(np.dot(x, y)))
+    n = b.size if n is None else n  # global length (itmax = 2n); arrays are this rank's b.size
+    x = np.zeros(b.size)
+    xr = np.zeros(b.size) if restart else x
     w = b.copy()
-    beta = np.linalg.norm(w)
+    beta = math.sqrt(dot(w, w))
     rNorm = beta
     hist = [rNorm]
     eps_ = atol + rtol * rNorm
@@ -169,7 +174,7 @@ def gmres(A, b, *, memory=20, restart=False, reorthogonalization=False, atol=SQR
             if npass >= 1:
                 w = b - A(x)
                 nmv += 1
-        beta = np.linalg.norm(w)
+        beta = math.sqrt(dot(w, w))
         z[0] = beta
         V.append(w / beta)
         npass += 1
@@ -181,15 +186,15 @@ def gmres(A, b, *, memory=20, restart=False, reorthogonalization=False, atol=SQR
             nmv += 1
             col = []
             for i in range(k):
-                h = float(np.dot(V[i], w))
+                h = dot(V[i], w)
                 col.append(h)
                 w = w - h * V[i]
             if reorthogonalization:
                 for i in range(k):
-                    h = float(np.dot(V[i], w))
+                    h = dot(V[i], w)
                     col[i] += h
                     w = w - h * V[i]
-            Hbis = float(np.linalg.norm(w))
+            Hbis = math.sqrt(dot(w, w))
             for i in range(k - 1):
                 rtmp = c[i] * col[i] + s[i] * col[i + 1]
                 col[i + 1] = s[i] * col[i] - c[i] * col[i + 1]

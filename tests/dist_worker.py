@@ -1,0 +1,76 @@
+"""Worker for the multi-rank GPU test (launched by tests/test_hip_dist.py through torch.distributed.run).
+
+Every rank owns a slab of a 2D Bratu grid, builds its device vectors from the global initial
+condition, runs the distributed HIP path (RCCL halo exchange + all-reduced inner products inside
+libnkhip.so) and rank 0 writes the gathered solution, one Jv product and the solver stats.
+On a one-GPU box all ranks share device 0 (NK_WORKER_SHARED_DEVICE=1).
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import _nkpath  # noqa: F401,E402
+import ariadne_hip as ah  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--out", required=True)
+ap.add_argument("--nx", type=int, default=48)
+ap.add_argument("--ny", type=int, default=40)
+ap.add_argument("--jv", default="exact")
+args = ap.parse_args()
+
+dist.init_process_group("gloo")
+rank, world = dist.get_rank(), dist.get_world_size()
+device = 0 if os.environ.get("NK_WORKER_SHARED_DEVICE") == "1" else int(os.environ.get("LOCAL_RANK", "0"))
+ctx = ah.Context(device)
+ah.set_default_context(ctx)
+
+
+def bcast(obj, src):
+    box = [obj]
+    dist.broadcast_object_list(box, src=src)
+    return box[0]
+
+
+try:
+    ah.init_distributed(ctx, rank, world, bcast)
+except ah.NKError as e:
+    if rank == 0:
+        json.dump({"skip": f"RCCL communicator could not be created: {e}"}, open(args.out + ".json", "w"))
+    sys.exit(0)
+
+nx, ny = args.nx, args.ny
+grid = ah.slab((nx, ny), rank, world)
+hx, hy, lam = 1.0 / (nx + 1), 1.0 / (ny + 1), 3.51382
+xs = np.arange(1, nx + 1) * hx
+y0, nyl = grid.offset, grid.shape_xyz[1]
+ys = np.arange(y0 + 1, y0 + nyl + 1) * hy
+u0 = np.sin(np.pi * ys)[:, None] * np.sin(np.pi * xs)[None, :]
+v_glob = np.random.default_rng(7).standard_normal((ny, nx))
+p = (hx, hy, lam)
+
+u = ah.DeviceArray.from_numpy(u0, grid, ctx)
+res = u.zero()
+vd = ah.DeviceArray.from_numpy(np.ascontiguousarray(v_glob[y0:y0 + nyl]), grid, ctx)
+out = u.zero()
+ah.bratu2d_(res, u, p)
+ah.mul_(out, ah.JacobianOperator(ah.bratu2d_, res, u, p, jv=args.jv), vd)
+jv_loc = out.to_numpy()
+F_loc = res.to_numpy()
+dot = ah.kdot(len(u), u, vd)
+u, r = ah.newton_krylov_(ah.bratu2d_, u, p, res, memory=10, tol_rel=1e-9, krylov_kwargs=dict(restart=True), jv=args.jv)
+parts = [None] * world
+dist.all_gather_object(parts, dict(y0=y0, u=u.to_numpy(), jv=jv_loc, F=F_loc))
+if rank == 0:
+    parts.sort(key=lambda d: d["y0"])
+    np.savez(args.out + ".npz", u=np.concatenate([d["u"] for d in parts]), jv=np.concatenate([d["jv"] for d in parts]),
+             F=np.concatenate([d["F"] for d in parts]), v=v_glob)
+    json.dump(dict(solved=bool(r.solved), outer=r.stats.outer_iterations, inner=r.stats.inner_iterations,
+                   n_res=r.stats.n_res, dot=dot, world=world), open(args.out + ".json", "w"))
+dist.barrier()
+ctx.sync()

@@ -1,0 +1,140 @@
+"""Multi-rank protocol of the slab decomposition, on CPU with gloo (world_size 2 and 3).
+
+libnkhip.so's distributed path (nk_dist.cpp) does exactly two things beyond the single-GPU code:
+before every stencil application it fills the two ghost planes of the input vector with the
+neighbouring slabs' boundary planes (RCCL send/recv), and it completes every inner product with a
+sum over ranks (RCCL all-reduce) before any consumer reads it.  Its kernels cannot run here, so
+this test drives the SAME protocol -- the product's own slab partition (ariadne_hip.slab), ghost
+planes filled by gloo send/recv from the neighbours, all-reduced dots -- around a numpy stand-in
+for the stencil kernels, and checks it reproduces the single-domain CPU oracle: residuals, Jv,
+the GMRES(10) history, and the converged Newton iterate.  (The RCCL plumbing itself is checked on
+the GPU box by tests/test_hip_dist.py.)
+"""
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import _nkpath  # noqa: F401
+import ariadne_hip as ah
+from oracle import ariadne_ref as ar
+from oracle import oracle as oc
+
+NX, NY = 20, 17
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class Slab:
+    """One rank's slab with ghost rows, exchanged like nk_dist.cpp halo_exchange."""
+
+    def __init__(self, rank, world):
+        self.rank, self.world = rank, world
+        self.grid = ah.slab((NX, NY), rank, world)
+        self.y0, self.nyl = self.grid.offset, self.grid.shape_xyz[1]
+        self.hx, self.hy, self.lam = 1.0 / (NX + 1), 1.0 / (NY + 1), oc.LAMBDA_BRATU
+
+    def padded(self, a):
+        """Interior rows + ghost rows from the neighbours (zero on the physical boundary)."""
+        pad = np.zeros((self.nyl + 2, NX))
+        pad[1:-1] = a
+        reqs = []
+        lo = torch.zeros(NX, dtype=torch.float64)
+        hi = torch.zeros(NX, dtype=torch.float64)
+        if self.rank > 0:  # my first plane -> lower neighbour's upper ghost; its last -> my lower ghost
+            reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(a[0])), self.rank - 1))
+            reqs.append(dist.irecv(lo, self.rank - 1))
+        if self.rank < self.world - 1:
+            reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(a[-1])), self.rank + 1))
+            reqs.append(dist.irecv(hi, self.rank + 1))
+        for r in reqs:
+            r.wait()
+        pad[0], pad[-1] = lo.numpy(), hi.numpy()
+        return pad
+
+    def lap(self, a):
+        p = self.padded(a)
+        c = p[1:-1]
+        e = np.pad(c, ((0, 0), (0, 1)))[:, 1:]
+        w = np.pad(c, ((0, 0), (1, 0)))[:, :-1]
+        return ((e - 2.0 * c) + w) / (self.hx * self.hx) + ((p[2:] - 2.0 * c) + p[:-2]) / (self.hy * self.hy)
+
+    def residual(self, u):
+        return self.lap(u) + self.lam * np.exp(u)
+
+    def jv(self, u, v):
+        return self.lap(v) + self.lam * (np.exp(u) * v)
+
+    def dot(self, x, y):
+        t = torch.tensor([float(np.sum(x * y))], dtype=torch.float64)
+        dist.all_reduce(t)
+        return float(t.item())
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    S = Slab(rank, world)
+    P = oc.bratu2d(NX, NY)
+    U0 = oc.sin_ic(P)
+    u0 = U0[S.y0:S.y0 + S.nyl].copy()
+    v = np.random.default_rng(3).standard_normal((NY, NX))[S.y0:S.y0 + S.nyl]
+    F = S.residual(u0)
+    Jv = S.jv(u0, v)
+    shape = u0.shape
+    A = lambda x: S.jv(u0, x.reshape(shape)).ravel()
+    kw = dict(memory=10, restart=True, atol=0.0, rtol=1e-10, itmax=60, dot=lambda a, b: S.dot(a, b), n=NX * NY)
+    x, st, hist = ar.gmres(A, F.ravel(), **kw)
+    # inexact Newton (src/Ariadne.jl:288-372) on the slabs with EW forcing
+    ew = ar.EisenstatWalker()
+    u = u0.copy()
+    res = S.residual(u)
+    n_res = math.sqrt(S.dot(res, res))
+    tol = 1e-9 * n_res + 1e-12
+    eta, outer, inner = ew.initial(), 0, 0
+    while n_res > tol and outer <= 50:
+        uu = u.copy()
+        d, kst, _ = ar.gmres(lambda z: S.jv(uu, z.reshape(shape)).ravel(), res.ravel(), memory=10, restart=True,
+                             rtol=eta, dot=lambda a, b: S.dot(a, b), n=NX * NY)
+        u = u - d.reshape(shape)
+        prior, res = n_res, S.residual(u)
+        n_res = math.sqrt(S.dot(res, res))
+        eta = ew(eta, tol, n_res, prior)
+        outer, inner = outer + 1, inner + kst.niter
+    parts = [None] * world
+    dist.all_gather_object(parts, dict(y0=S.y0, F=F, Jv=Jv, x=x.reshape(shape), u=u))
+    if rank == 0:
+        parts.sort(key=lambda d: d["y0"])
+        np.savez(out, **{k: np.concatenate([d[k] for d in parts]) for k in ("F", "Jv", "x", "u")},
+                 hist=np.array(hist), niter=st.niter, outer=outer, inner=inner)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_slab_protocol_matches_single_domain(tmp_path, world):
+    out = str(tmp_path / "dist.npz")
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    d = np.load(out)
+    P = oc.bratu2d(NX, NY)
+    U0 = oc.sin_ic(P)
+    v = np.random.default_rng(3).standard_normal((NY, NX))
+    F = oc.residual(P, U0)
+    assert np.max(np.abs(d["F"] - F)) <= 1e-12 * np.max(np.abs(F))
+    assert np.max(np.abs(d["Jv"] - oc.jv_exact(P, U0, v))) <= 1e-12 * np.max(np.abs(d["Jv"]))
+    xo, sto, ho = oc.krylov_solve(P, U0, F, memory=10, restart=True, atol=0.0, rtol=1e-10, itmax=60)
+    assert int(d["niter"]) == sto["niter"]
+    assert np.allclose(d["hist"][:11], ho[:11], rtol=1e-9)
+    assert np.max(np.abs(d["x"] - xo)) <= 1e-7 * np.max(np.abs(xo))
+    uo, so = oc.newton_krylov(P, U0, memory=10, restart=True, tol_rel=1e-9)
+    assert (int(d["outer"]), int(d["inner"])) == (so["outer_iterations"], so["inner_iterations"])
+    assert np.max(np.abs(d["u"] - uo)) <= 1e-9 * np.max(np.abs(uo))

@@ -1,0 +1,88 @@
+"""GPU tests of the distributed (RCCL) path of libnkhip.so.
+
+* one rank with a forced RCCL communicator: every reduction goes through finalize -> ncclAllReduce
+  -> consumer, which must reproduce the single-GPU run bit for bit (same partials, same order);
+* 2 and 3 ranks (slabs of a 2D Bratu grid; on a one-GPU box all ranks share device 0): halo
+  exchange + all-reduced dots against the CPU oracle on the whole grid.
+"""
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import _nkpath  # noqa: F401
+import ariadne_hip as ah
+from oracle import oracle as oc
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def gmres_run(ctx, P, u0, b):
+    g = ah.Grid.full(P.nx, P.ny)
+    u = ah.DeviceArray.from_numpy(u0, g, ctx)
+    bd = ah.DeviceArray.from_numpy(b, g, ctx)
+    res = u.zero()
+    p = (P.hx, P.hy, P.lam)
+    ah.bratu2d_(res, u, p)
+    ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=10))
+    ah.krylov_solve_(ws, ah.JacobianOperator(ah.bratu2d_, res, u, p), bd, restart=True, atol=0.0, rtol=0.0, itmax=40,
+                     history=True)
+    return ws.x.to_numpy(), ws.stats, ah.knorm(len(u), u)
+
+
+def test_forced_rccl_one_rank_is_bitwise(monkeypatch):
+    P = oc.bratu2d(48)
+    u0 = oc.sin_ic(P)
+    b = oc.residual(P, u0)
+    plain = ah.Context(0)
+    x1, s1, n1 = gmres_run(plain, P, u0, b)
+    monkeypatch.setenv("NK_DIST_FORCE", "1")
+    forced = ah.Context(0)
+    forced.init_distributed(0, 1, ah.dist_unique_id())
+    x2, s2, n2 = gmres_run(forced, P, u0, b)
+    assert s1.niter == s2.niter == 40
+    assert s1.residuals == s2.residuals
+    assert np.array_equal(x1, x2) and n1 == n2
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_slabs_match_oracle(tmp_path, world):
+    out = str(tmp_path / "dist")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out]
+    env = dict(os.environ, NK_WORKER_SHARED_DEVICE="1")
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
+    try:
+        log, _ = proc.communicate(timeout=180)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, signal.SIGKILL)
+        pytest.fail("distributed worker timed out")
+    assert proc.returncode == 0, log.decode()[-3000:]
+    meta = json.load(open(out + ".json"))
+    if "skip" in meta:
+        pytest.skip(meta["skip"])
+    d = np.load(out + ".npz")
+    P = oc.bratu2d(48, 40)
+    u0 = oc.sin_ic(P)
+    F = oc.residual(P, u0)
+    assert np.all(np.abs(d["F"] - F) <= 4 * np.finfo(float).eps * P.lam * np.exp(u0) + 2 * np.spacing(np.abs(F)))
+    ref = oc.jv_exact(P, u0, d["v"])
+    assert np.max(np.abs(d["jv"] - ref)) <= 1e-12 * np.max(np.abs(ref))  # halo rows came from the neighbours
+    assert abs(meta["dot"] - float(np.sum(u0 * d["v"]))) <= 1e-12 * np.sqrt(u0.size)
+    uo, so = oc.newton_krylov(P, u0, memory=10, restart=True, tol_rel=1e-9)
+    assert meta["solved"] and so["solved"]
+    assert (meta["outer"], meta["inner"]) == (so["outer_iterations"], so["inner_iterations"])
+    assert np.max(np.abs(d["u"] - uo)) <= 1e-8 * np.max(np.abs(uo))

@@ -19,7 +19,8 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        name = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "").strip()
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+        name = re.sub(r"\(.*", "", name).strip()
         acc[name].append(float(r["Counter_Value"]) * 1024.0)
     return acc
 
