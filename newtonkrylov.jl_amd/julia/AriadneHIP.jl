@@ -1,0 +1,228 @@
+# AriadneHIP.jl -- the reference-side binding of libnkhip.so (include/nkhip.h) for Ariadne.jl.
+#
+# UNTESTED: the build image has no Julia toolchain (SURVEY.md §8c).  This file is the `ccall` shim
+# a maintainer would add so that Ariadne's own `newton_krylov!` (src/Ariadne.jl:288-372) runs its
+# hot path on an MI355X without modification: device vectors (`HipVector`), the Krylov.jl vector
+# primitives (the overload points examples/halovector.jl:51-147 demonstrates), the Jacobian
+# operator `mul!` (src/Ariadne.jl:48-57) and, optionally, the whole device-resident GMRES/CG.
+# The Python host mirror (newtonkrylov.jl_amd/ariadne_hip) binds the same symbols with ctypes and
+# is what the test-suite exercises.
+module AriadneHIP
+
+using Ariadne, Krylov, LinearAlgebra
+import LinearAlgebra: mul!, norm
+import Krylov: kdot, knorm, kscal!, kaxpy!, kaxpby!, kcopy!, kfill!, kdivcopy!, kref!
+
+const libnkhip = joinpath(@__DIR__, "..", "lib", "libnkhip.so")
+
+const NK_BRATU1D, NK_BRATU2D, NK_HEAT2D_EULER, NK_HEAT3D_EULER = Int32(1), Int32(2), Int32(3), Int32(4)
+const NK_JV_EXACT, NK_JV_FD = Int32(0), Int32(1)
+
+check(rc, ctx, what) = rc == 0 || error("$what failed ($rc): " *
+                                        unsafe_string(ccall((:nk_last_error, libnkhip), Cstring, (Ptr{Cvoid},), ctx.ptr)))
+
+# --------------------------------------------------------------------------- context
+mutable struct HipContext
+    ptr::Ptr{Cvoid}
+    function HipContext(device::Integer = 0)
+        r = Ref{Ptr{Cvoid}}(C_NULL)
+        rc = ccall((:nk_ctx_create, libnkhip), Cint, (Cint, Ref{Ptr{Cvoid}}), device, r)
+        rc == 0 || error("nk_ctx_create($device) failed: no usable GPU (there is no CPU fallback)")
+        ctx = new(r[])
+        finalizer(c -> ccall((:nk_ctx_destroy, libnkhip), Cint, (Ptr{Cvoid},), c.ptr), ctx)
+    end
+end
+
+# --------------------------------------------------------------------------- nk_problem (C layout)
+struct NkProblem
+    kind::Int32
+    bc::Int32
+    nx::Int64
+    ny::Int64
+    nz::Int64
+    hx::Float64
+    hy::Float64
+    hz::Float64
+    lambda::Float64
+    a::Float64
+    dt::Float64
+    un::Ptr{Float64}
+end
+geometry(grid::NTuple{3, Int}) = NkProblem(grid[3] > 1 ? NK_HEAT3D_EULER : (grid[2] > 1 ? NK_BRATU2D : NK_BRATU1D),
+                                            0, grid..., 1.0, 1.0, 1.0, 0.0, 0.0, 0.0, Ptr{Float64}(1))
+
+# --------------------------------------------------------------------------- HipVector (device HaloVector)
+"""Grid function in HBM: interior x-fastest (the column-major order of a Julia array), one ghost
+plane on each side of the slowest axis (zero = Dirichlet boundary; filled by the halo exchange
+when distributed).  `length` is the interior count, like HaloVector (halovector.jl:17-26)."""
+mutable struct HipVector <: AbstractVector{Float64}
+    ctx::HipContext
+    ptr::Ptr{Float64}
+    grid::NTuple{3, Int}
+    function HipVector(ctx::HipContext, grid::NTuple{3, Int})
+        r = Ref{Ptr{Float64}}(C_NULL)
+        p = geometry(grid)
+        check(ccall((:nk_vec_alloc, libnkhip), Cint, (Ptr{Cvoid}, Ref{NkProblem}, Ref{Ptr{Float64}}), ctx.ptr, p, r),
+              ctx, "nk_vec_alloc")
+        v = new(ctx, r[], grid)
+        finalizer(x -> ccall((:nk_vec_free, libnkhip), Cint, (Ptr{Cvoid}, Ptr{Float64}), x.ctx.ptr, x.ptr), v)
+    end
+    # non-owning view of library-owned storage (e.g. the Krylov workspace's x)
+    HipVector(ctx::HipContext, ptr::Ptr{Float64}, grid::NTuple{3, Int}) = new(ctx, ptr, grid)
+end
+Base.size(v::HipVector) = (prod(v.grid),)
+Base.similar(v::HipVector) = HipVector(v.ctx, v.grid)          # zero-filled, ghosts included
+Base.zero(v::HipVector) = HipVector(v.ctx, v.grid)
+Base.copy(v::HipVector) = (w = similar(v); kcopy!(length(v), w, v); w)
+Base.getindex(::HipVector, ::Int) = error("scalar indexing of a HipVector; copy it to the host with Array(v)")
+function Base.Array(v::HipVector)
+    a = Array{Float64}(undef, v.grid)
+    check(ccall((:nk_memcpy_d2h, libnkhip), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Int64),
+                v.ctx.ptr, a, v.ptr, length(v)), v.ctx, "nk_memcpy_d2h")
+    return a
+end
+function HipVector(ctx::HipContext, a::AbstractArray{Float64})
+    grid = (size(a, 1), size(a, 2), size(a, 3))
+    v = HipVector(ctx, grid)
+    b = Array(a)
+    check(ccall((:nk_memcpy_h2d, libnkhip), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Int64),
+                ctx.ptr, v.ptr, b, length(b)), ctx, "nk_memcpy_h2d")
+    return v
+end
+
+# `u .-= s .* d` (src/Ariadne.jl:344) -> one axpy kernel
+function Base.Broadcast.materialize!(u::HipVector, bc::Base.Broadcast.Broadcasted)
+    if bc.f === (-) && bc.args[1] === u && bc.args[2] isa Base.Broadcast.Broadcasted && bc.args[2].f === (*)
+        s, d = bc.args[2].args
+        return kaxpy!(length(u), -Float64(s), d::HipVector, u)
+    end
+    error("unsupported broadcast on HipVector: $(bc.f)")
+end
+norm(v::HipVector) = knorm(length(v), v)
+
+# --------------------------------------------------------------------------- Krylov vector primitives
+const VP = Ptr{Cvoid}
+function kdot(n::Integer, x::HipVector, y::HipVector)
+    r = Ref{Float64}()
+    check(ccall((:nk_dot, libnkhip), Cint, (VP, Int64, Ptr{Float64}, Ptr{Float64}, Ref{Float64}), x.ctx.ptr, n, x.ptr, y.ptr, r),
+          x.ctx, "kdot")
+    return r[]
+end
+function knorm(n::Integer, x::HipVector)
+    r = Ref{Float64}()
+    check(ccall((:nk_norm, libnkhip), Cint, (VP, Int64, Ptr{Float64}, Ref{Float64}), x.ctx.ptr, n, x.ptr, r), x.ctx, "knorm")
+    return r[]
+end
+kscal!(n::Integer, s::Float64, x::HipVector) =
+    (check(ccall((:nk_scal, libnkhip), Cint, (VP, Int64, Float64, Ptr{Float64}), x.ctx.ptr, n, s, x.ptr), x.ctx, "kscal!"); x)
+kaxpy!(n::Integer, s::Float64, x::HipVector, y::HipVector) =
+    (check(ccall((:nk_axpy, libnkhip), Cint, (VP, Int64, Float64, Ptr{Float64}, Ptr{Float64}), y.ctx.ptr, n, s, x.ptr, y.ptr),
+           y.ctx, "kaxpy!"); y)
+kaxpby!(n::Integer, s::Float64, x::HipVector, t::Float64, y::HipVector) =
+    (check(ccall((:nk_axpby, libnkhip), Cint, (VP, Int64, Float64, Ptr{Float64}, Float64, Ptr{Float64}),
+                 y.ctx.ptr, n, s, x.ptr, t, y.ptr), y.ctx, "kaxpby!"); y)
+kcopy!(n::Integer, y::HipVector, x::HipVector) =
+    (check(ccall((:nk_copy, libnkhip), Cint, (VP, Int64, Ptr{Float64}, Ptr{Float64}), y.ctx.ptr, n, y.ptr, x.ptr), y.ctx, "kcopy!"); y)
+kfill!(x::HipVector, v::Float64) =
+    (check(ccall((:nk_fill, libnkhip), Cint, (VP, Int64, Ptr{Float64}, Float64), x.ctx.ptr, length(x), x.ptr, v), x.ctx, "kfill!"); x)
+kdivcopy!(n::Integer, y::HipVector, x::HipVector, s::Float64) =
+    (check(ccall((:nk_divcopy, libnkhip), Cint, (VP, Int64, Ptr{Float64}, Ptr{Float64}, Float64), y.ctx.ptr, n, y.ptr, x.ptr, s),
+           y.ctx, "kdivcopy!"); y)
+kref!(n::Integer, x::HipVector, y::HipVector, c::Float64, s::Float64) =
+    (check(ccall((:nk_ref, libnkhip), Cint, (VP, Int64, Ptr{Float64}, Ptr{Float64}, Float64, Float64),
+                 x.ctx.ptr, n, x.ptr, y.ptr, c, s), x.ctx, "kref!"); (x, y))
+
+# --------------------------------------------------------------------------- residuals (F!) and mul!
+"""A residual `F!(res, u, p)` with a hand-written HIP stencil (same `p` tuples as the examples)."""
+struct HipResidual{K}
+    jv::Int32   # NK_JV_EXACT (Enzyme parity, default) or NK_JV_FD (north-star FD operator)
+end
+HipResidual{K}() where {K} = HipResidual{K}(NK_JV_EXACT)
+const bratu! = HipResidual{:bratu1d}()        # examples/bratu.jl:14-24, p = (Δx, λ)
+const bratu2d! = HipResidual{:bratu2d}()      # p = (Δx, Δy, λ)
+const heat2d_euler! = HipResidual{:heat2d}()  # G_Euler! ∘ diffusion!, p = (uₙ, Δt, du, (a, Δx, Δy, bc!), t)
+
+problem(::HipResidual{:bratu1d}, u::HipVector, (dx, λ)) = NkProblem(NK_BRATU1D, 0, u.grid..., dx, 1, 1, λ, 0, 0, C_NULL)
+problem(::HipResidual{:bratu2d}, u::HipVector, (dx, dy, λ)) = NkProblem(NK_BRATU2D, 0, u.grid..., dx, dy, 1, λ, 0, 0, C_NULL)
+problem(::HipResidual{:heat2d}, u::HipVector, (un, Δt, _, (a, dx, dy, _bc), _t)) =
+    NkProblem(NK_HEAT2D_EULER, 0, u.grid..., dx, dy, 1, 0, a, Δt, un.ptr)
+
+function (F::HipResidual)(res::HipVector, u::HipVector, p)
+    check(ccall((:nk_residual, libnkhip), Cint, (VP, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}),
+                u.ctx.ptr, problem(F, u, p), res.ptr, u.ptr), u.ctx, "F!")
+    return nothing
+end
+
+# mul!(out, J, v): more specific than Ariadne's Enzyme method (src/Ariadne.jl:48) by dispatch
+function mul!(out::HipVector, J::Ariadne.JacobianOperator{<:HipResidual, <:HipVector}, v::HipVector)
+    F0 = J.f.jv == NK_JV_FD ? J.res.ptr : Ptr{Float64}(C_NULL)
+    check(ccall((:nk_jv, libnkhip), Cint, (VP, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int32, Float64),
+                out.ctx.ptr, problem(J.f, J.u, J.p), out.ptr, J.u.ptr, v.ptr, F0, J.f.jv, 0.0), out.ctx, "mul!")
+    return nothing
+end
+
+# --------------------------------------------------------------------------- optional: device-resident Krylov solve
+# With only the definitions above, Krylov.jl's own gmres! runs on HipVectors: one ccall per
+# primitive, a host sync per kdot/knorm.  The workspace below moves the whole Arnoldi loop into
+# libnkhip.so (fused MGS passes, one sync per Arnoldi step); Ariadne reaches it through
+# `krylov_workspace(algo, KrylovConstructor(res))` and `krylov_solve!` unchanged.
+mutable struct HipStats      # Ariadne reads workspace.stats.niter (src/Ariadne.jl:363,367)
+    niter::Int
+    solved::Bool
+end
+
+mutable struct HipKrylovWorkspace
+    ptr::Ptr{Cvoid}
+    ctx::HipContext
+    x::HipVector
+    stats::HipStats
+end
+
+struct NkKrylovOpts
+    restart::Int32
+    reorthogonalization::Int32
+    itmax::Int32
+    jv_mode::Int32
+    atol::Float64
+    rtol::Float64
+end
+struct NkKrylovStats
+    niter::Int64
+    solved::Int32
+    inconsistent::Int32
+    breakdown::Int32
+    status::Int32
+    n_matvec::Int64
+end
+
+function Krylov.krylov_workspace(method::Symbol, kc::KrylovConstructor{<:HipVector}; memory::Integer = 20)
+    algo = method === :gmres ? Int32(0) : method === :cg ? Int32(1) :
+           error("HIP path implements :gmres and :cg")
+    res = kc.vm
+    r = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:nk_workspace_create, libnkhip), Cint, (VP, Int32, Ref{NkProblem}, Int32, Ref{Ptr{Cvoid}}),
+                res.ctx.ptr, algo, geometry(res.grid), memory, r), res.ctx, "krylov_workspace")
+    xptr = ccall((:nk_workspace_x, libnkhip), Ptr{Float64}, (Ptr{Cvoid},), r[])
+    x = HipVector(res.ctx, xptr, res.grid)  # non-owning view (defined below)
+    ws = HipKrylovWorkspace(r[], res.ctx, x, HipStats(0, false))
+    finalizer(w -> ccall((:nk_workspace_destroy, libnkhip), Cint, (Ptr{Cvoid},), w.ptr), ws)
+    return ws
+end
+
+function Krylov.krylov_solve!(ws::HipKrylovWorkspace, J::Ariadne.JacobianOperator{<:HipResidual, <:HipVector}, b::HipVector;
+                              restart::Bool = false, reorthogonalization::Bool = false, itmax::Integer = 0,
+                              atol::Real = sqrt(eps(Float64)), rtol::Real = sqrt(eps(Float64)), kwargs...)
+    opts = NkKrylovOpts(restart, reorthogonalization, itmax, J.f.jv, atol, rtol)
+    st = Ref{NkKrylovStats}()
+    hl = Ref{Int64}(0)
+    F0 = J.f.jv == NK_JV_FD ? J.res.ptr : Ptr{Float64}(C_NULL)
+    check(ccall((:nk_krylov_solve, libnkhip), Cint,
+                (Ptr{Cvoid}, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ref{NkKrylovOpts}, Ref{NkKrylovStats},
+                 Ptr{Float64}, Int64, Ref{Int64}),
+                ws.ptr, problem(J.f, J.u, J.p), J.u.ptr, F0, b.ptr, opts, st, C_NULL, 0, hl), ws.ctx, "krylov_solve!")
+    ws.stats.niter = st[].niter
+    ws.stats.solved = st[].solved != 0
+    return ws
+end
+
+end # module
