@@ -34,7 +34,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 ROOT = os.path.dirname(os.path.abspath(__file__))
 # bench kernel class -> rocprofv3 kernel name prefix (for the PMC traffic of profiles/*/pmc_traffic.json)
 PMC_NAME = {"mgs_pass": "nk::k_mgs_pass<true,", "mgs_pass_last": "nk::k_mgs_pass<false,",
-            "jv_fd_dot": "nk::k_st2d<2, 2, 2,", "jv_exact_dot": "nk::k_st2d<2, 1, 2,", "divcopy": "nk::k_divcopy"}
+            "jv_fd_dot_norm": "nk::k_st2d<2, 2, 2,", "jv_exact_dot_norm": "nk::k_st2d<2, 1, 2,",
+            "divcopy": "nk::k_divcopy"}
 LAMBDA = 3.51382       # examples/bratu.jl:41
 
 
@@ -179,7 +180,7 @@ def main():
                 "timed_launches": v["timed"]}
 
     dominant = next(iter(kernels), None)
-    jv_kernel = "jv_fd_dot" if args.jv == "fd" else "jv_exact_dot"
+    jv_kernel = "jv_fd_dot_norm" if args.jv == "fd" else "jv_exact_dot_norm"  # Jv fused with V_k = q / h
 
     if rank == 0:
         value = matvecs * world / elapsed

@@ -135,6 +135,8 @@ struct StencilIn {
     const double* F0;
     const double* aux; // EPI_DOT: dot partner; EPI_RESID: b (out = b - J v)
     double eps;
+    const double* vdiv = nullptr;  // device scalar h: the operator is applied to v / h ...
+    double* vout = nullptr;        // ... and v / h is stored here (fused kdivcopy!)
 };
 // returns the partial sums (when epi != EPI_NONE) in *red
 int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red);

@@ -75,7 +75,17 @@ struct KArgs {
     int tiles_x, tiles_y, rows;
     int fast;            // 1: multiply by reciprocals instead of dividing (measurement variant, not bit-faithful)
     double ihx2, ihy2, ihz2, ieps;
+    // fused Arnoldi normalisation: the stencil input is v = src / *vdiv (kdivcopy!, bit-identical),
+    // and the block's own points of v are stored to vout (V_k) -- saves the separate divcopy pass
+    const double* vdiv;
+    double* vout;
+    double hd;           // *vdiv, loaded once per block
 };
+
+__device__ __forceinline__ double vin(const KArgs& A, int64_t o) {
+    const double v = A.v[o];
+    return A.vdiv ? v / A.hd : v;
+}
 
 // ((p - 2c) + m) / h^2 exactly as the reference writes it; `fast` multiplies by 1/h^2 instead
 __device__ __forceinline__ double lapk(const KArgs& A, double c, double p, double m, double h2, double ih2) {
@@ -86,8 +96,8 @@ __device__ __forceinline__ double lapk(const KArgs& A, double c, double p, doubl
 template <int MODE>
 __device__ __forceinline__ double fieldval(const KArgs& A, int64_t o) {
     if (MODE == MODE_RES) return A.u[o];
-    if (MODE == MODE_JEXACT) return A.v[o];
-    return A.u[o] + A.eps * A.v[o];  // w = u + eps v
+    if (MODE == MODE_JEXACT) return vin(A, o);
+    return A.u[o] + A.eps * vin(A, o);  // w = u + eps v
 }
 
 template <int MODE, int VEC>
@@ -157,8 +167,10 @@ __device__ __forceinline__ double epilogue(double& val, double ax, double acc) {
 
 // ------------------------------------------------------------------------------ 1D stencil
 template <int MODE, int EPI>
-__global__ __launch_bounds__(kBlock) void k_st1d(KArgs A) {
+__global__ __launch_bounds__(kBlock) void k_st1d(KArgs A0) {
     __shared__ double sh[8];
+    KArgs A = A0;
+    A.hd = A.vdiv ? *A.vdiv : 1.0;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     double acc = 0.0;
     if (i < A.nx) {
@@ -170,6 +182,7 @@ __global__ __launch_bounds__(kBlock) void k_st1d(KArgs A) {
         const double ax = (EPI == EPI_DOT || EPI == EPI_RESID) ? A.aux[i] : 0.0;
         acc = epilogue<EPI>(val, ax, acc);
         A.out[i] = val;
+        if (MODE != MODE_RES && A.vout) A.vout[i] = A.v[i] / A.hd;
     }
     if (EPI != EPI_NONE) {
         const double s = block_sum(acc, sh);
@@ -195,11 +208,13 @@ __device__ __forceinline__ Row<VEC> field_row(const KArgs& A, int64_t o, bool ok
                     const double2 q = *reinterpret_cast<const double2*>(A.u + o + h);
                     r.v[h] = q.x; r.v[h + 1] = q.y;
                 } else if constexpr (MODE == MODE_JEXACT) {
-                    const double2 q = *reinterpret_cast<const double2*>(A.v + o + h);
+                    double2 q = *reinterpret_cast<const double2*>(A.v + o + h);
+                    if (A.vdiv) { q.x = q.x / A.hd; q.y = q.y / A.hd; }
                     r.v[h] = q.x; r.v[h + 1] = q.y;
                 } else {
                     const double2 qu = *reinterpret_cast<const double2*>(A.u + o + h);
-                    const double2 qv = *reinterpret_cast<const double2*>(A.v + o + h);
+                    double2 qv = *reinterpret_cast<const double2*>(A.v + o + h);
+                    if (A.vdiv) { qv.x = qv.x / A.hd; qv.y = qv.y / A.hd; }
                     r.v[h] = qu.x + A.eps * qv.x;  // w = u + eps v
                     r.v[h + 1] = qu.y + A.eps * qv.y;
                 }
@@ -244,13 +259,24 @@ __device__ __forceinline__ void store_row(double* __restrict__ p, int64_t o, con
     }
 }
 
+// store the normalised basis vector of this row segment (fused kdivcopy!)
+template <int VEC>
+__device__ __forceinline__ void store_vout(const KArgs& A, int64_t o) {
+    Row<VEC> v = data_row<VEC>(A.v, o, true);  // re-read: an L1/L2 hit (this row was streamed in)
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) v.v[k] = v.v[k] / A.hd;
+    store_row<VEC>(A.vout, o, v);
+}
+
 // ------------------------------------------------------------------------------ 2D stencil
 // Block = 256 threads x VEC columns (one row segment), marching A.rows rows in y.  Software
 // pipeline: while row j is computed, the stencil field of row j+2 and the centre operands of
 // row j+1 are in flight, so no iteration waits on a load it issued itself.
 template <int KIND, int MODE, int EPI, int VEC>
-__global__ __launch_bounds__(kBlock) void k_st2d(KArgs A) {
+__global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     __shared__ double sh[8];
+    KArgs A = A0;
+    A.hd = A.vdiv ? *A.vdiv : 1.0;
     const int lane = threadIdx.x & 63;
     const int nb = gridDim.x, b = blockIdx.x;
     const int t = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;  // XCD-contiguous tile bands
@@ -318,6 +344,9 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A) {
                     val.v[k] = r;
                 }
                 store_row<VEC>(A.out, o, val);
+                if constexpr (MODE != MODE_RES) {
+                    if (A.vout) store_vout<VEC>(A, o);
+                }
             }
             fm = fc;
             fc = fp;
@@ -341,8 +370,10 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A) {
 // ------------------------------------------------------------------------------ 3D stencil
 // Block = 4 waves = 4 rows (y) x 64*VEC columns, marching A.rows planes in z.
 template <int KIND, int MODE, int EPI, int VEC>
-__global__ __launch_bounds__(kBlock) void k_st3d(KArgs A) {
+__global__ __launch_bounds__(kBlock) void k_st3d(KArgs A0) {
     __shared__ double sh[8];
+    KArgs A = A0;
+    A.hd = A.vdiv ? *A.vdiv : 1.0;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const int nb = gridDim.x, b = blockIdx.x;
@@ -396,6 +427,9 @@ __global__ __launch_bounds__(kBlock) void k_st3d(KArgs A) {
                     val.v[q] = r;
                 }
                 store_row<VEC>(A.out, o, val);
+                if constexpr (MODE != MODE_RES) {
+                    if (A.vout) store_vout<VEC>(A, o);
+                }
             }
             fm = fc;
             fc = fp;
@@ -550,7 +584,7 @@ __device__ __forceinline__ void st2(dx2* p, dx2 v) {
 
 // rev = 1 sweeps the vectors from the end: consecutive passes alternate direction so each pass
 // starts on the lines the previous pass touched last (still in the 256 MB Infinity Cache).
-template <bool HAS_NEXT, int U, bool NT>
+template <bool HAS_NEXT, int U, bool NT, bool NTW = false>
 __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restrict__ q, const double* __restrict__ vi,
                                                     const double* __restrict__ vnext, const double* __restrict__ red_in,
                                                     int red_len, double* __restrict__ h_out, double* __restrict__ part,
@@ -573,7 +607,7 @@ __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restri
             const int64_t e = base + sgn * (i + u * st);
             a[u] = ld2<false>(q2 + e);
             bv[u] = ld2<NT>(v2 + e);
-            if constexpr (HAS_NEXT) cv[u] = ld2<false>(w2 + e);
+            if constexpr (HAS_NEXT) cv[u] = ld2<NTW>(w2 + e);
         }
     }
     const double h = reduce_input(red_in, red_len, sh);
@@ -587,7 +621,7 @@ __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restri
                 const int64_t e = base + sgn * (i + u * st);
                 a[u] = ld2<false>(q2 + e);
                 bv[u] = ld2<NT>(v2 + e);
-                if constexpr (HAS_NEXT) cv[u] = ld2<false>(w2 + e);
+                if constexpr (HAS_NEXT) cv[u] = ld2<NTW>(w2 + e);
             }
         }
 #pragma unroll
@@ -612,7 +646,7 @@ __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restri
         a.y = fma(mh, b.y, a.y);
         q2[e] = a;
         if constexpr (HAS_NEXT) {
-            const dx2 c = w2[e];
+            const dx2 c = ld2<NTW>(w2 + e);
             acc = fma(c.x, a.x, acc);
             acc = fma(c.y, a.y, acc);
         } else {
@@ -781,6 +815,8 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     A.hx2 = p->hx * p->hx; A.hy2 = p->hy * p->hy; A.hz2 = p->hz * p->hz;
     A.lam = p->lambda; A.a = p->a; A.dt = p->dt; A.eps = in.eps;
     A.fast = fast;
+    A.vdiv = in.vdiv;
+    A.vout = in.vout;
     A.ihx2 = 1.0 / A.hx2; A.ihy2 = 1.0 / A.hy2; A.ihz2 = 1.0 / A.hz2; A.ieps = in.eps != 0.0 ? 1.0 / in.eps : 0.0;
     int vec = 1, grid = 1;
     if (g.dim == 1) {
@@ -825,14 +861,17 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     else if (in.mode == MODE_JEXACT) words += 1 + (heat ? 0 : 1);
     else words += 3 + (heat ? 1 : 0);
     if (in.epi == EPI_DOT || in.epi == EPI_RESID) words += 1;
+    if (in.vout) words += 1;  // fused kdivcopy!: V_k is written
     const double bytes = 8.0 * words * (double)g.n;
     static const char* names[3][4] = {
         {"residual", "residual_norm", "residual_dot", "residual_resid"},
         {"jv_exact", "jv_exact_sumsq", "jv_exact_dot", "jv_exact_resid"},
         {"jv_fd", "jv_fd_sumsq", "jv_fd_dot", "jv_fd_resid"}};
+    static const char* fused_names[3] = {"residual", "jv_exact_dot_norm", "jv_fd_dot_norm"};
     const int kind = p->kind, mode = in.mode, epi = in.epi;
     hipStream_t s = c->stream;
-    return launch(c, names[mode][epi], bytes, [&] {
+    const char* kname = (in.vout && epi == EPI_DOT) ? fused_names[mode] : names[mode][epi];
+    return launch(c, kname, bytes, [&] {
         switch (kind) {
         case NK_BRATU1D: go_stencil_mode<NK_BRATU1D>(A, mode, epi, vec, grid, s); break;
         case NK_BRATU2D: go_stencil_mode<NK_BRATU2D>(A, mode, epi, vec, grid, s); break;
@@ -888,8 +927,8 @@ void mgs_dispatch(int variant, int g, hipStream_t s, int64_t n, double* q, const
     case 0: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, false>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
     case 1: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
     case 2: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
-    case 3: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 8, false>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
-    default: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 8, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
+    case 3: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
+    default: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
     }
 }
 }  // namespace
@@ -969,9 +1008,9 @@ extern "C" int nkb_mgs_seq(nk_ctx* c, int64_t n, int k, int variant, int alt, in
     using namespace nk;
     if (!c || n < 2 || k < 1 || reps < 1 || !us_out) return NK_E_ARG;
     std::vector<double*> V(k + 2, nullptr);
-    for (auto& p : V) {
-        NK_HIP(c, hipMalloc(&p, sizeof(double) * n));
-        NK_HIP(c, hipMemsetAsync(p, 0, sizeof(double) * n, c->stream));
+    for (size_t v = 0; v < V.size(); ++v) {  // non-zero data (zero-filled streams flatter HBM/DVFS)
+        NK_HIP(c, hipMalloc(&V[v], sizeof(double) * n));
+        NK_TRY(launch_fill(c, n, V[v], 0.37 + 0.01 * (double)v));
     }
     double* q = V[k + 1];
     const int g = red_blocks(n);

@@ -19,6 +19,7 @@
 
 #include <cfloat>
 #include <cmath>
+#include <cstring>
 #include <vector>
 
 #include "nk_internal.hpp"
@@ -30,35 +31,51 @@ struct nk_workspace {
     int mem = 20;
     int64_t n = 0;
     double* x = nullptr;
-    double* w = nullptr;   // gmres: q (= w); cg: Ap
+    double* w = nullptr;   // gmres: q (= w) of odd steps / restart residual; cg: Ap
+    double* w2 = nullptr;  // gmres: q of even steps (the fused Jv reads q_{k-1} while writing q_k)
     double* xr = nullptr;  // gmres restart: Δx (chunked x update);  cg: r
     double* p = nullptr;   // cg: search direction
     std::vector<double*> V;
-    double* hdev = nullptr;  // device Hessenberg column (2*cap + 2 doubles)
+    double* hdev = nullptr;  // device Hessenberg columns: 2 slots of (2*cap + 2) doubles (steps k, k+1 in flight)
     double* ydev = nullptr;  // device y (cap doubles)
-    double* hpin = nullptr;  // pinned host mirror of hdev
+    double* hpin = nullptr;  // pinned host mirror of hdev (2 slots)
     double* ypin = nullptr;  // pinned host y
+    hipEvent_t col_ready[2] = {nullptr, nullptr};  // Hessenberg column of slot s has landed in hpin
     int cap = 0;             // capacity of hdev / ydev / pinned buffers (in basis vectors)
 };
 
 namespace nk {
 namespace {
 
+// Grow the Hessenberg/y buffers to hold `need` basis vectors.  Contents are preserved: with the
+// one-step-ahead pipeline a column may still be waiting to be read when the basis grows.
 int ws_scalars(nk_workspace* ws, int need) {
     if (need <= ws->cap) return NK_OK;
     nk_ctx* c = ws->c;
     int cap = ws->cap ? ws->cap : 64;
     while (cap < need) cap *= 2;
     NK_HIP(c, hipStreamSynchronize(c->stream));
-    if (ws->hdev) (void)hipFree(ws->hdev);
-    if (ws->ydev) (void)hipFree(ws->ydev);
-    if (ws->hpin) (void)hipHostFree(ws->hpin);
-    if (ws->ypin) (void)hipHostFree(ws->ypin);
-    ws->hdev = ws->ydev = ws->hpin = ws->ypin = nullptr;
-    NK_HIP(c, hipMalloc(&ws->hdev, sizeof(double) * (2 * (size_t)cap + 2)));
-    NK_HIP(c, hipMalloc(&ws->ydev, sizeof(double) * (size_t)cap));
-    NK_HIP(c, hipHostMalloc(&ws->hpin, sizeof(double) * (2 * (size_t)cap + 2), hipHostMallocDefault));
-    NK_HIP(c, hipHostMalloc(&ws->ypin, sizeof(double) * (size_t)cap, hipHostMallocDefault));
+    const size_t ostride = 2 * (size_t)ws->cap + 2, nstride = 2 * (size_t)cap + 2;
+    double *hdev = nullptr, *ydev = nullptr, *hpin = nullptr, *ypin = nullptr;
+    NK_HIP(c, hipMalloc(&hdev, sizeof(double) * 2 * nstride));
+    NK_HIP(c, hipMalloc(&ydev, sizeof(double) * (size_t)cap));
+    NK_HIP(c, hipHostMalloc(&hpin, sizeof(double) * 2 * nstride, hipHostMallocDefault));
+    NK_HIP(c, hipHostMalloc(&ypin, sizeof(double) * (size_t)cap, hipHostMallocDefault));
+    if (ws->cap) {
+        for (int slot = 0; slot < 2; ++slot) {
+            NK_HIP(c, hipMemcpy(hdev + slot * nstride, ws->hdev + slot * ostride, sizeof(double) * ostride,
+                                hipMemcpyDeviceToDevice));
+            std::memcpy(hpin + slot * nstride, ws->hpin + slot * ostride, sizeof(double) * ostride);
+        }
+        (void)hipFree(ws->hdev);
+        (void)hipFree(ws->ydev);
+        (void)hipHostFree(ws->hpin);
+        (void)hipHostFree(ws->ypin);
+    }
+    ws->hdev = hdev;
+    ws->ydev = ydev;
+    ws->hpin = hpin;
+    ws->ypin = ypin;
     ws->cap = cap;
     return NK_OK;
 }
@@ -73,6 +90,12 @@ int ws_basis(nk_workspace* ws, int need) {
 }
 
 inline double sgn(double x) { return (double)((x > 0) - (x < 0)); }
+
+// NK_MGS_ALT=1: alternate the sweep direction of consecutive MGS passes (see k_mgs_pass)
+const int mgs_alt = [] {
+    const char* e = getenv("NK_MGS_ALT");
+    return (e && *e) ? atoi(e) : 0;
+}();
 
 // Krylov.jl sym_givens (real case)
 void sym_givens(double a, double b, double* c, double* s, double* rho) {
@@ -118,7 +141,9 @@ struct Op {
     int64_t n_matvec = 0;
 
     // out = J v  (+ epilogue).  vnorm: ||v|| for the FD step (1 for Arnoldi basis vectors).
-    int apply(double* out, const double* v, double vnorm, int epi, const double* aux, Red* red) {
+    // With vdiv/vout the operator is applied to v / *vdiv, which is also stored to vout.
+    int apply(double* out, const double* v, double vnorm, int epi, const double* aux, Red* red,
+              const double* vdiv = nullptr, double* vout = nullptr) {
         ++n_matvec;
         double eps = 0.0;
         if (mode == NK_JV_FD) {
@@ -134,7 +159,7 @@ struct Op {
             eps = std::sqrt(DBL_EPSILON) * std::fmax(1.0, unorm) / vnorm;
         }
         NK_TRY(halo_exchange(c, p, v));
-        StencilIn in{p, mode == NK_JV_FD ? MODE_JFD : MODE_JEXACT, epi, out, u, v, F0, aux, eps};
+        StencilIn in{p, mode == NK_JV_FD ? MODE_JFD : MODE_JEXACT, epi, out, u, v, F0, aux, eps, vdiv, vout};
         return launch_stencil(c, in, red);
     }
     int64_t ws_n() const { return p->nx * p->ny * p->nz; }
@@ -155,7 +180,7 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
     int64_t itmax = o->itmax;
     int64_t nh = 0;
     double* x = ws->x;
-    double* w = ws->w;
+    double* W[2] = {ws->w, ws->w2};  // q_k lives in W[k & 1]
 
     // host Krylov state (same layout as Krylov.jl: R column-packed)
     int hcap = mem;
@@ -180,19 +205,50 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         if (hist_len) *hist_len = nh;
         return NK_OK;
     }
+    if (itmax == 0) itmax = 2 * n;
+    const double btol = std::pow(DBL_EPSILON, 0.75);
+
+    // Issue Arnoldi step k (kernels + async copy of its Hessenberg column) without waiting.
+    // Step 1 applies J to the materialised V_1; step k >= 2 applies J to q_{k-1} / h_{k,k-1},
+    // reading h from the device and storing V_k on the way (fused kdivcopy!).
+    auto slot_dev = [&](int k) { return ws->hdev + (size_t)(k & 1) * (2 * ws->cap + 2); };
+    auto slot_pin = [&](int k) { return ws->hpin + (size_t)(k & 1) * (2 * ws->cap + 2); };
+    auto npasses_of = [&](int k) { return reorth ? 2 * k : k; };
+    auto issue = [&](int k) -> int {
+        NK_TRY(ws_basis(ws, k));
+        NK_TRY(ws_scalars(ws, k + 1));
+        const int np = npasses_of(k);
+        double* col = slot_dev(k);
+        double* q = W[k & 1];
+        Red red{};
+        if (k == 1) {
+            NK_TRY(A.apply(q, ws->V[0], 1.0, EPI_DOT, ws->V[0], &red));
+        } else {
+            const double* hprev = slot_dev(k - 1) + npasses_of(k - 1);
+            NK_TRY(A.apply(q, W[(k - 1) & 1], 1.0, EPI_DOT, ws->V[0], &red, hprev, ws->V[k - 1]));
+        }
+        for (int t = 0; t < np; ++t) {
+            const double* vi = ws->V[t % k];
+            const double* vnext = (t + 1 < np) ? ws->V[(t + 1) % k] : nullptr;
+            NK_TRY(finish_reduction(c, &red));
+            Red nxt{};
+            NK_TRY(launch_mgs_pass(c, n, q, vi, vnext, red, col + t, &nxt, mgs_alt ? (t & 1) : 0));
+            red = nxt;
+        }
+        NK_TRY(finish_reduction(c, &red));
+        NK_TRY(launch_finalize(c, red, col + np, 1));  // h_{k+1,k} = ||q||
+        NK_HIP(c, hipMemcpyAsync(slot_pin(k), col, sizeof(double) * (np + 1), hipMemcpyDeviceToHost, c->stream));
+        NK_HIP(c, hipEventRecord(ws->col_ready[k & 1], c->stream));
+        return NK_OK;
+    };
+
     int npass = 0;
     int64_t iter = 0, inner_iter = 0;
-    if (itmax == 0) itmax = 2 * n;
     int64_t inner_itmax = itmax;
-    const double btol = std::pow(DBL_EPSILON, 0.75);
     bool breakdown = false, inconsistent = false;
     bool solved = rNorm <= eps_;
     bool tired = iter >= itmax;
     double xnorm = 0.0;  // ||x|| for the FD restart residual (from the fused x update)
-    static const int mgs_alt = [] {
-        const char* e = getenv("NK_MGS_ALT");
-        return (e && *e) ? atoi(e) : 0;  // alternating sweeps: no gain once V_i is loaded non-temporally
-    }();
     while (!(solved || tired || breakdown)) {
         int64_t nr = 0;
         std::fill(cs.begin(), cs.end(), 0.0);
@@ -202,15 +258,16 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         const double* src = b;
         if (restart && npass >= 1) {
             Red rr{};
-            NK_TRY(A.apply(w, x, xnorm, EPI_RESID, b, &rr));  // w = b - A x, fused ||w||^2 partials
+            NK_TRY(A.apply(W[0], x, xnorm, EPI_RESID, b, &rr));  // w = b - A x, fused ||w||^2 partials
             NK_TRY(host_scalar(c, rr, 1, &beta));
-            src = w;
+            src = W[0];
         }
         z[0] = beta;
         NK_TRY(launch_divcopy(c, n, ws->V[0], src, beta));  // V1 = r0 / beta
         npass++;
         inner_iter = 0;
         bool inner_tired = false;
+        NK_TRY(issue(1));
         while (!(solved || inner_tired || breakdown)) {
             inner_iter++;
             const int k = (int)inner_iter;
@@ -222,28 +279,18 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
                 R.resize((size_t)nc * (nc + 1) / 2, 0.0);
                 hcap = nc;
             }
-            const int npasses = reorth ? 2 * k : k;
-            NK_TRY(ws_scalars(ws, npasses + 1));
-            // q = A V_k, fused with the partials of <V_1, q>
-            Red red{};
-            NK_TRY(A.apply(w, ws->V[k - 1], 1.0, EPI_DOT, ws->V[0], &red));
-            for (int t = 0; t < npasses; ++t) {
-                const double* vi = ws->V[t % k];
-                const double* vnext = (t + 1 < npasses) ? ws->V[(t + 1) % k] : nullptr;
-                NK_TRY(finish_reduction(c, &red));
-                Red nxt{};
-                NK_TRY(launch_mgs_pass(c, n, w, vi, vnext, red, ws->hdev + t, &nxt, mgs_alt ? (t & 1) : 0));
-                red = nxt;
-            }
-            NK_TRY(finish_reduction(c, &red));
-            NK_TRY(launch_finalize(c, red, ws->hdev + npasses, 1));  // h_{k+1,k} = ||q||
-            NK_HIP(c, hipMemcpyAsync(ws->hpin, ws->hdev, sizeof(double) * (npasses + 1), hipMemcpyDeviceToHost, c->stream));
-            NK_HIP(c, hipStreamSynchronize(c->stream));
+            // speculate: step k+1 unless the cycle certainly ends at k (its kernels only write
+            // V_{k+1}, q_{k+1} and slot (k+1)&1, none of which is read if the cycle stops here)
+            const bool last = restart ? (inner_iter >= std::min<int64_t>(mem, inner_itmax)) : (inner_iter >= inner_itmax);
+            if (!last) NK_TRY(issue(k + 1));
+            NK_HIP(c, hipEventSynchronize(ws->col_ready[k & 1]));
             if (c->prof) prof_drain(c, false);
-            for (int i = 0; i < k; ++i) R[nr + i] = ws->hpin[i];
+            const double* hcol = slot_pin(k);
+            const int np = npasses_of(k);
+            for (int i = 0; i < k; ++i) R[nr + i] = hcol[i];
             if (reorth)
-                for (int i = 0; i < k; ++i) R[nr + i] += ws->hpin[k + i];
-            const double Hbis = ws->hpin[npasses];
+                for (int i = 0; i < k; ++i) R[nr + i] += hcol[k + i];
+            const double Hbis = hcol[np];
             for (int i = 1; i <= k - 1; ++i) {
                 const double Rtmp = cs[i - 1] * R[nr + i - 1] + sn[i - 1] * R[nr + i];
                 R[nr + i] = sn[i - 1] * R[nr + i - 1] - cs[i - 1] * R[nr + i];
@@ -258,12 +305,9 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
             const bool mach = (rNorm + 1.0 <= 1.0);
             solved = (rNorm <= eps_) || mach;
             breakdown = Hbis <= btol;
-            inner_tired = restart ? (inner_iter >= std::min<int64_t>(mem, inner_itmax)) : (inner_iter >= inner_itmax);
-            if (!(solved || inner_tired || breakdown)) {
-                NK_TRY(ws_basis(ws, k + 1));
-                NK_TRY(launch_divcopy(c, n, ws->V[k], w, Hbis));  // V_{k+1} = q / h_{k+1,k}
-                z[k] = zeta;
-            }
+            inner_tired = last;
+            if (!(solved || inner_tired || breakdown)) z[k] = zeta;  // V_{k+1} = q/h was stored by step k+1
+            else if (!last) A.n_matvec -= 1;  // the speculative step k+1 is discarded: not a mul!(J) of the solve
         }
         // back substitution R y = z (Krylov.jl, y stored in z)
         const int kk = (int)inner_iter;
@@ -397,7 +441,11 @@ int nk_workspace_create(nk_ctx* c, int32_t algo, const nk_problem* p, int32_t me
     ws->n = g.n;
     int rc = NK_OK;
     if ((rc = nk_vec_alloc(c, &ws->prob, &ws->x)) != NK_OK || (rc = nk_vec_alloc(c, &ws->prob, &ws->w)) != NK_OK ||
-        (rc = nk_vec_alloc(c, &ws->prob, &ws->xr)) != NK_OK) {
+        (rc = nk_vec_alloc(c, &ws->prob, &ws->xr)) != NK_OK ||
+        (algo == NK_ALGO_GMRES && (rc = nk_vec_alloc(c, &ws->prob, &ws->w2)) != NK_OK) ||
+        hipEventCreateWithFlags(&ws->col_ready[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ws->col_ready[1], hipEventDisableTiming) != hipSuccess) {
+        if (rc == NK_OK) rc = fail(c, NK_E_HIP, "hipEventCreate failed");
         nk_workspace_destroy(ws);
         return rc;
     }
@@ -420,8 +468,10 @@ int nk_workspace_destroy(nk_workspace* ws) {
     if (!ws) return NK_OK;
     nk_ctx* c = ws->c;
     for (double* v : ws->V) nk_vec_free(c, v);
-    for (double* v : {ws->x, ws->w, ws->xr, ws->p})
+    for (double* v : {ws->x, ws->w, ws->w2, ws->xr, ws->p})
         if (v) nk_vec_free(c, v);
+    for (hipEvent_t e : ws->col_ready)
+        if (e) (void)hipEventDestroy(e);
     if (ws->hdev) (void)hipFree(ws->hdev);
     if (ws->ydev) (void)hipFree(ws->ydev);
     if (ws->hpin) (void)hipHostFree(ws->hpin);

@@ -29,10 +29,10 @@ lib.nkb_stencil.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_int, 
 n = args.n
 side = int(round(n ** 0.5))
 
-MGS = {0: "U2", 1: "U2+nt(V_i)", 2: "U4+nt(V_i)", 3: "U8", 4: "U8+nt(V_i)"}
+MGS = {0: "U2", 1: "U2+nt(V_i)", 2: "U4+nt(V_i)", 3: "U2+nt(V_i,V_i+1)", 4: "U4+nt(V_i,V_i+1)"}
 configs = [("copy", None, None, None)]
 if "mgs" in args.what:
-    configs += [("mgs", v, 0, k) for k in (16, 30) for v in MGS]
+    configs += [("mgs", v, 0, k) for k in (8, 16, 30) for v in MGS]
 ST = {(2, 2): ("jv_fd_dot", 40.0), (1, 2): ("jv_exact_dot", 32.0), (0, 1): ("residual_norm", 16.0)}
 if "stencil" in args.what:
     configs += [("st", mode_epi, rows, fast) for mode_epi in ST for rows in (8, 16, 32) for fast in (0, 2, 4, 6)]
