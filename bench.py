@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Krylov matvecs/s + achieved HBM GB/s, 2D Bratu 4096^2, GMRES(30) -- BASELINE.json config 2.
 
+(--workload heat2d / heat3d runs BASELINE configs 3 / 5 instead: implicit-Euler time steps of the
+2D heat equation at 8192^2 / the 3D heat equation at 512^3, one time step per step.)
+
 One *step* = one inexact-Newton step of newton_krylov_ on the 2D Bratu problem (BASELINE.json
 configs[1]): F!(res,u) + ||F|| (fused), one device GMRES(30) solve with the fixed Krylov budget
 krylov_kwargs = (restart=true, rtol=0, atol=0, itmax=300) -> 300 Arnoldi matvecs + 9 restart
@@ -32,20 +35,29 @@ import ariadne_hip as ah
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 ROOT = os.path.dirname(os.path.abspath(__file__))
-# bench kernel class -> rocprofv3 kernel name prefix (for the PMC traffic of profiles/*/pmc_traffic.json)
-PMC_NAME = {"mgs_pass": "nk::k_mgs_pass<true,", "mgs_pass_last": "nk::k_mgs_pass<false,",
-            "jv_fd_dot_norm": "nk::k_st2d<2, 2, 2,", "jv_exact_dot_norm": "nk::k_st2d<2, 1, 2,",
-            "divcopy": "nk::k_divcopy"}
+# bench kernel class -> rocprofv3 kernel name prefix (for the PMC traffic of profiles/*/pmc_traffic_*.json);
+# the stencil template is <KIND, MODE, EPI, VEC>: KIND 2 Bratu 2D, 3 heat 2D, 4 heat 3D; MODE 1 exact, 2 FD
+STENCIL = {"bratu2d": "nk::k_st2d<2, ", "heat2d": "nk::k_st2d<3, ", "heat3d": "nk::k_st3d<4, "}
+
+
+def pmc_name(workload, kernel):
+    st = STENCIL[workload]
+    return {"mgs_pass": "nk::k_mgs_pass<true,", "mgs_pass_last": "nk::k_mgs_pass<false,",
+            "jv_fd_dot_norm": st + "2, 2,", "jv_exact_dot_norm": st + "1, 2,", "jv_fd_dot": st + "2, 2,",
+            "residual_norm": st + "0, 1,", "divcopy": "nk::k_divcopy", "update_x": "nk::k_update_x"}.get(kernel)
 LAMBDA = 3.51382       # examples/bratu.jl:41
 
 
 def parse():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--workload", choices=["bratu2d", "heat2d", "heat3d"], default="bratu2d",
+                    help="bratu2d: BASELINE config 2 (default); heat2d: config 3 (8192^2 implicit Euler time "
+                         "steps); heat3d: config 5 (512^3 implicit Euler time steps)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=4096, help="per-GPU slab is n x n")
-    ap.add_argument("--memory", type=int, default=30)
+    ap.add_argument("--n", type=int, default=0, help="per-GPU slab side (default 4096 / 8192 / 512 by workload)")
+    ap.add_argument("--memory", type=int, default=0, help="Krylov memory (default 30 for bratu2d, 20 for heat)")
     ap.add_argument("--itmax", type=int, default=300)
     ap.add_argument("--jv", choices=["fd", "exact"], default="fd")
     ap.add_argument("--no-prof", action="store_true", help="do not time kernels with HIP events")
@@ -54,37 +66,138 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-itmax", type=int, default=30, help="Arnoldi steps in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os.cpu_count())")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"),
-                    help="per-kernel HBM traffic from separate rocprofv3 --pmc passes (tools/pmc_traffic.py)")
+    ap.add_argument("--traffic-json", default="",
+                    help="per-kernel HBM traffic from separate rocprofv3 --pmc passes (tools/pmc_traffic.py); "
+                         "default profiles/r01/pmc_traffic_<workload>.json when present")
     return ap.parse_args()
 
 
-def slab_ic(nx, ny_loc, ny_glob, y0):
-    hx, hy = 1.0 / (nx + 1), 1.0 / (ny_glob + 1)
-    xs = np.arange(1, nx + 1) * hx
-    ys = np.arange(y0 + 1, y0 + ny_loc + 1) * hy
-    return np.ascontiguousarray(np.sin(np.pi * ys)[:, None] * np.sin(np.pi * xs)[None, :]), hx, hy
+def noisy(shape_rows, nx, seed_rows):
+    """0.1 U(-1, 1) noise whose every row is seeded by its GLOBAL index, so a slab sees the same field."""
+    return np.stack([0.1 * np.random.default_rng([0, int(r)]).uniform(-1.0, 1.0, nx) for r in seed_rows]).reshape(
+        shape_rows + (nx,))
 
 
-def cpu_baseline(n, memory, itmax, jv, threads):
-    """The C oracle (oracle/nk_oracle.c, test infrastructure) on a bounded sample of the same workload."""
-    from oracle import oracle as oc
+class Bratu2D:
+    """BASELINE config 2: one inexact-Newton step of 2D Bratu with GMRES(30) and a fixed Krylov budget."""
 
-    oc.set_threads(threads)
-    P = oc.bratu2d(n)
-    u0 = oc.sin_ic(P)
-    F0 = oc.residual(P, u0)
-    t0 = time.perf_counter()
-    x, st, _ = oc.krylov_solve(P, u0, F0, jv=jv, F0=F0, memory=memory, restart=True, itmax=itmax, atol=0.0, rtol=0.0,
-                               history=False)
-    dt = time.perf_counter() - t0
-    return dict(value=st["n_matvec"] / dt, unit="matvecs/s", cores=oc.get_threads(), kind="port",
-                sample=f"oracle/nk_oracle.c GMRES({memory}) restart cycle: {st['n_matvec']} {jv.upper()} matvecs "
-                       f"(MGS, same schedule) on the same {n}x{n} Bratu problem, {dt:.2f} s")
+    def __init__(self, args, ctx, rank, world):
+        n = args.n or 4096
+        self.n, self.world = n, world
+        ny_glob = n * world
+        self.hx, self.hy = 1.0 / (n + 1), 1.0 / (ny_glob + 1)
+        xs = np.arange(1, n + 1) * self.hx
+        ys = np.arange(rank * n + 1, rank * n + n + 1) * self.hy
+        u0 = np.ascontiguousarray(np.sin(np.pi * ys)[:, None] * np.sin(np.pi * xs)[None, :])
+        grid = ah.Grid((n, n), (n, ny_glob), rank * n)
+        self.u = ah.DeviceArray.from_numpy(u0, grid, ctx)
+        self.res = self.u.zero()
+        self.ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(self.res, memory=args.memory))
+        self.p = (self.hx, self.hy, LAMBDA)
+        self.kw = dict(restart=True, rtol=0.0, atol=0.0, itmax=args.itmax)
+        self.args = args
+        self.jv_kernel = "jv_fd_dot_norm" if args.jv == "fd" else "jv_exact_dot_norm"
+        self.workload = (f"2D Bratu {n}x{n * world} ({n}x{n} per GPU), one inexact-Newton step per step: "
+                         f"GMRES({args.memory}) restart, itmax={args.itmax}, rtol=atol=0, {args.jv.upper()} Jv")
+        self.metric = f"Krylov matvecs/sec + achieved HBM GB/s, 2D Bratu {n}^2"
+
+    def step(self):
+        _, r = ah.newton_krylov_(ah.bratu2d_, self.u, self.p, self.res, max_niter=0, tol_rel=0.0, tol_abs=0.0,
+                                 memory=self.args.memory, krylov_kwargs=self.kw, jv=self.args.jv, workspace=self.ws)
+        return r.n_matvec, r
+
+    def cpu_baseline(self, threads):
+        """The C oracle (test infrastructure) on one GMRES restart cycle of the same problem."""
+        from oracle import oracle as oc
+
+        oc.set_threads(threads)
+        P = oc.bratu2d(self.n)
+        u0 = oc.sin_ic(P)
+        F0 = oc.residual(P, u0)
+        t0 = time.perf_counter()
+        _, st, _ = oc.krylov_solve(P, u0, F0, jv=self.args.jv, F0=F0, memory=self.args.memory, restart=True,
+                                   itmax=self.args.cpu_itmax, atol=0.0, rtol=0.0, history=False)
+        dt = time.perf_counter() - t0
+        return dict(value=st["n_matvec"] / dt, unit="matvecs/s", cores=oc.get_threads(), kind="port",
+                    sample=f"oracle/nk_oracle.c GMRES({self.args.memory}) restart cycle: {st['n_matvec']} "
+                           f"{self.args.jv.upper()} matvecs (MGS, same schedule) on the same {self.n}x{self.n} "
+                           f"Bratu problem, {dt:.2f} s")
+
+    def free(self):
+        self.ws.free()
+
+
+class HeatEuler:
+    """BASELINE configs 3 / 5: implicit-Euler time steps (examples/implicit.jl `solve`) of the 2D / 3D heat
+    equation, noisy IC, unrestarted GMRES (memory 20), tol_abs = 6e-6; one step = one time step."""
+
+    def __init__(self, args, ctx, rank, world, dim):
+        n = args.n or (8192 if dim == 2 else 512)
+        self.n, self.dim, self.args, self.world = n, dim, args, world
+        self.a = 0.01
+        glob = (n,) * (dim - 1) + (n * world,)
+        hs = [1.0 / (m + 1) for m in glob]
+        self.hs = hs
+        if dim == 2:
+            self.dt = hs[0] ** 2 * hs[1] ** 2 / (2.0 * self.a * (hs[0] ** 2 + hs[1] ** 2))  # heat_2D.jl:72
+        else:
+            self.dt = 1.0 / (2.0 * self.a * sum(1.0 / h ** 2 for h in hs))
+        grid = ah.Grid((n,) * dim, glob, rank * n)
+        sines = [np.sin(np.pi * np.arange(1, n + 1) * hs[0])]
+        rows0 = rank * n
+        if dim == 2:
+            ys = np.sin(np.pi * np.arange(rows0 + 1, rows0 + n + 1) * hs[1])
+            u0 = ys[:, None] * sines[0][None, :] + noisy((n,), n, range(rows0, rows0 + n))
+        else:
+            ys = np.sin(np.pi * np.arange(1, n + 1) * hs[1])
+            zs = np.sin(np.pi * np.arange(rows0 + 1, rows0 + n + 1) * hs[2])
+            base = zs[:, None, None] * ys[None, :, None] * sines[0][None, None, :]
+            u0 = base + noisy((n, n), n, range(rows0 * n, (rows0 + n) * n))
+        self.u0 = np.ascontiguousarray(u0)
+        self.un = ah.DeviceArray.from_numpy(self.u0, grid, ctx)
+        self.u = self.un.copy()
+        self.res = self.u.zero()
+        self.ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(self.res, memory=args.memory or 20))
+        self.F = ah.heat2d_euler_ if dim == 2 else ah.heat3d_euler_
+        fp = (self.a, hs[0], hs[1], ah.bc_zero_) if dim == 2 else (self.a, hs[0], hs[1], hs[2], ah.bc_zero_)
+        self.p = (self.un, self.dt, None, fp, 0.0)
+        self.jv_kernel = "jv_fd_dot_norm" if args.jv == "fd" else "jv_exact_dot_norm"
+        shape = "x".join([str(n)] * (dim - 1) + [str(n * world)])
+        self.workload = (f"{dim}D heat implicit Euler {shape} ({n}^{dim} per GPU), one time step per step: "
+                         f"newton_krylov! tol_abs=6e-6, GMRES memory {args.memory or 20} (unrestarted), "
+                         f"{args.jv.upper()} Jv, IC sin*sin + 0.1 U(-1,1)")
+        self.metric = f"Krylov matvecs/sec + achieved HBM GB/s, {dim}D heat implicit Euler {n}^{dim}"
+
+    def step(self):
+        _, r = ah.newton_krylov_(self.F, self.u, self.p, self.res, tol_abs=6.0e-6, memory=self.args.memory or 20,
+                                 jv=self.args.jv, workspace=self.ws)
+        ah.kcopy_(len(self.un), self.un, self.u)  # uₙ .= u  (implicit.jl:75)
+        return r.n_matvec, r
+
+    def cpu_baseline(self, threads):
+        from oracle import oracle as oc
+
+        oc.set_threads(threads)
+        m = self.n  # bounded sample: one time step of the same problem
+        P = oc.heat2d_euler(m) if self.dim == 2 else oc.heat3d_euler(m)
+        u0 = oc.sin_ic(P) + 0.1 * np.random.default_rng(0).uniform(-1, 1, P.shape)
+        P.un = u0
+        t0 = time.perf_counter()
+        _, st = oc.newton_krylov(P, u0, tol_abs=6e-6, memory=self.args.memory or 20, jv=self.args.jv)
+        dt = time.perf_counter() - t0
+        return dict(value=st["n_matvec"] / dt, unit="matvecs/s", cores=oc.get_threads(), kind="port",
+                    sample=f"oracle/nk_oracle.c one implicit-Euler time step ({st['outer_iterations']} Newton, "
+                           f"{st['n_matvec']} matvecs) of the same {self.dim}D heat problem at {m}^{self.dim} "
+                           f"(noise from numpy default_rng(0)), {dt:.2f} s")
+
+    def free(self):
+        self.ws.free()
 
 
 def main():
     args = parse()
+    if args.workload == "bratu2d" and not args.memory:
+        args.memory = 30
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -100,23 +213,14 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         ctx.init_distributed(rank, world, obj[0])
 
-    n = args.n
-    ny_glob = n * world
-    u0, hx, hy = slab_ic(n, n, ny_glob, rank * n)
-    grid = ah.Grid((n, n), (n, ny_glob), rank * n)
-    u = ah.DeviceArray.from_numpy(u0, grid, ctx)
-    res = u.zero()
-    ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=args.memory))
-    p = (hx, hy, LAMBDA)
-    kw = dict(restart=True, rtol=0.0, atol=0.0, itmax=args.itmax)
-
-    def step():
-        _, r = ah.newton_krylov_(ah.bratu2d_, u, p, res, max_niter=0, tol_rel=0.0, tol_abs=0.0, memory=args.memory,
-                                 krylov_kwargs=kw, jv=args.jv, workspace=ws)
-        return ws.stats.n_matvec, r
+    if args.workload == "bratu2d":
+        W = Bratu2D(args, ctx, rank, world)
+    else:
+        W = HeatEuler(args, ctx, rank, world, 2 if args.workload == "heat2d" else 3)
+    step = W.step
 
     def barrier():
-        ctx.sync()
+        ctx.sync()  # every kernel of this process runs on the library's stream: this is the device sync
         if dist is not None:
             dist.barrier()
 
@@ -155,13 +259,15 @@ def main():
                for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"] / max(1, kv[1]["timed"]) * kv[1]["launches"])}
 
     pmc = {}
-    if args.traffic_json and os.path.exists(args.traffic_json):
+    if not args.traffic_json:
+        args.traffic_json = os.path.join(ROOT, "profiles", "r01", f"pmc_traffic_{args.workload}.json")
+    if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             pmc = json.load(f)
 
     def traffic(name):
         """PMC HBM bytes per launch of this kernel class as a rate over the same launch duration."""
-        pre = PMC_NAME.get(name)
+        pre = pmc_name(args.workload, name)
         hit = [v for k, v in pmc.items() if pre and k.startswith(pre)]
         return hit[0]["traffic_bytes"] if hit else None
 
@@ -180,12 +286,12 @@ def main():
                 "timed_launches": v["timed"]}
 
     dominant = next(iter(kernels), None)
-    jv_kernel = "jv_fd_dot_norm" if args.jv == "fd" else "jv_exact_dot_norm"  # Jv fused with V_k = q / h
+    jv_kernel = W.jv_kernel  # the Jv fused with V_k = q / h
 
     if rank == 0:
         value = matvecs * world / elapsed
         out = {
-            "metric": "Krylov matvecs/sec + achieved HBM GB/s, 2D Bratu 4096^2",
+            "metric": W.metric,
             "value": round(value, 3),
             "unit": "matvecs/s",
             "n_gpus": world,
@@ -196,11 +302,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (u0 = sin(pi x) sin(pi y), lambda = 3.51382)",
-            "config": {"workload": f"2D Bratu {n}x{n * world} ({n}x{n} per GPU), one inexact-Newton step per step: "
-                                   f"GMRES({args.memory}) restart, itmax={args.itmax}, rtol=atol=0, "
-                                   f"{args.jv.upper()} Jv",
-                       "matvecs_per_step": matvecs // max(1, args.steps), "parallelism": f"slab{world}"},
+            "data": "synthetic (see config.workload)",
+            "config": {"workload": W.workload, "matvecs_per_step": matvecs // max(1, args.steps),
+                       "parallelism": f"slab{world}"},
             "hbm_gbs_algorithmic": round(world * total_bytes / elapsed / 1e9, 1) if total_bytes else None,
             "roofline": roof(dominant) if dominant else None,
             "jv_roofline": roof(jv_kernel),
@@ -210,12 +314,12 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(n, args.memory, args.cpu_itmax, args.jv, threads)
+            out["cpu_baseline"] = W.cpu_baseline(threads)
             out["cpu_baseline"]["value"] = round(out["cpu_baseline"]["value"], 4)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
-    ws.free()
+    W.free()
     if dist is not None:
         dist.destroy_process_group()
 

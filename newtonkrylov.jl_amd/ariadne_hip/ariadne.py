@@ -117,10 +117,11 @@ class Stats(NamedTuple):
 
 
 class Result(NamedTuple):
-    """(; solved, stats, t) -- src/Ariadne.jl:370-371."""
+    """(; solved, stats, t) -- src/Ariadne.jl:370-371 (+ n_matvec: mul!(J) calls of all Krylov solves)."""
     solved: bool
     stats: Stats
     t: float
+    n_matvec: int = 0
 
 
 def newton_krylov_(F_: DeviceResidual, u: DeviceArray, p=None, res: DeviceArray | None = None, *,
@@ -159,6 +160,7 @@ def newton_krylov_(F_: DeviceResidual, u: DeviceArray, p=None, res: DeviceArray 
         raise ValueError("workspace algo does not match `algo`")
 
     stats = Stats(0, 0, n_res)
+    n_matvec = 0
     while n_res > tol and stats.outer_iterations <= max_niter:
         kwargs = dict(krylov_kwargs)
         if forcing is not None:
@@ -166,6 +168,7 @@ def newton_krylov_(F_: DeviceResidual, u: DeviceArray, p=None, res: DeviceArray 
         # Solve J d = F(u).  The reference passes copy(res) because Enzyme rewrites res inside
         # mul!; the device operator never writes res, so res itself is the right-hand side.
         krylov_solve_(workspace, J, res, **kwargs)
+        n_matvec += workspace.stats.n_matvec
         d = workspace.x
         kaxpy_(n, -1.0, d, u)  # u .-= 1 .* d  (Newton step s = 1, :341-344)
         n_res_prior = n_res
@@ -184,7 +187,7 @@ def newton_krylov_(F_: DeviceResidual, u: DeviceArray, p=None, res: DeviceArray 
     t = (time.perf_counter_ns() - t0) / 1.0e9
     if own_ws:
         workspace.free()
-    return u, Result(n_res <= tol, stats, t)
+    return u, Result(n_res <= tol, stats, t, n_matvec)
 
 
 def newton_krylov(F: DeviceResidual, u0: DeviceArray, p=None, **kwargs):

@@ -269,9 +269,83 @@ __device__ __forceinline__ void store_vout(const KArgs& A, int64_t o) {
 }
 
 // ------------------------------------------------------------------------------ 2D stencil
-// Block = 256 threads x VEC columns (one row segment), marching A.rows rows in y.  Software
-// pipeline: while row j is computed, the stencil field of row j+2 and the centre operands of
-// row j+1 are in flight, so no iteration waits on a load it issued itself.
+// Raw (un-cooked) loads of one row segment: VEC centre values + one "edge" value per field.  The
+// edge load is issued by every lane (no divergence): lane 0 reads column x0-1, lane 63 column
+// x0+VEC, the others re-read their own x0 (a cache-hot dummy).  No arithmetic touches the loaded
+// registers until the next iteration, so the compiler's s_waitcnt can leave them in flight.
+template <int MODE, int VEC>
+struct RawRow {
+    double a[VEC], ae;  // u (RES, JFD) or v (JEXACT)
+    double b[VEC], be;  // v (JFD)
+};
+
+template <int MODE, int VEC>
+__device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o, int64_t oe) {
+    RawRow<MODE, VEC> r;
+    const double* __restrict__ pa = (MODE == MODE_JEXACT) ? A.v : A.u;
+    if constexpr (VEC % 2 == 0) {
+#pragma unroll
+        for (int h = 0; h < VEC; h += 2) {
+            const double2 q = *reinterpret_cast<const double2*>(pa + o + h);
+            r.a[h] = q.x; r.a[h + 1] = q.y;
+        }
+    } else {
+        r.a[0] = pa[o];
+    }
+    r.ae = pa[oe];
+    if constexpr (MODE == MODE_JFD) {
+        if constexpr (VEC % 2 == 0) {
+#pragma unroll
+            for (int h = 0; h < VEC; h += 2) {
+                const double2 q = *reinterpret_cast<const double2*>(A.v + o + h);
+                r.b[h] = q.x; r.b[h + 1] = q.y;
+            }
+        } else {
+            r.b[0] = A.v[o];
+        }
+        r.be = A.v[oe];
+    }
+    return r;
+}
+
+// cooked stencil field of a row: centres, the lane's edge value, and (fused normalisation) v / h
+template <int VEC>
+struct Field {
+    double c[VEC], e;
+    double vn[VEC];
+};
+
+template <int MODE, int VEC>
+__device__ __forceinline__ Field<VEC> cook(const KArgs& A, const RawRow<MODE, VEC>& r, bool act, bool edge_ok) {
+    Field<VEC> f;
+    const bool div = A.vdiv != nullptr;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+        double v;
+        if constexpr (MODE == MODE_RES) {
+            f.c[k] = r.a[k];
+            v = 0.0;
+        } else if constexpr (MODE == MODE_JEXACT) {
+            v = div ? r.a[k] / A.hd : r.a[k];
+            f.c[k] = v;
+        } else {
+            v = div ? r.b[k] / A.hd : r.b[k];
+            f.c[k] = r.a[k] + A.eps * v;  // w = u + eps v
+        }
+        f.vn[k] = v;
+        if (!act) f.c[k] = 0.0;  // lanes past the row end act as the zero boundary for their neighbour
+    }
+    double e;
+    if constexpr (MODE == MODE_RES) e = r.ae;
+    else if constexpr (MODE == MODE_JEXACT) e = div ? r.ae / A.hd : r.ae;
+    else e = r.ae + A.eps * (div ? r.be / A.hd : r.be);
+    f.e = edge_ok ? e : 0.0;
+    return f;
+}
+
+// Block = 256 threads x VEC columns (one row segment), marching A.rows rows in y.  Pipeline: at
+// iteration j the raw loads of row j+2 and the centre operands of row j+1 are issued, row j+1's
+// raw data (issued one iteration earlier) is cooked, and row j is computed from registers.
 template <int KIND, int MODE, int EPI, int VEC>
 __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     __shared__ double sh[8];
@@ -284,77 +358,74 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     const int64_t nx = A.nx, ny = A.ny;
     const int64_t x0 = (int64_t)tx * (kBlock * VEC) + (int64_t)threadIdx.x * VEC;
     const bool act = x0 < nx;
-    const bool probe = (A.fast & 2) != 0;  // cost probe (bench hook only): skip the edge loads
-    const bool left_lane = !probe && lane == 0 && x0 >= 1 && x0 - 1 < nx;  // wave-edge lanes load their outer column
-    const bool right_lane = !probe && lane == 63 && x0 + VEC < nx;
+    const int64_t xc = act ? x0 : 0;  // clamped column: every load stays inside the allocation
+    const bool left_ok = lane == 0 && act && x0 >= 1;
+    const bool right_ok = lane == 63 && act && x0 + VEC < nx;
+    const int64_t de = left_ok ? -1 : (right_ok ? VEC : 0);  // edge element offset (0: dummy)
+    const bool edge_ok = left_ok || right_ok;
     const int64_t y0 = (int64_t)ty * A.rows;
     const int64_t y1 = y0 + A.rows < ny ? y0 + A.rows : ny;
     constexpr bool kU = MODE == MODE_JEXACT && KIND == NK_BRATU2D;
     constexpr bool kUn = KIND == NK_HEAT2D_EULER && MODE != MODE_JEXACT;
     constexpr bool kF0 = MODE == MODE_JFD;
     constexpr bool kAx = EPI == EPI_DOT || EPI == EPI_RESID;
+    const bool vout = MODE != MODE_RES && A.vout != nullptr;
     double acc = 0.0;
     if (y0 < ny) {
-        // rows y0-1 .. y0+1 (row -1 / row ny are the ghost planes: zero, or the neighbour slab's row)
-        Row<VEC> fm = field_row<MODE, VEC>(A, (y0 - 1) * nx + x0, act);
-        Row<VEC> fc = field_row<MODE, VEC>(A, y0 * nx + x0, act);
-        Row<VEC> fp = field_row<MODE, VEC>(A, (y0 + 1) * nx + x0, act);
-        double elc = left_lane ? fieldval<MODE>(A, y0 * nx + x0 - 1) : 0.0;
-        double erc = right_lane ? fieldval<MODE>(A, y0 * nx + x0 + VEC) : 0.0;
-        const bool has1 = y0 + 1 < ny;
-        double elp = (left_lane && has1) ? fieldval<MODE>(A, (y0 + 1) * nx + x0 - 1) : 0.0;
-        double erp = (right_lane && has1) ? fieldval<MODE>(A, (y0 + 1) * nx + x0 + VEC) : 0.0;
+        // rows y0-1 (ghost plane when y0 = 0) and y0 cooked up front; row y0+1 raw in flight
+        Field<VEC> fm = cook<MODE, VEC>(A, load_raw<MODE, VEC>(A, (y0 - 1) * nx + xc, (y0 - 1) * nx + xc + de), act, false);
+        Field<VEC> fc = cook<MODE, VEC>(A, load_raw<MODE, VEC>(A, y0 * nx + xc, y0 * nx + xc + de), act, edge_ok);
+        RawRow<MODE, VEC> rp = load_raw<MODE, VEC>(A, (y0 + 1) * nx + xc, (y0 + 1) * nx + xc + de);
         Row<VEC> uc{}, unc{}, f0c{}, ax{};
         {
-            const int64_t o = y0 * nx + x0;
-            if constexpr (kU) uc = data_row<VEC>(A.u, o, act);
-            if constexpr (kUn) unc = data_row<VEC>(A.un, o, act);
-            if constexpr (kF0) f0c = data_row<VEC>(A.F0, o, act);
-            if constexpr (kAx) ax = data_row<VEC>(A.aux, o, act);
+            const int64_t o = y0 * nx + xc;
+            if constexpr (kU) uc = data_row<VEC>(A.u, o, true);
+            if constexpr (kUn) unc = data_row<VEC>(A.un, o, true);
+            if constexpr (kF0) f0c = data_row<VEC>(A.F0, o, true);
+            if constexpr (kAx) ax = data_row<VEC>(A.aux, o, true);
         }
         for (int64_t j = y0; j < y1; ++j) {
-            const int64_t o = j * nx + x0;
-            // ---- issue: stencil field of row j+2, centre operands of row j+1
-            const bool f2 = act && j + 1 < y1;  // row j+2 is needed only if row j+1 is computed here
-            const Row<VEC> fpp = field_row<MODE, VEC>(A, o + 2 * nx, f2);
-            const bool e2 = j + 2 < ny && j + 1 < y1;
-            const double elpp = (left_lane && e2) ? fieldval<MODE>(A, o + 2 * nx - 1) : 0.0;
-            const double erpp = (right_lane && e2) ? fieldval<MODE>(A, o + 2 * nx + VEC) : 0.0;
-            const bool pre = act && j + 1 < y1;
+            const int64_t o = j * nx + xc;
+            // ---- issue: raw row j+2 (rows up to ny are the ghost plane; y1 <= ny keeps j+2 <= ny+1
+            //      in range only when j+1 < y1, so clamp to row j+1 otherwise)
+            const int64_t o2 = (j + 1 < y1) ? o + 2 * nx : o + nx;
+            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC>(A, o2, o2 + de);
             Row<VEC> ucn{}, uncn{}, f0cn{}, axn{};
-            if constexpr (kU) ucn = data_row<VEC>(A.u, o + nx, pre);
-            if constexpr (kUn) uncn = data_row<VEC>(A.un, o + nx, pre);
-            if constexpr (kF0) f0cn = data_row<VEC>(A.F0, o + nx, pre);
-            if constexpr (kAx) axn = data_row<VEC>(A.aux, o + nx, pre);
-            // ---- compute row j from registers loaded in earlier iterations
-            double lft = __shfl_up(fc.v[VEC - 1], 1, 64);
-            double rgt = __shfl_down(fc.v[0], 1, 64);
-            if (lane == 0) lft = elc;
-            if (lane == 63) rgt = erc;
+            const int64_t o1 = (j + 1 < y1) ? o + nx : o;
+            if constexpr (kU) ucn = data_row<VEC>(A.u, o1, true);
+            if constexpr (kUn) uncn = data_row<VEC>(A.un, o1, true);
+            if constexpr (kF0) f0cn = data_row<VEC>(A.F0, o1, true);
+            if constexpr (kAx) axn = data_row<VEC>(A.aux, o1, true);
+            // ---- cook row j+1 (its loads were issued one iteration ago)
+            const Field<VEC> fp = cook<MODE, VEC>(A, rp, act, edge_ok && j + 1 < ny);
+            // ---- compute row j from registers
+            double lft = __shfl_up(fc.c[VEC - 1], 1, 64);
+            double rgt = __shfl_down(fc.c[0], 1, 64);
+            if (lane == 0) lft = fc.e;
+            if (lane == 63) rgt = fc.e;
             if (act) {
                 Row<VEC> val;
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) {
-                    const double w = (k == 0) ? lft : fc.v[k == 0 ? 0 : k - 1];
-                    const double e = (k == VEC - 1) ? rgt : fc.v[k == VEC - 1 ? k : k + 1];
-                    const double c = fc.v[k];
-                    const double lsum = lapk(A, c, e, w, A.hx2, A.ihx2) + lapk(A, c, fp.v[k], fm.v[k], A.hy2, A.ihy2);
+                    const double w = (k == 0) ? lft : fc.c[k == 0 ? 0 : k - 1];
+                    const double e = (k == VEC - 1) ? rgt : fc.c[k == VEC - 1 ? k : k + 1];
+                    const double c = fc.c[k];
+                    const double lsum = lapk(A, c, e, w, A.hx2, A.ihx2) + lapk(A, c, fp.c[k], fm.c[k], A.hy2, A.ihy2);
                     double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unc.v[k], f0c.v[k]);
                     acc = epilogue<EPI>(r, ax.v[k], acc);
                     val.v[k] = r;
                 }
                 store_row<VEC>(A.out, o, val);
-                if constexpr (MODE != MODE_RES) {
-                    if (A.vout) store_vout<VEC>(A, o);
+                if (vout) {
+                    Row<VEC> vn;
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) vn.v[k] = fc.vn[k];
+                    store_row<VEC>(A.vout, o, vn);
                 }
             }
             fm = fc;
             fc = fp;
-            fp = fpp;
-            elc = elp;
-            erc = erp;
-            elp = elpp;
-            erp = erpp;
+            rp = rpp;
             uc = ucn;
             unc = uncn;
             f0c = f0cn;
