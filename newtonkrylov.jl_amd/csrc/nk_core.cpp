@@ -50,12 +50,17 @@ double* red_slot(nk_ctx* c) {
 
 int finish_reduction(nk_ctx* c, Red* r) {
     if (!c->comm) return NK_OK;
-    // collapse this rank's partials to one scalar, then sum the scalars over ranks (RCCL)
-    double* dst = red_slot(c);
-    NK_TRY(launch_finalize(c, *r, dst, 0));
+    // collapse this rank's partials to one scalar (normally already done by the producing
+    // kernel's last block), then sum the scalars over ranks (RCCL)
+    double* dst = r->fin;
+    if (!dst) {
+        dst = red_slot(c);
+        NK_TRY(launch_finalize(c, *r, dst, 0));
+    }
     NK_TRY(allreduce_scalar(c, dst, 1));
     r->ptr = dst;
     r->len = 1;
+    r->fin = nullptr;
     return NK_OK;
 }
 

@@ -119,8 +119,10 @@ int launch(nk_ctx* c, const char* name, double bytes, F&& f) {
 struct Red {
     const double* ptr;
     int len;
+    double* fin = nullptr;  // multi-rank: the producing kernel already folded its partials here
 };
 double* red_slot(nk_ctx* c);                 // next partial-sum slot of the ring
+double* red_out(nk_ctx* c, int len, Red* r, int* fin);  // slot for a reduction launch (+ fold flag)
 int finish_reduction(nk_ctx* c, Red* r);     // multi-rank: collapse + RCCL all-reduce
 int red_blocks(int64_t n);                   // grid size of streaming reductions
 

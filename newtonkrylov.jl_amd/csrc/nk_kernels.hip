@@ -60,6 +60,30 @@ __device__ __forceinline__ double reduce_input(const double* __restrict__ in, in
     return sh[4];
 }
 
+// Block partial -> part[blockIdx.x].  With `fin` (a communicator is attached) the last block to
+// arrive also folds all partials -- the same fixed-order sum k_finalize computes -- into
+// part[kRedCap - 1], so the RCCL all-reduce can follow without a separate finaliser launch.  The
+// arrival counter lives in part[kRedCap - 2] and is reset by that last block.
+__device__ __forceinline__ void publish(double acc, double* part, int fin, double* sh) {
+    __shared__ unsigned ticket;
+    const double s = block_sum(acc, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+    if (!fin) return;
+    unsigned* cnt = reinterpret_cast<unsigned*>(part + kRedCap - 2);
+    if (threadIdx.x == 0) {
+        __threadfence();  // release this block's partial
+        ticket = atomicAdd(cnt, 1u);
+    }
+    __syncthreads();
+    if (ticket != gridDim.x - 1) return;
+    __threadfence();  // acquire every other block's partial
+    const double t = reduce_input(part, (int)gridDim.x, sh);
+    if (threadIdx.x == 0) {
+        part[kRedCap - 1] = t;
+        *cnt = 0u;
+    }
+}
+
 __device__ __forceinline__ double lap(double c, double p, double m, double h2) { return ((p - 2.0 * c) + m) / h2; }
 
 struct KArgs {
@@ -80,6 +104,7 @@ struct KArgs {
     const double* vdiv;
     double* vout;
     double hd;           // *vdiv, loaded once per block
+    int fin;             // fold the partials in-kernel (publish)
 };
 
 __device__ __forceinline__ double vin(const KArgs& A, int64_t o) {
@@ -184,10 +209,7 @@ __global__ __launch_bounds__(kBlock) void k_st1d(KArgs A0) {
         A.out[i] = val;
         if (MODE != MODE_RES && A.vout) A.vout[i] = A.v[i] / A.hd;
     }
-    if (EPI != EPI_NONE) {
-        const double s = block_sum(acc, sh);
-        if (threadIdx.x == 0) A.part[blockIdx.x] = s;
-    }
+    if (EPI != EPI_NONE) publish(acc, A.part, A.fin, sh);
 }
 
 // ------------------------------------------------------------------------------ row fragments
@@ -279,7 +301,7 @@ struct RawRow {
     double b[VEC], be;  // v (JFD)
 };
 
-template <int MODE, int VEC>
+template <int MODE, int VEC, bool EDGE = true>
 __device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o, int64_t oe) {
     RawRow<MODE, VEC> r;
     const double* __restrict__ pa = (MODE == MODE_JEXACT) ? A.v : A.u;
@@ -292,7 +314,8 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o,
     } else {
         r.a[0] = pa[o];
     }
-    r.ae = pa[oe];
+    if constexpr (EDGE) r.ae = pa[oe];
+    else r.ae = 0.0;
     if constexpr (MODE == MODE_JFD) {
         if constexpr (VEC % 2 == 0) {
 #pragma unroll
@@ -303,7 +326,8 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o,
         } else {
             r.b[0] = A.v[o];
         }
-        r.be = A.v[oe];
+        if constexpr (EDGE) r.be = A.v[oe];
+        else r.be = 0.0;
     }
     return r;
 }
@@ -432,14 +456,15 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
             ax = axn;
         }
     }
-    if constexpr (EPI != EPI_NONE) {
-        const double s = block_sum(acc, sh);
-        if (threadIdx.x == 0) A.part[blockIdx.x] = s;
-    }
+    if constexpr (EPI != EPI_NONE) publish(acc, A.part, A.fin, sh);
 }
 
 // ------------------------------------------------------------------------------ 3D stencil
-// Block = 4 waves = 4 rows (y) x 64*VEC columns, marching A.rows planes in z.
+// Block = 4 waves = 4 rows (y) x 64*VEC columns, marching A.rows planes in z.  Same pipeline as
+// the 2D kernel: at iteration k the raw loads of the centre row of plane k+2 and of the y-
+// neighbour rows of plane k+1 are issued, plane k+1's centre row and plane k's y-neighbours
+// (issued one iteration earlier) are cooked, and plane k is computed from registers.  The y-
+// neighbour rows are mostly L2 hits (the adjacent waves of the block stream them).
 template <int KIND, int MODE, int EPI, int VEC>
 __global__ __launch_bounds__(kBlock) void k_st3d(KArgs A0) {
     __shared__ double sh[8];
@@ -456,62 +481,85 @@ __global__ __launch_bounds__(kBlock) void k_st3d(KArgs A0) {
     const int64_t x0 = (int64_t)tx * (64 * VEC) + (int64_t)lane * VEC;
     const int64_t j = (int64_t)ty * 4 + wv;
     const bool act = x0 < nx && j < ny;
+    const int64_t oj = (act ? j * nx + x0 : 0);  // clamped: every load stays inside the allocation
     const bool has_n = act && j + 1 < ny, has_s = act && j >= 1;
-    const bool left_lane = lane == 0 && j < ny && x0 >= 1 && x0 - 1 < nx;
-    const bool right_lane = lane == 63 && j < ny && x0 + VEC < nx;
+    const int64_t dn = has_n ? nx : 0, ds = has_s ? -nx : 0;  // 0: dummy (own row), cooked to zero
+    const bool left_ok = lane == 0 && act && x0 >= 1;
+    const bool right_ok = lane == 63 && act && x0 + VEC < nx;
+    const int64_t de = left_ok ? -1 : (right_ok ? VEC : 0);
+    const bool edge_ok = left_ok || right_ok;
     const int64_t z0 = (int64_t)tz * A.rows;
     const int64_t z1 = z0 + A.rows < nz ? z0 + A.rows : nz;
+    constexpr bool kUn = MODE != MODE_JEXACT;
+    constexpr bool kF0 = MODE == MODE_JFD;
+    constexpr bool kAx = EPI == EPI_DOT || EPI == EPI_RESID;
+    const bool vout = MODE != MODE_RES && A.vout != nullptr;
     double acc = 0.0;
     if (z0 < nz) {
-        const int64_t oj = j * nx + x0;
-        Row<VEC> fm = field_row<MODE, VEC>(A, (z0 - 1) * pl + oj, act);  // plane -1: ghost plane
-        Row<VEC> fc = field_row<MODE, VEC>(A, z0 * pl + oj, act);
-        double elc = left_lane ? fieldval<MODE>(A, z0 * pl + oj - 1) : 0.0;
-        double erc = right_lane ? fieldval<MODE>(A, z0 * pl + oj + VEC) : 0.0;
+        const int64_t o0 = z0 * pl + oj;
+        Field<VEC> fm = cook<MODE, VEC>(A, load_raw<MODE, VEC, false>(A, o0 - pl, 0), act, false);  // plane -1: ghost
+        Field<VEC> fc = cook<MODE, VEC>(A, load_raw<MODE, VEC>(A, o0, o0 + de), act, edge_ok);
+        RawRow<MODE, VEC> rp = load_raw<MODE, VEC>(A, o0 + pl, o0 + pl + de);  // plane nz: ghost
+        RawRow<MODE, VEC> rn = load_raw<MODE, VEC, false>(A, o0 + dn, 0);
+        RawRow<MODE, VEC> rs = load_raw<MODE, VEC, false>(A, o0 + ds, 0);
+        Row<VEC> unc{}, f0c{}, ax{};
+        if constexpr (kUn) unc = data_row<VEC>(A.un, o0, true);
+        if constexpr (kF0) f0c = data_row<VEC>(A.F0, o0, true);
+        if constexpr (kAx) ax = data_row<VEC>(A.aux, o0, true);
         for (int64_t k = z0; k < z1; ++k) {
             const int64_t o = k * pl + oj;
-            const Row<VEC> fp = field_row<MODE, VEC>(A, o + pl, act);  // plane nz: ghost plane
-            const bool nxt = k + 1 < nz;
-            const double elp = (left_lane && nxt) ? fieldval<MODE>(A, o + pl - 1) : 0.0;
-            const double erp = (right_lane && nxt) ? fieldval<MODE>(A, o + pl + VEC) : 0.0;
-            const Row<VEC> fn = field_row<MODE, VEC>(A, o + nx, has_n);
-            const Row<VEC> fs = field_row<MODE, VEC>(A, o - nx, has_s);
-            Row<VEC> unc{}, f0c{}, ax{};
-            if constexpr (MODE != MODE_JEXACT) unc = data_row<VEC>(A.un, o, act);
-            if constexpr (MODE == MODE_JFD) f0c = data_row<VEC>(A.F0, o, act);
-            if constexpr (EPI == EPI_DOT || EPI == EPI_RESID) ax = data_row<VEC>(A.aux, o, act);
-            double lft = __shfl_up(fc.v[VEC - 1], 1, 64);
-            double rgt = __shfl_down(fc.v[0], 1, 64);
-            if (lane == 0) lft = elc;
-            if (lane == 63) rgt = erc;
+            // ---- issue: centre row of plane k+2, y-neighbour rows and centre data of plane k+1
+            const bool more = k + 1 < z1;
+            const int64_t o2 = more ? o + 2 * pl : o + pl;
+            const int64_t o1 = more ? o + pl : o;
+            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC>(A, o2, o2 + de);
+            const RawRow<MODE, VEC> rnn = load_raw<MODE, VEC, false>(A, o1 + dn, 0);
+            const RawRow<MODE, VEC> rss = load_raw<MODE, VEC, false>(A, o1 + ds, 0);
+            Row<VEC> uncn{}, f0cn{}, axn{};
+            if constexpr (kUn) uncn = data_row<VEC>(A.un, o1, true);
+            if constexpr (kF0) f0cn = data_row<VEC>(A.F0, o1, true);
+            if constexpr (kAx) axn = data_row<VEC>(A.aux, o1, true);
+            // ---- cook what was issued one iteration ago
+            const Field<VEC> fp = cook<MODE, VEC>(A, rp, act, edge_ok);
+            const Field<VEC> fn = cook<MODE, VEC>(A, rn, has_n, false);
+            const Field<VEC> fs = cook<MODE, VEC>(A, rs, has_s, false);
+            // ---- compute plane k
+            double lft = __shfl_up(fc.c[VEC - 1], 1, 64);
+            double rgt = __shfl_down(fc.c[0], 1, 64);
+            if (lane == 0) lft = fc.e;
+            if (lane == 63) rgt = fc.e;
             if (act) {
                 Row<VEC> val;
 #pragma unroll
                 for (int q = 0; q < VEC; ++q) {
-                    const double w = (q == 0) ? lft : fc.v[q == 0 ? 0 : q - 1];
-                    const double e = (q == VEC - 1) ? rgt : fc.v[q == VEC - 1 ? q : q + 1];
-                    const double c = fc.v[q];
-                    const double lsum = (lapk(A, c, e, w, A.hx2, A.ihx2) + lapk(A, c, fn.v[q], fs.v[q], A.hy2, A.ihy2)) +
-                                        lapk(A, c, fp.v[q], fm.v[q], A.hz2, A.ihz2);
+                    const double w = (q == 0) ? lft : fc.c[q == 0 ? 0 : q - 1];
+                    const double e = (q == VEC - 1) ? rgt : fc.c[q == VEC - 1 ? q : q + 1];
+                    const double c = fc.c[q];
+                    const double lsum = (lapk(A, c, e, w, A.hx2, A.ihx2) + lapk(A, c, fn.c[q], fs.c[q], A.hy2, A.ihy2)) +
+                                        lapk(A, c, fp.c[q], fm.c[q], A.hz2, A.ihz2);
                     double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unc.v[q], f0c.v[q]);
                     acc = epilogue<EPI>(r, ax.v[q], acc);
                     val.v[q] = r;
                 }
                 store_row<VEC>(A.out, o, val);
-                if constexpr (MODE != MODE_RES) {
-                    if (A.vout) store_vout<VEC>(A, o);
+                if (vout) {
+                    Row<VEC> vn;
+#pragma unroll
+                    for (int q = 0; q < VEC; ++q) vn.v[q] = fc.vn[q];
+                    store_row<VEC>(A.vout, o, vn);
                 }
             }
             fm = fc;
             fc = fp;
-            elc = elp;
-            erc = erp;
+            rp = rpp;
+            rn = rnn;
+            rs = rss;
+            unc = uncn;
+            f0c = f0cn;
+            ax = axn;
         }
     }
-    if constexpr (EPI != EPI_NONE) {
-        const double s = block_sum(acc, sh);
-        if (threadIdx.x == 0) A.part[blockIdx.x] = s;
-    }
+    if constexpr (EPI != EPI_NONE) publish(acc, A.part, A.fin, sh);
 }
 
 // ------------------------------------------------------------------------------ BLAS-1
@@ -522,7 +570,7 @@ __global__ __launch_bounds__(kBlock) void k_st3d(KArgs A0) {
 #define NK_TAIL (((n & 1) != 0) && blockIdx.x == 0 && threadIdx.x == 0)
 
 __global__ __launch_bounds__(kBlock) void k_dot(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
-                                               double* __restrict__ part) {
+                                               double* __restrict__ part, int fin) {
     __shared__ double sh[8];
     const double2* x2 = reinterpret_cast<const double2*>(x);
     const double2* y2 = reinterpret_cast<const double2*>(y);
@@ -533,11 +581,10 @@ __global__ __launch_bounds__(kBlock) void k_dot(int64_t n, const double* __restr
         acc = fma(a.y, b.y, acc);
     }
     if (NK_TAIL) acc = fma(x[n - 1], y[n - 1], acc);
-    const double s = block_sum(acc, sh);
-    if (threadIdx.x == 0) part[blockIdx.x] = s;
+    publish(acc, part, fin, sh);
 }
 
-__global__ __launch_bounds__(kBlock) void k_sumsq(int64_t n, const double* __restrict__ x, double* __restrict__ part) {
+__global__ __launch_bounds__(kBlock) void k_sumsq(int64_t n, const double* __restrict__ x, double* __restrict__ part, int fin) {
     __shared__ double sh[8];
     const double2* x2 = reinterpret_cast<const double2*>(x);
     double acc = 0.0;
@@ -547,8 +594,7 @@ __global__ __launch_bounds__(kBlock) void k_sumsq(int64_t n, const double* __res
         acc = fma(a.y, a.y, acc);
     }
     if (NK_TAIL) acc = fma(x[n - 1], x[n - 1], acc);
-    const double s = block_sum(acc, sh);
-    if (threadIdx.x == 0) part[blockIdx.x] = s;
+    publish(acc, part, fin, sh);
 }
 
 __global__ __launch_bounds__(kBlock) void k_finalize(const double* __restrict__ in, int len, double* __restrict__ dst, int sqrt_it) {
@@ -659,7 +705,7 @@ template <bool HAS_NEXT, int U, bool NT, bool NTW = false>
 __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restrict__ q, const double* __restrict__ vi,
                                                     const double* __restrict__ vnext, const double* __restrict__ red_in,
                                                     int red_len, double* __restrict__ h_out, double* __restrict__ part,
-                                                    int rev) {
+                                                    int rev, int fin) {
     __shared__ double sh[8];
     dx2* q2 = reinterpret_cast<dx2*>(q);
     const dx2* v2 = reinterpret_cast<const dx2*>(vi);
@@ -730,8 +776,7 @@ __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restri
         q[n - 1] = a;
         acc = HAS_NEXT ? fma(vnext[n - 1], a, acc) : fma(a, a, acc);
     }
-    const double s = block_sum(acc, sh);
-    if (threadIdx.x == 0) part[blockIdx.x] = s;
+    publish(acc, part, fin, sh);
 }
 
 struct UpdArgs {
@@ -741,7 +786,7 @@ struct UpdArgs {
     const double* y;
     double* part;
     int64_t n;
-    int k, first, last, restart;
+    int k, first, last, restart, fin;
 };
 
 // xr = Σ y_i V_i (the kaxpy! chain of gmres!, from xr = 0); on the last chunk x = x + xr
@@ -792,15 +837,12 @@ __global__ __launch_bounds__(kBlock) void k_update_x(UpdArgs A) {
             A.xr[i] = t;
         }
     }
-    if (A.part) {
-        const double s = block_sum(acc, sh);
-        if (threadIdx.x == 0) A.part[blockIdx.x] = s;
-    }
+    if (A.part) publish(acc, A.part, A.fin, sh);
 }
 
 __global__ __launch_bounds__(kBlock) void k_cg_update(int64_t n, double alpha, double* __restrict__ x, double* __restrict__ r,
                                                      const double* __restrict__ p, const double* __restrict__ Ap,
-                                                     double* __restrict__ part) {
+                                                     double* __restrict__ part, int fin) {
     __shared__ double sh[8];
     double acc = 0.0;
     const double ma = -alpha;
@@ -811,8 +853,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(int64_t n, double alpha, d
         r[i] = rv;
         acc = fma(rv, rv, acc);
     }
-    const double s = block_sum(acc, sh);
-    if (threadIdx.x == 0) part[blockIdx.x] = s;
+    publish(acc, part, fin, sh);
 }
 
 __global__ __launch_bounds__(kBlock) void k_cg_direction(int64_t n, double beta, double* __restrict__ p, const double* __restrict__ r) {
@@ -860,6 +901,17 @@ int env_int(const char* name, int dflt) {
 }
 
 }  // namespace
+
+// partial-sum slot of a reduction launch.  With a communicator the kernel also folds its partials
+// in place (publish) and finish_reduction only has to all-reduce part[kRedCap - 1].
+double* red_out(nk_ctx* c, int len, Red* r, int* fin) {
+    double* part = red_slot(c);
+    *fin = c->comm ? 1 : 0;
+    r->ptr = part;
+    r->len = len;
+    r->fin = *fin ? part + kRedCap - 1 : nullptr;
+    return part;
+}
 
 int red_blocks(int64_t n) {
     static const int cap = env_int("NK_RED_BLOCKS", kMaxRedBlocks);
@@ -920,10 +972,8 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         grid = A.tiles_x * A.tiles_y * (int)((p->nz + planes - 1) / planes);
     }
     if (in.epi != EPI_NONE) {
-        if (grid > kRedCap) return fail(c, NK_E_ARG, "stencil grid exceeds reduction capacity");
-        A.part = red_slot(c);
-        red->ptr = A.part;
-        red->len = grid;
+        if (grid > kRedCap - 2) return fail(c, NK_E_ARG, "stencil grid exceeds reduction capacity");
+        A.part = red_out(c, grid, red, &A.fin);
     }
     // algorithmic (compulsory) bytes per launch
     const bool heat = p->kind == NK_HEAT2D_EULER || p->kind == NK_HEAT3D_EULER;
@@ -955,18 +1005,16 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
 
 int launch_dot(nk_ctx* c, int64_t n, const double* x, const double* y, Red* red) {
     const int g = red_blocks(n);
-    double* part = red_slot(c);
-    red->ptr = part;
-    red->len = g;
-    return launch(c, "dot", 16.0 * n, [&] { hipLaunchKernelGGL(k_dot, dim3(g), dim3(kBlock), 0, c->stream, n, x, y, part); });
+    int fin;
+    double* part = red_out(c, g, red, &fin);
+    return launch(c, "dot", 16.0 * n, [&] { hipLaunchKernelGGL(k_dot, dim3(g), dim3(kBlock), 0, c->stream, n, x, y, part, fin); });
 }
 
 int launch_sumsq(nk_ctx* c, int64_t n, const double* x, Red* red) {
     const int g = red_blocks(n);
-    double* part = red_slot(c);
-    red->ptr = part;
-    red->len = g;
-    return launch(c, "norm", 8.0 * n, [&] { hipLaunchKernelGGL(k_sumsq, dim3(g), dim3(kBlock), 0, c->stream, n, x, part); });
+    int fin;
+    double* part = red_out(c, g, red, &fin);
+    return launch(c, "norm", 8.0 * n, [&] { hipLaunchKernelGGL(k_sumsq, dim3(g), dim3(kBlock), 0, c->stream, n, x, part, fin); });
 }
 
 int launch_finalize(nk_ctx* c, Red r, double* dst, int sqrt_it) {
@@ -993,13 +1041,13 @@ int launch_ref(nk_ctx* c, int64_t n, double* x, double* y, double cc, double ss)
 namespace {
 template <bool HAS_NEXT>
 void mgs_dispatch(int variant, int g, hipStream_t s, int64_t n, double* q, const double* vi, const double* vn,
-                  const double* red, int len, double* h, double* part, int rev) {
+                  const double* red, int len, double* h, double* part, int rev, int fin) {
     switch (variant) {  // unroll depth x non-temporal V_i loads (tools/kbench.py measures them)
-    case 0: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, false>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
-    case 1: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
-    case 2: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
-    case 3: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
-    default: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev); break;
+    case 0: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, false>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev, fin); break;
+    case 1: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev, fin); break;
+    case 2: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev, fin); break;
+    case 3: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev, fin); break;
+    default: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev, fin); break;
     }
 }
 }  // namespace
@@ -1008,15 +1056,14 @@ int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const dou
                     int rev) {
     static const int variant = env_int("NK_MGS_VARIANT", kMgsVariant);
     const int g = red_blocks(n);
-    double* part = red_slot(c);
-    out->ptr = part;
-    out->len = g;
+    int fin;
+    double* part = red_out(c, g, out, &fin);
     if (vnext)
         return launch(c, "mgs_pass", 32.0 * n, [&] {
-            mgs_dispatch<true>(variant, g, c->stream, n, q, vi, vnext, in.ptr, in.len, h_out, part, rev);
+            mgs_dispatch<true>(variant, g, c->stream, n, q, vi, vnext, in.ptr, in.len, h_out, part, rev, fin);
         });
     return launch(c, "mgs_pass_last", 24.0 * n, [&] {
-        mgs_dispatch<false>(variant, g, c->stream, n, q, vi, vnext, in.ptr, in.len, h_out, part, rev);
+        mgs_dispatch<false>(variant, g, c->stream, n, q, vi, vnext, in.ptr, in.len, h_out, part, rev, fin);
     });
 }
 
@@ -1038,11 +1085,7 @@ int launch_update_x(nk_ctx* c, int64_t n, double* x, double* xr, const double* c
         A.last = done + m == k;
         A.restart = restart;
         A.part = nullptr;
-        if (A.last && xnorm) {
-            A.part = red_slot(c);
-            xnorm->ptr = A.part;
-            xnorm->len = g;
-        }
+        if (A.last && xnorm) A.part = red_out(c, g, xnorm, &A.fin);
         // every chunk reads m basis vectors and (after the first) xr; the last writes x (reading it on restart)
         const double bytes = 8.0 * n * (m + (A.first ? 0 : 1) + (A.last ? (restart ? 2 : 1) : 1));
         NK_TRY(launch(c, "update_x", bytes, [&] {
@@ -1055,11 +1098,10 @@ int launch_update_x(nk_ctx* c, int64_t n, double* x, double* xr, const double* c
 
 int launch_cg_update(nk_ctx* c, int64_t n, double alpha, double* x, double* r, const double* p, const double* Ap, Red* rr) {
     const int g = red_blocks(n);
-    double* part = red_slot(c);
-    rr->ptr = part;
-    rr->len = g;
+    int fin;
+    double* part = red_out(c, g, rr, &fin);
     return launch(c, "cg_update", 48.0 * n, [&] {
-        hipLaunchKernelGGL(k_cg_update, dim3(g), dim3(kBlock), 0, c->stream, n, alpha, x, r, p, Ap, part);
+        hipLaunchKernelGGL(k_cg_update, dim3(g), dim3(kBlock), 0, c->stream, n, alpha, x, r, p, Ap, part, fin);
     });
 }
 
@@ -1095,8 +1137,8 @@ extern "C" int nkb_mgs_seq(nk_ctx* c, int64_t n, int k, int variant, int alt, in
             const int rev = alt ? (i & 1) : 0;
             const double* in = parts[i & 1];
             double* out = parts[(i + 1) & 1];
-            if (i + 1 < k) mgs_dispatch<true>(variant, g, c->stream, n, q, V[i], V[i + 1], in, g, hs + 1, out, rev);
-            else mgs_dispatch<false>(variant, g, c->stream, n, q, V[i], nullptr, in, g, hs + 1, out, rev);
+            if (i + 1 < k) mgs_dispatch<true>(variant, g, c->stream, n, q, V[i], V[i + 1], in, g, hs + 1, out, rev, 0);
+            else mgs_dispatch<false>(variant, g, c->stream, n, q, V[i], nullptr, in, g, hs + 1, out, rev, 0);
         }
     };
     sweep();
