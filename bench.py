@@ -36,14 +36,15 @@ import ariadne_hip as ah
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 ROOT = os.path.dirname(os.path.abspath(__file__))
 # bench kernel class -> rocprofv3 kernel name prefix (for the PMC traffic of profiles/*/pmc_traffic_*.json);
-# the stencil template is <KIND, MODE, EPI, VEC>: KIND 2 Bratu 2D, 3 heat 2D, 4 heat 3D; MODE 1 exact, 2 FD
+# the stencil template is <KIND, MODE, EPI, VEC>: KIND 2 Bratu 2D, 3 heat 2D, 4 heat 3D; MODE 1 exact, 2 FD;
+# EPI 1 sumsq, 2 dot, 4 dot + fused V_k = q / h store
 STENCIL = {"bratu2d": "nk::k_st2d<2, ", "heat2d": "nk::k_st2d<3, ", "heat3d": "nk::k_st3d<4, "}
 
 
 def pmc_name(workload, kernel):
     st = STENCIL[workload]
     return {"mgs_pass": "nk::k_mgs_pass<true,", "mgs_pass_last": "nk::k_mgs_pass<false,",
-            "jv_fd_dot_norm": st + "2, 2,", "jv_exact_dot_norm": st + "1, 2,", "jv_fd_dot": st + "2, 2,",
+            "jv_fd_dot_norm": st + "2, 4,", "jv_exact_dot_norm": st + "1, 4,", "jv_fd_dot": st + "2, 2,",
             "residual_norm": st + "0, 1,", "divcopy": "nk::k_divcopy", "update_x": "nk::k_update_x"}.get(kernel)
 LAMBDA = 3.51382       # examples/bratu.jl:41
 

@@ -21,10 +21,10 @@ constexpr int kRedSlots = 4;         // ring of partial-sum slots
 constexpr int kRedCap = 16384;       // doubles per slot (a stencil launch may have more blocks)
 constexpr int kScalCap = 8192;       // device scalar area (Hessenberg column, y, norms)
 constexpr int kMaxUpdateVecs = 32;   // basis vectors folded per x-update launch
-constexpr int kMgsVariant = 1;       // MGS-pass variant (unroll x non-temporal V_i), see mgs_dispatch
+constexpr int kMgsVariant = 5;       // MGS-pass variant (unroll x non-temporal V_i), see mgs_dispatch
 
 enum Mode { MODE_RES = 0, MODE_JEXACT = 1, MODE_JFD = 2 };
-enum Epi { EPI_NONE = 0, EPI_SUMSQ = 1, EPI_DOT = 2, EPI_RESID = 3 };
+enum Epi { EPI_NONE = 0, EPI_SUMSQ = 1, EPI_DOT = 2, EPI_RESID = 3, EPI_DOTV = 4 /* EPI_DOT + vout (kernel-internal) */ };
 
 struct ProfPending {
     int kid;

@@ -29,7 +29,8 @@ lib.nkb_stencil.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_int, 
 n = args.n
 side = int(round(n ** 0.5))
 
-MGS = {0: "U2", 1: "U2+nt(V_i)", 2: "U4+nt(V_i)", 3: "U2+nt(V_i,V_i+1)", 4: "U4+nt(V_i,V_i+1)"}
+MGS = {0: "U2", 1: "U2+nt(V_i)", 2: "U4+nt(V_i)", 3: "U2+nt(V_i,V_i+1)", 4: "U4+nt(V_i,V_i+1)",
+       5: "U2+nt(V_i) chunked", 6: "U4+nt(V_i) chunked"}
 configs = [("copy", None, None, None)]
 if "mgs" in args.what:
     configs += [("mgs", v, 0, k) for k in (8, 16, 30) for v in MGS]
