@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--prof-every", type=int, default=16,
                     help="time every k-th launch of each kernel class (HIP events; k > 1 keeps their cost out)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-itmax", type=int, default=30, help="Arnoldi steps in the CPU-baseline sample")
+    ap.add_argument("--cpu-itmax", type=int, default=300, help="Arnoldi steps in the CPU-baseline sample (300 = one bench step)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os.cpu_count())")
     ap.add_argument("--traffic-json", default="",
                     help="per-kernel HBM traffic from separate rocprofv3 --pmc passes (tools/pmc_traffic.py); "
@@ -91,6 +91,7 @@ class Bratu2D:
         ys = np.arange(rank * n + 1, rank * n + n + 1) * self.hy
         u0 = np.ascontiguousarray(np.sin(np.pi * ys)[:, None] * np.sin(np.pi * xs)[None, :])
         grid = ah.Grid((n, n), (n, ny_glob), rank * n)
+        self.u0 = u0
         self.u = ah.DeviceArray.from_numpy(u0, grid, ctx)
         self.res = self.u.zero()
         self.ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(self.res, memory=args.memory))
@@ -116,13 +117,39 @@ class Bratu2D:
         u0 = oc.sin_ic(P)
         F0 = oc.residual(P, u0)
         t0 = time.perf_counter()
-        _, st, _ = oc.krylov_solve(P, u0, F0, jv=self.args.jv, F0=F0, memory=self.args.memory, restart=True,
+        x, st, _ = oc.krylov_solve(P, u0, F0, jv=self.args.jv, F0=F0, memory=self.args.memory, restart=True,
                                    itmax=self.args.cpu_itmax, atol=0.0, rtol=0.0, history=False)
         dt = time.perf_counter() - t0
+        self.x_cpu = x
         return dict(value=st["n_matvec"] / dt, unit="matvecs/s", cores=oc.get_threads(), kind="port",
-                    sample=f"oracle/nk_oracle.c GMRES({self.args.memory}) restart cycle: {st['n_matvec']} "
-                           f"{self.args.jv.upper()} matvecs (MGS, same schedule) on the same {self.n}x{self.n} "
-                           f"Bratu problem, {dt:.2f} s")
+                    sample=f"oracle/nk_oracle.c: the Krylov solve of one bench step -- GMRES({self.args.memory}) with "
+                           f"restarts, itmax={self.args.cpu_itmax}, {st['n_matvec']} {self.args.jv.upper()} matvecs "
+                           f"(MGS, same schedule) on the same {self.n}x{self.n} Bratu problem, {dt:.2f} s")
+
+    def agreement(self):
+        """The CPU sample's Newton step repeated on the GPU from the same u0: the north-star quantity is
+        ||F(u0 - x)||, which must agree to 1e-10 relative; the raw Krylov iterates are reported as well."""
+        from oracle import oracle as oc
+
+        u = ah.DeviceArray.from_numpy(self.u0, self.u.grid, self.u.ctx)
+        res = u.zero()
+        ah.bratu2d_(res, u, self.p)
+        J = ah.JacobianOperator(ah.bratu2d_, res, u, self.p, jv=self.args.jv)
+        ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=self.args.memory))
+        ah.krylov_solve_(ws, J, res, restart=True, itmax=self.args.cpu_itmax, atol=0.0, rtol=0.0)
+        x = ws.x.to_numpy()
+        ah.kaxpy_(len(u), -1.0, ws.x, u)  # u .-= d (src/Ariadne.jl:344)
+        ah.bratu2d_(res, u, self.p)
+        n_gpu = ah.knorm(len(res), res)
+        ws.free()
+        P = oc.bratu2d(self.n)
+        n_cpu = float(np.linalg.norm(oc.residual(P, self.u0 - self.x_cpu)))
+        d = abs(n_gpu - n_cpu) / n_cpu
+        dx = float(np.linalg.norm(x - self.x_cpu) / np.linalg.norm(self.x_cpu))
+        return {"quantity": f"||F(u0 - x)|| after one Newton step (GMRES({self.args.memory}), "
+                            f"{self.args.cpu_itmax} Arnoldi steps), GPU vs CPU, relative",
+                "value": d, "tolerance": 1e-10, "ok": d <= 1e-10, "n_res_gpu": n_gpu, "n_res_cpu": n_cpu,
+                "x_rel_diff": dx}
 
     def free(self):
         self.ws.free()
@@ -317,6 +344,8 @@ def main():
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
             out["cpu_baseline"] = W.cpu_baseline(threads)
             out["cpu_baseline"]["value"] = round(out["cpu_baseline"]["value"], 4)
+            if hasattr(W, "agreement"):
+                out["cpu_gpu_agreement"] = W.agreement()
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
