@@ -33,12 +33,17 @@ extern "C" {
 #define NK_E_NOMEM (-3)
 #define NK_E_RCCL (-4)
 #define NK_E_STATE (-5)
+#define NK_E_USER (-6)     /* a user residual / tangent callback returned non-zero */
 
 /* ---------------------------------------------------------------- problem kinds */
 #define NK_BRATU1D 1       /* examples/bratu.jl:14-24  bratu!(res, y, (Δx, λ))                         */
 #define NK_BRATU2D 2       /* build-defined 2D generalisation                       */
 #define NK_HEAT2D_EULER 3  /* examples/implicit.jl:8-13 G_Euler! ∘ examples/heat_2D.jl:45-62 diffusion! */
 #define NK_HEAT3D_EULER 4  /* build-defined 3D generalisation                      */
+
+#define NK_USER1D 16       /* user residual F!(res, u, p) given as callbacks, */
+#define NK_USER2D 17       /* on a 1D / 2D / 3D grid (the kind fixes the slab axis, as for the      */
+#define NK_USER3D 18       /* built-in kinds)                                                      */
 
 #define NK_BC_ZERO 0       /* bc_zero!, examples/heat_2D.jl:28-38 */
 
@@ -51,17 +56,33 @@ extern "C" {
 typedef struct nk_ctx nk_ctx;
 typedef struct nk_workspace nk_workspace;
 
+/* A user residual (kinds NK_USER1D/2D/3D): any F!(res, u, p) the caller can evaluate on device vectors of
+ * the problem's grid -- the plug-in point of newton_krylov!'s residual callback
+ * (src/Ariadne.jl:288 `F!`, :302, :349).  The callbacks must enqueue their device work on
+ * nk_ctx_stream(ctx) (or finish it before returning) and return 0 on success.  When they run, the
+ * ghost planes of u (and v) are current: zero (Dirichlet) or the neighbour slab's plane.
+ * F is required; J (the exact tangent, what Enzyme's forward mode gives the reference's mul!) is
+ * optional -- without it only NK_JV_FD is available. */
+typedef int (*nk_user_residual)(void* data, nk_ctx* ctx, double* res, const double* u);
+typedef int (*nk_user_tangent)(void* data, nk_ctx* ctx, double* out, const double* u, const double* v);
+typedef struct nk_user_ops {
+    nk_user_residual F;
+    nk_user_tangent J;
+    void* data;
+} nk_user_ops;
+
 /* F!(res, u, p) of one problem on this rank's slab.  Dimensions are LOCAL interior extents;
  * spacings are global (h = 1/(N_global + 1)).  x is the fastest axis (the reference's
  * column-major first index). */
 typedef struct nk_problem {
-    int32_t kind;           /* NK_BRATU1D … NK_HEAT3D_EULER */
+    int32_t kind;           /* NK_BRATU1D … NK_HEAT3D_EULER, NK_USER1D … NK_USER3D */
     int32_t bc;             /* NK_BC_ZERO */
     int64_t nx, ny, nz;     /* local interior extents (ny = nz = 1 in 1D, nz = 1 in 2D) */
     double hx, hy, hz;      /* grid spacings */
     double lambda;          /* Bratu λ */
     double a, dt;           /* heat diffusivity and time step Δt */
     const double* un;       /* heat: device interior pointer to u_n (borrowed for the call) */
+    const nk_user_ops* user;  /* NK_USER*: the callbacks (borrowed for the call) */
 } nk_problem;
 
 /* ---------------------------------------------------------------- context / memory */
@@ -70,6 +91,8 @@ int nk_ctx_create(int device, nk_ctx** out);
 int nk_ctx_destroy(nk_ctx* ctx);
 const char* nk_last_error(nk_ctx* ctx);
 int nk_sync(nk_ctx* ctx);
+/* the context's HIP stream (hipStream_t): every library kernel and every user callback's work runs on it */
+void* nk_ctx_stream(nk_ctx* ctx);
 
 /* similar(u) / zero(u) for a grid function of `p`'s local grid: zero-filled incl. ghost planes. */
 int nk_vec_alloc(nk_ctx* ctx, const nk_problem* p, double** out);

@@ -11,13 +11,13 @@ from .distributed import dist_unique_id, init_distributed, slab
 from .implicit import G_Euler_, G_Midpoint_, G_Trapezoid_, diffusion3d_, diffusion_, solve
 from .krylov import (KrylovConstructor, kaxpby_, kaxpy_, kcopy_, kdivcopy_, kdot, kfill_, knorm, kref_, krylov_solve_,
                      krylov_workspace, kscal_)
-from .problems import DeviceResidual, bc_zero_, bratu2d_, bratu_, heat2d_euler_, heat3d_euler_
+from .problems import DeviceResidual, UserResidual, bc_zero_, bratu2d_, bratu_, heat2d_euler_, heat3d_euler_
 
 __all__ = [
     "NKError", "device_count", "load", "EisenstatWalker", "Fixed", "Forcing", "JacobianOperator", "Result", "Stats",
     "mul_", "newton_krylov", "newton_krylov_", "Context", "DeviceArray", "Grid", "default_context",
     "set_default_context", "dist_unique_id", "init_distributed", "slab", "G_Euler_", "G_Midpoint_", "G_Trapezoid_", "diffusion_", "diffusion3d_", "solve",
     "KrylovConstructor", "kaxpby_", "kaxpy_", "kcopy_", "kdivcopy_", "kdot", "kfill_", "knorm", "kref_",
-    "krylov_solve_", "krylov_workspace", "kscal_", "DeviceResidual", "bc_zero_", "bratu2d_", "bratu_",
+    "krylov_solve_", "krylov_workspace", "kscal_", "DeviceResidual", "UserResidual", "bc_zero_", "bratu2d_", "bratu_",
     "heat2d_euler_", "heat3d_euler_",
 ]

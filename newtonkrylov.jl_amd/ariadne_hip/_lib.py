@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libnkhip.so")
@@ -15,11 +16,12 @@ HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "nkhip.h")
 
 NK_OK = 0
 NK_BRATU1D, NK_BRATU2D, NK_HEAT2D_EULER, NK_HEAT3D_EULER = 1, 2, 3, 4
+NK_USER1D, NK_USER2D, NK_USER3D = 16, 17, 18
 NK_BC_ZERO = 0
 NK_JV_EXACT, NK_JV_FD = 0, 1
 NK_ALGO_GMRES, NK_ALGO_CG = 0, 1
 
-_ERRORS = {-1: "HIP error", -2: "invalid argument", -3: "out of device memory", -4: "RCCL error", -5: "bad state"}
+_ERRORS = {-1: "HIP error", -2: "invalid argument", -3: "out of device memory", -4: "RCCL error", -5: "bad state", -6: "user callback failed"}
 
 
 class NKError(RuntimeError):
@@ -31,7 +33,16 @@ class nk_problem(C.Structure):
                 ("nx", C.c_int64), ("ny", C.c_int64), ("nz", C.c_int64),
                 ("hx", C.c_double), ("hy", C.c_double), ("hz", C.c_double),
                 ("lam", C.c_double), ("a", C.c_double), ("dt", C.c_double),
-                ("un", C.c_void_p)]
+                ("un", C.c_void_p), ("user", C.c_void_p)]
+
+
+# nk_user_ops: int F(void* data, nk_ctx*, double* res, const double* u); int J(data, ctx, out, u, v)
+NK_USER_RESIDUAL = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p)
+NK_USER_TANGENT = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p)
+
+
+class nk_user_ops(C.Structure):
+    _fields_ = [("F", NK_USER_RESIDUAL), ("J", NK_USER_TANGENT), ("data", C.c_void_p)]
 
 
 class nk_krylov_opts(C.Structure):
@@ -58,6 +69,7 @@ SIGNATURES = {
     "nk_ctx_destroy": (C.c_int, [_VP]),
     "nk_last_error": (C.c_char_p, [_VP]),
     "nk_sync": (C.c_int, [_VP]),
+    "nk_ctx_stream": (_VP, [_VP]),
     "nk_vec_alloc": (C.c_int, [_VP, _PP, C.POINTER(_VP)]),
     "nk_vec_free": (C.c_int, [_VP, _VP]),
     "nk_memcpy_h2d": (C.c_int, [_VP, _VP, _VP, _I64]),
@@ -89,6 +101,7 @@ SIGNATURES = {
 }
 
 _lib = None
+TORCH_FIRST = False
 
 
 def load():
@@ -98,6 +111,8 @@ def load():
         if not os.path.exists(LIB_PATH):
             raise NKError(f"libnkhip.so not built ({LIB_PATH}); run `make -C newtonkrylov.jl_amd` -- "
                           "there is no CPU fallback")
+        global TORCH_FIRST
+        TORCH_FIRST = "torch" in sys.modules  # then libnkhip binds torch's HIP runtime (one runtime per process)
         lib = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             f = getattr(lib, name)
@@ -107,13 +122,35 @@ def load():
     return _lib
 
 
+_user_error = None
+
+
+def set_user_error(e: BaseException):
+    """A user-residual callback raised: remembered here, re-raised by the C call that ran it."""
+    global _user_error
+    _user_error = e
+
+
+def require_torch_first():
+    """torch interop needs ONE HIP runtime in the process: torch must be imported before libnkhip.so loads."""
+    if not TORCH_FIRST:
+        raise NKError("torch interop: import torch before ariadne_hip loads libnkhip.so, so that both use the "
+                      "same HIP runtime (torch bundles its own)")
+
+
 def check(rc: int, ctx=None, what: str = ""):
+    global _user_error
     if rc != NK_OK:
         msg = ""
         if ctx is not None:
             m = load().nk_last_error(ctx)
             msg = m.decode() if m else ""
-        raise NKError(f"{what}: {_ERRORS.get(rc, rc)} {msg}".strip())
+        cause, _user_error = _user_error, None
+        if rc != -6:
+            cause = None
+        if cause is not None:
+            msg += f" ({type(cause).__name__}: {cause})"
+        raise NKError(f"{what}: {_ERRORS.get(rc, rc)} {msg}".strip()) from cause
 
 
 def device_count() -> int:

@@ -74,6 +74,8 @@ class JacobianOperator:
                             "generic Python callables have no kernel")
         if jv not in ("exact", "fd"):
             raise ValueError("jv must be 'exact' or 'fd'")
+        if jv == "exact" and getattr(f, "J", True) is None:
+            raise ValueError(f"{f}: a UserResidual without a tangent J has only the FD operator -- pass jv='fd'")
         self.f, self.res, self.u, self.p = f, res, u, p
         self.jv = jv
 

@@ -42,6 +42,18 @@ class Context:
     def sync(self):
         self.check(load().nk_sync(self.handle), "nk_sync")
 
+    @property
+    def stream(self) -> int:
+        """The library's hipStream_t (every kernel and every user-residual callback runs on it)."""
+        return load().nk_ctx_stream(self.handle) or 0
+
+    def torch_stream(self):
+        """`with ctx.torch_stream(): ...` makes torch enqueue on the library's stream (for user residuals)."""
+        import torch
+
+        _lib.require_torch_first()
+        return torch.cuda.stream(torch.cuda.ExternalStream(self.stream, device=torch.device("cuda", self.device)))
+
     def close(self):
         if getattr(self, "handle", None):
             load().nk_ctx_destroy(self.handle)
@@ -185,6 +197,22 @@ class DeviceArray:
         d = DeviceArray(grid, ctx)
         d.ctx.check(load().nk_memcpy_h2d(d.ctx.handle, d.ptr, a.ctypes.data, a.size), "nk_memcpy_h2d")
         return d
+
+    def torch(self, ghosts: bool = False):
+        """Zero-copy torch view (numpy-order shape, x fastest) -- for user residuals.  ghosts=True
+        includes the ghost plane on each side of the slowest axis (zero Dirichlet, or the neighbour
+        slab's plane when distributed): shape (n_slow + 2, ...)."""
+        import torch
+
+        _lib.require_torch_first()
+        shape, ptr = self.grid.np_shape, self.ptr
+        if ghosts:
+            plane = int(np.prod(shape[1:])) if len(shape) > 1 else 1
+            shape, ptr = (shape[0] + 2,) + tuple(shape[1:]), self.ptr - 8 * plane
+        view = type("_CAI", (), {})()
+        view.__cuda_array_interface__ = {"shape": shape, "typestr": "<f8", "data": (ptr, False), "version": 3,
+                                         "strides": None}
+        return torch.as_tensor(view, device=torch.device("cuda", self.ctx.device))
 
     def to_numpy(self) -> np.ndarray:
         out = np.empty(self.grid.np_shape, dtype=np.float64)

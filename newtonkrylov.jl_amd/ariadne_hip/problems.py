@@ -10,10 +10,12 @@ loop, and `JacobianOperator` maps it to the matching fused Jv kernel (nk_jv) ins
 | `bratu2d_`    | 2D generalisation                  | `(dx, dy, lam)`                      |
 | `heat2d_euler_` | `G_Euler!` ∘ `diffusion!` implicit.jl:8-13 + heat_2D.jl:45-62 | `(u_n, dt, du, (a, dx, dy, bc_zero_), t)` |
 | `heat3d_euler_` | 3D generalisation                | `(u_n, dt, du, (a, dx, dy, dz, bc_zero_), t)` |
+| `UserResidual(F[, J])` | any `F!(res, u, p)` evaluated on the device by the caller | the caller's |
 """
 from __future__ import annotations
 
 import ctypes as C
+import sys
 
 from . import _lib
 from ._lib import load
@@ -103,3 +105,58 @@ bratu_ = _Bratu1D()
 bratu2d_ = _Bratu2D()
 heat2d_euler_ = _HeatEuler(2)
 heat3d_euler_ = _HeatEuler(3)
+
+
+# ----------------------------------------------------------------------------- user residuals
+class UserResidual(DeviceResidual):
+    """F!(res, u, p) written by the caller -- the residual callback newton_krylov! takes
+    (src/Ariadne.jl:288; e.g. the KernelAbstractions residual of examples/bratu_ka.jl) -- for
+    residuals that have no built-in kernel (kinds NK_USER1D/2D/3D).
+
+    `F(res, u, p)` gets DeviceArray views of device vectors on u's grid and must evaluate the
+    residual ON THE DEVICE, enqueued on the library's stream: the call already runs inside
+    `ctx.torch_stream()` when torch is loaded, so `res.torch()[...] = f(u.torch())` just works.
+    Ghost planes of u are current (zero Dirichlet, or the neighbour slab's plane).
+    `J(out, u, v, p)` (optional) is the exact tangent -- what Enzyme's forward mode computes for the
+    reference's mul! (src/Ariadne.jl:48-57); without it use JacobianOperator(..., jv="fd"), whose
+    FD quotient, basis normalisation and reductions the library runs around F on the device.
+    """
+
+    kind = _lib.NK_USER2D  # per call: NK_USER1D/2D/3D by the grid's dimension
+
+    def __init__(self, F, J=None, name: str | None = None):
+        self.F, self.J = F, J
+        self.name = name or (getattr(F, "__name__", "user") + "!")
+        self._live = {}
+
+    def _callbacks(self, grid, ctx, p):
+        def run(fn, *ptrs):
+            try:
+                views = [DeviceArray(grid, ctx, _ptr=q) for q in ptrs]
+                if "torch" in sys.modules:
+                    with ctx.torch_stream():
+                        fn(*views, p)
+                else:
+                    fn(*views, p)
+                return 0
+            except BaseException as e:  # reported by the C call that invoked the callback
+                _lib.set_user_error(e)
+                return 1
+
+        cf = _lib.NK_USER_RESIDUAL(lambda _d, _c, res, u: run(self.F, res, u))
+        cj = _lib.NK_USER_TANGENT(lambda _d, _c, out, u, v: run(self.J, out, u, v)) if self.J else _lib.NK_USER_TANGENT()
+        ops = _lib.nk_user_ops(cf, cj, None)
+        return ops, cf, cj
+
+    def problem(self, u, p):
+        key = (u.grid, id(u.ctx), id(p))
+        hit = self._live.get(key)
+        if hit is None:
+            if len(self._live) > 16:
+                self._live.clear()
+            ops, cf, cj = self._callbacks(u.grid, u.ctx, p)
+            hit = self._live[key] = (ops, cf, cj, p)  # keeps the callbacks (and p) alive
+        nx, ny, nz = u.grid.nxyz
+        kind = (_lib.NK_USER1D, _lib.NK_USER2D, _lib.NK_USER3D)[u.grid.dim - 1]
+        return _lib.nk_problem(kind, 0, nx, ny, nz, 1.0, 1.0, 1.0, 0.0, 0.0, 0.0, None,
+                               C.cast(C.pointer(hit[0]), C.c_void_p))

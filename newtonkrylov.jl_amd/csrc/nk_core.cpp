@@ -31,6 +31,20 @@ int geometry(nk_ctx* c, const nk_problem* p, Geo* g) {
     case NK_HEAT3D_EULER:
         g->dim = 3; g->plane = p->nx * p->ny; g->nplanes = p->nz;
         break;
+    case NK_USER1D:
+    case NK_USER2D:
+    case NK_USER3D:
+        if (!p->user || !p->user->F) return fail(c, NK_E_ARG, "user problem needs user->F");
+        if (p->kind == NK_USER1D) {
+            if (p->ny != 1 || p->nz != 1) return fail(c, NK_E_ARG, "1D problem needs ny = nz = 1");
+            g->dim = 1; g->plane = 1; g->nplanes = p->nx;
+        } else if (p->kind == NK_USER2D) {
+            if (p->nz != 1) return fail(c, NK_E_ARG, "2D problem needs nz = 1");
+            g->dim = 2; g->plane = p->nx; g->nplanes = p->ny;
+        } else {
+            g->dim = 3; g->plane = p->nx * p->ny; g->nplanes = p->nz;
+        }
+        break;
     default:
         return fail(c, NK_E_ARG, "unknown problem kind");
     }
@@ -182,6 +196,8 @@ int nk_ctx_destroy(nk_ctx* c) {
 }
 
 const char* nk_last_error(nk_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void* nk_ctx_stream(nk_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int nk_sync(nk_ctx* c) {
     if (!c) return NK_E_ARG;

@@ -57,6 +57,9 @@ struct nk_ctx {
     std::vector<std::string> kid_names;
     std::map<std::string, int> kid_of;
     std::vector<nk::ProfAcc> acc;
+    // user kinds: the FD evaluation point w = u + eps v (one grid function, reallocated on a new geometry)
+    double* user_w = nullptr;
+    int64_t user_w_n = -1, user_w_plane = -1;
     // distribution
     int rank = 0, nranks = 1;
     nk::Comm* comm = nullptr;
@@ -165,6 +168,14 @@ int launch_update_x(nk_ctx* c, int64_t n, double* x, double* xr, const double* c
 int launch_cg_update(nk_ctx* c, int64_t n, double alpha, double* x, double* r, const double* p,
                      const double* Ap, Red* rr);
 int launch_cg_direction(nk_ctx* c, int64_t n, double beta, double* p, const double* r);
+// NK_USER pieces: w = u + eps (v / *vdiv) (w may be null) and vout = v / *vdiv (vout may be null);
+// and the epilogue pass after a user F / J: out = (out - F0) / eps when fd, + the `epi` partials.
+int launch_fd_point(nk_ctx* c, int64_t n, double* w, const double* u, const double* v, const double* vdiv,
+                    double eps, double* vout);
+int launch_user_epi(nk_ctx* c, int64_t n, int fd, double* out, const double* F0, double eps, int epi,
+                    const double* aux, Red* red);
+int launch_user(nk_ctx* c, const StencilIn& in, Red* red);  // nk_user.cpp
+inline bool nk_is_user(int kind) { return kind >= NK_USER1D && kind <= NK_USER3D; }
 
 // ---------------------------------------------------------------- distribution (nk_dist.cpp)
 int halo_exchange(nk_ctx* c, const nk_problem* p, const double* v);

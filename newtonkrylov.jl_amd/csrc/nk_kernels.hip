@@ -872,6 +872,37 @@ __global__ __launch_bounds__(kBlock) void k_cg_direction(int64_t n, double beta,
     NK_CHUNKED(i, n) p[i] = fma(beta, p[i], 1.0 * r[i]);
 }
 
+// ------------------------------------------------------------------------------ NK_USER pieces
+// w = u + eps * (v / h) -- the same expression the fused FD stencils evaluate in registers -- and
+// the normalised basis vector v / h (fused kdivcopy!), h = *vdiv on the device (1 when null).
+__global__ __launch_bounds__(kBlock) void k_fd_point(int64_t n, double* __restrict__ w, const double* __restrict__ u,
+                                                    const double* __restrict__ v, const double* __restrict__ vdiv,
+                                                    double eps, double* __restrict__ vout) {
+    const double hd = vdiv ? *vdiv : 1.0;
+    NK_CHUNKED(i, n) {
+        const double vi = vdiv ? v[i] / hd : v[i];
+        if (w) w[i] = u[i] + eps * vi;
+        if (vout) vout[i] = vi;
+    }
+}
+
+// after a user F (FD: out = F(w)) or J: out = (out - F0) / eps (FD), then the stencil epilogue
+template <int EPI>
+__global__ __launch_bounds__(kBlock) void k_user_epi(int64_t n, int fd, double* __restrict__ out,
+                                                    const double* __restrict__ F0, double eps,
+                                                    const double* __restrict__ aux, double* __restrict__ part, int fin) {
+    __shared__ double sh[8];
+    double acc = 0.0;
+    NK_CHUNKED(i, n) {
+        double r = out[i];
+        if (fd) r = (r - F0[i]) / eps;
+        const double ax = (EPI == EPI_DOT || EPI == EPI_RESID) ? aux[i] : 0.0;
+        acc = epilogue<EPI>(r, ax, acc);
+        if (fd || EPI == EPI_RESID) out[i] = r;
+    }
+    if constexpr (EPI != EPI_NONE) publish(acc, part, fin, sh);
+}
+
 // ------------------------------------------------------------------------------ stencil dispatch
 template <int KIND, int MODE, int EPI>
 void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s) {
@@ -937,7 +968,10 @@ namespace {
 int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_override, int fast);
 }
 
-int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red) { return launch_stencil_ex(c, in, red, 0, 0); }
+int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red) {
+    if (in.p && nk_is_user(in.p->kind)) return launch_user(c, in, red);
+    return launch_stencil_ex(c, in, red, 0, 0);
+}
 
 namespace {
 int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_override, int fast) {
@@ -1118,6 +1152,28 @@ int launch_cg_update(nk_ctx* c, int64_t n, double alpha, double* x, double* r, c
     double* part = red_out(c, g, rr, &fin);
     return launch(c, "cg_update", 48.0 * n, [&] {
         hipLaunchKernelGGL(k_cg_update, dim3(g), dim3(kBlock), 0, c->stream, n, alpha, x, r, p, Ap, part, fin);
+    });
+}
+
+int launch_fd_point(nk_ctx* c, int64_t n, double* w, const double* u, const double* v, const double* vdiv,
+                    double eps, double* vout) {
+    NK_STREAM_LAUNCH("user_fd_point", 8.0 * (1 + (w ? 2 : 0) + (vout ? 1 : 0)), k_fd_point, n, w, u, v, vdiv, eps, vout);
+}
+
+int launch_user_epi(nk_ctx* c, int64_t n, int fd, double* out, const double* F0, double eps, int epi, const double* aux,
+                    Red* red) {
+    const int g = red_blocks(n);
+    int fin = 0;
+    double* part = nullptr;
+    if (epi != EPI_NONE) part = red_out(c, g, red, &fin);
+    const double words = 1 + (fd ? 2 : 0) + ((epi == EPI_DOT || epi == EPI_RESID) ? 1 : 0) + (epi == EPI_RESID ? 1 : 0);
+    return launch(c, "user_epilogue", 8.0 * words * n, [&] {
+        switch (epi) {
+        case EPI_NONE: hipLaunchKernelGGL(k_user_epi<EPI_NONE>, dim3(g), dim3(kBlock), 0, c->stream, n, fd, out, F0, eps, aux, part, fin); break;
+        case EPI_SUMSQ: hipLaunchKernelGGL(k_user_epi<EPI_SUMSQ>, dim3(g), dim3(kBlock), 0, c->stream, n, fd, out, F0, eps, aux, part, fin); break;
+        case EPI_DOT: hipLaunchKernelGGL(k_user_epi<EPI_DOT>, dim3(g), dim3(kBlock), 0, c->stream, n, fd, out, F0, eps, aux, part, fin); break;
+        default: hipLaunchKernelGGL(k_user_epi<EPI_RESID>, dim3(g), dim3(kBlock), 0, c->stream, n, fd, out, F0, eps, aux, part, fin); break;
+        }
     });
 }
 

@@ -4,6 +4,11 @@ import sys
 
 import pytest
 
+try:  # torch first: libnkhip.so must bind the same HIP runtime torch uses (user residuals run torch code)
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover
+    torch = None
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

@@ -1,5 +1,6 @@
 """CPU-only checks of the product boundary: libnkhip.so loads, exports every symbol the public
 header declares, and the host mirror fails loudly without a GPU (no CPU fallback)."""
+import ctypes as C
 import os
 import re
 
@@ -16,7 +17,7 @@ HEADER = _lib.HEADER
 
 def header_functions():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|double\*|const char\*)\s+(nk_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|double\*|void\*|const char\*)\s+(nk_\w+)\s*\(", src, re.M)))
 
 
 def test_library_built_in_tree():
@@ -43,6 +44,32 @@ def test_header_structs_match_ctypes():
     want = [f if f != "lambda" else "lam" for f in fields]
     got = [f[0] for f in _lib.nk_problem._fields_]
     assert got == want
+
+
+def test_struct_layouts_match_c(tmp_path):
+    """sizeof/offsetof of the public structs as gcc lays them out == the ctypes mirrors."""
+    import subprocess
+
+    structs = {"nk_problem": _lib.nk_problem, "nk_krylov_opts": _lib.nk_krylov_opts,
+               "nk_krylov_stats": _lib.nk_krylov_stats, "nk_prof_entry": _lib.nk_prof_entry,
+               "nk_user_ops": _lib.nk_user_ops}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
+    for sname, cls in structs.items():
+        lines.append(f'printf("{sname} %zu\\n", sizeof({sname}));')
+        for fname, _ in cls._fields_:
+            cname = "lambda" if fname == "lam" else fname
+            lines.append(f'printf("{sname}.{fname} %zu\\n", offsetof({sname}, {cname}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-o", str(exe), str(src)], check=True)
+    got = dict(line.split() for line in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                       text=True).stdout.splitlines())
+    for sname, cls in structs.items():
+        assert int(got[sname]) == C.sizeof(cls), sname
+        for fname, _ in cls._fields_:
+            assert int(got[f"{sname}.{fname}"]) == getattr(cls, fname).offset, f"{sname}.{fname}"
 
 
 def test_no_gpu_fails_loudly():
