@@ -16,6 +16,7 @@ import Krylov: kdot, knorm, kscal!, kaxpy!, kaxpby!, kcopy!, kfill!, kdivcopy!, 
 const libnkhip = joinpath(@__DIR__, "..", "lib", "libnkhip.so")
 
 const NK_BRATU1D, NK_BRATU2D, NK_HEAT2D_EULER, NK_HEAT3D_EULER = Int32(1), Int32(2), Int32(3), Int32(4)
+const NK_USER1D, NK_USER2D, NK_USER3D = Int32(16), Int32(17), Int32(18)
 const NK_JV_EXACT, NK_JV_FD = Int32(0), Int32(1)
 
 check(rc, ctx, what) = rc == 0 || error("$what failed ($rc): " *
@@ -47,9 +48,10 @@ struct NkProblem
     a::Float64
     dt::Float64
     un::Ptr{Float64}
+    user::Ptr{Cvoid}   # nk_user_ops* (NK_USER1D/2D/3D)
 end
 geometry(grid::NTuple{3, Int}) = NkProblem(grid[3] > 1 ? NK_HEAT3D_EULER : (grid[2] > 1 ? NK_BRATU2D : NK_BRATU1D),
-                                            0, grid..., 1.0, 1.0, 1.0, 0.0, 0.0, 0.0, Ptr{Float64}(1))
+                                            0, grid..., 1.0, 1.0, 1.0, 0.0, 0.0, 0.0, Ptr{Float64}(1), C_NULL)
 
 # --------------------------------------------------------------------------- HipVector (device HaloVector)
 """Grid function in HBM: interior x-fastest (the column-major order of a Julia array), one ghost
@@ -142,10 +144,48 @@ const bratu! = HipResidual{:bratu1d}()        # examples/bratu.jl:14-24, p = (Δ
 const bratu2d! = HipResidual{:bratu2d}()      # p = (Δx, Δy, λ)
 const heat2d_euler! = HipResidual{:heat2d}()  # G_Euler! ∘ diffusion!, p = (uₙ, Δt, du, (a, Δx, Δy, bc!), t)
 
-problem(::HipResidual{:bratu1d}, u::HipVector, (dx, λ)) = NkProblem(NK_BRATU1D, 0, u.grid..., dx, 1, 1, λ, 0, 0, C_NULL)
-problem(::HipResidual{:bratu2d}, u::HipVector, (dx, dy, λ)) = NkProblem(NK_BRATU2D, 0, u.grid..., dx, dy, 1, λ, 0, 0, C_NULL)
+problem(::HipResidual{:bratu1d}, u::HipVector, (dx, λ)) = NkProblem(NK_BRATU1D, 0, u.grid..., dx, 1, 1, λ, 0, 0, C_NULL, C_NULL)
+problem(::HipResidual{:bratu2d}, u::HipVector, (dx, dy, λ)) = NkProblem(NK_BRATU2D, 0, u.grid..., dx, dy, 1, λ, 0, 0, C_NULL, C_NULL)
 problem(::HipResidual{:heat2d}, u::HipVector, (un, Δt, _, (a, dx, dy, _bc), _t)) =
-    NkProblem(NK_HEAT2D_EULER, 0, u.grid..., dx, dy, 1, 0, a, Δt, un.ptr)
+    NkProblem(NK_HEAT2D_EULER, 0, u.grid..., dx, dy, 1, 0, a, Δt, un.ptr, C_NULL)
+
+# --------------------------------------------------------------------------- user residuals (NK_USER*)
+# Any F!(res, u, p) the caller evaluates on the device (e.g. an AMDGPU.jl / KernelAbstractions
+# kernel like examples/bratu_ka.jl) -- launched on the library's stream, nk_ctx_stream(ctx).  The
+# library runs the FD quotient, the GMRES basis normalisation and every reduction around it.
+struct NkUserOps
+    F::Ptr{Cvoid}
+    J::Ptr{Cvoid}
+    data::Ptr{Cvoid}
+end
+struct HipUserResidual{F, J}
+    f!::F            # f!(res::HipVector, u::HipVector, p)
+    jvp!::J          # jvp!(out, u, v, p) (exact tangent) or nothing: then only NK_JV_FD
+    jv::Int32
+end
+HipUserResidual(f!; jvp! = nothing) = HipUserResidual(f!, jvp!, jvp! === nothing ? NK_JV_FD : NK_JV_EXACT)
+libstream(ctx::HipContext) = ccall((:nk_ctx_stream, libnkhip), Ptr{Cvoid}, (Ptr{Cvoid},), ctx.ptr)
+
+const _live = IdDict{Any, Any}()   # keeps the @cfunction closures rooted while the library may call them
+function problem(F::HipUserResidual, u::HipVector, p)
+    view(ptr) = HipVector(u.ctx, Ptr{Float64}(ptr), u.grid)     # non-owning
+    fF = (_d, _c, res, x) -> (try F.f!(view(res), view(x), p); Cint(0) catch; Cint(1) end)
+    cF = @cfunction($fF, Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}))
+    cJ = F.jvp! === nothing ? nothing :
+         @cfunction($((_d, _c, out, x, v) -> (try F.jvp!(view(out), view(x), view(v), p); Cint(0) catch; Cint(1) end)),
+                    Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}))
+    ops = Ref(NkUserOps(Base.unsafe_convert(Ptr{Cvoid}, cF),
+                        cJ === nothing ? C_NULL : Base.unsafe_convert(Ptr{Cvoid}, cJ), C_NULL))
+    _live[F] = (cF, cJ, ops, p)
+    kind = u.grid[3] > 1 ? NK_USER3D : (u.grid[2] > 1 ? NK_USER2D : NK_USER1D)
+    return NkProblem(kind, 0, u.grid..., 1, 1, 1, 0, 0, 0, C_NULL, Base.unsafe_convert(Ptr{Cvoid}, ops))
+end
+function (F::HipUserResidual)(res::HipVector, u::HipVector, p)
+    check(ccall((:nk_residual, libnkhip), Cint, (VP, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}),
+                u.ctx.ptr, problem(F, u, p), res.ptr, u.ptr), u.ctx, "F!")
+    return nothing
+end
+const AnyHipResidual = Union{HipResidual, HipUserResidual}
 
 function (F::HipResidual)(res::HipVector, u::HipVector, p)
     check(ccall((:nk_residual, libnkhip), Cint, (VP, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}),
@@ -154,7 +194,7 @@ function (F::HipResidual)(res::HipVector, u::HipVector, p)
 end
 
 # mul!(out, J, v): more specific than Ariadne's Enzyme method (src/Ariadne.jl:48) by dispatch
-function mul!(out::HipVector, J::Ariadne.JacobianOperator{<:HipResidual, <:HipVector}, v::HipVector)
+function mul!(out::HipVector, J::Ariadne.JacobianOperator{<:AnyHipResidual, <:HipVector}, v::HipVector)
     F0 = J.f.jv == NK_JV_FD ? J.res.ptr : Ptr{Float64}(C_NULL)
     check(ccall((:nk_jv, libnkhip), Cint, (VP, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int32, Float64),
                 out.ctx.ptr, problem(J.f, J.u, J.p), out.ptr, J.u.ptr, v.ptr, F0, J.f.jv, 0.0), out.ctx, "mul!")
@@ -209,7 +249,7 @@ function Krylov.krylov_workspace(method::Symbol, kc::KrylovConstructor{<:HipVect
     return ws
 end
 
-function Krylov.krylov_solve!(ws::HipKrylovWorkspace, J::Ariadne.JacobianOperator{<:HipResidual, <:HipVector}, b::HipVector;
+function Krylov.krylov_solve!(ws::HipKrylovWorkspace, J::Ariadne.JacobianOperator{<:AnyHipResidual, <:HipVector}, b::HipVector;
                               restart::Bool = false, reorthogonalization::Bool = false, itmax::Integer = 0,
                               atol::Real = sqrt(eps(Float64)), rtol::Real = sqrt(eps(Float64)), kwargs...)
     opts = NkKrylovOpts(restart, reorthogonalization, itmax, J.f.jv, atol, rtol)
