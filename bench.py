@@ -62,7 +62,7 @@ def parse():
     ap.add_argument("--itmax", type=int, default=300)
     ap.add_argument("--jv", choices=["fd", "exact"], default="fd")
     ap.add_argument("--no-prof", action="store_true", help="do not time kernels with HIP events")
-    ap.add_argument("--prof-every", type=int, default=16,
+    ap.add_argument("--prof-every", type=int, default=64,
                     help="time every k-th launch of each kernel class (HIP events; k > 1 keeps their cost out)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-itmax", type=int, default=300, help="Arnoldi steps in the CPU-baseline sample (300 = one bench step)")
