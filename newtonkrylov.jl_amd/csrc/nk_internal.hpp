@@ -148,7 +148,7 @@ int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red);
 
 int launch_dot(nk_ctx* c, int64_t n, const double* x, const double* y, Red* red);
 int launch_sumsq(nk_ctx* c, int64_t n, const double* x, Red* red);
-int launch_finalize(nk_ctx* c, Red r, double* dst, int sqrt_it);  // dst[0] = sum (or sqrt(sum))
+int launch_finalize(nk_ctx* c, Red r, double* dst, int sqrt_it, double* mirror = nullptr);  // dst[0] = sum (or sqrt(sum))
 int launch_axpy(nk_ctx* c, int64_t n, double s, const double* x, double* y);
 int launch_axpby(nk_ctx* c, int64_t n, double s, const double* x, double t, double* y);
 int launch_scal(nk_ctx* c, int64_t n, double s, double* x);
@@ -157,9 +157,9 @@ int launch_fill(nk_ctx* c, int64_t n, double* x, double v);
 int launch_divcopy(nk_ctx* c, int64_t n, double* y, const double* x, double s);
 int launch_ref(nk_ctx* c, int64_t n, double* x, double* y, double cc, double ss);
 // one fused modified-Gram-Schmidt pass: h = Σ in; q -= h vi; partials of <vnext, q> (or <q,q>
-// when vnext == nullptr).  Block 0 stores h at h_out.
+// when vnext == nullptr).  Block 0 stores h at h_out (and at h_host, a mapped host address, if given).
 int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const double* vnext, Red in,
-                    double* h_out, Red* out, int rev);
+                    double* h_out, double* h_host, Red* out, int rev);
 // xr = Σ_i y_i V_i (fma chain from 0 in i order, y on device); then x = x + xr (restart) or
 // x = xr; optional partial sums of ||x||^2.
 int launch_update_x(nk_ctx* c, int64_t n, double* x, double* xr, const double* const* V, int k,

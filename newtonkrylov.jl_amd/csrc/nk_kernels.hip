@@ -600,10 +600,17 @@ __global__ __launch_bounds__(kBlock) void k_sumsq(int64_t n, const double* __res
     publish(acc, part, fin, sh);
 }
 
-__global__ __launch_bounds__(kBlock) void k_finalize(const double* __restrict__ in, int len, double* __restrict__ dst, int sqrt_it) {
+// dst[0] = Σ in (or its sqrt); `mirror` (optional): the same value into mapped host memory, so
+// the host can read it after the stream event without a separate device-to-host copy
+__global__ __launch_bounds__(kBlock) void k_finalize(const double* __restrict__ in, int len, double* __restrict__ dst, int sqrt_it,
+                                                    double* __restrict__ mirror) {
     __shared__ double sh[8];
     const double t = reduce_input(in, len, sh);
-    if (threadIdx.x == 0) dst[0] = sqrt_it ? sqrt(t) : t;
+    if (threadIdx.x == 0) {
+        const double r = sqrt_it ? sqrt(t) : t;
+        dst[0] = r;
+        if (mirror) mirror[0] = r;
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_axpy(int64_t n, double s, const double* __restrict__ x, double* __restrict__ y) {
@@ -709,7 +716,8 @@ __device__ __forceinline__ void st2(dx2* p, dx2 v) {
 template <bool HAS_NEXT, int U, bool NT, bool NTW = false, bool CH = false>
 __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restrict__ q, const double* __restrict__ vi,
                                                     const double* __restrict__ vnext, const double* __restrict__ red_in,
-                                                    int red_len, double* __restrict__ h_out, double* __restrict__ part,
+                                                    int red_len, double* __restrict__ h_out, double* __restrict__ h_host,
+                                                    double* __restrict__ part,
                                                     int rev, int fin) {
     __shared__ double sh[8];
     dx2* q2 = reinterpret_cast<dx2*>(q);
@@ -743,7 +751,10 @@ __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restri
         }
     }
     const double h = reduce_input(red_in, red_len, sh);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *h_out = h;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *h_out = h;
+        if (h_host) *h_host = h;  // mapped host mirror of the Hessenberg column
+    }
     const double mh = -h;
     double acc = 0.0;
     for (; have; i += U * st, have = i + (U - 1) * st < lim) {
@@ -1065,8 +1076,9 @@ int launch_sumsq(nk_ctx* c, int64_t n, const double* x, Red* red) {
     return launch(c, "norm", 8.0 * n, [&] { hipLaunchKernelGGL(k_sumsq, dim3(g), dim3(kBlock), 0, c->stream, n, x, part, fin); });
 }
 
-int launch_finalize(nk_ctx* c, Red r, double* dst, int sqrt_it) {
-    return launch(c, "finalize", 0.0, [&] { hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, c->stream, r.ptr, r.len, dst, sqrt_it); });
+int launch_finalize(nk_ctx* c, Red r, double* dst, int sqrt_it, double* mirror) {
+    return launch(c, "finalize", 0.0,
+                  [&] { hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, c->stream, r.ptr, r.len, dst, sqrt_it, mirror); });
 }
 
 #define NK_STREAM_LAUNCH(name, bytes_per, kern, ...)                                              \
@@ -1089,20 +1101,21 @@ int launch_ref(nk_ctx* c, int64_t n, double* x, double* y, double cc, double ss)
 namespace {
 template <bool HAS_NEXT>
 void mgs_dispatch(int variant, int g, hipStream_t s, int64_t n, double* q, const double* vi, const double* vn,
-                  const double* red, int len, double* h, double* part, int rev, int fin) {
+                  const double* red, int len, double* h, double* hm, double* part, int rev, int fin) {
     switch (variant) {  // unroll depth x non-temporal V_i loads (tools/kbench.py measures them)
-    case 0: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, false>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev, fin); break;
-    case 1: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev, fin); break;
-    case 2: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev, fin); break;
-    case 3: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev, fin); break;
-    case 4: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev, fin); break;
-    case 5: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, false, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev, fin); break;
-    default: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true, false, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, part, rev, fin); break;
+    case 0: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, false>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
+    case 1: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
+    case 2: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
+    case 3: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
+    case 4: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
+    case 5: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, false, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
+    default: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true, false, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
     }
 }
 }  // namespace
 
-int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const double* vnext, Red in, double* h_out, Red* out,
+int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const double* vnext, Red in, double* h_out,
+                    double* h_host, Red* out,
                     int rev) {
     static const int variant = env_int("NK_MGS_VARIANT", kMgsVariant);
     const int g = red_blocks(n);
@@ -1110,10 +1123,10 @@ int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const dou
     double* part = red_out(c, g, out, &fin);
     if (vnext)
         return launch(c, "mgs_pass", 32.0 * n, [&] {
-            mgs_dispatch<true>(variant, g, c->stream, n, q, vi, vnext, in.ptr, in.len, h_out, part, rev, fin);
+            mgs_dispatch<true>(variant, g, c->stream, n, q, vi, vnext, in.ptr, in.len, h_out, h_host, part, rev, fin);
         });
     return launch(c, "mgs_pass_last", 24.0 * n, [&] {
-        mgs_dispatch<false>(variant, g, c->stream, n, q, vi, vnext, in.ptr, in.len, h_out, part, rev, fin);
+        mgs_dispatch<false>(variant, g, c->stream, n, q, vi, vnext, in.ptr, in.len, h_out, h_host, part, rev, fin);
     });
 }
 
@@ -1209,8 +1222,8 @@ extern "C" int nkb_mgs_seq(nk_ctx* c, int64_t n, int k, int variant, int alt, in
             const int rev = alt ? (i & 1) : 0;
             const double* in = parts[i & 1];
             double* out = parts[(i + 1) & 1];
-            if (i + 1 < k) mgs_dispatch<true>(variant, g, c->stream, n, q, V[i], V[i + 1], in, g, hs + 1, out, rev, 0);
-            else mgs_dispatch<false>(variant, g, c->stream, n, q, V[i], nullptr, in, g, hs + 1, out, rev, 0);
+            if (i + 1 < k) mgs_dispatch<true>(variant, g, c->stream, n, q, V[i], V[i + 1], in, g, hs + 1, nullptr, out, rev, 0);
+            else mgs_dispatch<false>(variant, g, c->stream, n, q, V[i], nullptr, in, g, hs + 1, nullptr, out, rev, 0);
         }
     };
     sweep();

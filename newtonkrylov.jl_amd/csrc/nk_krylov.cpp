@@ -38,7 +38,8 @@ struct nk_workspace {
     std::vector<double*> V;
     double* hdev = nullptr;  // device Hessenberg columns: 2 slots of (2*cap + 2) doubles (steps k, k+1 in flight)
     double* ydev = nullptr;  // device y (cap doubles)
-    double* hpin = nullptr;  // pinned host mirror of hdev (2 slots)
+    double* hpin = nullptr;  // pinned host mirror of hdev (2 slots), written by the kernels themselves
+    double* hpin_dev = nullptr;  // hpin's device address
     double* ypin = nullptr;  // pinned host y
     hipEvent_t col_ready[2] = {nullptr, nullptr};  // Hessenberg column of slot s has landed in hpin
     int cap = 0;             // capacity of hdev / ydev / pinned buffers (in basis vectors)
@@ -59,7 +60,8 @@ int ws_scalars(nk_workspace* ws, int need) {
     double *hdev = nullptr, *ydev = nullptr, *hpin = nullptr, *ypin = nullptr;
     NK_HIP(c, hipMalloc(&hdev, sizeof(double) * 2 * nstride));
     NK_HIP(c, hipMalloc(&ydev, sizeof(double) * (size_t)cap));
-    NK_HIP(c, hipHostMalloc(&hpin, sizeof(double) * 2 * nstride, hipHostMallocDefault));
+    // fine-grained (coherent) so the kernels' stores are host-visible once the step's event fires
+    NK_HIP(c, hipHostMalloc(&hpin, sizeof(double) * 2 * nstride, hipHostMallocMapped | hipHostMallocCoherent));
     NK_HIP(c, hipHostMalloc(&ypin, sizeof(double) * (size_t)cap, hipHostMallocDefault));
     if (ws->cap) {
         for (int slot = 0; slot < 2; ++slot) {
@@ -76,6 +78,7 @@ int ws_scalars(nk_workspace* ws, int need) {
     ws->ydev = ydev;
     ws->hpin = hpin;
     ws->ypin = ypin;
+    NK_HIP(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&ws->hpin_dev), hpin, 0));
     ws->cap = cap;
     return NK_OK;
 }
@@ -213,12 +216,14 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
     // reading h from the device and storing V_k on the way (fused kdivcopy!).
     auto slot_dev = [&](int k) { return ws->hdev + (size_t)(k & 1) * (2 * ws->cap + 2); };
     auto slot_pin = [&](int k) { return ws->hpin + (size_t)(k & 1) * (2 * ws->cap + 2); };
+    auto slot_pin_dev = [&](int k) { return ws->hpin_dev + (size_t)(k & 1) * (2 * ws->cap + 2); };
     auto npasses_of = [&](int k) { return reorth ? 2 * k : k; };
     auto issue = [&](int k) -> int {
         NK_TRY(ws_basis(ws, k));
         NK_TRY(ws_scalars(ws, k + 1));
         const int np = npasses_of(k);
         double* col = slot_dev(k);
+        double* colh = slot_pin_dev(k);  // the kernels mirror every entry into pinned host memory
         double* q = W[k & 1];
         Red red{};
         if (k == 1) {
@@ -232,13 +237,12 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
             const double* vnext = (t + 1 < np) ? ws->V[(t + 1) % k] : nullptr;
             NK_TRY(finish_reduction(c, &red));
             Red nxt{};
-            NK_TRY(launch_mgs_pass(c, n, q, vi, vnext, red, col + t, &nxt, mgs_alt ? (t & 1) : 0));
+            NK_TRY(launch_mgs_pass(c, n, q, vi, vnext, red, col + t, colh + t, &nxt, mgs_alt ? (t & 1) : 0));
             red = nxt;
         }
         NK_TRY(finish_reduction(c, &red));
-        NK_TRY(launch_finalize(c, red, col + np, 1));  // h_{k+1,k} = ||q||
-        NK_HIP(c, hipMemcpyAsync(slot_pin(k), col, sizeof(double) * (np + 1), hipMemcpyDeviceToHost, c->stream));
-        NK_HIP(c, hipEventRecord(ws->col_ready[k & 1], c->stream));
+        NK_TRY(launch_finalize(c, red, col + np, 1, colh + np));  // h_{k+1,k} = ||q||
+        NK_HIP(c, hipEventRecord(ws->col_ready[k & 1], c->stream));  // column complete in pinned memory
         return NK_OK;
     };
 
