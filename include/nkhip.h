@@ -153,6 +153,35 @@ int nk_krylov_solve(nk_workspace* ws, const nk_problem* p, const double* u, cons
                     const nk_krylov_opts* opts, nk_krylov_stats* stats, double* hist, int64_t hist_cap,
                     int64_t* hist_len);
 
+/* ---------------------------------------------------------------- the Newton driver
+ * newton_krylov!(F!, u, p, res; kwargs...) (src/Ariadne.jl:288-372) for C / C++ callers: the same
+ * loop the Julia and Python hosts run, on top of the calls above.  u is updated in place, res
+ * holds F(u) on return. */
+#define NK_FORCING_NONE 0   /* forcing = nothing: Krylov's own rtol                        */
+#define NK_FORCING_FIXED 1  /* Fixed(η), src/Ariadne.jl:185-192                             */
+#define NK_FORCING_EW 2     /* EisenstatWalker(η_max, γ), src/Ariadne.jl:197-217 (default)  */
+typedef struct nk_newton_opts {
+    double tol_rel, tol_abs;      /* 1e-6, 1e-12: tol = tol_rel ||F(u0)|| + tol_abs            */
+    int32_t max_niter;            /* 50 (the loop runs while outer <= max_niter, :336)         */
+    int32_t forcing;              /* NK_FORCING_*                                              */
+    double eta;                   /* Fixed η (0.1)                                             */
+    double eta_max, gamma;        /* EisenstatWalker (0.999, 0.9)                              */
+    int32_t algo;                 /* NK_ALGO_GMRES / NK_ALGO_CG                                */
+    int32_t memory;               /* Krylov workspace memory (20)                              */
+    nk_krylov_opts krylov;        /* krylov_kwargs; jv_mode selects the operator               */
+    int32_t rtol_user;            /* krylov.rtol came from krylov_kwargs: it wins (:330-333)   */
+} nk_newton_opts;
+typedef struct nk_newton_stats {
+    int64_t outer_iterations, inner_iterations;  /* Stats (src/Ariadne.jl:265-276)            */
+    double n_res, tol;
+    int32_t solved;               /* n_res <= tol (:370)                                       */
+    int64_t n_matvec, n_residual; /* mul!(J) and F! evaluations                                */
+} nk_newton_stats;
+int nk_newton_defaults(nk_newton_opts* opts);
+/* nres_hist (optional, host): ||F|| after every Newton step, starting with ||F(u0)||. */
+int nk_newton_krylov(nk_ctx* ctx, const nk_problem* p, double* u, double* res, const nk_newton_opts* opts,
+                     nk_newton_stats* stats, double* nres_hist, int64_t hist_cap, int64_t* hist_len);
+
 /* ---------------------------------------------------------------- multi-GPU (one process per GPU)
  * Slab decomposition along the slowest axis; rank r's lower/upper neighbours are r-1 / r+1.
  * After nk_dist_init every residual / Jv exchanges ghost planes (RCCL send/recv over xGMI) and

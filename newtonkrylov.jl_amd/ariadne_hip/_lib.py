@@ -55,6 +55,20 @@ class nk_krylov_stats(C.Structure):
                 ("breakdown", C.c_int32), ("status", C.c_int32), ("n_matvec", C.c_int64)]
 
 
+NK_FORCING_NONE, NK_FORCING_FIXED, NK_FORCING_EW = 0, 1, 2
+
+
+class nk_newton_opts(C.Structure):
+    _fields_ = [("tol_rel", C.c_double), ("tol_abs", C.c_double), ("max_niter", C.c_int32), ("forcing", C.c_int32),
+                ("eta", C.c_double), ("eta_max", C.c_double), ("gamma", C.c_double), ("algo", C.c_int32),
+                ("memory", C.c_int32), ("krylov", nk_krylov_opts), ("rtol_user", C.c_int32)]
+
+
+class nk_newton_stats(C.Structure):
+    _fields_ = [("outer_iterations", C.c_int64), ("inner_iterations", C.c_int64), ("n_res", C.c_double),
+                ("tol", C.c_double), ("solved", C.c_int32), ("n_matvec", C.c_int64), ("n_residual", C.c_int64)]
+
+
 class nk_prof_entry(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("timed", C.c_int64), ("total_ms", C.c_double),
                 ("bytes", C.c_double)]
@@ -91,6 +105,9 @@ SIGNATURES = {
     "nk_workspace_x": (_VP, [_VP]),
     "nk_krylov_solve": (C.c_int, [_VP, _PP, _VP, _VP, _VP, C.POINTER(nk_krylov_opts), C.POINTER(nk_krylov_stats),
                                   _PD, _I64, C.POINTER(_I64)]),
+    "nk_newton_defaults": (C.c_int, [C.POINTER(nk_newton_opts)]),
+    "nk_newton_krylov": (C.c_int, [_VP, _PP, _VP, _VP, C.POINTER(nk_newton_opts), C.POINTER(nk_newton_stats),
+                                   _PD, _I64, C.POINTER(_I64)]),
     "nk_dist_unique_id": (C.c_int, [C.c_char_p]),
     "nk_dist_init": (C.c_int, [_VP, _I32, _I32, C.c_char_p]),
     "nk_dist_allreduce_sum": (C.c_int, [_VP, _VP, _I64]),

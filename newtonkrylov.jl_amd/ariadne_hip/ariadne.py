@@ -192,6 +192,51 @@ def newton_krylov_(F_: DeviceResidual, u: DeviceArray, p=None, res: DeviceArray 
     return u, Result(n_res <= tol, stats, t, n_matvec)
 
 
+def newton_krylov_native(F_: DeviceResidual, u: DeviceArray, p=None, res: DeviceArray | None = None, *,
+                         tol_rel: float = 1.0e-6, tol_abs: float = 1.0e-12, max_niter: int = 50,
+                         forcing: Forcing | None = EisenstatWalker(), algo: str = "gmres",
+                         krylov_kwargs: dict | None = None, memory: int = 20, jv: str = "exact"):
+    """newton_krylov_ with the loop itself in libnkhip.so (nk_newton_krylov, the C/C++ callers' entry
+    point).  Same arguments, same result; returns (u, Result) with the histories of ||F||."""
+    kk = dict(krylov_kwargs or {})
+    unknown = set(kk) - {"restart", "reorthogonalization", "itmax", "atol", "rtol"}
+    if unknown:
+        raise TypeError(f"unsupported Krylov keyword(s): {sorted(unknown)}")
+    if res is None:
+        res = u.zero()
+    o = _lib.nk_newton_opts()
+    load().nk_newton_defaults(C.byref(o))
+    o.tol_rel, o.tol_abs, o.max_niter = float(tol_rel), float(tol_abs), int(max_niter)
+    if forcing is None:
+        o.forcing = _lib.NK_FORCING_NONE
+    elif isinstance(forcing, Fixed):
+        o.forcing, o.eta = _lib.NK_FORCING_FIXED, float(forcing.eta)
+    elif isinstance(forcing, EisenstatWalker):
+        o.forcing, o.eta_max, o.gamma = _lib.NK_FORCING_EW, float(forcing.eta_max), float(forcing.gamma)
+    else:
+        raise TypeError("forcing must be Fixed, EisenstatWalker or None")
+    o.algo = {"gmres": _lib.NK_ALGO_GMRES, "cg": _lib.NK_ALGO_CG}[str(algo).lstrip(":")]
+    o.memory = int(memory)
+    o.krylov.restart = int(bool(kk.get("restart", False)))
+    o.krylov.reorthogonalization = int(bool(kk.get("reorthogonalization", False)))
+    o.krylov.itmax = int(kk.get("itmax", 0))
+    o.krylov.jv_mode = _lib.NK_JV_FD if jv == "fd" else _lib.NK_JV_EXACT
+    o.krylov.atol = float(kk.get("atol", o.krylov.atol))
+    if "rtol" in kk:
+        o.krylov.rtol, o.rtol_user = float(kk["rtol"]), 1
+    st = _lib.nk_newton_stats()
+    cap = int(max_niter) + 2
+    hist = (C.c_double * cap)()
+    hl = C.c_int64(0)
+    t0 = time.perf_counter_ns()
+    prob = F_.problem(u, p)
+    u.ctx.check(load().nk_newton_krylov(u.ctx.handle, C.byref(prob), u.ptr, res.ptr, C.byref(o), C.byref(st), hist,
+                                        cap, C.byref(hl)), "nk_newton_krylov")
+    t = (time.perf_counter_ns() - t0) / 1.0e9
+    stats = Stats(int(st.outer_iterations), int(st.inner_iterations), float(st.n_res))
+    return u, Result(bool(st.solved), stats, t, int(st.n_matvec))
+
+
 def newton_krylov(F: DeviceResidual, u0: DeviceArray, p=None, **kwargs):
     """newton_krylov(F, u₀, p; kwargs...) -- out-of-place form (src/Ariadne.jl:245-248).
     The device residual computes in place; u₀ is not modified."""
