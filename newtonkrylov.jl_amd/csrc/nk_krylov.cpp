@@ -191,7 +191,8 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
 
     NK_TRY(ws_basis(ws, mem));
     NK_TRY(ws_scalars(ws, mem + 1));
-    NK_TRY(launch_fill(c, n, x, 0.0));  // x .= 0 ; r0 = b - A*0 = b
+    // x .= 0 ; r0 = b - A*0 = b.  x is only materialised when no cycle runs: the first cycle's
+    // update writes x = Σ y_i V_i directly (bit-identical to 0 + Σ y_i V_i), saving a pass over x.
     Red rb{};
     NK_TRY(launch_sumsq(c, n, b, &rb));
     double beta = 0.0;
@@ -202,6 +203,7 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
     st->inconsistent = 0;
     st->breakdown = 0;
     if (beta == 0.0) {
+        NK_TRY(launch_fill(c, n, x, 0.0));
         st->niter = 0;
         st->solved = 1;
         st->status = 1;
@@ -336,12 +338,14 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         tired = iter >= itmax;
         const bool need_xnorm = restart && A.mode == NK_JV_FD && !(solved || tired || breakdown);
         Red xr{};
-        NK_TRY(launch_update_x(c, n, x, ws->xr, ws->V.data(), kk, ws->ydev, restart, need_xnorm ? &xr : nullptr));
+        NK_TRY(launch_update_x(c, n, x, ws->xr, ws->V.data(), kk, ws->ydev, restart && npass > 1,
+                               need_xnorm ? &xr : nullptr));
         if (need_xnorm) NK_TRY(host_scalar(c, xr, 1, &xnorm));
         else {
             NK_HIP(c, hipStreamSynchronize(c->stream));  // ypin may be rewritten next cycle
         }
     }
+    if (npass == 0) NK_TRY(launch_fill(c, n, x, 0.0));  // solved (or tired) before the first cycle
     st->niter = iter;
     st->solved = solved;
     st->inconsistent = inconsistent;
