@@ -240,6 +240,8 @@ def main():
         obj = [ah.dist_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         ctx.init_distributed(rank, world, obj[0])
+    elif os.environ.get("NK_DIST_FORCE") == "1":  # diagnostic: a 1-rank RCCL communicator (every reduction
+        ctx.init_distributed(0, 1, ah.dist_unique_id())  # pays the all-reduce path on one GPU)
 
     if args.workload == "bratu2d":
         W = Bratu2D(args, ctx, rank, world)

@@ -43,17 +43,26 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
 
 // fixed-order sum of in[0..len), broadcast to the whole block.  All 256 threads load (8
 // independent loads in flight each), so a block pays ~one L2 round trip, not 32 dependent ones.
+// SC1 = true reads with agent-scope (sc1) loads: values other blocks of the SAME launch stored
+// write-through (publish), which this CU's L1 or this XCD's L2 may hold stale copies of.
+template <bool SC1 = false>
+__device__ __forceinline__ double ld_part(const double* p) {
+    if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return *p;
+}
+
+template <bool SC1 = false>
 __device__ __forceinline__ double reduce_input(const double* __restrict__ in, int len, double* sh) {
     double t = 0.0;
     int m = threadIdx.x;
     for (; m + 7 * kBlock < len; m += 8 * kBlock) {
         double a[8];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) a[r] = in[m + r * kBlock];
+        for (int r = 0; r < 8; ++r) a[r] = ld_part<SC1>(in + m + r * kBlock);
 #pragma unroll
         for (int r = 0; r < 8; ++r) t += a[r];
     }
-    for (; m < len; m += kBlock) t += in[m];
+    for (; m < len; m += kBlock) t += ld_part<SC1>(in + m);
     t = block_sum(t, sh);
     if (threadIdx.x == 0) sh[4] = t;
     __syncthreads();
@@ -64,24 +73,29 @@ __device__ __forceinline__ double reduce_input(const double* __restrict__ in, in
 // arrive also folds all partials -- the same fixed-order sum k_finalize computes -- into
 // part[kRedCap - 1], so the RCCL all-reduce can follow without a separate finaliser launch.  The
 // arrival counter lives in part[kRedCap - 2] and is reset by that last block.
+// Hand-off without fences (cdna_hip_programming.md §6 Guideline 16, R1/R2 forms): the partial is
+// stored write-through (agent-scope atomic store = sc1) and drained before the ticket; the last
+// block reads the partials with sc1 loads.  An agent-scope RELEASE fence here would write back the
+// XCD's whole L2 -- full of this kernel's streamed output -- once per block (measured: 2x slower).
 __device__ __forceinline__ void publish(double acc, double* part, int fin, double* sh) {
     __shared__ unsigned ticket;
     const double s = block_sum(acc, sh);
-    if (threadIdx.x == 0) part[blockIdx.x] = s;
-    if (!fin) return;
+    if (!fin) {
+        if (threadIdx.x == 0) part[blockIdx.x] = s;
+        return;
+    }
     unsigned* cnt = reinterpret_cast<unsigned*>(part + kRedCap - 2);
     if (threadIdx.x == 0) {  // the partial's only writer is this lane
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep: the fence's own wait can be dropped
+        __hip_atomic_store(part + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         ticket = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (ticket != gridDim.x - 1) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // drop stale L1 lines before reading the partials
-    const double t = reduce_input(part, (int)gridDim.x, sh);
+    const double t = reduce_input<true>(part, (int)gridDim.x, sh);
     if (threadIdx.x == 0) {
         part[kRedCap - 1] = t;
-        *cnt = 0u;
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
