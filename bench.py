@@ -13,11 +13,13 @@ operator (F(u + eps v) - F(u)) / eps (--jv exact selects the dual-number tangent
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): weak scaling, every rank owns
 a 4096 x 4096 slab of a 4096 x (4096 N) grid; ghost rows go over RCCL send/recv and every inner
 product is an RCCL all-reduce.  `value` counts slab matvecs (4096^2-DoF operator applications)
-summed over ranks.
+summed over ranks.  --global-n G instead splits ONE G x G problem into G/N-row slabs (strong
+scaling; --gpus 8 --global-n 16384 is BASELINE config 4); `value` then counts global matvecs.
 
 Timing: W warm-up steps, barrier + device sync, K timed steps, barrier + device sync; the max over
 ranks is reported.  Inputs are resident in HBM before the timed region.  Per-kernel durations come
-from HIP events recorded around every launch on the library's stream inside the timed region.
+from HIP events recorded around every 64th launch of each kernel class on the library's stream
+inside the timed region.
 """
 from __future__ import annotations
 
@@ -58,6 +60,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--n", type=int, default=0, help="per-GPU slab side (default 4096 / 8192 / 512 by workload)")
+    ap.add_argument("--global-n", type=int, default=0,
+                    help="bratu2d strong scaling: one global N x N problem in row slabs over the GPUs "
+                         "(--gpus 8 --global-n 16384 is BASELINE config 4)")
     ap.add_argument("--memory", type=int, default=0, help="Krylov memory (default 30 for bratu2d, 20 for heat)")
     ap.add_argument("--itmax", type=int, default=300)
     ap.add_argument("--jv", choices=["fd", "exact"], default="fd")
@@ -83,14 +88,20 @@ class Bratu2D:
     """BASELINE config 2: one inexact-Newton step of 2D Bratu with GMRES(30) and a fixed Krylov budget."""
 
     def __init__(self, args, ctx, rank, world):
-        n = args.n or 4096
-        self.n, self.world = n, world
-        ny_glob = n * world
+        if args.global_n:  # strong scaling: one global G x G problem, G / world rows per rank
+            G = args.global_n
+            if G % world:
+                raise SystemExit(f"--global-n {G} must be divisible by the number of GPUs {world}")
+            n, ny_glob, rows = G, G, G // world
+        else:  # weak scaling: an n x n slab per rank
+            n = args.n or 4096
+            ny_glob, rows = n * world, n
+        self.n, self.world, self.rows = n, world, rows
         self.hx, self.hy = 1.0 / (n + 1), 1.0 / (ny_glob + 1)
         xs = np.arange(1, n + 1) * self.hx
-        ys = np.arange(rank * n + 1, rank * n + n + 1) * self.hy
+        ys = np.arange(rank * rows + 1, rank * rows + rows + 1) * self.hy
         u0 = np.ascontiguousarray(np.sin(np.pi * ys)[:, None] * np.sin(np.pi * xs)[None, :])
-        grid = ah.Grid((n, n), (n, ny_glob), rank * n)
+        grid = ah.Grid((n, rows), (n, ny_glob), rank * rows)
         self.u0 = u0
         self.u = ah.DeviceArray.from_numpy(u0, grid, ctx)
         self.res = self.u.zero()
@@ -99,7 +110,9 @@ class Bratu2D:
         self.kw = dict(restart=True, rtol=0.0, atol=0.0, itmax=args.itmax)
         self.args = args
         self.jv_kernel = "jv_fd_dot_norm" if args.jv == "fd" else "jv_exact_dot_norm"
-        self.workload = (f"2D Bratu {n}x{n * world} ({n}x{n} per GPU), one inexact-Newton step per step: "
+        self.scaling = "strong" if args.global_n else "weak"
+        self.units_per_matvec = 1 if args.global_n else world  # matvecs counted over the whole problem
+        self.workload = (f"2D Bratu {n}x{ny_glob} ({n}x{rows} per GPU), one inexact-Newton step per step: "
                          f"GMRES({args.memory}) restart, itmax={args.itmax}, rtol=atol=0, {args.jv.upper()} Jv")
         self.metric = f"Krylov matvecs/sec + achieved HBM GB/s, 2D Bratu {n}^2"
 
@@ -319,7 +332,7 @@ def main():
     jv_kernel = W.jv_kernel  # the Jv fused with V_k = q / h
 
     if rank == 0:
-        value = matvecs * world / elapsed
+        value = matvecs * getattr(W, "units_per_matvec", world) / elapsed
         out = {
             "metric": W.metric,
             "value": round(value, 3),
@@ -329,7 +342,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": getattr(W, "scaling", "weak"),
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (see config.workload)",
