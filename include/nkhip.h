@@ -120,6 +120,9 @@ int nk_scal(nk_ctx* ctx, int64_t n, double s, double* x);                       
 int nk_axpy(nk_ctx* ctx, int64_t n, double s, const double* x, double* y);             /* y = s x + y   */
 int nk_axpby(nk_ctx* ctx, int64_t n, double s, const double* x, double t, double* y);  /* y = s x + t y */
 int nk_copy(nk_ctx* ctx, int64_t n, double* y, const double* x);                       /* y = x         */
+/* y = s x + y and ||y|| in one pass: the Newton update u .-= d (src/Ariadne.jl:344) together with the
+ * ||u|| the next FD operator needs (nk_krylov_opts.u_norm). */
+int nk_axpy_norm(nk_ctx* ctx, int64_t n, double s, const double* x, double* y, double* ynorm);
 int nk_fill(nk_ctx* ctx, int64_t n, double* x, double v);                              /* x .= v        */
 int nk_divcopy(nk_ctx* ctx, int64_t n, double* y, const double* x, double s);          /* y = x / s     */
 int nk_ref(nk_ctx* ctx, int64_t n, double* x, double* y, double c, double s);          /* Givens        */
@@ -135,6 +138,8 @@ typedef struct nk_krylov_opts {
     int32_t itmax;                /* 0 => 2n                                          */
     int32_t jv_mode;              /* NK_JV_EXACT / NK_JV_FD                           */
     double atol, rtol;            /* Krylov stopping: ||r|| <= atol + rtol ||b||      */
+    double b_norm;                /* > 0: ||b|| is known (the Newton loop just computed ||F(u)||): not recomputed */
+    double u_norm;                /* > 0: ||u|| is known (FD step size): not recomputed                          */
 } nk_krylov_opts;
 
 typedef struct nk_krylov_stats {

@@ -9,7 +9,7 @@ from .ariadne import (EisenstatWalker, Fixed, Forcing, JacobianOperator, Result,
 from .device import Context, DeviceArray, Grid, default_context, set_default_context
 from .distributed import dist_unique_id, init_distributed, slab
 from .implicit import G_Euler_, G_Midpoint_, G_Trapezoid_, diffusion3d_, diffusion_, solve
-from .krylov import (KrylovConstructor, kaxpby_, kaxpy_, kcopy_, kdivcopy_, kdot, kfill_, knorm, kref_, krylov_solve_,
+from .krylov import (KrylovConstructor, kaxpby_, kaxpy_, kaxpy_norm_, kcopy_, kdivcopy_, kdot, kfill_, knorm, kref_, krylov_solve_,
                      krylov_workspace, kscal_)
 from .problems import DeviceResidual, UserResidual, bc_zero_, bratu2d_, bratu_, heat2d_euler_, heat3d_euler_
 
@@ -17,7 +17,7 @@ __all__ = [
     "NKError", "device_count", "load", "EisenstatWalker", "Fixed", "Forcing", "JacobianOperator", "Result", "Stats",
     "mul_", "newton_krylov", "newton_krylov_", "newton_krylov_native", "Context", "DeviceArray", "Grid", "default_context",
     "set_default_context", "dist_unique_id", "init_distributed", "slab", "G_Euler_", "G_Midpoint_", "G_Trapezoid_", "diffusion_", "diffusion3d_", "solve",
-    "KrylovConstructor", "kaxpby_", "kaxpy_", "kcopy_", "kdivcopy_", "kdot", "kfill_", "knorm", "kref_",
+    "KrylovConstructor", "kaxpby_", "kaxpy_", "kaxpy_norm_", "kcopy_", "kdivcopy_", "kdot", "kfill_", "knorm", "kref_",
     "krylov_solve_", "krylov_workspace", "kscal_", "DeviceResidual", "UserResidual", "bc_zero_", "bratu2d_", "bratu_",
     "heat2d_euler_", "heat3d_euler_",
 ]

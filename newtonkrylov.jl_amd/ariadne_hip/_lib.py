@@ -47,7 +47,8 @@ class nk_user_ops(C.Structure):
 
 class nk_krylov_opts(C.Structure):
     _fields_ = [("restart", C.c_int32), ("reorthogonalization", C.c_int32), ("itmax", C.c_int32),
-                ("jv_mode", C.c_int32), ("atol", C.c_double), ("rtol", C.c_double)]
+                ("jv_mode", C.c_int32), ("atol", C.c_double), ("rtol", C.c_double), ("b_norm", C.c_double),
+                ("u_norm", C.c_double)]
 
 
 class nk_krylov_stats(C.Structure):
@@ -97,6 +98,7 @@ SIGNATURES = {
     "nk_axpy": (C.c_int, [_VP, _I64, _D, _VP, _VP]),
     "nk_axpby": (C.c_int, [_VP, _I64, _D, _VP, _D, _VP]),
     "nk_copy": (C.c_int, [_VP, _I64, _VP, _VP]),
+    "nk_axpy_norm": (C.c_int, [_VP, _I64, _D, _VP, _VP, _PD]),
     "nk_fill": (C.c_int, [_VP, _I64, _VP, _D]),
     "nk_divcopy": (C.c_int, [_VP, _I64, _VP, _VP, _D]),
     "nk_ref": (C.c_int, [_VP, _I64, _VP, _VP, _D, _D]),

@@ -17,7 +17,7 @@ from typing import NamedTuple
 from . import _lib
 from ._lib import load
 from .device import DeviceArray
-from .krylov import KrylovConstructor, kaxpy_, krylov_solve_, krylov_workspace
+from .krylov import KrylovConstructor, kaxpy_norm_, krylov_solve_, krylov_workspace
 from .problems import DeviceResidual
 
 log = logging.getLogger("ariadne_hip")
@@ -163,16 +163,17 @@ def newton_krylov_(F_: DeviceResidual, u: DeviceArray, p=None, res: DeviceArray 
 
     stats = Stats(0, 0, n_res)
     n_matvec = 0
+    u_norm = 0.0  # ||u|| from the fused update below (the FD step size of the next solve); 0 = unknown
     while n_res > tol and stats.outer_iterations <= max_niter:
         kwargs = dict(krylov_kwargs)
         if forcing is not None:
             kwargs = {"rtol": eta, **kwargs}  # user krylov_kwargs win (:330-333)
         # Solve J d = F(u).  The reference passes copy(res) because Enzyme rewrites res inside
         # mul!; the device operator never writes res, so res itself is the right-hand side.
-        krylov_solve_(workspace, J, res, **kwargs)
+        krylov_solve_(workspace, J, res, _b_norm=n_res, _u_norm=u_norm, **kwargs)
         n_matvec += workspace.stats.n_matvec
         d = workspace.x
-        kaxpy_(n, -1.0, d, u)  # u .-= 1 .* d  (Newton step s = 1, :341-344)
+        u_norm = kaxpy_norm_(n, -1.0, d, u)  # u .-= 1 .* d  (Newton step s = 1, :341-344), + ||u||
         n_res_prior = n_res
         n_res = F_.residual_norm(res, u, p)
         callback(u, res, n_res)

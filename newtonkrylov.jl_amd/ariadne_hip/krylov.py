@@ -49,6 +49,14 @@ def kaxpy_(n: int, s: float, x: DeviceArray, y: DeviceArray):
     return y
 
 
+def kaxpy_norm_(n: int, s: float, x: DeviceArray, y: DeviceArray) -> float:
+    """y = s x + y, returning ||y|| from the same pass (nk_axpy_norm): the Newton update u .-= d
+    (src/Ariadne.jl:344) fused with the ||u|| the next FD operator needs."""
+    out = C.c_double()
+    y.ctx.check(load().nk_axpy_norm(_h(y), n, float(s), x.ptr, y.ptr, C.byref(out)), "kaxpy!")
+    return out.value
+
+
 def kaxpby_(n: int, s: float, x: DeviceArray, t: float, y: DeviceArray):
     y.ctx.check(load().nk_axpby(_h(y), n, float(s), x.ptr, float(t), y.ptr), "kaxpby!")
     return y
@@ -138,8 +146,10 @@ def krylov_workspace(algo, kc: KrylovConstructor) -> KrylovWorkspace:
 
 def krylov_solve_(ws: KrylovWorkspace, J, b: DeviceArray, *, restart=False, reorthogonalization=False,
                   atol=SQRT_EPS, rtol=SQRT_EPS, itmax=0, history=False, verbose=0, M=None, N=None, ldiv=False,
-                  **unknown):
-    """krylov_solve!(workspace, J, b; kwargs...) for a JacobianOperator J on device vectors."""
+                  _b_norm=0.0, _u_norm=0.0, **unknown):
+    """krylov_solve!(workspace, J, b; kwargs...) for a JacobianOperator J on device vectors.
+    (_b_norm / _u_norm: norms the Newton loop already holds -- ||F(u)|| and ||u|| -- so the solve
+    does not stream b and u once more just to recompute them.)"""
     if unknown:
         raise TypeError(f"unsupported Krylov keyword(s): {sorted(unknown)}")
     if M is not None or N is not None:
@@ -148,7 +158,7 @@ def krylov_solve_(ws: KrylovWorkspace, J, b: DeviceArray, *, restart=False, reor
         raise TypeError("restart / reorthogonalization are GMRES keywords")
     prob = J.problem()
     opts = _lib.nk_krylov_opts(int(bool(restart)), int(bool(reorthogonalization)), int(itmax), J.jv_mode,
-                               float(atol), float(rtol))
+                               float(atol), float(rtol), float(_b_norm), float(_u_norm))
     st = _lib.nk_krylov_stats()
     cap = ((int(itmax) or 4096) + 64) if history else 0
     hist = (C.c_double * max(cap, 1))()

@@ -317,6 +317,12 @@ int nk_norm(nk_ctx* c, int64_t n, const double* x, double* out) {
 
 int nk_scal(nk_ctx* c, int64_t n, double s, double* x) { return c ? launch_scal(c, n, s, x) : NK_E_ARG; }
 int nk_axpy(nk_ctx* c, int64_t n, double s, const double* x, double* y) { return c ? launch_axpy(c, n, s, x, y) : NK_E_ARG; }
+int nk_axpy_norm(nk_ctx* c, int64_t n, double s, const double* x, double* y, double* ynorm) {
+    if (!c || !ynorm || n < 0) return NK_E_ARG;
+    Red r{};
+    NK_TRY(launch_axpy_sumsq(c, n, s, x, y, &r));
+    return scalar_result(c, r, 1, ynorm);
+}
 int nk_axpby(nk_ctx* c, int64_t n, double s, const double* x, double t, double* y) {
     return c ? launch_axpby(c, n, s, x, t, y) : NK_E_ARG;
 }

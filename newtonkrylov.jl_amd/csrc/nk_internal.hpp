@@ -150,6 +150,7 @@ int launch_dot(nk_ctx* c, int64_t n, const double* x, const double* y, Red* red)
 int launch_sumsq(nk_ctx* c, int64_t n, const double* x, Red* red);
 int launch_finalize(nk_ctx* c, Red r, double* dst, int sqrt_it, double* mirror = nullptr);  // dst[0] = sum (or sqrt(sum))
 int launch_axpy(nk_ctx* c, int64_t n, double s, const double* x, double* y);
+int launch_axpy_sumsq(nk_ctx* c, int64_t n, double s, const double* x, double* y, Red* red);  // + ||y||^2 partials
 int launch_axpby(nk_ctx* c, int64_t n, double s, const double* x, double t, double* y);
 int launch_scal(nk_ctx* c, int64_t n, double s, double* x);
 int launch_copy(nk_ctx* c, int64_t n, double* y, const double* x);

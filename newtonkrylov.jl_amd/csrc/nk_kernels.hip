@@ -640,6 +640,30 @@ __global__ __launch_bounds__(kBlock) void k_axpy(int64_t n, double s, const doub
     if (NK_TAIL) y[n - 1] = fma(s, x[n - 1], y[n - 1]);
 }
 
+// y = s x + y with the partials of ||y||^2 (the Newton update and the next FD step's ||u||)
+__global__ __launch_bounds__(kBlock) void k_axpy_sumsq(int64_t n, double s, const double* __restrict__ x,
+                                                      double* __restrict__ y, double* __restrict__ part, int fin) {
+    __shared__ double sh[8];
+    const double2* x2 = reinterpret_cast<const double2*>(x);
+    double2* y2 = reinterpret_cast<double2*>(y);
+    double acc = 0.0;
+    NK_GRID_STRIDE2(i) {
+        const double2 a = x2[i];
+        double2 b = y2[i];
+        b.x = fma(s, a.x, b.x);
+        b.y = fma(s, a.y, b.y);
+        y2[i] = b;
+        acc = fma(b.x, b.x, acc);
+        acc = fma(b.y, b.y, acc);
+    }
+    if (NK_TAIL) {
+        const double b = fma(s, x[n - 1], y[n - 1]);
+        y[n - 1] = b;
+        acc = fma(b, b, acc);
+    }
+    publish(acc, part, fin, sh);
+}
+
 __global__ __launch_bounds__(kBlock) void k_axpby(int64_t n, double s, const double* __restrict__ x, double t,
                                                  double* __restrict__ y) {
     const double2* x2 = reinterpret_cast<const double2*>(x);
@@ -1101,6 +1125,13 @@ int launch_finalize(nk_ctx* c, Red r, double* dst, int sqrt_it, double* mirror) 
                   [&] { hipLaunchKernelGGL(kern, dim3(g), dim3(kBlock), 0, c->stream, __VA_ARGS__); })
 
 int launch_axpy(nk_ctx* c, int64_t n, double s, const double* x, double* y) { NK_STREAM_LAUNCH("axpy", 24.0, k_axpy, n, s, x, y); }
+int launch_axpy_sumsq(nk_ctx* c, int64_t n, double s, const double* x, double* y, Red* red) {
+    const int g = red_blocks(n);
+    int fin;
+    double* part = red_out(c, g, red, &fin);
+    return launch(c, "axpy_norm", 24.0 * n,
+                  [&] { hipLaunchKernelGGL(k_axpy_sumsq, dim3(g), dim3(kBlock), 0, c->stream, n, s, x, y, part, fin); });
+}
 int launch_axpby(nk_ctx* c, int64_t n, double s, const double* x, double t, double* y) {
     NK_STREAM_LAUNCH("axpby", 24.0, k_axpby, n, s, x, t, y);
 }

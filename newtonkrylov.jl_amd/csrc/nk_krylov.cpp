@@ -194,9 +194,11 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
     // x .= 0 ; r0 = b - A*0 = b.  x is only materialised when no cycle runs: the first cycle's
     // update writes x = Σ y_i V_i directly (bit-identical to 0 + Σ y_i V_i), saving a pass over x.
     Red rb{};
-    NK_TRY(launch_sumsq(c, n, b, &rb));
-    double beta = 0.0;
-    NK_TRY(host_scalar(c, rb, 1, &beta));
+    double beta = o->b_norm;  // the caller may know ||b|| already (Newton: b = F(u), ||F(u)|| just computed)
+    if (!(beta > 0.0)) {
+        NK_TRY(launch_sumsq(c, n, b, &rb));
+        NK_TRY(host_scalar(c, rb, 1, &beta));
+    }
     double rNorm = beta;
     PUSH_HIST(rNorm);
     const double eps_ = o->atol + o->rtol * rNorm;
@@ -502,9 +504,12 @@ int nk_krylov_solve(nk_workspace* ws, const nk_problem* p, const double* u, cons
     Op A{c, p, o->jv_mode, u, F0, 0.0};
     NK_TRY(halo_exchange(c, p, u));  // u is constant during the solve: one exchange
     if (o->jv_mode == NK_JV_FD) {
-        Red ru{};
-        NK_TRY(launch_sumsq(c, ws->n, u, &ru));
-        NK_TRY(host_scalar(c, ru, 1, &A.unorm));
+        A.unorm = o->u_norm;  // known from the fused Newton update (nk_axpy_norm), else one pass
+        if (!(A.unorm > 0.0)) {
+            Red ru{};
+            NK_TRY(launch_sumsq(c, ws->n, u, &ru));
+            NK_TRY(host_scalar(c, ru, 1, &A.unorm));
+        }
     }
     int rc = (ws->algo == NK_ALGO_CG) ? cg(ws, A, b, o, st, hist, hist_cap, hist_len)
                                       : gmres(ws, p, A, b, o, st, hist, hist_cap, hist_len);

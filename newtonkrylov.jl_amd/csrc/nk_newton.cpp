@@ -67,14 +67,17 @@ int nk_newton_krylov(nk_ctx* c, const nk_problem* p, double* u, double* res, con
     NK_TRY(nk_workspace_create(c, o->algo, p, o->memory > 0 ? o->memory : 20, &ws));
     int rc = NK_OK;
     int64_t outer = 0, inner = 0;
+    double u_norm = 0.0;  // ||u|| after the fused update (FD step size of the next solve); 0 = unknown
     while (n_res > tol && outer <= o->max_niter) {
         nk_krylov_opts ko = o->krylov;
         if (!o->rtol_user && o->forcing != NK_FORCING_NONE) ko.rtol = eta;
+        ko.b_norm = n_res;  // b = F(u): its norm is the n_res just computed
+        ko.u_norm = u_norm;
         nk_krylov_stats ks{};
         const double* F0 = ko.jv_mode == NK_JV_FD ? res : nullptr;
         if ((rc = nk_krylov_solve(ws, p, u, F0, res, &ko, &ks, nullptr, 0, nullptr)) != NK_OK) break;
         st->n_matvec += ks.n_matvec;
-        if ((rc = nk_axpy(c, g.n, -1.0, nk_workspace_x(ws), u)) != NK_OK) break;  // u .-= 1 .* d
+        if ((rc = nk_axpy_norm(c, g.n, -1.0, nk_workspace_x(ws), u, &u_norm)) != NK_OK) break;  // u .-= 1 .* d
         const double n_prior = n_res;
         if ((rc = nk_residual_norm(c, p, res, u, &n_res)) != NK_OK) break;
         st->n_residual++;

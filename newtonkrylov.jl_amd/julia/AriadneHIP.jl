@@ -225,6 +225,8 @@ struct NkKrylovOpts
     jv_mode::Int32
     atol::Float64
     rtol::Float64
+    b_norm::Float64   # 0: computed by the solve (Krylov.jl semantics)
+    u_norm::Float64   # 0: computed by the solve
 end
 struct NkKrylovStats
     niter::Int64
@@ -252,7 +254,7 @@ end
 function Krylov.krylov_solve!(ws::HipKrylovWorkspace, J::Ariadne.JacobianOperator{<:AnyHipResidual, <:HipVector}, b::HipVector;
                               restart::Bool = false, reorthogonalization::Bool = false, itmax::Integer = 0,
                               atol::Real = sqrt(eps(Float64)), rtol::Real = sqrt(eps(Float64)), kwargs...)
-    opts = NkKrylovOpts(restart, reorthogonalization, itmax, J.f.jv, atol, rtol)
+    opts = NkKrylovOpts(restart, reorthogonalization, itmax, J.f.jv, atol, rtol, 0.0, 0.0)
     st = Ref{NkKrylovStats}()
     hl = Ref{Int64}(0)
     F0 = J.f.jv == NK_JV_FD ? J.res.ptr : Ptr{Float64}(C_NULL)
