@@ -24,7 +24,11 @@ constexpr int kMaxUpdateVecs = 32;   // basis vectors folded per x-update launch
 constexpr int kMgsVariant = 5;       // MGS-pass variant (unroll x non-temporal V_i), see mgs_dispatch
 
 enum Mode { MODE_RES = 0, MODE_JEXACT = 1, MODE_JFD = 2 };
-enum Epi { EPI_NONE = 0, EPI_SUMSQ = 1, EPI_DOT = 2, EPI_RESID = 3, EPI_DOTV = 4 /* EPI_DOT + vout (kernel-internal) */ };
+enum Epi {
+    EPI_NONE = 0, EPI_SUMSQ = 1, EPI_DOT = 2, EPI_RESID = 3,
+    EPI_DOTV = 4,   // kernel-internal: EPI_DOT + vout (V_k = v / h stored)
+    EPI_DOTVS = 5   // kernel-internal: EPI_DOTV whose dot partner is that V_k itself (aux == nullptr)
+};
 
 struct ProfPending {
     int kid;

@@ -197,7 +197,7 @@ __device__ __forceinline__ double point_value(const KArgs& A, double c, double l
 template <int EPI>
 __device__ __forceinline__ double epilogue(double& val, double ax, double acc) {
     if (EPI == EPI_SUMSQ) return fma(val, val, acc);
-    if (EPI == EPI_DOT || EPI == EPI_DOTV) return fma(ax, val, acc);
+    if (EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_DOTVS) return fma(ax, val, acc);
     if (EPI == EPI_RESID) {
         val = ax - val;  // w = b - A x  (kaxpby!(n, 1, b, -1, w))
         return fma(val, val, acc);
@@ -219,10 +219,11 @@ __global__ __launch_bounds__(kBlock) void k_st1d(KArgs A0) {
         const double uc = (MODE == MODE_JEXACT) ? A.u[i] : 0.0;
         const double f0 = (MODE == MODE_JFD) ? A.F0[i] : 0.0;
         double val = point_value<NK_BRATU1D, MODE>(A, c, lap(c, r, l, A.hx2), uc, 0.0, f0);
-        const double ax = (EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID) ? A.aux[i] : 0.0;
+        const double ax = (EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID) ? A.aux[i]
+                          : (EPI == EPI_DOTVS ? A.v[i] / A.hd : 0.0);
         acc = epilogue<EPI>(val, ax, acc);
         A.out[i] = val;
-        if constexpr (MODE != MODE_RES && EPI == EPI_DOTV) A.vout[i] = A.v[i] / A.hd;
+        if constexpr (MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS)) A.vout[i] = A.v[i] / A.hd;
     }
     if (EPI != EPI_NONE) publish(acc, A.part, A.fin, sh);
 }
@@ -399,7 +400,7 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     constexpr bool kUn = KIND == NK_HEAT2D_EULER && MODE != MODE_JEXACT;
     constexpr bool kF0 = MODE == MODE_JFD;
     constexpr bool kAx = EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID;
-    constexpr bool vout = MODE != MODE_RES && EPI == EPI_DOTV;  // fused kdivcopy!: V_k is stored
+    constexpr bool vout = MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS);  // fused kdivcopy!: V_k stored
     double acc = 0.0;
     if (y0 < ny) {
         // rows y0-1 (ghost plane when y0 = 0) and y0 cooked up front; row y0+1 raw in flight
@@ -442,7 +443,7 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
                     const double c = fc.c[k];
                     const double lsum = lapk(A, c, e, w, A.hx2, A.ihx2) + lapk(A, c, fp.c[k], fm.c[k], A.hy2, A.ihy2);
                     double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unc.v[k], f0c.v[k]);
-                    acc = epilogue<EPI>(r, ax.v[k], acc);
+                    acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[k] : ax.v[k], acc);
                     val.v[k] = r;
                 }
                 store_row<VEC>(A.out, o, val);
@@ -499,7 +500,7 @@ __global__ __launch_bounds__(kBlock) void k_st3d(KArgs A0) {
     constexpr bool kUn = MODE != MODE_JEXACT;
     constexpr bool kF0 = MODE == MODE_JFD;
     constexpr bool kAx = EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID;
-    constexpr bool vout = MODE != MODE_RES && EPI == EPI_DOTV;  // fused kdivcopy!: V_k is stored
+    constexpr bool vout = MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS);  // fused kdivcopy!: V_k stored
     double acc = 0.0;
     if (z0 < nz) {
         const int64_t o0 = z0 * pl + oj;
@@ -544,7 +545,7 @@ __global__ __launch_bounds__(kBlock) void k_st3d(KArgs A0) {
                     const double lsum = (lapk(A, c, e, w, A.hx2, A.ihx2) + lapk(A, c, fn.c[q], fs.c[q], A.hy2, A.ihy2)) +
                                         lapk(A, c, fp.c[q], fm.c[q], A.hz2, A.ihz2);
                     double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unc.v[q], f0c.v[q]);
-                    acc = epilogue<EPI>(r, ax.v[q], acc);
+                    acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[q] : ax.v[q], acc);
                     val.v[q] = r;
                 }
                 store_row<VEC>(A.out, o, val);
@@ -974,6 +975,7 @@ void go_stencil_epi(const KArgs& A, int epi, int vec, int grid, hipStream_t s) {
     case EPI_SUMSQ: go_stencil<KIND, MODE, EPI_SUMSQ>(A, vec, grid, s); break;
     case EPI_DOT: go_stencil<KIND, MODE, EPI_DOT>(A, vec, grid, s); break;
     case EPI_DOTV: go_stencil<KIND, MODE, EPI_DOTV>(A, vec, grid, s); break;
+    case EPI_DOTVS: go_stencil<KIND, MODE, EPI_DOTVS>(A, vec, grid, s); break;
     default: go_stencil<KIND, MODE, EPI_RESID>(A, vec, grid, s); break;
     }
 }
@@ -1057,7 +1059,7 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         vec = (p->nx % 2 == 0) ? 2 : 1;
         A.tiles_x = (int)((p->nx + 64 * vec - 1) / (64 * vec));
         A.tiles_y = (int)((p->ny + 3) / 4);
-        static const int target = env_int("NK_ST_BLOCKS", 2048);
+        static const int target = env_int("NK_ST3_BLOCKS", 8192);  // shorter z-marches keep y-adjacent tiles in step (L2 reuse of the halo rows)
         int64_t planes = ((int64_t)p->nz * A.tiles_x * A.tiles_y + target - 1) / target;
         static const int min_planes = env_int("NK_ST_MINPLANES", 8);
         if (planes < min_planes) planes = min_planes;
@@ -1076,7 +1078,7 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     if (in.mode == MODE_RES) words += 1 + (heat ? 1 : 0);
     else if (in.mode == MODE_JEXACT) words += 1 + (heat ? 0 : 1);
     else words += 3 + (heat ? 1 : 0);
-    if (in.epi == EPI_DOT || in.epi == EPI_RESID) words += 1;
+    if (in.epi == EPI_RESID || (in.epi == EPI_DOT && in.aux)) words += 1;
     if (in.vout) words += 1;  // fused kdivcopy!: V_k is written
     const double bytes = 8.0 * words * (double)g.n;
     static const char* names[3][4] = {
@@ -1084,11 +1086,15 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         {"jv_exact", "jv_exact_sumsq", "jv_exact_dot", "jv_exact_resid"},
         {"jv_fd", "jv_fd_sumsq", "jv_fd_dot", "jv_fd_resid"}};
     static const char* fused_names[3] = {"residual", "jv_exact_dot_norm", "jv_fd_dot_norm"};
+    static const char* v1_names[3] = {"residual", "jv_exact_dot_v1", "jv_fd_dot_v1"};
     if (in.vout && in.epi != EPI_DOT) return fail(c, NK_E_ARG, "fused normalisation needs the dot epilogue");
     const int kind = p->kind, mode = in.mode;
-    const int epi = (in.vout && in.epi == EPI_DOT) ? EPI_DOTV : in.epi;  // distinct instantiation (own profile line)
+    // distinct instantiations (own profile lines): normalise-and-store V_k, and its V_1 = r0/beta form
+    // whose dot partner is the stored vector itself
+    const int epi = (in.vout && in.epi == EPI_DOT) ? (in.aux ? EPI_DOTV : EPI_DOTVS) : in.epi;
+    if (in.epi == EPI_DOT && !in.aux && !in.vout) return fail(c, NK_E_ARG, "dot epilogue needs its partner");
     hipStream_t s = c->stream;
-    const char* kname = epi == EPI_DOTV ? fused_names[mode] : names[mode][epi];
+    const char* kname = epi == EPI_DOTV ? fused_names[mode] : (epi == EPI_DOTVS ? v1_names[mode] : names[mode][epi]);
     return launch(c, kname, bytes, [&] {
         switch (kind) {
         case NK_BRATU1D: go_stencil_mode<NK_BRATU1D>(A, mode, epi, vec, grid, s); break;

@@ -38,6 +38,7 @@ struct nk_workspace {
     std::vector<double*> V;
     double* hdev = nullptr;  // device Hessenberg columns: 2 slots of (2*cap + 2) doubles (steps k, k+1 in flight)
     double* ydev = nullptr;  // device y (cap doubles)
+    double* bdev = nullptr;  // device beta of the current cycle (V_1 = r0 / beta is fused into step 1)
     double* hpin = nullptr;  // pinned host mirror of hdev (2 slots), written by the kernels themselves
     double* hpin_dev = nullptr;  // hpin's device address
     double* ypin = nullptr;  // pinned host y
@@ -222,6 +223,7 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
     auto slot_pin = [&](int k) { return ws->hpin + (size_t)(k & 1) * (2 * ws->cap + 2); };
     auto slot_pin_dev = [&](int k) { return ws->hpin_dev + (size_t)(k & 1) * (2 * ws->cap + 2); };
     auto npasses_of = [&](int k) { return reorth ? 2 * k : k; };
+    const double* v1_src = b;  // r0 of the current cycle; step 1 applies J to r0 / beta and stores V_1
     auto issue = [&](int k) -> int {
         NK_TRY(ws_basis(ws, k));
         NK_TRY(ws_scalars(ws, k + 1));
@@ -230,8 +232,8 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         double* colh = slot_pin_dev(k);  // the kernels mirror every entry into pinned host memory
         double* q = W[k & 1];
         Red red{};
-        if (k == 1) {
-            NK_TRY(A.apply(q, ws->V[0], 1.0, EPI_DOT, ws->V[0], &red));
+        if (k == 1) {  // fused kdivcopy!(V_1, r0, beta) + mul! + <V_1, Jv> (the dot partner is V_1 itself)
+            NK_TRY(A.apply(q, v1_src, 1.0, EPI_DOT, nullptr, &red, ws->bdev, ws->V[0]));
         } else {
             const double* hprev = slot_dev(k - 1) + npasses_of(k - 1);
             NK_TRY(A.apply(q, W[(k - 1) & 1], 1.0, EPI_DOT, ws->V[0], &red, hprev, ws->V[k - 1]));
@@ -271,7 +273,8 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
             src = W[0];
         }
         z[0] = beta;
-        NK_TRY(launch_divcopy(c, n, ws->V[0], src, beta));  // V1 = r0 / beta
+        NK_TRY(launch_fill(c, 1, ws->bdev, beta));  // V1 = r0 / beta happens inside step 1's Jv
+        v1_src = src;
         npass++;
         inner_iter = 0;
         bool inner_tired = false;
@@ -453,6 +456,7 @@ int nk_workspace_create(nk_ctx* c, int32_t algo, const nk_problem* p, int32_t me
     if ((rc = nk_vec_alloc(c, &ws->prob, &ws->x)) != NK_OK || (rc = nk_vec_alloc(c, &ws->prob, &ws->w)) != NK_OK ||
         (rc = nk_vec_alloc(c, &ws->prob, &ws->xr)) != NK_OK ||
         (algo == NK_ALGO_GMRES && (rc = nk_vec_alloc(c, &ws->prob, &ws->w2)) != NK_OK) ||
+        hipMalloc(&ws->bdev, 2 * sizeof(double)) != hipSuccess ||
         hipEventCreateWithFlags(&ws->col_ready[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ws->col_ready[1], hipEventDisableTiming) != hipSuccess) {
         if (rc == NK_OK) rc = fail(c, NK_E_HIP, "hipEventCreate failed");
@@ -484,6 +488,7 @@ int nk_workspace_destroy(nk_workspace* ws) {
         if (e) (void)hipEventDestroy(e);
     if (ws->hdev) (void)hipFree(ws->hdev);
     if (ws->ydev) (void)hipFree(ws->ydev);
+    if (ws->bdev) (void)hipFree(ws->bdev);
     if (ws->hpin) (void)hipHostFree(ws->hpin);
     if (ws->ypin) (void)hipHostFree(ws->ypin);
     delete ws;

@@ -71,7 +71,10 @@ int launch_user(nk_ctx* c, const StencilIn& in, Red* red) {
         break;
     }
     }
-    if (fd || in.epi != EPI_NONE) NK_TRY(launch_user_epi(c, g.n, fd, in.out, in.F0, in.eps, in.epi, in.aux, red));
+    // dot partner: aux, or (V_1 = r0 / beta fused into the first Jv) the normalised input just stored
+    const double* aux = (in.epi == EPI_DOT && !in.aux) ? in.vout : in.aux;
+    if (in.epi == EPI_DOT && !aux) return fail(c, NK_E_ARG, "dot epilogue needs its partner");
+    if (fd || in.epi != EPI_NONE) NK_TRY(launch_user_epi(c, g.n, fd, in.out, in.F0, in.eps, in.epi, aux, red));
     return NK_OK;
 }
 
