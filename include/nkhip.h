@@ -67,7 +67,8 @@ typedef int (*nk_user_residual)(void* data, nk_ctx* ctx, double* res, const doub
 typedef int (*nk_user_tangent)(void* data, nk_ctx* ctx, double* out, const double* u, const double* v);
 typedef struct nk_user_ops {
     nk_user_residual F;
-    nk_user_tangent J;
+    nk_user_tangent J;   /* optional: out = J(u) v                                   */
+    nk_user_tangent JT;  /* optional: out = J(u)^T v (Enzyme reverse mode's mul! on transpose(J)) */
     void* data;
 } nk_user_ops;
 
@@ -110,6 +111,11 @@ int nk_residual_norm(nk_ctx* ctx, const nk_problem* p, double* res, const double
  * eps = sqrt(eps_mach) * max(1, ||u||) / ||v||.  Unlike Enzyme, `res` is not rewritten. */
 int nk_jv(nk_ctx* ctx, const nk_problem* p, double* out, const double* u, const double* v,
           const double* F0, int32_t mode, double eps);
+
+/* mul!(out, transpose(J), v) (src/Ariadne.jl:87-107, Enzyme reverse mode): out = J(u)^T v.  The
+ * built-in residuals have symmetric Jacobians (3/5/7-point Laplacian plus a diagonal), so this is
+ * the exact tangent kernel; user problems need user->JT. */
+int nk_jtv(nk_ctx* ctx, const nk_problem* p, double* out, const double* u, const double* v);
 
 /* ---------------------------------------------------------------- Krylov vector primitives
  * Krylov.kdot/knorm/kscal!/kaxpy!/kaxpby!/kcopy!/kfill!/kdivcopy!/kref! -- the overload points

@@ -4,7 +4,7 @@ Reference: vchuravy/NewtonKrylov.jl (package Ariadne.jl), src/Ariadne.jl.  The J
 1:1 with `!` -> trailing `_`:  newton_krylov! -> newton_krylov_, mul! -> mul_, kaxpy! -> kaxpy_.
 """
 from ._lib import NKError, device_count, load
-from .ariadne import (EisenstatWalker, Fixed, Forcing, JacobianOperator, Result, Stats, mul_, newton_krylov, newton_krylov_native,
+from .ariadne import (EisenstatWalker, Fixed, Forcing, JacobianOperator, Result, Stats, mul_, newton_krylov, newton_krylov_native, transpose, collect, TransposeOperator,
                       newton_krylov_)
 from .device import Context, DeviceArray, Grid, default_context, set_default_context
 from .distributed import dist_unique_id, init_distributed, slab
@@ -15,7 +15,7 @@ from .problems import DeviceResidual, UserResidual, bc_zero_, bratu2d_, bratu_, 
 
 __all__ = [
     "NKError", "device_count", "load", "EisenstatWalker", "Fixed", "Forcing", "JacobianOperator", "Result", "Stats",
-    "mul_", "newton_krylov", "newton_krylov_", "newton_krylov_native", "Context", "DeviceArray", "Grid", "default_context",
+    "mul_", "newton_krylov", "newton_krylov_", "newton_krylov_native", "transpose", "collect", "TransposeOperator", "Context", "DeviceArray", "Grid", "default_context",
     "set_default_context", "dist_unique_id", "init_distributed", "slab", "G_Euler_", "G_Midpoint_", "G_Trapezoid_", "diffusion_", "diffusion3d_", "solve",
     "KrylovConstructor", "kaxpby_", "kaxpy_", "kaxpy_norm_", "kcopy_", "kdivcopy_", "kdot", "kfill_", "knorm", "kref_",
     "krylov_solve_", "krylov_workspace", "kscal_", "DeviceResidual", "UserResidual", "bc_zero_", "bratu2d_", "bratu_",

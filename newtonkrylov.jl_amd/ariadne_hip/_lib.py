@@ -42,7 +42,7 @@ NK_USER_TANGENT = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_v
 
 
 class nk_user_ops(C.Structure):
-    _fields_ = [("F", NK_USER_RESIDUAL), ("J", NK_USER_TANGENT), ("data", C.c_void_p)]
+    _fields_ = [("F", NK_USER_RESIDUAL), ("J", NK_USER_TANGENT), ("JT", NK_USER_TANGENT), ("data", C.c_void_p)]
 
 
 class nk_krylov_opts(C.Structure):
@@ -92,6 +92,7 @@ SIGNATURES = {
     "nk_residual": (C.c_int, [_VP, _PP, _VP, _VP]),
     "nk_residual_norm": (C.c_int, [_VP, _PP, _VP, _VP, _PD]),
     "nk_jv": (C.c_int, [_VP, _PP, _VP, _VP, _VP, _VP, _I32, _D]),
+    "nk_jtv": (C.c_int, [_VP, _PP, _VP, _VP, _VP]),
     "nk_dot": (C.c_int, [_VP, _I64, _VP, _VP, _PD]),
     "nk_norm": (C.c_int, [_VP, _I64, _VP, _PD]),
     "nk_scal": (C.c_int, [_VP, _I64, _D, _VP]),

@@ -98,13 +98,114 @@ class JacobianOperator:
         return self.size[0] * self.size[1]
 
 
-def mul_(out: DeviceArray, J: JacobianOperator, v: DeviceArray, eps: float = 0.0):
-    """mul!(out, J, v) (src/Ariadne.jl:48-57).  Unlike Enzyme it does not rewrite J.res."""
+class TransposeOperator:
+    """transpose(J) / J' of a JacobianOperator (src/Ariadne.jl:87-107): mul_ gives J(u)^T v."""
+
+    def __init__(self, J: JacobianOperator):
+        self.J = J
+
+    @property
+    def size(self):
+        return tuple(reversed(self.J.size))
+
+    def problem(self) -> _lib.nk_problem:
+        return self.J.problem()
+
+
+def transpose(J: JacobianOperator) -> TransposeOperator:
+    return TransposeOperator(J)
+
+
+JacobianOperator.T = property(transpose)
+
+
+def mul_(out, J, v, eps: float = 0.0):
+    """mul!(out, J, v) (src/Ariadne.jl:48-57); mul!(out, transpose(J), v) (:87-107).  Unlike Enzyme
+    it does not rewrite J.res.  Lists of vectors are the batched form (:59-85, :109-138): one
+    product per column, each exactly the single-vector result."""
+    if isinstance(out, (list, tuple)):
+        if not isinstance(v, (list, tuple)) or len(out) != len(v):
+            raise ValueError("batched mul!: out and v must be lists of equal length")
+        for o, w in zip(out, v):
+            mul_(o, J, w, eps)
+        return None
+    if isinstance(J, TransposeOperator):
+        prob = J.problem()
+        out.ctx.check(load().nk_jtv(out.ctx.handle, C.byref(prob), out.ptr, J.J.u.ptr, v.ptr), "mul!(out, J', v)")
+        return None
     prob = J.problem()
     F0 = J.res.ptr if J.jv_mode == _lib.NK_JV_FD else None
     out.ctx.check(load().nk_jv(out.ctx.handle, C.byref(prob), out.ptr, J.u.ptr, v.ptr, F0, J.jv_mode, float(eps)),
                   "mul!(out, J, v)")
     return None
+
+
+def _stencil_colors(grid):
+    """Distance-2 colouring of the 3/5/7-point stencil graph: colour(i, j, k) = (i + 2j + 3k) mod
+    (2 dim + 1) gives the point and its 2 dim neighbours pairwise different colours."""
+    import numpy as np
+
+    nx, ny, nz = grid.nxyz
+    ncol = 2 * grid.dim + 1
+    k, j, i = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    return ((i + 2 * j + 3 * k) % ncol).reshape(grid.np_shape), ncol
+
+
+def collect(J, *, coloring: str | None = None):
+    """collect(J) (src/Ariadne.jl:140-162): the Jacobian as a scipy.sparse CSC matrix, row/column
+    index = interior point in memory order (x fastest).  The reference applies J to the n unit
+    vectors; here the built-in stencils are probed with 2 dim + 1 coloured vectors instead (a
+    distance-2 colouring of the stencil: every probe entry then holds exactly one Jacobian entry,
+    computed by the same kernel from the same operands as the unit-vector probe, so the values are
+    identical).  coloring="dense" (the default for user residuals, whose coupling is unknown)
+    probes the n unit vectors like the reference.  transpose(J) gives the transpose."""
+    import numpy as np
+    import scipy.sparse as sp
+
+    transposed = isinstance(J, TransposeOperator)
+    Jo = J.J if transposed else J
+    grid = Jo.u.grid
+    if Jo.u.ctx.nranks > 1:
+        raise NotImplementedError("collect(J) of a distributed operator: gather the slabs first")
+    user = getattr(Jo.f, "kind", 0) >= _lib.NK_USER1D
+    coloring = coloring or ("dense" if user else "stencil")
+    n = grid.n
+    out = Jo.u.zero()
+    if coloring == "dense":
+        if n > 4096:
+            raise ValueError(f"dense collect(J) probes n = {n} unit vectors; use coloring='stencil'")
+        cols = []
+        e = np.zeros(n)
+        for j in range(n):
+            e[j] = 1.0
+            mul_(out, J, DeviceArray.from_numpy(e.reshape(grid.np_shape), grid, Jo.u.ctx))
+            e[j] = 0.0
+            cols.append(sp.csc_matrix(out.to_numpy().reshape(n, 1)))
+        return sp.hstack(cols, format="csc")
+    if coloring != "stencil":
+        raise ValueError("coloring must be 'stencil' or 'dense'")
+    color, ncol = _stencil_colors(grid)
+    color = color.reshape(-1)
+    nx, ny, nz = grid.nxyz
+    idx = np.arange(n)
+    i, j, k = idx % nx, (idx // nx) % ny, idx // (nx * ny)
+    offs = [(0, 0, 0), (1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)][: 2 * grid.dim + 1]
+    rows, cols, vals = [], [], []
+    probes = []
+    for c in range(ncol):
+        v = DeviceArray.from_numpy((color == c).astype(np.float64).reshape(grid.np_shape), grid, Jo.u.ctx)
+        mul_(out, J, v)
+        probes.append(out.to_numpy().reshape(-1))
+    for di, dj, dk in offs:  # entry (row p, column q = p + offset) sits in the probe of q's colour
+        ii, jj, kk = i + di, j + dj, k + dk
+        ok = (ii >= 0) & (ii < nx) & (jj >= 0) & (jj < ny) & (kk >= 0) & (kk < nz)
+        q = (kk * ny + jj) * nx + ii
+        p_ok, q_ok = idx[ok], q[ok]
+        rows.append(p_ok)
+        cols.append(q_ok)
+        vals.append(np.array([probes[c][r] for c, r in zip(color[q_ok], p_ok)]) if len(p_ok) else np.zeros(0))
+    M = sp.csc_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))), shape=(n, n))
+    return M
 
 
 # ----------------------------------------------------------------------------- Newton-Krylov

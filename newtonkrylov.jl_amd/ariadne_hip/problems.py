@@ -117,6 +117,7 @@ class UserResidual(DeviceResidual):
     residual ON THE DEVICE, enqueued on the library's stream: the call already runs inside
     `ctx.torch_stream()` when torch is loaded, so `res.torch()[...] = f(u.torch())` just works.
     Ghost planes of u are current (zero Dirichlet, or the neighbour slab's plane).
+    `JT(out, u, v, p)` (optional) is the transpose product J(u)^T v (mul! on transpose(J)).
     `J(out, u, v, p)` (optional) is the exact tangent -- what Enzyme's forward mode computes for the
     reference's mul! (src/Ariadne.jl:48-57); without it use JacobianOperator(..., jv="fd"), whose
     FD quotient, basis normalisation and reductions the library runs around F on the device.
@@ -124,8 +125,8 @@ class UserResidual(DeviceResidual):
 
     kind = _lib.NK_USER2D  # per call: NK_USER1D/2D/3D by the grid's dimension
 
-    def __init__(self, F, J=None, name: str | None = None):
-        self.F, self.J = F, J
+    def __init__(self, F, J=None, name: str | None = None, JT=None):
+        self.F, self.J, self.JT = F, J, JT
         self.name = name or (getattr(F, "__name__", "user") + "!")
         self._live = {}
 
@@ -145,8 +146,10 @@ class UserResidual(DeviceResidual):
 
         cf = _lib.NK_USER_RESIDUAL(lambda _d, _c, res, u: run(self.F, res, u))
         cj = _lib.NK_USER_TANGENT(lambda _d, _c, out, u, v: run(self.J, out, u, v)) if self.J else _lib.NK_USER_TANGENT()
-        ops = _lib.nk_user_ops(cf, cj, None)
-        return ops, cf, cj
+        ct = (_lib.NK_USER_TANGENT(lambda _d, _c, out, u, v: run(self.JT, out, u, v)) if self.JT
+              else _lib.NK_USER_TANGENT())
+        ops = _lib.nk_user_ops(cf, cj, ct, None)
+        return ops, cf, (cj, ct)
 
     def problem(self, u, p):
         key = (u.grid, id(u.ctx), id(p))

@@ -291,6 +291,22 @@ int nk_jv(nk_ctx* c, const nk_problem* p, double* out, const double* u, const do
     return launch_stencil(c, in, &r);
 }
 
+int nk_jtv(nk_ctx* c, const nk_problem* p, double* out, const double* u, const double* v) {
+    if (!c || !out || !u || !v) return NK_E_ARG;
+    Geo g;
+    NK_TRY(geometry(c, p, &g));
+    if (!nk_is_user(p->kind))  // symmetric Jacobians: J^T v = J v, the exact tangent
+        return nk_jv(c, p, out, u, v, nullptr, NK_JV_EXACT, 0.0);
+    const nk_user_ops* ops = p->user;
+    if (!ops->JT) return fail(c, NK_E_ARG, "transpose product of a user problem needs user->JT");
+    NK_TRY(halo_exchange(c, p, u));
+    NK_TRY(halo_exchange(c, p, v));
+    int rc = 0;
+    NK_TRY(launch(c, "user_JT", 0.0, [&] { rc = ops->JT(ops->data, c, out, u, v); }));
+    if (rc != 0) return fail(c, NK_E_USER, "user transpose-tangent callback returned " + std::to_string(rc));
+    return NK_OK;
+}
+
 // ---------------------------------------------------------------- Krylov vector primitives
 static int scalar_result(nk_ctx* c, Red r, int sqrt_it, double* out) {
     NK_TRY(finish_reduction(c, &r));

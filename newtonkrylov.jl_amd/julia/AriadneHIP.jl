@@ -156,6 +156,7 @@ problem(::HipResidual{:heat2d}, u::HipVector, (un, Δt, _, (a, dx, dy, _bc), _t)
 struct NkUserOps
     F::Ptr{Cvoid}
     J::Ptr{Cvoid}
+    JT::Ptr{Cvoid}
     data::Ptr{Cvoid}
 end
 struct HipUserResidual{F, J}
@@ -175,7 +176,7 @@ function problem(F::HipUserResidual, u::HipVector, p)
          @cfunction($((_d, _c, out, x, v) -> (try F.jvp!(view(out), view(x), view(v), p); Cint(0) catch; Cint(1) end)),
                     Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}))
     ops = Ref(NkUserOps(Base.unsafe_convert(Ptr{Cvoid}, cF),
-                        cJ === nothing ? C_NULL : Base.unsafe_convert(Ptr{Cvoid}, cJ), C_NULL))
+                        cJ === nothing ? C_NULL : Base.unsafe_convert(Ptr{Cvoid}, cJ), C_NULL, C_NULL))
     _live[F] = (cF, cJ, ops, p)
     kind = u.grid[3] > 1 ? NK_USER3D : (u.grid[2] > 1 ? NK_USER2D : NK_USER1D)
     return NkProblem(kind, 0, u.grid..., 1, 1, 1, 0, 0, 0, C_NULL, Base.unsafe_convert(Ptr{Cvoid}, ops))

@@ -1,0 +1,145 @@
+"""GPU tests of the operator API around mul!: transpose(J) (src/Ariadne.jl:87-107), the batched
+form (:59-85), collect(J) (:140-162) -- pinned by the reference's own known answers
+(test/runtests.jl:4-54, run through a user residual on the device) and by the oracle.
+
+Tolerances: heat entries bit-identical (no transcendental); Bratu entries identical up to exp
+(torch / ocml vs glibc, <= 1 ulp of lambda e^u); colour-probed and unit-probed collect(J) are
+bit-identical (every probe entry is one Jacobian entry computed from the same operands).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import _nkpath  # noqa: F401
+import ariadne_hip as ah
+from oracle import oracle as oc
+
+pytestmark = pytest.mark.gpu
+ULP = np.finfo(np.float64).eps
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = ah.Context(0)
+    ah.set_default_context(c)
+    yield c
+    c.sync()
+
+
+def oracle_dense_jacobian(P, u):
+    n = P.n
+    J = np.zeros((n, n))
+    for j in range(n):
+        e = np.zeros(n)
+        e[j] = 1.0
+        J[:, j] = oc.jv_exact(P, u, e.reshape(P.shape)).reshape(-1)
+    return J
+
+
+@pytest.mark.parametrize("kind", ["bratu1d", "bratu2d", "heat2d", "heat3d"])
+def test_collect_matches_oracle_and_unit_probing(ctx, kind):
+    rng = np.random.default_rng(5)
+    if kind == "bratu1d":
+        P = oc.bratu1d(17)
+        u0 = oc.sin_ic(P)
+        F, p = ah.bratu_, (P.hx, P.lam)
+    elif kind == "bratu2d":
+        P = oc.bratu2d(9, 7)
+        u0 = oc.sin_ic(P) + 0.1 * rng.standard_normal(P.shape)
+        F, p = ah.bratu2d_, (P.hx, P.hy, P.lam)
+    elif kind == "heat2d":
+        un = rng.standard_normal((6, 11))
+        P = oc.heat2d_euler(11, 6, un=un)
+        u0 = un.copy()
+        F, p = ah.heat2d_euler_, (ah.DeviceArray.from_numpy(un), P.dt, None, (P.a, P.hx, P.hy, ah.bc_zero_), 0.0)
+    else:
+        un = rng.standard_normal((4, 5, 6))
+        P = oc.heat3d_euler(6, 5, 4, un=un)
+        u0 = un.copy()
+        F, p = ah.heat3d_euler_, (ah.DeviceArray.from_numpy(un), P.dt, None, (P.a, P.hx, P.hy, P.hz, ah.bc_zero_), 0.0)
+    u = ah.DeviceArray.from_numpy(u0)
+    res = u.zero()
+    J = ah.JacobianOperator(F, res, u, p)
+    A = ah.collect(J).toarray()
+    B = ah.collect(J, coloring="dense").toarray()
+    np.testing.assert_array_equal(A, B)
+    ref = oracle_dense_jacobian(P, u0)
+    assert np.array_equal(A != 0, ref != 0)  # the stencil pattern
+    if kind.startswith("heat"):
+        np.testing.assert_array_equal(A, ref)
+    else:
+        lam_e = P.lam * np.exp(u0.reshape(-1))
+        np.testing.assert_allclose(np.diag(A), np.diag(ref), rtol=0, atol=0 + (4 * ULP * lam_e + 2 * np.spacing(np.abs(np.diag(ref)))).max())
+        off = ~np.eye(P.n, dtype=bool)
+        np.testing.assert_array_equal(A[off], ref[off])
+    # transpose: collect(transpose(J)) == transpose(collect(J))  (runtests.jl:54)
+    np.testing.assert_array_equal(ah.collect(ah.transpose(J)).toarray(), A.T)
+
+
+def test_transpose_and_batched_mul(ctx):
+    P = oc.bratu2d(40, 33)
+    u0 = oc.sin_ic(P)
+    u = ah.DeviceArray.from_numpy(u0)
+    res = u.zero()
+    J = ah.JacobianOperator(ah.bratu2d_, res, u, (P.hx, P.hy, P.lam))
+    rng = np.random.default_rng(0)
+    vs = [ah.DeviceArray.from_numpy(rng.standard_normal(P.shape)) for _ in range(3)]
+    outs = [u.zero() for _ in vs]
+    ah.mul_(outs, J, vs)  # batched
+    for o, v in zip(outs, vs):
+        single = u.zero()
+        ah.mul_(single, J, v)
+        np.testing.assert_array_equal(o.to_numpy(), single.to_numpy())
+        t = u.zero()
+        ah.mul_(t, J.T, v)  # symmetric Jacobian
+        np.testing.assert_array_equal(t.to_numpy(), single.to_numpy())
+    assert J.T.size == tuple(reversed(J.size))
+
+
+def _kelley_user():
+    """runtests.jl's 2x2 problem, F(x) = [x1^2 + x2^2 - 2, exp(x1 - 1) + x2^2 - 2], as a device user
+    residual (torch), with its tangent and transpose tangent."""
+    import torch
+
+    def F(res, x, p):
+        X = x.torch()
+        r = res.torch()
+        r[0] = X[0] ** 2 + X[1] ** 2 - 2
+        r[1] = torch.exp(X[0] - 1) + X[1] ** 2 - 2
+
+    def J(out, x, v, p):
+        X, V, o = x.torch(), v.torch(), out.torch()
+        o[0] = 2 * X[0] * V[0] + 2 * X[1] * V[1]
+        o[1] = torch.exp(X[0] - 1) * V[0] + 2 * X[1] * V[1]
+
+    def JT(out, x, w, p):
+        X, W, o = x.torch(), w.torch(), out.torch()
+        o[0] = 2 * X[0] * W[0] + torch.exp(X[0] - 1) * W[1]
+        o[1] = 2 * X[1] * W[0] + 2 * X[1] * W[1]
+
+    return ah.UserResidual(F, J, name="kelley!", JT=JT)
+
+
+def test_reference_known_answers_through_the_device(ctx, golden_dir):
+    with open(os.path.join(golden_dir, "kelley2x2.json")) as f:
+        ka = json.load(f)
+    K = _kelley_user()
+    x = ah.DeviceArray.from_numpy(np.array(ka["x_jvp"]))
+    res = x.zero()
+    J = ah.JacobianOperator(K, res, x, None)
+    out = x.zero()
+    ah.mul_(out, J, ah.DeviceArray.from_numpy(np.array([1.0, 0.0])))  # runtests.jl:36-38
+    np.testing.assert_allclose(out.to_numpy(), ka["jvp_e1"], rtol=ULP, atol=0)
+    ah.mul_(out, J.T, ah.DeviceArray.from_numpy(np.array([1.0, 0.0])))  # runtests.jl:40-42
+    np.testing.assert_array_equal(out.to_numpy(), ka["vjp_e1"])
+    A = ah.collect(J).toarray()  # runtests.jl:44-46
+    np.testing.assert_allclose(A, np.array(ka["jacobian"]), rtol=ULP, atol=0)
+    np.testing.assert_array_equal(ah.collect(J.T).toarray(), A.T)  # runtests.jl:54
+    for x0 in ka["starts_inplace"]:  # runtests.jl:15-18: newton_krylov! from (2, 0.5) is solved
+        u, r = ah.newton_krylov_(K, ah.DeviceArray.from_numpy(np.array(x0)), None)
+        assert r.solved
+        np.testing.assert_allclose(u.to_numpy(), ka["root"], atol=1e-5)
+        u, r = ah.newton_krylov_(K, ah.DeviceArray.from_numpy(np.array(x0)), None, jv="fd")
+        assert r.solved
