@@ -201,6 +201,12 @@ int nk_dist_unique_id(char out[128]);
 int nk_dist_init(nk_ctx* ctx, int32_t rank, int32_t nranks, const char id[128]);
 int nk_dist_allreduce_sum(nk_ctx* ctx, double* dev_buf, int64_t count);
 int nk_halo_exchange(nk_ctx* ctx, const nk_problem* p, double* v);
+/* The one-shot peer all-reduce nk_dist_init sets up by itself (NK_DIST_MAILBOX=0 turns it off):
+ * every reduction scalar goes from the producing kernel straight into each rank's mailbox
+ * (fine-grained memory, IPC-mapped over xGMI) -- no collective launch per inner product.  For
+ * callers that exchange the 64-byte IPC handles themselves (no RCCL communicator: reductions only). */
+int nk_dist_mailbox_handle(nk_ctx* ctx, char out[64]);
+int nk_dist_mailbox_open(nk_ctx* ctx, int32_t rank, int32_t nranks, const char* handles /* nranks x 64 */);
 
 /* ---------------------------------------------------------------- profiling (HIP events, per kernel class) */
 #define NK_PROF_NAME 32

@@ -66,6 +66,20 @@ class Context:
             pass
 
     # -- distribution ------------------------------------------------------------------------
+    def mailbox_handle(self) -> bytes:
+        """64-byte IPC handle of this context's peer mailbox (nk_dist_mailbox_handle)."""
+        buf = C.create_string_buffer(64)
+        self.check(load().nk_dist_mailbox_handle(self.handle, buf), "nk_dist_mailbox_handle")
+        return buf.raw
+
+    def mailbox_open(self, rank: int, nranks: int, handles: bytes):
+        """Reductions across `nranks` contexts through their mailboxes, without an RCCL communicator
+        (nk_dist_mailbox_open; `handles` = the ranks' mailbox_handle() concatenated in rank order)."""
+        if len(handles) != 64 * nranks:
+            raise ValueError("handles must hold nranks x 64 bytes")
+        self.check(load().nk_dist_mailbox_open(self.handle, rank, nranks, handles), "nk_dist_mailbox_open")
+        self.rank, self.nranks = rank, nranks
+
     def init_distributed(self, rank: int, nranks: int, unique_id: bytes):
         self.check(load().nk_dist_init(self.handle, rank, nranks, unique_id), "nk_dist_init")
         self.rank, self.nranks = rank, nranks

@@ -62,7 +62,20 @@ double* red_slot(nk_ctx* c) {
     return s;
 }
 
+int mb_check(nk_ctx* c) {
+    if (c->mb_err && *(volatile int*)c->mb_err)
+        return fail(c, NK_E_RCCL, "peer all-reduce: a rank's value never arrived (timeout)");
+    return NK_OK;
+}
+
 int finish_reduction(nk_ctx* c, Red* r) {
+    if (r->epoch) {  // the producing kernel already sent its value to every rank's mailbox
+        r->ptr = nullptr;
+        r->len = -(int)r->epoch;
+        r->epoch = 0;
+        r->fin = nullptr;
+        return NK_OK;
+    }
     if (!c->comm) return NK_OK;
     // collapse this rank's partials to one scalar (normally already done by the producing
     // kernel's last block), then sum the scalars over ranks (RCCL)
@@ -199,11 +212,12 @@ const char* nk_last_error(nk_ctx* c) { return c ? c->err.c_str() : "null context
 
 void* nk_ctx_stream(nk_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
+
 int nk_sync(nk_ctx* c) {
     if (!c) return NK_E_ARG;
     NK_HIP(c, hipStreamSynchronize(c->stream));
     if (c->prof) prof_drain(c, false);
-    return NK_OK;
+    return mb_check(c);
 }
 
 int nk_vec_alloc(nk_ctx* c, const nk_problem* p, double** out) {

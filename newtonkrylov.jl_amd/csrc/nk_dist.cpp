@@ -60,6 +60,103 @@ int allreduce_scalar(nk_ctx* c, double* dev, int64_t count) {
     return NK_OK;
 }
 
+// ---------------------------------------------------------------- peer mailbox (one-shot all-reduce)
+// Every reduction scalar goes straight from the producing kernel to every rank's mailbox over
+// xGMI (nk_kernels.hip: mb_send / mb_recv); RCCL keeps the halo exchange.  Set up collectively at
+// nk_dist_init, verified by a self-test whose verdict all ranks agree on; any failure falls back
+// to the RCCL all-reduce.
+static int mb_alloc(nk_ctx* c) {
+    if (c->mb_self) return NK_OK;
+    NK_HIP(c, hipSetDevice(c->device));
+    const size_t bytes = sizeof(uint64_t) * 2 * kMbSlots * kMbRanks;
+    void* p = nullptr;
+    if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) != hipSuccess)
+        return fail(c, NK_E_NOMEM, "mailbox: fine-grained allocation failed");
+    NK_HIP(c, hipMemset(p, 0, bytes));
+    c->mb_self = static_cast<uint64_t*>(p);
+    if (!c->mb_err) {
+        int* h = nullptr;
+        NK_HIP(c, hipHostMalloc(&h, 4 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+        h[0] = 0;
+        NK_HIP(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->mb_err_dev), h, 0));
+        c->mb_err = h;
+    }
+    return NK_OK;
+}
+
+static void mb_disable(nk_ctx* c) {
+    c->mb_on = false;
+    (void)mailbox_bind(c);
+    for (void* p : c->mb_opened) (void)hipIpcCloseMemHandle(p);
+    c->mb_opened.clear();
+    if (c->mb_peers_dev) (void)hipFree(c->mb_peers_dev);
+    c->mb_peers_dev = nullptr;
+}
+
+void mb_free(nk_ctx* c) {
+    mb_disable(c);
+    if (c->mb_self) (void)hipFree(c->mb_self);
+    c->mb_self = nullptr;
+    if (c->mb_err) (void)hipHostFree(c->mb_err);
+    c->mb_err = nullptr;
+    c->mb_err_dev = nullptr;
+}
+
+// open the peers' mailboxes (local: IPC mappings + device table + kernel binding)
+static int mb_open_peers(nk_ctx* c, int rank, int nranks, const char* handles) {
+    NK_TRY(mb_alloc(c));
+    mb_disable(c);
+    std::vector<uint64_t*> peers((size_t)nranks);
+    for (int r = 0; r < nranks; ++r) {
+        if (r == rank) {
+            peers[r] = c->mb_self;
+            continue;
+        }
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handles + 64 * (size_t)r, 64);
+        void* p = nullptr;
+        if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+            mb_disable(c);
+            return fail(c, NK_E_HIP, "mailbox: hipIpcOpenMemHandle failed for rank " + std::to_string(r));
+        }
+        c->mb_opened.push_back(p);
+        peers[r] = static_cast<uint64_t*>(p);
+    }
+    NK_HIP(c, hipMalloc(reinterpret_cast<void**>(&c->mb_peers_dev), sizeof(uint64_t*) * nranks));
+    NK_HIP(c, hipMemcpy(c->mb_peers_dev, peers.data(), sizeof(uint64_t*) * nranks, hipMemcpyHostToDevice));
+    *c->mb_err = 0;
+    c->mb_on = true;
+    return mailbox_bind(c);
+}
+
+// a rank whose mailbox is not open still waits out the self-test's timeout on the others: every
+// rank reaches the collective verdict, nobody hangs
+static int mb_verdict(nk_ctx* c, bool local_ok) {
+    bool ok = local_ok;
+    if (c->mb_on) {
+        bool t = false;
+        if (mailbox_selftest(c, &t) != NK_OK) t = false;
+        ok = ok && t;
+    }
+    if (c->comm) {  // all ranks must take the same path: min over ranks
+        double v = ok ? 1.0 : 0.0;
+        NK_HIP(c, hipMemcpy(c->scal, &v, sizeof(double), hipMemcpyHostToDevice));
+        if (ncclAllReduce(c->scal, c->scal, 1, ncclFloat64, ncclMin, c->comm->comm, c->stream) != ncclSuccess) v = 0.0;
+        else {
+            NK_HIP(c, hipMemcpyAsync(c->hpin, c->scal, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+            NK_HIP(c, hipStreamSynchronize(c->stream));
+            v = c->hpin[0];
+        }
+        ok = ok && v == 1.0;
+    }
+    if (c->mb_err) *c->mb_err = 0;
+    if (!ok) {
+        mb_disable(c);
+        return fail(c, NK_E_RCCL, "peer mailbox self-test failed (values did not arrive)");
+    }
+    return NK_OK;
+}
+
 }  // namespace nk
 
 using namespace nk;
@@ -96,10 +193,57 @@ int nk_dist_init(nk_ctx* c, int32_t rank, int32_t nranks, const char id[128]) {
     c->comm = cm;
     c->rank = rank;
     c->nranks = nranks;
+    const char* mbe = getenv("NK_DIST_MAILBOX");
+    // one-shot peer all-reduce of the scalars: on by default with several ranks; NK_DIST_MAILBOX=1
+    // also turns it on for a forced 1-rank communicator (exercises the path on one GPU), =0 off
+    const bool mb_want = (mbe && *mbe == '1') || (nranks > 1 && !(mbe && *mbe == '0'));
+    if (mb_want && nranks <= kMbRanks) {
+        std::vector<char> all((size_t)64 * nranks, 0);
+        char* dbuf = nullptr;
+        int rc = nk_dist_mailbox_handle(c, all.data() + 64 * (size_t)rank);
+        if (hipMalloc(&dbuf, all.size()) != hipSuccess) {
+            std::fprintf(stderr, "[nkhip] rank %d: no memory for the handle exchange\n", rank);
+            return fail(c, NK_E_NOMEM, "hipMalloc (mailbox handles)");
+        }
+        // allgather the IPC handles: collective, every rank takes part whatever its local state
+        (void)hipMemcpy(dbuf + 64 * (size_t)rank, all.data() + 64 * (size_t)rank, 64, hipMemcpyHostToDevice);
+        const ncclResult_t ag = ncclAllGather(dbuf + 64 * (size_t)rank, dbuf, 64, ncclChar, cm->comm, c->stream);
+        if (ag != ncclSuccess || hipStreamSynchronize(c->stream) != hipSuccess ||
+            hipMemcpy(all.data(), dbuf, all.size(), hipMemcpyDeviceToHost) != hipSuccess)
+            rc = NK_E_RCCL;
+        (void)hipFree(dbuf);
+        if (ag != ncclSuccess) return rccl_fail(c, ag, "ncclAllGather (mailbox handles)");
+        if (rc == NK_OK) rc = mb_open_peers(c, rank, nranks, all.data());
+        if (mb_verdict(c, rc == NK_OK) != NK_OK) {
+            std::fprintf(stderr, "[nkhip] rank %d: peer mailbox off (%s); reductions use ncclAllReduce\n", rank,
+                         c->err.c_str());
+            c->err.clear();
+        }
+    }
     return NK_OK;
 }
 
+int nk_dist_mailbox_handle(nk_ctx* c, char out[64]) {
+    if (!c || !out) return NK_E_ARG;
+    NK_TRY(mb_alloc(c));
+    hipIpcMemHandle_t h;
+    NK_HIP(c, hipIpcGetMemHandle(&h, c->mb_self));
+    static_assert(sizeof(h) == 64, "hipIpcMemHandle_t size");
+    std::memcpy(out, &h, 64);
+    return NK_OK;
+}
+
+int nk_dist_mailbox_open(nk_ctx* c, int32_t rank, int32_t nranks, const char* handles) {
+    if (!c || !handles || nranks < 1 || nranks > kMbRanks || rank < 0 || rank >= nranks) return NK_E_ARG;
+    if (c->comm) return fail(c, NK_E_STATE, "nk_dist_init already set up the mailbox of this context");
+    c->rank = rank;  // mailbox-only (no RCCL communicator): reductions across ranks, no halo exchange
+    c->nranks = nranks;
+    const int rc = mb_open_peers(c, rank, nranks, handles);
+    return mb_verdict(c, rc == NK_OK);
+}
+
 int nk_dist_free(nk_ctx* c) {
+    if (c) mb_free(c);
     if (!c || !c->comm) return NK_OK;
     ncclCommDestroy(c->comm->comm);
     delete c->comm;

@@ -64,6 +64,15 @@ struct nk_ctx {
     // user kinds: the FD evaluation point w = u + eps v (one grid function, reallocated on a new geometry)
     double* user_w = nullptr;
     int64_t user_w_n = -1, user_w_plane = -1;
+    // one-shot peer all-reduce of reduction scalars (nk_dist.cpp "mailbox"): fine-grained device
+    // memory every rank can write over xGMI; epochs tag the granules
+    bool mb_on = false;
+    uint64_t* mb_self = nullptr;           // my mailbox (kMbSlots x kMbRanks x 2 granules)
+    uint64_t** mb_peers_dev = nullptr;     // device table: rank -> that rank's mailbox (IPC-mapped)
+    std::vector<void*> mb_opened;          // IPC mappings to close
+    int* mb_err = nullptr;                 // pinned host flag: a consumer timed out waiting for a peer
+    int* mb_err_dev = nullptr;             // its device address
+    unsigned mb_epoch = 1;
     // distribution
     int rank = 0, nranks = 1;
     nk::Comm* comm = nullptr;
@@ -125,13 +134,19 @@ int launch(nk_ctx* c, const char* name, double bytes, F&& f) {
 // order, so every block (and every run) sees the bit-identical value.
 struct Red {
     const double* ptr;
-    int len;
+    int len;                // < 0: the value arrives through the peer mailbox, epoch = -len
     double* fin = nullptr;  // multi-rank: the producing kernel already folded its partials here
+    unsigned epoch = 0;     // mailbox epoch the producing kernel published under (0: none)
 };
 double* red_slot(nk_ctx* c);                 // next partial-sum slot of the ring
 double* red_out(nk_ctx* c, int len, Red* r, int* fin);  // slot for a reduction launch (+ fold flag)
 int finish_reduction(nk_ctx* c, Red* r);     // multi-rank: collapse + RCCL all-reduce
+int mb_check(nk_ctx* c);                     // after a host sync: did a mailbox wait time out?
 int red_blocks(int64_t n);                   // grid size of streaming reductions
+constexpr int kMbSlots = 256;                // mailbox ring (epoch % kMbSlots)
+constexpr int kMbRanks = 64;                 // max ranks of the mailbox all-reduce
+int mailbox_bind(nk_ctx* c);                 // make c's mailbox the one the kernels use (nk_kernels.hip)
+int mailbox_selftest(nk_ctx* c, bool* ok);   // a few epochs through the mailbox vs the expected sums
 
 // ---------------------------------------------------------------- kernel launchers (nk_kernels.hip)
 struct StencilIn {

@@ -43,6 +43,69 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
 
 // fixed-order sum of in[0..len), broadcast to the whole block.  All 256 threads load (8
 // independent loads in flight each), so a block pays ~one L2 round trip, not 32 dependent ones.
+// ------------------------------------------------------------------------------ peer mailbox
+// One-shot all-reduce of a reduction scalar across ranks without a collective launch: the
+// producing kernel's last block writes its folded value into EVERY rank's mailbox (fine-grained
+// device memory, IPC-mapped over xGMI), the consuming kernel polls the nranks entries of its own
+// mailbox and sums them in rank order -- the same order on every rank, so every rank holds the
+// bit-identical scalar.  Each 64-bit value travels as two self-validating 8-byte granules
+// {epoch:32 | half:32} (cdna_hip_programming.md §6 G16, R2: no flag, no fence, no tearing).
+// Spins are bounded: a peer that never arrives sets the error flag instead of hanging the GPU.
+struct MbInfo {
+    uint64_t* self;
+    uint64_t* const* peers;
+    int rank, nranks;
+    int* err;            // pinned host flag
+    unsigned spin_limit;
+};
+__device__ MbInfo g_mb;
+
+__device__ __forceinline__ uint64_t* mb_cell(uint64_t* base, unsigned epoch, int rank) {
+    return base + ((size_t)(epoch % kMbSlots) * kMbRanks + rank) * 2;
+}
+
+// lanes r < nranks (first wave) send {epoch, t} to rank r
+__device__ __forceinline__ void mb_send(double t, unsigned epoch) {
+    const int l = threadIdx.x;
+    if (l < g_mb.nranks) {
+        const uint64_t bits = (uint64_t)__double_as_longlong(t);
+        const uint64_t tag = (uint64_t)epoch << 32;
+        uint64_t* cell = mb_cell(g_mb.peers[l], epoch, g_mb.rank);
+        __hip_atomic_store(cell, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(cell + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// Σ_r value_r of `epoch` in rank order, broadcast to the whole block (all threads must call)
+__device__ double mb_recv(unsigned epoch, double* sh) {
+    if (threadIdx.x < 64) {
+        const int l = threadIdx.x, nr = g_mb.nranks;
+        uint32_t half = 0;
+        if (l < 2 * nr) {
+            const uint64_t* g = mb_cell(g_mb.self, epoch, l >> 1) + (l & 1);
+            uint64_t x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            unsigned spins = 0;
+            while ((unsigned)(x >> 32) != epoch) {
+                if (++spins > g_mb.spin_limit) {
+                    __hip_atomic_store(g_mb.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    x = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+                x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            half = (uint32_t)x;
+        }
+        const uint32_t hi = __shfl_down(half, 1, 64);
+        const double v = __longlong_as_double((long long)(((uint64_t)hi << 32) | half));
+        double t = 0.0;
+        for (int r = 0; r < nr; ++r) t += __shfl(v, 2 * r, 64);  // fixed rank order
+        if (l == 0) sh[4] = t;
+    }
+    __syncthreads();
+    return sh[4];
+}
+
 // SC1 = true reads with agent-scope (sc1) loads: values other blocks of the SAME launch stored
 // write-through (publish), which this CU's L1 or this XCD's L2 may hold stale copies of.
 template <bool SC1 = false>
@@ -53,6 +116,7 @@ __device__ __forceinline__ double ld_part(const double* p) {
 
 template <bool SC1 = false>
 __device__ __forceinline__ double reduce_input(const double* __restrict__ in, int len, double* sh) {
+    if (len < 0) return mb_recv((unsigned)(-len), sh);  // all-reduced through the peer mailbox
     double t = 0.0;
     int m = threadIdx.x;
     for (; m + 7 * kBlock < len; m += 8 * kBlock) {
@@ -97,6 +161,7 @@ __device__ __forceinline__ void publish(double acc, double* part, int fin, doubl
         part[kRedCap - 1] = t;
         __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (fin >= 2) mb_send(t, (unsigned)fin);  // fin = mailbox epoch: straight to every rank
 }
 
 __device__ __forceinline__ double lap(double c, double p, double m, double h2) { return ((p - 2.0 * c) + m) / h2; }
@@ -997,14 +1062,60 @@ int env_int(const char* name, int dflt) {
 }  // namespace
 
 // partial-sum slot of a reduction launch.  With a communicator the kernel also folds its partials
-// in place (publish) and finish_reduction only has to all-reduce part[kRedCap - 1].
+// in place (publish) and finish_reduction only has to all-reduce part[kRedCap - 1]; with the peer
+// mailbox the kernel also sends the folded value to every rank (fin = the epoch, >= 2).
 double* red_out(nk_ctx* c, int len, Red* r, int* fin) {
     double* part = red_slot(c);
     *fin = c->comm ? 1 : 0;
+    r->epoch = 0;
+    if (c->mb_on) {
+        if (c->mb_epoch >= 0x7ffffff0u) c->mb_epoch = 1;  // epochs 2 .. 2^31: kernel-argument ints
+        r->epoch = ++c->mb_epoch;
+        *fin = (int)r->epoch;
+    }
     r->ptr = part;
     r->len = len;
     r->fin = *fin ? part + kRedCap - 1 : nullptr;
     return part;
+}
+
+int mailbox_bind(nk_ctx* c) {
+    MbInfo m{};
+    if (c->mb_on) {
+        m.self = c->mb_self;
+        m.peers = c->mb_peers_dev;
+        m.rank = c->rank;
+        m.nranks = c->nranks;
+        m.err = c->mb_err_dev;
+        const char* e = getenv("NK_MB_SPIN_LIMIT");
+        m.spin_limit = (e && *e) ? (unsigned)atoll(e) : (1u << 24);  // ~1 s of polling
+    }
+    NK_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(g_mb), &m, sizeof(m)));
+    return NK_OK;
+}
+
+namespace {
+__global__ void k_mb_test(unsigned epoch, double value, double* out) {
+    __shared__ double sh[8];
+    mb_send(value, epoch);
+    const double t = mb_recv(epoch, sh);
+    if (threadIdx.x == 0) *out = t;
+}
+}  // namespace
+
+// every rank sends (rank + 1) (e + 1) for a few epochs; the sums must arrive exactly
+int mailbox_selftest(nk_ctx* c, bool* ok) {
+    *ok = true;
+    for (int e = 0; e < 4; ++e) {
+        const unsigned epoch = ++c->mb_epoch;
+        hipLaunchKernelGGL(k_mb_test, dim3(1), dim3(64), 0, c->stream, epoch, (double)(c->rank + 1) * (e + 1), c->scal);
+        NK_HIP(c, hipGetLastError());
+        NK_HIP(c, hipMemcpyAsync(c->hpin, c->scal, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        NK_HIP(c, hipStreamSynchronize(c->stream));
+        const double want = (double)c->nranks * (c->nranks + 1) / 2 * (e + 1);
+        if (c->hpin[0] != want || *c->mb_err) *ok = false;
+    }
+    return NK_OK;
 }
 
 int red_blocks(int64_t n) {

@@ -131,6 +131,7 @@ int host_scalar(nk_ctx* c, Red r, int sqrt_it, double* out) {
     NK_HIP(c, hipMemcpyAsync(c->hpin, c->scal, sizeof(double), hipMemcpyDeviceToHost, c->stream));
     NK_HIP(c, hipStreamSynchronize(c->stream));
     if (c->prof) prof_drain(c, false);
+    NK_TRY(mb_check(c));
     *out = c->hpin[0];
     return NK_OK;
 }
@@ -295,6 +296,7 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
             const bool last = restart ? (inner_iter >= std::min<int64_t>(mem, inner_itmax)) : (inner_iter >= inner_itmax);
             if (!last) NK_TRY(issue(k + 1));
             NK_HIP(c, hipEventSynchronize(ws->col_ready[k & 1]));
+            NK_TRY(mb_check(c));
             if (c->prof) prof_drain(c, false);
             const double* hcol = slot_pin(k);
             const int np = npasses_of(k);

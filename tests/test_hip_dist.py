@@ -51,6 +51,44 @@ def test_forced_rccl_one_rank_is_bitwise(monkeypatch):
     assert np.array_equal(x1, x2) and n1 == n2
 
 
+def test_forced_one_rank_mailbox_is_bitwise(monkeypatch):
+    """The same, with every reduction scalar travelling through the peer mailbox (self-send)."""
+    P = oc.bratu2d(48)
+    u0 = oc.sin_ic(P)
+    b = oc.residual(P, u0)
+    plain = ah.Context(0)
+    x1, s1, n1 = gmres_run(plain, P, u0, b)
+    monkeypatch.setenv("NK_DIST_FORCE", "1")
+    monkeypatch.setenv("NK_DIST_MAILBOX", "1")
+    forced = ah.Context(0)
+    forced.init_distributed(0, 1, ah.dist_unique_id())
+    x2, s2, n2 = gmres_run(forced, P, u0, b)
+    assert s1.niter == s2.niter == 40
+    assert s1.residuals == s2.residuals
+    assert np.array_equal(x1, x2) and n1 == n2
+
+
+def test_mailbox_two_ranks_one_gpu(tmp_path):
+    """Two processes on one GPU reduce through each other's mailboxes (IPC, no RCCL)."""
+    out = str(tmp_path / "mb")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tests", "mailbox_worker.py"), "--out", out]
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
+    try:
+        log, _ = proc.communicate(timeout=180)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, signal.SIGKILL)
+        pytest.fail("mailbox worker timed out")
+    assert proc.returncode == 0, log.decode()[-3000:]
+    meta = json.load(open(out + ".json"))
+    n = meta["n"]
+    y = np.arange(n, dtype=np.float64) % 7
+    for k, (dot, nrm2) in enumerate(meta["results"], start=1):
+        assert dot == sum((r + k) * y.sum() for r in range(2))
+        assert abs(nrm2 - 2 * (y * y).sum()) <= 1e-9 * nrm2  # sqrt then square: a few ulp
+
+
 def free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
