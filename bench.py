@@ -347,7 +347,9 @@ def main():
             "dtype": "f64",
             "data": "synthetic (see config.workload)",
             "config": {"workload": W.workload, "matvecs_per_step": matvecs // max(1, args.steps),
-                       "parallelism": f"slab{world}"},
+                       "parallelism": f"slab{world}",
+                       "reductions": ("peer mailbox (IPC/xGMI)" if ctx.mailbox_active else
+                                      ("ncclAllReduce" if world > 1 else "local"))},
             "hbm_gbs_algorithmic": round(world * total_bytes / elapsed / 1e9, 1) if total_bytes else None,
             "roofline": roof(dominant) if dominant else None,
             "jv_roofline": roof(jv_kernel),

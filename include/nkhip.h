@@ -207,6 +207,7 @@ int nk_halo_exchange(nk_ctx* ctx, const nk_problem* p, double* v);
  * callers that exchange the 64-byte IPC handles themselves (no RCCL communicator: reductions only). */
 int nk_dist_mailbox_handle(nk_ctx* ctx, char out[64]);
 int nk_dist_mailbox_open(nk_ctx* ctx, int32_t rank, int32_t nranks, const char* handles /* nranks x 64 */);
+int nk_dist_mailbox_active(nk_ctx* ctx);  /* 1: reductions use the peer mailbox, 0: RCCL / single rank */
 
 /* ---------------------------------------------------------------- profiling (HIP events, per kernel class) */
 #define NK_PROF_NAME 32

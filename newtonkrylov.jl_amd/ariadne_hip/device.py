@@ -66,6 +66,10 @@ class Context:
             pass
 
     # -- distribution ------------------------------------------------------------------------
+    @property
+    def mailbox_active(self) -> bool:
+        return bool(load().nk_dist_mailbox_active(self.handle))
+
     def mailbox_handle(self) -> bytes:
         """64-byte IPC handle of this context's peer mailbox (nk_dist_mailbox_handle)."""
         buf = C.create_string_buffer(64)

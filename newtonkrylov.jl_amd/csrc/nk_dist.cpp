@@ -242,6 +242,8 @@ int nk_dist_mailbox_open(nk_ctx* c, int32_t rank, int32_t nranks, const char* ha
     return mb_verdict(c, rc == NK_OK);
 }
 
+int nk_dist_mailbox_active(nk_ctx* c) { return (c && c->mb_on) ? 1 : 0; }
+
 int nk_dist_free(nk_ctx* c) {
     if (c) mb_free(c);
     if (!c || !c->comm) return NK_OK;
