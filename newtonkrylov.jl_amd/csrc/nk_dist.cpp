@@ -22,10 +22,12 @@ static int rccl_fail(nk_ctx* c, ncclResult_t r, const char* what) {
 }
 
 int halo_exchange(nk_ctx* c, const nk_problem* p, const double* v) {
-    if (!c->comm) return NK_OK;
+    if (!c->comm && !c->mb_on) return NK_OK;
     Geo g;
     NK_TRY(geometry(c, p, &g));
     double* vv = const_cast<double*>(v);  // only the ghost planes are written
+    if (c->mb_on && g.plane <= c->halo_cap) return launch_halo_ipc(c, vv, g.plane, g.nplanes);
+    if (!c->comm) return fail(c, NK_E_ARG, "ghost plane larger than the IPC inbox (NK_HALO_CAP) and no RCCL communicator");
     const size_t pl = (size_t)g.plane;
     const int up = c->rank + 1, dn = c->rank - 1;
     ncclComm_t comm = c->comm->comm;
@@ -68,7 +70,9 @@ int allreduce_scalar(nk_ctx* c, double* dev, int64_t count) {
 static int mb_alloc(nk_ctx* c) {
     if (c->mb_self) return NK_OK;
     NK_HIP(c, hipSetDevice(c->device));
-    const size_t bytes = sizeof(uint64_t) * 2 * kMbSlots * kMbRanks;
+    const char* hc = getenv("NK_HALO_CAP");  // doubles per inbox plane (default 1M: a 1024^2 3D plane)
+    c->halo_cap = (hc && *hc) ? atoll(hc) : ((int64_t)1 << 20);
+    const size_t bytes = sizeof(uint64_t) * (kMbWords + kHaloFlagWords) + sizeof(double) * 4 * (size_t)c->halo_cap;
     void* p = nullptr;
     if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) != hipSuccess)
         return fail(c, NK_E_NOMEM, "mailbox: fine-grained allocation failed");

@@ -73,6 +73,8 @@ struct nk_ctx {
     int* mb_err = nullptr;                 // pinned host flag: a consumer timed out waiting for a peer
     int* mb_err_dev = nullptr;             // its device address
     unsigned mb_epoch = 1;
+    int64_t halo_cap = 0;                  // doubles per inbox plane (0: no IPC halo exchange)
+    uint64_t halo_epoch = 0;
     // distribution
     int rank = 0, nranks = 1;
     nk::Comm* comm = nullptr;
@@ -145,8 +147,17 @@ int mb_check(nk_ctx* c);                     // after a host sync: did a mailbox
 int red_blocks(int64_t n);                   // grid size of streaming reductions
 constexpr int kMbSlots = 256;                // mailbox ring (epoch % kMbSlots)
 constexpr int kMbRanks = 64;                 // max ranks of the mailbox all-reduce
+constexpr int kHaloBlocks = 64;              // blocks (= flags per side) of the IPC ghost-plane exchange
+// one fine-grained region per rank, IPC-mapped by every other rank:
+//   [mailbox: kMbSlots x kMbRanks x 2 u64][halo flags: 2 parity x 2 sides x kHaloBlocks u64]
+//   [halo inbox: 2 parity x 2 sides x halo_cap doubles]   (side 0: from the lower rank, 1: from the upper)
+constexpr size_t kMbWords = (size_t)2 * kMbSlots * kMbRanks;
+constexpr size_t kHaloFlagWords = (size_t)2 * 2 * kHaloBlocks;
 int mailbox_bind(nk_ctx* c);                 // make c's mailbox the one the kernels use (nk_kernels.hip)
 int mailbox_selftest(nk_ctx* c, bool* ok);   // a few epochs through the mailbox vs the expected sums
+// ghost planes of v (interior pointer, `plane` doubles per plane, `nplanes` planes) through the peer
+// inboxes: push my boundary planes into the neighbours' inboxes, pull theirs into my ghost planes
+int launch_halo_ipc(nk_ctx* c, double* v, int64_t plane, int64_t nplanes);
 
 // ---------------------------------------------------------------- kernel launchers (nk_kernels.hip)
 struct StencilIn {

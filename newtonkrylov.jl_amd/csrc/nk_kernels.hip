@@ -1103,6 +1103,87 @@ __global__ void k_mb_test(unsigned epoch, double value, double* out) {
 }
 }  // namespace
 
+namespace {
+__device__ __forceinline__ uint64_t* halo_flags(uint64_t* base) { return base + kMbWords; }
+__device__ __forceinline__ uint64_t* halo_inbox(uint64_t* base, int par, int side, int64_t cap) {
+    return base + kMbWords + kHaloFlagWords + (size_t)(par * 2 + side) * (size_t)cap;
+}
+
+// Ghost planes through the peers' inboxes (IPC-mapped fine-grained memory over xGMI).  Block b
+// owns chunk b of the plane: it pushes my boundary-plane chunks into the lower / upper
+// neighbour's inbox (system-scope stores), drains, raises its epoch flag there, then waits for the
+// neighbours' block b flags in my region and copies their chunks into my ghost planes.  Inboxes
+// alternate by epoch parity: epoch e's push can only start after the neighbour finished epoch e-2.
+__global__ __launch_bounds__(kBlock) void k_halo_ipc(double* __restrict__ v, int64_t plane, int64_t nplanes,
+                                                    uint64_t epoch, int64_t cap) {
+    __shared__ int ready;
+    const int b = blockIdx.x, rank = g_mb.rank, nr = g_mb.nranks;
+    const bool lo = rank > 0, hi = rank + 1 < nr;
+    const int par = (int)(epoch & 1);
+    const int64_t per = (plane + gridDim.x - 1) / gridDim.x;
+    const int64_t c0 = (int64_t)b * per, c1 = c0 + per < plane ? c0 + per : plane;
+    const double* first = v;
+    const double* last = v + (nplanes - 1) * plane;
+    if (lo) {  // my first interior plane -> the lower rank's "from upper" inbox
+        uint64_t* dst = halo_inbox(g_mb.peers[rank - 1], par, 1, cap);
+        for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
+            __hip_atomic_store(dst + i, (uint64_t)__double_as_longlong(first[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (hi) {  // my last interior plane -> the upper rank's "from lower" inbox
+        uint64_t* dst = halo_inbox(g_mb.peers[rank + 1], par, 0, cap);
+        for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
+            __hip_atomic_store(dst + i, (uint64_t)__double_as_longlong(last[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every thread drains its stores before the flag
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (lo) __hip_atomic_store(halo_flags(g_mb.peers[rank - 1]) + (par * 2 + 1) * kHaloBlocks + b, epoch,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (hi) __hip_atomic_store(halo_flags(g_mb.peers[rank + 1]) + (par * 2 + 0) * kHaloBlocks + b, epoch,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ready = 1;
+        for (int side = 0; side < 2; ++side) {
+            if ((side == 0 && !lo) || (side == 1 && !hi)) continue;
+            const uint64_t* f = halo_flags(g_mb.self) + (par * 2 + side) * kHaloBlocks + b;
+            unsigned spins = 0;
+            while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+                if (++spins > g_mb.spin_limit) {
+                    __hip_atomic_store(g_mb.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    ready = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+    }
+    __syncthreads();
+    if (!ready) return;
+    if (lo) {
+        const uint64_t* src = halo_inbox(g_mb.self, par, 0, cap);
+        for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
+            v[i - plane] = __longlong_as_double((long long)__hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    }
+    if (hi) {
+        const uint64_t* src = halo_inbox(g_mb.self, par, 1, cap);
+        for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
+            v[nplanes * plane + i] =
+                __longlong_as_double((long long)__hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    }
+}
+}  // namespace
+
+int launch_halo_ipc(nk_ctx* c, double* v, int64_t plane, int64_t nplanes) {
+    if (c->nranks < 2) return NK_OK;
+    const uint64_t epoch = ++c->halo_epoch;
+    int nb = (int)((plane + 1023) / 1024);
+    if (nb > kHaloBlocks) nb = kHaloBlocks;
+    if (nb < 1) nb = 1;
+    const int nbrs = (c->rank > 0) + (c->rank + 1 < c->nranks);
+    return launch(c, "halo", 16.0 * plane * nbrs, [&] {
+        hipLaunchKernelGGL(k_halo_ipc, dim3(nb), dim3(kBlock), 0, c->stream, v, plane, nplanes, epoch, c->halo_cap);
+    });
+}
+
 // every rank sends (rank + 1) (e + 1) for a few epochs; the sums must arrive exactly
 int mailbox_selftest(nk_ctx* c, bool* ok) {
     *ok = true;

@@ -22,6 +22,9 @@ ap.add_argument("--out", required=True)
 ap.add_argument("--nx", type=int, default=48)
 ap.add_argument("--ny", type=int, default=40)
 ap.add_argument("--jv", default="exact")
+ap.add_argument("--transport", choices=["rccl", "mailbox"], default="rccl",
+                help="rccl: nk_dist_init (RCCL bootstrap, then the peer mailbox / RCCL fallback); mailbox: "
+                     "IPC handles exchanged over gloo, no RCCL at all (works with every rank on one GPU)")
 args = ap.parse_args()
 
 dist.init_process_group("gloo")
@@ -37,12 +40,17 @@ def bcast(obj, src):
     return box[0]
 
 
-try:
-    ah.init_distributed(ctx, rank, world, bcast)
-except ah.NKError as e:
-    if rank == 0:
-        json.dump({"skip": f"RCCL communicator could not be created: {e}"}, open(args.out + ".json", "w"))
-    sys.exit(0)
+if args.transport == "mailbox":
+    handles = [None] * world
+    dist.all_gather_object(handles, ctx.mailbox_handle())
+    ctx.mailbox_open(rank, world, b"".join(handles))
+else:
+    try:
+        ah.init_distributed(ctx, rank, world, bcast)
+    except ah.NKError as e:
+        if rank == 0:
+            json.dump({"skip": f"RCCL communicator could not be created: {e}"}, open(args.out + ".json", "w"))
+        sys.exit(0)
 
 nx, ny = args.nx, args.ny
 grid = ah.slab((nx, ny), rank, world)

@@ -95,12 +95,17 @@ def free_port():
         return s.getsockname()[1]
 
 
+@pytest.mark.parametrize("transport", ["mailbox", "rccl"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_slabs_match_oracle(tmp_path, world):
+def test_slabs_match_oracle(tmp_path, world, transport):
+    """Slabs of one 2D Bratu grid on `world` ranks: residual, Jv (ghost rows from the neighbours),
+    a dot, and a whole Newton-GMRES solve against the oracle on the full grid.  transport=mailbox
+    runs ghost planes and reductions through the IPC-mapped peer regions only (no RCCL), so all
+    ranks can share the one GPU of the test box; transport=rccl needs one GPU per rank."""
     out = str(tmp_path / "dist")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out]
+           os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", transport]
     env = dict(os.environ, NK_WORKER_SHARED_DEVICE="1")
     proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
     try:
