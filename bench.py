@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--prof-every", type=int, default=64,
                     help="time every k-th launch of each kernel class (HIP events; k > 1 keeps their cost out)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--transport", choices=["rccl", "mailbox"], default="rccl",
+                    help="N > 1: rccl = nk_dist_init (RCCL bootstrap; peer mailbox + IPC ghost planes when available); "
+                         "mailbox = IPC handles over gloo, no RCCL (diagnostic: lets ranks share one GPU)")
     ap.add_argument("--cpu-itmax", type=int, default=300, help="Arnoldi steps in the CPU-baseline sample (300 = one bench step)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os.cpu_count())")
     ap.add_argument("--traffic-json", default="",
@@ -247,9 +250,13 @@ def main():
         import torch.distributed as dist
 
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    ctx = ah.Context(local)
+    ctx = ah.Context(int(os.environ.get("NK_BENCH_DEVICE", local)))  # NK_BENCH_DEVICE: diagnostic override
     ah.set_default_context(ctx)
-    if world > 1:
+    if world > 1 and args.transport == "mailbox":
+        handles = [None] * world
+        dist.all_gather_object(handles, ctx.mailbox_handle())
+        ctx.mailbox_open(rank, world, b"".join(handles))
+    elif world > 1:
         obj = [ah.dist_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         ctx.init_distributed(rank, world, obj[0])
