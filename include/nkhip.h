@@ -146,12 +146,15 @@ typedef struct nk_krylov_opts {
     double atol, rtol;            /* Krylov stopping: ||r|| <= atol + rtol ||b||      */
     double b_norm;                /* > 0: ||b|| is known (the Newton loop just computed ||F(u)||): not recomputed */
     double u_norm;                /* > 0: ||u|| is known (FD step size): not recomputed                          */
+    double* u_update;             /* non-null: the Newton update u .-= x is fused into the solve's last pass;
+                                     x is then NOT stored and stats.u_norm = ||u|| afterwards                */
 } nk_krylov_opts;
 
 typedef struct nk_krylov_stats {
     int64_t niter;                /* workspace.stats.niter (Arnoldi / CG iterations)  */
     int32_t solved, inconsistent, breakdown, status; /* status 1 solved 2 tired 3 breakdown 4 zero curvature */
     int64_t n_matvec;             /* mul!(J) calls incl. restart residuals            */
+    double u_norm;                /* ||u|| after the fused update (opts.u_update)     */
 } nk_krylov_stats;
 
 /* memory = Krylov workspace memory (GMRES restart length; default 20 like Krylov.jl). */

@@ -48,12 +48,12 @@ class nk_user_ops(C.Structure):
 class nk_krylov_opts(C.Structure):
     _fields_ = [("restart", C.c_int32), ("reorthogonalization", C.c_int32), ("itmax", C.c_int32),
                 ("jv_mode", C.c_int32), ("atol", C.c_double), ("rtol", C.c_double), ("b_norm", C.c_double),
-                ("u_norm", C.c_double)]
+                ("u_norm", C.c_double), ("u_update", C.c_void_p)]
 
 
 class nk_krylov_stats(C.Structure):
     _fields_ = [("niter", C.c_int64), ("solved", C.c_int32), ("inconsistent", C.c_int32),
-                ("breakdown", C.c_int32), ("status", C.c_int32), ("n_matvec", C.c_int64)]
+                ("breakdown", C.c_int32), ("status", C.c_int32), ("n_matvec", C.c_int64), ("u_norm", C.c_double)]
 
 
 NK_FORCING_NONE, NK_FORCING_FIXED, NK_FORCING_EW = 0, 1, 2

@@ -17,7 +17,7 @@ from typing import NamedTuple
 from . import _lib
 from ._lib import load
 from .device import DeviceArray
-from .krylov import KrylovConstructor, kaxpy_norm_, krylov_solve_, krylov_workspace
+from .krylov import KrylovConstructor, krylov_solve_, krylov_workspace
 from .problems import DeviceResidual
 
 log = logging.getLogger("ariadne_hip")
@@ -271,10 +271,11 @@ def newton_krylov_(F_: DeviceResidual, u: DeviceArray, p=None, res: DeviceArray 
             kwargs = {"rtol": eta, **kwargs}  # user krylov_kwargs win (:330-333)
         # Solve J d = F(u).  The reference passes copy(res) because Enzyme rewrites res inside
         # mul!; the device operator never writes res, so res itself is the right-hand side.
-        krylov_solve_(workspace, J, res, _b_norm=n_res, _u_norm=u_norm, **kwargs)
+        # u .-= 1 .* d (Newton step s = 1, :341-344) is fused into the solve's last pass (d =
+        # workspace.x is consumed there, not stored), which also returns ||u|| for the next FD step
+        krylov_solve_(workspace, J, res, _b_norm=n_res, _u_norm=u_norm, _u_update=u, **kwargs)
         n_matvec += workspace.stats.n_matvec
-        d = workspace.x
-        u_norm = kaxpy_norm_(n, -1.0, d, u)  # u .-= 1 .* d  (Newton step s = 1, :341-344), + ||u||
+        u_norm = workspace.stats.u_norm
         n_res_prior = n_res
         n_res = F_.residual_norm(res, u, p)
         callback(u, res, n_res)

@@ -102,6 +102,7 @@ class KrylovStats:
     status: str = "unknown"
     n_matvec: int = 0
     residuals: list = field(default_factory=list)
+    u_norm: float = 0.0  # ||u|| after a fused Newton update (_u_update)
 
 
 _STATUS = {0: "unknown", 1: "solution good enough given atol and rtol", 2: "maximum number of iterations exceeded",
@@ -146,10 +147,11 @@ def krylov_workspace(algo, kc: KrylovConstructor) -> KrylovWorkspace:
 
 def krylov_solve_(ws: KrylovWorkspace, J, b: DeviceArray, *, restart=False, reorthogonalization=False,
                   atol=SQRT_EPS, rtol=SQRT_EPS, itmax=0, history=False, verbose=0, M=None, N=None, ldiv=False,
-                  _b_norm=0.0, _u_norm=0.0, **unknown):
+                  _b_norm=0.0, _u_norm=0.0, _u_update=None, **unknown):
     """krylov_solve!(workspace, J, b; kwargs...) for a JacobianOperator J on device vectors.
     (_b_norm / _u_norm: norms the Newton loop already holds -- ||F(u)|| and ||u|| -- so the solve
-    does not stream b and u once more just to recompute them.)"""
+    does not stream b and u once more just to recompute them.  _u_update = u: the Newton update
+    u .-= x is fused into the last pass; ws.x is then not stored and ws.stats.u_norm = ||u||.)"""
     if unknown:
         raise TypeError(f"unsupported Krylov keyword(s): {sorted(unknown)}")
     if M is not None or N is not None:
@@ -158,7 +160,8 @@ def krylov_solve_(ws: KrylovWorkspace, J, b: DeviceArray, *, restart=False, reor
         raise TypeError("restart / reorthogonalization are GMRES keywords")
     prob = J.problem()
     opts = _lib.nk_krylov_opts(int(bool(restart)), int(bool(reorthogonalization)), int(itmax), J.jv_mode,
-                               float(atol), float(rtol), float(_b_norm), float(_u_norm))
+                               float(atol), float(rtol), float(_b_norm), float(_u_norm),
+                               _u_update.ptr if _u_update is not None else None)
     st = _lib.nk_krylov_stats()
     cap = ((int(itmax) or 4096) + 64) if history else 0
     hist = (C.c_double * max(cap, 1))()
@@ -168,7 +171,7 @@ def krylov_solve_(ws: KrylovWorkspace, J, b: DeviceArray, *, restart=False, reor
                                         hist, cap, C.byref(hl)), "krylov_solve!")
     ws.stats = KrylovStats(niter=int(st.niter), solved=bool(st.solved), inconsistent=bool(st.inconsistent),
                            status=_STATUS.get(st.status, "unknown"), n_matvec=int(st.n_matvec),
-                           residuals=list(hist[: min(hl.value, cap)]) if history else [])
+                           residuals=list(hist[: min(hl.value, cap)]) if history else [], u_norm=float(st.u_norm))
     if verbose:
         print(f"{ws.algo.upper()}: niter={ws.stats.niter} status={ws.stats.status}")
     return ws

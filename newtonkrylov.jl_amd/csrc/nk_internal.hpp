@@ -193,8 +193,10 @@ int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const dou
                     double* h_out, double* h_host, Red* out, int rev);
 // xr = Σ_i y_i V_i (fma chain from 0 in i order, y on device); then x = x + xr (restart) or
 // x = xr; optional partial sums of ||x||^2.
+// u (optional): the Newton update is fused into the last chunk -- u -= x_final, x is NOT stored,
+// and xnorm receives ||u||^2 partials instead of ||x||^2.
 int launch_update_x(nk_ctx* c, int64_t n, double* x, double* xr, const double* const* V, int k,
-                    const double* y_dev, int restart, Red* xnorm);
+                    const double* y_dev, int restart, Red* xnorm, double* u = nullptr);
 // CG pieces: x += a p ; r -= a Ap ; partial <r,r>   and   p = r + b p
 int launch_cg_update(nk_ctx* c, int64_t n, double alpha, double* x, double* r, const double* p,
                      const double* Ap, Red* rr);

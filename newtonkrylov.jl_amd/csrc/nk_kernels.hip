@@ -912,6 +912,7 @@ __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restri
 struct UpdArgs {
     const double* V[kMaxUpdateVecs];
     double* x;
+    double* u;           // Newton update fused in: u -= x_final (x itself is not stored), partials of ||u||^2
     double* xr;
     const double* y;
     double* part;
@@ -944,7 +945,15 @@ __global__ __launch_bounds__(kBlock) void k_update_x(UpdArgs A) {
                 xv.x = fma(1.0, t.x, x0.x);
                 xv.y = fma(1.0, t.y, x0.y);
             }
-            reinterpret_cast<dx2*>(A.x)[i] = xv;
+            if (A.u) {  // u .-= 1 .* d, exactly kaxpy!(n, -1, x, u) on the x that would have been stored
+                dx2 uv = reinterpret_cast<const dx2*>(A.u)[i];
+                uv.x = fma(-1.0, xv.x, uv.x);
+                uv.y = fma(-1.0, xv.y, uv.y);
+                reinterpret_cast<dx2*>(A.u)[i] = uv;
+                xv = uv;  // the norm below is ||u||
+            } else {
+                reinterpret_cast<dx2*>(A.x)[i] = xv;
+            }
             acc = fma(xv.x, xv.x, acc);
             acc = fma(xv.y, xv.y, acc);
         } else {
@@ -958,8 +967,13 @@ __global__ __launch_bounds__(kBlock) void k_update_x(UpdArgs A) {
         for (int m = 0; m < kMaxUpdateVecs; ++m)
             if (m < A.k) t = fma(yv[m], A.V[m][i], t);
         if (A.last) {
-            const double xv = A.restart ? fma(1.0, t, A.x[i]) : t;
-            A.x[i] = xv;
+            double xv = A.restart ? fma(1.0, t, A.x[i]) : t;
+            if (A.u) {
+                xv = fma(-1.0, xv, A.u[i]);
+                A.u[i] = xv;
+            } else {
+                A.x[i] = xv;
+            }
             acc = fma(xv, xv, acc);
         } else {
             A.xr[i] = t;
@@ -1374,11 +1388,12 @@ int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const dou
 }
 
 int launch_update_x(nk_ctx* c, int64_t n, double* x, double* xr, const double* const* V, int k, const double* y_dev,
-                    int restart, Red* xnorm) {
+                    int restart, Red* xnorm, double* u) {
     const int g = red_blocks(n);
     int done = 0;
     if (k == 0) {  // nothing to add: x unchanged (restart) or x = 0
         if (!restart) NK_TRY(launch_fill(c, n, x, 0.0));
+        if (u) return launch_axpy_sumsq(c, n, -1.0, x, u, xnorm);
         if (xnorm) return launch_sumsq(c, n, x, xnorm);
         return NK_OK;
     }
@@ -1390,10 +1405,11 @@ int launch_update_x(nk_ctx* c, int64_t n, double* x, double* xr, const double* c
         A.first = done == 0;
         A.last = done + m == k;
         A.restart = restart;
+        A.u = A.last ? u : nullptr;
         A.part = nullptr;
         if (A.last && xnorm) A.part = red_out(c, g, xnorm, &A.fin);
         // every chunk reads m basis vectors and (after the first) xr; the last writes x (reading it on restart)
-        const double bytes = 8.0 * n * (m + (A.first ? 0 : 1) + (A.last ? (restart ? 2 : 1) : 1));
+        const double bytes = 8.0 * n * (m + (A.first ? 0 : 1) + (A.last ? (restart ? 2 : 1) + (u ? 1 : 0) : 1));
         NK_TRY(launch(c, "update_x", bytes, [&] {
             hipLaunchKernelGGL(k_update_x, dim3(g), dim3(kBlock), 0, c->stream, A);
         }));

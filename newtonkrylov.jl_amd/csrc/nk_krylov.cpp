@@ -39,6 +39,7 @@ struct nk_workspace {
     double* hdev = nullptr;  // device Hessenberg columns: 2 slots of (2*cap + 2) doubles (steps k, k+1 in flight)
     double* ydev = nullptr;  // device y (cap doubles)
     double* bdev = nullptr;  // device beta of the current cycle (V_1 = r0 / beta is fused into step 1)
+    bool u_fused = false;    // the last solve applied opts.u_update inside its final x update
     double* hpin = nullptr;  // pinned host mirror of hdev (2 slots), written by the kernels themselves
     double* hpin_dev = nullptr;  // hpin's device address
     double* ypin = nullptr;  // pinned host y
@@ -343,11 +344,17 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         iter += inner_iter;
         inner_itmax = itmax - iter;
         tired = iter >= itmax;
-        const bool need_xnorm = restart && A.mode == NK_JV_FD && !(solved || tired || breakdown);
+        const bool final_cycle = solved || tired || breakdown;
+        const bool need_xnorm = restart && A.mode == NK_JV_FD && !final_cycle;
+        double* uu = final_cycle ? o->u_update : nullptr;  // fused Newton update u .-= x
         Red xr{};
         NK_TRY(launch_update_x(c, n, x, ws->xr, ws->V.data(), kk, ws->ydev, restart && npass > 1,
-                               need_xnorm ? &xr : nullptr));
-        if (need_xnorm) NK_TRY(host_scalar(c, xr, 1, &xnorm));
+                               (need_xnorm || uu) ? &xr : nullptr, uu));
+        if (uu) {
+            NK_TRY(host_scalar(c, xr, 1, &st->u_norm));
+            ws->u_fused = true;
+        }
+        else if (need_xnorm) NK_TRY(host_scalar(c, xr, 1, &xnorm));
         else {
             NK_HIP(c, hipStreamSynchronize(c->stream));  // ypin may be rewritten next cycle
         }
@@ -518,9 +525,15 @@ int nk_krylov_solve(nk_workspace* ws, const nk_problem* p, const double* u, cons
             NK_TRY(host_scalar(c, ru, 1, &A.unorm));
         }
     }
+    ws->u_fused = false;
     int rc = (ws->algo == NK_ALGO_CG) ? cg(ws, A, b, o, st, hist, hist_cap, hist_len)
                                       : gmres(ws, p, A, b, o, st, hist, hist_cap, hist_len);
     st->n_matvec = A.n_matvec;
+    if (rc == NK_OK && o->u_update && !ws->u_fused) {  // not fused (CG, early exits): u .-= x, ||u||
+        Red ru{};
+        NK_TRY(launch_axpy_sumsq(c, ws->n, -1.0, ws->x, o->u_update, &ru));
+        NK_TRY(host_scalar(c, ru, 1, &st->u_norm));
+    }
     return rc;
 }
 

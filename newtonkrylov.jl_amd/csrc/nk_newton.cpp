@@ -73,11 +73,12 @@ int nk_newton_krylov(nk_ctx* c, const nk_problem* p, double* u, double* res, con
         if (!o->rtol_user && o->forcing != NK_FORCING_NONE) ko.rtol = eta;
         ko.b_norm = n_res;  // b = F(u): its norm is the n_res just computed
         ko.u_norm = u_norm;
+        ko.u_update = u;    // u .-= d fused into the solve's last pass (d = workspace.x is not stored)
         nk_krylov_stats ks{};
         const double* F0 = ko.jv_mode == NK_JV_FD ? res : nullptr;
         if ((rc = nk_krylov_solve(ws, p, u, F0, res, &ko, &ks, nullptr, 0, nullptr)) != NK_OK) break;
         st->n_matvec += ks.n_matvec;
-        if ((rc = nk_axpy_norm(c, g.n, -1.0, nk_workspace_x(ws), u, &u_norm)) != NK_OK) break;  // u .-= 1 .* d
+        u_norm = ks.u_norm;  // ||u|| after u .-= 1 .* d (:344)
         const double n_prior = n_res;
         if ((rc = nk_residual_norm(c, p, res, u, &n_res)) != NK_OK) break;
         st->n_residual++;
