@@ -146,7 +146,7 @@ int finish_reduction(nk_ctx* c, Red* r);     // multi-rank: collapse + RCCL all-
 int mb_check(nk_ctx* c);                     // after a host sync: did a mailbox wait time out?
 int red_blocks(int64_t n);                   // grid size of streaming reductions
 constexpr int kMbSlots = 256;                // mailbox ring (epoch % kMbSlots)
-constexpr int kMbRanks = 64;                 // max ranks of the mailbox all-reduce
+constexpr int kMbRanks = 32;                 // max ranks of the mailbox all-reduce (2 granules each: one wave polls them all)
 constexpr int kHaloBlocks = 64;              // blocks (= flags per side) of the IPC ghost-plane exchange
 // one fine-grained region per rank, IPC-mapped by every other rank:
 //   [mailbox: kMbSlots x kMbRanks x 2 u64][halo flags: 2 parity x 2 sides x kHaloBlocks u64]
