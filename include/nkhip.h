@@ -52,6 +52,21 @@ extern "C" {
 
 #define NK_ALGO_GMRES 0    /* krylov_workspace(:gmres, …), src/Ariadne.jl:317-318 */
 #define NK_ALGO_CG 1       /* krylov_workspace(:cg, …)    (examples/bratu.jl:59-63) */
+#define NK_ALGO_FGMRES 2   /* krylov_workspace(:fgmres, …) (examples/bratu.jl:131-157): flexible right-preconditioned GMRES */
+
+/* Right preconditioner N (Krylov.jl's `N`, ldiv = false: z = N v approximates A^{-1} v).  With
+ * NK_ALGO_GMRES and a preconditioner the solve runs in the flexible form (Z_k = N V_k stored,
+ * x = x0 + Z y) -- the same iterates in exact arithmetic as x = x0 + N (V y). */
+#define NK_PRECOND_NONE 0
+#define NK_PRECOND_DIAG 1  /* z = diag .* v  (e.g. Jacobi: diag = 1 ./ diag(J), nk_jacobian_diag) */
+#define NK_PRECOND_USER 2  /* z = apply(data, ctx, z, v), enqueued on nk_ctx_stream(ctx)          */
+typedef int (*nk_user_precond)(void* data, struct nk_ctx* ctx, double* out, const double* in);
+typedef struct nk_precond {
+    int32_t kind;          /* NK_PRECOND_*                                   */
+    const double* diag;    /* NK_PRECOND_DIAG: device grid function          */
+    nk_user_precond apply; /* NK_PRECOND_USER                                */
+    void* data;
+} nk_precond;
 
 typedef struct nk_ctx nk_ctx;
 typedef struct nk_workspace nk_workspace;
@@ -112,6 +127,10 @@ int nk_residual_norm(nk_ctx* ctx, const nk_problem* p, double* res, const double
 int nk_jv(nk_ctx* ctx, const nk_problem* p, double* out, const double* u, const double* v,
           const double* F0, int32_t mode, double eps);
 
+/* diag(J(u)) of a built-in residual, bit-identical to the diagonal of collect(J) (the tangent
+ * kernel's arithmetic on a unit vector); reciprocal = 1 gives 1 ./ diag(J), the Jacobi preconditioner. */
+int nk_jacobian_diag(nk_ctx* ctx, const nk_problem* p, double* out, const double* u, int32_t reciprocal);
+
 /* mul!(out, transpose(J), v) (src/Ariadne.jl:87-107, Enzyme reverse mode): out = J(u)^T v.  The
  * built-in residuals have symmetric Jacobians (3/5/7-point Laplacian plus a diagonal), so this is
  * the exact tangent kernel; user problems need user->JT. */
@@ -148,6 +167,7 @@ typedef struct nk_krylov_opts {
     double u_norm;                /* > 0: ||u|| is known (FD step size): not recomputed                          */
     double* u_update;             /* non-null: the Newton update u .-= x is fused into the solve's last pass;
                                      x is then NOT stored and stats.u_norm = ||u|| afterwards                */
+    const nk_precond* N;          /* right preconditioner (null: none)                                      */
 } nk_krylov_opts;
 
 typedef struct nk_krylov_stats {

@@ -19,7 +19,8 @@ NK_BRATU1D, NK_BRATU2D, NK_HEAT2D_EULER, NK_HEAT3D_EULER = 1, 2, 3, 4
 NK_USER1D, NK_USER2D, NK_USER3D = 16, 17, 18
 NK_BC_ZERO = 0
 NK_JV_EXACT, NK_JV_FD = 0, 1
-NK_ALGO_GMRES, NK_ALGO_CG = 0, 1
+NK_ALGO_GMRES, NK_ALGO_CG, NK_ALGO_FGMRES = 0, 1, 2
+NK_PRECOND_NONE, NK_PRECOND_DIAG, NK_PRECOND_USER = 0, 1, 2
 
 _ERRORS = {-1: "HIP error", -2: "invalid argument", -3: "out of device memory", -4: "RCCL error", -5: "bad state", -6: "user callback failed"}
 
@@ -41,6 +42,13 @@ NK_USER_RESIDUAL = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_
 NK_USER_TANGENT = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p)
 
 
+NK_USER_PRECOND = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p)
+
+
+class nk_precond(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("diag", C.c_void_p), ("apply", NK_USER_PRECOND), ("data", C.c_void_p)]
+
+
 class nk_user_ops(C.Structure):
     _fields_ = [("F", NK_USER_RESIDUAL), ("J", NK_USER_TANGENT), ("JT", NK_USER_TANGENT), ("data", C.c_void_p)]
 
@@ -48,7 +56,7 @@ class nk_user_ops(C.Structure):
 class nk_krylov_opts(C.Structure):
     _fields_ = [("restart", C.c_int32), ("reorthogonalization", C.c_int32), ("itmax", C.c_int32),
                 ("jv_mode", C.c_int32), ("atol", C.c_double), ("rtol", C.c_double), ("b_norm", C.c_double),
-                ("u_norm", C.c_double), ("u_update", C.c_void_p)]
+                ("u_norm", C.c_double), ("u_update", C.c_void_p), ("N", C.c_void_p)]
 
 
 class nk_krylov_stats(C.Structure):
@@ -93,6 +101,7 @@ SIGNATURES = {
     "nk_residual_norm": (C.c_int, [_VP, _PP, _VP, _VP, _PD]),
     "nk_jv": (C.c_int, [_VP, _PP, _VP, _VP, _VP, _VP, _I32, _D]),
     "nk_jtv": (C.c_int, [_VP, _PP, _VP, _VP, _VP]),
+    "nk_jacobian_diag": (C.c_int, [_VP, _PP, _VP, _VP, _I32]),
     "nk_dot": (C.c_int, [_VP, _I64, _VP, _VP, _PD]),
     "nk_norm": (C.c_int, [_VP, _I64, _VP, _PD]),
     "nk_scal": (C.c_int, [_VP, _I64, _D, _VP]),

@@ -107,7 +107,7 @@ class KrylovStats:
 
 _STATUS = {0: "unknown", 1: "solution good enough given atol and rtol", 2: "maximum number of iterations exceeded",
            3: "breakdown", 4: "zero curvature detected"}
-_ALGOS = {"gmres": _lib.NK_ALGO_GMRES, "cg": _lib.NK_ALGO_CG}
+_ALGOS = {"gmres": _lib.NK_ALGO_GMRES, "cg": _lib.NK_ALGO_CG, "fgmres": _lib.NK_ALGO_FGMRES}
 
 
 class KrylovWorkspace:
@@ -115,7 +115,7 @@ class KrylovWorkspace:
 
     def __init__(self, algo: str, kc: KrylovConstructor):
         if algo not in _ALGOS:
-            raise NotImplementedError(f"algo = :{algo} -- the HIP path implements :gmres and :cg "
+            raise NotImplementedError(f"algo = :{algo} -- the HIP path implements :gmres, :fgmres and :cg "
                                       "(other Krylov methods are out of scope, SURVEY.md §2 C16)")
         self.algo = algo
         self.memory = int(kc.memory)
@@ -154,14 +154,19 @@ def krylov_solve_(ws: KrylovWorkspace, J, b: DeviceArray, *, restart=False, reor
     u .-= x is fused into the last pass; ws.x is then not stored and ws.stats.u_norm = ||u||.)"""
     if unknown:
         raise TypeError(f"unsupported Krylov keyword(s): {sorted(unknown)}")
-    if M is not None or N is not None:
-        raise NotImplementedError("preconditioners M/N are out of scope for the HIP path (SURVEY.md §2 C15)")
+    if M is not None:
+        raise NotImplementedError("left preconditioner M: the HIP path implements right preconditioning (N) only")
+    if ldiv:
+        raise NotImplementedError("ldiv = true: give N as the operator that approximates J^{-1} (ldiv = false)")
+    if N is not None and not hasattr(N, "as_c"):
+        raise TypeError("N must be an ariadne_hip preconditioner (DiagonalPreconditioner, UserPreconditioner, jacobi(J))")
     if ws.algo == "cg" and (restart or reorthogonalization):
         raise TypeError("restart / reorthogonalization are GMRES keywords")
     prob = J.problem()
     opts = _lib.nk_krylov_opts(int(bool(restart)), int(bool(reorthogonalization)), int(itmax), J.jv_mode,
                                float(atol), float(rtol), float(_b_norm), float(_u_norm),
-                               _u_update.ptr if _u_update is not None else None)
+                               _u_update.ptr if _u_update is not None else None,
+                               C.cast(C.pointer(N.as_c()), C.c_void_p) if N is not None else None)
     st = _lib.nk_krylov_stats()
     cap = ((int(itmax) or 4096) + 64) if history else 0
     hist = (C.c_double * max(cap, 1))()

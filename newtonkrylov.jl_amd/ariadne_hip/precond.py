@@ -1,0 +1,76 @@
+"""Right preconditioners for the device GMRES / FGMRES (Krylov.jl's `N`, ldiv = false: z = N v
+approximates J^{-1} v).  SURVEY.md §8f rank 3: a device Jacobi preconditioner built from the
+Jacobian's diagonal; any other preconditioner can be supplied as device code (UserPreconditioner).
+
+`newton_krylov_(…, N=factory)`: a factory is called as `factory(J)` once per Newton step (the
+JacobianOperator of that step) and returns one of these (e.g. `N=jacobi`).
+"""
+from __future__ import annotations
+
+import sys
+
+from . import _lib
+from ._lib import load
+from .device import DeviceArray
+
+
+class Preconditioner:
+    """Base: `as_c()` returns the nk_precond descriptor (kept alive by the object)."""
+
+    def as_c(self) -> _lib.nk_precond:
+        raise NotImplementedError
+
+
+class DiagonalPreconditioner(Preconditioner):
+    """z = d .* v with a device grid function d (NK_PRECOND_DIAG)."""
+
+    def __init__(self, d: DeviceArray):
+        self.d = d
+        self._c = _lib.nk_precond(_lib.NK_PRECOND_DIAG, d.ptr, _lib.NK_USER_PRECOND(), None)
+
+    def as_c(self):
+        return self._c
+
+
+class UserPreconditioner(Preconditioner):
+    """z = N v computed by `apply(z, v)` on DeviceArray views, on the library's stream (runs inside
+    ctx.torch_stream() when torch is loaded, like a UserResidual)."""
+
+    def __init__(self, apply, grid, ctx):
+        self.apply, self.grid, self.ctx = apply, grid, ctx
+
+        def run(_d, _c, out, inp):
+            try:
+                o, i = DeviceArray(grid, ctx, _ptr=out), DeviceArray(grid, ctx, _ptr=inp)
+                if "torch" in sys.modules:
+                    with ctx.torch_stream():
+                        apply(o, i)
+                else:
+                    apply(o, i)
+                return 0
+            except BaseException as e:
+                _lib.set_user_error(e)
+                return 1
+
+        self._cb = _lib.NK_USER_PRECOND(run)
+        self._c = _lib.nk_precond(_lib.NK_PRECOND_USER, None, self._cb, None)
+
+    def as_c(self):
+        return self._c
+
+
+def jacobian_diag(J, reciprocal: bool = False) -> DeviceArray:
+    """diag(J(u)) of a built-in residual on the device (bit-identical to the diagonal of collect(J))."""
+    import ctypes as C
+
+    out = J.u.zero()
+    prob = J.problem()
+    J.u.ctx.check(load().nk_jacobian_diag(J.u.ctx.handle, C.byref(prob), out.ptr, J.u.ptr, int(bool(reciprocal))),
+                  "nk_jacobian_diag")
+    return out
+
+
+def jacobi(J) -> DiagonalPreconditioner:
+    """Jacobi preconditioner N = diag(J(u))^{-1} (the reference's examples build theirs from
+    collect(J), bratu.jl:121-137); use as `N=jacobi` in newton_krylov_ (called per Newton step)."""
+    return DiagonalPreconditioner(jacobian_diag(J, reciprocal=True))

@@ -305,6 +305,14 @@ int nk_jv(nk_ctx* c, const nk_problem* p, double* out, const double* u, const do
     return launch_stencil(c, in, &r);
 }
 
+int nk_jacobian_diag(nk_ctx* c, const nk_problem* p, double* out, const double* u, int32_t reciprocal) {
+    if (!c || !out || !u) return NK_E_ARG;
+    Geo g;
+    NK_TRY(geometry(c, p, &g));
+    if (nk_is_user(p->kind)) return fail(c, NK_E_ARG, "diag(J) of a user residual: probe it with collect(J)");
+    return launch_jdiag(c, p, out, u, reciprocal);
+}
+
 int nk_jtv(nk_ctx* c, const nk_problem* p, double* out, const double* u, const double* v) {
     if (!c || !out || !u || !v) return NK_E_ARG;
     Geo g;

@@ -16,6 +16,7 @@
 //    to the CPU oracle; only exp (ocml vs glibc, <= 1 ulp) and reduction order differ.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 
 #include "nk_internal.hpp"
@@ -1032,6 +1033,35 @@ __global__ __launch_bounds__(kBlock) void k_user_epi(int64_t n, int fd, double* 
     if constexpr (EPI != EPI_NONE) publish(acc, part, fin, sh);
 }
 
+// ------------------------------------------------------------------------------ preconditioning
+// z = d .* v (diagonal right preconditioner) with the partials of ||z||^2 (the FD step size)
+__global__ __launch_bounds__(kBlock) void k_diag_apply(int64_t n, double* __restrict__ z, const double* __restrict__ d,
+                                                      const double* __restrict__ v, double* __restrict__ part, int fin) {
+    __shared__ double sh[8];
+    double acc = 0.0;
+    NK_CHUNKED(i, n) {
+        const double zi = d[i] * v[i];
+        z[i] = zi;
+        acc = fma(zi, zi, acc);
+    }
+    if (part) publish(acc, part, fin, sh);
+}
+
+// diag(J(u)): the exact tangent at point i applied to the unit vector e_i -- the centre value 1,
+// every neighbour 0 -- through the same lapk / point_value arithmetic as the stencil kernels
+template <int KIND, int DIM>
+__global__ __launch_bounds__(kBlock) void k_jdiag(KArgs A, double* __restrict__ out, int recip) {
+    const int64_t n = A.nx * A.ny * A.nz;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        double lsum = lapk(A, 1.0, 0.0, 0.0, A.hx2, A.ihx2);
+        if (DIM >= 2) lsum = lsum + lapk(A, 1.0, 0.0, 0.0, A.hy2, A.ihy2);
+        if (DIM == 3) lsum = lsum + lapk(A, 1.0, 0.0, 0.0, A.hz2, A.ihz2);
+        const double uc = (KIND == NK_BRATU1D || KIND == NK_BRATU2D) ? A.u[i] : 0.0;
+        const double d = point_value<KIND, MODE_JEXACT>(A, 1.0, lsum, uc, 0.0, 0.0);
+        out[i] = recip ? 1.0 / d : d;
+    }
+}
+
 // ------------------------------------------------------------------------------ stencil dispatch
 template <int KIND, int MODE, int EPI>
 void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s) {
@@ -1445,6 +1475,33 @@ int launch_user_epi(nk_ctx* c, int64_t n, int fd, double* out, const double* F0,
         case EPI_SUMSQ: hipLaunchKernelGGL(k_user_epi<EPI_SUMSQ>, dim3(g), dim3(kBlock), 0, c->stream, n, fd, out, F0, eps, aux, part, fin); break;
         case EPI_DOT: hipLaunchKernelGGL(k_user_epi<EPI_DOT>, dim3(g), dim3(kBlock), 0, c->stream, n, fd, out, F0, eps, aux, part, fin); break;
         default: hipLaunchKernelGGL(k_user_epi<EPI_RESID>, dim3(g), dim3(kBlock), 0, c->stream, n, fd, out, F0, eps, aux, part, fin); break;
+        }
+    });
+}
+
+int launch_diag_apply(nk_ctx* c, int64_t n, double* z, const double* d, const double* v, Red* red) {
+    const int g = red_blocks(n);
+    int fin = 0;
+    double* part = red ? red_out(c, g, red, &fin) : nullptr;
+    return launch(c, "precond_diag", 24.0 * n, [&] {
+        hipLaunchKernelGGL(k_diag_apply, dim3(g), dim3(kBlock), 0, c->stream, n, z, d, v, part, fin);
+    });
+}
+
+int launch_jdiag(nk_ctx* c, const nk_problem* p, double* out, const double* u, int recip) {
+    KArgs A{};
+    A.u = u;
+    A.nx = p->nx; A.ny = p->ny; A.nz = p->nz;
+    A.hx2 = p->hx * p->hx; A.hy2 = p->hy * p->hy; A.hz2 = p->hz * p->hz;
+    A.lam = p->lambda; A.a = p->a; A.dt = p->dt;
+    const int64_t n = p->nx * p->ny * p->nz;
+    const int g = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, 4096);
+    return launch(c, "jacobian_diag", 16.0 * n, [&] {
+        switch (p->kind) {
+        case NK_BRATU1D: hipLaunchKernelGGL((k_jdiag<NK_BRATU1D, 1>), dim3(g), dim3(kBlock), 0, c->stream, A, out, recip); break;
+        case NK_BRATU2D: hipLaunchKernelGGL((k_jdiag<NK_BRATU2D, 2>), dim3(g), dim3(kBlock), 0, c->stream, A, out, recip); break;
+        case NK_HEAT2D_EULER: hipLaunchKernelGGL((k_jdiag<NK_HEAT2D_EULER, 2>), dim3(g), dim3(kBlock), 0, c->stream, A, out, recip); break;
+        default: hipLaunchKernelGGL((k_jdiag<NK_HEAT3D_EULER, 3>), dim3(g), dim3(kBlock), 0, c->stream, A, out, recip); break;
         }
     });
 }

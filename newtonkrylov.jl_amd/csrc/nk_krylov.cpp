@@ -36,6 +36,7 @@ struct nk_workspace {
     double* xr = nullptr;  // gmres restart: Δx (chunked x update);  cg: r
     double* p = nullptr;   // cg: search direction
     std::vector<double*> V;
+    std::vector<double*> Z;  // flexible form: Z_k = N V_k (right preconditioner)
     double* hdev = nullptr;  // device Hessenberg columns: 2 slots of (2*cap + 2) doubles (steps k, k+1 in flight)
     double* ydev = nullptr;  // device y (cap doubles)
     double* bdev = nullptr;  // device beta of the current cycle (V_1 = r0 / beta is fused into step 1)
@@ -94,6 +95,16 @@ int ws_basis(nk_workspace* ws, int need) {
     return NK_OK;
 }
 
+int ws_zbasis(nk_workspace* ws, int need) {
+    while ((int)ws->Z.size() < need) {
+        double* v = nullptr;
+        NK_TRY(nk_vec_alloc(ws->c, &ws->prob, &v));
+        ws->Z.push_back(v);
+    }
+    return NK_OK;
+}
+
+
 inline double sgn(double x) { return (double)((x > 0) - (x < 0)); }
 
 // NK_MGS_ALT=1: alternate the sweep direction of consecutive MGS passes (see k_mgs_pass)
@@ -134,6 +145,27 @@ int host_scalar(nk_ctx* c, Red r, int sqrt_it, double* out) {
     if (c->prof) prof_drain(c, false);
     NK_TRY(mb_check(c));
     *out = c->hpin[0];
+    return NK_OK;
+}
+
+// z = N v (right preconditioner); *znorm = ||z|| when the FD operator needs it
+int apply_precond(nk_ctx* c, const nk_problem* p, const nk_precond* N, int64_t n, double* z, const double* v,
+                  bool need_norm, double* znorm) {
+    Red rz{};
+    if (N->kind == NK_PRECOND_DIAG) {
+        if (!N->diag) return fail(c, NK_E_ARG, "diagonal preconditioner without its diagonal");
+        NK_TRY(launch_diag_apply(c, n, z, N->diag, v, need_norm ? &rz : nullptr));
+    } else if (N->kind == NK_PRECOND_USER) {
+        if (!N->apply) return fail(c, NK_E_ARG, "user preconditioner without its apply callback");
+        NK_TRY(halo_exchange(c, p, v));
+        int rc = 0;
+        NK_TRY(launch(c, "precond_user", 0.0, [&] { rc = N->apply(N->data, c, z, v); }));
+        if (rc != 0) return fail(c, NK_E_USER, "user preconditioner callback returned " + std::to_string(rc));
+        if (need_norm) NK_TRY(launch_sumsq(c, n, z, &rz));
+    } else {
+        return fail(c, NK_E_ARG, "unknown preconditioner kind");
+    }
+    if (need_norm) NK_TRY(host_scalar(c, rz, 1, znorm));
     return NK_OK;
 }
 
@@ -226,6 +258,10 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
     auto slot_pin_dev = [&](int k) { return ws->hpin_dev + (size_t)(k & 1) * (2 * ws->cap + 2); };
     auto npasses_of = [&](int k) { return reorth ? 2 * k : k; };
     const double* v1_src = b;  // r0 of the current cycle; step 1 applies J to r0 / beta and stores V_1
+    // right preconditioner: the flexible form (Z_k = N V_k stored, x += Z y), without the
+    // one-step-ahead issue (the FD step size needs ||Z_k|| on the host)
+    const nk_precond* N = (o->N && o->N->kind != NK_PRECOND_NONE) ? o->N : nullptr;
+    const bool spec = N == nullptr;
     auto issue = [&](int k) -> int {
         NK_TRY(ws_basis(ws, k));
         NK_TRY(ws_scalars(ws, k + 1));
@@ -234,11 +270,18 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         double* colh = slot_pin_dev(k);  // the kernels mirror every entry into pinned host memory
         double* q = W[k & 1];
         Red red{};
-        if (k == 1) {  // fused kdivcopy!(V_1, r0, beta) + mul! + <V_1, Jv> (the dot partner is V_1 itself)
+        const double* hprev = k > 1 ? slot_dev(k - 1) + npasses_of(k - 1) : ws->bdev;
+        const double* qprev = k > 1 ? W[(k - 1) & 1] : v1_src;
+        if (N) {  // V_k = q_{k-1} / h (r0 / beta), Z_k = N V_k, q = J Z_k, <V_1, q>
+            NK_TRY(launch_fd_point(c, n, nullptr, nullptr, qprev, hprev, 0.0, ws->V[k - 1]));
+            NK_TRY(ws_zbasis(ws, k));
+            double znorm = 1.0;
+            NK_TRY(apply_precond(c, p, N, n, ws->Z[k - 1], ws->V[k - 1], A.mode == NK_JV_FD, &znorm));
+            NK_TRY(A.apply(q, ws->Z[k - 1], znorm, EPI_DOT, ws->V[0], &red));
+        } else if (k == 1) {  // fused kdivcopy!(V_1, r0, beta) + mul! + <V_1, Jv> (the dot partner is V_1 itself)
             NK_TRY(A.apply(q, v1_src, 1.0, EPI_DOT, nullptr, &red, ws->bdev, ws->V[0]));
         } else {
-            const double* hprev = slot_dev(k - 1) + npasses_of(k - 1);
-            NK_TRY(A.apply(q, W[(k - 1) & 1], 1.0, EPI_DOT, ws->V[0], &red, hprev, ws->V[k - 1]));
+            NK_TRY(A.apply(q, qprev, 1.0, EPI_DOT, ws->V[0], &red, hprev, ws->V[k - 1]));
         }
         for (int t = 0; t < np; ++t) {
             const double* vi = ws->V[t % k];
@@ -295,7 +338,8 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
             // speculate: step k+1 unless the cycle certainly ends at k (its kernels only write
             // V_{k+1}, q_{k+1} and slot (k+1)&1, none of which is read if the cycle stops here)
             const bool last = restart ? (inner_iter >= std::min<int64_t>(mem, inner_itmax)) : (inner_iter >= inner_itmax);
-            if (!last) NK_TRY(issue(k + 1));
+            if (!spec && k > 1) NK_TRY(issue(k));  // preconditioned: step k is issued when it is needed
+            if (spec && !last) NK_TRY(issue(k + 1));
             NK_HIP(c, hipEventSynchronize(ws->col_ready[k & 1]));
             NK_TRY(mb_check(c));
             if (c->prof) prof_drain(c, false);
@@ -321,7 +365,7 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
             breakdown = Hbis <= btol;
             inner_tired = last;
             if (!(solved || inner_tired || breakdown)) z[k] = zeta;  // V_{k+1} = q/h was stored by step k+1
-            else if (!last) A.n_matvec -= 1;  // the speculative step k+1 is discarded: not a mul!(J) of the solve
+            else if (spec && !last) A.n_matvec -= 1;  // the speculative step k+1 is discarded: not a mul!(J) of the solve
         }
         // back substitution R y = z (Krylov.jl, y stored in z)
         const int kk = (int)inner_iter;
@@ -348,7 +392,7 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         const bool need_xnorm = restart && A.mode == NK_JV_FD && !final_cycle;
         double* uu = final_cycle ? o->u_update : nullptr;  // fused Newton update u .-= x
         Red xr{};
-        NK_TRY(launch_update_x(c, n, x, ws->xr, ws->V.data(), kk, ws->ydev, restart && npass > 1,
+        NK_TRY(launch_update_x(c, n, x, ws->xr, N ? ws->Z.data() : ws->V.data(), kk, ws->ydev, restart && npass > 1,
                                (need_xnorm || uu) ? &xr : nullptr, uu));
         if (uu) {
             NK_TRY(host_scalar(c, xr, 1, &st->u_norm));
@@ -451,7 +495,8 @@ extern "C" {
 
 int nk_workspace_create(nk_ctx* c, int32_t algo, const nk_problem* p, int32_t memory, nk_workspace** out) {
     if (!c || !p || !out) return NK_E_ARG;
-    if (algo != NK_ALGO_GMRES && algo != NK_ALGO_CG) return fail(c, NK_E_ARG, "unsupported Krylov algorithm");
+    if (algo != NK_ALGO_GMRES && algo != NK_ALGO_CG && algo != NK_ALGO_FGMRES)
+        return fail(c, NK_E_ARG, "unsupported Krylov algorithm");
     Geo g;
     NK_TRY(geometry(c, p, &g));
     nk_workspace* ws = new nk_workspace();
@@ -464,7 +509,7 @@ int nk_workspace_create(nk_ctx* c, int32_t algo, const nk_problem* p, int32_t me
     int rc = NK_OK;
     if ((rc = nk_vec_alloc(c, &ws->prob, &ws->x)) != NK_OK || (rc = nk_vec_alloc(c, &ws->prob, &ws->w)) != NK_OK ||
         (rc = nk_vec_alloc(c, &ws->prob, &ws->xr)) != NK_OK ||
-        (algo == NK_ALGO_GMRES && (rc = nk_vec_alloc(c, &ws->prob, &ws->w2)) != NK_OK) ||
+        (algo != NK_ALGO_CG && (rc = nk_vec_alloc(c, &ws->prob, &ws->w2)) != NK_OK) ||
         hipMalloc(&ws->bdev, 2 * sizeof(double)) != hipSuccess ||
         hipEventCreateWithFlags(&ws->col_ready[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ws->col_ready[1], hipEventDisableTiming) != hipSuccess) {
@@ -491,6 +536,7 @@ int nk_workspace_destroy(nk_workspace* ws) {
     if (!ws) return NK_OK;
     nk_ctx* c = ws->c;
     for (double* v : ws->V) nk_vec_free(c, v);
+    for (double* v : ws->Z) nk_vec_free(c, v);
     for (double* v : {ws->x, ws->w, ws->w2, ws->xr, ws->p})
         if (v) nk_vec_free(c, v);
     for (hipEvent_t e : ws->col_ready)
@@ -526,6 +572,8 @@ int nk_krylov_solve(nk_workspace* ws, const nk_problem* p, const double* u, cons
         }
     }
     ws->u_fused = false;
+    if (ws->algo == NK_ALGO_CG && o->N && o->N->kind != NK_PRECOND_NONE)
+        return fail(c, NK_E_ARG, "the device CG takes no right preconditioner (use GMRES / FGMRES)");
     int rc = (ws->algo == NK_ALGO_CG) ? cg(ws, A, b, o, st, hist, hist_cap, hist_len)
                                       : gmres(ws, p, A, b, o, st, hist, hist_cap, hist_len);
     st->n_matvec = A.n_matvec;

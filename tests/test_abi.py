@@ -53,7 +53,7 @@ def test_struct_layouts_match_c(tmp_path):
     structs = {"nk_problem": _lib.nk_problem, "nk_krylov_opts": _lib.nk_krylov_opts,
                "nk_krylov_stats": _lib.nk_krylov_stats, "nk_prof_entry": _lib.nk_prof_entry,
                "nk_user_ops": _lib.nk_user_ops, "nk_newton_opts": _lib.nk_newton_opts,
-               "nk_newton_stats": _lib.nk_newton_stats}
+               "nk_newton_stats": _lib.nk_newton_stats, "nk_precond": _lib.nk_precond}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
     for sname, cls in structs.items():
         lines.append(f'printf("{sname} %zu\\n", sizeof({sname}));')
