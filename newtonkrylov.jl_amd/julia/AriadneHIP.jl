@@ -229,6 +229,7 @@ struct NkKrylovOpts
     b_norm::Float64   # 0: computed by the solve (Krylov.jl semantics)
     u_norm::Float64   # 0: computed by the solve
     u_update::Ptr{Float64}  # C_NULL: workspace.x holds the step (Ariadne applies u .-= d itself)
+    N::Ptr{Cvoid}           # nk_precond* right preconditioner, C_NULL: none
 end
 struct NkKrylovStats
     niter::Int64
@@ -257,7 +258,7 @@ end
 function Krylov.krylov_solve!(ws::HipKrylovWorkspace, J::Ariadne.JacobianOperator{<:AnyHipResidual, <:HipVector}, b::HipVector;
                               restart::Bool = false, reorthogonalization::Bool = false, itmax::Integer = 0,
                               atol::Real = sqrt(eps(Float64)), rtol::Real = sqrt(eps(Float64)), kwargs...)
-    opts = NkKrylovOpts(restart, reorthogonalization, itmax, J.f.jv, atol, rtol, 0.0, 0.0, C_NULL)
+    opts = NkKrylovOpts(restart, reorthogonalization, itmax, J.f.jv, atol, rtol, 0.0, 0.0, C_NULL, C_NULL)
     st = Ref{NkKrylovStats}()
     hl = Ref{Int64}(0)
     F0 = J.f.jv == NK_JV_FD ? J.res.ptr : Ptr{Float64}(C_NULL)
