@@ -18,6 +18,8 @@ ap.add_argument("--n", type=int, default=4096 * 4096)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--what", default="mgs,stencil")
+ap.add_argument("--rows", default="8,16,32", help="stencil rows per tile")
+ap.add_argument("--fast", default="0,2,4,6", help="stencil variant bits (launch_stencil_ex): 1 reciprocals, 4 VEC=4")
 args = ap.parse_args()
 
 ctx = ah.Context(0)
@@ -34,9 +36,11 @@ MGS = {0: "U2", 1: "U2+nt(V_i)", 2: "U4+nt(V_i)", 3: "U2+nt(V_i,V_i+1)", 4: "U4+
 configs = [("copy", None, None, None)]
 if "mgs" in args.what:
     configs += [("mgs", v, 0, k) for k in (8, 16, 30) for v in MGS]
+ROWS = [int(x) for x in args.rows.split(",")]
+FASTS = [int(x) for x in args.fast.split(",")]
 ST = {(2, 2): ("jv_fd_dot", 40.0), (1, 2): ("jv_exact_dot", 32.0), (0, 1): ("residual_norm", 16.0)}
 if "stencil" in args.what:
-    configs += [("st", mode_epi, rows, fast) for mode_epi in ST for rows in (8, 16, 32) for fast in (0, 2, 4, 6)]
+    configs += [("st", mode_epi, rows, fast) for mode_epi in ST for rows in ROWS for fast in FASTS]
 res = {c: [] for c in configs}
 for _ in range(args.rounds):
     for cfg in configs:
