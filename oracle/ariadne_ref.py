@@ -56,6 +56,8 @@ class Dual:
 
     def __truediv__(self, o):
         o = Dual.lift(o)
+        if o.d == 0.0:  # Enzyme's forward FDiv: dx/c + (-(x dc)/c²) with dc = 0 is dx/c exactly
+            return Dual(self.v / o.v, self.d / o.v)
         return Dual(self.v / o.v, (self.d * o.v - self.v * o.d) / (o.v * o.v))
 
     def __rtruediv__(self, o):
@@ -348,3 +350,92 @@ def newton_krylov(F, u0, p=None, **kw):
     def F_(res, u, p):
         res[:] = F(u, p)
     return newton_krylov_(F_, u0, p, **kw)
+
+
+# ----------------------------------------------------------------------------- heat examples on halo arrays
+# A literal restatement of examples/heat_2D.jl (bc_periodic!, bc_zero!, diffusion!) and
+# examples/implicit.jl (G_Euler!, G_Midpoint!, G_Trapezoid!) on (N+2) x (M+2) halo arrays indexed
+# [i, j] like the reference's OffsetArray (i = x, the column-major fast index; 0 and N+1 are ghosts).
+# Arrays may hold Dual numbers: evaluating G! on u = Dual(u, v) gives F(u) and the forward-mode
+# tangent J(u) v, independently of the C oracle's hand-derived tangents.
+def bc_periodic_h(u):
+    """heat_2D.jl:15-26 (note: N is reused for the second dimension -- square grids)."""
+    N, M = u.shape
+    N, M = N - 2, M - 2
+    u[0, :] = u[N, :]
+    u[N + 1, :] = u[1, :]
+    u[:, 0] = u[:, N]
+    u[:, N + 1] = u[:, 1]
+
+
+def bc_zero_h(u):
+    """heat_2D.jl:28-38."""
+    N, M = u.shape
+    N, M = N - 2, M - 2
+    u[0, :] = 0.0
+    u[N + 1, :] = 0.0
+    u[:, 0] = 0.0
+    u[:, N + 1] = 0.0
+
+
+def diffusion_h(du, u, p, _t):
+    """heat_2D.jl:45-62: bc!(u), then the 5-point Laplacian, i outer / j inner."""
+    a, dx, dy, bc = p
+    N, M = u.shape
+    N, M = N - 2, M - 2
+    bc(u)
+    for i in range(1, N + 1):
+        for j in range(1, M + 1):
+            du[i, j] = a * ((u[i + 1, j] - 2 * u[i, j] + u[i - 1, j]) / (dx * dx)
+                            + (u[i, j + 1] - 2 * u[i, j] + u[i, j - 1]) / (dy * dy))
+
+
+def _interior(x):
+    return x[1:-1, 1:-1]
+
+
+def G_Euler_h(res, un, dt, f, du, u, p, t):
+    """implicit.jl:8-13."""
+    f(du, u, p, t)
+    _interior(res)[...] = _interior(un) + dt * _interior(du) - _interior(u)
+
+
+def G_Midpoint_h(res, un, dt, f, du, u, p, t, alpha=0.5):
+    """implicit.jl:17-25: res is the temporary for α uₙ + (1 - α) u (interior broadcast)."""
+    uu = res
+    _interior(uu)[...] = alpha * _interior(un) + (1 - alpha) * _interior(u)
+    f(du, uu, p, t + alpha * dt)
+    _interior(res)[...] = _interior(un) + dt * _interior(du) - _interior(u)
+
+
+def G_Trapezoid_h(res, un, dt, f, du, u, p, t):
+    """implicit.jl:29-37: res is the temporary for du(uₙ)."""
+    dun = res
+    f(dun, un, p, t)
+    f(du, u, p, t + dt)
+    _interior(res)[...] = _interior(un) + (dt / 2) * (_interior(dun) + _interior(du)) - _interior(u)
+
+
+def heat_halo_jvp(G, un, u, v, a, dx, dy, dt, bc, **kw):
+    """(G(u), J(u) v) of G!(res, uₙ, Δt, diffusion!, du, u, (a, Δx, Δy, bc!), t) on interior arrays
+    shaped (M, N) (row-major, x fastest: the oracle layout); returns the same layout."""
+    M, N = u.shape
+    H = np.empty((N + 2, M + 2), dtype=object)
+    for idx in np.ndindex(H.shape):
+        H[idx] = Dual(0.0)
+    Un = H.copy()
+    for idx in np.ndindex(H.shape):
+        Un[idx] = Dual(0.0)
+    for j in range(M):
+        for i in range(N):
+            H[i + 1, j + 1] = Dual(u[j, i], v[j, i])
+            Un[i + 1, j + 1] = Dual(un[j, i], 0.0)
+    res = np.empty_like(H)
+    du = np.empty_like(H)
+    for idx in np.ndindex(H.shape):
+        res[idx] = Dual(0.0)
+        du[idx] = Dual(0.0)
+    G(res, Un, dt, diffusion_h, du, H, (a, dx, dy, bc), 0.0, **kw)
+    val = np.array([[Dual.lift(res[i + 1, j + 1]).v for i in range(N)] for j in range(M)])
+    tan = np.array([[Dual.lift(res[i + 1, j + 1]).d for i in range(N)] for j in range(M)])
+    return val, tan

@@ -15,9 +15,10 @@
  *     SURVEY.md Appendix A.  Iterates and iteration counts are therefore "parity unpinned"
  *     against the reference; tests pin this oracle with the reference's own known answers
  *     (test/runtests.jl) and with independent numpy/scipy goldens in tests/golden/.)
- *   - residuals: 1D Bratu examples/bratu.jl:14-24, 2D heat + G_Euler!
- *     examples/heat_2D.jl:28-62 + examples/implicit.jl:8-13, and their build-defined
- *     generalisations 2D Bratu and 3D heat.
+ *   - residuals: 1D Bratu examples/bratu.jl:14-24, 2D heat diffusion! with bc_zero! /
+ *     bc_periodic! (examples/heat_2D.jl:15-62) composed with G_Euler! / G_Midpoint! /
+ *     G_Trapezoid! (examples/implicit.jl:8-37), and their build-defined generalisations
+ *     2D Bratu and 3D heat.
  *
  * Layout: dense interior arrays, x fastest: idx = (k*ny + j)*nx + i (the same memory order as
  * the reference's column-major u[i,j]).  Zero-Dirichlet boundaries are applied by predication
@@ -36,19 +37,22 @@
 #include <float.h>
 #include <omp.h>
 
-enum { OC_BRATU1D = 1, OC_BRATU2D = 2, OC_HEAT2D_EULER = 3, OC_HEAT3D_EULER = 4 };
+enum { OC_BRATU1D = 1, OC_BRATU2D = 2, OC_HEAT2D_EULER = 3, OC_HEAT3D_EULER = 4,
+       OC_HEAT2D_MIDPOINT = 5, OC_HEAT3D_MIDPOINT = 6, OC_HEAT2D_TRAPEZOID = 7, OC_HEAT3D_TRAPEZOID = 8 };
+enum { OC_BC_ZERO = 0, OC_BC_PERIODIC = 1 };
 enum { OC_JV_EXACT = 0, OC_JV_FD = 1 };
 enum { OC_FORCING_NONE = 0, OC_FORCING_FIXED = 1, OC_FORCING_EW = 2 };
 enum { OC_ALGO_GMRES = 0, OC_ALGO_CG = 1 };
 
 typedef struct {
     int32_t kind;
-    int32_t bc;             /* 0 = zero Dirichlet */
+    int32_t bc;             /* OC_BC_ZERO (bc_zero!) or OC_BC_PERIODIC (bc_periodic!), heat kinds */
     int64_t nx, ny, nz;
     double hx, hy, hz;
     double lambda;          /* Bratu */
     double a, dt;           /* heat diffusivity and time step */
     const double* un;       /* heat: u_n (borrowed) */
+    double alpha;           /* G_Midpoint! α (implicit.jl:17, default 0.5) */
 } oc_problem;
 
 typedef struct {
@@ -140,10 +144,69 @@ void oc_ref(int64_t n, double* x, double* y, double c, double s) { /* Givens on 
 }
 
 /* ------------------------------------------------------------------ residuals */
-/* ((p - 2c) + m) / (h*h): Julia's (u[i+1] - 2u[i] + u[i-1]) / Δx^2 (bratu.jl:19, heat_2D.jl:65) */
+/* ((p - 2c) + m) / (h*h): Julia's (u[i+1] - 2u[i] + u[i-1]) / Δx^2 (bratu.jl:19, heat_2D.jl:57-59) */
 static inline double lap1(double c, double p, double m, double h) { return ((p - 2.0 * c) + m) / (h * h); }
 
 #define AT(arr, i, j, k) ((arr)[((int64_t)(k) * ny + (j)) * nx + (i)])
+
+static inline int oc_heat_dim(int kind) {
+    return (kind == OC_HEAT2D_EULER || kind == OC_HEAT2D_MIDPOINT || kind == OC_HEAT2D_TRAPEZOID) ? 2 : 3;
+}
+static inline int oc_scheme(int kind) {  /* 0 G_Euler!, 1 G_Midpoint!, 2 G_Trapezoid! (implicit.jl:8-37) */
+    if (kind == OC_HEAT2D_MIDPOINT || kind == OC_HEAT3D_MIDPOINT) return 1;
+    if (kind == OC_HEAT2D_TRAPEZOID || kind == OC_HEAT3D_TRAPEZOID) return 2;
+    return 0;
+}
+
+/* The 7 stencil positions (centre, +x, -x, +y, -y, +z, -z) of point (i,j,k): linear index, or -1 for
+ * a zero ghost cell.  bc_zero! (heat_2D.jl:28-38) makes every ghost 0; bc_periodic! (heat_2D.jl:15-26)
+ * copies the opposite interior edge into it, i.e. the neighbour index wraps around. */
+static inline void stencil_idx(const oc_problem* P, int64_t i, int64_t j, int64_t k, int64_t q[7]) {
+    const int64_t nx = P->nx, ny = P->ny, nz = P->nz;
+    const int per = P->bc == OC_BC_PERIODIC;
+    const int64_t ii[7] = {i, i + 1, i - 1, i, i, i, i};
+    const int64_t jj[7] = {j, j, j, j + 1, j - 1, j, j};
+    const int64_t kk[7] = {k, k, k, k, k, k + 1, k - 1};
+    for (int s = 0; s < 7; ++s) {
+        int64_t a = ii[s], b = jj[s], c = kk[s];
+        if (per) {
+            a = a < 0 ? a + nx : (a >= nx ? a - nx : a);
+            b = b < 0 ? b + ny : (b >= ny ? b - ny : b);
+            c = c < 0 ? c + nz : (c >= nz ? c - nz : c);
+        }
+        q[s] = (a < 0 || a >= nx || b < 0 || b >= ny || c < 0 || c >= nz) ? -1 : (c * ny + b) * nx + a;
+    }
+}
+
+/* diffusion!'s Laplacian sum at the centre of f[7] (heat_2D.jl:55-60; 3D: ((x + y) + z)) */
+static inline double heat_lap(const oc_problem* P, const double f[7], int dim) {
+    double l = lap1(f[0], f[1], f[2], P->hx) + lap1(f[0], f[3], f[4], P->hy);
+    if (dim == 3) l = l + lap1(f[0], f[5], f[6], P->hz);
+    return l;
+}
+
+/* G(u + eps v) at one point of a heat problem (v == NULL: G(u)).  du = a * lap(.):
+ *   G_Euler!     (implicit.jl:8-13)  res = (u_n + Δt du(w)) - w
+ *   G_Midpoint!  (implicit.jl:17-25) m = α u_n + (1 - α) w (elementwise, bc! applied to m);
+ *                                    res = (u_n + Δt du(m)) - w
+ *   G_Trapezoid! (implicit.jl:29-37) res = (u_n + (Δt/2)(du(u_n) + du(w))) - w               */
+static inline double heat_point(const oc_problem* P, const double* u, const double* v, double eps, int64_t i,
+                                int64_t j, int64_t k) {
+    int64_t q[7];
+    stencil_idx(P, i, j, k, q);
+    const int dim = oc_heat_dim(P->kind), sch = oc_scheme(P->kind);
+    const int ns = dim == 3 ? 7 : 5;
+    double w[7] = {0}, un[7] = {0}, m[7] = {0};
+    for (int s = 0; s < ns; ++s) {
+        if (q[s] < 0) continue;
+        w[s] = v ? u[q[s]] + eps * v[q[s]] : u[q[s]];
+        un[s] = P->un[q[s]];
+        m[s] = P->alpha * un[s] + (1.0 - P->alpha) * w[s];
+    }
+    if (sch == 1) return (un[0] + P->dt * (P->a * heat_lap(P, m, dim))) - w[0];
+    if (sch == 2) return (un[0] + (P->dt / 2.0) * (P->a * heat_lap(P, un, dim) + P->a * heat_lap(P, w, dim))) - w[0];
+    return (un[0] + P->dt * (P->a * heat_lap(P, w, dim))) - w[0];
+}
 
 /* value of w at (i,j,k) with zero Dirichlet outside, where w = u (+ eps*v when v != NULL) */
 static inline double wval(const double* u, const double* v, double eps, int64_t nx, int64_t ny, int64_t nz,
@@ -169,21 +232,9 @@ static inline double point_residual(const oc_problem* P, const double* u, const 
         double n = wval(u, v, eps, nx, ny, nz, i, j + 1, k), s = wval(u, v, eps, nx, ny, nz, i, j - 1, k);
         return (lap1(c, e, w, P->hx) + lap1(c, n, s, P->hy)) + P->lambda * exp(c);
     }
-    case OC_HEAT2D_EULER: {
-        double e = wval(u, v, eps, nx, ny, nz, i + 1, j, k), w = wval(u, v, eps, nx, ny, nz, i - 1, j, k);
-        double n = wval(u, v, eps, nx, ny, nz, i, j + 1, k), s = wval(u, v, eps, nx, ny, nz, i, j - 1, k);
-        double du = P->a * (lap1(c, e, w, P->hx) + lap1(c, n, s, P->hy));
-        return (AT(P->un, i, j, k) + P->dt * du) - c;
+    default:
+        return heat_point(P, u, v, eps, i, j, k);
     }
-    case OC_HEAT3D_EULER: {
-        double e = wval(u, v, eps, nx, ny, nz, i + 1, j, k), w = wval(u, v, eps, nx, ny, nz, i - 1, j, k);
-        double n = wval(u, v, eps, nx, ny, nz, i, j + 1, k), s = wval(u, v, eps, nx, ny, nz, i, j - 1, k);
-        double t = wval(u, v, eps, nx, ny, nz, i, j, k + 1), b = wval(u, v, eps, nx, ny, nz, i, j, k - 1);
-        double du = P->a * ((lap1(c, e, w, P->hx) + lap1(c, n, s, P->hy)) + lap1(c, t, b, P->hz));
-        return (AT(P->un, i, j, k) + P->dt * du) - c;
-    }
-    }
-    return NAN;
 }
 
 void oc_residual(const oc_problem* P, double* res, const double* u) {
@@ -192,6 +243,26 @@ void oc_residual(const oc_problem* P, double* res, const double* u) {
     for (int64_t k = 0; k < nz; ++k)
         for (int64_t j = 0; j < ny; ++j)
             for (int64_t i = 0; i < nx; ++i) AT(res, i, j, k) = point_residual(P, u, NULL, 0.0, i, j, k);
+}
+
+/* exact JVP of a heat problem: the forward-mode tangent Enzyme computes through G! ∘ diffusion!.
+ * u_n and du are constants (zero shadows), so 0 + x = x throughout:
+ *   Euler     Δt (a lap(v)) - v
+ *   Midpoint  Δt (a lap((1 - α) v)) - v      (the shadow of α u_n + (1 - α) u is (1 - α) v)
+ *   Trapezoid (Δt/2) (a lap(v)) - v          (the shadow of du(u_n) is 0)                        */
+static inline double heat_tangent(const oc_problem* P, const double* v, int64_t i, int64_t j, int64_t k) {
+    int64_t q[7];
+    stencil_idx(P, i, j, k, q);
+    const int dim = oc_heat_dim(P->kind), sch = oc_scheme(P->kind);
+    const int ns = dim == 3 ? 7 : 5;
+    double f[7] = {0};
+    for (int s = 0; s < ns; ++s) {
+        if (q[s] < 0) continue;
+        f[s] = sch == 1 ? (1.0 - P->alpha) * v[q[s]] : v[q[s]];
+    }
+    const double vc = v[q[0]];
+    if (sch == 2) return (P->dt / 2.0) * (P->a * heat_lap(P, f, dim)) - vc;
+    return P->dt * (P->a * heat_lap(P, f, dim)) - vc;
 }
 
 /* exact JVP: the forward-mode tangent Enzyme computes for each residual (Ariadne.jl:48-57) */
@@ -212,16 +283,8 @@ void oc_jv_exact(const oc_problem* P, double* out, const double* u, const double
                     r = (lap1(c, e, w, P->hx) + lap1(c, n, s, P->hy)) + P->lambda * (exp(AT(u, i, j, k)) * c);
                     break;
                 }
-                case OC_HEAT2D_EULER: {
-                    double n = wval(v, NULL, 0, nx, ny, nz, i, j + 1, k), s = wval(v, NULL, 0, nx, ny, nz, i, j - 1, k);
-                    r = P->dt * (P->a * (lap1(c, e, w, P->hx) + lap1(c, n, s, P->hy))) - c;
-                    break;
-                }
-                default: {
-                    double n = wval(v, NULL, 0, nx, ny, nz, i, j + 1, k), s = wval(v, NULL, 0, nx, ny, nz, i, j - 1, k);
-                    double t = wval(v, NULL, 0, nx, ny, nz, i, j, k + 1), b = wval(v, NULL, 0, nx, ny, nz, i, j, k - 1);
-                    r = P->dt * (P->a * ((lap1(c, e, w, P->hx) + lap1(c, n, s, P->hy)) + lap1(c, t, b, P->hz))) - c;
-                }
+                default:
+                    r = heat_tangent(P, v, i, j, k);
                 }
                 AT(out, i, j, k) = r;
             }

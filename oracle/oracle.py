@@ -23,6 +23,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "libnkoracle.so")
 
 BRATU1D, BRATU2D, HEAT2D_EULER, HEAT3D_EULER = 1, 2, 3, 4
+HEAT2D_MIDPOINT, HEAT3D_MIDPOINT, HEAT2D_TRAPEZOID, HEAT3D_TRAPEZOID = 5, 6, 7, 8
+BC_ZERO, BC_PERIODIC = 0, 1
+HEAT_KINDS = {  # (scheme, dim) -> kind; schemes of examples/implicit.jl:8-37
+    ("euler", 2): HEAT2D_EULER, ("euler", 3): HEAT3D_EULER,
+    ("midpoint", 2): HEAT2D_MIDPOINT, ("midpoint", 3): HEAT3D_MIDPOINT,
+    ("trapezoid", 2): HEAT2D_TRAPEZOID, ("trapezoid", 3): HEAT3D_TRAPEZOID,
+}
 JV_EXACT, JV_FD = 0, 1
 FORCING_NONE, FORCING_FIXED, FORCING_EW = 0, 1, 2
 ALGO_GMRES, ALGO_CG = 0, 1
@@ -34,7 +41,7 @@ class _Problem(C.Structure):
                 ("nx", C.c_int64), ("ny", C.c_int64), ("nz", C.c_int64),
                 ("hx", C.c_double), ("hy", C.c_double), ("hz", C.c_double),
                 ("lam", C.c_double), ("a", C.c_double), ("dt", C.c_double),
-                ("un", C.POINTER(C.c_double))]
+                ("un", C.POINTER(C.c_double)), ("alpha", C.c_double)]
 
 
 class _KrylovOpts(C.Structure):
@@ -119,6 +126,8 @@ class Problem:
     a: float = 0.0
     dt: float = 0.0
     un: np.ndarray | None = field(default=None, repr=False)
+    bc: int = BC_ZERO
+    alpha: float = 0.5  # G_Midpoint! α (implicit.jl:17)
 
     @property
     def n(self) -> int:
@@ -130,10 +139,13 @@ class Problem:
 
     @property
     def dim(self) -> int:
-        return 1 if self.kind == BRATU1D else (3 if self.kind == HEAT3D_EULER else 2)
+        if self.kind == BRATU1D:
+            return 1
+        return 3 if self.kind in (HEAT3D_EULER, HEAT3D_MIDPOINT, HEAT3D_TRAPEZOID) else 2
 
     def _c(self) -> _Problem:
-        s = _Problem(self.kind, 0, self.nx, self.ny, self.nz, self.hx, self.hy, self.hz, self.lam, self.a, self.dt, None)
+        s = _Problem(self.kind, self.bc, self.nx, self.ny, self.nz, self.hx, self.hy, self.hz, self.lam, self.a,
+                     self.dt, None, self.alpha)
         if self.un is not None:
             self._un_keep = np.ascontiguousarray(self.un, dtype=np.float64).reshape(-1)
             assert self._un_keep.size == self.n
@@ -159,23 +171,26 @@ def heat_dt_2d(hx, hy, a):
     return hx ** 2 * hy ** 2 / (2.0 * a * (hx ** 2 + hy ** 2))  # heat_2D.jl:72
 
 
-def heat2d_euler(nx: int, ny: int | None = None, a: float = 0.01, dt: float | None = None, un=None) -> Problem:
+def heat2d_euler(nx: int, ny: int | None = None, a: float = 0.01, dt: float | None = None, un=None,
+                 scheme: str = "euler", bc: int = BC_ZERO, alpha: float = 0.5) -> Problem:
+    """G!(res, u_n, Δt, diffusion!, du, u, (a, Δx, Δy, bc!), t) for G in implicit.jl:8-37."""
     ny = nx if ny is None else ny
     hx, hy = 1.0 / (nx + 1), 1.0 / (ny + 1)
     dt = heat_dt_2d(hx, hy, a) if dt is None else dt
-    return Problem(HEAT2D_EULER, nx, ny, hx=hx, hy=hy, a=a, dt=dt, un=un)
+    return Problem(HEAT_KINDS[scheme, 2], nx, ny, hx=hx, hy=hy, a=a, dt=dt, un=un, bc=bc, alpha=alpha)
 
 
 def heat_dt_3d(hx, hy, hz, a):
     return 1.0 / (2.0 * a * (1.0 / hx ** 2 + 1.0 / hy ** 2 + 1.0 / hz ** 2))
 
 
-def heat3d_euler(nx: int, ny=None, nz=None, a: float = 0.01, dt=None, un=None) -> Problem:
+def heat3d_euler(nx: int, ny=None, nz=None, a: float = 0.01, dt=None, un=None, scheme: str = "euler",
+                 bc: int = BC_ZERO, alpha: float = 0.5) -> Problem:
     ny = nx if ny is None else ny
     nz = nx if nz is None else nz
     hx, hy, hz = 1.0 / (nx + 1), 1.0 / (ny + 1), 1.0 / (nz + 1)
     dt = heat_dt_3d(hx, hy, hz, a) if dt is None else dt
-    return Problem(HEAT3D_EULER, nx, ny, nz, hx=hx, hy=hy, hz=hz, a=a, dt=dt, un=un)
+    return Problem(HEAT_KINDS[scheme, 3], nx, ny, nz, hx=hx, hy=hy, hz=hz, a=a, dt=dt, un=un, bc=bc, alpha=alpha)
 
 
 def sin_ic(P: Problem) -> np.ndarray:

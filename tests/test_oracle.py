@@ -254,3 +254,71 @@ def test_heat2d_reference_ic_one_step(golden_dir):
     assert st["inner_iterations"] == 1
     assert np.max(np.abs(u - g["u1"])) < 1e-10
     assert np.max(np.abs(u - g["decay"] * g["u0"])) < 1e-10
+
+
+# ----------------------------------------------------------------------------- time-stepping schemes (§8f rank 1)
+SCHEMES = [("euler", ar.G_Euler_h, {}), ("midpoint", ar.G_Midpoint_h, {}),
+           ("midpoint", ar.G_Midpoint_h, {"alpha": 0.3}), ("trapezoid", ar.G_Trapezoid_h, {})]
+
+
+@pytest.mark.parametrize("bc", [oc.BC_ZERO, oc.BC_PERIODIC])
+@pytest.mark.parametrize("scheme,G,kw", SCHEMES, ids=["euler", "midpoint", "midpoint_a0.3", "trapezoid"])
+def test_heat_schemes_match_halo_restatement(scheme, G, kw, bc):
+    """The C oracle's G! ∘ diffusion! (all three implicit.jl schemes, bc_zero! / bc_periodic!) against
+    a literal restatement of implicit.jl:8-37 + heat_2D.jl:15-62 on halo arrays, differentiated by
+    dual numbers: residual and exact JVP bit for bit (square grid: the reference's bc! reuse N for
+    the second axis, heat_2D.jl:23-24, 35-36)."""
+    rng = np.random.default_rng(7)
+    N = 12
+    un, u, v = (rng.standard_normal((N, N)) for _ in range(3))
+    P = oc.heat2d_euler(N, un=un, scheme=scheme, bc=bc, alpha=kw.get("alpha", 0.5))
+    bch = ar.bc_periodic_h if bc == oc.BC_PERIODIC else ar.bc_zero_h
+    val, tan = ar.heat_halo_jvp(G, un, u, v, P.a, P.hx, P.hy, P.dt, bch, **kw)
+    assert np.array_equal(oc.residual(P, u), val)
+    assert np.array_equal(oc.jv_exact(P, u, v), tan)
+    assert _rel(oc.jv_fd(P, u, v), tan) < 1e-6
+
+
+def _decay(scheme, dt, mu, alpha=0.5):
+    """Exact one-step amplification of an eigenvector of the discrete Laplacian (eigenvalue mu)."""
+    if scheme == "euler":
+        return 1.0 / (1.0 - dt * mu)
+    if scheme == "midpoint":
+        return (1.0 + alpha * dt * mu) / (1.0 - (1.0 - alpha) * dt * mu)
+    return (1.0 + 0.5 * dt * mu) / (1.0 - 0.5 * dt * mu)
+
+
+@pytest.mark.parametrize("scheme,alpha", [("euler", 0.5), ("midpoint", 0.5), ("midpoint", 0.25), ("trapezoid", 0.5)])
+@pytest.mark.parametrize("bc", [oc.BC_ZERO, oc.BC_PERIODIC])
+def test_heat_schemes_eigen_decay(scheme, alpha, bc):
+    """One implicit step (tol_abs = 6e-6, implicit.jl:67-70) from an eigenvector IC -- sin(πx)sin(πy)
+    for bc_zero!, cos(2πi/N)cos(2πj/N) for bc_periodic! -- reproduces the scheme's exact amplification
+    factor with a single Krylov iteration."""
+    N = 40
+    P = oc.heat2d_euler(N, scheme=scheme, bc=bc, alpha=alpha)
+    h = P.hx
+    if bc == oc.BC_ZERO:
+        u0 = oc.sin_ic(P)
+        s2 = math.sin(math.pi * h / 2) ** 2
+    else:
+        ph = np.cos(2 * np.pi * np.arange(N) / N)
+        u0 = np.ascontiguousarray(ph[:, None] * ph[None, :])
+        s2 = math.sin(math.pi / N) ** 2
+    mu = -P.a * 8.0 / (h * h) * s2
+    P.un = u0
+    u, st = oc.newton_krylov(P, u0, tol_abs=6e-6)
+    assert st["solved"] and st["inner_iterations"] == 1
+    assert np.max(np.abs(u - _decay(scheme, P.dt, mu, alpha) * u0)) < 1e-10
+
+
+def test_heat3d_schemes_periodic_eigen_decay():
+    """3D (build-defined) analogue: the periodic cos mode in x, y, z, every scheme."""
+    N = 10
+    c = np.cos(2 * np.pi * np.arange(N) / N)
+    u0 = np.ascontiguousarray(c[:, None, None] * c[None, :, None] * c[None, None, :])
+    for scheme in ("euler", "midpoint", "trapezoid"):
+        P = oc.heat3d_euler(N, scheme=scheme, bc=oc.BC_PERIODIC, un=u0)
+        mu = -P.a * 12.0 / (P.hx * P.hx) * math.sin(math.pi / N) ** 2
+        u, st = oc.newton_krylov(P, u0, tol_abs=6e-6)
+        assert st["solved"] and st["inner_iterations"] == 1
+        assert np.max(np.abs(u - _decay(scheme, P.dt, mu) * u0)) < 1e-10
