@@ -40,12 +40,20 @@ extern "C" {
 #define NK_BRATU2D 2       /* build-defined 2D generalisation                       */
 #define NK_HEAT2D_EULER 3  /* examples/implicit.jl:8-13 G_Euler! ∘ examples/heat_2D.jl:45-62 diffusion! */
 #define NK_HEAT3D_EULER 4  /* build-defined 3D generalisation                      */
+/* the other implicit schemes of examples/implicit.jl composed with diffusion! */
+#define NK_HEAT2D_MIDPOINT 5   /* G_Midpoint!  implicit.jl:17-25 (α = nk_problem.alpha)  */
+#define NK_HEAT3D_MIDPOINT 6
+#define NK_HEAT2D_TRAPEZOID 7  /* G_Trapezoid! implicit.jl:29-37                         */
+#define NK_HEAT3D_TRAPEZOID 8
 
 #define NK_USER1D 16       /* user residual F!(res, u, p) given as callbacks, */
 #define NK_USER2D 17       /* on a 1D / 2D / 3D grid (the kind fixes the slab axis, as for the      */
 #define NK_USER3D 18       /* built-in kinds)                                                      */
 
 #define NK_BC_ZERO 0       /* bc_zero!, examples/heat_2D.jl:28-38 */
+#define NK_BC_PERIODIC 1   /* bc_periodic!, examples/heat_2D.jl:15-26 (heat kinds; every extent >= 3):
+                              x / y wrap inside the kernels, the slab axis through the ghost planes
+                              (a ring exchange: rank 0's lower neighbour is rank nranks - 1)       */
 
 #define NK_JV_EXACT 0      /* exact JVP == Enzyme Forward in mul!(out, J, v), src/Ariadne.jl:48-57 */
 #define NK_JV_FD 1         /* (F(u + eps v) - F(u)) / eps, BASELINE.json north star                */
@@ -91,14 +99,17 @@ typedef struct nk_user_ops {
  * spacings are global (h = 1/(N_global + 1)).  x is the fastest axis (the reference's
  * column-major first index). */
 typedef struct nk_problem {
-    int32_t kind;           /* NK_BRATU1D … NK_HEAT3D_EULER, NK_USER1D … NK_USER3D */
-    int32_t bc;             /* NK_BC_ZERO */
+    int32_t kind;           /* NK_BRATU1D … NK_HEAT3D_TRAPEZOID, NK_USER1D … NK_USER3D */
+    int32_t bc;             /* NK_BC_ZERO / NK_BC_PERIODIC */
     int64_t nx, ny, nz;     /* local interior extents (ny = nz = 1 in 1D, nz = 1 in 2D) */
     double hx, hy, hz;      /* grid spacings */
     double lambda;          /* Bratu λ */
     double a, dt;           /* heat diffusivity and time step Δt */
-    const double* un;       /* heat: device interior pointer to u_n (borrowed for the call) */
+    const double* un;       /* heat: device interior pointer to u_n (borrowed for the call).  Midpoint /
+                               trapezoid read its neighbours too: it must be an nk_vec_alloc grid function
+                               (its ghost planes are exchanged / wrapped by the library) */
     const nk_user_ops* user;  /* NK_USER*: the callbacks (borrowed for the call) */
+    double alpha;           /* NK_HEAT*_MIDPOINT: G_Midpoint!'s α (the reference's default is 0.5) */
 } nk_problem;
 
 /* ---------------------------------------------------------------- context / memory */

@@ -12,7 +12,8 @@ from .implicit import G_Euler_, G_Midpoint_, G_Trapezoid_, diffusion3d_, diffusi
 from .krylov import (KrylovConstructor, kaxpby_, kaxpy_, kaxpy_norm_, kcopy_, kdivcopy_, kdot, kfill_, knorm, kref_, krylov_solve_,
                      krylov_workspace, kscal_)
 from .precond import DiagonalPreconditioner, Preconditioner, UserPreconditioner, jacobi, jacobian_diag
-from .problems import DeviceResidual, UserResidual, bc_zero_, bratu2d_, bratu_, heat2d_euler_, heat3d_euler_
+from .problems import (DeviceResidual, UserResidual, bc_periodic_, bc_zero_, bratu2d_, bratu_, heat2d_euler_, heat2d_midpoint_,
+                       heat2d_trapezoid_, heat3d_euler_, heat3d_midpoint_, heat3d_trapezoid_)
 
 __all__ = [
     "NKError", "device_count", "load", "EisenstatWalker", "Fixed", "Forcing", "JacobianOperator", "Result", "Stats",
@@ -21,5 +22,6 @@ __all__ = [
     "KrylovConstructor", "kaxpby_", "kaxpy_", "kaxpy_norm_", "kcopy_", "kdivcopy_", "kdot", "kfill_", "knorm", "kref_",
     "DiagonalPreconditioner", "Preconditioner", "UserPreconditioner", "jacobi", "jacobian_diag",
     "krylov_solve_", "krylov_workspace", "kscal_", "DeviceResidual", "UserResidual", "bc_zero_", "bratu2d_", "bratu_",
-    "heat2d_euler_", "heat3d_euler_",
+    "heat2d_euler_", "heat3d_euler_", "heat2d_midpoint_", "heat3d_midpoint_", "heat2d_trapezoid_", "heat3d_trapezoid_",
+    "bc_periodic_",
 ]

@@ -16,8 +16,9 @@ HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "nkhip.h")
 
 NK_OK = 0
 NK_BRATU1D, NK_BRATU2D, NK_HEAT2D_EULER, NK_HEAT3D_EULER = 1, 2, 3, 4
+NK_HEAT2D_MIDPOINT, NK_HEAT3D_MIDPOINT, NK_HEAT2D_TRAPEZOID, NK_HEAT3D_TRAPEZOID = 5, 6, 7, 8
 NK_USER1D, NK_USER2D, NK_USER3D = 16, 17, 18
-NK_BC_ZERO = 0
+NK_BC_ZERO, NK_BC_PERIODIC = 0, 1
 NK_JV_EXACT, NK_JV_FD = 0, 1
 NK_ALGO_GMRES, NK_ALGO_CG, NK_ALGO_FGMRES = 0, 1, 2
 NK_PRECOND_NONE, NK_PRECOND_DIAG, NK_PRECOND_USER = 0, 1, 2
@@ -34,7 +35,7 @@ class nk_problem(C.Structure):
                 ("nx", C.c_int64), ("ny", C.c_int64), ("nz", C.c_int64),
                 ("hx", C.c_double), ("hy", C.c_double), ("hz", C.c_double),
                 ("lam", C.c_double), ("a", C.c_double), ("dt", C.c_double),
-                ("un", C.c_void_p), ("user", C.c_void_p)]
+                ("un", C.c_void_p), ("user", C.c_void_p), ("alpha", C.c_double)]
 
 
 # nk_user_ops: int F(void* data, nk_ctx*, double* res, const double* u); int J(data, ctx, out, u, v)

@@ -2,9 +2,9 @@
 
 `solve(G_Euler_, diffusion_, uₙ, p, Δt, ts)` mirrors `solve(G!, f!, uₙ, p, Δt, ts; …)`
 (implicit.jl:54-78): one `newton_krylov_` per time step with tol_abs = 6e-6, warn-and-march-on
-when a step fails, `uₙ .= u` after each step.  The composition G_Euler! ∘ diffusion! is one
-fused device residual (heat2d_euler_ / heat3d_euler_).  G_Midpoint!/G_Trapezoid! and periodic
-boundaries are SURVEY.md §8f "next" items and raise NotImplementedError.
+when a step fails, `uₙ .= u` after each step.  Each composition G! ∘ diffusion! of the three
+schemes (G_Euler!, G_Midpoint! with its α keyword, G_Trapezoid!; implicit.jl:8-37) is one fused
+device residual (problems._Heat), with bc_zero_ or bc_periodic_ (heat_2D.jl:15-38) in p.
 """
 from __future__ import annotations
 
@@ -13,7 +13,7 @@ import logging
 from .ariadne import newton_krylov_
 from .device import DeviceArray
 from .krylov import KrylovConstructor, kcopy_, krylov_workspace
-from .problems import heat2d_euler_, heat3d_euler_
+from .problems import _Heat
 
 log = logging.getLogger("ariadne_hip")
 
@@ -33,20 +33,25 @@ diffusion3d_ = _Diffusion(3)
 
 
 class _Scheme:
-    def __init__(self, name):
+    """G_Euler! / G_Midpoint! / G_Trapezoid! (implicit.jl:8-37) as markers: `bind(f)` returns the fused
+    device residual of G ∘ f.  `G_Midpoint_(alpha=…)` is G_Midpoint!'s keyword (default 0.5)."""
+
+    def __init__(self, name, alpha=0.5):
         self.name = name
+        self.alpha = float(alpha)
+
+    def __call__(self, *, alpha):
+        if self.name != "G_Midpoint!":
+            raise TypeError(f"{self.name} takes no keywords")
+        return _Scheme(self.name, alpha)
 
     def bind(self, f):
-        if self.name != "G_Euler!":
-            raise NotImplementedError(f"{self.name} on the device is a SURVEY.md §8f 'next' item")
-        if f is diffusion_:
-            return heat2d_euler_
-        if f is diffusion3d_:
-            return heat3d_euler_
-        raise NotImplementedError(f"no fused device residual for {self.name} ∘ {f}")
+        if not isinstance(f, _Diffusion):
+            raise NotImplementedError(f"no fused device residual for {self.name} ∘ {f}")
+        return _Heat(f.dim, self.name, self.alpha)
 
     def __repr__(self):
-        return self.name
+        return self.name if self.alpha == 0.5 else f"{self.name}(α = {self.alpha})"
 
 
 G_Euler_ = _Scheme("G_Euler!")

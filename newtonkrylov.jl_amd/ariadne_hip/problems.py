@@ -10,6 +10,7 @@ loop, and `JacobianOperator` maps it to the matching fused Jv kernel (nk_jv) ins
 | `bratu2d_`    | 2D generalisation                  | `(dx, dy, lam)`                      |
 | `heat2d_euler_` | `G_Euler!` ∘ `diffusion!` implicit.jl:8-13 + heat_2D.jl:45-62 | `(u_n, dt, du, (a, dx, dy, bc_zero_), t)` |
 | `heat3d_euler_` | 3D generalisation                | `(u_n, dt, du, (a, dx, dy, dz, bc_zero_), t)` |
+| `heat{2,3}d_midpoint_`, `heat{2,3}d_trapezoid_` | `G_Midpoint!` / `G_Trapezoid!` ∘ `diffusion!` implicit.jl:17-37 | as above; `bc_periodic_` (heat_2D.jl:15-26) for any heat residual |
 | `UserResidual(F[, J])` | any `F!(res, u, p)` evaluated on the device by the caller | the caller's |
 """
 from __future__ import annotations
@@ -75,13 +76,37 @@ class _Bratu2D(DeviceResidual):
         return _lib.nk_problem(self.kind, 0, nx, ny, 1, float(dx), float(dy), 1.0, float(lam), 0.0, 0.0, None)
 
 
-class _HeatEuler(DeviceResidual):
-    """F!(res, u, (uₙ, Δt, du, p, t)) = G_Euler!(res, uₙ, Δt, diffusion!, du, u, p, t)."""
+def bc_periodic_(u):
+    """`bc_periodic!` (heat_2D.jl:15-26): a marker.  The kernels wrap x (and y in 3D) and the library
+    fills the ghost planes along the slab axis with the opposite edge (a ring exchange when
+    distributed) before every stencil, including for the tangent v -- what Enzyme's forward
+    mode does to the shadow ghosts."""
+    return None
 
-    def __init__(self, dim: int):
-        self.dim = dim
-        self.kind = _lib.NK_HEAT2D_EULER if dim == 2 else _lib.NK_HEAT3D_EULER
-        self.name = f"G_Euler!∘diffusion{dim}d!"
+
+_SCHEMES = {  # implicit.jl:8-37
+    ("G_Euler!", 2): _lib.NK_HEAT2D_EULER, ("G_Euler!", 3): _lib.NK_HEAT3D_EULER,
+    ("G_Midpoint!", 2): _lib.NK_HEAT2D_MIDPOINT, ("G_Midpoint!", 3): _lib.NK_HEAT3D_MIDPOINT,
+    ("G_Trapezoid!", 2): _lib.NK_HEAT2D_TRAPEZOID, ("G_Trapezoid!", 3): _lib.NK_HEAT3D_TRAPEZOID,
+}
+
+
+class _Heat(DeviceResidual):
+    """F!(res, u, (uₙ, Δt, du, p, t)) = G!(res, uₙ, Δt, diffusion!, du, u, p, t) for G ∈ {G_Euler!,
+    G_Midpoint!(α), G_Trapezoid!} (implicit.jl:8-37, 61), p = (a, Δx, Δy[, Δz], bc!) with bc! one of
+    bc_zero_ / bc_periodic_ (heat_2D.jl:15-38).  One fused stencil kernel per call."""
+
+    def __init__(self, dim: int, scheme: str = "G_Euler!", alpha: float = 0.5):
+        self.dim, self.scheme, self.alpha = dim, scheme, float(alpha)
+        self.kind = _SCHEMES[scheme, dim]
+        a = f"(α = {self.alpha})" if scheme == "G_Midpoint!" and self.alpha != 0.5 else ""
+        self.name = f"{scheme}{a}∘diffusion{dim}d!"
+
+    def with_alpha(self, alpha: float) -> "_Heat":
+        """G_Midpoint!(…; α) -- the keyword of implicit.jl:17."""
+        if self.scheme != "G_Midpoint!":
+            raise ValueError("α is a G_Midpoint! keyword")
+        return _Heat(self.dim, self.scheme, alpha)
 
     def problem(self, u, p):
         un, dt, _du, fp, _t = p
@@ -92,19 +117,29 @@ class _HeatEuler(DeviceResidual):
             dz = 1.0
         else:
             a, dx, dy, dz, bc = fp
-        if bc is not bc_zero_:
-            raise NotImplementedError("only bc_zero! is implemented on the device (periodic BC: SURVEY.md §8f)")
+        if bc is bc_zero_:
+            code = _lib.NK_BC_ZERO
+        elif bc is bc_periodic_:
+            code = _lib.NK_BC_PERIODIC
+        else:
+            raise NotImplementedError(f"boundary {bc!r}: the device kernels implement bc_zero_ and bc_periodic_")
         if not isinstance(un, DeviceArray) or un.grid != u.grid:
             raise ValueError("u_n must be a DeviceArray on u's grid")
         nx, ny, nz = u.grid.nxyz
-        return _lib.nk_problem(self.kind, 0, nx, ny, nz, float(dx), float(dy), float(dz), 0.0, float(a), float(dt),
-                               un.ptr)
+        return _lib.nk_problem(self.kind, code, nx, ny, nz, float(dx), float(dy), float(dz), 0.0, float(a), float(dt),
+                               un.ptr, None, self.alpha)
 
+
+_HeatEuler = _Heat  # backwards-compatible name
 
 bratu_ = _Bratu1D()
 bratu2d_ = _Bratu2D()
-heat2d_euler_ = _HeatEuler(2)
-heat3d_euler_ = _HeatEuler(3)
+heat2d_euler_ = _Heat(2)
+heat3d_euler_ = _Heat(3)
+heat2d_midpoint_ = _Heat(2, "G_Midpoint!")
+heat3d_midpoint_ = _Heat(3, "G_Midpoint!")
+heat2d_trapezoid_ = _Heat(2, "G_Trapezoid!")
+heat3d_trapezoid_ = _Heat(3, "G_Trapezoid!")
 
 
 # ----------------------------------------------------------------------------- user residuals

@@ -25,10 +25,14 @@ int geometry(nk_ctx* c, const nk_problem* p, Geo* g) {
         break;
     case NK_BRATU2D:
     case NK_HEAT2D_EULER:
+    case NK_HEAT2D_MIDPOINT:
+    case NK_HEAT2D_TRAPEZOID:
         if (p->nz != 1) return fail(c, NK_E_ARG, "2D problem needs nz = 1");
         g->dim = 2; g->plane = p->nx; g->nplanes = p->ny;
         break;
     case NK_HEAT3D_EULER:
+    case NK_HEAT3D_MIDPOINT:
+    case NK_HEAT3D_TRAPEZOID:
         g->dim = 3; g->plane = p->nx * p->ny; g->nplanes = p->nz;
         break;
     case NK_USER1D:
@@ -48,9 +52,15 @@ int geometry(nk_ctx* c, const nk_problem* p, Geo* g) {
     default:
         return fail(c, NK_E_ARG, "unknown problem kind");
     }
-    if (p->bc != NK_BC_ZERO) return fail(c, NK_E_ARG, "only zero-Dirichlet boundaries are implemented");
-    if ((p->kind == NK_HEAT2D_EULER || p->kind == NK_HEAT3D_EULER) && !p->un)
-        return fail(c, NK_E_ARG, "heat problem needs u_n");
+    if (p->bc == NK_BC_PERIODIC) {
+        if (!nk_is_heat(p->kind)) return fail(c, NK_E_ARG, "periodic boundaries are defined for the heat problems (bc_periodic!)");
+        // every wrapped axis needs >= 3 points (the slab axis: the whole grid when not distributed)
+        if (p->nx < 3 || (g->dim == 3 && p->ny < 3) || (c->nranks <= 1 && g->nplanes < 3))
+            return fail(c, NK_E_ARG, "periodic boundaries need >= 3 points along every axis");
+    } else if (p->bc != NK_BC_ZERO) {
+        return fail(c, NK_E_ARG, "unknown boundary condition");
+    }
+    if (nk_is_heat(p->kind) && !p->un) return fail(c, NK_E_ARG, "heat problem needs u_n");
     g->n = p->nx * p->ny * p->nz;
     g->front = (g->plane + 31) / 32 * 32;
     return NK_OK;
@@ -263,6 +273,7 @@ int nk_memcpy_d2h(nk_ctx* c, double* dst, const double* src, int64_t n) {
 int nk_residual(nk_ctx* c, const nk_problem* p, double* res, const double* u) {
     if (!c || !res || !u) return NK_E_ARG;
     NK_TRY(halo_exchange(c, p, u));
+    NK_TRY(exchange_un(c, p));
     StencilIn in{p, MODE_RES, EPI_NONE, res, u, nullptr, nullptr, nullptr, 0.0};
     Red r{};
     return launch_stencil(c, in, &r);
@@ -271,6 +282,7 @@ int nk_residual(nk_ctx* c, const nk_problem* p, double* res, const double* u) {
 int nk_residual_norm(nk_ctx* c, const nk_problem* p, double* res, const double* u, double* n_res) {
     if (!c || !res || !u || !n_res) return NK_E_ARG;
     NK_TRY(halo_exchange(c, p, u));
+    NK_TRY(exchange_un(c, p));
     StencilIn in{p, MODE_RES, EPI_SUMSQ, res, u, nullptr, nullptr, nullptr, 0.0};
     Red r{};
     NK_TRY(launch_stencil(c, in, &r));
@@ -299,6 +311,7 @@ int nk_jv(nk_ctx* c, const nk_problem* p, double* out, const double* u, const do
         }
     }
     NK_TRY(halo_exchange(c, p, u));
+    NK_TRY(exchange_un(c, p));
     NK_TRY(halo_exchange(c, p, v));
     StencilIn in{p, mode == NK_JV_FD ? MODE_JFD : MODE_JEXACT, EPI_NONE, out, u, v, F0, nullptr, eps};
     Red r{};

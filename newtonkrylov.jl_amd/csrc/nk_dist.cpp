@@ -21,35 +21,46 @@ static int rccl_fail(nk_ctx* c, ncclResult_t r, const char* what) {
     return fail(c, NK_E_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
+// bc_periodic! (heat_2D.jl:15-26) along the slab axis makes the slabs a ring: the lone slab wraps
+// onto itself (a local copy), rank 0's lower neighbour is rank nranks-1 and vice versa.
 int halo_exchange(nk_ctx* c, const nk_problem* p, const double* v) {
-    if (!c->comm && !c->mb_on) return NK_OK;
+    const bool ring = p && p->bc == NK_BC_PERIODIC;
+    if (!ring && !c->comm && !c->mb_on) return NK_OK;
     Geo g;
     NK_TRY(geometry(c, p, &g));
     double* vv = const_cast<double*>(v);  // only the ghost planes are written
-    if (c->mb_on && g.plane <= c->halo_cap) return launch_halo_ipc(c, vv, g.plane, g.nplanes);
+    if (ring && c->nranks <= 1) return launch_periodic_fill(c, vv, g.plane, g.nplanes);
+    if (!c->comm && !c->mb_on) return NK_OK;
+    if (c->mb_on && g.plane <= c->halo_cap) return launch_halo_ipc(c, vv, g.plane, g.nplanes, ring);
     if (!c->comm) return fail(c, NK_E_ARG, "ghost plane larger than the IPC inbox (NK_HALO_CAP) and no RCCL communicator");
     const size_t pl = (size_t)g.plane;
-    const int up = c->rank + 1, dn = c->rank - 1;
+    const int n = c->nranks;
+    const int up = c->rank + 1 < n ? c->rank + 1 : (ring ? 0 : -1);
+    const int dn = c->rank > 0 ? c->rank - 1 : (ring ? n - 1 : -1);
     ncclComm_t comm = c->comm->comm;
-    if (dn < 0 && up >= c->nranks) return NK_OK;  // a lone slab has only physical boundaries
+    if (dn < 0 && up < 0) return NK_OK;  // a lone slab has only physical boundaries
     ncclResult_t r = ncclSuccess;
     auto chk = [&r](ncclResult_t x) {
         if (r == ncclSuccess) r = x;
     };
-    NK_TRY(launch(c, "halo", 16.0 * pl * ((dn >= 0) + (up < c->nranks)), [&] {
+    // Posting order matters when both neighbours are the same rank (a ring of two): sends go up
+    // then down, receives come from below then above, so the FIFO matching per peer pairs my
+    // lower ghost with the neighbour's last plane and my upper ghost with its first.
+    NK_TRY(launch(c, "halo", 16.0 * pl * ((dn >= 0) + (up >= 0)), [&] {
         chk(ncclGroupStart());
-        if (dn >= 0) {  // my first interior plane -> lower neighbour's upper ghost; its last -> my lower ghost
-            chk(ncclSend(vv, pl, ncclFloat64, dn, comm, c->stream));
-            chk(ncclRecv(vv - pl, pl, ncclFloat64, dn, comm, c->stream));
-        }
-        if (up < c->nranks) {
-            chk(ncclSend(vv + (size_t)(g.nplanes - 1) * pl, pl, ncclFloat64, up, comm, c->stream));
-            chk(ncclRecv(vv + (size_t)g.nplanes * pl, pl, ncclFloat64, up, comm, c->stream));
-        }
+        if (up >= 0) chk(ncclSend(vv + (size_t)(g.nplanes - 1) * pl, pl, ncclFloat64, up, comm, c->stream));
+        if (dn >= 0) chk(ncclSend(vv, pl, ncclFloat64, dn, comm, c->stream));
+        if (dn >= 0) chk(ncclRecv(vv - pl, pl, ncclFloat64, dn, comm, c->stream));
+        if (up >= 0) chk(ncclRecv(vv + (size_t)g.nplanes * pl, pl, ncclFloat64, up, comm, c->stream));
         chk(ncclGroupEnd());
     }));
     if (r != ncclSuccess) return rccl_fail(c, r, "halo send/recv");
     return NK_OK;
+}
+
+int exchange_un(nk_ctx* c, const nk_problem* p) {
+    if (!p || !nk_is_heat(p->kind) || nk_scheme(p->kind) == 0 || !p->un) return NK_OK;
+    return halo_exchange(c, p, p->un);
 }
 
 int allreduce_scalar(nk_ctx* c, double* dev, int64_t count) {

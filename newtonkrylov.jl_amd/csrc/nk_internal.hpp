@@ -157,7 +157,8 @@ int mailbox_bind(nk_ctx* c);                 // make c's mailbox the one the ker
 int mailbox_selftest(nk_ctx* c, bool* ok);   // a few epochs through the mailbox vs the expected sums
 // ghost planes of v (interior pointer, `plane` doubles per plane, `nplanes` planes) through the peer
 // inboxes: push my boundary planes into the neighbours' inboxes, pull theirs into my ghost planes
-int launch_halo_ipc(nk_ctx* c, double* v, int64_t plane, int64_t nplanes);
+int launch_halo_ipc(nk_ctx* c, double* v, int64_t plane, int64_t nplanes, bool ring);
+int launch_periodic_fill(nk_ctx* c, double* v, int64_t plane, int64_t nplanes);
 
 // ---------------------------------------------------------------- kernel launchers (nk_kernels.hip)
 struct StencilIn {
@@ -211,9 +212,17 @@ int launch_user_epi(nk_ctx* c, int64_t n, int fd, double* out, const double* F0,
                     const double* aux, Red* red);
 int launch_user(nk_ctx* c, const StencilIn& in, Red* red);  // nk_user.cpp
 inline bool nk_is_user(int kind) { return kind >= NK_USER1D && kind <= NK_USER3D; }
+inline bool nk_is_heat(int kind) { return kind >= NK_HEAT2D_EULER && kind <= NK_HEAT3D_TRAPEZOID; }
+// implicit.jl scheme of a heat kind: 0 G_Euler!, 1 G_Midpoint!, 2 G_Trapezoid!
+inline int nk_scheme(int kind) {
+    return (kind == NK_HEAT2D_MIDPOINT || kind == NK_HEAT3D_MIDPOINT) ? 1
+           : ((kind == NK_HEAT2D_TRAPEZOID || kind == NK_HEAT3D_TRAPEZOID) ? 2 : 0);
+}
 
 // ---------------------------------------------------------------- distribution (nk_dist.cpp)
 int halo_exchange(nk_ctx* c, const nk_problem* p, const double* v);
+// ghost planes of u_n when the residual reads its neighbours (G_Midpoint!, G_Trapezoid!)
+int exchange_un(nk_ctx* c, const nk_problem* p);
 int allreduce_scalar(nk_ctx* c, double* dev, int64_t count);
 
 }  // namespace nk

@@ -186,7 +186,20 @@ struct KArgs {
     double* vout;
     double hd;           // *vdiv, loaded once per block
     int fin;             // fold the partials in-kernel (publish)
+    double alpha;        // G_Midpoint! α
 };
+
+// implicit.jl scheme of a heat kind: 0 G_Euler! (and the Bratu kinds), 1 G_Midpoint!, 2 G_Trapezoid!
+template <int KIND>
+constexpr int scheme_of() {
+    return (KIND == NK_HEAT2D_MIDPOINT || KIND == NK_HEAT3D_MIDPOINT)
+               ? 1
+               : ((KIND == NK_HEAT2D_TRAPEZOID || KIND == NK_HEAT3D_TRAPEZOID) ? 2 : 0);
+}
+template <int KIND>
+constexpr bool heat_kind() {
+    return KIND >= NK_HEAT2D_EULER && KIND <= NK_HEAT3D_TRAPEZOID;
+}
 
 __device__ __forceinline__ double vin(const KArgs& A, int64_t o) {
     const double v = A.v[o];
@@ -246,16 +259,24 @@ __device__ __forceinline__ void storevec(double* __restrict__ p, int64_t o, cons
 }
 
 // residual / JVP value at one point from the stencil field (c + neighbours) and centre data.
-// lsum = Laplacian-like sum in the reference's association order.
+// lsum = Laplacian-like sum of the stencil field in the reference's association order.  Heat kinds:
+// xc = the centre of w = u (+ eps v) -- or of v for the tangent -- before G_Midpoint!'s mixing (the
+// "- u" term), unc = u_n, lsumg = the Laplacian sum of u_n (G_Trapezoid!'s du(u_n)).  du = a * lsum:
+//   Euler      (u_n + Δt du(w)) - w                      tangent  Δt (a lap(v)) - v
+//   Midpoint   (u_n + Δt du(α u_n + (1-α) w)) - w        tangent  Δt (a lap((1-α) v)) - v
+//   Trapezoid  (u_n + (Δt/2) (du(u_n) + du(w))) - w      tangent  (Δt/2) (a lap(v)) - v
 template <int KIND, int MODE>
-__device__ __forceinline__ double point_value(const KArgs& A, double c, double lsum, double uc, double unc, double f0c) {
-    if (KIND == NK_BRATU1D || KIND == NK_BRATU2D) {
+__device__ __forceinline__ double point_value(const KArgs& A, double c, double lsum, double uc, double unc, double f0c,
+                                              double xc, double lsumg) {
+    if constexpr (KIND == NK_BRATU1D || KIND == NK_BRATU2D) {
         if (MODE == MODE_JEXACT) return lsum + A.lam * (exp(uc) * c);  // Enzyme tangent of λ exp(u)
         const double r = lsum + A.lam * exp(c);
         return MODE == MODE_JFD ? ((A.fast & 1) ? (r - f0c) * A.ieps : (r - f0c) / A.eps) : r;
-    } else {  // implicit Euler: res = (u_n + dt f(u)) - u  (implicit.jl:8-13)
-        if (MODE == MODE_JEXACT) return A.dt * (A.a * lsum) - c;
-        const double r = (unc + A.dt * (A.a * lsum)) - c;
+    } else {  // implicit.jl:8-37
+        constexpr int SCH = scheme_of<KIND>();
+        if (MODE == MODE_JEXACT) return (SCH == 2 ? A.dt / 2.0 : A.dt) * (A.a * lsum) - xc;
+        const double r = SCH == 2 ? (unc + (A.dt / 2.0) * (A.a * lsumg + A.a * lsum)) - xc
+                                  : (unc + A.dt * (A.a * lsum)) - xc;
         return MODE == MODE_JFD ? ((A.fast & 1) ? (r - f0c) * A.ieps : (r - f0c) / A.eps) : r;
     }
 }
@@ -284,7 +305,7 @@ __global__ __launch_bounds__(kBlock) void k_st1d(KArgs A0) {
         const double c = fieldval<MODE>(A, i), l = fieldval<MODE>(A, i - 1), r = fieldval<MODE>(A, i + 1);
         const double uc = (MODE == MODE_JEXACT) ? A.u[i] : 0.0;
         const double f0 = (MODE == MODE_JFD) ? A.F0[i] : 0.0;
-        double val = point_value<NK_BRATU1D, MODE>(A, c, lap(c, r, l, A.hx2), uc, 0.0, f0);
+        double val = point_value<NK_BRATU1D, MODE>(A, c, lap(c, r, l, A.hx2), uc, 0.0, f0, c, 0.0);
         const double ax = (EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID) ? A.aux[i]
                           : (EPI == EPI_DOTVS ? A.v[i] / A.hd : 0.0);
         acc = epilogue<EPI>(val, ax, acc);
@@ -368,14 +389,18 @@ __device__ __forceinline__ void store_row(double* __restrict__ p, int64_t o, con
 // edge load is issued by every lane (no divergence): lane 0 reads column x0-1, lane 63 column
 // x0+VEC, the others re-read their own x0 (a cache-hot dummy).  No arithmetic touches the loaded
 // registers until the next iteration, so the compiler's s_waitcnt can leave them in flight.
+// Periodic kernels (PER) carry a second edge slot: *e = the left edge, *e2 = the right edge (with
+// the x-wrap one lane can need both); G = the row of u_n is loaded as well (G_Midpoint! mixes it
+// into the stencil field, G_Trapezoid! takes its Laplacian).
 template <int MODE, int VEC>
 struct RawRow {
-    double a[VEC], ae;  // u (RES, JFD) or v (JEXACT)
-    double b[VEC], be;  // v (JFD)
+    double a[VEC], ae, ae2;  // u (RES, JFD) or v (JEXACT)
+    double b[VEC], be, be2;  // v (JFD)
+    double g[VEC], ge, ge2;  // u_n (G)
 };
 
-template <int MODE, int VEC, bool EDGE = true>
-__device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o, int64_t oe) {
+template <int MODE, int VEC, bool EDGE = true, bool G = false, bool PER = false>
+__device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o, int64_t oe, int64_t oe2 = 0) {
     RawRow<MODE, VEC> r;
     const double* __restrict__ pa = (MODE == MODE_JEXACT) ? A.v : A.u;
     if constexpr (VEC % 2 == 0) {
@@ -389,6 +414,7 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o,
     }
     if constexpr (EDGE) r.ae = pa[oe];
     else r.ae = 0.0;
+    if constexpr (EDGE && PER) r.ae2 = pa[oe2];
     if constexpr (MODE == MODE_JFD) {
         if constexpr (VEC % 2 == 0) {
 #pragma unroll
@@ -401,53 +427,147 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o,
         }
         if constexpr (EDGE) r.be = A.v[oe];
         else r.be = 0.0;
+        if constexpr (EDGE && PER) r.be2 = A.v[oe2];
+    }
+    if constexpr (G) {
+        if constexpr (VEC % 2 == 0) {
+#pragma unroll
+            for (int h = 0; h < VEC; h += 2) {
+                const double2 q = *reinterpret_cast<const double2*>(A.un + o + h);
+                r.g[h] = q.x; r.g[h + 1] = q.y;
+            }
+        } else {
+            r.g[0] = A.un[o];
+        }
+        if constexpr (EDGE) r.ge = A.un[oe];
+        else r.ge = 0.0;
+        if constexpr (EDGE && PER) r.ge2 = A.un[oe2];
     }
     return r;
 }
 
-// cooked stencil field of a row: centres, the lane's edge value, and (fused normalisation) v / h
+// cooked stencil field of a row: centres, the lane's edge value(s), and (fused normalisation) v / h
 template <int VEC>
 struct Field {
-    double c[VEC], e;
-    double vn[VEC];
+    double c[VEC], e, e2;    // the stencil field (G_Midpoint!: α u_n + (1-α) w); edges (e2: PER right edge)
+    double vn[VEC];          // v / h (the stored basis vector)
+    double x[VEC];           // w = u (+ eps v) or v before the midpoint mixing: the "- u" term
+    double g[VEC], ge, ge2;  // u_n (G)
 };
 
-template <int MODE, int VEC>
-__device__ __forceinline__ Field<VEC> cook(const KArgs& A, const RawRow<MODE, VEC>& r, bool act, bool edge_ok) {
+struct WV {
+    double w, v;  // the stencil input w = u (+ eps v) or v, and v / h
+};
+template <int MODE>
+__device__ __forceinline__ WV cook_w(const KArgs& A, double ra, double rb, bool div) {
+    WV r;
+    if constexpr (MODE == MODE_RES) {
+        r.v = 0.0;
+        r.w = ra;
+    } else if constexpr (MODE == MODE_JEXACT) {
+        r.v = div ? ra / A.hd : ra;
+        r.w = r.v;
+    } else {
+        r.v = div ? rb / A.hd : rb;
+        r.w = ra + A.eps * r.v;  // w = u + eps v
+    }
+    return r;
+}
+
+template <int MODE, int SCH>
+__device__ __forceinline__ double mix(const KArgs& A, double w, double g) {
+    if constexpr (SCH != 1) return w;
+    // G_Midpoint!: uuₙ .= α .* uₙ .+ (1 - α) .* u; its tangent (u_n has a zero shadow) is (1 - α) v
+    else if constexpr (MODE == MODE_JEXACT) return (1.0 - A.alpha) * w;
+    else return A.alpha * g + (1.0 - A.alpha) * w;
+}
+
+template <int MODE, int VEC, int SCH = 0, bool G = false, bool PER = false>
+__device__ __forceinline__ Field<VEC> cook(const KArgs& A, const RawRow<MODE, VEC>& r, bool act, bool edge_ok,
+                                           bool edge_ok2 = false) {
     Field<VEC> f;
     const bool div = A.vdiv != nullptr;
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
-        double v;
-        if constexpr (MODE == MODE_RES) {
-            f.c[k] = r.a[k];
-            v = 0.0;
-        } else if constexpr (MODE == MODE_JEXACT) {
-            v = div ? r.a[k] / A.hd : r.a[k];
-            f.c[k] = v;
-        } else {
-            v = div ? r.b[k] / A.hd : r.b[k];
-            f.c[k] = r.a[k] + A.eps * v;  // w = u + eps v
+        const WV q = cook_w<MODE>(A, r.a[k], MODE == MODE_JFD ? r.b[k] : 0.0, div);
+        const double w = q.w;
+        f.vn[k] = q.v;
+        f.x[k] = w;
+        f.c[k] = mix<MODE, SCH>(A, w, G ? r.g[k] : 0.0);
+        if constexpr (G) f.g[k] = r.g[k];
+        if (!act) {  // lanes past the row end act as the zero boundary for their neighbour
+            f.c[k] = 0.0;
+            if constexpr (G) f.g[k] = 0.0;
         }
-        f.vn[k] = v;
-        if (!act) f.c[k] = 0.0;  // lanes past the row end act as the zero boundary for their neighbour
     }
-    double e;
-    if constexpr (MODE == MODE_RES) e = r.ae;
-    else if constexpr (MODE == MODE_JEXACT) e = div ? r.ae / A.hd : r.ae;
-    else e = r.ae + A.eps * (div ? r.be / A.hd : r.be);
+    const double e = mix<MODE, SCH>(A, cook_w<MODE>(A, r.ae, MODE == MODE_JFD ? r.be : 0.0, div).w, G ? r.ge : 0.0);
     f.e = edge_ok ? e : 0.0;
+    if constexpr (G) f.ge = edge_ok ? r.ge : 0.0;
+    if constexpr (PER) {
+        const double e2 = mix<MODE, SCH>(A, cook_w<MODE>(A, r.ae2, MODE == MODE_JFD ? r.be2 : 0.0, div).w, G ? r.ge2 : 0.0);
+        f.e2 = edge_ok2 ? e2 : 0.0;
+        if constexpr (G) f.ge2 = edge_ok2 ? r.ge2 : 0.0;
+    }
     return f;
+}
+
+// x-edge geometry of one lane.  Without PER: lane 0 reads column x0-1, lane 63 column x0+VEC (zero
+// beyond the grid).  With PER (bc_periodic!): lane 0 reads its left neighbour into e (column nx-1 at
+// x0 = 0), and lane 63 -- or the lane holding the last column -- its right neighbour into e2
+// (column 0 after the last column).
+struct XEdge {
+    int64_t de, de2;
+    bool ok, ok2, rwrap;
+};
+template <int VEC, bool PER>
+__device__ __forceinline__ XEdge x_edge(int lane, bool act, int64_t x0, int64_t nx) {
+    XEdge x{};
+    if constexpr (!PER) {
+        const bool left_ok = lane == 0 && act && x0 >= 1;
+        const bool right_ok = lane == 63 && act && x0 + VEC < nx;
+        x.de = left_ok ? -1 : (right_ok ? VEC : 0);  // edge element offset (0: dummy)
+        x.ok = left_ok || right_ok;
+        x.de2 = 0;
+        x.ok2 = false;
+        x.rwrap = false;
+    } else {
+        x.ok = lane == 0 && act;
+        x.de = x.ok ? (x0 >= 1 ? -1 : nx - 1) : 0;
+        x.rwrap = act && x0 + VEC == nx;
+        x.ok2 = act && ((lane == 63 && x0 + VEC < nx) || x.rwrap);
+        x.de2 = x.ok2 ? (x.rwrap ? -x0 : VEC) : 0;
+    }
+    return x;
+}
+
+// west / east neighbours of the VEC points of a lane: lane shuffles, the wave-edge lanes' edge values
+struct LR {
+    double l, r;
+};
+template <bool PER>
+__device__ __forceinline__ LR x_nbrs(double cfirst, double clast, double e, double e2, int lane, bool rwrap) {
+    LR o;
+    o.l = __shfl_up(clast, 1, 64);
+    o.r = __shfl_down(cfirst, 1, 64);
+    if (lane == 0) o.l = e;
+    if constexpr (PER) {
+        if (lane == 63 || rwrap) o.r = e2;
+    } else {
+        if (lane == 63) o.r = e;
+    }
+    return o;
 }
 
 // Block = 256 threads x VEC columns (one row segment), marching A.rows rows in y.  Pipeline: at
 // iteration j the raw loads of row j+2 and the centre operands of row j+1 are issued, row j+1's
 // raw data (issued one iteration earlier) is cooked, and row j is computed from registers.
-template <int KIND, int MODE, int EPI, int VEC>
+template <int KIND, int MODE, int EPI, int VEC, bool PER = false>
 __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     __shared__ double sh[8];
     KArgs A = A0;
     A.hd = A.vdiv ? *A.vdiv : 1.0;
+    constexpr int SCH = scheme_of<KIND>();
+    constexpr bool kG = SCH != 0 && MODE != MODE_JEXACT;  // u_n rows with the stencil field
     const int lane = threadIdx.x & 63;
     const int nb = gridDim.x, b = blockIdx.x;
     const int t = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;  // XCD-contiguous tile bands
@@ -456,10 +576,9 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     const int64_t x0 = (int64_t)tx * (kBlock * VEC) + (int64_t)threadIdx.x * VEC;
     const bool act = x0 < nx;
     const int64_t xc = act ? x0 : 0;  // clamped column: every load stays inside the allocation
-    const bool left_ok = lane == 0 && act && x0 >= 1;
-    const bool right_ok = lane == 63 && act && x0 + VEC < nx;
-    const int64_t de = left_ok ? -1 : (right_ok ? VEC : 0);  // edge element offset (0: dummy)
-    const bool edge_ok = left_ok || right_ok;
+    const XEdge xe = x_edge<VEC, PER>(lane, act, x0, nx);
+    const int64_t de = xe.de, de2 = xe.de2;
+    const bool edge_ok = xe.ok, edge_ok2 = xe.ok2;
     const int64_t y0 = (int64_t)ty * A.rows;
     const int64_t y1 = y0 + A.rows < ny ? y0 + A.rows : ny;
     constexpr bool kU = MODE == MODE_JEXACT && KIND == NK_BRATU2D;
@@ -470,9 +589,14 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     double acc = 0.0;
     if (y0 < ny) {
         // rows y0-1 (ghost plane when y0 = 0) and y0 cooked up front; row y0+1 raw in flight
-        Field<VEC> fm = cook<MODE, VEC>(A, load_raw<MODE, VEC>(A, (y0 - 1) * nx + xc, (y0 - 1) * nx + xc + de), act, false);
-        Field<VEC> fc = cook<MODE, VEC>(A, load_raw<MODE, VEC>(A, y0 * nx + xc, y0 * nx + xc + de), act, edge_ok);
-        RawRow<MODE, VEC> rp = load_raw<MODE, VEC>(A, (y0 + 1) * nx + xc, (y0 + 1) * nx + xc + de);
+        Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(
+            A, load_raw<MODE, VEC, true, kG, PER>(A, (y0 - 1) * nx + xc, (y0 - 1) * nx + xc + de, (y0 - 1) * nx + xc + de2),
+            act, false, false);
+        Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(
+            A, load_raw<MODE, VEC, true, kG, PER>(A, y0 * nx + xc, y0 * nx + xc + de, y0 * nx + xc + de2), act, edge_ok,
+            edge_ok2);
+        RawRow<MODE, VEC> rp =
+            load_raw<MODE, VEC, true, kG, PER>(A, (y0 + 1) * nx + xc, (y0 + 1) * nx + xc + de, (y0 + 1) * nx + xc + de2);
         Row<VEC> uc{}, unc{}, f0c{}, ax{};
         {
             const int64_t o = y0 * nx + xc;
@@ -486,7 +610,7 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
             // ---- issue: raw row j+2 (rows up to ny are the ghost plane; y1 <= ny keeps j+2 <= ny+1
             //      in range only when j+1 < y1, so clamp to row j+1 otherwise)
             const int64_t o2 = (j + 1 < y1) ? o + 2 * nx : o + nx;
-            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC>(A, o2, o2 + de);
+            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2);
             Row<VEC> ucn{}, uncn{}, f0cn{}, axn{};
             const int64_t o1 = (j + 1 < y1) ? o + nx : o;
             if constexpr (kU) ucn = data_row<VEC>(A.u, o1, true);
@@ -494,12 +618,16 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
             if constexpr (kF0) f0cn = data_row<VEC>(A.F0, o1, true);
             if constexpr (kAx) axn = data_row<VEC>(A.aux, o1, true);
             // ---- cook row j+1 (its loads were issued one iteration ago)
-            const Field<VEC> fp = cook<MODE, VEC>(A, rp, act, edge_ok && j + 1 < ny);
+            const Field<VEC> fp = cook<MODE, VEC, SCH, kG, PER>(A, rp, act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
             // ---- compute row j from registers
-            double lft = __shfl_up(fc.c[VEC - 1], 1, 64);
-            double rgt = __shfl_down(fc.c[0], 1, 64);
-            if (lane == 0) lft = fc.e;
-            if (lane == 63) rgt = fc.e;
+            const LR xn = x_nbrs<PER>(fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
+            const double lft = xn.l, rgt = xn.r;
+            double glft = 0.0, grgt = 0.0;
+            if constexpr (SCH == 2 && kG) {
+                const LR gn = x_nbrs<PER>(fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
+                glft = gn.l;
+                grgt = gn.r;
+            }
             if (act) {
                 Row<VEC> val;
 #pragma unroll
@@ -508,7 +636,14 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
                     const double e = (k == VEC - 1) ? rgt : fc.c[k == VEC - 1 ? k : k + 1];
                     const double c = fc.c[k];
                     const double lsum = lapk(A, c, e, w, A.hx2, A.ihx2) + lapk(A, c, fp.c[k], fm.c[k], A.hy2, A.ihy2);
-                    double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unc.v[k], f0c.v[k]);
+                    double lsumg = 0.0;
+                    if constexpr (SCH == 2 && kG) {
+                        const double gw = (k == 0) ? glft : fc.g[k == 0 ? 0 : k - 1];
+                        const double ge = (k == VEC - 1) ? grgt : fc.g[k == VEC - 1 ? k : k + 1];
+                        lsumg = lapk(A, fc.g[k], ge, gw, A.hx2, A.ihx2) + lapk(A, fc.g[k], fp.g[k], fm.g[k], A.hy2, A.ihy2);
+                    }
+                    const double unk = kG ? fc.g[k] : unc.v[k];
+                    double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unk, f0c.v[k], SCH == 1 ? fc.x[k] : c, lsumg);
                     acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[k] : ax.v[k], acc);
                     val.v[k] = r;
                 }
@@ -537,12 +672,15 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
 // the 2D kernel: at iteration k the raw loads of the centre row of plane k+2 and of the y-
 // neighbour rows of plane k+1 are issued, plane k+1's centre row and plane k's y-neighbours
 // (issued one iteration earlier) are cooked, and plane k is computed from registers.  The y-
-// neighbour rows are mostly L2 hits (the adjacent waves of the block stream them).
-template <int KIND, int MODE, int EPI, int VEC>
+// neighbour rows are mostly L2 hits (the adjacent waves of the block stream them).  PER: the
+// y-neighbours of rows 0 and ny-1 wrap (bc_periodic!), x as in the 2D kernel.
+template <int KIND, int MODE, int EPI, int VEC, bool PER = false>
 __global__ __launch_bounds__(kBlock) void k_st3d(KArgs A0) {
     __shared__ double sh[8];
     KArgs A = A0;
     A.hd = A.vdiv ? *A.vdiv : 1.0;
+    constexpr int SCH = scheme_of<KIND>();
+    constexpr bool kG = SCH != 0 && MODE != MODE_JEXACT;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const int nb = gridDim.x, b = blockIdx.x;
@@ -555,26 +693,37 @@ __global__ __launch_bounds__(kBlock) void k_st3d(KArgs A0) {
     const int64_t j = (int64_t)ty * 4 + wv;
     const bool act = x0 < nx && j < ny;
     const int64_t oj = (act ? j * nx + x0 : 0);  // clamped: every load stays inside the allocation
-    const bool has_n = act && j + 1 < ny, has_s = act && j >= 1;
-    const int64_t dn = has_n ? nx : 0, ds = has_s ? -nx : 0;  // 0: dummy (own row), cooked to zero
-    const bool left_ok = lane == 0 && act && x0 >= 1;
-    const bool right_ok = lane == 63 && act && x0 + VEC < nx;
-    const int64_t de = left_ok ? -1 : (right_ok ? VEC : 0);
-    const bool edge_ok = left_ok || right_ok;
+    bool has_n, has_s;
+    int64_t dn, ds;  // 0: dummy (own row), cooked to zero
+    if constexpr (PER) {
+        has_n = act;
+        has_s = act;
+        dn = !act ? 0 : (j + 1 < ny ? nx : -(ny - 1) * nx);
+        ds = !act ? 0 : (j >= 1 ? -nx : (ny - 1) * nx);
+    } else {
+        has_n = act && j + 1 < ny;
+        has_s = act && j >= 1;
+        dn = has_n ? nx : 0;
+        ds = has_s ? -nx : 0;
+    }
+    const XEdge xe = x_edge<VEC, PER>(lane, act, x0, nx);
+    const int64_t de = xe.de, de2 = xe.de2;
+    const bool edge_ok = xe.ok, edge_ok2 = xe.ok2;
     const int64_t z0 = (int64_t)tz * A.rows;
     const int64_t z1 = z0 + A.rows < nz ? z0 + A.rows : nz;
-    constexpr bool kUn = MODE != MODE_JEXACT;
+    constexpr bool kUn = SCH == 0 && MODE != MODE_JEXACT;
     constexpr bool kF0 = MODE == MODE_JFD;
     constexpr bool kAx = EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID;
     constexpr bool vout = MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS);  // fused kdivcopy!: V_k stored
     double acc = 0.0;
     if (z0 < nz) {
         const int64_t o0 = z0 * pl + oj;
-        Field<VEC> fm = cook<MODE, VEC>(A, load_raw<MODE, VEC, false>(A, o0 - pl, 0), act, false);  // plane -1: ghost
-        Field<VEC> fc = cook<MODE, VEC>(A, load_raw<MODE, VEC>(A, o0, o0 + de), act, edge_ok);
-        RawRow<MODE, VEC> rp = load_raw<MODE, VEC>(A, o0 + pl, o0 + pl + de);  // plane nz: ghost
-        RawRow<MODE, VEC> rn = load_raw<MODE, VEC, false>(A, o0 + dn, 0);
-        RawRow<MODE, VEC> rs = load_raw<MODE, VEC, false>(A, o0 + ds, 0);
+        Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(A, load_raw<MODE, VEC, false, kG, PER>(A, o0 - pl, 0), act, false);  // plane -1: ghost
+        Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, load_raw<MODE, VEC, true, kG, PER>(A, o0, o0 + de, o0 + de2), act,
+                                                      edge_ok, edge_ok2);
+        RawRow<MODE, VEC> rp = load_raw<MODE, VEC, true, kG, PER>(A, o0 + pl, o0 + pl + de, o0 + pl + de2);  // plane nz: ghost
+        RawRow<MODE, VEC> rn = load_raw<MODE, VEC, false, kG, PER>(A, o0 + dn, 0);
+        RawRow<MODE, VEC> rs = load_raw<MODE, VEC, false, kG, PER>(A, o0 + ds, 0);
         Row<VEC> unc{}, f0c{}, ax{};
         if constexpr (kUn) unc = data_row<VEC>(A.un, o0, true);
         if constexpr (kF0) f0c = data_row<VEC>(A.F0, o0, true);
@@ -585,22 +734,26 @@ __global__ __launch_bounds__(kBlock) void k_st3d(KArgs A0) {
             const bool more = k + 1 < z1;
             const int64_t o2 = more ? o + 2 * pl : o + pl;
             const int64_t o1 = more ? o + pl : o;
-            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC>(A, o2, o2 + de);
-            const RawRow<MODE, VEC> rnn = load_raw<MODE, VEC, false>(A, o1 + dn, 0);
-            const RawRow<MODE, VEC> rss = load_raw<MODE, VEC, false>(A, o1 + ds, 0);
+            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2);
+            const RawRow<MODE, VEC> rnn = load_raw<MODE, VEC, false, kG, PER>(A, o1 + dn, 0);
+            const RawRow<MODE, VEC> rss = load_raw<MODE, VEC, false, kG, PER>(A, o1 + ds, 0);
             Row<VEC> uncn{}, f0cn{}, axn{};
             if constexpr (kUn) uncn = data_row<VEC>(A.un, o1, true);
             if constexpr (kF0) f0cn = data_row<VEC>(A.F0, o1, true);
             if constexpr (kAx) axn = data_row<VEC>(A.aux, o1, true);
             // ---- cook what was issued one iteration ago
-            const Field<VEC> fp = cook<MODE, VEC>(A, rp, act, edge_ok);
-            const Field<VEC> fn = cook<MODE, VEC>(A, rn, has_n, false);
-            const Field<VEC> fs = cook<MODE, VEC>(A, rs, has_s, false);
+            const Field<VEC> fp = cook<MODE, VEC, SCH, kG, PER>(A, rp, act, edge_ok, edge_ok2);
+            const Field<VEC> fn = cook<MODE, VEC, SCH, kG, PER>(A, rn, has_n, false);
+            const Field<VEC> fs = cook<MODE, VEC, SCH, kG, PER>(A, rs, has_s, false);
             // ---- compute plane k
-            double lft = __shfl_up(fc.c[VEC - 1], 1, 64);
-            double rgt = __shfl_down(fc.c[0], 1, 64);
-            if (lane == 0) lft = fc.e;
-            if (lane == 63) rgt = fc.e;
+            const LR xn = x_nbrs<PER>(fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
+            const double lft = xn.l, rgt = xn.r;
+            double glft = 0.0, grgt = 0.0;
+            if constexpr (SCH == 2 && kG) {
+                const LR gn = x_nbrs<PER>(fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
+                glft = gn.l;
+                grgt = gn.r;
+            }
             if (act) {
                 Row<VEC> val;
 #pragma unroll
@@ -610,7 +763,16 @@ __global__ __launch_bounds__(kBlock) void k_st3d(KArgs A0) {
                     const double c = fc.c[q];
                     const double lsum = (lapk(A, c, e, w, A.hx2, A.ihx2) + lapk(A, c, fn.c[q], fs.c[q], A.hy2, A.ihy2)) +
                                         lapk(A, c, fp.c[q], fm.c[q], A.hz2, A.ihz2);
-                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unc.v[q], f0c.v[q]);
+                    double lsumg = 0.0;
+                    if constexpr (SCH == 2 && kG) {
+                        const double g = fc.g[q];
+                        const double gw = (q == 0) ? glft : fc.g[q == 0 ? 0 : q - 1];
+                        const double ge = (q == VEC - 1) ? grgt : fc.g[q == VEC - 1 ? q : q + 1];
+                        lsumg = (lapk(A, g, ge, gw, A.hx2, A.ihx2) + lapk(A, g, fn.g[q], fs.g[q], A.hy2, A.ihy2)) +
+                                lapk(A, g, fp.g[q], fm.g[q], A.hz2, A.ihz2);
+                    }
+                    const double unq = kG ? fc.g[q] : unc.v[q];
+                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0c.v[q], SCH == 1 ? fc.x[q] : c, lsumg);
                     acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[q] : ax.v[q], acc);
                     val.v[q] = r;
                 }
@@ -1053,48 +1215,64 @@ template <int KIND, int DIM>
 __global__ __launch_bounds__(kBlock) void k_jdiag(KArgs A, double* __restrict__ out, int recip) {
     const int64_t n = A.nx * A.ny * A.nz;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-        double lsum = lapk(A, 1.0, 0.0, 0.0, A.hx2, A.ihx2);
-        if (DIM >= 2) lsum = lsum + lapk(A, 1.0, 0.0, 0.0, A.hy2, A.ihy2);
-        if (DIM == 3) lsum = lsum + lapk(A, 1.0, 0.0, 0.0, A.hz2, A.ihz2);
+        // G_Midpoint!'s stencil field is (1 - α) v: its centre (1 - α), the "- v" term 1
+        const double c = scheme_of<KIND>() == 1 ? (1.0 - A.alpha) * 1.0 : 1.0;
+        double lsum = lapk(A, c, 0.0, 0.0, A.hx2, A.ihx2);
+        if (DIM >= 2) lsum = lsum + lapk(A, c, 0.0, 0.0, A.hy2, A.ihy2);
+        if (DIM == 3) lsum = lsum + lapk(A, c, 0.0, 0.0, A.hz2, A.ihz2);
         const double uc = (KIND == NK_BRATU1D || KIND == NK_BRATU2D) ? A.u[i] : 0.0;
-        const double d = point_value<KIND, MODE_JEXACT>(A, 1.0, lsum, uc, 0.0, 0.0);
+        const double d = point_value<KIND, MODE_JEXACT>(A, c, lsum, uc, 0.0, 0.0, 1.0, 0.0);
         out[i] = recip ? 1.0 / d : d;
     }
 }
 
 // ------------------------------------------------------------------------------ stencil dispatch
 template <int KIND, int MODE, int EPI>
-void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s) {
+void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
+    constexpr bool k2d = KIND == NK_BRATU2D || KIND == NK_HEAT2D_EULER || KIND == NK_HEAT2D_MIDPOINT ||
+                         KIND == NK_HEAT2D_TRAPEZOID;
     if constexpr (KIND == NK_BRATU1D) {
         hipLaunchKernelGGL((k_st1d<MODE, EPI>), dim3(grid), dim3(kBlock), 0, s, A);
-    } else if constexpr (KIND == NK_BRATU2D || KIND == NK_HEAT2D_EULER) {
+    } else if constexpr (k2d) {
+        if constexpr (heat_kind<KIND>()) {  // bc_periodic! instantiations: heat only, VEC <= 2
+            if (per) {
+                if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2, true>), dim3(grid), dim3(kBlock), 0, s, A);
+                else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1, true>), dim3(grid), dim3(kBlock), 0, s, A);
+                return;
+            }
+        }
         if (vec == 4) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 4>), dim3(grid), dim3(kBlock), 0, s, A);
         else if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
         else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1>), dim3(grid), dim3(kBlock), 0, s, A);
     } else {
+        if (per) {
+            if (vec == 2) hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 2, true>), dim3(grid), dim3(kBlock), 0, s, A);
+            else hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 1, true>), dim3(grid), dim3(kBlock), 0, s, A);
+            return;
+        }
         if (vec == 2) hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
         else hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 1>), dim3(grid), dim3(kBlock), 0, s, A);
     }
 }
 
 template <int KIND, int MODE>
-void go_stencil_epi(const KArgs& A, int epi, int vec, int grid, hipStream_t s) {
+void go_stencil_epi(const KArgs& A, int epi, int vec, int grid, hipStream_t s, bool per) {
     switch (epi) {
-    case EPI_NONE: go_stencil<KIND, MODE, EPI_NONE>(A, vec, grid, s); break;
-    case EPI_SUMSQ: go_stencil<KIND, MODE, EPI_SUMSQ>(A, vec, grid, s); break;
-    case EPI_DOT: go_stencil<KIND, MODE, EPI_DOT>(A, vec, grid, s); break;
-    case EPI_DOTV: go_stencil<KIND, MODE, EPI_DOTV>(A, vec, grid, s); break;
-    case EPI_DOTVS: go_stencil<KIND, MODE, EPI_DOTVS>(A, vec, grid, s); break;
-    default: go_stencil<KIND, MODE, EPI_RESID>(A, vec, grid, s); break;
+    case EPI_NONE: go_stencil<KIND, MODE, EPI_NONE>(A, vec, grid, s, per); break;
+    case EPI_SUMSQ: go_stencil<KIND, MODE, EPI_SUMSQ>(A, vec, grid, s, per); break;
+    case EPI_DOT: go_stencil<KIND, MODE, EPI_DOT>(A, vec, grid, s, per); break;
+    case EPI_DOTV: go_stencil<KIND, MODE, EPI_DOTV>(A, vec, grid, s, per); break;
+    case EPI_DOTVS: go_stencil<KIND, MODE, EPI_DOTVS>(A, vec, grid, s, per); break;
+    default: go_stencil<KIND, MODE, EPI_RESID>(A, vec, grid, s, per); break;
     }
 }
 
 template <int KIND>
-void go_stencil_mode(const KArgs& A, int mode, int epi, int vec, int grid, hipStream_t s) {
+void go_stencil_mode(const KArgs& A, int mode, int epi, int vec, int grid, hipStream_t s, bool per) {
     switch (mode) {
-    case MODE_RES: go_stencil_epi<KIND, MODE_RES>(A, epi, vec, grid, s); break;
-    case MODE_JEXACT: go_stencil_epi<KIND, MODE_JEXACT>(A, epi, vec, grid, s); break;
-    default: go_stencil_epi<KIND, MODE_JFD>(A, epi, vec, grid, s); break;
+    case MODE_RES: go_stencil_epi<KIND, MODE_RES>(A, epi, vec, grid, s, per); break;
+    case MODE_JEXACT: go_stencil_epi<KIND, MODE_JEXACT>(A, epi, vec, grid, s, per); break;
+    default: go_stencil_epi<KIND, MODE_JFD>(A, epi, vec, grid, s, per); break;
     }
 }
 
@@ -1158,32 +1336,34 @@ __device__ __forceinline__ uint64_t* halo_inbox(uint64_t* base, int par, int sid
 // neighbour's inbox (system-scope stores), drains, raises its epoch flag there, then waits for the
 // neighbours' block b flags in my region and copies their chunks into my ghost planes.  Inboxes
 // alternate by epoch parity: epoch e's push can only start after the neighbour finished epoch e-2.
+// ring = 1 (bc_periodic! along the slab axis): rank 0's lower neighbour is rank nranks-1 and vice versa.
 __global__ __launch_bounds__(kBlock) void k_halo_ipc(double* __restrict__ v, int64_t plane, int64_t nplanes,
-                                                    uint64_t epoch, int64_t cap) {
+                                                    uint64_t epoch, int64_t cap, int ring) {
     __shared__ int ready;
     const int b = blockIdx.x, rank = g_mb.rank, nr = g_mb.nranks;
-    const bool lo = rank > 0, hi = rank + 1 < nr;
+    const bool lo = rank > 0 || ring, hi = rank + 1 < nr || ring;
+    const int rlo = rank > 0 ? rank - 1 : nr - 1, rhi = rank + 1 < nr ? rank + 1 : 0;
     const int par = (int)(epoch & 1);
     const int64_t per = (plane + gridDim.x - 1) / gridDim.x;
     const int64_t c0 = (int64_t)b * per, c1 = c0 + per < plane ? c0 + per : plane;
     const double* first = v;
     const double* last = v + (nplanes - 1) * plane;
     if (lo) {  // my first interior plane -> the lower rank's "from upper" inbox
-        uint64_t* dst = halo_inbox(g_mb.peers[rank - 1], par, 1, cap);
+        uint64_t* dst = halo_inbox(g_mb.peers[rlo], par, 1, cap);
         for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
             __hip_atomic_store(dst + i, (uint64_t)__double_as_longlong(first[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (hi) {  // my last interior plane -> the upper rank's "from lower" inbox
-        uint64_t* dst = halo_inbox(g_mb.peers[rank + 1], par, 0, cap);
+        uint64_t* dst = halo_inbox(g_mb.peers[rhi], par, 0, cap);
         for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
             __hip_atomic_store(dst + i, (uint64_t)__double_as_longlong(last[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every thread drains its stores before the flag
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (lo) __hip_atomic_store(halo_flags(g_mb.peers[rank - 1]) + (par * 2 + 1) * kHaloBlocks + b, epoch,
+        if (lo) __hip_atomic_store(halo_flags(g_mb.peers[rlo]) + (par * 2 + 1) * kHaloBlocks + b, epoch,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (hi) __hip_atomic_store(halo_flags(g_mb.peers[rank + 1]) + (par * 2 + 0) * kHaloBlocks + b, epoch,
+        if (hi) __hip_atomic_store(halo_flags(g_mb.peers[rhi]) + (par * 2 + 0) * kHaloBlocks + b, epoch,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         ready = 1;
         for (int side = 0; side < 2; ++side) {
@@ -1214,17 +1394,34 @@ __global__ __launch_bounds__(kBlock) void k_halo_ipc(double* __restrict__ v, int
                 __longlong_as_double((long long)__hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     }
 }
+
+// bc_periodic! along the slab axis of a lone slab: ghost plane -1 <- the last interior plane,
+// ghost plane nplanes <- the first (heat_2D.jl:20-21 / 23-24)
+__global__ __launch_bounds__(kBlock) void k_periodic_fill(double* __restrict__ v, int64_t plane, int64_t nplanes) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < plane; i += (int64_t)gridDim.x * kBlock) {
+        v[i - plane] = v[(nplanes - 1) * plane + i];
+        v[nplanes * plane + i] = v[i];
+    }
+}
 }  // namespace
 
-int launch_halo_ipc(nk_ctx* c, double* v, int64_t plane, int64_t nplanes) {
+int launch_halo_ipc(nk_ctx* c, double* v, int64_t plane, int64_t nplanes, bool ring) {
     if (c->nranks < 2) return NK_OK;
     const uint64_t epoch = ++c->halo_epoch;
     int nb = (int)((plane + 1023) / 1024);
     if (nb > kHaloBlocks) nb = kHaloBlocks;
     if (nb < 1) nb = 1;
-    const int nbrs = (c->rank > 0) + (c->rank + 1 < c->nranks);
+    const int nbrs = ring ? 2 : (c->rank > 0) + (c->rank + 1 < c->nranks);
     return launch(c, "halo", 16.0 * plane * nbrs, [&] {
-        hipLaunchKernelGGL(k_halo_ipc, dim3(nb), dim3(kBlock), 0, c->stream, v, plane, nplanes, epoch, c->halo_cap);
+        hipLaunchKernelGGL(k_halo_ipc, dim3(nb), dim3(kBlock), 0, c->stream, v, plane, nplanes, epoch, c->halo_cap,
+                           ring ? 1 : 0);
+    });
+}
+
+int launch_periodic_fill(nk_ctx* c, double* v, int64_t plane, int64_t nplanes) {
+    const int g = (int)std::min<int64_t>((plane + kBlock - 1) / kBlock, 1024);
+    return launch(c, "periodic_fill", 16.0 * plane, [&] {
+        hipLaunchKernelGGL(k_periodic_fill, dim3(g), dim3(kBlock), 0, c->stream, v, plane, nplanes);
     });
 }
 
@@ -1274,13 +1471,15 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     A.vdiv = in.vdiv;
     A.vout = in.vout;
     A.ihx2 = 1.0 / A.hx2; A.ihy2 = 1.0 / A.hy2; A.ihz2 = 1.0 / A.hz2; A.ieps = in.eps != 0.0 ? 1.0 / in.eps : 0.0;
+    A.alpha = p->alpha;
+    const bool per = p->bc == NK_BC_PERIODIC;
     int vec = 1, grid = 1;
     if (g.dim == 1) {
         grid = (int)((p->nx + kBlock - 1) / kBlock);
     } else if (g.dim == 2) {
         static const int vec_pref = env_int("NK_ST_VEC", 2);
         vec = (p->nx % 2 == 0) ? 2 : 1;
-        if (((fast & 4) || vec_pref == 4) && p->nx % 4 == 0) vec = 4;
+        if (((fast & 4) || vec_pref == 4) && p->nx % 4 == 0 && !per) vec = 4;
         A.tiles_x = (int)((p->nx + kBlock * vec - 1) / (kBlock * vec));
         static const int target = env_int("NK_ST_BLOCKS", 2048);
         int64_t rows = (p->ny * A.tiles_x + target - 1) / target;
@@ -1309,7 +1508,7 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         A.part = red_out(c, grid, red, &A.fin);
     }
     // algorithmic (compulsory) bytes per launch
-    const bool heat = p->kind == NK_HEAT2D_EULER || p->kind == NK_HEAT3D_EULER;
+    const bool heat = nk_is_heat(p->kind);
     int words = 1;  // out
     if (in.mode == MODE_RES) words += 1 + (heat ? 1 : 0);
     else if (in.mode == MODE_JEXACT) words += 1 + (heat ? 0 : 1);
@@ -1333,10 +1532,14 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     const char* kname = epi == EPI_DOTV ? fused_names[mode] : (epi == EPI_DOTVS ? v1_names[mode] : names[mode][epi]);
     return launch(c, kname, bytes, [&] {
         switch (kind) {
-        case NK_BRATU1D: go_stencil_mode<NK_BRATU1D>(A, mode, epi, vec, grid, s); break;
-        case NK_BRATU2D: go_stencil_mode<NK_BRATU2D>(A, mode, epi, vec, grid, s); break;
-        case NK_HEAT2D_EULER: go_stencil_mode<NK_HEAT2D_EULER>(A, mode, epi, vec, grid, s); break;
-        default: go_stencil_mode<NK_HEAT3D_EULER>(A, mode, epi, vec, grid, s); break;
+        case NK_BRATU1D: go_stencil_mode<NK_BRATU1D>(A, mode, epi, vec, grid, s, false); break;
+        case NK_BRATU2D: go_stencil_mode<NK_BRATU2D>(A, mode, epi, vec, grid, s, false); break;
+        case NK_HEAT2D_EULER: go_stencil_mode<NK_HEAT2D_EULER>(A, mode, epi, vec, grid, s, per); break;
+        case NK_HEAT2D_MIDPOINT: go_stencil_mode<NK_HEAT2D_MIDPOINT>(A, mode, epi, vec, grid, s, per); break;
+        case NK_HEAT2D_TRAPEZOID: go_stencil_mode<NK_HEAT2D_TRAPEZOID>(A, mode, epi, vec, grid, s, per); break;
+        case NK_HEAT3D_MIDPOINT: go_stencil_mode<NK_HEAT3D_MIDPOINT>(A, mode, epi, vec, grid, s, per); break;
+        case NK_HEAT3D_TRAPEZOID: go_stencil_mode<NK_HEAT3D_TRAPEZOID>(A, mode, epi, vec, grid, s, per); break;
+        default: go_stencil_mode<NK_HEAT3D_EULER>(A, mode, epi, vec, grid, s, per); break;
         }
     });
 }
@@ -1493,17 +1696,23 @@ int launch_jdiag(nk_ctx* c, const nk_problem* p, double* out, const double* u, i
     A.u = u;
     A.nx = p->nx; A.ny = p->ny; A.nz = p->nz;
     A.hx2 = p->hx * p->hx; A.hy2 = p->hy * p->hy; A.hz2 = p->hz * p->hz;
-    A.lam = p->lambda; A.a = p->a; A.dt = p->dt;
+    A.lam = p->lambda; A.a = p->a; A.dt = p->dt; A.alpha = p->alpha;
     const int64_t n = p->nx * p->ny * p->nz;
     const int g = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, 4096);
+#define NK_JDIAG(K, D) hipLaunchKernelGGL((k_jdiag<K, D>), dim3(g), dim3(kBlock), 0, c->stream, A, out, recip)
     return launch(c, "jacobian_diag", 16.0 * n, [&] {
         switch (p->kind) {
-        case NK_BRATU1D: hipLaunchKernelGGL((k_jdiag<NK_BRATU1D, 1>), dim3(g), dim3(kBlock), 0, c->stream, A, out, recip); break;
-        case NK_BRATU2D: hipLaunchKernelGGL((k_jdiag<NK_BRATU2D, 2>), dim3(g), dim3(kBlock), 0, c->stream, A, out, recip); break;
-        case NK_HEAT2D_EULER: hipLaunchKernelGGL((k_jdiag<NK_HEAT2D_EULER, 2>), dim3(g), dim3(kBlock), 0, c->stream, A, out, recip); break;
-        default: hipLaunchKernelGGL((k_jdiag<NK_HEAT3D_EULER, 3>), dim3(g), dim3(kBlock), 0, c->stream, A, out, recip); break;
+        case NK_BRATU1D: NK_JDIAG(NK_BRATU1D, 1); break;
+        case NK_BRATU2D: NK_JDIAG(NK_BRATU2D, 2); break;
+        case NK_HEAT2D_EULER: NK_JDIAG(NK_HEAT2D_EULER, 2); break;
+        case NK_HEAT2D_MIDPOINT: NK_JDIAG(NK_HEAT2D_MIDPOINT, 2); break;
+        case NK_HEAT2D_TRAPEZOID: NK_JDIAG(NK_HEAT2D_TRAPEZOID, 2); break;
+        case NK_HEAT3D_MIDPOINT: NK_JDIAG(NK_HEAT3D_MIDPOINT, 3); break;
+        case NK_HEAT3D_TRAPEZOID: NK_JDIAG(NK_HEAT3D_TRAPEZOID, 3); break;
+        default: NK_JDIAG(NK_HEAT3D_EULER, 3); break;
         }
     });
+#undef NK_JDIAG
 }
 
 int launch_cg_direction(nk_ctx* c, int64_t n, double beta, double* p, const double* r) {

@@ -562,7 +562,8 @@ int nk_krylov_solve(nk_workspace* ws, const nk_problem* p, const double* u, cons
     if (o->jv_mode == NK_JV_FD && !F0) return fail(c, NK_E_ARG, "FD Jv needs F0 = F(u)");
     *st = nk_krylov_stats{};
     Op A{c, p, o->jv_mode, u, F0, 0.0};
-    NK_TRY(halo_exchange(c, p, u));  // u is constant during the solve: one exchange
+    NK_TRY(halo_exchange(c, p, u));  // u (and u_n) are constant during the solve: one exchange
+    NK_TRY(exchange_un(c, p));
     if (o->jv_mode == NK_JV_FD) {
         A.unorm = o->u_norm;  // known from the fused Newton update (nk_axpy_norm), else one pass
         if (!(A.unorm > 0.0)) {

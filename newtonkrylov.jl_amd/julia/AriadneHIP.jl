@@ -16,6 +16,8 @@ import Krylov: kdot, knorm, kscal!, kaxpy!, kaxpby!, kcopy!, kfill!, kdivcopy!, 
 const libnkhip = joinpath(@__DIR__, "..", "lib", "libnkhip.so")
 
 const NK_BRATU1D, NK_BRATU2D, NK_HEAT2D_EULER, NK_HEAT3D_EULER = Int32(1), Int32(2), Int32(3), Int32(4)
+const NK_HEAT2D_MIDPOINT, NK_HEAT3D_MIDPOINT, NK_HEAT2D_TRAPEZOID, NK_HEAT3D_TRAPEZOID = Int32(5), Int32(6), Int32(7), Int32(8)
+const NK_BC_ZERO, NK_BC_PERIODIC = Int32(0), Int32(1)
 const NK_USER1D, NK_USER2D, NK_USER3D = Int32(16), Int32(17), Int32(18)
 const NK_JV_EXACT, NK_JV_FD = Int32(0), Int32(1)
 
@@ -49,9 +51,10 @@ struct NkProblem
     dt::Float64
     un::Ptr{Float64}
     user::Ptr{Cvoid}   # nk_user_ops* (NK_USER1D/2D/3D)
+    alpha::Float64     # G_Midpoint!'s α (implicit.jl:17)
 end
 geometry(grid::NTuple{3, Int}) = NkProblem(grid[3] > 1 ? NK_HEAT3D_EULER : (grid[2] > 1 ? NK_BRATU2D : NK_BRATU1D),
-                                            0, grid..., 1.0, 1.0, 1.0, 0.0, 0.0, 0.0, Ptr{Float64}(1), C_NULL)
+                                            0, grid..., 1.0, 1.0, 1.0, 0.0, 0.0, 0.0, Ptr{Float64}(1), C_NULL, 0.5)
 
 # --------------------------------------------------------------------------- HipVector (device HaloVector)
 """Grid function in HBM: interior x-fastest (the column-major order of a Julia array), one ghost
@@ -143,11 +146,17 @@ HipResidual{K}() where {K} = HipResidual{K}(NK_JV_EXACT)
 const bratu! = HipResidual{:bratu1d}()        # examples/bratu.jl:14-24, p = (Δx, λ)
 const bratu2d! = HipResidual{:bratu2d}()      # p = (Δx, Δy, λ)
 const heat2d_euler! = HipResidual{:heat2d}()  # G_Euler! ∘ diffusion!, p = (uₙ, Δt, du, (a, Δx, Δy, bc!), t)
+const heat2d_midpoint! = HipResidual{:heat2d_midpoint}()    # G_Midpoint! ∘ diffusion! (α = 0.5), implicit.jl:17-25
+const heat2d_trapezoid! = HipResidual{:heat2d_trapezoid}()  # G_Trapezoid! ∘ diffusion!, implicit.jl:29-37
 
-problem(::HipResidual{:bratu1d}, u::HipVector, (dx, λ)) = NkProblem(NK_BRATU1D, 0, u.grid..., dx, 1, 1, λ, 0, 0, C_NULL, C_NULL)
-problem(::HipResidual{:bratu2d}, u::HipVector, (dx, dy, λ)) = NkProblem(NK_BRATU2D, 0, u.grid..., dx, dy, 1, λ, 0, 0, C_NULL, C_NULL)
-problem(::HipResidual{:heat2d}, u::HipVector, (un, Δt, _, (a, dx, dy, _bc), _t)) =
-    NkProblem(NK_HEAT2D_EULER, 0, u.grid..., dx, dy, 1, 0, a, Δt, un.ptr, C_NULL)
+# bc_zero! / bc_periodic! of examples/heat_2D.jl:15-38, recognised by name
+bccode(bc) = nameof(bc) === :bc_periodic! ? NK_BC_PERIODIC : NK_BC_ZERO
+const HEAT_KINDS = (heat2d = NK_HEAT2D_EULER, heat2d_midpoint = NK_HEAT2D_MIDPOINT, heat2d_trapezoid = NK_HEAT2D_TRAPEZOID)
+
+problem(::HipResidual{:bratu1d}, u::HipVector, (dx, λ)) = NkProblem(NK_BRATU1D, 0, u.grid..., dx, 1, 1, λ, 0, 0, C_NULL, C_NULL, 0.5)
+problem(::HipResidual{:bratu2d}, u::HipVector, (dx, dy, λ)) = NkProblem(NK_BRATU2D, 0, u.grid..., dx, dy, 1, λ, 0, 0, C_NULL, C_NULL, 0.5)
+problem(::HipResidual{K}, u::HipVector, (un, Δt, _, (a, dx, dy, bc), _t)) where {K} =
+    NkProblem(HEAT_KINDS[K], bccode(bc), u.grid..., dx, dy, 1, 0, a, Δt, un.ptr, C_NULL, 0.5)
 
 # --------------------------------------------------------------------------- user residuals (NK_USER*)
 # Any F!(res, u, p) the caller evaluates on the device (e.g. an AMDGPU.jl / KernelAbstractions
@@ -179,7 +188,7 @@ function problem(F::HipUserResidual, u::HipVector, p)
                         cJ === nothing ? C_NULL : Base.unsafe_convert(Ptr{Cvoid}, cJ), C_NULL, C_NULL))
     _live[F] = (cF, cJ, ops, p)
     kind = u.grid[3] > 1 ? NK_USER3D : (u.grid[2] > 1 ? NK_USER2D : NK_USER1D)
-    return NkProblem(kind, 0, u.grid..., 1, 1, 1, 0, 0, 0, C_NULL, Base.unsafe_convert(Ptr{Cvoid}, ops))
+    return NkProblem(kind, 0, u.grid..., 1, 1, 1, 0, 0, 0, C_NULL, Base.unsafe_convert(Ptr{Cvoid}, ops), 0.5)
 end
 function (F::HipUserResidual)(res::HipVector, u::HipVector, p)
     check(ccall((:nk_residual, libnkhip), Cint, (VP, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}),

@@ -22,6 +22,9 @@ ap.add_argument("--out", required=True)
 ap.add_argument("--nx", type=int, default=48)
 ap.add_argument("--ny", type=int, default=40)
 ap.add_argument("--jv", default="exact")
+ap.add_argument("--problem", choices=["bratu", "heat_periodic"], default="bratu",
+                help="heat_periodic: G_Trapezoid! ∘ diffusion! with bc_periodic! -- u_n's ghost planes are "
+                     "exchanged too and the slabs form a ring (rank 0 <-> rank world-1)")
 ap.add_argument("--transport", choices=["rccl", "mailbox"], default="rccl",
                 help="rccl: nk_dist_init (RCCL bootstrap, then the peer mailbox / RCCL fallback); mailbox: "
                      "IPC handles exchanged over gloo, no RCCL at all (works with every rank on one GPU)")
@@ -58,20 +61,32 @@ hx, hy, lam = 1.0 / (nx + 1), 1.0 / (ny + 1), 3.51382
 xs = np.arange(1, nx + 1) * hx
 y0, nyl = grid.offset, grid.shape_xyz[1]
 ys = np.arange(y0 + 1, y0 + nyl + 1) * hy
-u0 = np.sin(np.pi * ys)[:, None] * np.sin(np.pi * xs)[None, :]
 v_glob = np.random.default_rng(7).standard_normal((ny, nx))
-p = (hx, hy, lam)
+if args.problem == "bratu":
+    u0 = np.sin(np.pi * ys)[:, None] * np.sin(np.pi * xs)[None, :]
+    F_, p = ah.bratu2d_, (hx, hy, lam)
+    kw = dict(memory=10, tol_rel=1e-9, krylov_kwargs=dict(restart=True))
+else:
+    rng = np.random.default_rng(5)
+    un_glob = rng.standard_normal((ny, nx))
+    u_glob = un_glob + 0.01 * rng.standard_normal((ny, nx))
+    u0 = np.ascontiguousarray(u_glob[y0:y0 + nyl])
+    a = 0.01
+    dt = hx ** 2 * hy ** 2 / (2.0 * a * (hx ** 2 + hy ** 2))
+    und = ah.DeviceArray.from_numpy(np.ascontiguousarray(un_glob[y0:y0 + nyl]), grid, ctx)
+    F_, p = ah.heat2d_trapezoid_, (und, dt, None, (a, hx, hy, ah.bc_periodic_), 0.0)
+    kw = dict(tol_abs=6e-6, krylov_kwargs=dict(reorthogonalization=True))
 
 u = ah.DeviceArray.from_numpy(u0, grid, ctx)
 res = u.zero()
 vd = ah.DeviceArray.from_numpy(np.ascontiguousarray(v_glob[y0:y0 + nyl]), grid, ctx)
 out = u.zero()
-ah.bratu2d_(res, u, p)
-ah.mul_(out, ah.JacobianOperator(ah.bratu2d_, res, u, p, jv=args.jv), vd)
+F_(res, u, p)
+ah.mul_(out, ah.JacobianOperator(F_, res, u, p, jv=args.jv), vd)
 jv_loc = out.to_numpy()
 F_loc = res.to_numpy()
 dot = ah.kdot(len(u), u, vd)
-u, r = ah.newton_krylov_(ah.bratu2d_, u, p, res, memory=10, tol_rel=1e-9, krylov_kwargs=dict(restart=True), jv=args.jv)
+u, r = ah.newton_krylov_(F_, u, p, res, jv=args.jv, **kw)
 parts = [None] * world
 dist.all_gather_object(parts, dict(y0=y0, u=u.to_numpy(), jv=jv_loc, F=F_loc))
 if rank == 0:

@@ -120,4 +120,6 @@ def test_unsupported_algo_and_generic_residual_rejected():
     with pytest.raises(TypeError):
         ah.JacobianOperator(lambda r, u, p: None, None, None)
     with pytest.raises(NotImplementedError):
-        ah.G_Midpoint_.bind(ah.diffusion_)
+        ah.G_Midpoint_.bind(lambda du, u, p, t: None)  # only diffusion! has a fused device residual
+    with pytest.raises(TypeError):
+        ah.G_Euler_(alpha=0.3)  # α is G_Midpoint!'s keyword

@@ -138,3 +138,57 @@ def test_slab_protocol_matches_single_domain(tmp_path, world):
     uo, so = oc.newton_krylov(P, U0, memory=10, restart=True, tol_rel=1e-9)
     assert (int(d["outer"]), int(d["inner"])) == (so["outer_iterations"], so["inner_iterations"])
     assert np.max(np.abs(d["u"] - uo)) <= 1e-9 * np.max(np.abs(uo))
+
+
+# ----------------------------------------------------------------------------- bc_periodic! ring
+def ring_padded(a, rank, world):
+    """Ghost rows of a periodic slab ring, posted in nk_dist.cpp's halo_exchange order (sends up then
+    down, receives from below then above): with two ranks both neighbours are the same rank, and only
+    this order pairs my lower ghost with the neighbour's last row under per-peer FIFO matching."""
+    up, dn = (rank + 1) % world, (rank - 1) % world
+    lo = torch.zeros(a.shape[1], dtype=torch.float64)
+    hi = torch.zeros(a.shape[1], dtype=torch.float64)
+    reqs = [dist.isend(torch.from_numpy(np.ascontiguousarray(a[-1])), up),
+            dist.isend(torch.from_numpy(np.ascontiguousarray(a[0])), dn),
+            dist.irecv(lo, dn), dist.irecv(hi, up)]
+    for r in reqs:
+        r.wait()
+    return np.concatenate([lo.numpy()[None], a, hi.numpy()[None]])
+
+
+def _ring_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = ah.slab((NX, NY), rank, world)
+    y0, nyl = g.offset, g.shape_xyz[1]
+    rng = np.random.default_rng(5)
+    un_g = rng.standard_normal((NY, NX))
+    u_g = un_g + 0.01 * rng.standard_normal((NY, NX))
+    P = oc.heat2d_euler(NX, NY, scheme="trapezoid", bc=oc.BC_PERIODIC)
+
+    def lap(a):  # diffusion!'s sum with the x wrap in-row and the y wrap through the ring ghosts
+        p = ring_padded(a, rank, world)
+        c = p[1:-1]
+        e, w = np.roll(c, -1, axis=1), np.roll(c, 1, axis=1)
+        return ((e - 2.0 * c) + w) / (P.hx * P.hx) + ((p[2:] - 2.0 * c) + p[:-2]) / (P.hy * P.hy)
+
+    un, u = un_g[y0:y0 + nyl], u_g[y0:y0 + nyl]
+    G = (un + (P.dt / 2.0) * (P.a * lap(un) + P.a * lap(u))) - u  # implicit.jl:29-37
+    parts = [None] * world
+    dist.all_gather_object(parts, dict(y0=y0, G=G))
+    if rank == 0:
+        parts.sort(key=lambda d: d["y0"])
+        np.savez(out, G=np.concatenate([d["G"] for d in parts]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_periodic_ring_protocol(tmp_path, world):
+    out = str(tmp_path / "ring.npz")
+    mp.spawn(_ring_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    rng = np.random.default_rng(5)
+    un = rng.standard_normal((NY, NX))
+    u = un + 0.01 * rng.standard_normal((NY, NX))
+    P = oc.heat2d_euler(NX, NY, un=un, scheme="trapezoid", bc=oc.BC_PERIODIC)
+    assert np.array_equal(np.load(out)["G"], oc.residual(P, u))

@@ -129,3 +129,39 @@ def test_slabs_match_oracle(tmp_path, world, transport):
     assert meta["solved"] and so["solved"]
     assert (meta["outer"], meta["inner"]) == (so["outer_iterations"], so["inner_iterations"])
     assert np.max(np.abs(d["u"] - uo)) <= 1e-8 * np.max(np.abs(uo))
+
+
+@pytest.mark.parametrize("transport", ["mailbox", "rccl"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_periodic_trapezoid_ring_matches_oracle(tmp_path, world, transport):
+    """G_Trapezoid! ∘ diffusion! with bc_periodic! on `world` slabs: u_n's ghost planes are exchanged
+    as well, and the slabs form a ring (rank 0's lower ghost is rank world-1's last plane; with two
+    ranks both neighbours are the same rank).  Residual and exact JVP bit-identical to the oracle on
+    the whole grid; one implicit step with equal Newton/Krylov counts."""
+    out = str(tmp_path / "ring")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", transport,
+           "--problem", "heat_periodic"]
+    env = dict(os.environ, NK_WORKER_SHARED_DEVICE="1")
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
+    try:
+        log, _ = proc.communicate(timeout=180)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, signal.SIGKILL)
+        pytest.fail("distributed worker timed out")
+    assert proc.returncode == 0, log.decode()[-3000:]
+    meta = json.load(open(out + ".json"))
+    if "skip" in meta:
+        pytest.skip(meta["skip"])
+    d = np.load(out + ".npz")
+    rng = np.random.default_rng(5)
+    un = rng.standard_normal((40, 48))
+    u0 = un + 0.01 * rng.standard_normal((40, 48))
+    P = oc.heat2d_euler(48, 40, un=un, scheme="trapezoid", bc=oc.BC_PERIODIC)
+    assert np.array_equal(d["F"], oc.residual(P, u0))
+    assert np.array_equal(d["jv"], oc.jv_exact(P, u0, d["v"]))
+    uo, so = oc.newton_krylov(P, u0, tol_abs=6e-6, reorthogonalization=True)
+    assert meta["solved"] and so["solved"]
+    assert (meta["outer"], meta["inner"]) == (so["outer_iterations"], so["inner_iterations"])
+    assert np.max(np.abs(d["u"] - uo)) <= 1e-10
