@@ -2,7 +2,8 @@
 """Krylov matvecs/s + achieved HBM GB/s, 2D Bratu 4096^2, GMRES(30) -- BASELINE.json config 2.
 
 (--workload heat2d / heat3d runs BASELINE configs 3 / 5 instead: implicit-Euler time steps of the
-2D heat equation at 8192^2 / the 3D heat equation at 512^3, one time step per step.)
+2D heat equation at 8192^2 / the 3D heat equation at 512^3, one time step per step; --scheme
+midpoint / trapezoid and --bc periodic select the other implicit.jl schemes and bc_periodic!.)
 
 One *step* = one inexact-Newton step of newton_krylov_ on the 2D Bratu problem (BASELINE.json
 configs[1]): F!(res,u) + ||F|| (fused), one device GMRES(30) solve with the fixed Krylov budget
@@ -38,13 +39,20 @@ import ariadne_hip as ah
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 ROOT = os.path.dirname(os.path.abspath(__file__))
 # bench kernel class -> rocprofv3 kernel name prefix (for the PMC traffic of profiles/*/pmc_traffic_*.json);
-# the stencil template is <KIND, MODE, EPI, VEC>: KIND 2 Bratu 2D, 3 heat 2D, 4 heat 3D; MODE 1 exact, 2 FD;
-# EPI 1 sumsq, 2 dot, 4 dot + fused V_k = q / h store
-STENCIL = {"bratu2d": "nk::k_st2d<2, ", "heat2d": "nk::k_st2d<3, ", "heat3d": "nk::k_st3d<4, "}
+# the stencil template is <KIND, MODE, EPI, VEC, PER>: KIND 2 Bratu 2D, 3/5/7 heat 2D Euler/midpoint/trapezoid,
+# 4/6/8 heat 3D; MODE 1 exact, 2 FD; EPI 1 sumsq, 2 dot, 4 dot + fused V_k = q / h store
+KIND = {("heat2d", "euler"): 3, ("heat3d", "euler"): 4, ("heat2d", "midpoint"): 5, ("heat3d", "midpoint"): 6,
+        ("heat2d", "trapezoid"): 7, ("heat3d", "trapezoid"): 8}
 
 
-def pmc_name(workload, kernel):
-    st = STENCIL[workload]
+def stencil_prefix(workload, scheme="euler"):
+    if workload == "bratu2d":
+        return "nk::k_st2d<2, "
+    return f"nk::k_st{workload[-2:]}<{KIND[workload, scheme]}, "
+
+
+def pmc_name(workload, kernel, scheme="euler"):
+    st = stencil_prefix(workload, scheme)
     return {"mgs_pass": "nk::k_mgs_pass<true,", "mgs_pass_last": "nk::k_mgs_pass<false,",
             "jv_fd_dot_norm": st + "2, 4,", "jv_exact_dot_norm": st + "1, 4,", "jv_fd_dot": st + "2, 2,",
             "residual_norm": st + "0, 1,", "divcopy": "nk::k_divcopy", "update_x": "nk::k_update_x"}.get(kernel)
@@ -57,6 +65,10 @@ def parse():
     ap.add_argument("--workload", choices=["bratu2d", "heat2d", "heat3d"], default="bratu2d",
                     help="bratu2d: BASELINE config 2 (default); heat2d: config 3 (8192^2 implicit Euler time "
                          "steps); heat3d: config 5 (512^3 implicit Euler time steps)")
+    ap.add_argument("--scheme", choices=["euler", "midpoint", "trapezoid"], default="euler",
+                    help="heat workloads: G_Euler! / G_Midpoint! (α = 0.5) / G_Trapezoid! (implicit.jl:8-37)")
+    ap.add_argument("--bc", choices=["zero", "periodic"], default="zero",
+                    help="heat workloads: bc_zero! / bc_periodic! (heat_2D.jl:15-38)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--n", type=int, default=0, help="per-GPU slab side (default 4096 / 8192 / 512 by workload)")
@@ -173,7 +185,8 @@ class Bratu2D:
 
 class HeatEuler:
     """BASELINE configs 3 / 5: implicit-Euler time steps (examples/implicit.jl `solve`) of the 2D / 3D heat
-    equation, noisy IC, unrestarted GMRES (memory 20), tol_abs = 6e-6; one step = one time step."""
+    equation, noisy IC, unrestarted GMRES (memory 20), tol_abs = 6e-6; one step = one time step.
+    --scheme / --bc: the same loop with G_Midpoint! / G_Trapezoid! and bc_periodic!."""
 
     def __init__(self, args, ctx, rank, world, dim):
         n = args.n or (8192 if dim == 2 else 512)
@@ -202,15 +215,19 @@ class HeatEuler:
         self.u = self.un.copy()
         self.res = self.u.zero()
         self.ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(self.res, memory=args.memory or 20))
-        self.F = ah.heat2d_euler_ if dim == 2 else ah.heat3d_euler_
-        fp = (self.a, hs[0], hs[1], ah.bc_zero_) if dim == 2 else (self.a, hs[0], hs[1], hs[2], ah.bc_zero_)
+        G = {"euler": ah.G_Euler_, "midpoint": ah.G_Midpoint_, "trapezoid": ah.G_Trapezoid_}[args.scheme]
+        self.F = G.bind(ah.diffusion_ if dim == 2 else ah.diffusion3d_)
+        bc = ah.bc_periodic_ if args.bc == "periodic" else ah.bc_zero_
+        fp = (self.a, hs[0], hs[1], bc) if dim == 2 else (self.a, hs[0], hs[1], hs[2], bc)
         self.p = (self.un, self.dt, None, fp, 0.0)
         self.jv_kernel = "jv_fd_dot_norm" if args.jv == "fd" else "jv_exact_dot_norm"
         shape = "x".join([str(n)] * (dim - 1) + [str(n * world)])
-        self.workload = (f"{dim}D heat implicit Euler {shape} ({n}^{dim} per GPU), one time step per step: "
+        sname = {"euler": "implicit Euler", "midpoint": "implicit midpoint", "trapezoid": "implicit trapezoid"}[args.scheme]
+        bcname = "" if args.bc == "zero" else ", bc_periodic!"
+        self.workload = (f"{dim}D heat {sname}{bcname} {shape} ({n}^{dim} per GPU), one time step per step: "
                          f"newton_krylov! tol_abs=6e-6, GMRES memory {args.memory or 20} (unrestarted), "
                          f"{args.jv.upper()} Jv, IC sin*sin + 0.1 U(-1,1)")
-        self.metric = f"Krylov matvecs/sec + achieved HBM GB/s, {dim}D heat implicit Euler {n}^{dim}"
+        self.metric = f"Krylov matvecs/sec + achieved HBM GB/s, {dim}D heat {sname}{bcname} {n}^{dim}"
 
     def step(self):
         _, r = ah.newton_krylov_(self.F, self.u, self.p, self.res, tol_abs=6.0e-6, memory=self.args.memory or 20,
@@ -223,14 +240,16 @@ class HeatEuler:
 
         oc.set_threads(threads)
         m = self.n  # bounded sample: one time step of the same problem
-        P = oc.heat2d_euler(m) if self.dim == 2 else oc.heat3d_euler(m)
+        bcc = oc.BC_PERIODIC if self.args.bc == "periodic" else oc.BC_ZERO
+        P = (oc.heat2d_euler(m, scheme=self.args.scheme, bc=bcc) if self.dim == 2
+             else oc.heat3d_euler(m, scheme=self.args.scheme, bc=bcc))
         u0 = oc.sin_ic(P) + 0.1 * np.random.default_rng(0).uniform(-1, 1, P.shape)
         P.un = u0
         t0 = time.perf_counter()
         _, st = oc.newton_krylov(P, u0, tol_abs=6e-6, memory=self.args.memory or 20, jv=self.args.jv)
         dt = time.perf_counter() - t0
         return dict(value=st["n_matvec"] / dt, unit="matvecs/s", cores=oc.get_threads(), kind="port",
-                    sample=f"oracle/nk_oracle.c one implicit-Euler time step ({st['outer_iterations']} Newton, "
+                    sample=f"oracle/nk_oracle.c one {self.args.scheme} time step ({st['outer_iterations']} Newton, "
                            f"{st['n_matvec']} matvecs) of the same {self.dim}D heat problem at {m}^{self.dim} "
                            f"(noise from numpy default_rng(0)), {dt:.2f} s")
 
@@ -310,14 +329,15 @@ def main():
 
     pmc = {}
     if not args.traffic_json:
-        args.traffic_json = os.path.join(ROOT, "profiles", "r01", f"pmc_traffic_{args.workload}.json")
+        tag = args.workload + ("" if args.scheme == "euler" else "_" + args.scheme) + ("" if args.bc == "zero" else "_periodic")
+        args.traffic_json = os.path.join(ROOT, "profiles", "r01", f"pmc_traffic_{tag}.json")
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             pmc = json.load(f)
 
     def traffic(name):
         """PMC HBM bytes per launch of this kernel class as a rate over the same launch duration."""
-        pre = pmc_name(args.workload, name)
+        pre = pmc_name(args.workload, name, args.scheme)
         hit = [v for k, v in pmc.items() if pre and k.startswith(pre)]
         return hit[0]["traffic_bytes"] if hit else None
 
