@@ -62,18 +62,23 @@ extern "C" {
 #define NK_ALGO_CG 1       /* krylov_workspace(:cg, …)    (examples/bratu.jl:59-63) */
 #define NK_ALGO_FGMRES 2   /* krylov_workspace(:fgmres, …) (examples/bratu.jl:131-157): flexible right-preconditioned GMRES */
 
-/* Right preconditioner N (Krylov.jl's `N`, ldiv = false: z = N v approximates A^{-1} v).  With
- * NK_ALGO_GMRES and a preconditioner the solve runs in the flexible form (Z_k = N V_k stored,
- * x = x0 + Z y) -- the same iterates in exact arithmetic as x = x0 + N (V y). */
+/* Right preconditioner N (Krylov.jl's `N`, ldiv = false: z = N v approximates A^{-1} v), as Krylov.jl
+ * 0.10 applies it: NK_ALGO_GMRES multiplies J N V_k and updates x += N (V y) once per cycle;
+ * NK_ALGO_FGMRES stores Z_k = N V_k and updates x += Z y (N may change from step to step). */
 #define NK_PRECOND_NONE 0
 #define NK_PRECOND_DIAG 1  /* z = diag .* v  (e.g. Jacobi: diag = 1 ./ diag(J), nk_jacobian_diag) */
 #define NK_PRECOND_USER 2  /* z = apply(data, ctx, z, v), enqueued on nk_ctx_stream(ctx)          */
+#define NK_PRECOND_GMRES 3 /* z = gmres(J, v; itmax): the GmresPreconditioner of examples/bratu.jl:139-157
+                              (Krylov.jl gmres defaults: memory 20, no restart, atol = rtol = √eps), run
+                              in `inner` (an NK_ALGO_GMRES workspace of the problem's grid)              */
 typedef int (*nk_user_precond)(void* data, struct nk_ctx* ctx, double* out, const double* in);
 typedef struct nk_precond {
     int32_t kind;          /* NK_PRECOND_*                                   */
     const double* diag;    /* NK_PRECOND_DIAG: device grid function          */
     nk_user_precond apply; /* NK_PRECOND_USER                                */
     void* data;
+    struct nk_workspace* inner;  /* NK_PRECOND_GMRES: the inner solve's workspace */
+    int32_t itmax;               /* NK_PRECOND_GMRES: its itmax                   */
 } nk_precond;
 
 typedef struct nk_ctx nk_ctx;

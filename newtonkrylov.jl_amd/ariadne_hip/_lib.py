@@ -21,7 +21,7 @@ NK_USER1D, NK_USER2D, NK_USER3D = 16, 17, 18
 NK_BC_ZERO, NK_BC_PERIODIC = 0, 1
 NK_JV_EXACT, NK_JV_FD = 0, 1
 NK_ALGO_GMRES, NK_ALGO_CG, NK_ALGO_FGMRES = 0, 1, 2
-NK_PRECOND_NONE, NK_PRECOND_DIAG, NK_PRECOND_USER = 0, 1, 2
+NK_PRECOND_NONE, NK_PRECOND_DIAG, NK_PRECOND_USER, NK_PRECOND_GMRES = 0, 1, 2, 3
 
 _ERRORS = {-1: "HIP error", -2: "invalid argument", -3: "out of device memory", -4: "RCCL error", -5: "bad state", -6: "user callback failed"}
 
@@ -47,7 +47,8 @@ NK_USER_PRECOND = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_v
 
 
 class nk_precond(C.Structure):
-    _fields_ = [("kind", C.c_int32), ("diag", C.c_void_p), ("apply", NK_USER_PRECOND), ("data", C.c_void_p)]
+    _fields_ = [("kind", C.c_int32), ("diag", C.c_void_p), ("apply", NK_USER_PRECOND), ("data", C.c_void_p),
+                ("inner", C.c_void_p), ("itmax", C.c_int32)]
 
 
 class nk_user_ops(C.Structure):

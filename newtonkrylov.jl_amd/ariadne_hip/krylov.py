@@ -159,7 +159,8 @@ def krylov_solve_(ws: KrylovWorkspace, J, b: DeviceArray, *, restart=False, reor
     if ldiv:
         raise NotImplementedError("ldiv = true: give N as the operator that approximates J^{-1} (ldiv = false)")
     if N is not None and not hasattr(N, "as_c"):
-        raise TypeError("N must be an ariadne_hip preconditioner (DiagonalPreconditioner, UserPreconditioner, jacobi(J))")
+        raise TypeError("N must be an ariadne_hip preconditioner (DiagonalPreconditioner, UserPreconditioner, "
+                        "GmresPreconditioner, jacobi(J))")
     if ws.algo == "cg" and (restart or reorthogonalization):
         raise TypeError("restart / reorthogonalization are GMRES keywords")
     prob = J.problem()

@@ -74,3 +74,35 @@ def jacobi(J) -> DiagonalPreconditioner:
     """Jacobi preconditioner N = diag(J(u))^{-1} (the reference's examples build theirs from
     collect(J), bratu.jl:121-137); use as `N=jacobi` in newton_krylov_ (called per Newton step)."""
     return DiagonalPreconditioner(jacobian_diag(J, reciprocal=True))
+
+
+class GmresPreconditioner(Preconditioner):
+    """`GmresPreconditioner(J, itmax)` of examples/bratu.jl:139-157: mul!(y, P, x) runs
+    `gmres(P.J, x; P.itmax)` (Krylov.jl defaults: memory 20, no restart, atol = rtol = √eps) and copies
+    the solution into y.  Here the inner solve is the device GMRES on J's operator (NK_PRECOND_GMRES),
+    in a workspace of its own; use it with algo="fgmres" (N changes from step to step)."""
+
+    def __init__(self, J, itmax: int, workspace=None):
+        from .krylov import KrylovConstructor, krylov_workspace
+
+        self.J, self.itmax = J, int(itmax)
+        self.ws = workspace or krylov_workspace("gmres", KrylovConstructor(J.u, memory=20))
+        self._c = _lib.nk_precond(_lib.NK_PRECOND_GMRES, None, _lib.NK_USER_PRECOND(), None, self.ws.handle, self.itmax)
+
+    def as_c(self):
+        return self._c
+
+
+def gmres_preconditioner(itmax: int):
+    """N factory `(J) -> GmresPreconditioner(J, itmax)` for newton_krylov_ (bratu.jl:150-155); the
+    inner workspace is allocated once and reused by every Newton step."""
+    cache = {}
+
+    def factory(J):
+        key = (id(J.u.ctx), J.u.grid)
+        if key not in cache:
+            cache.clear()
+            cache[key] = GmresPreconditioner(J, itmax).ws
+        return GmresPreconditioner(J, itmax, workspace=cache[key])
+
+    return factory

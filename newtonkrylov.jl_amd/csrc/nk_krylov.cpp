@@ -148,26 +148,9 @@ int host_scalar(nk_ctx* c, Red r, int sqrt_it, double* out) {
     return NK_OK;
 }
 
-// z = N v (right preconditioner); *znorm = ||z|| when the FD operator needs it
-int apply_precond(nk_ctx* c, const nk_problem* p, const nk_precond* N, int64_t n, double* z, const double* v,
-                  bool need_norm, double* znorm) {
-    Red rz{};
-    if (N->kind == NK_PRECOND_DIAG) {
-        if (!N->diag) return fail(c, NK_E_ARG, "diagonal preconditioner without its diagonal");
-        NK_TRY(launch_diag_apply(c, n, z, N->diag, v, need_norm ? &rz : nullptr));
-    } else if (N->kind == NK_PRECOND_USER) {
-        if (!N->apply) return fail(c, NK_E_ARG, "user preconditioner without its apply callback");
-        NK_TRY(halo_exchange(c, p, v));
-        int rc = 0;
-        NK_TRY(launch(c, "precond_user", 0.0, [&] { rc = N->apply(N->data, c, z, v); }));
-        if (rc != 0) return fail(c, NK_E_USER, "user preconditioner callback returned " + std::to_string(rc));
-        if (need_norm) NK_TRY(launch_sumsq(c, n, z, &rz));
-    } else {
-        return fail(c, NK_E_ARG, "unknown preconditioner kind");
-    }
-    if (need_norm) NK_TRY(host_scalar(c, rz, 1, znorm));
-    return NK_OK;
-}
+struct Op;
+int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const nk_krylov_opts* o, nk_krylov_stats* st,
+          double* hist, int64_t hist_cap, int64_t* hist_len);
 
 struct Op {
     nk_ctx* c;
@@ -202,6 +185,43 @@ struct Op {
     }
     int64_t ws_n() const { return p->nx * p->ny * p->nz; }
 };
+
+// z = N v (right preconditioner); *znorm = ||z|| when the FD operator needs it.
+//   DIAG   z = d .* v (Jacobi)
+//   USER   the caller's device callback
+//   GMRES  sol, _ = gmres(J, v; itmax); copyto!(z, sol) -- the GmresPreconditioner of
+//          examples/bratu.jl:139-157: Krylov.jl's gmres defaults (memory 20, no restart,
+//          atol = rtol = √eps, x0 = 0) on the same operator, in the preconditioner's own workspace
+int apply_precond(nk_ctx* c, const nk_problem* p, const nk_precond* N, Op& A, int64_t n, double* z, const double* v,
+                  bool need_norm, double* znorm) {
+    Red rz{};
+    if (N->kind == NK_PRECOND_DIAG) {
+        if (!N->diag) return fail(c, NK_E_ARG, "diagonal preconditioner without its diagonal");
+        NK_TRY(launch_diag_apply(c, n, z, N->diag, v, need_norm ? &rz : nullptr));
+    } else if (N->kind == NK_PRECOND_USER) {
+        if (!N->apply) return fail(c, NK_E_ARG, "user preconditioner without its apply callback");
+        NK_TRY(halo_exchange(c, p, v));
+        int rc = 0;
+        NK_TRY(launch(c, "precond_user", 0.0, [&] { rc = N->apply(N->data, c, z, v); }));
+        if (rc != 0) return fail(c, NK_E_USER, "user preconditioner callback returned " + std::to_string(rc));
+        if (need_norm) NK_TRY(launch_sumsq(c, n, z, &rz));
+    } else if (N->kind == NK_PRECOND_GMRES) {
+        if (!N->inner || N->inner->algo != NK_ALGO_GMRES || N->inner->n != n)
+            return fail(c, NK_E_ARG, "GMRES preconditioner needs a GMRES workspace of the problem's size");
+        nk_krylov_opts io{};
+        io.itmax = N->itmax;
+        io.jv_mode = A.mode;
+        io.atol = io.rtol = std::sqrt(DBL_EPSILON);
+        nk_krylov_stats is{};
+        NK_TRY(gmres(N->inner, p, A, v, &io, &is, nullptr, 0, nullptr));
+        NK_TRY(launch_copy(c, n, z, N->inner->x));
+        if (need_norm) NK_TRY(launch_sumsq(c, n, z, &rz));
+    } else {
+        return fail(c, NK_E_ARG, "unknown preconditioner kind");
+    }
+    if (need_norm) NK_TRY(host_scalar(c, rz, 1, znorm));
+    return NK_OK;
+}
 
 #define PUSH_HIST(v)                                   \
     do {                                               \
@@ -258,9 +278,11 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
     auto slot_pin_dev = [&](int k) { return ws->hpin_dev + (size_t)(k & 1) * (2 * ws->cap + 2); };
     auto npasses_of = [&](int k) { return reorth ? 2 * k : k; };
     const double* v1_src = b;  // r0 of the current cycle; step 1 applies J to r0 / beta and stores V_1
-    // right preconditioner: the flexible form (Z_k = N V_k stored, x += Z y), without the
-    // one-step-ahead issue (the FD step size needs ||Z_k|| on the host)
+    // right preconditioner, without the one-step-ahead issue (the FD step size needs ||N V_k|| on
+    // the host): fgmres! stores Z_k = N V_k and updates x += Z y; gmres! applies N to p = N V_k
+    // only for the product and updates x += N (V y) (Krylov.jl 0.10 gmres! / fgmres!)
     const nk_precond* N = (o->N && o->N->kind != NK_PRECOND_NONE) ? o->N : nullptr;
+    const bool flex = N && ws->algo == NK_ALGO_FGMRES;
     const bool spec = N == nullptr;
     auto issue = [&](int k) -> int {
         NK_TRY(ws_basis(ws, k));
@@ -274,10 +296,11 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         const double* qprev = k > 1 ? W[(k - 1) & 1] : v1_src;
         if (N) {  // V_k = q_{k-1} / h (r0 / beta), Z_k = N V_k, q = J Z_k, <V_1, q>
             NK_TRY(launch_fd_point(c, n, nullptr, nullptr, qprev, hprev, 0.0, ws->V[k - 1]));
-            NK_TRY(ws_zbasis(ws, k));
+            NK_TRY(ws_zbasis(ws, flex ? k : 1));  // gmres!: one p = N V_k buffer; fgmres!: Z_k kept
+            double* zk = ws->Z[flex ? k - 1 : 0];
             double znorm = 1.0;
-            NK_TRY(apply_precond(c, p, N, n, ws->Z[k - 1], ws->V[k - 1], A.mode == NK_JV_FD, &znorm));
-            NK_TRY(A.apply(q, ws->Z[k - 1], znorm, EPI_DOT, ws->V[0], &red));
+            NK_TRY(apply_precond(c, p, N, A, n, zk, ws->V[k - 1], A.mode == NK_JV_FD, &znorm));
+            NK_TRY(A.apply(q, zk, znorm, EPI_DOT, ws->V[0], &red));
         } else if (k == 1) {  // fused kdivcopy!(V_1, r0, beta) + mul! + <V_1, Jv> (the dot partner is V_1 itself)
             NK_TRY(A.apply(q, v1_src, 1.0, EPI_DOT, nullptr, &red, ws->bdev, ws->V[0]));
         } else {
@@ -392,8 +415,18 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         const bool need_xnorm = restart && A.mode == NK_JV_FD && !final_cycle;
         double* uu = final_cycle ? o->u_update : nullptr;  // fused Newton update u .-= x
         Red xr{};
-        NK_TRY(launch_update_x(c, n, x, ws->xr, N ? ws->Z.data() : ws->V.data(), kk, ws->ydev, restart && npass > 1,
-                               (need_xnorm || uu) ? &xr : nullptr, uu));
+        if (N && !flex) {  // gmres!: xr = V y; p = xr; xr = N p; x += xr (restart) -- x = xr otherwise
+            uu = nullptr;  // not fused: nk_krylov_solve applies u .-= x afterwards
+            NK_TRY(launch_update_x(c, n, W[0], ws->xr, ws->V.data(), kk, ws->ydev, 0, nullptr, nullptr));
+            double dummy = 0.0;
+            NK_TRY(apply_precond(c, p, N, A, n, ws->Z[0], W[0], false, &dummy));
+            if (restart && npass > 1) NK_TRY(launch_axpy(c, n, 1.0, ws->Z[0], x));
+            else NK_TRY(launch_copy(c, n, x, ws->Z[0]));
+            if (need_xnorm) NK_TRY(launch_sumsq(c, n, x, &xr));
+        } else {
+            NK_TRY(launch_update_x(c, n, x, ws->xr, N ? ws->Z.data() : ws->V.data(), kk, ws->ydev, restart && npass > 1,
+                                   (need_xnorm || uu) ? &xr : nullptr, uu));
+        }
         if (uu) {
             NK_TRY(host_scalar(c, xr, 1, &st->u_norm));
             ws->u_fused = true;

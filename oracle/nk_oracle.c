@@ -42,7 +42,16 @@ enum { OC_BRATU1D = 1, OC_BRATU2D = 2, OC_HEAT2D_EULER = 3, OC_HEAT3D_EULER = 4,
 enum { OC_BC_ZERO = 0, OC_BC_PERIODIC = 1 };
 enum { OC_JV_EXACT = 0, OC_JV_FD = 1 };
 enum { OC_FORCING_NONE = 0, OC_FORCING_FIXED = 1, OC_FORCING_EW = 2 };
-enum { OC_ALGO_GMRES = 0, OC_ALGO_CG = 1 };
+enum { OC_ALGO_GMRES = 0, OC_ALGO_CG = 1, OC_ALGO_FGMRES = 2 };
+/* right preconditioner N (Krylov.jl's `N`, ldiv = false):  DIAG z = d .* v (Jacobi: d = 1 ./ diag(J));
+ * GMRES: z = gmres(J, v; itmax) -- the GmresPreconditioner of examples/bratu.jl:139-157 */
+enum { OC_PRECOND_NONE = 0, OC_PRECOND_DIAG = 1, OC_PRECOND_GMRES = 3, OC_PRECOND_JACOBI = 4 };
+
+typedef struct {
+    int32_t kind;           /* OC_PRECOND_DIAG / OC_PRECOND_GMRES */
+    int32_t itmax;          /* GMRES: the inner solve's itmax */
+    const double* diag;     /* DIAG */
+} oc_precond;
 
 typedef struct {
     int32_t kind;
@@ -61,6 +70,8 @@ typedef struct {
     int32_t reorthogonalization;
     int32_t itmax;          /* 0 => 2n */
     double atol, rtol;
+    int32_t flexible;       /* fgmres! (Z_k = N V_k stored, x += Z y) instead of gmres! (x += N (V y)) */
+    const oc_precond* N;    /* right preconditioner or NULL */
 } oc_krylov_opts;
 
 typedef struct {
@@ -78,6 +89,8 @@ typedef struct {
     int32_t jv_mode;        /* OC_JV_* */
     oc_krylov_opts krylov;
     int32_t rtol_user;      /* krylov_kwargs carries rtol: it wins over the forcing (Ariadne.jl:330-333) */
+    int32_t precond;        /* N factory called per Newton step: OC_PRECOND_NONE / _JACOBI / _GMRES */
+    int32_t precond_itmax;  /* OC_PRECOND_GMRES: GmresPreconditioner(J, itmax) */
 } oc_newton_opts;
 
 typedef struct {
@@ -347,7 +360,46 @@ void oc_sym_givens(double a, double b, double* c, double* s, double* rho) {
     }
 }
 
-/* ------------------------------------------------------------------ GMRES (Krylov.jl 0.10 gmres!, M = N = I) */
+/* diag(J(u)): the exact tangent of each residual on the unit vector e_i (the diagonal of collect(J),
+ * src/Ariadne.jl:140-162): centre field 1 -- (1 - α) for G_Midpoint! -- every neighbour 0 */
+void oc_jacobian_diag(const oc_problem* P, double* out, const double* u, int reciprocal) {
+    const int64_t n = oc_n(P);
+    const int heat = P->kind >= OC_HEAT2D_EULER && P->kind <= OC_HEAT3D_TRAPEZOID;
+    const int dim = P->kind == OC_BRATU1D ? 1 : (P->kind == OC_BRATU2D ? 2 : oc_heat_dim(P->kind));
+    const int sch = heat ? oc_scheme(P->kind) : 0;
+    const double c = sch == 1 ? (1.0 - P->alpha) * 1.0 : 1.0;
+    double lsum = lap1(c, 0.0, 0.0, P->hx);
+    if (dim >= 2) lsum = lsum + lap1(c, 0.0, 0.0, P->hy);
+    if (dim == 3) lsum = lsum + lap1(c, 0.0, 0.0, P->hz);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+        double d;
+        if (!heat) d = lsum + P->lambda * (exp(u[i]) * 1.0);
+        else if (sch == 2) d = (P->dt / 2.0) * (P->a * lsum) - 1.0;
+        else d = P->dt * (P->a * lsum) - 1.0;
+        out[i] = reciprocal ? 1.0 / d : d;
+    }
+}
+
+int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_krylov_stats* st,
+             double* hist, int64_t hist_cap, int64_t* hist_len);
+
+/* z = N v */
+static void prec_apply(oc_op* A, const oc_precond* N, double* z, const double* v) {
+    const int64_t n = oc_n(A->P);
+    if (N->kind == OC_PRECOND_DIAG) {
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < n; ++i) z[i] = N->diag[i] * v[i];
+    } else { /* mul!(y, P::GmresPreconditioner, x): sol, _ = gmres(P.J, x; P.itmax); copyto!(y, sol) -- Krylov's
+                gmres defaults: memory 20, no restart, atol = rtol = √eps, x0 = 0 */
+        oc_krylov_opts io = {20, 0, 0, N->itmax, sqrt(DBL_EPSILON), sqrt(DBL_EPSILON), 0, NULL};
+        oc_krylov_stats is;
+        memset(&is, 0, sizeof is);
+        oc_gmres(A, v, z, &io, &is, NULL, 0, NULL);
+    }
+}
+
+/* ------------------------------------------------------------------ GMRES / FGMRES (Krylov.jl 0.10 gmres! / fgmres!, M = I) */
 static void* xrealloc(void* p, size_t sz) { void* q = realloc(p, sz); if (!q) abort(); return q; }
 
 int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_krylov_stats* st,
@@ -362,9 +414,15 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
 
     double* w = (double*)malloc(sizeof(double) * n);
     double* xr = restart ? (double*)malloc(sizeof(double) * n) : x;
+    const oc_precond* N = (o->N && o->N->kind != OC_PRECOND_NONE) ? o->N : NULL;
+    const int flex = N && o->flexible;
+    double* pv = N ? (double*)malloc(sizeof(double) * n) : NULL; /* gmres!: p = N V_k, and N (V y) */
     int vcap = mem;
     double** V = (double**)calloc((size_t)vcap, sizeof(double*));
     for (int i = 0; i < vcap; ++i) V[i] = (double*)malloc(sizeof(double) * n);
+    double** Z = flex ? (double**)calloc((size_t)vcap, sizeof(double*)) : NULL; /* fgmres!: Z_k = N V_k */
+    if (flex)
+        for (int i = 0; i < vcap; ++i) Z[i] = (double*)malloc(sizeof(double) * n);
     int cap = mem;  /* capacity of c, s, z (z has cap entries) and R (cap(cap+1)/2) */
     double* c = (double*)calloc((size_t)cap, sizeof(double));
     double* s = (double*)calloc((size_t)cap, sizeof(double));
@@ -420,7 +478,15 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
                     R = (double*)xrealloc(R, sizeof(double) * nR); memset(R + oR, 0, sizeof(double) * (nR - oR));
                     cap = ncap;
                 }
-                op_apply(A, w, V[k - 1], 1.0);
+                if (flex) {
+                    prec_apply(A, N, Z[k - 1], V[k - 1]);
+                    op_apply(A, w, Z[k - 1], -1.0);
+                } else if (N) {
+                    prec_apply(A, N, pv, V[k - 1]);
+                    op_apply(A, w, pv, -1.0);
+                } else {
+                    op_apply(A, w, V[k - 1], 1.0);
+                }
                 for (int i = 1; i <= k; ++i) {
                     R[nr + i - 1] = oc_dot(n, V[i - 1], w);
                     oc_axpy(n, -R[nr + i - 1], V[i - 1], w);
@@ -453,6 +519,10 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
                         int nv = vcap * 2;
                         V = (double**)xrealloc(V, sizeof(double*) * nv);
                         for (int i = vcap; i < nv; ++i) V[i] = (double*)malloc(sizeof(double) * n);
+                        if (flex) {
+                            Z = (double**)xrealloc(Z, sizeof(double*) * nv);
+                            for (int i = vcap; i < nv; ++i) Z[i] = (double*)malloc(sizeof(double) * n);
+                        }
                         vcap = nv;
                     }
                     oc_divcopy(n, V[k], w, Hbis);
@@ -470,7 +540,11 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
                 if (fabs(R[pos - 1]) <= btol) { z[i - 1] = 0.0; inconsistent = 1; }
                 else z[i - 1] = z[i - 1] / R[pos - 1];
             }
-            for (int i = 1; i <= kk; ++i) oc_axpy(n, z[i - 1], V[i - 1], xr);
+            for (int i = 1; i <= kk; ++i) oc_axpy(n, z[i - 1], flex ? Z[i - 1] : V[i - 1], xr);
+            if (N && !flex) { /* gmres!: xr = N (V y) */
+                oc_copy(n, pv, xr);
+                prec_apply(A, N, xr, pv);
+            }
             if (restart) oc_axpy(n, 1.0, xr, x);
             iter += inner_iter;
             inner_itmax = itmax - iter;
@@ -488,6 +562,11 @@ done:
     free(w);
     if (restart) free(xr);
     for (int i = 0; i < vcap; ++i) free(V[i]);
+    if (flex) {
+        for (int i = 0; i < vcap; ++i) free(Z[i]);
+        free(Z);
+    }
+    free(pv);
     free(V); free(c); free(s); free(z); free(R);
     return 0;
 #undef PUSH_HIST
@@ -567,6 +646,7 @@ int oc_newton_krylov(const oc_problem* P, double* u, const oc_newton_opts* o, oc
     const int64_t n = oc_n(P);
     double* res = (double*)malloc(sizeof(double) * n);
     double* d = (double*)malloc(sizeof(double) * n);
+    double* dinv = o->precond == OC_PRECOND_JACOBI ? (double*)malloc(sizeof(double) * n) : NULL;
     oc_op A = {P, o->jv_mode, u, res, 0.0, 0};
     int64_t nres_count = 0;
     oc_residual(P, res, u);
@@ -586,6 +666,17 @@ int oc_newton_krylov(const oc_problem* P, double* u, const oc_newton_opts* o, oc
         oc_krylov_stats ks;
         memset(&ks, 0, sizeof ks);
         if (o->jv_mode == OC_JV_FD) A.unorm = oc_norm(n, u);
+        /* N = factory(J) for this step (Ariadne.jl:318-333 passes N through to krylov_solve!) */
+        oc_precond Np = {OC_PRECOND_NONE, o->precond_itmax, NULL};
+        if (o->precond == OC_PRECOND_JACOBI) {
+            oc_jacobian_diag(P, dinv, u, 1);
+            Np.kind = OC_PRECOND_DIAG;
+            Np.diag = dinv;
+        } else if (o->precond == OC_PRECOND_GMRES) {
+            Np.kind = OC_PRECOND_GMRES;
+        }
+        ko.N = Np.kind != OC_PRECOND_NONE ? &Np : NULL;
+        ko.flexible = o->algo == OC_ALGO_FGMRES;
         /* b = copy(res) (Ariadne.jl:338): res is not overwritten by our operator, so pass it directly */
         if (o->algo == OC_ALGO_CG) oc_cg(&A, res, d, &ko, &ks, NULL, 0, NULL);
         else oc_gmres(&A, res, d, &ko, &ks, NULL, 0, NULL);
@@ -609,7 +700,7 @@ int oc_newton_krylov(const oc_problem* P, double* u, const oc_newton_opts* o, oc
     st->n_matvec = A.n_matvec;
     st->n_residual = nres_count;
     st->tol = tol;
-    free(res); free(d);
+    free(res); free(d); free(dinv);
     return 0;
 }
 
@@ -620,7 +711,9 @@ int oc_krylov_solve(const oc_problem* P, int jv_mode, int algo, const double* u,
     oc_op A = {P, jv_mode, u, F0, 0.0, 0};
     if (jv_mode == OC_JV_FD) A.unorm = oc_norm(oc_n(P), u);
     if (algo == OC_ALGO_CG) return oc_cg(&A, b, x, o, st, hist, hist_cap, hist_len);
-    return oc_gmres(&A, b, x, o, st, hist, hist_cap, hist_len);
+    oc_krylov_opts oo = *o;
+    oo.flexible = algo == OC_ALGO_FGMRES;
+    return oc_gmres(&A, b, x, &oo, st, hist, hist_cap, hist_len);
 }
 
 void oc_set_threads(int t) { if (t > 0) omp_set_num_threads(t); }

@@ -32,7 +32,9 @@ HEAT_KINDS = {  # (scheme, dim) -> kind; schemes of examples/implicit.jl:8-37
 }
 JV_EXACT, JV_FD = 0, 1
 FORCING_NONE, FORCING_FIXED, FORCING_EW = 0, 1, 2
-ALGO_GMRES, ALGO_CG = 0, 1
+ALGO_GMRES, ALGO_CG, ALGO_FGMRES = 0, 1, 2
+PRECOND_NONE, PRECOND_DIAG, PRECOND_GMRES, PRECOND_JACOBI = 0, 1, 3, 4
+_ALGO = {"gmres": ALGO_GMRES, "cg": ALGO_CG, "fgmres": ALGO_FGMRES}
 SQRT_EPS = math.sqrt(np.finfo(np.float64).eps)
 
 
@@ -44,9 +46,14 @@ class _Problem(C.Structure):
                 ("un", C.POINTER(C.c_double)), ("alpha", C.c_double)]
 
 
+class _Precond(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("itmax", C.c_int32), ("diag", C.POINTER(C.c_double))]
+
+
 class _KrylovOpts(C.Structure):
     _fields_ = [("memory", C.c_int32), ("restart", C.c_int32), ("reorthogonalization", C.c_int32),
-                ("itmax", C.c_int32), ("atol", C.c_double), ("rtol", C.c_double)]
+                ("itmax", C.c_int32), ("atol", C.c_double), ("rtol", C.c_double), ("flexible", C.c_int32),
+                ("N", C.POINTER(_Precond))]
 
 
 class _KrylovStats(C.Structure):
@@ -58,7 +65,8 @@ class _NewtonOpts(C.Structure):
     _fields_ = [("tol_rel", C.c_double), ("tol_abs", C.c_double), ("max_niter", C.c_int32),
                 ("forcing", C.c_int32), ("eta_fixed", C.c_double), ("eta_max", C.c_double),
                 ("gamma", C.c_double), ("algo", C.c_int32), ("jv_mode", C.c_int32),
-                ("krylov", _KrylovOpts), ("rtol_user", C.c_int32)]
+                ("krylov", _KrylovOpts), ("rtol_user", C.c_int32), ("precond", C.c_int32),
+                ("precond_itmax", C.c_int32)]
 
 
 class _NewtonStats(C.Structure):
@@ -98,6 +106,7 @@ def lib():
         L.oc_newton_krylov.argtypes = [C.POINTER(_Problem), P, C.POINTER(_NewtonOpts), C.POINTER(_NewtonStats),
                                        P, I64, C.POINTER(I64)]
         L.oc_sym_givens.argtypes = [D, D, P, P, P]
+        L.oc_jacobian_diag.argtypes = [C.POINTER(_Problem), P, P, C.c_int]
         L.oc_set_threads.argtypes = [C.c_int]
         L.oc_get_threads.restype = C.c_int
         for name in ("oc_axpy",):
@@ -222,6 +231,28 @@ def jv_exact(P: Problem, u, v) -> np.ndarray:
     return out
 
 
+def jacobian_diag(P: Problem, u, reciprocal=False) -> np.ndarray:
+    """diag(J(u)) -- the diagonal of collect(J) (src/Ariadne.jl:140-162); reciprocal: Jacobi's 1 ./ diag."""
+    u = np.ascontiguousarray(u, dtype=np.float64)
+    out = np.empty_like(u)
+    cp = P._c()
+    lib().oc_jacobian_diag(C.byref(cp), _p(out), _p(u), int(bool(reciprocal)))
+    return out
+
+
+def _precond(N):
+    """N = None | ("diag", d) | ("gmres", itmax) -> (_Precond or None, keep-alive)."""
+    if N is None:
+        return None, None
+    kind, arg = N
+    if kind == "diag":
+        d = np.ascontiguousarray(arg, dtype=np.float64).reshape(-1)
+        return _Precond(PRECOND_DIAG, 0, _p(d)), d
+    if kind == "gmres":
+        return _Precond(PRECOND_GMRES, int(arg), None), None
+    raise ValueError(kind)
+
+
 def fd_eps(unorm: float, vnorm: float) -> float:
     return lib().oc_fd_eps(unorm, vnorm)
 
@@ -268,22 +299,25 @@ def get_threads() -> int:
 
 
 def krylov_solve(P: Problem, u, b, *, algo="gmres", jv="exact", F0=None, memory=20, restart=False,
-                 reorthogonalization=False, itmax=0, atol=SQRT_EPS, rtol=SQRT_EPS, history=True):
-    """One Krylov.jl-style solve of J(u) x = b; returns (x, stats dict, residual-norm history)."""
+                 reorthogonalization=False, itmax=0, atol=SQRT_EPS, rtol=SQRT_EPS, history=True, N=None):
+    """One Krylov.jl-style solve of J(u) x = b; returns (x, stats dict, residual-norm history).
+    algo: gmres | fgmres | cg; N: right preconditioner ("diag", d) or ("gmres", itmax)."""
     u = np.ascontiguousarray(u, dtype=np.float64)
     b = np.ascontiguousarray(b, dtype=np.float64)
     if jv == "fd" and F0 is None:
         F0 = residual(P, u)
     F0 = np.ascontiguousarray(F0 if F0 is not None else u, dtype=np.float64)
     x = np.empty_like(u)
-    o = _KrylovOpts(memory, int(restart), int(reorthogonalization), itmax, atol, rtol)
+    Np, _keep = _precond(N)
+    o = _KrylovOpts(memory, int(restart), int(reorthogonalization), itmax, atol, rtol, int(algo == "fgmres"),
+                    C.pointer(Np) if Np is not None else None)
     st = _KrylovStats()
     cap = (itmax if itmax else 2 * P.n) + 16 if history else 0
     cap = min(cap, 1 << 22)
     hist = np.zeros(max(cap, 1))
     hl = C.c_int64(0)
     cp = P._c()
-    lib().oc_krylov_solve(C.byref(cp), JV_FD if jv == "fd" else JV_EXACT, ALGO_CG if algo == "cg" else ALGO_GMRES,
+    lib().oc_krylov_solve(C.byref(cp), JV_FD if jv == "fd" else JV_EXACT, _ALGO[algo],
                           _p(u), _p(F0), _p(b), _p(x), C.byref(o), C.byref(st), _p(hist), cap, C.byref(hl))
     stats = dict(niter=st.niter, solved=bool(st.solved), inconsistent=bool(st.inconsistent),
                  breakdown=bool(st.breakdown), status=st.status, n_matvec=st.n_matvec)
@@ -292,14 +326,21 @@ def krylov_solve(P: Problem, u, b, *, algo="gmres", jv="exact", F0=None, memory=
 
 def newton_krylov(P: Problem, u0, *, tol_rel=1e-6, tol_abs=1e-12, max_niter=50, forcing="ew", eta=0.1,
                   eta_max=0.999, gamma=0.9, algo="gmres", jv="exact", memory=20, restart=False,
-                  reorthogonalization=False, itmax=0, atol=SQRT_EPS, rtol=None):
-    """Ariadne newton_krylov! restated (src/Ariadne.jl:288-372). rtol given => krylov_kwargs rtol wins."""
+                  reorthogonalization=False, itmax=0, atol=SQRT_EPS, rtol=None, N=None):
+    """Ariadne newton_krylov! restated (src/Ariadne.jl:288-372). rtol given => krylov_kwargs rtol wins.
+    N: a factory called per Newton step -- "jacobi" (1 ./ diag(J(u))) or ("gmres", itmax), the
+    GmresPreconditioner of examples/bratu.jl:139-157."""
     u = np.array(u0, dtype=np.float64, order="C", copy=True)
     fk = {"none": FORCING_NONE, None: FORCING_NONE, "fixed": FORCING_FIXED, "ew": FORCING_EW}[forcing]
     ko = _KrylovOpts(memory, int(restart), int(reorthogonalization), itmax, atol, 0.0 if rtol is None else rtol)
+    pk, pit = PRECOND_NONE, 0
+    if N == "jacobi":
+        pk = PRECOND_JACOBI
+    elif N is not None:
+        pk, pit = PRECOND_GMRES, int(N[1])
     o = _NewtonOpts(tol_rel, tol_abs, max_niter, fk, eta, eta_max, gamma,
-                    ALGO_CG if algo == "cg" else ALGO_GMRES, JV_FD if jv == "fd" else JV_EXACT, ko,
-                    0 if rtol is None else 1)
+                    _ALGO[algo], JV_FD if jv == "fd" else JV_EXACT, ko,
+                    0 if rtol is None else 1, pk, pit)
     st = _NewtonStats()
     cap = max_niter + 4
     hist = np.zeros(cap)
