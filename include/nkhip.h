@@ -71,6 +71,9 @@ extern "C" {
 #define NK_PRECOND_GMRES 3 /* z = gmres(J, v; itmax): the GmresPreconditioner of examples/bratu.jl:139-157
                               (Krylov.jl gmres defaults: memory 20, no restart, atol = rtol = √eps), run
                               in `inner` (an NK_ALGO_GMRES workspace of the problem's grid)              */
+#define NK_PRECOND_ILU0 4  /* z = (L U)^-1 v: ILU(0) of J in natural order, the `ilu(collect(J))` of examples/bratu.jl:
+                              119-137 on J's own pattern (exact LU for the 1D tridiagonal J); diag = D~ from
+                              nk_ilu0_factor.  Distributed: block Jacobi (each slab factored on its own) */
 typedef int (*nk_user_precond)(void* data, struct nk_ctx* ctx, double* out, const double* in);
 typedef struct nk_precond {
     int32_t kind;          /* NK_PRECOND_*                                   */
@@ -147,6 +150,11 @@ int nk_jv(nk_ctx* ctx, const nk_problem* p, double* out, const double* u, const 
  * kernel's arithmetic on a unit vector); reciprocal = 1 gives 1 ./ diag(J), the Jacobi preconditioner. */
 int nk_jacobian_diag(nk_ctx* ctx, const nk_problem* p, double* out, const double* u, int32_t reciprocal);
 
+/* ILU(0) factor of J(u) for NK_PRECOND_ILU0: dtilde (a grid function) receives the pivots D~ of
+ * L = I + L_J D~^-1, U = D~ + U_J (J's off-diagonals are constant per axis for the built-in kinds).
+ * bc_zero! only. */
+int nk_ilu0_factor(nk_ctx* ctx, const nk_problem* p, const double* u, double* dtilde);
+
 /* mul!(out, transpose(J), v) (src/Ariadne.jl:87-107, Enzyme reverse mode): out = J(u)^T v.  The
  * built-in residuals have symmetric Jacobians (3/5/7-point Laplacian plus a diagonal), so this is
  * the exact tangent kernel; user problems need user->JT. */
@@ -192,6 +200,11 @@ typedef struct nk_krylov_stats {
     int64_t n_matvec;             /* mul!(J) calls incl. restart residuals            */
     double u_norm;                /* ||u|| after the fused update (opts.u_update)     */
 } nk_krylov_stats;
+
+/* z = N v: Krylov.jl's mulorldiv!(z, N, v, ldiv) for one preconditioner (u, F0, jv_mode: the operator a
+ * GMRES preconditioner solves with; unused otherwise).  Synchronises. */
+int nk_precond_apply(nk_ctx* ctx, const nk_problem* p, const nk_precond* N, const double* u, const double* F0,
+                     int32_t jv_mode, double* z, const double* v);
 
 /* memory = Krylov workspace memory (GMRES restart length; default 20 like Krylov.jl). */
 int nk_workspace_create(nk_ctx* ctx, int32_t algo, const nk_problem* p, int32_t memory, nk_workspace** out);

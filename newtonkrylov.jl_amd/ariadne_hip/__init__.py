@@ -11,8 +11,8 @@ from .distributed import dist_unique_id, init_distributed, slab
 from .implicit import G_Euler_, G_Midpoint_, G_Trapezoid_, diffusion3d_, diffusion_, solve
 from .krylov import (KrylovConstructor, kaxpby_, kaxpy_, kaxpy_norm_, kcopy_, kdivcopy_, kdot, kfill_, knorm, kref_, krylov_solve_,
                      krylov_workspace, kscal_)
-from .precond import (DiagonalPreconditioner, GmresPreconditioner, Preconditioner, UserPreconditioner, gmres_preconditioner,
-                      jacobi, jacobian_diag)
+from .precond import (DiagonalPreconditioner, GmresPreconditioner, Ilu0Preconditioner, Preconditioner, UserPreconditioner,
+                      gmres_preconditioner, ilu0, jacobi, jacobian_diag)
 from .problems import (DeviceResidual, UserResidual, bc_periodic_, bc_zero_, bratu2d_, bratu_, heat2d_euler_, heat2d_midpoint_,
                        heat2d_trapezoid_, heat3d_euler_, heat3d_midpoint_, heat3d_trapezoid_)
 
@@ -21,7 +21,8 @@ __all__ = [
     "mul_", "newton_krylov", "newton_krylov_", "newton_krylov_native", "transpose", "collect", "TransposeOperator", "Context", "DeviceArray", "Grid", "default_context",
     "set_default_context", "dist_unique_id", "init_distributed", "slab", "G_Euler_", "G_Midpoint_", "G_Trapezoid_", "diffusion_", "diffusion3d_", "solve",
     "KrylovConstructor", "kaxpby_", "kaxpy_", "kaxpy_norm_", "kcopy_", "kdivcopy_", "kdot", "kfill_", "knorm", "kref_",
-    "DiagonalPreconditioner", "GmresPreconditioner", "Preconditioner", "UserPreconditioner", "gmres_preconditioner",
+    "DiagonalPreconditioner", "GmresPreconditioner", "Ilu0Preconditioner", "Preconditioner", "UserPreconditioner",
+    "gmres_preconditioner", "ilu0",
     "jacobi", "jacobian_diag",
     "krylov_solve_", "krylov_workspace", "kscal_", "DeviceResidual", "UserResidual", "bc_zero_", "bratu2d_", "bratu_",
     "heat2d_euler_", "heat3d_euler_", "heat2d_midpoint_", "heat3d_midpoint_", "heat2d_trapezoid_", "heat3d_trapezoid_",

@@ -21,7 +21,7 @@ NK_USER1D, NK_USER2D, NK_USER3D = 16, 17, 18
 NK_BC_ZERO, NK_BC_PERIODIC = 0, 1
 NK_JV_EXACT, NK_JV_FD = 0, 1
 NK_ALGO_GMRES, NK_ALGO_CG, NK_ALGO_FGMRES = 0, 1, 2
-NK_PRECOND_NONE, NK_PRECOND_DIAG, NK_PRECOND_USER, NK_PRECOND_GMRES = 0, 1, 2, 3
+NK_PRECOND_NONE, NK_PRECOND_DIAG, NK_PRECOND_USER, NK_PRECOND_GMRES, NK_PRECOND_ILU0 = 0, 1, 2, 3, 4
 
 _ERRORS = {-1: "HIP error", -2: "invalid argument", -3: "out of device memory", -4: "RCCL error", -5: "bad state", -6: "user callback failed"}
 
@@ -104,6 +104,8 @@ SIGNATURES = {
     "nk_jv": (C.c_int, [_VP, _PP, _VP, _VP, _VP, _VP, _I32, _D]),
     "nk_jtv": (C.c_int, [_VP, _PP, _VP, _VP, _VP]),
     "nk_jacobian_diag": (C.c_int, [_VP, _PP, _VP, _VP, _I32]),
+    "nk_ilu0_factor": (C.c_int, [_VP, _PP, _VP, _VP]),
+    "nk_precond_apply": (C.c_int, [_VP, _PP, _VP, _VP, _VP, _I32, _VP, _VP]),
     "nk_dot": (C.c_int, [_VP, _I64, _VP, _VP, _PD]),
     "nk_norm": (C.c_int, [_VP, _I64, _VP, _PD]),
     "nk_scal": (C.c_int, [_VP, _I64, _D, _VP]),

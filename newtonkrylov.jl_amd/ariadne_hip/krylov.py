@@ -156,8 +156,9 @@ def krylov_solve_(ws: KrylovWorkspace, J, b: DeviceArray, *, restart=False, reor
         raise TypeError(f"unsupported Krylov keyword(s): {sorted(unknown)}")
     if M is not None:
         raise NotImplementedError("left preconditioner M: the HIP path implements right preconditioning (N) only")
-    if ldiv:
-        raise NotImplementedError("ldiv = true: give N as the operator that approximates J^{-1} (ldiv = false)")
+    if ldiv and not getattr(N, "ldiv", False):
+        raise NotImplementedError("ldiv = true: give N as the operator that approximates J^{-1} (ldiv = false), "
+                                  "or a factorisation (ilu0)")
     if N is not None and not hasattr(N, "as_c"):
         raise TypeError("N must be an ariadne_hip preconditioner (DiagonalPreconditioner, UserPreconditioner, "
                         "GmresPreconditioner, jacobi(J))")

@@ -20,6 +20,18 @@ class Preconditioner:
     def as_c(self) -> _lib.nk_precond:
         raise NotImplementedError
 
+    def apply(self, J, v: DeviceArray, z: DeviceArray | None = None) -> DeviceArray:
+        """z = N v (Krylov.jl's mulorldiv!(z, N, v, ldiv)); J = the JacobianOperator a GMRES
+        preconditioner solves with (its u / F0 / Jv mode)."""
+        import ctypes as C
+
+        z = v.zero() if z is None else z
+        prob = J.problem()
+        F0 = J.res.ptr if J.jv_mode == _lib.NK_JV_FD else None
+        v.ctx.check(load().nk_precond_apply(v.ctx.handle, C.byref(prob), C.byref(self.as_c()), J.u.ptr, F0,
+                                            J.jv_mode, z.ptr, v.ptr), "mul!(z, N, v)")
+        return z
+
 
 class DiagonalPreconditioner(Preconditioner):
     """z = d .* v with a device grid function d (NK_PRECOND_DIAG)."""
@@ -106,3 +118,30 @@ def gmres_preconditioner(itmax: int):
         return GmresPreconditioner(J, itmax, workspace=cache[key])
 
     return factory
+
+
+class Ilu0Preconditioner(Preconditioner):
+    """`ilu(collect(J))` (examples/bratu.jl:119-137, used with krylov_kwargs = (; ldiv = true)) on the
+    device: ILU(0) of J(u) in natural order on J's own sparsity pattern -- for the 1D Bratu Jacobian
+    (tridiagonal) this is its exact LU, as IncompleteLU.jl's threshold ILU is there.  Factored once
+    (nk_ilu0_factor), applied as z = (L U)^-1 v by two wavefront sweeps (NK_PRECOND_ILU0).  A
+    factorisation: it is applied by division, so ldiv=True is accepted (and implied)."""
+
+    ldiv = True
+
+    def __init__(self, J):
+        import ctypes as C
+
+        self.J = J
+        self.d = J.u.zero()
+        prob = J.problem()
+        J.u.ctx.check(load().nk_ilu0_factor(J.u.ctx.handle, C.byref(prob), J.u.ptr, self.d.ptr), "nk_ilu0_factor")
+        self._c = _lib.nk_precond(_lib.NK_PRECOND_ILU0, self.d.ptr, _lib.NK_USER_PRECOND(), None, None, 0)
+
+    def as_c(self):
+        return self._c
+
+
+def ilu0(J) -> Ilu0Preconditioner:
+    """N factory: `N = ilu0` is the device counterpart of `N = (J) -> ilu(collect(J))`."""
+    return Ilu0Preconditioner(J)

@@ -326,6 +326,16 @@ int nk_jacobian_diag(nk_ctx* c, const nk_problem* p, double* out, const double* 
     return launch_jdiag(c, p, out, u, reciprocal);
 }
 
+int nk_ilu0_factor(nk_ctx* c, const nk_problem* p, const double* u, double* dtilde) {
+    if (!c || !dtilde || !u) return NK_E_ARG;
+    Geo g;
+    NK_TRY(geometry(c, p, &g));
+    if (nk_is_user(p->kind)) return fail(c, NK_E_ARG, "ILU(0) of a user residual: assemble it with collect(J)");
+    if (p->bc == NK_BC_PERIODIC) return fail(c, NK_E_ARG, "ILU(0) is implemented for bc_zero! (the wrap breaks the banded pattern)");
+    NK_TRY(launch_jdiag(c, p, dtilde, u, 0));
+    return launch_ilu0_factor(c, p, g.dim, dtilde);
+}
+
 int nk_jtv(nk_ctx* c, const nk_problem* p, double* out, const double* u, const double* v) {
     if (!c || !out || !u || !v) return NK_E_ARG;
     Geo g;

@@ -1715,6 +1715,106 @@ int launch_jdiag(nk_ctx* c, const nk_problem* p, double* out, const double* u, i
 #undef NK_JDIAG
 }
 
+// ------------------------------------------------------------------------------ ILU(0)
+// ILU(0) of the stencil Jacobian in natural order (x fastest) -- the `N = (J) -> ilu(collect(J))` of
+// examples/bratu.jl:119-137 restricted to J's own sparsity pattern.  For 3/5/7-point stencils the
+// IKJ elimination only updates the diagonal (no pattern entry of a lower neighbour is an upper
+// neighbour of another), so the factor is L = I + L_A D~^-1, U = D~ + U_A with
+//   D~_i = ((a_ii - (c_z / D~_b) c_z) - (c_y / D~_s) c_y) - (c_x / D~_w) c_x     (lower neighbours in
+// increasing index order: below, south, west; c_* = the constant off-diagonals of J).  Point i
+// depends on its lower neighbours only, so every anti-diagonal level x + y + z = L is independent:
+// one work-group sweeps the levels with a barrier in between (the same arithmetic, in the same
+// order per point, as the oracle's sequential loop -- bit-identical).  A block-Jacobi factor when
+// distributed: each slab is factored on its own (no ghost couplings).
+struct IluArgs {
+    int64_t nx, ny, nz;
+    double cx, cy, cz;  // off-diagonal entries of J along x, y, z
+};
+
+template <typename F>
+__device__ __forceinline__ void ilu_levels(const IluArgs& I, bool reverse, F&& f) {
+    const int64_t nlev = (I.nx - 1) + (I.ny - 1) + (I.nz - 1) + 1;
+    const int64_t nyz = I.ny * I.nz;
+    for (int64_t t = 0; t < nlev; ++t) {
+        const int64_t L = reverse ? nlev - 1 - t : t;
+        // the (y, z) pairs whose x = L - y - z lies in [0, nx)
+        const int64_t zlo = L - (I.nx - 1) - (I.ny - 1) > 0 ? L - (I.nx - 1) - (I.ny - 1) : 0;
+        const int64_t zhi = L < I.nz - 1 ? L : I.nz - 1;
+        const int64_t cnt = (zhi - zlo + 1) * I.ny;
+        for (int64_t q = threadIdx.x; q < cnt && cnt > 0; q += blockDim.x) {
+            const int64_t z = zlo + q / I.ny, y = q % I.ny, x = L - y - z;
+            if (x >= 0 && x < I.nx) f(x, y, z, (z * I.ny + y) * I.nx + x);
+        }
+        (void)nyz;
+        __syncthreads();
+    }
+}
+
+// d: on entry diag(J) (nk_jacobian_diag), on exit D~
+__global__ __launch_bounds__(1024) void k_ilu0_factor(IluArgs I, double* __restrict__ d) {
+    ilu_levels(I, false, [&](int64_t x, int64_t y, int64_t z, int64_t i) {
+        double a = d[i];
+        if (z > 0) a = a - (I.cz / d[i - I.nx * I.ny]) * I.cz;
+        if (y > 0) a = a - (I.cy / d[i - I.nx]) * I.cy;
+        if (x > 0) a = a - (I.cx / d[i - 1]) * I.cx;
+        d[i] = a;
+    });
+}
+
+// z = U^-1 L^-1 v: forward sweep y_i = ((v_i - l_b y_b) - l_s y_s) - l_w y_w (into z), then the
+// backward sweep z_i = (((y_i - c_x z_e) - c_y z_n) - c_z z_t) / D~_i
+__global__ __launch_bounds__(1024) void k_ilu0_solve(IluArgs I, const double* __restrict__ d, double* __restrict__ zz,
+                                                     const double* __restrict__ v) {
+    ilu_levels(I, false, [&](int64_t x, int64_t y, int64_t z, int64_t i) {
+        double a = v[i];
+        if (z > 0) a = a - (I.cz / d[i - I.nx * I.ny]) * zz[i - I.nx * I.ny];
+        if (y > 0) a = a - (I.cy / d[i - I.nx]) * zz[i - I.nx];
+        if (x > 0) a = a - (I.cx / d[i - 1]) * zz[i - 1];
+        zz[i] = a;
+    });
+    ilu_levels(I, true, [&](int64_t x, int64_t y, int64_t z, int64_t i) {
+        double a = zz[i];
+        if (x + 1 < I.nx) a = a - I.cx * zz[i + 1];
+        if (y + 1 < I.ny) a = a - I.cy * zz[i + I.nx];
+        if (z + 1 < I.nz) a = a - I.cz * zz[i + I.nx * I.ny];
+        zz[i] = a / d[i];
+    });
+}
+
+// off-diagonal entry of J along one axis: the exact tangent at point i of the unit vector on its
+// neighbour (the entry collect(J) holds): lap = f / h^2 with f = 1 ((1 - α) for G_Midpoint!), the
+// other axes add +0, Bratu adds λ (e^u · 0) = +0, heat: (Δt or Δt/2) (a lap) - 0
+double ilu_offdiag(const nk_problem* p, double h) {
+    const int sch = nk_is_heat(p->kind) ? nk_scheme(p->kind) : 0;
+    const double f = sch == 1 ? (1.0 - p->alpha) * 1.0 : 1.0;
+    const double lsum = ((f - 2.0 * 0.0) + 0.0) / (h * h);
+    if (!nk_is_heat(p->kind)) return lsum;
+    return (sch == 2 ? p->dt / 2.0 : p->dt) * (p->a * lsum) - 0.0;
+}
+
+IluArgs ilu_args(const nk_problem* p, int dim) {
+    IluArgs I{};
+    I.nx = p->nx; I.ny = p->ny; I.nz = p->nz;
+    I.cx = ilu_offdiag(p, p->hx);
+    I.cy = dim >= 2 ? ilu_offdiag(p, p->hy) : 0.0;
+    I.cz = dim == 3 ? ilu_offdiag(p, p->hz) : 0.0;
+    return I;
+}
+
+int launch_ilu0_factor(nk_ctx* c, const nk_problem* p, int dim, double* d) {
+    const IluArgs I = ilu_args(p, dim);
+    return launch(c, "ilu0_factor", 16.0 * (double)(p->nx * p->ny * p->nz), [&] {
+        hipLaunchKernelGGL(k_ilu0_factor, dim3(1), dim3(1024), 0, c->stream, I, d);
+    });
+}
+
+int launch_ilu0_solve(nk_ctx* c, const nk_problem* p, int dim, const double* d, double* z, const double* v) {
+    const IluArgs I = ilu_args(p, dim);
+    return launch(c, "ilu0_solve", 48.0 * (double)(p->nx * p->ny * p->nz), [&] {
+        hipLaunchKernelGGL(k_ilu0_solve, dim3(1), dim3(1024), 0, c->stream, I, d, z, v);
+    });
+}
+
 int launch_cg_direction(nk_ctx* c, int64_t n, double beta, double* p, const double* r) {
     NK_STREAM_LAUNCH("cg_direction", 24.0, k_cg_direction, n, beta, p, r);
 }

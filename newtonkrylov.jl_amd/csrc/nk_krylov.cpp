@@ -205,6 +205,12 @@ int apply_precond(nk_ctx* c, const nk_problem* p, const nk_precond* N, Op& A, in
         NK_TRY(launch(c, "precond_user", 0.0, [&] { rc = N->apply(N->data, c, z, v); }));
         if (rc != 0) return fail(c, NK_E_USER, "user preconditioner callback returned " + std::to_string(rc));
         if (need_norm) NK_TRY(launch_sumsq(c, n, z, &rz));
+    } else if (N->kind == NK_PRECOND_ILU0) {
+        if (!N->diag) return fail(c, NK_E_ARG, "ILU(0) preconditioner without its factor (nk_ilu0_factor)");
+        Geo g;
+        NK_TRY(geometry(c, p, &g));
+        NK_TRY(launch_ilu0_solve(c, p, g.dim, N->diag, z, v));
+        if (need_norm) NK_TRY(launch_sumsq(c, n, z, &rz));
     } else if (N->kind == NK_PRECOND_GMRES) {
         if (!N->inner || N->inner->algo != NK_ALGO_GMRES || N->inner->n != n)
             return fail(c, NK_E_ARG, "GMRES preconditioner needs a GMRES workspace of the problem's size");
@@ -525,6 +531,29 @@ int cg(nk_workspace* ws, Op& A, const double* b, const nk_krylov_opts* o, nk_kry
 using namespace nk;
 
 extern "C" {
+
+int nk_precond_apply(nk_ctx* c, const nk_problem* p, const nk_precond* N, const double* u, const double* F0,
+                     int32_t jv_mode, double* z, const double* v) {
+    if (!c || !p || !N || !z || !v) return NK_E_ARG;
+    Geo g;
+    NK_TRY(geometry(c, p, &g));
+    if (N->kind == NK_PRECOND_NONE) return launch_copy(c, g.n, z, v);
+    if (N->kind == NK_PRECOND_GMRES && (!u || (jv_mode == NK_JV_FD && !F0)))
+        return fail(c, NK_E_ARG, "the GMRES preconditioner needs the operator's u (and F0 for FD)");
+    Op A{c, p, jv_mode, u, F0, 0.0};
+    if (N->kind == NK_PRECOND_GMRES) {
+        NK_TRY(halo_exchange(c, p, u));
+        NK_TRY(exchange_un(c, p));
+        if (jv_mode == NK_JV_FD) {
+            Red ru{};
+            NK_TRY(launch_sumsq(c, g.n, u, &ru));
+            NK_TRY(host_scalar(c, ru, 1, &A.unorm));
+        }
+    }
+    double dummy = 0.0;
+    NK_TRY(apply_precond(c, p, N, A, g.n, z, v, false, &dummy));
+    return nk_sync(c);
+}
 
 int nk_workspace_create(nk_ctx* c, int32_t algo, const nk_problem* p, int32_t memory, nk_workspace** out) {
     if (!c || !p || !out) return NK_E_ARG;

@@ -45,15 +45,17 @@ enum { OC_FORCING_NONE = 0, OC_FORCING_FIXED = 1, OC_FORCING_EW = 2 };
 enum { OC_ALGO_GMRES = 0, OC_ALGO_CG = 1, OC_ALGO_FGMRES = 2 };
 /* right preconditioner N (Krylov.jl's `N`, ldiv = false):  DIAG z = d .* v (Jacobi: d = 1 ./ diag(J));
  * GMRES: z = gmres(J, v; itmax) -- the GmresPreconditioner of examples/bratu.jl:139-157 */
-enum { OC_PRECOND_NONE = 0, OC_PRECOND_DIAG = 1, OC_PRECOND_GMRES = 3, OC_PRECOND_JACOBI = 4 };
+enum { OC_PRECOND_NONE = 0, OC_PRECOND_DIAG = 1, OC_PRECOND_GMRES = 3, OC_PRECOND_JACOBI = 4, OC_PRECOND_ILU0 = 5,
+       OC_PRECOND_ILU = 6 /* Newton factory: ILU(0) of J(u) each step */ };
 
 typedef struct {
     int32_t kind;           /* OC_PRECOND_DIAG / OC_PRECOND_GMRES */
     int32_t itmax;          /* GMRES: the inner solve's itmax */
-    const double* diag;     /* DIAG */
+    const double* diag;     /* DIAG: d;  ILU0: the pivots D~ */
+    const struct oc_problem* P;  /* ILU0: J's off-diagonals */
 } oc_precond;
 
-typedef struct {
+typedef struct oc_problem {
     int32_t kind;
     int32_t bc;             /* OC_BC_ZERO (bc_zero!) or OC_BC_PERIODIC (bc_periodic!), heat kinds */
     int64_t nx, ny, nz;
@@ -384,12 +386,72 @@ void oc_jacobian_diag(const oc_problem* P, double* out, const double* u, int rec
 int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_krylov_stats* st,
              double* hist, int64_t hist_cap, int64_t* hist_len);
 
+/* ILU(0) of J in natural order (x fastest) on J's own pattern -- `ilu(collect(J))` of
+ * examples/bratu.jl:119-137 without fill (for the 1D tridiagonal J this is the exact LU).  IKJ
+ * elimination: for the 3/5/7-point stencil it only updates the diagonal,
+ *   D~_i = ((a_ii - (c_z / D~_b) c_z) - (c_y / D~_s) c_y) - (c_x / D~_w) c_x,
+ * lower neighbours in increasing index order; c_* = J's constant off-diagonal entry per axis (the
+ * exact tangent at i of the unit vector on the neighbour: f / h^2, f = 1 or G_Midpoint!'s 1 - α). */
+static double ilu_offdiag(const oc_problem* P, double h) {
+    const int heat = P->kind >= OC_HEAT2D_EULER && P->kind <= OC_HEAT3D_TRAPEZOID;
+    const int sch = heat ? oc_scheme(P->kind) : 0;
+    const double f = sch == 1 ? (1.0 - P->alpha) * 1.0 : 1.0;
+    const double lsum = ((f - 2.0 * 0.0) + 0.0) / (h * h);
+    if (!heat) return lsum;
+    return (sch == 2 ? P->dt / 2.0 : P->dt) * (P->a * lsum) - 0.0;
+}
+static int oc_dim(const oc_problem* P) {
+    return P->kind == OC_BRATU1D ? 1 : (P->kind == OC_BRATU2D ? 2 : oc_heat_dim(P->kind));
+}
+void oc_ilu0_factor(const oc_problem* P, const double* u, double* d) {
+    const int64_t nx = P->nx, ny = P->ny, nz = P->nz;
+    const int dim = oc_dim(P);
+    const double cx = ilu_offdiag(P, P->hx), cy = dim >= 2 ? ilu_offdiag(P, P->hy) : 0.0,
+                 cz = dim == 3 ? ilu_offdiag(P, P->hz) : 0.0;
+    oc_jacobian_diag(P, d, u, 0);
+    for (int64_t k = 0; k < nz; ++k)
+        for (int64_t j = 0; j < ny; ++j)
+            for (int64_t i = 0; i < nx; ++i) {
+                const int64_t q = (k * ny + j) * nx + i;
+                double a = d[q];
+                if (k > 0) a = a - (cz / d[q - nx * ny]) * cz;
+                if (j > 0) a = a - (cy / d[q - nx]) * cy;
+                if (i > 0) a = a - (cx / d[q - 1]) * cx;
+                d[q] = a;
+            }
+}
+/* z = U^-1 L^-1 v */
+void oc_ilu0_solve(const oc_problem* P, const double* d, double* z, const double* v) {
+    const int64_t nx = P->nx, ny = P->ny, nz = P->nz, n = nx * ny * nz;
+    const int dim = oc_dim(P);
+    const double cx = ilu_offdiag(P, P->hx), cy = dim >= 2 ? ilu_offdiag(P, P->hy) : 0.0,
+                 cz = dim == 3 ? ilu_offdiag(P, P->hz) : 0.0;
+    for (int64_t q = 0; q < n; ++q) {
+        const int64_t i = q % nx, j = (q / nx) % ny, k = q / (nx * ny);
+        double a = v[q];
+        if (k > 0) a = a - (cz / d[q - nx * ny]) * z[q - nx * ny];
+        if (j > 0) a = a - (cy / d[q - nx]) * z[q - nx];
+        if (i > 0) a = a - (cx / d[q - 1]) * z[q - 1];
+        z[q] = a;
+    }
+    for (int64_t q = n - 1; q >= 0; --q) {
+        const int64_t i = q % nx, j = (q / nx) % ny, k = q / (nx * ny);
+        double a = z[q];
+        if (i + 1 < nx) a = a - cx * z[q + 1];
+        if (j + 1 < ny) a = a - cy * z[q + nx];
+        if (k + 1 < nz) a = a - cz * z[q + nx * ny];
+        z[q] = a / d[q];
+    }
+}
+
 /* z = N v */
 static void prec_apply(oc_op* A, const oc_precond* N, double* z, const double* v) {
     const int64_t n = oc_n(A->P);
     if (N->kind == OC_PRECOND_DIAG) {
 #pragma omp parallel for schedule(static)
         for (int64_t i = 0; i < n; ++i) z[i] = N->diag[i] * v[i];
+    } else if (N->kind == OC_PRECOND_ILU0) {
+        oc_ilu0_solve(N->P ? N->P : A->P, N->diag, z, v);
     } else { /* mul!(y, P::GmresPreconditioner, x): sol, _ = gmres(P.J, x; P.itmax); copyto!(y, sol) -- Krylov's
                 gmres defaults: memory 20, no restart, atol = rtol = √eps, x0 = 0 */
         oc_krylov_opts io = {20, 0, 0, N->itmax, sqrt(DBL_EPSILON), sqrt(DBL_EPSILON), 0, NULL};
@@ -646,7 +708,7 @@ int oc_newton_krylov(const oc_problem* P, double* u, const oc_newton_opts* o, oc
     const int64_t n = oc_n(P);
     double* res = (double*)malloc(sizeof(double) * n);
     double* d = (double*)malloc(sizeof(double) * n);
-    double* dinv = o->precond == OC_PRECOND_JACOBI ? (double*)malloc(sizeof(double) * n) : NULL;
+    double* dinv = (o->precond == OC_PRECOND_JACOBI || o->precond == OC_PRECOND_ILU) ? (double*)malloc(sizeof(double) * n) : NULL;
     oc_op A = {P, o->jv_mode, u, res, 0.0, 0};
     int64_t nres_count = 0;
     oc_residual(P, res, u);
@@ -667,10 +729,14 @@ int oc_newton_krylov(const oc_problem* P, double* u, const oc_newton_opts* o, oc
         memset(&ks, 0, sizeof ks);
         if (o->jv_mode == OC_JV_FD) A.unorm = oc_norm(n, u);
         /* N = factory(J) for this step (Ariadne.jl:318-333 passes N through to krylov_solve!) */
-        oc_precond Np = {OC_PRECOND_NONE, o->precond_itmax, NULL};
+        oc_precond Np = {OC_PRECOND_NONE, o->precond_itmax, NULL, P};
         if (o->precond == OC_PRECOND_JACOBI) {
             oc_jacobian_diag(P, dinv, u, 1);
             Np.kind = OC_PRECOND_DIAG;
+            Np.diag = dinv;
+        } else if (o->precond == OC_PRECOND_ILU) {
+            oc_ilu0_factor(P, u, dinv);
+            Np.kind = OC_PRECOND_ILU0;
             Np.diag = dinv;
         } else if (o->precond == OC_PRECOND_GMRES) {
             Np.kind = OC_PRECOND_GMRES;

@@ -33,7 +33,7 @@ HEAT_KINDS = {  # (scheme, dim) -> kind; schemes of examples/implicit.jl:8-37
 JV_EXACT, JV_FD = 0, 1
 FORCING_NONE, FORCING_FIXED, FORCING_EW = 0, 1, 2
 ALGO_GMRES, ALGO_CG, ALGO_FGMRES = 0, 1, 2
-PRECOND_NONE, PRECOND_DIAG, PRECOND_GMRES, PRECOND_JACOBI = 0, 1, 3, 4
+PRECOND_NONE, PRECOND_DIAG, PRECOND_GMRES, PRECOND_JACOBI, PRECOND_ILU0, PRECOND_ILU = 0, 1, 3, 4, 5, 6
 _ALGO = {"gmres": ALGO_GMRES, "cg": ALGO_CG, "fgmres": ALGO_FGMRES}
 SQRT_EPS = math.sqrt(np.finfo(np.float64).eps)
 
@@ -47,7 +47,7 @@ class _Problem(C.Structure):
 
 
 class _Precond(C.Structure):
-    _fields_ = [("kind", C.c_int32), ("itmax", C.c_int32), ("diag", C.POINTER(C.c_double))]
+    _fields_ = [("kind", C.c_int32), ("itmax", C.c_int32), ("diag", C.POINTER(C.c_double)), ("P", C.c_void_p)]
 
 
 class _KrylovOpts(C.Structure):
@@ -107,6 +107,8 @@ def lib():
                                        P, I64, C.POINTER(I64)]
         L.oc_sym_givens.argtypes = [D, D, P, P, P]
         L.oc_jacobian_diag.argtypes = [C.POINTER(_Problem), P, P, C.c_int]
+        L.oc_ilu0_factor.argtypes = [C.POINTER(_Problem), P, P]
+        L.oc_ilu0_solve.argtypes = [C.POINTER(_Problem), P, P, P]
         L.oc_set_threads.argtypes = [C.c_int]
         L.oc_get_threads.restype = C.c_int
         for name in ("oc_axpy",):
@@ -240,16 +242,35 @@ def jacobian_diag(P: Problem, u, reciprocal=False) -> np.ndarray:
     return out
 
 
+def ilu0_factor(P: Problem, u) -> np.ndarray:
+    """The pivots D~ of ILU(0) of J(u) (see nk_oracle.c oc_ilu0_factor)."""
+    u = np.ascontiguousarray(u, dtype=np.float64)
+    d = np.empty_like(u)
+    cp = P._c()
+    lib().oc_ilu0_factor(C.byref(cp), _p(u), _p(d))
+    return d
+
+
+def ilu0_solve(P: Problem, d, v) -> np.ndarray:
+    d = np.ascontiguousarray(d, dtype=np.float64)
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    z = np.empty_like(v)
+    cp = P._c()
+    lib().oc_ilu0_solve(C.byref(cp), _p(d), _p(z), _p(v))
+    return z
+
+
 def _precond(N):
-    """N = None | ("diag", d) | ("gmres", itmax) -> (_Precond or None, keep-alive)."""
+    """N = None | ("diag", d) | ("ilu0", D~) | ("gmres", itmax) -> (_Precond or None, keep-alive).
+    (ILU0 reads J's off-diagonals from the solve's own problem.)"""
     if N is None:
         return None, None
     kind, arg = N
-    if kind == "diag":
+    if kind in ("diag", "ilu0"):
         d = np.ascontiguousarray(arg, dtype=np.float64).reshape(-1)
-        return _Precond(PRECOND_DIAG, 0, _p(d)), d
+        return _Precond(PRECOND_DIAG if kind == "diag" else PRECOND_ILU0, 0, _p(d), None), d
     if kind == "gmres":
-        return _Precond(PRECOND_GMRES, int(arg), None), None
+        return _Precond(PRECOND_GMRES, int(arg), None, None), None
     raise ValueError(kind)
 
 
@@ -336,6 +357,8 @@ def newton_krylov(P: Problem, u0, *, tol_rel=1e-6, tol_abs=1e-12, max_niter=50, 
     pk, pit = PRECOND_NONE, 0
     if N == "jacobi":
         pk = PRECOND_JACOBI
+    elif N == "ilu":
+        pk = PRECOND_ILU
     elif N is not None:
         pk, pit = PRECOND_GMRES, int(N[1])
     o = _NewtonOpts(tol_rel, tol_abs, max_niter, fk, eta, eta_max, gamma,

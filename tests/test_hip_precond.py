@@ -173,3 +173,62 @@ def test_newton_preconditioned_bratu1d_config1(ctx, N, algo):
     assert r.stats.outer_iterations == so["outer_iterations"]
     assert abs(r.stats.inner_iterations - so["inner_iterations"]) <= 0.05 * so["inner_iterations"]
     np.testing.assert_allclose(u.to_numpy(), ref, rtol=0, atol=1e-6 * np.abs(ref).max())
+
+
+# ----------------------------------------------------------------------------- ILU(0)
+@pytest.mark.parametrize("case", ["bratu1d", "bratu2d", "heat3d_midpoint", "heat2d_trapezoid", "bratu2d_wide"])
+def test_ilu0_factor_and_solve_bitwise(ctx, case):
+    """nk_ilu0_factor pivots and the two wavefront sweeps against the oracle's sequential loops: the
+    same arithmetic per point in the same order -> bit-identical."""
+    rng = np.random.default_rng(3)
+    if case == "bratu1d":
+        P = oc.bratu1d(1000)
+        F, p = ah.bratu_, (P.hx, P.lam)
+    elif case.startswith("bratu2d"):
+        P = oc.bratu2d(*((300, 7) if case.endswith("wide") else (33, 21)))
+        F, p = ah.bratu2d_, (P.hx, P.hy, P.lam)
+    elif case == "heat3d_midpoint":
+        P = oc.heat3d_euler(9, 7, 5, un=rng.standard_normal((5, 7, 9)), scheme="midpoint", alpha=0.3)
+        F, p = ah.heat3d_midpoint_.with_alpha(0.3), (ah.DeviceArray.from_numpy(P.un), P.dt, None,
+                                                     (P.a, P.hx, P.hy, P.hz, ah.bc_zero_), 0.0)
+    else:
+        P = oc.heat2d_euler(17, 12, un=rng.standard_normal((12, 17)), scheme="trapezoid")
+        F, p = ah.heat2d_trapezoid_, (ah.DeviceArray.from_numpy(P.un), P.dt, None, (P.a, P.hx, P.hy, ah.bc_zero_), 0.0)
+    u0 = (oc.sin_ic(P) if P.kind in (oc.BRATU1D, oc.BRATU2D) else P.un) + 0.05 * rng.standard_normal(P.shape)
+    u = ah.DeviceArray.from_numpy(u0)
+    res = u.zero()
+    J = ah.JacobianOperator(F, res, u, p)
+    N = ah.ilu0(J)
+    d = oc.ilu0_factor(P, u0)
+    np.testing.assert_array_equal(N.d.to_numpy(), d)
+    v = rng.standard_normal(P.shape)
+    z = N.apply(J, ah.DeviceArray.from_numpy(v))  # nk_precond_apply: z = (L U)^-1 v
+    np.testing.assert_array_equal(z.to_numpy(), oc.ilu0_solve(P, d, v))
+
+
+@pytest.mark.parametrize("algo", ["gmres", "fgmres"])
+def test_newton_ilu_bratu1d_config1(ctx, algo, golden_dir):
+    """examples/bratu.jl:119-137 as written: N = (J) -> ilu(collect(J)), krylov_kwargs = (; ldiv = true),
+    1D Bratu at config-1 size.  The exact LU makes every Newton step one Krylov iteration: equal
+    Newton / Krylov counts with the oracle, the analytic solution to the discretisation error."""
+    g = np.load(f"{golden_dir}/bratu1d_n1000.npz")
+    P = oc.bratu1d(1000)
+    u0 = oc.sin_ic(P)
+    ref, so = oc.newton_krylov(P, u0, algo=algo, N="ilu")
+    u, r = ah.newton_krylov_(ah.bratu_, ah.DeviceArray.from_numpy(u0), (P.hx, P.lam), N=ah.ilu0, algo=algo,
+                             krylov_kwargs={"ldiv": True})
+    assert r.solved and so["solved"]
+    assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
+    assert r.stats.inner_iterations == r.stats.outer_iterations
+    assert np.max(np.abs(u.to_numpy() - g["true_sol"])) < 3e-4
+
+
+def test_newton_ilu_bratu2d_matches_oracle(ctx):
+    P = oc.bratu2d(48, 40)
+    u0 = oc.sin_ic(P)
+    ref, so = oc.newton_krylov(P, u0, algo="gmres", N="ilu", memory=30, restart=True)
+    u, r = ah.newton_krylov_(ah.bratu2d_, ah.DeviceArray.from_numpy(u0), (P.hx, P.hy, P.lam), N=ah.ilu0,
+                             memory=30, krylov_kwargs={"restart": True, "ldiv": True})
+    assert r.solved and so["solved"]
+    assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
+    np.testing.assert_allclose(u.to_numpy(), ref, rtol=0, atol=1e-9 * np.abs(ref).max())

@@ -322,3 +322,75 @@ def test_heat3d_schemes_periodic_eigen_decay():
         u, st = oc.newton_krylov(P, u0, tol_abs=6e-6)
         assert st["solved"] and st["inner_iterations"] == 1
         assert np.max(np.abs(u - _decay(scheme, P.dt, mu) * u0)) < 1e-10
+
+
+# ----------------------------------------------------------------------------- preconditioners
+def _dense_ilu0(J):
+    """Textbook IKJ ILU(0) on J's own sparsity pattern (dense storage, small n)."""
+    A = J.copy()
+    pat = A != 0
+    n = len(A)
+    for i in range(n):
+        for k in range(i):
+            if pat[i, k]:
+                A[i, k] = A[i, k] / A[k, k]
+                for j in range(k + 1, n):
+                    if pat[i, j]:
+                        A[i, j] = A[i, j] - A[i, k] * A[k, j]
+    return np.tril(A, -1) + np.eye(n), np.triu(A)
+
+
+@pytest.mark.parametrize("P", [oc.bratu1d(30), oc.bratu2d(7, 5),
+                               oc.heat3d_euler(4, 3, 5, un=np.zeros((5, 3, 4)), scheme="midpoint", alpha=0.3),
+                               oc.heat2d_euler(6, 4, un=np.zeros((4, 6)), scheme="trapezoid")],
+                         ids=["bratu1d", "bratu2d", "heat3d-midpoint", "heat2d-trapezoid"])
+def test_ilu0_matches_textbook_ilu0_of_collect(P):
+    """oc_ilu0_factor's pivots == the diagonal of a textbook IKJ ILU(0) of collect(J) (bit for bit);
+    the two-sweep solve == (LU)^-1 v; for the 1D tridiagonal J, L U == J (the exact LU that
+    ilu(collect(J)) is for bratu.jl's 1D problem)."""
+    u = oc.sin_ic(P) if P.kind in (oc.BRATU1D, oc.BRATU2D) else np.random.default_rng(0).standard_normal(P.shape)
+    n = P.n
+    J = np.stack([oc.jv_exact(P, u, np.eye(n)[j].reshape(P.shape)).reshape(-1) for j in range(n)], axis=1)
+    L, U = _dense_ilu0(J)
+    d = oc.ilu0_factor(P, u).reshape(-1)
+    assert np.array_equal(np.diag(U), d)
+    v = np.random.default_rng(1).standard_normal(n)
+    z = oc.ilu0_solve(P, d, v.reshape(P.shape)).reshape(-1)
+    zref = np.linalg.solve(U, np.linalg.solve(L, v))
+    assert np.max(np.abs(z - zref)) <= 1e-13 * np.max(np.abs(zref))
+    if P.kind == oc.BRATU1D:
+        assert np.max(np.abs(L @ U - J)) <= 1e-9 * np.max(np.abs(J))
+
+
+def test_ilu_preconditioned_newton_bratu1d(golden_dir):
+    """bratu.jl:119-137 (GMRES / FGMRES + ilu(collect(J))) at config-1 size: with the exact LU every
+    Newton step takes one Krylov iteration; the root is the analytic solution's discretisation
+    (bratu.jl:33-37, to the discretisation error like the unpreconditioned solve)."""
+    g = np.load(os.path.join(golden_dir, "bratu1d_n1000.npz"))
+    P = oc.bratu1d(1000)
+    u0 = oc.sin_ic(P)
+    for algo in ("gmres", "fgmres"):
+        u, st = oc.newton_krylov(P, u0, algo=algo, N="ilu")
+        assert st["solved"] and st["inner_iterations"] == st["outer_iterations"]
+        assert np.max(np.abs(u - g["true_sol"])) < 3e-4
+
+
+def test_preconditioned_gmres_restatements():
+    """gmres! with N applies N once per cycle (x += N (V y)), fgmres! stores Z_k = N V_k: for a fixed
+    diagonal N both give the same residual history; the GMRES preconditioner (bratu.jl:139-157) only
+    makes sense flexibly and cuts the outer iterations."""
+    P = oc.bratu2d(24, 20)
+    u0 = oc.sin_ic(P)
+    b = oc.residual(P, u0)
+    d = oc.jacobian_diag(P, u0, reciprocal=True)
+    kw = dict(restart=True, memory=10, itmax=60, atol=0.0, rtol=1e-10)
+    xg, sg, hg = oc.krylov_solve(P, u0, b, algo="gmres", N=("diag", d), **kw)
+    xf, sf, hf = oc.krylov_solve(P, u0, b, algo="fgmres", N=("diag", d), **kw)
+    assert sg["niter"] == sf["niter"]
+    np.testing.assert_allclose(hg[:11], hf[:11], rtol=1e-12)
+    assert np.linalg.norm(xg - xf) <= 1e-10 * np.linalg.norm(xf)
+    x0, s0, _ = oc.krylov_solve(P, u0, b, **kw)
+    x5, s5, _ = oc.krylov_solve(P, u0, b, algo="fgmres", N=("gmres", 5), **kw)
+    assert s5["solved"] and s5["niter"] < s0["niter"]
+    xs, ss, _ = oc.krylov_solve(P, u0, b, memory=100, itmax=1000, atol=0.0, rtol=1e-13)
+    assert ss["solved"] and np.linalg.norm(x5 - xs) <= 1e-8 * np.linalg.norm(xs)
