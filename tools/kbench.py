@@ -35,7 +35,7 @@ MGS = {0: "U2", 1: "U2+nt(V_i)", 2: "U4+nt(V_i)", 3: "U2+nt(V_i,V_i+1)", 4: "U4+
        5: "U2+nt(V_i) chunked", 6: "U4+nt(V_i) chunked"}
 configs = [("copy", None, None, None)]
 if "mgs" in args.what:
-    configs += [("mgs", v, 0, k) for k in (8, 16, 30) for v in MGS]
+    configs += [("mgs", v, alt, k) for k in (8, 16, 30) for v in MGS for alt in ((0, 1) if v in (5, 6) else (0,))]
 ROWS = [int(x) for x in args.rows.split(",")]
 FASTS = [int(x) for x in args.fast.split(",")]
 ST = {(2, 2): ("jv_fd_dot", 40.0), (1, 2): ("jv_exact_dot", 32.0), (0, 1): ("residual_norm", 16.0)}
