@@ -250,9 +250,50 @@ struct NkKrylovStats
     u_norm::Float64
 end
 
+# --------------------------------------------------------------------------- right preconditioners (N)
+# Ariadne passes `N` (a factory called with the step's JacobianOperator, src/Ariadne.jl:318-333) to
+# krylov_solve!.  The device counterparts of examples/bratu.jl:119-157:
+#   N = hip_jacobi                           1 ./ diag(J)
+#   N = hip_ilu0, krylov_kwargs = (; ldiv = true)   for  N = (J) -> ilu(collect(J))
+#   N = (J) -> HipGmresPreconditioner(J, 5)  the GmresPreconditioner (algo = :fgmres)
+struct NkPrecond
+    kind::Int32
+    diag::Ptr{Float64}
+    apply::Ptr{Cvoid}
+    data::Ptr{Cvoid}
+    inner::Ptr{Cvoid}   # nk_workspace* (NK_PRECOND_GMRES)
+    itmax::Int32
+end
+const NK_PRECOND_DIAG, NK_PRECOND_GMRES, NK_PRECOND_ILU0 = Int32(1), Int32(3), Int32(4)
+abstract type HipPreconditioner end
+struct HipDiagPreconditioner <: HipPreconditioner
+    d::HipVector
+    kind::Int32
+end
+nkprecond(P::HipDiagPreconditioner) = NkPrecond(P.kind, P.d.ptr, C_NULL, C_NULL, C_NULL, 0)
+function hip_jacobi(J::Ariadne.JacobianOperator)
+    d = similar(J.u)
+    check(ccall((:nk_jacobian_diag, libnkhip), Cint, (VP, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}, Int32),
+                J.u.ctx.ptr, problem(J.f, J.u, J.p), d.ptr, J.u.ptr, 1), J.u.ctx, "jacobi")
+    return HipDiagPreconditioner(d, NK_PRECOND_DIAG)
+end
+function hip_ilu0(J::Ariadne.JacobianOperator)
+    d = similar(J.u)
+    check(ccall((:nk_ilu0_factor, libnkhip), Cint, (VP, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}),
+                J.u.ctx.ptr, problem(J.f, J.u, J.p), J.u.ptr, d.ptr), J.u.ctx, "ilu0")
+    return HipDiagPreconditioner(d, NK_PRECOND_ILU0)
+end
+struct HipGmresPreconditioner <: HipPreconditioner
+    ws::Any      # HipKrylovWorkspace of the inner solve
+    itmax::Int
+end
+HipGmresPreconditioner(J::Ariadne.JacobianOperator, itmax::Integer) =
+    HipGmresPreconditioner(Krylov.krylov_workspace(:gmres, KrylovConstructor(J.res); memory = 20), itmax)
+nkprecond(P::HipGmresPreconditioner) = NkPrecond(NK_PRECOND_GMRES, C_NULL, C_NULL, C_NULL, P.ws.ptr, P.itmax)
+
 function Krylov.krylov_workspace(method::Symbol, kc::KrylovConstructor{<:HipVector}; memory::Integer = 20)
-    algo = method === :gmres ? Int32(0) : method === :cg ? Int32(1) :
-           error("HIP path implements :gmres and :cg")
+    algo = method === :gmres ? Int32(0) : method === :cg ? Int32(1) : method === :fgmres ? Int32(2) :
+           error("HIP path implements :gmres, :fgmres and :cg")
     res = kc.vm
     r = Ref{Ptr{Cvoid}}(C_NULL)
     check(ccall((:nk_workspace_create, libnkhip), Cint, (VP, Int32, Ref{NkProblem}, Int32, Ref{Ptr{Cvoid}}),
@@ -266,8 +307,13 @@ end
 
 function Krylov.krylov_solve!(ws::HipKrylovWorkspace, J::Ariadne.JacobianOperator{<:AnyHipResidual, <:HipVector}, b::HipVector;
                               restart::Bool = false, reorthogonalization::Bool = false, itmax::Integer = 0,
-                              atol::Real = sqrt(eps(Float64)), rtol::Real = sqrt(eps(Float64)), kwargs...)
-    opts = NkKrylovOpts(restart, reorthogonalization, itmax, J.f.jv, atol, rtol, 0.0, 0.0, C_NULL, C_NULL)
+                              atol::Real = sqrt(eps(Float64)), rtol::Real = sqrt(eps(Float64)),
+                              N = nothing, ldiv::Bool = false, kwargs...)
+    ldiv && !(N isa HipDiagPreconditioner && N.kind == NK_PRECOND_ILU0) &&
+        error("ldiv = true: the HIP path takes factorisations (hip_ilu0) for N")
+    Nc = N === nothing ? nothing : Ref(nkprecond(N))
+    opts = NkKrylovOpts(restart, reorthogonalization, itmax, J.f.jv, atol, rtol, 0.0, 0.0, C_NULL,
+                        Nc === nothing ? C_NULL : Ptr{Cvoid}(Base.unsafe_convert(Ptr{NkPrecond}, Nc)))
     st = Ref{NkKrylovStats}()
     hl = Ref{Int64}(0)
     F0 = J.f.jv == NK_JV_FD ? J.res.ptr : Ptr{Float64}(C_NULL)
@@ -275,6 +321,7 @@ function Krylov.krylov_solve!(ws::HipKrylovWorkspace, J::Ariadne.JacobianOperato
                 (Ptr{Cvoid}, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ref{NkKrylovOpts}, Ref{NkKrylovStats},
                  Ptr{Float64}, Int64, Ref{Int64}),
                 ws.ptr, problem(J.f, J.u, J.p), J.u.ptr, F0, b.ptr, opts, st, C_NULL, 0, hl), ws.ctx, "krylov_solve!")
+    Nc === nothing || GC.@preserve Nc nothing
     ws.stats.niter = st[].niter
     ws.stats.solved = st[].solved != 0
     return ws

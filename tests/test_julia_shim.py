@@ -13,7 +13,7 @@ from ariadne_hip import _lib
 SHIM = os.path.join(os.path.dirname(_lib.PKG_DIR), "newtonkrylov.jl_amd", "julia", "AriadneHIP.jl")
 JL_SIZE = {"Int32": 4, "Int64": 8, "Float64": 8, "Bool": 1}
 PAIRS = [("NkProblem", _lib.nk_problem), ("NkKrylovOpts", _lib.nk_krylov_opts),
-         ("NkKrylovStats", _lib.nk_krylov_stats), ("NkUserOps", _lib.nk_user_ops)]
+         ("NkKrylovStats", _lib.nk_krylov_stats), ("NkUserOps", _lib.nk_user_ops), ("NkPrecond", _lib.nk_precond)]
 
 
 def jl_fields(name):
