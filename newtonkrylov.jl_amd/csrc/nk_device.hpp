@@ -1,0 +1,164 @@
+// nk_device.hpp -- device-side primitives shared by the kernel translation units: fixed-order
+// block reductions, the peer-mailbox all-reduce (mb_send / mb_recv), the partial-sum hand-off
+// (publish).  Included by nk_kernels.hip and by every stencil instantiation unit
+// (nk_stencil_inst.hip); everything here has internal linkage, so each unit owns its own copy of
+// the g_mb binding, which mailbox_bind (nk_kernels.hip) sets in every unit.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "nk_internal.hpp"
+
+namespace nk {
+
+// mailbox binding of one rank (set by mailbox_bind)
+struct MbInfo {
+    uint64_t* self;
+    uint64_t* const* peers;
+    int rank, nranks;
+    int* err;            // pinned host flag
+    unsigned spin_limit;
+};
+
+namespace {
+
+// ------------------------------------------------------------------------------ reductions
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;  // lane 0's value is used: a fixed association order
+}
+
+// sum over the 256 threads; valid in thread 0
+__device__ __forceinline__ double block_sum(double v, double* sh) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) sh[w] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (threadIdx.x == 0) r = ((sh[0] + sh[1]) + sh[2]) + sh[3];
+    return r;
+}
+
+// fixed-order sum of in[0..len), broadcast to the whole block.  All 256 threads load (8
+// independent loads in flight each), so a block pays ~one L2 round trip, not 32 dependent ones.
+// ------------------------------------------------------------------------------ peer mailbox
+// One-shot all-reduce of a reduction scalar across ranks without a collective launch: the
+// producing kernel's last block writes its folded value into EVERY rank's mailbox (fine-grained
+// device memory, IPC-mapped over xGMI), the consuming kernel polls the nranks entries of its own
+// mailbox and sums them in rank order -- the same order on every rank, so every rank holds the
+// bit-identical scalar.  Each 64-bit value travels as two self-validating 8-byte granules
+// {epoch:32 | half:32} (cdna_hip_programming.md §6 G16, R2: no flag, no fence, no tearing).
+// Spins are bounded: a peer that never arrives sets the error flag instead of hanging the GPU.
+// one copy of g_mb per translation unit (internal linkage): mailbox_bind sets every copy
+__device__ MbInfo g_mb;
+
+__device__ __forceinline__ uint64_t* mb_cell(uint64_t* base, unsigned epoch, int rank) {
+    return base + ((size_t)(epoch % kMbSlots) * kMbRanks + rank) * 2;
+}
+
+// lanes r < nranks (first wave) send {epoch, t} to rank r
+__device__ __forceinline__ void mb_send(double t, unsigned epoch) {
+    const int l = threadIdx.x;
+    if (l < g_mb.nranks) {
+        const uint64_t bits = (uint64_t)__double_as_longlong(t);
+        const uint64_t tag = (uint64_t)epoch << 32;
+        uint64_t* cell = mb_cell(g_mb.peers[l], epoch, g_mb.rank);
+        __hip_atomic_store(cell, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(cell + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// Σ_r value_r of `epoch` in rank order, broadcast to the whole block (all threads must call)
+__device__ double mb_recv(unsigned epoch, double* sh) {
+    if (threadIdx.x < 64) {
+        const int l = threadIdx.x, nr = g_mb.nranks;
+        uint32_t half = 0;
+        if (l < 2 * nr) {
+            const uint64_t* g = mb_cell(g_mb.self, epoch, l >> 1) + (l & 1);
+            uint64_t x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            unsigned spins = 0;
+            while ((unsigned)(x >> 32) != epoch) {
+                if (++spins > g_mb.spin_limit) {
+                    __hip_atomic_store(g_mb.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    x = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+                x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            half = (uint32_t)x;
+        }
+        const uint32_t hi = __shfl_down(half, 1, 64);
+        const double v = __longlong_as_double((long long)(((uint64_t)hi << 32) | half));
+        double t = 0.0;
+        for (int r = 0; r < nr; ++r) t += __shfl(v, 2 * r, 64);  // fixed rank order
+        if (l == 0) sh[4] = t;
+    }
+    __syncthreads();
+    return sh[4];
+}
+
+// SC1 = true reads with agent-scope (sc1) loads: values other blocks of the SAME launch stored
+// write-through (publish), which this CU's L1 or this XCD's L2 may hold stale copies of.
+template <bool SC1 = false>
+__device__ __forceinline__ double ld_part(const double* p) {
+    if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return *p;
+}
+
+template <bool SC1 = false>
+__device__ __forceinline__ double reduce_input(const double* __restrict__ in, int len, double* sh) {
+    if (len < 0) return mb_recv((unsigned)(-len), sh);  // all-reduced through the peer mailbox
+    double t = 0.0;
+    int m = threadIdx.x;
+    for (; m + 7 * kBlock < len; m += 8 * kBlock) {
+        double a[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) a[r] = ld_part<SC1>(in + m + r * kBlock);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) t += a[r];
+    }
+    for (; m < len; m += kBlock) t += ld_part<SC1>(in + m);
+    t = block_sum(t, sh);
+    if (threadIdx.x == 0) sh[4] = t;
+    __syncthreads();
+    return sh[4];
+}
+
+// Block partial -> part[blockIdx.x].  With `fin` (a communicator is attached) the last block to
+// arrive also folds all partials -- the same fixed-order sum k_finalize computes -- into
+// part[kRedCap - 1], so the RCCL all-reduce can follow without a separate finaliser launch.  The
+// arrival counter lives in part[kRedCap - 2] and is reset by that last block.
+// Hand-off without fences (cdna_hip_programming.md §6 Guideline 16, R1/R2 forms): the partial is
+// stored write-through (agent-scope atomic store = sc1) and drained before the ticket; the last
+// block reads the partials with sc1 loads.  An agent-scope RELEASE fence here would write back the
+// XCD's whole L2 -- full of this kernel's streamed output -- once per block (measured: 2x slower).
+__device__ __forceinline__ void publish(double acc, double* part, int fin, double* sh) {
+    __shared__ unsigned ticket;
+    const double s = block_sum(acc, sh);
+    if (!fin) {
+        if (threadIdx.x == 0) part[blockIdx.x] = s;
+        return;
+    }
+    unsigned* cnt = reinterpret_cast<unsigned*>(part + kRedCap - 2);
+    if (threadIdx.x == 0) {  // the partial's only writer is this lane
+        __hip_atomic_store(part + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ticket = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (ticket != gridDim.x - 1) return;
+    const double t = reduce_input<true>(part, (int)gridDim.x, sh);
+    if (threadIdx.x == 0) {
+        part[kRedCap - 1] = t;
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (fin >= 2) mb_send(t, (unsigned)fin);  // fin = mailbox epoch: straight to every rank
+}
+
+__device__ __forceinline__ double lap(double c, double p, double m, double h2) { return ((p - 2.0 * c) + m) / h2; }
+
+}  // namespace
+}  // namespace nk

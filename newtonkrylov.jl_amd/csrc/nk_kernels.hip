@@ -19,783 +19,10 @@
 #include <algorithm>
 #include <cmath>
 
-#include "nk_internal.hpp"
+#include "nk_stencil.hpp"
 
 namespace nk {
 namespace {
-
-// ------------------------------------------------------------------------------ reductions
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;  // lane 0's value is used: a fixed association order
-}
-
-// sum over the 256 threads; valid in thread 0
-__device__ __forceinline__ double block_sum(double v, double* sh) {
-    v = wave_sum(v);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) sh[w] = v;
-    __syncthreads();
-    double r = 0.0;
-    if (threadIdx.x == 0) r = ((sh[0] + sh[1]) + sh[2]) + sh[3];
-    return r;
-}
-
-// fixed-order sum of in[0..len), broadcast to the whole block.  All 256 threads load (8
-// independent loads in flight each), so a block pays ~one L2 round trip, not 32 dependent ones.
-// ------------------------------------------------------------------------------ peer mailbox
-// One-shot all-reduce of a reduction scalar across ranks without a collective launch: the
-// producing kernel's last block writes its folded value into EVERY rank's mailbox (fine-grained
-// device memory, IPC-mapped over xGMI), the consuming kernel polls the nranks entries of its own
-// mailbox and sums them in rank order -- the same order on every rank, so every rank holds the
-// bit-identical scalar.  Each 64-bit value travels as two self-validating 8-byte granules
-// {epoch:32 | half:32} (cdna_hip_programming.md §6 G16, R2: no flag, no fence, no tearing).
-// Spins are bounded: a peer that never arrives sets the error flag instead of hanging the GPU.
-struct MbInfo {
-    uint64_t* self;
-    uint64_t* const* peers;
-    int rank, nranks;
-    int* err;            // pinned host flag
-    unsigned spin_limit;
-};
-__device__ MbInfo g_mb;
-
-__device__ __forceinline__ uint64_t* mb_cell(uint64_t* base, unsigned epoch, int rank) {
-    return base + ((size_t)(epoch % kMbSlots) * kMbRanks + rank) * 2;
-}
-
-// lanes r < nranks (first wave) send {epoch, t} to rank r
-__device__ __forceinline__ void mb_send(double t, unsigned epoch) {
-    const int l = threadIdx.x;
-    if (l < g_mb.nranks) {
-        const uint64_t bits = (uint64_t)__double_as_longlong(t);
-        const uint64_t tag = (uint64_t)epoch << 32;
-        uint64_t* cell = mb_cell(g_mb.peers[l], epoch, g_mb.rank);
-        __hip_atomic_store(cell, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(cell + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
-// Σ_r value_r of `epoch` in rank order, broadcast to the whole block (all threads must call)
-__device__ double mb_recv(unsigned epoch, double* sh) {
-    if (threadIdx.x < 64) {
-        const int l = threadIdx.x, nr = g_mb.nranks;
-        uint32_t half = 0;
-        if (l < 2 * nr) {
-            const uint64_t* g = mb_cell(g_mb.self, epoch, l >> 1) + (l & 1);
-            uint64_t x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            unsigned spins = 0;
-            while ((unsigned)(x >> 32) != epoch) {
-                if (++spins > g_mb.spin_limit) {
-                    __hip_atomic_store(g_mb.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    x = 0;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-                x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-            half = (uint32_t)x;
-        }
-        const uint32_t hi = __shfl_down(half, 1, 64);
-        const double v = __longlong_as_double((long long)(((uint64_t)hi << 32) | half));
-        double t = 0.0;
-        for (int r = 0; r < nr; ++r) t += __shfl(v, 2 * r, 64);  // fixed rank order
-        if (l == 0) sh[4] = t;
-    }
-    __syncthreads();
-    return sh[4];
-}
-
-// SC1 = true reads with agent-scope (sc1) loads: values other blocks of the SAME launch stored
-// write-through (publish), which this CU's L1 or this XCD's L2 may hold stale copies of.
-template <bool SC1 = false>
-__device__ __forceinline__ double ld_part(const double* p) {
-    if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return *p;
-}
-
-template <bool SC1 = false>
-__device__ __forceinline__ double reduce_input(const double* __restrict__ in, int len, double* sh) {
-    if (len < 0) return mb_recv((unsigned)(-len), sh);  // all-reduced through the peer mailbox
-    double t = 0.0;
-    int m = threadIdx.x;
-    for (; m + 7 * kBlock < len; m += 8 * kBlock) {
-        double a[8];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) a[r] = ld_part<SC1>(in + m + r * kBlock);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) t += a[r];
-    }
-    for (; m < len; m += kBlock) t += ld_part<SC1>(in + m);
-    t = block_sum(t, sh);
-    if (threadIdx.x == 0) sh[4] = t;
-    __syncthreads();
-    return sh[4];
-}
-
-// Block partial -> part[blockIdx.x].  With `fin` (a communicator is attached) the last block to
-// arrive also folds all partials -- the same fixed-order sum k_finalize computes -- into
-// part[kRedCap - 1], so the RCCL all-reduce can follow without a separate finaliser launch.  The
-// arrival counter lives in part[kRedCap - 2] and is reset by that last block.
-// Hand-off without fences (cdna_hip_programming.md §6 Guideline 16, R1/R2 forms): the partial is
-// stored write-through (agent-scope atomic store = sc1) and drained before the ticket; the last
-// block reads the partials with sc1 loads.  An agent-scope RELEASE fence here would write back the
-// XCD's whole L2 -- full of this kernel's streamed output -- once per block (measured: 2x slower).
-__device__ __forceinline__ void publish(double acc, double* part, int fin, double* sh) {
-    __shared__ unsigned ticket;
-    const double s = block_sum(acc, sh);
-    if (!fin) {
-        if (threadIdx.x == 0) part[blockIdx.x] = s;
-        return;
-    }
-    unsigned* cnt = reinterpret_cast<unsigned*>(part + kRedCap - 2);
-    if (threadIdx.x == 0) {  // the partial's only writer is this lane
-        __hip_atomic_store(part + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        ticket = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (ticket != gridDim.x - 1) return;
-    const double t = reduce_input<true>(part, (int)gridDim.x, sh);
-    if (threadIdx.x == 0) {
-        part[kRedCap - 1] = t;
-        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (fin >= 2) mb_send(t, (unsigned)fin);  // fin = mailbox epoch: straight to every rank
-}
-
-__device__ __forceinline__ double lap(double c, double p, double m, double h2) { return ((p - 2.0 * c) + m) / h2; }
-
-struct KArgs {
-    double* out;
-    const double* u;
-    const double* v;
-    const double* F0;
-    const double* un;
-    const double* aux;
-    double* part;
-    int64_t nx, ny, nz;
-    double hx2, hy2, hz2, lam, a, dt, eps;
-    int tiles_x, tiles_y, rows;
-    int fast;            // 1: multiply by reciprocals instead of dividing (measurement variant, not bit-faithful)
-    double ihx2, ihy2, ihz2, ieps;
-    // fused Arnoldi normalisation: the stencil input is v = src / *vdiv (kdivcopy!, bit-identical),
-    // and the block's own points of v are stored to vout (V_k) -- saves the separate divcopy pass
-    const double* vdiv;
-    double* vout;
-    double hd;           // *vdiv, loaded once per block
-    int fin;             // fold the partials in-kernel (publish)
-    double alpha;        // G_Midpoint! α
-};
-
-// implicit.jl scheme of a heat kind: 0 G_Euler! (and the Bratu kinds), 1 G_Midpoint!, 2 G_Trapezoid!
-template <int KIND>
-constexpr int scheme_of() {
-    return (KIND == NK_HEAT2D_MIDPOINT || KIND == NK_HEAT3D_MIDPOINT)
-               ? 1
-               : ((KIND == NK_HEAT2D_TRAPEZOID || KIND == NK_HEAT3D_TRAPEZOID) ? 2 : 0);
-}
-template <int KIND>
-constexpr bool heat_kind() {
-    return KIND >= NK_HEAT2D_EULER && KIND <= NK_HEAT3D_TRAPEZOID;
-}
-
-__device__ __forceinline__ double vin(const KArgs& A, int64_t o) {
-    const double v = A.v[o];
-    return A.vdiv ? v / A.hd : v;
-}
-
-// ((p - 2c) + m) / h^2 exactly as the reference writes it; `fast` multiplies by 1/h^2 instead
-__device__ __forceinline__ double lapk(const KArgs& A, double c, double p, double m, double h2, double ih2) {
-    const double s = (p - 2.0 * c) + m;
-    return (A.fast & 1) ? s * ih2 : s / h2;
-}
-
-template <int MODE>
-__device__ __forceinline__ double fieldval(const KArgs& A, int64_t o) {
-    if (MODE == MODE_RES) return A.u[o];
-    if (MODE == MODE_JEXACT) return vin(A, o);
-    return A.u[o] + A.eps * vin(A, o);  // w = u + eps v
-}
-
-template <int MODE, int VEC>
-__device__ __forceinline__ void fieldvec(const KArgs& A, int64_t o, double* f) {
-    if (VEC == 2) {
-        if (MODE == MODE_RES) {
-            const double2 q = *reinterpret_cast<const double2*>(A.u + o);
-            f[0] = q.x; f[1] = q.y;
-        } else if (MODE == MODE_JEXACT) {
-            const double2 q = *reinterpret_cast<const double2*>(A.v + o);
-            f[0] = q.x; f[1] = q.y;
-        } else {
-            const double2 qu = *reinterpret_cast<const double2*>(A.u + o);
-            const double2 qv = *reinterpret_cast<const double2*>(A.v + o);
-            f[0] = qu.x + A.eps * qv.x;
-            f[1] = qu.y + A.eps * qv.y;
-        }
-    } else {
-        f[0] = fieldval<MODE>(A, o);
-    }
-}
-
-template <int VEC>
-__device__ __forceinline__ void loadvec(const double* __restrict__ p, int64_t o, double* f) {
-    if (VEC == 2) {
-        const double2 q = *reinterpret_cast<const double2*>(p + o);
-        f[0] = q.x; f[1] = q.y;
-    } else {
-        f[0] = p[o];
-    }
-}
-
-template <int VEC>
-__device__ __forceinline__ void storevec(double* __restrict__ p, int64_t o, const double* f) {
-    if (VEC == 2) {
-        *reinterpret_cast<double2*>(p + o) = make_double2(f[0], f[1]);
-    } else {
-        p[o] = f[0];
-    }
-}
-
-// residual / JVP value at one point from the stencil field (c + neighbours) and centre data.
-// lsum = Laplacian-like sum of the stencil field in the reference's association order.  Heat kinds:
-// xc = the centre of w = u (+ eps v) -- or of v for the tangent -- before G_Midpoint!'s mixing (the
-// "- u" term), unc = u_n, lsumg = the Laplacian sum of u_n (G_Trapezoid!'s du(u_n)).  du = a * lsum:
-//   Euler      (u_n + Δt du(w)) - w                      tangent  Δt (a lap(v)) - v
-//   Midpoint   (u_n + Δt du(α u_n + (1-α) w)) - w        tangent  Δt (a lap((1-α) v)) - v
-//   Trapezoid  (u_n + (Δt/2) (du(u_n) + du(w))) - w      tangent  (Δt/2) (a lap(v)) - v
-template <int KIND, int MODE>
-__device__ __forceinline__ double point_value(const KArgs& A, double c, double lsum, double uc, double unc, double f0c,
-                                              double xc, double lsumg) {
-    if constexpr (KIND == NK_BRATU1D || KIND == NK_BRATU2D) {
-        if (MODE == MODE_JEXACT) return lsum + A.lam * (exp(uc) * c);  // Enzyme tangent of λ exp(u)
-        const double r = lsum + A.lam * exp(c);
-        return MODE == MODE_JFD ? ((A.fast & 1) ? (r - f0c) * A.ieps : (r - f0c) / A.eps) : r;
-    } else {  // implicit.jl:8-37
-        constexpr int SCH = scheme_of<KIND>();
-        if (MODE == MODE_JEXACT) return (SCH == 2 ? A.dt / 2.0 : A.dt) * (A.a * lsum) - xc;
-        const double r = SCH == 2 ? (unc + (A.dt / 2.0) * (A.a * lsumg + A.a * lsum)) - xc
-                                  : (unc + A.dt * (A.a * lsum)) - xc;
-        return MODE == MODE_JFD ? ((A.fast & 1) ? (r - f0c) * A.ieps : (r - f0c) / A.eps) : r;
-    }
-}
-
-template <int EPI>
-__device__ __forceinline__ double epilogue(double& val, double ax, double acc) {
-    if (EPI == EPI_SUMSQ) return fma(val, val, acc);
-    if (EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_DOTVS) return fma(ax, val, acc);
-    if (EPI == EPI_RESID) {
-        val = ax - val;  // w = b - A x  (kaxpby!(n, 1, b, -1, w))
-        return fma(val, val, acc);
-    }
-    return acc;
-}
-
-// ------------------------------------------------------------------------------ 1D stencil
-template <int MODE, int EPI>
-__global__ __launch_bounds__(kBlock) void k_st1d(KArgs A0) {
-    __shared__ double sh[8];
-    KArgs A = A0;
-    A.hd = A.vdiv ? *A.vdiv : 1.0;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    double acc = 0.0;
-    if (i < A.nx) {
-        // ghost cells at -1 and nx exist (zero Dirichlet) -- examples/bratu.jl:17-18
-        const double c = fieldval<MODE>(A, i), l = fieldval<MODE>(A, i - 1), r = fieldval<MODE>(A, i + 1);
-        const double uc = (MODE == MODE_JEXACT) ? A.u[i] : 0.0;
-        const double f0 = (MODE == MODE_JFD) ? A.F0[i] : 0.0;
-        double val = point_value<NK_BRATU1D, MODE>(A, c, lap(c, r, l, A.hx2), uc, 0.0, f0, c, 0.0);
-        const double ax = (EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID) ? A.aux[i]
-                          : (EPI == EPI_DOTVS ? A.v[i] / A.hd : 0.0);
-        acc = epilogue<EPI>(val, ax, acc);
-        A.out[i] = val;
-        if constexpr (MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS)) A.vout[i] = A.v[i] / A.hd;
-    }
-    if (EPI != EPI_NONE) publish(acc, A.part, A.fin, sh);
-}
-
-// ------------------------------------------------------------------------------ row fragments
-// VEC consecutive x-points of one row, held by value (no address taken -> stays in VGPRs).
-template <int VEC>
-struct Row {
-    double v[VEC];
-};
-
-template <int MODE, int VEC>
-__device__ __forceinline__ Row<VEC> field_row(const KArgs& A, int64_t o, bool ok) {
-    Row<VEC> r;
-    if (ok) {
-        if constexpr (VEC % 2 == 0) {
-#pragma unroll
-            for (int h = 0; h < VEC; h += 2) {
-                if constexpr (MODE == MODE_RES) {
-                    const double2 q = *reinterpret_cast<const double2*>(A.u + o + h);
-                    r.v[h] = q.x; r.v[h + 1] = q.y;
-                } else if constexpr (MODE == MODE_JEXACT) {
-                    double2 q = *reinterpret_cast<const double2*>(A.v + o + h);
-                    if (A.vdiv) { q.x = q.x / A.hd; q.y = q.y / A.hd; }
-                    r.v[h] = q.x; r.v[h + 1] = q.y;
-                } else {
-                    const double2 qu = *reinterpret_cast<const double2*>(A.u + o + h);
-                    double2 qv = *reinterpret_cast<const double2*>(A.v + o + h);
-                    if (A.vdiv) { qv.x = qv.x / A.hd; qv.y = qv.y / A.hd; }
-                    r.v[h] = qu.x + A.eps * qv.x;  // w = u + eps v
-                    r.v[h + 1] = qu.y + A.eps * qv.y;
-                }
-            }
-        } else {
-            r.v[0] = fieldval<MODE>(A, o);
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) r.v[k] = 0.0;
-    }
-    return r;
-}
-
-template <int VEC>
-__device__ __forceinline__ Row<VEC> data_row(const double* __restrict__ p, int64_t o, bool ok) {
-    Row<VEC> r;
-    if (ok) {
-        if constexpr (VEC % 2 == 0) {
-#pragma unroll
-            for (int h = 0; h < VEC; h += 2) {
-                const double2 q = *reinterpret_cast<const double2*>(p + o + h);
-                r.v[h] = q.x; r.v[h + 1] = q.y;
-            }
-        } else {
-            r.v[0] = p[o];
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) r.v[k] = 0.0;
-    }
-    return r;
-}
-
-template <int VEC>
-__device__ __forceinline__ void store_row(double* __restrict__ p, int64_t o, const Row<VEC>& r) {
-    if constexpr (VEC % 2 == 0) {
-#pragma unroll
-        for (int h = 0; h < VEC; h += 2) *reinterpret_cast<double2*>(p + o + h) = make_double2(r.v[h], r.v[h + 1]);
-    } else {
-        p[o] = r.v[0];
-    }
-}
-
-// ------------------------------------------------------------------------------ 2D stencil
-// Raw (un-cooked) loads of one row segment: VEC centre values + one "edge" value per field.  The
-// edge load is issued by every lane (no divergence): lane 0 reads column x0-1, lane 63 column
-// x0+VEC, the others re-read their own x0 (a cache-hot dummy).  No arithmetic touches the loaded
-// registers until the next iteration, so the compiler's s_waitcnt can leave them in flight.
-// Periodic kernels (PER) carry a second edge slot: *e = the left edge, *e2 = the right edge (with
-// the x-wrap one lane can need both); G = the row of u_n is loaded as well (G_Midpoint! mixes it
-// into the stencil field, G_Trapezoid! takes its Laplacian).
-template <int MODE, int VEC>
-struct RawRow {
-    double a[VEC], ae, ae2;  // u (RES, JFD) or v (JEXACT)
-    double b[VEC], be, be2;  // v (JFD)
-    double g[VEC], ge, ge2;  // u_n (G)
-};
-
-template <int MODE, int VEC, bool EDGE = true, bool G = false, bool PER = false>
-__device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o, int64_t oe, int64_t oe2 = 0) {
-    RawRow<MODE, VEC> r;
-    const double* __restrict__ pa = (MODE == MODE_JEXACT) ? A.v : A.u;
-    if constexpr (VEC % 2 == 0) {
-#pragma unroll
-        for (int h = 0; h < VEC; h += 2) {
-            const double2 q = *reinterpret_cast<const double2*>(pa + o + h);
-            r.a[h] = q.x; r.a[h + 1] = q.y;
-        }
-    } else {
-        r.a[0] = pa[o];
-    }
-    if constexpr (EDGE) r.ae = pa[oe];
-    else r.ae = 0.0;
-    if constexpr (EDGE && PER) r.ae2 = pa[oe2];
-    if constexpr (MODE == MODE_JFD) {
-        if constexpr (VEC % 2 == 0) {
-#pragma unroll
-            for (int h = 0; h < VEC; h += 2) {
-                const double2 q = *reinterpret_cast<const double2*>(A.v + o + h);
-                r.b[h] = q.x; r.b[h + 1] = q.y;
-            }
-        } else {
-            r.b[0] = A.v[o];
-        }
-        if constexpr (EDGE) r.be = A.v[oe];
-        else r.be = 0.0;
-        if constexpr (EDGE && PER) r.be2 = A.v[oe2];
-    }
-    if constexpr (G) {
-        if constexpr (VEC % 2 == 0) {
-#pragma unroll
-            for (int h = 0; h < VEC; h += 2) {
-                const double2 q = *reinterpret_cast<const double2*>(A.un + o + h);
-                r.g[h] = q.x; r.g[h + 1] = q.y;
-            }
-        } else {
-            r.g[0] = A.un[o];
-        }
-        if constexpr (EDGE) r.ge = A.un[oe];
-        else r.ge = 0.0;
-        if constexpr (EDGE && PER) r.ge2 = A.un[oe2];
-    }
-    return r;
-}
-
-// cooked stencil field of a row: centres, the lane's edge value(s), and (fused normalisation) v / h
-template <int VEC>
-struct Field {
-    double c[VEC], e, e2;    // the stencil field (G_Midpoint!: α u_n + (1-α) w); edges (e2: PER right edge)
-    double vn[VEC];          // v / h (the stored basis vector)
-    double x[VEC];           // w = u (+ eps v) or v before the midpoint mixing: the "- u" term
-    double g[VEC], ge, ge2;  // u_n (G)
-};
-
-struct WV {
-    double w, v;  // the stencil input w = u (+ eps v) or v, and v / h
-};
-template <int MODE>
-__device__ __forceinline__ WV cook_w(const KArgs& A, double ra, double rb, bool div) {
-    WV r;
-    if constexpr (MODE == MODE_RES) {
-        r.v = 0.0;
-        r.w = ra;
-    } else if constexpr (MODE == MODE_JEXACT) {
-        r.v = div ? ra / A.hd : ra;
-        r.w = r.v;
-    } else {
-        r.v = div ? rb / A.hd : rb;
-        r.w = ra + A.eps * r.v;  // w = u + eps v
-    }
-    return r;
-}
-
-template <int MODE, int SCH>
-__device__ __forceinline__ double mix(const KArgs& A, double w, double g) {
-    if constexpr (SCH != 1) return w;
-    // G_Midpoint!: uuₙ .= α .* uₙ .+ (1 - α) .* u; its tangent (u_n has a zero shadow) is (1 - α) v
-    else if constexpr (MODE == MODE_JEXACT) return (1.0 - A.alpha) * w;
-    else return A.alpha * g + (1.0 - A.alpha) * w;
-}
-
-template <int MODE, int VEC, int SCH = 0, bool G = false, bool PER = false>
-__device__ __forceinline__ Field<VEC> cook(const KArgs& A, const RawRow<MODE, VEC>& r, bool act, bool edge_ok,
-                                           bool edge_ok2 = false) {
-    Field<VEC> f;
-    const bool div = A.vdiv != nullptr;
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-        const WV q = cook_w<MODE>(A, r.a[k], MODE == MODE_JFD ? r.b[k] : 0.0, div);
-        const double w = q.w;
-        f.vn[k] = q.v;
-        f.x[k] = w;
-        f.c[k] = mix<MODE, SCH>(A, w, G ? r.g[k] : 0.0);
-        if constexpr (G) f.g[k] = r.g[k];
-        if (!act) {  // lanes past the row end act as the zero boundary for their neighbour
-            f.c[k] = 0.0;
-            if constexpr (G) f.g[k] = 0.0;
-        }
-    }
-    const double e = mix<MODE, SCH>(A, cook_w<MODE>(A, r.ae, MODE == MODE_JFD ? r.be : 0.0, div).w, G ? r.ge : 0.0);
-    f.e = edge_ok ? e : 0.0;
-    if constexpr (G) f.ge = edge_ok ? r.ge : 0.0;
-    if constexpr (PER) {
-        const double e2 = mix<MODE, SCH>(A, cook_w<MODE>(A, r.ae2, MODE == MODE_JFD ? r.be2 : 0.0, div).w, G ? r.ge2 : 0.0);
-        f.e2 = edge_ok2 ? e2 : 0.0;
-        if constexpr (G) f.ge2 = edge_ok2 ? r.ge2 : 0.0;
-    }
-    return f;
-}
-
-// x-edge geometry of one lane.  Without PER: lane 0 reads column x0-1, lane 63 column x0+VEC (zero
-// beyond the grid).  With PER (bc_periodic!): lane 0 reads its left neighbour into e (column nx-1 at
-// x0 = 0), and lane 63 -- or the lane holding the last column -- its right neighbour into e2
-// (column 0 after the last column).
-struct XEdge {
-    int64_t de, de2;
-    bool ok, ok2, rwrap;
-};
-template <int VEC, bool PER>
-__device__ __forceinline__ XEdge x_edge(int lane, bool act, int64_t x0, int64_t nx) {
-    XEdge x{};
-    if constexpr (!PER) {
-        const bool left_ok = lane == 0 && act && x0 >= 1;
-        const bool right_ok = lane == 63 && act && x0 + VEC < nx;
-        x.de = left_ok ? -1 : (right_ok ? VEC : 0);  // edge element offset (0: dummy)
-        x.ok = left_ok || right_ok;
-        x.de2 = 0;
-        x.ok2 = false;
-        x.rwrap = false;
-    } else {
-        x.ok = lane == 0 && act;
-        x.de = x.ok ? (x0 >= 1 ? -1 : nx - 1) : 0;
-        x.rwrap = act && x0 + VEC == nx;
-        x.ok2 = act && ((lane == 63 && x0 + VEC < nx) || x.rwrap);
-        x.de2 = x.ok2 ? (x.rwrap ? -x0 : VEC) : 0;
-    }
-    return x;
-}
-
-// west / east neighbours of the VEC points of a lane: lane shuffles, the wave-edge lanes' edge values
-struct LR {
-    double l, r;
-};
-template <bool PER>
-__device__ __forceinline__ LR x_nbrs(double cfirst, double clast, double e, double e2, int lane, bool rwrap) {
-    LR o;
-    o.l = __shfl_up(clast, 1, 64);
-    o.r = __shfl_down(cfirst, 1, 64);
-    if (lane == 0) o.l = e;
-    if constexpr (PER) {
-        if (lane == 63 || rwrap) o.r = e2;
-    } else {
-        if (lane == 63) o.r = e;
-    }
-    return o;
-}
-
-// Block = 256 threads x VEC columns (one row segment), marching A.rows rows in y.  Pipeline: at
-// iteration j the raw loads of row j+2 and the centre operands of row j+1 are issued, row j+1's
-// raw data (issued one iteration earlier) is cooked, and row j is computed from registers.
-template <int KIND, int MODE, int EPI, int VEC, bool PER = false>
-__global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
-    __shared__ double sh[8];
-    KArgs A = A0;
-    A.hd = A.vdiv ? *A.vdiv : 1.0;
-    constexpr int SCH = scheme_of<KIND>();
-    constexpr bool kG = SCH != 0 && MODE != MODE_JEXACT;  // u_n rows with the stencil field
-    const int lane = threadIdx.x & 63;
-    const int nb = gridDim.x, b = blockIdx.x;
-    const int t = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;  // XCD-contiguous tile bands
-    const int tx = t % A.tiles_x, ty = t / A.tiles_x;
-    const int64_t nx = A.nx, ny = A.ny;
-    const int64_t x0 = (int64_t)tx * (kBlock * VEC) + (int64_t)threadIdx.x * VEC;
-    const bool act = x0 < nx;
-    const int64_t xc = act ? x0 : 0;  // clamped column: every load stays inside the allocation
-    const XEdge xe = x_edge<VEC, PER>(lane, act, x0, nx);
-    const int64_t de = xe.de, de2 = xe.de2;
-    const bool edge_ok = xe.ok, edge_ok2 = xe.ok2;
-    const int64_t y0 = (int64_t)ty * A.rows;
-    const int64_t y1 = y0 + A.rows < ny ? y0 + A.rows : ny;
-    constexpr bool kU = MODE == MODE_JEXACT && KIND == NK_BRATU2D;
-    constexpr bool kUn = KIND == NK_HEAT2D_EULER && MODE != MODE_JEXACT;
-    constexpr bool kF0 = MODE == MODE_JFD;
-    constexpr bool kAx = EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID;
-    constexpr bool vout = MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS);  // fused kdivcopy!: V_k stored
-    double acc = 0.0;
-    if (y0 < ny) {
-        // rows y0-1 (ghost plane when y0 = 0) and y0 cooked up front; row y0+1 raw in flight
-        Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(
-            A, load_raw<MODE, VEC, true, kG, PER>(A, (y0 - 1) * nx + xc, (y0 - 1) * nx + xc + de, (y0 - 1) * nx + xc + de2),
-            act, false, false);
-        Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(
-            A, load_raw<MODE, VEC, true, kG, PER>(A, y0 * nx + xc, y0 * nx + xc + de, y0 * nx + xc + de2), act, edge_ok,
-            edge_ok2);
-        RawRow<MODE, VEC> rp =
-            load_raw<MODE, VEC, true, kG, PER>(A, (y0 + 1) * nx + xc, (y0 + 1) * nx + xc + de, (y0 + 1) * nx + xc + de2);
-        Row<VEC> uc{}, unc{}, f0c{}, ax{};
-        {
-            const int64_t o = y0 * nx + xc;
-            if constexpr (kU) uc = data_row<VEC>(A.u, o, true);
-            if constexpr (kUn) unc = data_row<VEC>(A.un, o, true);
-            if constexpr (kF0) f0c = data_row<VEC>(A.F0, o, true);
-            if constexpr (kAx) ax = data_row<VEC>(A.aux, o, true);
-        }
-        for (int64_t j = y0; j < y1; ++j) {
-            const int64_t o = j * nx + xc;
-            // ---- issue: raw row j+2 (rows up to ny are the ghost plane; y1 <= ny keeps j+2 <= ny+1
-            //      in range only when j+1 < y1, so clamp to row j+1 otherwise)
-            const int64_t o2 = (j + 1 < y1) ? o + 2 * nx : o + nx;
-            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2);
-            Row<VEC> ucn{}, uncn{}, f0cn{}, axn{};
-            const int64_t o1 = (j + 1 < y1) ? o + nx : o;
-            if constexpr (kU) ucn = data_row<VEC>(A.u, o1, true);
-            if constexpr (kUn) uncn = data_row<VEC>(A.un, o1, true);
-            if constexpr (kF0) f0cn = data_row<VEC>(A.F0, o1, true);
-            if constexpr (kAx) axn = data_row<VEC>(A.aux, o1, true);
-            // ---- cook row j+1 (its loads were issued one iteration ago)
-            const Field<VEC> fp = cook<MODE, VEC, SCH, kG, PER>(A, rp, act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
-            // ---- compute row j from registers
-            const LR xn = x_nbrs<PER>(fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
-            const double lft = xn.l, rgt = xn.r;
-            double glft = 0.0, grgt = 0.0;
-            if constexpr (SCH == 2 && kG) {
-                const LR gn = x_nbrs<PER>(fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
-                glft = gn.l;
-                grgt = gn.r;
-            }
-            if (act) {
-                Row<VEC> val;
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) {
-                    const double w = (k == 0) ? lft : fc.c[k == 0 ? 0 : k - 1];
-                    const double e = (k == VEC - 1) ? rgt : fc.c[k == VEC - 1 ? k : k + 1];
-                    const double c = fc.c[k];
-                    const double lsum = lapk(A, c, e, w, A.hx2, A.ihx2) + lapk(A, c, fp.c[k], fm.c[k], A.hy2, A.ihy2);
-                    double lsumg = 0.0;
-                    if constexpr (SCH == 2 && kG) {
-                        const double gw = (k == 0) ? glft : fc.g[k == 0 ? 0 : k - 1];
-                        const double ge = (k == VEC - 1) ? grgt : fc.g[k == VEC - 1 ? k : k + 1];
-                        lsumg = lapk(A, fc.g[k], ge, gw, A.hx2, A.ihx2) + lapk(A, fc.g[k], fp.g[k], fm.g[k], A.hy2, A.ihy2);
-                    }
-                    const double unk = kG ? fc.g[k] : unc.v[k];
-                    double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unk, f0c.v[k], SCH == 1 ? fc.x[k] : c, lsumg);
-                    acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[k] : ax.v[k], acc);
-                    val.v[k] = r;
-                }
-                store_row<VEC>(A.out, o, val);
-                if (vout) {
-                    Row<VEC> vn;
-#pragma unroll
-                    for (int k = 0; k < VEC; ++k) vn.v[k] = fc.vn[k];
-                    store_row<VEC>(A.vout, o, vn);
-                }
-            }
-            fm = fc;
-            fc = fp;
-            rp = rpp;
-            uc = ucn;
-            unc = uncn;
-            f0c = f0cn;
-            ax = axn;
-        }
-    }
-    if constexpr (EPI != EPI_NONE) publish(acc, A.part, A.fin, sh);
-}
-
-// ------------------------------------------------------------------------------ 3D stencil
-// Block = 4 waves = 4 rows (y) x 64*VEC columns, marching A.rows planes in z.  Same pipeline as
-// the 2D kernel: at iteration k the raw loads of the centre row of plane k+2 and of the y-
-// neighbour rows of plane k+1 are issued, plane k+1's centre row and plane k's y-neighbours
-// (issued one iteration earlier) are cooked, and plane k is computed from registers.  The y-
-// neighbour rows are mostly L2 hits (the adjacent waves of the block stream them).  PER: the
-// y-neighbours of rows 0 and ny-1 wrap (bc_periodic!), x as in the 2D kernel.
-template <int KIND, int MODE, int EPI, int VEC, bool PER = false>
-__global__ __launch_bounds__(kBlock) void k_st3d(KArgs A0) {
-    __shared__ double sh[8];
-    KArgs A = A0;
-    A.hd = A.vdiv ? *A.vdiv : 1.0;
-    constexpr int SCH = scheme_of<KIND>();
-    constexpr bool kG = SCH != 0 && MODE != MODE_JEXACT;
-    const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
-    const int nb = gridDim.x, b = blockIdx.x;
-    const int t = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;
-    const int tpl = A.tiles_x * A.tiles_y;
-    const int tz = t / tpl, txy = t % tpl;
-    const int ty = txy / A.tiles_x, tx = txy % A.tiles_x;
-    const int64_t nx = A.nx, ny = A.ny, nz = A.nz, pl = nx * ny;
-    const int64_t x0 = (int64_t)tx * (64 * VEC) + (int64_t)lane * VEC;
-    const int64_t j = (int64_t)ty * 4 + wv;
-    const bool act = x0 < nx && j < ny;
-    const int64_t oj = (act ? j * nx + x0 : 0);  // clamped: every load stays inside the allocation
-    bool has_n, has_s;
-    int64_t dn, ds;  // 0: dummy (own row), cooked to zero
-    if constexpr (PER) {
-        has_n = act;
-        has_s = act;
-        dn = !act ? 0 : (j + 1 < ny ? nx : -(ny - 1) * nx);
-        ds = !act ? 0 : (j >= 1 ? -nx : (ny - 1) * nx);
-    } else {
-        has_n = act && j + 1 < ny;
-        has_s = act && j >= 1;
-        dn = has_n ? nx : 0;
-        ds = has_s ? -nx : 0;
-    }
-    const XEdge xe = x_edge<VEC, PER>(lane, act, x0, nx);
-    const int64_t de = xe.de, de2 = xe.de2;
-    const bool edge_ok = xe.ok, edge_ok2 = xe.ok2;
-    const int64_t z0 = (int64_t)tz * A.rows;
-    const int64_t z1 = z0 + A.rows < nz ? z0 + A.rows : nz;
-    constexpr bool kUn = SCH == 0 && MODE != MODE_JEXACT;
-    constexpr bool kF0 = MODE == MODE_JFD;
-    constexpr bool kAx = EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID;
-    constexpr bool vout = MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS);  // fused kdivcopy!: V_k stored
-    double acc = 0.0;
-    if (z0 < nz) {
-        const int64_t o0 = z0 * pl + oj;
-        Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(A, load_raw<MODE, VEC, false, kG, PER>(A, o0 - pl, 0), act, false);  // plane -1: ghost
-        Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, load_raw<MODE, VEC, true, kG, PER>(A, o0, o0 + de, o0 + de2), act,
-                                                      edge_ok, edge_ok2);
-        RawRow<MODE, VEC> rp = load_raw<MODE, VEC, true, kG, PER>(A, o0 + pl, o0 + pl + de, o0 + pl + de2);  // plane nz: ghost
-        RawRow<MODE, VEC> rn = load_raw<MODE, VEC, false, kG, PER>(A, o0 + dn, 0);
-        RawRow<MODE, VEC> rs = load_raw<MODE, VEC, false, kG, PER>(A, o0 + ds, 0);
-        Row<VEC> unc{}, f0c{}, ax{};
-        if constexpr (kUn) unc = data_row<VEC>(A.un, o0, true);
-        if constexpr (kF0) f0c = data_row<VEC>(A.F0, o0, true);
-        if constexpr (kAx) ax = data_row<VEC>(A.aux, o0, true);
-        for (int64_t k = z0; k < z1; ++k) {
-            const int64_t o = k * pl + oj;
-            // ---- issue: centre row of plane k+2, y-neighbour rows and centre data of plane k+1
-            const bool more = k + 1 < z1;
-            const int64_t o2 = more ? o + 2 * pl : o + pl;
-            const int64_t o1 = more ? o + pl : o;
-            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2);
-            const RawRow<MODE, VEC> rnn = load_raw<MODE, VEC, false, kG, PER>(A, o1 + dn, 0);
-            const RawRow<MODE, VEC> rss = load_raw<MODE, VEC, false, kG, PER>(A, o1 + ds, 0);
-            Row<VEC> uncn{}, f0cn{}, axn{};
-            if constexpr (kUn) uncn = data_row<VEC>(A.un, o1, true);
-            if constexpr (kF0) f0cn = data_row<VEC>(A.F0, o1, true);
-            if constexpr (kAx) axn = data_row<VEC>(A.aux, o1, true);
-            // ---- cook what was issued one iteration ago
-            const Field<VEC> fp = cook<MODE, VEC, SCH, kG, PER>(A, rp, act, edge_ok, edge_ok2);
-            const Field<VEC> fn = cook<MODE, VEC, SCH, kG, PER>(A, rn, has_n, false);
-            const Field<VEC> fs = cook<MODE, VEC, SCH, kG, PER>(A, rs, has_s, false);
-            // ---- compute plane k
-            const LR xn = x_nbrs<PER>(fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
-            const double lft = xn.l, rgt = xn.r;
-            double glft = 0.0, grgt = 0.0;
-            if constexpr (SCH == 2 && kG) {
-                const LR gn = x_nbrs<PER>(fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
-                glft = gn.l;
-                grgt = gn.r;
-            }
-            if (act) {
-                Row<VEC> val;
-#pragma unroll
-                for (int q = 0; q < VEC; ++q) {
-                    const double w = (q == 0) ? lft : fc.c[q == 0 ? 0 : q - 1];
-                    const double e = (q == VEC - 1) ? rgt : fc.c[q == VEC - 1 ? q : q + 1];
-                    const double c = fc.c[q];
-                    const double lsum = (lapk(A, c, e, w, A.hx2, A.ihx2) + lapk(A, c, fn.c[q], fs.c[q], A.hy2, A.ihy2)) +
-                                        lapk(A, c, fp.c[q], fm.c[q], A.hz2, A.ihz2);
-                    double lsumg = 0.0;
-                    if constexpr (SCH == 2 && kG) {
-                        const double g = fc.g[q];
-                        const double gw = (q == 0) ? glft : fc.g[q == 0 ? 0 : q - 1];
-                        const double ge = (q == VEC - 1) ? grgt : fc.g[q == VEC - 1 ? q : q + 1];
-                        lsumg = (lapk(A, g, ge, gw, A.hx2, A.ihx2) + lapk(A, g, fn.g[q], fs.g[q], A.hy2, A.ihy2)) +
-                                lapk(A, g, fp.g[q], fm.g[q], A.hz2, A.ihz2);
-                    }
-                    const double unq = kG ? fc.g[q] : unc.v[q];
-                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0c.v[q], SCH == 1 ? fc.x[q] : c, lsumg);
-                    acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[q] : ax.v[q], acc);
-                    val.v[q] = r;
-                }
-                store_row<VEC>(A.out, o, val);
-                if (vout) {
-                    Row<VEC> vn;
-#pragma unroll
-                    for (int q = 0; q < VEC; ++q) vn.v[q] = fc.vn[q];
-                    store_row<VEC>(A.vout, o, vn);
-                }
-            }
-            fm = fc;
-            fc = fp;
-            rp = rpp;
-            rn = rnn;
-            rs = rss;
-            unc = uncn;
-            f0c = f0cn;
-            ax = axn;
-        }
-    }
-    if constexpr (EPI != EPI_NONE) publish(acc, A.part, A.fin, sh);
-}
 
 // ------------------------------------------------------------------------------ BLAS-1
 // Block-contiguous chunks of `len` elements (a multiple of the block size), threads interleaved
@@ -1226,56 +453,6 @@ __global__ __launch_bounds__(kBlock) void k_jdiag(KArgs A, double* __restrict__ 
     }
 }
 
-// ------------------------------------------------------------------------------ stencil dispatch
-template <int KIND, int MODE, int EPI>
-void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
-    constexpr bool k2d = KIND == NK_BRATU2D || KIND == NK_HEAT2D_EULER || KIND == NK_HEAT2D_MIDPOINT ||
-                         KIND == NK_HEAT2D_TRAPEZOID;
-    if constexpr (KIND == NK_BRATU1D) {
-        hipLaunchKernelGGL((k_st1d<MODE, EPI>), dim3(grid), dim3(kBlock), 0, s, A);
-    } else if constexpr (k2d) {
-        if constexpr (heat_kind<KIND>()) {  // bc_periodic! instantiations: heat only, VEC <= 2
-            if (per) {
-                if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2, true>), dim3(grid), dim3(kBlock), 0, s, A);
-                else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1, true>), dim3(grid), dim3(kBlock), 0, s, A);
-                return;
-            }
-        }
-        if (vec == 4) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 4>), dim3(grid), dim3(kBlock), 0, s, A);
-        else if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
-        else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1>), dim3(grid), dim3(kBlock), 0, s, A);
-    } else {
-        if (per) {
-            if (vec == 2) hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 2, true>), dim3(grid), dim3(kBlock), 0, s, A);
-            else hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 1, true>), dim3(grid), dim3(kBlock), 0, s, A);
-            return;
-        }
-        if (vec == 2) hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
-        else hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 1>), dim3(grid), dim3(kBlock), 0, s, A);
-    }
-}
-
-template <int KIND, int MODE>
-void go_stencil_epi(const KArgs& A, int epi, int vec, int grid, hipStream_t s, bool per) {
-    switch (epi) {
-    case EPI_NONE: go_stencil<KIND, MODE, EPI_NONE>(A, vec, grid, s, per); break;
-    case EPI_SUMSQ: go_stencil<KIND, MODE, EPI_SUMSQ>(A, vec, grid, s, per); break;
-    case EPI_DOT: go_stencil<KIND, MODE, EPI_DOT>(A, vec, grid, s, per); break;
-    case EPI_DOTV: go_stencil<KIND, MODE, EPI_DOTV>(A, vec, grid, s, per); break;
-    case EPI_DOTVS: go_stencil<KIND, MODE, EPI_DOTVS>(A, vec, grid, s, per); break;
-    default: go_stencil<KIND, MODE, EPI_RESID>(A, vec, grid, s, per); break;
-    }
-}
-
-template <int KIND>
-void go_stencil_mode(const KArgs& A, int mode, int epi, int vec, int grid, hipStream_t s, bool per) {
-    switch (mode) {
-    case MODE_RES: go_stencil_epi<KIND, MODE_RES>(A, epi, vec, grid, s, per); break;
-    case MODE_JEXACT: go_stencil_epi<KIND, MODE_JEXACT>(A, epi, vec, grid, s, per); break;
-    default: go_stencil_epi<KIND, MODE_JFD>(A, epi, vec, grid, s, per); break;
-    }
-}
-
 int env_int(const char* name, int dflt) {
     const char* s = getenv(name);
     return (s && *s) ? atoi(s) : dflt;
@@ -1313,6 +490,10 @@ int mailbox_bind(nk_ctx* c) {
         m.spin_limit = (e && *e) ? (unsigned)atoll(e) : (1u << 24);  // ~1 s of polling
     }
     NK_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(g_mb), &m, sizeof(m)));
+    // and the copy in every stencil instantiation unit
+    for (auto bind : {stencil_bind_mb_1, stencil_bind_mb_2, stencil_bind_mb_3, stencil_bind_mb_4, stencil_bind_mb_5,
+                      stencil_bind_mb_6, stencil_bind_mb_7, stencil_bind_mb_8})
+        NK_HIP(c, bind(m));
     return NK_OK;
 }
 
@@ -1531,15 +712,15 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     hipStream_t s = c->stream;
     const char* kname = epi == EPI_DOTV ? fused_names[mode] : (epi == EPI_DOTVS ? v1_names[mode] : names[mode][epi]);
     return launch(c, kname, bytes, [&] {
-        switch (kind) {
-        case NK_BRATU1D: go_stencil_mode<NK_BRATU1D>(A, mode, epi, vec, grid, s, false); break;
-        case NK_BRATU2D: go_stencil_mode<NK_BRATU2D>(A, mode, epi, vec, grid, s, false); break;
-        case NK_HEAT2D_EULER: go_stencil_mode<NK_HEAT2D_EULER>(A, mode, epi, vec, grid, s, per); break;
-        case NK_HEAT2D_MIDPOINT: go_stencil_mode<NK_HEAT2D_MIDPOINT>(A, mode, epi, vec, grid, s, per); break;
-        case NK_HEAT2D_TRAPEZOID: go_stencil_mode<NK_HEAT2D_TRAPEZOID>(A, mode, epi, vec, grid, s, per); break;
-        case NK_HEAT3D_MIDPOINT: go_stencil_mode<NK_HEAT3D_MIDPOINT>(A, mode, epi, vec, grid, s, per); break;
-        case NK_HEAT3D_TRAPEZOID: go_stencil_mode<NK_HEAT3D_TRAPEZOID>(A, mode, epi, vec, grid, s, per); break;
-        default: go_stencil_mode<NK_HEAT3D_EULER>(A, mode, epi, vec, grid, s, per); break;
+        switch (kind) {  // one translation unit per kind (nk_stencil_inst.hip)
+        case NK_BRATU1D: stencil_kind_1(A, mode, epi, vec, grid, s, false); break;
+        case NK_BRATU2D: stencil_kind_2(A, mode, epi, vec, grid, s, false); break;
+        case NK_HEAT2D_EULER: stencil_kind_3(A, mode, epi, vec, grid, s, per); break;
+        case NK_HEAT3D_EULER: stencil_kind_4(A, mode, epi, vec, grid, s, per); break;
+        case NK_HEAT2D_MIDPOINT: stencil_kind_5(A, mode, epi, vec, grid, s, per); break;
+        case NK_HEAT3D_MIDPOINT: stencil_kind_6(A, mode, epi, vec, grid, s, per); break;
+        case NK_HEAT2D_TRAPEZOID: stencil_kind_7(A, mode, epi, vec, grid, s, per); break;
+        default: stencil_kind_8(A, mode, epi, vec, grid, s, per); break;
         }
     });
 }

@@ -1,0 +1,21 @@
+// nk_stencil_inst.hip -- instantiates the stencil kernels of ONE problem kind (NK_ST_KIND, set by
+// the Makefile: one object per kind, compiled in parallel).
+#include "nk_stencil.hpp"
+
+#ifndef NK_ST_KIND
+#error "compile with -DNK_ST_KIND=<problem kind>"
+#endif
+#define NK_CAT2(a, b) a##b
+#define NK_CAT(a, b) NK_CAT2(a, b)
+
+namespace nk {
+
+void NK_CAT(stencil_kind_, NK_ST_KIND)(const KArgs& A, int mode, int epi, int vec, int grid, hipStream_t s, bool per) {
+    go_stencil_mode<NK_ST_KIND>(A, mode, epi, vec, grid, s, per);
+}
+
+hipError_t NK_CAT(stencil_bind_mb_, NK_ST_KIND)(const MbInfo& m) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_mb), &m, sizeof(m));
+}
+
+}  // namespace nk
