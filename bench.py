@@ -73,8 +73,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--n", type=int, default=0, help="per-GPU slab side (default 4096 / 8192 / 512 by workload)")
     ap.add_argument("--global-n", type=int, default=0,
-                    help="bratu2d strong scaling: one global N x N problem in row slabs over the GPUs "
-                         "(--gpus 8 --global-n 16384 is BASELINE config 4)")
+                    help="strong scaling: one global N^dim problem in slabs over the GPUs (--gpus 8 --global-n "
+                         "16384 is BASELINE config 4; --workload heat3d --gpus 8 --global-n 512 is config 5)")
     ap.add_argument("--memory", type=int, default=0, help="Krylov memory (default 30 for bratu2d, 20 for heat)")
     ap.add_argument("--itmax", type=int, default=300)
     ap.add_argument("--jv", choices=["fd", "exact"], default="fd")
@@ -189,27 +189,37 @@ class HeatEuler:
     --scheme / --bc: the same loop with G_Midpoint! / G_Trapezoid! and bc_periodic!."""
 
     def __init__(self, args, ctx, rank, world, dim):
-        n = args.n or (8192 if dim == 2 else 512)
+        if args.global_n:  # strong scaling: one global G^dim problem, G / world slab planes per rank
+            n = args.global_n
+            if n % world:
+                raise SystemExit(f"--global-n {n} must be divisible by the number of GPUs {world}")
+            planes = n // world
+            glob = (n,) * dim
+        else:  # weak scaling: an n^dim block per rank
+            n = args.n or (8192 if dim == 2 else 512)
+            planes = n
+            glob = (n,) * (dim - 1) + (n * world,)
         self.n, self.dim, self.args, self.world = n, dim, args, world
         self.a = 0.01
-        glob = (n,) * (dim - 1) + (n * world,)
         hs = [1.0 / (m + 1) for m in glob]
         self.hs = hs
         if dim == 2:
             self.dt = hs[0] ** 2 * hs[1] ** 2 / (2.0 * self.a * (hs[0] ** 2 + hs[1] ** 2))  # heat_2D.jl:72
         else:
             self.dt = 1.0 / (2.0 * self.a * sum(1.0 / h ** 2 for h in hs))
-        grid = ah.Grid((n,) * dim, glob, rank * n)
+        grid = ah.Grid((n,) * (dim - 1) + (planes,), glob, rank * planes)
         sines = [np.sin(np.pi * np.arange(1, n + 1) * hs[0])]
-        rows0 = rank * n
+        rows0 = rank * planes
         if dim == 2:
-            ys = np.sin(np.pi * np.arange(rows0 + 1, rows0 + n + 1) * hs[1])
-            u0 = ys[:, None] * sines[0][None, :] + noisy((n,), n, range(rows0, rows0 + n))
+            ys = np.sin(np.pi * np.arange(rows0 + 1, rows0 + planes + 1) * hs[1])
+            u0 = ys[:, None] * sines[0][None, :] + noisy((planes,), n, range(rows0, rows0 + planes))
         else:
             ys = np.sin(np.pi * np.arange(1, n + 1) * hs[1])
-            zs = np.sin(np.pi * np.arange(rows0 + 1, rows0 + n + 1) * hs[2])
+            zs = np.sin(np.pi * np.arange(rows0 + 1, rows0 + planes + 1) * hs[2])
             base = zs[:, None, None] * ys[None, :, None] * sines[0][None, None, :]
-            u0 = base + noisy((n, n), n, range(rows0 * n, (rows0 + n) * n))
+            u0 = base + noisy((planes, n), n, range(rows0 * n, (rows0 + planes) * n))
+        self.scaling = "strong" if args.global_n else "weak"
+        self.units_per_matvec = 1 if args.global_n else world
         self.u0 = np.ascontiguousarray(u0)
         self.un = ah.DeviceArray.from_numpy(self.u0, grid, ctx)
         self.u = self.un.copy()
@@ -221,10 +231,11 @@ class HeatEuler:
         fp = (self.a, hs[0], hs[1], bc) if dim == 2 else (self.a, hs[0], hs[1], hs[2], bc)
         self.p = (self.un, self.dt, None, fp, 0.0)
         self.jv_kernel = "jv_fd_dot_norm" if args.jv == "fd" else "jv_exact_dot_norm"
-        shape = "x".join([str(n)] * (dim - 1) + [str(n * world)])
+        shape = "x".join(str(m) for m in glob)
+        per_gpu = f"{n}^{dim - 1}x{planes} slab per GPU" if args.global_n else f"{n}^{dim} per GPU"
         sname = {"euler": "implicit Euler", "midpoint": "implicit midpoint", "trapezoid": "implicit trapezoid"}[args.scheme]
         bcname = "" if args.bc == "zero" else ", bc_periodic!"
-        self.workload = (f"{dim}D heat {sname}{bcname} {shape} ({n}^{dim} per GPU), one time step per step: "
+        self.workload = (f"{dim}D heat {sname}{bcname} {shape} ({per_gpu}), one time step per step: "
                          f"newton_krylov! tol_abs=6e-6, GMRES memory {args.memory or 20} (unrestarted), "
                          f"{args.jv.upper()} Jv, IC sin*sin + 0.1 U(-1,1)")
         self.metric = f"Krylov matvecs/sec + achieved HBM GB/s, {dim}D heat {sname}{bcname} {n}^{dim}"

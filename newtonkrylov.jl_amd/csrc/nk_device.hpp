@@ -30,14 +30,23 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;  // lane 0's value is used: a fixed association order
 }
 
-// sum over the 256 threads; valid in thread 0
+// sum over the NT threads of the block (NT / 64 waves, at most 16); valid in thread 0.  The wave sums
+// go to sh[0 .. NT/64) and are added in wave order (((w0 + w1) + w2) + ...); sh[kShB] is the slot
+// the callers broadcast through, disjoint from every wave slot.
+constexpr int kShB = 16, kShN = 17;
+template <int NT = kBlock>
 __device__ __forceinline__ double block_sum(double v, double* sh) {
+    static_assert(NT % 64 == 0 && NT / 64 <= kShB, "block_sum: 1 .. 16 waves");
     v = wave_sum(v);
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) sh[w] = v;
     __syncthreads();
     double r = 0.0;
-    if (threadIdx.x == 0) r = ((sh[0] + sh[1]) + sh[2]) + sh[3];
+    if (threadIdx.x == 0) {
+        r = sh[0];
+#pragma unroll
+        for (int k = 1; k < NT / 64; ++k) r += sh[k];
+    }
     return r;
 }
 
@@ -94,10 +103,10 @@ __device__ double mb_recv(unsigned epoch, double* sh) {
         const double v = __longlong_as_double((long long)(((uint64_t)hi << 32) | half));
         double t = 0.0;
         for (int r = 0; r < nr; ++r) t += __shfl(v, 2 * r, 64);  // fixed rank order
-        if (l == 0) sh[4] = t;
+        if (l == 0) sh[kShB] = t;
     }
     __syncthreads();
-    return sh[4];
+    return sh[kShB];
 }
 
 // SC1 = true reads with agent-scope (sc1) loads: values other blocks of the SAME launch stored
@@ -108,23 +117,23 @@ __device__ __forceinline__ double ld_part(const double* p) {
     return *p;
 }
 
-template <bool SC1 = false>
+template <bool SC1 = false, int NT = kBlock>
 __device__ __forceinline__ double reduce_input(const double* __restrict__ in, int len, double* sh) {
     if (len < 0) return mb_recv((unsigned)(-len), sh);  // all-reduced through the peer mailbox
     double t = 0.0;
     int m = threadIdx.x;
-    for (; m + 7 * kBlock < len; m += 8 * kBlock) {
+    for (; m + 7 * NT < len; m += 8 * NT) {
         double a[8];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) a[r] = ld_part<SC1>(in + m + r * kBlock);
+        for (int r = 0; r < 8; ++r) a[r] = ld_part<SC1>(in + m + r * NT);
 #pragma unroll
         for (int r = 0; r < 8; ++r) t += a[r];
     }
-    for (; m < len; m += kBlock) t += ld_part<SC1>(in + m);
-    t = block_sum(t, sh);
-    if (threadIdx.x == 0) sh[4] = t;
+    for (; m < len; m += NT) t += ld_part<SC1>(in + m);
+    t = block_sum<NT>(t, sh);
+    if (threadIdx.x == 0) sh[kShB] = t;
     __syncthreads();
-    return sh[4];
+    return sh[kShB];
 }
 
 // Block partial -> part[blockIdx.x].  With `fin` (a communicator is attached) the last block to
@@ -135,9 +144,10 @@ __device__ __forceinline__ double reduce_input(const double* __restrict__ in, in
 // stored write-through (agent-scope atomic store = sc1) and drained before the ticket; the last
 // block reads the partials with sc1 loads.  An agent-scope RELEASE fence here would write back the
 // XCD's whole L2 -- full of this kernel's streamed output -- once per block (measured: 2x slower).
+template <int NT = kBlock>
 __device__ __forceinline__ void publish(double acc, double* part, int fin, double* sh) {
     __shared__ unsigned ticket;
-    const double s = block_sum(acc, sh);
+    const double s = block_sum<NT>(acc, sh);
     if (!fin) {
         if (threadIdx.x == 0) part[blockIdx.x] = s;
         return;
@@ -150,7 +160,7 @@ __device__ __forceinline__ void publish(double acc, double* part, int fin, doubl
     }
     __syncthreads();
     if (ticket != gridDim.x - 1) return;
-    const double t = reduce_input<true>(part, (int)gridDim.x, sh);
+    const double t = reduce_input<true, NT>(part, (int)gridDim.x, sh);
     if (threadIdx.x == 0) {
         part[kRedCap - 1] = t;
         __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

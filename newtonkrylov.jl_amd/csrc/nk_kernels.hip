@@ -44,7 +44,7 @@ __device__ __forceinline__ Chunk block_chunk(int64_t len) {
 
 __global__ __launch_bounds__(kBlock) void k_dot(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
                                                double* __restrict__ part, int fin) {
-    __shared__ double sh[8];
+    __shared__ double sh[kShN];
     const double2* x2 = reinterpret_cast<const double2*>(x);
     const double2* y2 = reinterpret_cast<const double2*>(y);
     double acc = 0.0;
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(kBlock) void k_dot(int64_t n, const double* __restr
 }
 
 __global__ __launch_bounds__(kBlock) void k_sumsq(int64_t n, const double* __restrict__ x, double* __restrict__ part, int fin) {
-    __shared__ double sh[8];
+    __shared__ double sh[kShN];
     const double2* x2 = reinterpret_cast<const double2*>(x);
     double acc = 0.0;
     NK_GRID_STRIDE2(i) {
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(kBlock) void k_sumsq(int64_t n, const double* __res
 // the host can read it after the stream event without a separate device-to-host copy
 __global__ __launch_bounds__(kBlock) void k_finalize(const double* __restrict__ in, int len, double* __restrict__ dst, int sqrt_it,
                                                     double* __restrict__ mirror) {
-    __shared__ double sh[8];
+    __shared__ double sh[kShN];
     const double t = reduce_input(in, len, sh);
     if (threadIdx.x == 0) {
         const double r = sqrt_it ? sqrt(t) : t;
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kBlock) void k_axpy(int64_t n, double s, const doub
 // y = s x + y with the partials of ||y||^2 (the Newton update and the next FD step's ||u||)
 __global__ __launch_bounds__(kBlock) void k_axpy_sumsq(int64_t n, double s, const double* __restrict__ x,
                                                       double* __restrict__ y, double* __restrict__ part, int fin) {
-    __shared__ double sh[8];
+    __shared__ double sh[kShN];
     const double2* x2 = reinterpret_cast<const double2*>(x);
     double2* y2 = reinterpret_cast<double2*>(y);
     double acc = 0.0;
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restri
                                                     int red_len, double* __restrict__ h_out, double* __restrict__ h_host,
                                                     double* __restrict__ part,
                                                     int rev, int fin) {
-    __shared__ double sh[8];
+    __shared__ double sh[kShN];
     dx2* q2 = reinterpret_cast<dx2*>(q);
     const dx2* v2 = reinterpret_cast<const dx2*>(vi);
     const dx2* w2 = reinterpret_cast<const dx2*>(vnext);
@@ -313,7 +313,7 @@ struct UpdArgs {
 // xr = Σ y_i V_i (the kaxpy! chain of gmres!, from xr = 0); on the last chunk x = x + xr
 // (restart) or x = xr; optional partials of ||x||^2.  16-B accesses; V loads non-temporal.
 __global__ __launch_bounds__(kBlock) void k_update_x(UpdArgs A) {
-    __shared__ double sh[8];
+    __shared__ double sh[kShN];
     const int64_t n = A.n;
     double yv[kMaxUpdateVecs];
 #pragma unroll
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(kBlock) void k_update_x(UpdArgs A) {
 __global__ __launch_bounds__(kBlock) void k_cg_update(int64_t n, double alpha, double* __restrict__ x, double* __restrict__ r,
                                                      const double* __restrict__ p, const double* __restrict__ Ap,
                                                      double* __restrict__ part, int fin) {
-    __shared__ double sh[8];
+    __shared__ double sh[kShN];
     double acc = 0.0;
     const double ma = -alpha;
     NK_CHUNKED(i, n) {
@@ -410,7 +410,7 @@ template <int EPI>
 __global__ __launch_bounds__(kBlock) void k_user_epi(int64_t n, int fd, double* __restrict__ out,
                                                     const double* __restrict__ F0, double eps,
                                                     const double* __restrict__ aux, double* __restrict__ part, int fin) {
-    __shared__ double sh[8];
+    __shared__ double sh[kShN];
     double acc = 0.0;
     NK_CHUNKED(i, n) {
         double r = out[i];
@@ -426,7 +426,7 @@ __global__ __launch_bounds__(kBlock) void k_user_epi(int64_t n, int fd, double* 
 // z = d .* v (diagonal right preconditioner) with the partials of ||z||^2 (the FD step size)
 __global__ __launch_bounds__(kBlock) void k_diag_apply(int64_t n, double* __restrict__ z, const double* __restrict__ d,
                                                       const double* __restrict__ v, double* __restrict__ part, int fin) {
-    __shared__ double sh[8];
+    __shared__ double sh[kShN];
     double acc = 0.0;
     NK_CHUNKED(i, n) {
         const double zi = d[i] * v[i];
@@ -499,7 +499,7 @@ int mailbox_bind(nk_ctx* c) {
 
 namespace {
 __global__ void k_mb_test(unsigned epoch, double value, double* out) {
-    __shared__ double sh[8];
+    __shared__ double sh[kShN];
     mb_send(value, epoch);
     const double t = mb_recv(epoch, sh);
     if (threadIdx.x == 0) *out = t;
@@ -673,8 +673,9 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         grid = A.tiles_x * A.tiles_y;
     } else {
         vec = (p->nx % 2 == 0) ? 2 : 1;
+        A.nw = 4;  // rows per 3D tile (k_st3d's NW)
         A.tiles_x = (int)((p->nx + 64 * vec - 1) / (64 * vec));
-        A.tiles_y = (int)((p->ny + 3) / 4);
+        A.tiles_y = (int)((p->ny + A.nw - 1) / A.nw);
         static const int target = env_int("NK_ST3_BLOCKS", 8192);  // shorter z-marches keep y-adjacent tiles in step (L2 reuse of the halo rows)
         int64_t planes = ((int64_t)p->nz * A.tiles_x * A.tiles_y + target - 1) / target;
         static const int min_planes = env_int("NK_ST_MINPLANES", 8);
@@ -1070,6 +1071,35 @@ extern "C" int nkb_stencil(nk_ctx* c, int64_t nx, int64_t ny, int mode, int epi,
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     for (double* q : {u, v, F0, aux, out}) nk_vec_free(c, q);
+    return NK_OK;
+}
+
+// 3D heat (implicit Euler) stencil variants at n^3: fast bits 8 / 16 select 8- / 16-row tiles
+extern "C" int nkb_stencil3d(nk_ctx* c, int64_t n, int mode, int epi, int fast, int reps, double* us_out) {
+    using namespace nk;
+    if (!c || n < 2 || reps < 1 || !us_out) return NK_E_ARG;
+    const double h = 1.0 / (n + 1);
+    nk_problem p{NK_HEAT3D_EULER, NK_BC_ZERO, n, n, n, h, h, h, 0.0, 0.01, 1e-6, nullptr};
+    double *u = nullptr, *v = nullptr, *F0 = nullptr, *aux = nullptr, *out = nullptr, *un = nullptr;
+    p.un = reinterpret_cast<const double*>(1);  // geometry only while allocating
+    for (double** q : {&u, &v, &F0, &aux, &out, &un}) NK_TRY(nk_vec_alloc(c, &p, q));
+    p.un = un;
+    StencilIn in{&p, mode, epi, out, u, v, F0, aux, 1e-6};
+    Red r{};
+    hipEvent_t a, b;
+    NK_HIP(c, hipEventCreate(&a));
+    NK_HIP(c, hipEventCreate(&b));
+    NK_TRY(launch_stencil_ex(c, in, &r, 0, fast));
+    NK_HIP(c, hipEventRecord(a, c->stream));
+    for (int k = 0; k < reps; ++k) NK_TRY(launch_stencil_ex(c, in, &r, 0, fast));
+    NK_HIP(c, hipEventRecord(b, c->stream));
+    NK_HIP(c, hipEventSynchronize(b));
+    float ms = 0.f;
+    NK_HIP(c, hipEventElapsedTime(&ms, a, b));
+    *us_out = 1e3 * ms / reps;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    for (double* q : {u, v, F0, aux, out, un}) nk_vec_free(c, q);
     return NK_OK;
 }
 

@@ -27,6 +27,7 @@ struct KArgs {
     double hd;           // *vdiv, loaded once per block
     int fin;             // fold the partials in-kernel (publish)
     double alpha;        // G_Midpoint! α
+    int nw;              // 3D: rows (waves) per tile
 };
 
 // per-kind entry points (nk_stencil_inst.hip): launch one stencil kernel of kind K / bind its g_mb
@@ -151,7 +152,7 @@ __device__ __forceinline__ double epilogue(double& val, double ax, double acc) {
 // ------------------------------------------------------------------------------ 1D stencil
 template <int MODE, int EPI>
 __global__ __launch_bounds__(kBlock) void k_st1d(KArgs A0) {
-    __shared__ double sh[8];
+    __shared__ double sh[kShN];
     KArgs A = A0;
     A.hd = A.vdiv ? *A.vdiv : 1.0;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -419,7 +420,7 @@ __device__ __forceinline__ LR x_nbrs(double cfirst, double clast, double e, doub
 // raw data (issued one iteration earlier) is cooked, and row j is computed from registers.
 template <int KIND, int MODE, int EPI, int VEC, bool PER = false>
 __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
-    __shared__ double sh[8];
+    __shared__ double sh[kShN];
     KArgs A = A0;
     A.hd = A.vdiv ? *A.vdiv : 1.0;
     constexpr int SCH = scheme_of<KIND>();
@@ -524,15 +525,16 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
 }
 
 // ------------------------------------------------------------------------------ 3D stencil
-// Block = 4 waves = 4 rows (y) x 64*VEC columns, marching A.rows planes in z.  Same pipeline as
+// Block = NW waves = NW rows (y) x 64*VEC columns, marching A.rows planes in z (NW = A.nw: taller
+// tiles re-fetch fewer y-halo rows).  Same pipeline as
 // the 2D kernel: at iteration k the raw loads of the centre row of plane k+2 and of the y-
 // neighbour rows of plane k+1 are issued, plane k+1's centre row and plane k's y-neighbours
 // (issued one iteration earlier) are cooked, and plane k is computed from registers.  The y-
 // neighbour rows are mostly L2 hits (the adjacent waves of the block stream them).  PER: the
 // y-neighbours of rows 0 and ny-1 wrap (bc_periodic!), x as in the 2D kernel.
-template <int KIND, int MODE, int EPI, int VEC, bool PER = false>
-__global__ __launch_bounds__(kBlock) void k_st3d(KArgs A0) {
-    __shared__ double sh[8];
+template <int KIND, int MODE, int EPI, int VEC, bool PER = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
+    __shared__ double sh[kShN];
     KArgs A = A0;
     A.hd = A.vdiv ? *A.vdiv : 1.0;
     constexpr int SCH = scheme_of<KIND>();
@@ -546,7 +548,7 @@ __global__ __launch_bounds__(kBlock) void k_st3d(KArgs A0) {
     const int ty = txy / A.tiles_x, tx = txy % A.tiles_x;
     const int64_t nx = A.nx, ny = A.ny, nz = A.nz, pl = nx * ny;
     const int64_t x0 = (int64_t)tx * (64 * VEC) + (int64_t)lane * VEC;
-    const int64_t j = (int64_t)ty * 4 + wv;
+    const int64_t j = (int64_t)ty * NW + wv;
     const bool act = x0 < nx && j < ny;
     const int64_t oj = (act ? j * nx + x0 : 0);  // clamped: every load stays inside the allocation
     bool has_n, has_s;
@@ -650,10 +652,21 @@ __global__ __launch_bounds__(kBlock) void k_st3d(KArgs A0) {
             ax = axn;
         }
     }
-    if constexpr (EPI != EPI_NONE) publish(acc, A.part, A.fin, sh);
+    if constexpr (EPI != EPI_NONE) publish<64 * NW>(acc, A.part, A.fin, sh);
 }
 
 // ------------------------------------------------------------------------------ stencil dispatch
+template <int KIND, int MODE, int EPI, int NW>
+void go_st3d(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
+    if (per) {
+        if (vec == 2) hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 2, true, NW>), dim3(grid), dim3(64 * NW), 0, s, A);
+        else hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 1, true, NW>), dim3(grid), dim3(64 * NW), 0, s, A);
+        return;
+    }
+    if (vec == 2) hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 2, false, NW>), dim3(grid), dim3(64 * NW), 0, s, A);
+    else hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 1, false, NW>), dim3(grid), dim3(64 * NW), 0, s, A);
+}
+
 template <int KIND, int MODE, int EPI>
 void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
     constexpr bool k2d = KIND == NK_BRATU2D || KIND == NK_HEAT2D_EULER || KIND == NK_HEAT2D_MIDPOINT ||
@@ -672,13 +685,9 @@ void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
         else if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
         else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1>), dim3(grid), dim3(kBlock), 0, s, A);
     } else {
-        if (per) {
-            if (vec == 2) hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 2, true>), dim3(grid), dim3(kBlock), 0, s, A);
-            else hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 1, true>), dim3(grid), dim3(kBlock), 0, s, A);
-            return;
-        }
-        if (vec == 2) hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
-        else hipLaunchKernelGGL((k_st3d<KIND, MODE, EPI, 1>), dim3(grid), dim3(kBlock), 0, s, A);
+        // 4-row tiles: 8- and 16-row tiles (fewer y-halo re-reads) measured 2-9 % slower at 512^3
+        // (profiles/r01/kbench_stencil3d.log), so only NW = 4 is instantiated
+        go_st3d<KIND, MODE, EPI, 4>(A, vec, grid, s, per);
     }
 }
 
