@@ -13,6 +13,8 @@
 
 #include "nkhip.h"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 namespace nk {
 
 constexpr int kBlock = 256;          // threads per block for every streaming kernel (4 waves of 64)
@@ -213,6 +215,15 @@ int launch_fd_point(nk_ctx* c, int64_t n, double* w, const double* u, const doub
 int launch_user_epi(nk_ctx* c, int64_t n, int fd, double* out, const double* F0, double eps, int epi,
                     const double* aux, Red* red);
 int launch_user(nk_ctx* c, const StencilIn& in, Red* red);  // nk_user.cpp
+// roctx range for the lifetime of a scope (shows Newton steps / Krylov solves / GMRES cycles in
+// rocprofv3 --marker-trace timelines; a no-op when no profiler is attached)
+struct Range {
+    explicit Range(const char* name) { roctxRangePush(name); }
+    ~Range() { roctxRangePop(); }
+    Range(const Range&) = delete;
+    Range& operator=(const Range&) = delete;
+};
+
 inline bool nk_is_user(int kind) { return kind >= NK_USER1D && kind <= NK_USER3D; }
 inline bool nk_is_heat(int kind) { return kind >= NK_HEAT2D_EULER && kind <= NK_HEAT3D_TRAPEZOID; }
 // implicit.jl scheme of a heat kind: 0 G_Euler!, 1 G_Midpoint!, 2 G_Trapezoid!

@@ -346,6 +346,7 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
             NK_TRY(host_scalar(c, rr, 1, &beta));
             src = W[0];
         }
+        Range cycle_range("gmres_cycle");
         z[0] = beta;
         NK_TRY(launch_fill(c, 1, ws->bdev, beta));  // V1 = r0 / beta happens inside step 1's Jv
         v1_src = src;
@@ -623,6 +624,7 @@ int nk_krylov_solve(nk_workspace* ws, const nk_problem* p, const double* u, cons
     if (g.n != ws->n) return fail(c, NK_E_ARG, "problem size does not match the workspace");
     if (o->jv_mode == NK_JV_FD && !F0) return fail(c, NK_E_ARG, "FD Jv needs F0 = F(u)");
     *st = nk_krylov_stats{};
+    Range solve_range(ws->algo == NK_ALGO_CG ? "cg_solve" : "gmres_solve");
     Op A{c, p, o->jv_mode, u, F0, 0.0};
     NK_TRY(halo_exchange(c, p, u));  // u (and u_n) are constant during the solve: one exchange
     NK_TRY(exchange_un(c, p));

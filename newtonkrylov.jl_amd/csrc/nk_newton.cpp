@@ -69,6 +69,7 @@ int nk_newton_krylov(nk_ctx* c, const nk_problem* p, double* u, double* res, con
     int64_t outer = 0, inner = 0;
     double u_norm = 0.0;  // ||u|| after the fused update (FD step size of the next solve); 0 = unknown
     while (n_res > tol && outer <= o->max_niter) {
+        nk::Range step_range("newton_step");
         nk_krylov_opts ko = o->krylov;
         if (!o->rtol_user && o->forcing != NK_FORCING_NONE) ko.rtol = eta;
         ko.b_norm = n_res;  // b = F(u): its norm is the n_res just computed
