@@ -117,8 +117,11 @@ void mb_free(nk_ctx* c) {
     c->mb_err_dev = nullptr;
 }
 
-// open the peers' mailboxes (local: IPC mappings + device table + kernel binding)
-static int mb_open_peers(nk_ctx* c, int rank, int nranks, const char* handles) {
+// open the peers' mailboxes (local: IPC mappings + device table + kernel binding).  busids (optional,
+// nranks x 32 chars): each rank's PCI bus id -- a peer on another device must be reachable by
+// peer access (xGMI), and every mapping is probed by a host-initiated copy before any kernel
+// dereferences it, so a bad mapping disables the mailbox (RCCL fallback) instead of faulting a kernel.
+static int mb_open_peers(nk_ctx* c, int rank, int nranks, const char* handles, const char* busids = nullptr) {
     NK_TRY(mb_alloc(c));
     mb_disable(c);
     std::vector<uint64_t*> peers((size_t)nranks);
@@ -126,6 +129,23 @@ static int mb_open_peers(nk_ctx* c, int rank, int nranks, const char* handles) {
         if (r == rank) {
             peers[r] = c->mb_self;
             continue;
+        }
+        if (busids) {
+            char bus[33];
+            std::memcpy(bus, busids + 32 * (size_t)r, 32);
+            bus[32] = 0;
+            int dev = -1;
+            if (hipDeviceGetByPCIBusId(&dev, bus) != hipSuccess) {
+                mb_disable(c);
+                return fail(c, NK_E_HIP, "mailbox: rank " + std::to_string(r) + "'s device is not visible here");
+            }
+            if (dev != c->device) {
+                int can = 0;
+                if (hipDeviceCanAccessPeer(&can, c->device, dev) != hipSuccess || !can) {
+                    mb_disable(c);
+                    return fail(c, NK_E_HIP, "mailbox: no peer access to rank " + std::to_string(r) + "'s device");
+                }
+            }
         }
         hipIpcMemHandle_t h;
         std::memcpy(&h, handles + 64 * (size_t)r, 64);
@@ -135,6 +155,12 @@ static int mb_open_peers(nk_ctx* c, int rank, int nranks, const char* handles) {
             return fail(c, NK_E_HIP, "mailbox: hipIpcOpenMemHandle failed for rank " + std::to_string(r));
         }
         c->mb_opened.push_back(p);
+        uint64_t probe = 0;
+        if (hipMemcpy(&probe, p, sizeof(probe), hipMemcpyDeviceToHost) != hipSuccess) {
+            (void)hipGetLastError();
+            mb_disable(c);
+            return fail(c, NK_E_HIP, "mailbox: rank " + std::to_string(r) + "'s mapping cannot be read");
+        }
         peers[r] = static_cast<uint64_t*>(p);
     }
     NK_HIP(c, hipMalloc(reinterpret_cast<void**>(&c->mb_peers_dev), sizeof(uint64_t*) * nranks));
@@ -213,22 +239,33 @@ int nk_dist_init(nk_ctx* c, int32_t rank, int32_t nranks, const char id[128]) {
     // also turns it on for a forced 1-rank communicator (exercises the path on one GPU), =0 off
     const bool mb_want = (mbe && *mbe == '1') || (nranks > 1 && !(mbe && *mbe == '0'));
     if (mb_want && nranks <= kMbRanks) {
-        std::vector<char> all((size_t)64 * nranks, 0);
+        // per rank: 64-byte IPC handle + 32-byte PCI bus id of its device
+        constexpr size_t kRec = 96;
+        std::vector<char> all(kRec * nranks, 0);
         char* dbuf = nullptr;
-        int rc = nk_dist_mailbox_handle(c, all.data() + 64 * (size_t)rank);
+        int rc = nk_dist_mailbox_handle(c, all.data() + kRec * (size_t)rank);
+        if (rc == NK_OK && hipDeviceGetPCIBusId(all.data() + kRec * (size_t)rank + 64, 32, c->device) != hipSuccess)
+            rc = NK_E_HIP;
         if (hipMalloc(&dbuf, all.size()) != hipSuccess) {
             std::fprintf(stderr, "[nkhip] rank %d: no memory for the handle exchange\n", rank);
             return fail(c, NK_E_NOMEM, "hipMalloc (mailbox handles)");
         }
         // allgather the IPC handles: collective, every rank takes part whatever its local state
-        (void)hipMemcpy(dbuf + 64 * (size_t)rank, all.data() + 64 * (size_t)rank, 64, hipMemcpyHostToDevice);
-        const ncclResult_t ag = ncclAllGather(dbuf + 64 * (size_t)rank, dbuf, 64, ncclChar, cm->comm, c->stream);
+        (void)hipMemcpy(dbuf + kRec * (size_t)rank, all.data() + kRec * (size_t)rank, kRec, hipMemcpyHostToDevice);
+        const ncclResult_t ag = ncclAllGather(dbuf + kRec * (size_t)rank, dbuf, kRec, ncclChar, cm->comm, c->stream);
         if (ag != ncclSuccess || hipStreamSynchronize(c->stream) != hipSuccess ||
             hipMemcpy(all.data(), dbuf, all.size(), hipMemcpyDeviceToHost) != hipSuccess)
             rc = NK_E_RCCL;
         (void)hipFree(dbuf);
         if (ag != ncclSuccess) return rccl_fail(c, ag, "ncclAllGather (mailbox handles)");
-        if (rc == NK_OK) rc = mb_open_peers(c, rank, nranks, all.data());
+        if (rc == NK_OK) {
+            std::vector<char> handles(64 * (size_t)nranks), busids(32 * (size_t)nranks);
+            for (int r = 0; r < nranks; ++r) {
+                std::memcpy(handles.data() + 64 * (size_t)r, all.data() + kRec * (size_t)r, 64);
+                std::memcpy(busids.data() + 32 * (size_t)r, all.data() + kRec * (size_t)r + 64, 32);
+            }
+            rc = mb_open_peers(c, rank, nranks, handles.data(), busids.data());
+        }
         if (mb_verdict(c, rc == NK_OK) != NK_OK) {
             std::fprintf(stderr, "[nkhip] rank %d: peer mailbox off (%s); reductions use ncclAllReduce\n", rank,
                          c->err.c_str());
