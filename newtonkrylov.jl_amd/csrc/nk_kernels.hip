@@ -487,7 +487,7 @@ int mailbox_bind(nk_ctx* c) {
         m.nranks = c->nranks;
         m.err = c->mb_err_dev;
         const char* e = getenv("NK_MB_SPIN_LIMIT");
-        m.spin_limit = (e && *e) ? (unsigned)atoll(e) : (1u << 24);  // ~1 s of polling
+        m.spin_limit = (e && *e) ? (unsigned)atoll(e) : (1u << 26);  // a few s of polling: ranks may drift apart at start-up
     }
     NK_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(g_mb), &m, sizeof(m)));
     // and the copy in every stencil instantiation unit
