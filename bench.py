@@ -71,7 +71,9 @@ def parse():
                     help="heat workloads: bc_zero! / bc_periodic! (heat_2D.jl:15-38)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=0, help="per-GPU slab side (default 4096 / 8192 / 512 by workload)")
+    ap.add_argument("--side", "--n", dest="n", type=int, default=0,
+                    help="per-GPU slab side (default 4096 / 8192 / 512 by workload; spell it --side under torchrun, "
+                         "whose own parser claims the --n prefix)")
     ap.add_argument("--global-n", type=int, default=0,
                     help="strong scaling: one global N^dim problem in slabs over the GPUs (--gpus 8 --global-n "
                          "16384 is BASELINE config 4; --workload heat3d --gpus 8 --global-n 512 is config 5)")
