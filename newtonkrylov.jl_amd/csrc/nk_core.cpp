@@ -79,9 +79,8 @@ int mb_check(nk_ctx* c) {
 }
 
 int finish_reduction(nk_ctx* c, Red* r) {
-    if (r->epoch) {  // the producing kernel already sent its value to every rank's mailbox
-        r->ptr = nullptr;
-        r->len = -(int)r->epoch;
+    if (r->epoch) {  // the consuming kernel exchanges the per-rank sums through the peer mailbox
+        r->len = -(1 + (int)((r->epoch << 15) | (unsigned)r->len));  // = mb_encode (nk_device.hpp)
         r->epoch = 0;
         r->fin = nullptr;
         return NK_OK;

@@ -117,9 +117,22 @@ __device__ __forceinline__ double ld_part(const double* p) {
     return *p;
 }
 
+// A reduction handed to a consumer kernel: `len` partial sums at `in`, summed in a fixed order.
+// len < 0 encodes a cross-rank reduction through the peer mailbox: -(1 + (epoch << 15 | count)).
+// Every block sums this rank's `count` partials (the same value in every block), block 0 sends it
+// to every rank's mailbox under `epoch`, and all blocks wait for the nranks values and add them in
+// rank order -- no arrival ticket or serial fold at the end of the producing kernel.  (Block 0 is
+// dispatched first, so the blocks that wait cannot starve the sender.)
+__device__ __forceinline__ int mb_encode(unsigned epoch, int count) { return -(1 + (int)((epoch << 15) | (unsigned)count)); }
+
 template <bool SC1 = false, int NT = kBlock>
 __device__ __forceinline__ double reduce_input(const double* __restrict__ in, int len, double* sh) {
-    if (len < 0) return mb_recv((unsigned)(-len), sh);  // all-reduced through the peer mailbox
+    unsigned epoch = 0;
+    if (len < 0) {
+        const unsigned code = (unsigned)(-len - 1);
+        epoch = code >> 15;
+        len = (int)(code & 0x7fffu);
+    }
     double t = 0.0;
     int m = threadIdx.x;
     for (; m + 7 * NT < len; m += 8 * NT) {
@@ -133,7 +146,11 @@ __device__ __forceinline__ double reduce_input(const double* __restrict__ in, in
     t = block_sum<NT>(t, sh);
     if (threadIdx.x == 0) sh[kShB] = t;
     __syncthreads();
-    return sh[kShB];
+    if (epoch == 0) return sh[kShB];
+    const double mine = sh[kShB];
+    if (blockIdx.x == 0) mb_send(mine, epoch);
+    __syncthreads();  // every thread has read sh[kShB] before mb_recv reuses it
+    return mb_recv(epoch, sh);
 }
 
 // Block partial -> part[blockIdx.x].  With `fin` (a communicator is attached) the last block to

@@ -138,7 +138,7 @@ int launch(nk_ctx* c, const char* name, double bytes, F&& f) {
 // order, so every block (and every run) sees the bit-identical value.
 struct Red {
     const double* ptr;
-    int len;                // < 0: the value arrives through the peer mailbox, epoch = -len
+    int len;                // < 0: -(1 + (epoch << 15 | count)): cross-rank through the peer mailbox
     double* fin = nullptr;  // multi-rank: the producing kernel already folded its partials here
     unsigned epoch = 0;     // mailbox epoch the producing kernel published under (0: none)
 };

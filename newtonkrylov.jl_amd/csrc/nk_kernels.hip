@@ -460,18 +460,20 @@ int env_int(const char* name, int dflt) {
 
 }  // namespace
 
-// partial-sum slot of a reduction launch.  With a communicator the kernel also folds its partials
-// in place (publish) and finish_reduction only has to all-reduce part[kRedCap - 1]; with the peer
-// mailbox the kernel also sends the folded value to every rank (fin = the epoch, >= 2).
+// partial-sum slot of a reduction launch.  With an RCCL communicator the kernel also folds its
+// partials in place (publish) and finish_reduction only has to all-reduce part[kRedCap - 1].  With
+// the peer mailbox the producer only writes its partials; the CONSUMING kernel sums them and
+// exchanges the per-rank sums (reduce_input), under a mailbox epoch allotted here.
+unsigned next_mb_epoch(nk_ctx* c) {
+    if (c->mb_epoch >= 0xffffu) c->mb_epoch = 0;  // 16-bit epochs 1 .. 65535 (0 never tags a value)
+    return ++c->mb_epoch;
+}
+
 double* red_out(nk_ctx* c, int len, Red* r, int* fin) {
     double* part = red_slot(c);
-    *fin = c->comm ? 1 : 0;
+    *fin = (c->comm && !c->mb_on) ? 1 : 0;
     r->epoch = 0;
-    if (c->mb_on) {
-        if (c->mb_epoch >= 0x7ffffff0u) c->mb_epoch = 1;  // epochs 2 .. 2^31: kernel-argument ints
-        r->epoch = ++c->mb_epoch;
-        *fin = (int)r->epoch;
-    }
+    if (c->mb_on) r->epoch = next_mb_epoch(c);
     r->ptr = part;
     r->len = len;
     r->fin = *fin ? part + kRedCap - 1 : nullptr;
@@ -610,7 +612,7 @@ int launch_periodic_fill(nk_ctx* c, double* v, int64_t plane, int64_t nplanes) {
 int mailbox_selftest(nk_ctx* c, bool* ok) {
     *ok = true;
     for (int e = 0; e < 4; ++e) {
-        const unsigned epoch = ++c->mb_epoch;
+        const unsigned epoch = next_mb_epoch(c);
         hipLaunchKernelGGL(k_mb_test, dim3(1), dim3(64), 0, c->stream, epoch, (double)(c->rank + 1) * (e + 1), c->scal);
         NK_HIP(c, hipGetLastError());
         NK_HIP(c, hipMemcpyAsync(c->hpin, c->scal, sizeof(double), hipMemcpyDeviceToHost, c->stream));
