@@ -146,3 +146,38 @@ def test_trapezoid_periodic_eigen_decay_3d(ctx):
     g = (1 + 0.5 * P.dt * mu) / (1 - 0.5 * P.dt * mu)
     assert r.solved and r.stats.inner_iterations == 1
     assert np.max(np.abs(u.to_numpy() - g * u0)) < 1e-10
+
+
+# ----------------------------------------------------------------------------- BASELINE sizes
+@pytest.mark.parametrize("dim,scheme,bc", [(2, "euler", oc.BC_ZERO), (2, "trapezoid", oc.BC_PERIODIC),
+                                           (3, "euler", oc.BC_ZERO), (3, "midpoint", oc.BC_ZERO)],
+                         ids=["heat2d-8192-euler", "heat2d-8192-trapezoid-periodic", "heat3d-512-euler",
+                              "heat3d-512-midpoint"])
+def test_heat_config_size_bitwise(ctx, dim, scheme, bc):
+    """Configs 3 / 5 sizes (8192², 512³ = one GPU's bench slab): the residual and the fused FD Jv
+    (the bench's kernels) on the whole grid, bit-identical to the oracle; exact-JVP linearity."""
+    n = 8192 if dim == 2 else 512
+    rng = np.random.default_rng(21)
+    shape = (n,) * dim
+    un = rng.standard_normal(shape)
+    mk = oc.heat2d_euler if dim == 2 else oc.heat3d_euler
+    P = mk(n, un=un, scheme=scheme, bc=bc)
+    u = un + 0.01 * rng.standard_normal(shape)
+    F, p = device_residual(P)
+    ud = dev(u)
+    res = ud.zero()
+    F(res, ud, p)
+    F0 = oc.residual(P, u)
+    assert np.array_equal(res.to_numpy(), F0)
+    del un
+    v = rng.standard_normal(shape)
+    vd, out = dev(v), ud.zero()
+    eps = oc.fd_eps(oc.norm(u), oc.norm(v))
+    ah.mul_(out, ah.JacobianOperator(F, res, ud, p, jv="fd"), vd, eps=eps)
+    assert np.array_equal(out.to_numpy(), oc.jv_fd(P, u, v, F0, eps))
+    J = ah.JacobianOperator(F, res, ud, p, jv="exact")
+    ah.mul_(out, J, vd)
+    out2 = ud.zero()
+    ah.kscal_(len(vd), 2.0, vd)
+    ah.mul_(out2, J, vd)
+    assert np.array_equal(out2.to_numpy(), 2.0 * out.to_numpy())
