@@ -8,6 +8,7 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <vector>
 
 #include "nk_internal.hpp"
 
@@ -172,12 +173,34 @@ static int mb_open_peers(nk_ctx* c, int rank, int nranks, const char* handles, c
 
 // a rank whose mailbox is not open still waits out the self-test's timeout on the others: every
 // rank reaches the collective verdict, nobody hangs
+// one ring exchange of a small 2-plane grid function whose planes hold (rank, plane, index) codes:
+// every ghost plane must hold exactly the neighbour's boundary plane
+static bool halo_selftest(nk_ctx* c) {
+    if (c->nranks < 2) return true;
+    constexpr int64_t pl = 300, np = 2;  // 300 doubles: several blocks of the exchange kernel
+    double* base = nullptr;
+    if (hipMalloc(&base, sizeof(double) * pl * (np + 2)) != hipSuccess) return false;
+    std::vector<double> h((size_t)(pl * (np + 2)), -1.0);
+    auto code = [](int r, int64_t k, int64_t i) { return 1e6 * (r + 1) + 1e3 * (double)k + (double)i; };
+    for (int64_t k = 0; k < np; ++k)
+        for (int64_t i = 0; i < pl; ++i) h[(size_t)((k + 1) * pl + i)] = code(c->rank, k, i);
+    bool ok = hipMemcpy(base, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice) == hipSuccess &&
+              launch_halo_ipc(c, base + pl, pl, np, true) == NK_OK && hipStreamSynchronize(c->stream) == hipSuccess &&
+              hipMemcpy(h.data(), base, sizeof(double) * h.size(), hipMemcpyDeviceToHost) == hipSuccess &&
+              !*c->mb_err;
+    const int lo = (c->rank + c->nranks - 1) % c->nranks, hi = (c->rank + 1) % c->nranks;
+    for (int64_t i = 0; ok && i < pl; ++i)
+        ok = h[(size_t)i] == code(lo, np - 1, i) && h[(size_t)((np + 1) * pl + i)] == code(hi, 0, i);
+    (void)hipFree(base);
+    return ok;
+}
+
 static int mb_verdict(nk_ctx* c, bool local_ok) {
     bool ok = local_ok;
     if (c->mb_on) {
         bool t = false;
         if (mailbox_selftest(c, &t) != NK_OK) t = false;
-        ok = ok && t;
+        ok = ok && t && halo_selftest(c);  // reductions and ghost planes through the peer mappings
     }
     if (c->comm) {  // all ranks must take the same path: min over ranks
         double v = ok ? 1.0 : 0.0;
