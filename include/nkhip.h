@@ -176,6 +176,12 @@ int nk_fill(nk_ctx* ctx, int64_t n, double* x, double v);                       
 int nk_divcopy(nk_ctx* ctx, int64_t n, double* y, const double* x, double s);          /* y = x / s     */
 int nk_ref(nk_ctx* ctx, int64_t n, double* x, double* y, double c, double s);          /* Givens        */
 
+/* One modified-Gram-Schmidt sweep (Krylov.jl gmres! inner loop), fused
+ * as the device GMRES runs it: for i = 1..k  h_i = <V_i, q>; q -= h_i V_i  (reorth: a second sweep
+ * whose coefficients are added), then h_{k+1} = ||q||.  V: host array of k device pointers; h (host,
+ * k + 1 doubles) receives the Hessenberg column.  Synchronises. */
+int nk_mgs_step(nk_ctx* ctx, int64_t n, const double* const* V, int32_t k, double* q, int32_t reorth, double* h);
+
 /* ---------------------------------------------------------------- device-resident Krylov solves
  * krylov_workspace(algo, KrylovConstructor(res)) + krylov_solve!(workspace, J, b; kwargs...)
  * (src/Ariadne.jl:317-318, :338), restating Krylov.jl 0.10 gmres!/cg! with M = N = I.  The

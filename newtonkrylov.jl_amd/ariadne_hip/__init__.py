@@ -10,7 +10,7 @@ from .device import Context, DeviceArray, Grid, default_context, set_default_con
 from .distributed import dist_unique_id, init_distributed, slab
 from .implicit import G_Euler_, G_Midpoint_, G_Trapezoid_, diffusion3d_, diffusion_, solve
 from .krylov import (KrylovConstructor, kaxpby_, kaxpy_, kaxpy_norm_, kcopy_, kdivcopy_, kdot, kfill_, knorm, kref_, krylov_solve_,
-                     krylov_workspace, kscal_)
+                     krylov_workspace, kscal_, mgs_step_)
 from .precond import (DiagonalPreconditioner, GmresPreconditioner, Ilu0Preconditioner, Preconditioner, UserPreconditioner,
                       gmres_preconditioner, ilu0, jacobi, jacobian_diag)
 from .problems import (DeviceResidual, UserResidual, bc_periodic_, bc_zero_, bratu2d_, bratu_, heat2d_euler_, heat2d_midpoint_,
@@ -24,7 +24,7 @@ __all__ = [
     "DiagonalPreconditioner", "GmresPreconditioner", "Ilu0Preconditioner", "Preconditioner", "UserPreconditioner",
     "gmres_preconditioner", "ilu0",
     "jacobi", "jacobian_diag",
-    "krylov_solve_", "krylov_workspace", "kscal_", "DeviceResidual", "UserResidual", "bc_zero_", "bratu2d_", "bratu_",
+    "krylov_solve_", "krylov_workspace", "kscal_", "mgs_step_", "DeviceResidual", "UserResidual", "bc_zero_", "bratu2d_", "bratu_",
     "heat2d_euler_", "heat3d_euler_", "heat2d_midpoint_", "heat3d_midpoint_", "heat2d_trapezoid_", "heat3d_trapezoid_",
     "bc_periodic_",
 ]

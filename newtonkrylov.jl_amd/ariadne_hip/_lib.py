@@ -107,6 +107,7 @@ SIGNATURES = {
     "nk_ilu0_factor": (C.c_int, [_VP, _PP, _VP, _VP]),
     "nk_precond_apply": (C.c_int, [_VP, _PP, _VP, _VP, _VP, _I32, _VP, _VP]),
     "nk_dot": (C.c_int, [_VP, _I64, _VP, _VP, _PD]),
+    "nk_mgs_step": (C.c_int, [_VP, _I64, C.POINTER(_VP), _I32, _VP, _I32, _PD]),
     "nk_norm": (C.c_int, [_VP, _I64, _VP, _PD]),
     "nk_scal": (C.c_int, [_VP, _I64, _D, _VP]),
     "nk_axpy": (C.c_int, [_VP, _I64, _D, _VP, _VP]),

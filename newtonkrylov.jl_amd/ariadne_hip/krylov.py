@@ -82,6 +82,16 @@ def kref_(n: int, x: DeviceArray, y: DeviceArray, c: float, s: float):
     return x, y
 
 
+def mgs_step_(V, q: DeviceArray, reorthogonalization: bool = False):
+    """One fused modified-Gram-Schmidt sweep of q against the basis V (Krylov.jl gmres! inner loop):
+    q is orthogonalised in place; returns the Hessenberg column [h_1 .. h_k, ||q||] (nk_mgs_step)."""
+    k = len(V)
+    ptrs = (C.c_void_p * k)(*[v.ptr for v in V])
+    h = (C.c_double * (k + 1))()
+    q.ctx.check(load().nk_mgs_step(_h(q), len(q), ptrs, k, q.ptr, int(bool(reorthogonalization)), h), "mgs_step!")
+    return np.array(h[:])
+
+
 # -------------------------------------------------------------------------- workspace / solve
 @dataclass
 class KrylovConstructor:

@@ -391,6 +391,33 @@ int nk_fill(nk_ctx* c, int64_t n, double* x, double v) { return c ? launch_fill(
 int nk_divcopy(nk_ctx* c, int64_t n, double* y, const double* x, double s) { return c ? launch_divcopy(c, n, y, x, s) : NK_E_ARG; }
 int nk_ref(nk_ctx* c, int64_t n, double* x, double* y, double cc, double ss) { return c ? launch_ref(c, n, x, y, cc, ss) : NK_E_ARG; }
 
+// One modified-Gram-Schmidt sweep of q against V_1..V_k -- the fused passes the device GMRES runs per
+// Arnoldi step, for callers that drive Krylov.jl's loop themselves (SURVEY §8b nk_mgs_step).
+int nk_mgs_step(nk_ctx* c, int64_t n, const double* const* V, int32_t k, double* q, int32_t reorth, double* h) {
+    if (!c || n < 1 || !V || k < 1 || !q || !h) return NK_E_ARG;
+    const int np = reorth ? 2 * k : k;
+    if (np + 1 > kScalCap) return fail(c, NK_E_ARG, "nk_mgs_step: k too large for the context's scalar scratch");
+    double* col = c->scal;  // device column: h of every pass, then ||q||
+    Red red{};
+    NK_TRY(launch_dot(c, n, V[0], q, &red));  // partials of <V_1, q>
+    for (int t = 0; t < np; ++t) {
+        const double* vi = V[t % k];
+        const double* vnext = (t + 1 < np) ? V[(t + 1) % k] : nullptr;
+        NK_TRY(finish_reduction(c, &red));
+        Red nxt{};
+        NK_TRY(launch_mgs_pass(c, n, q, vi, vnext, red, col + t, nullptr, &nxt, 0));
+        red = nxt;
+    }
+    NK_TRY(finish_reduction(c, &red));
+    NK_TRY(launch_finalize(c, red, col + np, 1));
+    NK_HIP(c, hipMemcpyAsync(c->hpin, col, sizeof(double) * (np + 1), hipMemcpyDeviceToHost, c->stream));
+    NK_TRY(nk_sync(c));
+    NK_TRY(mb_check(c));
+    for (int i = 0; i < k; ++i) h[i] = reorth ? c->hpin[i] + c->hpin[k + i] : c->hpin[i];
+    h[k] = c->hpin[np];
+    return NK_OK;
+}
+
 // ---------------------------------------------------------------- profiling
 int nk_prof_enable(nk_ctx* c, int32_t every) {
     if (!c || every < 0) return NK_E_ARG;

@@ -143,3 +143,29 @@ def test_reference_known_answers_through_the_device(ctx, golden_dir):
         np.testing.assert_allclose(u.to_numpy(), ka["root"], atol=1e-5)
         u, r = ah.newton_krylov_(K, ah.DeviceArray.from_numpy(np.array(x0)), None, jv="fd")
         assert r.solved
+
+
+@pytest.mark.parametrize("reorth", [False, True])
+def test_mgs_step_matches_numpy(reorth):
+    """nk_mgs_step (the fused MGS sweep as a primitive) against a numpy MGS with Krylov.jl's
+    order: h_i = <V_i, q>, q -= h_i V_i (fma), then ||q||; reorthogonalization adds a second sweep."""
+    ctx = ah.Context(0)
+    ah.set_default_context(ctx)
+    rng = np.random.default_rng(4)
+    n, k = 5000, 6
+    Q, _ = np.linalg.qr(rng.standard_normal((n, k)))
+    q0 = rng.standard_normal(n)
+    g = ah.Grid.full(n)
+    V = [ah.DeviceArray.from_numpy(np.ascontiguousarray(Q[:, i]), g) for i in range(k)]
+    qd = ah.DeviceArray.from_numpy(q0, g)
+    h = ah.mgs_step_(V, qd, reorthogonalization=reorth)
+    q = q0.copy()
+    href = np.zeros(k + 1)
+    for _ in range(2 if reorth else 1):
+        for i in range(k):
+            hi = float(np.dot(Q[:, i], q))
+            href[i] += hi
+            q = q - hi * Q[:, i]
+    href[k] = np.linalg.norm(q)
+    np.testing.assert_allclose(h, href, rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(qd.to_numpy(), q, rtol=0, atol=1e-13)
