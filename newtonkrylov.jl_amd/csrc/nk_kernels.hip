@@ -816,7 +816,8 @@ int launch_update_x(nk_ctx* c, int64_t n, double* x, double* xr, const double* c
     }
     while (done < k) {
         UpdArgs A{};
-        const int m = (k - done) < kMaxUpdateVecs ? (k - done) : kMaxUpdateVecs;
+        static const int cap = std::max(1, std::min(kMaxUpdateVecs, env_int("NK_UPD_VECS", kMaxUpdateVecs)));
+        const int m = (k - done) < cap ? (k - done) : cap;
         for (int i = 0; i < m; ++i) A.V[i] = V[done + i];
         A.x = x; A.xr = xr; A.y = y_dev + done; A.n = n; A.k = m;
         A.first = done == 0;
