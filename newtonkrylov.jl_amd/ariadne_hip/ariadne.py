@@ -170,6 +170,27 @@ def collect(J, *, coloring: str | None = None):
     user = getattr(Jo.f, "kind", 0) >= _lib.NK_USER1D
     coloring = coloring or ("dense" if user else "stencil")
     n = grid.n
+    periodic = Jo.problem().bc == _lib.NK_BC_PERIODIC
+    nx, ny, nz = grid.nxyz
+    idx = np.arange(n)
+    i, j, k = idx % nx, (idx // nx) % ny, idx // (nx * ny)
+    offs = [(0, 0, 0), (1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)][: 2 * grid.dim + 1]
+    nbr = []  # (rows, columns) of each stencil offset; bc_periodic! wraps the neighbour index
+    for di, dj, dk in offs:
+        ii, jj, kk = i + di, j + dj, k + dk
+        if periodic:
+            ii, jj, kk = ii % nx, jj % ny, kk % nz
+        ok = (ii >= 0) & (ii < nx) & (jj >= 0) & (jj < ny) & (kk >= 0) & (kk < nz)
+        nbr.append((idx[ok], ((kk * ny + jj) * nx + ii)[ok]))
+    if coloring == "stencil" and periodic:
+        # the colouring stays distance-2 across the wrap only for extents the colour period divides
+        color_chk = _stencil_colors(grid)[0].reshape(-1)
+        seen = np.stack([color_chk[((k + dk) % nz * ny + (j + dj) % ny) * nx + (i + di) % nx] for di, dj, dk in offs])
+        if any(len(set(col)) != len(offs) for col in seen.T):
+            if n > 4096:
+                raise ValueError("collect(J) with bc_periodic!: the stencil colouring needs extents divisible by "
+                                 f"{2 * grid.dim + 1}; this grid has {n} points (too many for unit probing)")
+            coloring = "dense"
     out = Jo.u.zero()
     if coloring == "dense":
         if n > 4096:
@@ -186,21 +207,13 @@ def collect(J, *, coloring: str | None = None):
         raise ValueError("coloring must be 'stencil' or 'dense'")
     color, ncol = _stencil_colors(grid)
     color = color.reshape(-1)
-    nx, ny, nz = grid.nxyz
-    idx = np.arange(n)
-    i, j, k = idx % nx, (idx // nx) % ny, idx // (nx * ny)
-    offs = [(0, 0, 0), (1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)][: 2 * grid.dim + 1]
     rows, cols, vals = [], [], []
     probes = []
     for c in range(ncol):
         v = DeviceArray.from_numpy((color == c).astype(np.float64).reshape(grid.np_shape), grid, Jo.u.ctx)
         mul_(out, J, v)
         probes.append(out.to_numpy().reshape(-1))
-    for di, dj, dk in offs:  # entry (row p, column q = p + offset) sits in the probe of q's colour
-        ii, jj, kk = i + di, j + dj, k + dk
-        ok = (ii >= 0) & (ii < nx) & (jj >= 0) & (jj < ny) & (kk >= 0) & (kk < nz)
-        q = (kk * ny + jj) * nx + ii
-        p_ok, q_ok = idx[ok], q[ok]
+    for p_ok, q_ok in nbr:  # entry (row p, column q = p + offset) sits in the probe of q's colour
         rows.append(p_ok)
         cols.append(q_ok)
         vals.append(np.array([probes[c][r] for c, r in zip(color[q_ok], p_ok)]) if len(p_ok) else np.zeros(0))
