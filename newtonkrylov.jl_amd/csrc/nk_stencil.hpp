@@ -213,9 +213,11 @@ __device__ __forceinline__ Row<VEC> field_row(const KArgs& A, int64_t o, bool ok
 
 // NT: non-temporal (streams not re-read before they would be evicted anyway): between two Jv
 // launches the MGS passes stream ~16 vectors through the caches.  NK_ST_NT: F(u) loads and V_k
-// stores of the fused Jv; NK_ST_NTU: the FD operator's u loads.  Measured A/B on one box: FD Jv
+// stores of the fused Jv; NK_ST_NTU: the 2D FD operator's u loads.  Measured A/B on one box: FD Jv
 // 141 -> 129.5 -> 127.2 us at 4096^2 (+1.3 % whole bench), heat 8192^2 neutral.  The v (= q) and
-// V_1 loads stay cached: q was just written by the last MGS pass, V_1 is re-read by the next one.
+// V_1 loads stay cached: q was just written by the last MGS pass, V_1 is re-read by the next one;
+// the 3D kernel keeps u cached too (its y-neighbour rows are re-read by the adjacent waves: NT u
+// loads cost 12 % at 512^3).
 #ifndef NK_ST_NT
 #define NK_ST_NT 1
 #endif
@@ -276,14 +278,14 @@ struct RawRow {
     double g[VEC], ge, ge2;  // u_n (G)
 };
 
-template <int MODE, int VEC, bool EDGE = true, bool G = false, bool PER = false>
+template <int MODE, int VEC, bool EDGE = true, bool G = false, bool PER = false, bool NTU = false>
 __device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o, int64_t oe, int64_t oe2 = 0) {
     RawRow<MODE, VEC> r;
     const double* __restrict__ pa = (MODE == MODE_JEXACT) ? A.v : A.u;
     if constexpr (VEC % 2 == 0) {
 #pragma unroll
         for (int h = 0; h < VEC; h += 2) {
-            if constexpr (NK_ST_NTU && MODE == MODE_JFD) {
+            if constexpr (NTU && MODE == MODE_JFD) {
                 const dv2 q = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(pa + o + h));
                 r.a[h] = q.x; r.a[h + 1] = q.y;
             } else {
@@ -472,13 +474,13 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     if (y0 < ny) {
         // rows y0-1 (ghost plane when y0 = 0) and y0 cooked up front; row y0+1 raw in flight
         Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(
-            A, load_raw<MODE, VEC, true, kG, PER>(A, (y0 - 1) * nx + xc, (y0 - 1) * nx + xc + de, (y0 - 1) * nx + xc + de2),
+            A, load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 - 1) * nx + xc, (y0 - 1) * nx + xc + de, (y0 - 1) * nx + xc + de2),
             act, false, false);
         Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(
-            A, load_raw<MODE, VEC, true, kG, PER>(A, y0 * nx + xc, y0 * nx + xc + de, y0 * nx + xc + de2), act, edge_ok,
+            A, load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, y0 * nx + xc, y0 * nx + xc + de, y0 * nx + xc + de2), act, edge_ok,
             edge_ok2);
         RawRow<MODE, VEC> rp =
-            load_raw<MODE, VEC, true, kG, PER>(A, (y0 + 1) * nx + xc, (y0 + 1) * nx + xc + de, (y0 + 1) * nx + xc + de2);
+            load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 + 1) * nx + xc, (y0 + 1) * nx + xc + de, (y0 + 1) * nx + xc + de2);
         Row<VEC> uc{}, unc{}, f0c{}, ax{};
         {
             const int64_t o = y0 * nx + xc;
@@ -492,7 +494,7 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
             // ---- issue: raw row j+2 (rows up to ny are the ghost plane; y1 <= ny keeps j+2 <= ny+1
             //      in range only when j+1 < y1, so clamp to row j+1 otherwise)
             const int64_t o2 = (j + 1 < y1) ? o + 2 * nx : o + nx;
-            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2);
+            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, o2, o2 + de, o2 + de2);
             Row<VEC> ucn{}, uncn{}, f0cn{}, axn{};
             const int64_t o1 = (j + 1 < y1) ? o + nx : o;
             if constexpr (kU) ucn = data_row<VEC>(A.u, o1, true);
