@@ -224,6 +224,9 @@ __device__ __forceinline__ Row<VEC> field_row(const KArgs& A, int64_t o, bool ok
 #ifndef NK_ST_NTU
 #define NK_ST_NTU 1
 #endif
+#ifndef NK_ST_NTN  // u_n (centre-only loads of G_Euler!): +0.2-0.5 % heat 8192^2 / 512^3
+#define NK_ST_NTN 1
+#endif
 typedef double dv2 __attribute__((ext_vector_type(2)));
 template <int VEC, bool NT = false>
 __device__ __forceinline__ Row<VEC> data_row(const double* __restrict__ p, int64_t o, bool ok) {
@@ -485,7 +488,7 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
         {
             const int64_t o = y0 * nx + xc;
             if constexpr (kU) uc = data_row<VEC>(A.u, o, true);
-            if constexpr (kUn) unc = data_row<VEC>(A.un, o, true);
+            if constexpr (kUn) unc = data_row<VEC, NK_ST_NTN>(A.un, o, true);
             if constexpr (kF0) f0c = data_row<VEC, NK_ST_NT>(A.F0, o, true);
             if constexpr (kAx) ax = data_row<VEC>(A.aux, o, true);
         }
@@ -498,7 +501,7 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
             Row<VEC> ucn{}, uncn{}, f0cn{}, axn{};
             const int64_t o1 = (j + 1 < y1) ? o + nx : o;
             if constexpr (kU) ucn = data_row<VEC>(A.u, o1, true);
-            if constexpr (kUn) uncn = data_row<VEC>(A.un, o1, true);
+            if constexpr (kUn) uncn = data_row<VEC, NK_ST_NTN>(A.un, o1, true);
             if constexpr (kF0) f0cn = data_row<VEC, NK_ST_NT>(A.F0, o1, true);
             if constexpr (kAx) axn = data_row<VEC>(A.aux, o1, true);
             // ---- cook row j+1 (its loads were issued one iteration ago)
@@ -610,7 +613,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
         RawRow<MODE, VEC> rn = load_raw<MODE, VEC, false, kG, PER>(A, o0 + dn, 0);
         RawRow<MODE, VEC> rs = load_raw<MODE, VEC, false, kG, PER>(A, o0 + ds, 0);
         Row<VEC> unc{}, f0c{}, ax{};
-        if constexpr (kUn) unc = data_row<VEC>(A.un, o0, true);
+        if constexpr (kUn) unc = data_row<VEC, NK_ST_NTN>(A.un, o0, true);
         if constexpr (kF0) f0c = data_row<VEC, NK_ST_NT>(A.F0, o0, true);
         if constexpr (kAx) ax = data_row<VEC>(A.aux, o0, true);
         for (int64_t k = z0; k < z1; ++k) {
@@ -623,7 +626,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
             const RawRow<MODE, VEC> rnn = load_raw<MODE, VEC, false, kG, PER>(A, o1 + dn, 0);
             const RawRow<MODE, VEC> rss = load_raw<MODE, VEC, false, kG, PER>(A, o1 + ds, 0);
             Row<VEC> uncn{}, f0cn{}, axn{};
-            if constexpr (kUn) uncn = data_row<VEC>(A.un, o1, true);
+            if constexpr (kUn) uncn = data_row<VEC, NK_ST_NTN>(A.un, o1, true);
             if constexpr (kF0) f0cn = data_row<VEC, NK_ST_NT>(A.F0, o1, true);
             if constexpr (kAx) axn = data_row<VEC>(A.aux, o1, true);
             // ---- cook what was issued one iteration ago
