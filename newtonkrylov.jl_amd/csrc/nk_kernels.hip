@@ -207,7 +207,7 @@ __device__ __forceinline__ void st2(dx2* p, dx2 v) {
 // starts on the lines the previous pass touched last (still in the 256 MB Infinity Cache).
 // CH = true: block-contiguous chunks (each block sweeps its own range, threads interleaved) instead
 // of the grid-stride order -- fewer DRAM page switches once the vectors outgrow the Infinity Cache.
-template <bool HAS_NEXT, int U, bool NT, bool NTW = false, bool CH = false>
+template <bool HAS_NEXT, int U, bool NT, bool NTW = false, bool CH = false, bool NTQ = false>
 __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restrict__ q, const double* __restrict__ vi,
                                                     const double* __restrict__ vnext, const double* __restrict__ red_in,
                                                     int red_len, double* __restrict__ h_out, double* __restrict__ h_host,
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restri
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t e = base + sgn * (i + u * st);
-            a[u] = ld2<false>(q2 + e);
+            a[u] = ld2<NTQ>(q2 + e);
             bv[u] = ld2<NT>(v2 + e);
             if constexpr (HAS_NEXT) cv[u] = ld2<NTW>(w2 + e);
         }
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restri
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t e = base + sgn * (i + u * st);
-                a[u] = ld2<false>(q2 + e);
+                a[u] = ld2<NTQ>(q2 + e);
                 bv[u] = ld2<NT>(v2 + e);
                 if constexpr (HAS_NEXT) cv[u] = ld2<NTW>(w2 + e);
             }
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(kBlock) void k_mgs_pass(int64_t n, double* __restri
         for (int u = 0; u < U; ++u) {
             a[u].x = fma(mh, bv[u].x, a[u].x);
             a[u].y = fma(mh, bv[u].y, a[u].y);
-            st2<false>(q2 + base + sgn * (i + u * st), a[u]);
+            st2<NTQ>(q2 + base + sgn * (i + u * st), a[u]);
             if constexpr (HAS_NEXT) {
                 acc = fma(cv[u].x, a[u].x, acc);
                 acc = fma(cv[u].y, a[u].y, acc);
@@ -783,7 +783,9 @@ void mgs_dispatch(int variant, int g, hipStream_t s, int64_t n, double* q, const
     case 3: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
     case 4: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
     case 5: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, false, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
-    default: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true, false, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
+    case 6: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true, false, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
+    case 7: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
+    default: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, true, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
     }
 }
 }  // namespace
@@ -791,7 +793,11 @@ void mgs_dispatch(int variant, int g, hipStream_t s, int64_t n, double* q, const
 int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const double* vnext, Red in, double* h_out,
                     double* h_host, Red* out,
                     int rev) {
-    static const int variant = env_int("NK_MGS_VARIANT", kMgsVariant);
+    // vectors that fit the 256 MB Infinity Cache twice over (q + V_{i+1} re-read by the next pass):
+    // cached q / V_{i+1} (variant 5); larger ones stream every operand non-temporally (variant 8:
+    // +1.8 % heat 8192^2, +2.3 % heat 512^3; it costs 16 % at 4096^2)
+    static const int forced = env_int("NK_MGS_VARIANT", -1);
+    const int variant = forced >= 0 ? forced : (8.0 * (double)n > 256.0 * (1 << 20) ? 8 : kMgsVariant);
     const int g = red_blocks(n);
     int fin;
     double* part = red_out(c, g, out, &fin);
