@@ -86,7 +86,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--transport", choices=["rccl", "mailbox"], default="rccl",
                     help="N > 1: rccl = nk_dist_init (RCCL bootstrap; peer mailbox + IPC ghost planes when available); "
-                         "mailbox = IPC handles over gloo, no RCCL (diagnostic: lets ranks share one GPU)")
+                         "mailbox = IPC handles over gloo, no RCCL (diagnostic: lets ranks share one GPU -- with "
+                         "small slabs only (e.g. --side 1024): a rank's spin-waiting reduction consumers must leave "
+                         "the other rank's kernels room on the shared GPU)")
     ap.add_argument("--cpu-itmax", type=int, default=300, help="Arnoldi steps in the CPU-baseline sample (300 = one bench step)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os.cpu_count())")
     ap.add_argument("--traffic-json", default="",
