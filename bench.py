@@ -53,7 +53,7 @@ def stencil_prefix(workload, scheme="euler"):
 
 def pmc_name(workload, kernel, scheme="euler"):
     st = stencil_prefix(workload, scheme)
-    return {"mgs_pass": "nk::k_mgs_pass<true,", "mgs_pass_last": "nk::k_mgs_pass<false,",
+    return {"mgs_pass": "nk::k_mgs_pass<true,", "mgs_pass_last": "nk::k_mgs_pass<false,", "mgs_sweep": "nk::k_mgs_res<",
             "jv_fd_dot_norm": st + "2, 4,", "jv_exact_dot_norm": st + "1, 4,", "jv_fd_dot": st + "2, 2,",
             "residual_norm": st + "0, 1,", "divcopy": "nk::k_divcopy", "update_x": "nk::k_update_x"}.get(kernel)
 LAMBDA = 3.51382       # examples/bratu.jl:41

@@ -212,6 +212,8 @@ int nk_ctx_destroy(nk_ctx* c) {
     (void)hipFree(c->red);
     (void)hipFree(c->scal);
     (void)hipHostFree(c->hpin);
+    if (c->res_gran) (void)hipFree(c->res_gran);
+    if (c->res_err) (void)hipHostFree(c->res_err);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return NK_OK;

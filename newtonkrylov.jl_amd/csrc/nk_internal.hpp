@@ -77,6 +77,13 @@ struct nk_ctx {
     unsigned mb_epoch = 1;
     int64_t halo_cap = 0;                  // doubles per inbox plane (0: no IPC halo exchange)
     uint64_t halo_epoch = 0;
+    // resident MGS sweep (launch_mgs_sweep): one block per CU, q held in registers + LDS
+    bool res_ok = true;                    // false when another rank shares this GPU (co-residency)
+    uint64_t* res_gran = nullptr;          // partial-sum granules: 2 parities x res_blocks x 2
+    int* res_err = nullptr;                // pinned host flag: a granule poll timed out
+    int* res_err_dev = nullptr;
+    unsigned res_tag = 0;                  // granule tags handed out so far
+    int res_blocks = 0, res_rl = 0;        // grid (= CUs) and LDS double2 slots per thread
     // distribution
     int rank = 0, nranks = 1;
     nk::Comm* comm = nullptr;
@@ -147,6 +154,10 @@ double* red_out(nk_ctx* c, int len, Red* r, int* fin);  // slot for a reduction 
 int finish_reduction(nk_ctx* c, Red* r);     // multi-rank: collapse + RCCL all-reduce
 int mb_check(nk_ctx* c);                     // after a host sync: did a mailbox wait time out?
 int red_blocks(int64_t n);                   // grid size of streaming reductions
+// One Arnoldi step's MGS sweep in one launch (np passes over V[t % k], then ||q||) with q resident
+// on chip; returns 1 (nothing enqueued) when the resident path does not apply.
+int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, int k, int np, Red in, double* col,
+                     double* colh, int rv);
 constexpr int kMbSlots = 256;                // mailbox ring (epoch % kMbSlots)
 constexpr int kMbRanks = 32;                 // max ranks of the mailbox all-reduce (2 granules each: one wave polls them all)
 constexpr int kHaloBlocks = 64;              // blocks (= flags per side) of the IPC ghost-plane exchange

@@ -788,7 +788,296 @@ void mgs_dispatch(int variant, int g, hipStream_t s, int64_t n, double* q, const
     default: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, true, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
     }
 }
+
+// ------------------------------------------------------------------------------ resident MGS sweep
+// One Arnoldi step's whole MGS sweep (np passes + h_{k+1,k} = ||q||) in ONE launch, with q held
+// on chip: one block per CU owns a contiguous chunk of q; its first RV x 256 double2 live in
+// registers, the next rl x 256 in LDS, only the rest streams through memory.  A pass then reads
+// V_i and V_{i+1} (16 B/pt; V_{i+1} is re-read as the next pass's V_i from the Infinity Cache)
+// instead of q, V_i, V_{i+1} and the q write-back (32 B/pt).  Per-element arithmetic is exactly
+// k_mgs_pass's (q = fma(-h, V_i, q); acc = fma(V_{i+1}, q, acc)); only the partition of the
+// partial sums differs, and it is fixed, so results stay run-to-run bit reproducible.
+// Between passes every block needs h = Σ_b partial_b: each block publishes its partial as two
+// self-validating {tag:32 | half:32} granules (cdna_hip_programming.md §6 G16, R2 -- the data is
+// the flag, no fence) into a parity-double-buffered slot, then polls all G partials and sums them
+// in block order -- the same tree in every block, so every block holds the bit-identical h.
+// Double buffering is enough: a block can write pass t+2's granule only after reading everyone's
+// pass t+1 granule, i.e. after everyone finished reading pass t's.  Every spin is bounded.
+// Requires all G blocks co-resident: G = #CUs, 1 block per CU (the LDS share forces it).
+constexpr int kResMax = 64;  // passes per launch (reorthogonalisation: 2k)
+constexpr int kResThreads = 256;
+struct ResArgs {
+    const double* V[kResMax + 1];  // pass t: V_i = V[t], V_{i+1} = V[t + 1]
+    double* q;
+    double* col;   // h of every pass, ||q|| at [np]
+    double* colh;  // pinned host mirror
+    const double* red_in;  // partials of h of the first pass (the Jv's <V_1, q>)
+    uint64_t* gran;        // 2 parities x G blocks x 2 granules
+    int* err;              // pinned host flag: a poll timed out
+    int64_t n2;            // double2 elements
+    int np, red_len, rl;
+    unsigned tag0, mb0, spin;
+};
+
+template <int RV>
+struct ResState {
+    dx2 r[RV];
+};
+
+// `budget`: this thread's remaining polls for the whole launch (a stuck grid drains in bounded time)
+__device__ __forceinline__ double res_exchange(const ResArgs& A, double part, int t, double* sh, unsigned& budget) {
+    const int tid = threadIdx.x, G = gridDim.x;
+    const unsigned tag = A.tag0 + (unsigned)t;
+    uint64_t* slot = A.gran + (size_t)(t & 1) * G * 2;
+    if (tid == 0) {
+        const uint64_t bits = (uint64_t)__double_as_longlong(part);
+        __hip_atomic_store(slot + 2 * blockIdx.x, ((uint64_t)tag << 32) | (bits & 0xffffffffull), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(slot + 2 * blockIdx.x + 1, ((uint64_t)tag << 32) | (bits >> 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    double v = 0.0;
+    if (tid < G) {
+        const uint64_t* g = slot + 2 * tid;
+        uint64_t lo = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t hi = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while ((unsigned)(lo >> 32) != tag || (unsigned)(hi >> 32) != tag) {
+            if (budget == 0 || --budget == 0) {
+                __hip_atomic_store(A.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                lo = hi = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            lo = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            hi = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        v = __longlong_as_double((long long)(((hi & 0xffffffffull) << 32) | (lo & 0xffffffffull)));
+    }
+    __syncthreads();  // thread 0 is done with sh[] of the partial's block_sum
+    double s = block_sum<kResThreads>(v, sh);
+    if (tid == 0) sh[kShB] = s;
+    __syncthreads();
+    s = sh[kShB];
+    if (A.mb0 == 0) return s;
+    const unsigned epoch = A.mb0 + (unsigned)t;  // cross-rank: the peer mailbox, as reduce_input does
+    if (blockIdx.x == 0) mb_send(s, epoch);
+    __syncthreads();
+    return mb_recv(epoch, sh);
+}
+
+// one pass over this block's chunk: q -= h V_i, partial of <V_{i+1}, q> (NEXT) or <q, q>.  The
+// host guarantees every block's chunk covers its RV + rl resident slots (no predicates there).
+template <int RV>
+__device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx2* lq, int t, double mh, int64_t lo,
+                                           int64_t hi) {
+    const int tid = threadIdx.x;
+    const bool next = t + 1 < A.np;  // last pass: <q, q> instead of <V_{i+1}, q>
+    const dx2* vb = reinterpret_cast<const dx2*>(A.V[t]) + lo + tid;
+    const dx2* wb = reinterpret_cast<const dx2*>(A.V[next ? t + 1 : t]) + lo + tid;
+    double acc = 0.0;
+    auto upd = [&](dx2& a, const dx2 b, const dx2 c) {
+        a.x = fma(mh, b.x, a.x);
+        a.y = fma(mh, b.y, a.y);
+        const dx2 p = next ? c : a;
+        acc = fma(p.x, a.x, acc);
+        acc = fma(p.y, a.y, acc);
+    };
+    constexpr int B = RV > 64 ? 4 : 8;  // slots per batch: 2 x B 16-B loads in flight per lane
+#pragma unroll
+    for (int s0 = 0; s0 < RV; s0 += B) {
+        dx2 bv[B], cv[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            if (s0 + u < RV) {
+                bv[u] = __builtin_nontemporal_load(vb + (s0 + u) * kResThreads);
+                cv[u] = wb[(s0 + u) * kResThreads];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+            if (s0 + u < RV) upd(S.r[s0 + u], bv[u], cv[u]);
+        __builtin_amdgcn_sched_barrier(0);  // no hoisting across batches: registers hold q, not loads
+    }
+    const dx2* vl = vb + RV * kResThreads;
+    const dx2* wl = wb + RV * kResThreads;
+    const int rl = A.rl;
+    int s = 0;
+    for (; s + 4 <= rl; s += 4) {
+        dx2 bv[4], cv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            bv[u] = __builtin_nontemporal_load(vl + (s + u) * kResThreads);
+            cv[u] = wl[(s + u) * kResThreads];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            dx2 a = lq[(s + u) * kResThreads + tid];
+            upd(a, bv[u], cv[u]);
+            lq[(s + u) * kResThreads + tid] = a;
+        }
+    }
+    for (; s < rl; ++s) {
+        const dx2 b = __builtin_nontemporal_load(vl + s * kResThreads);
+        const dx2 cc = wl[s * kResThreads];
+        dx2 a = lq[s * kResThreads + tid];
+        upd(a, b, cc);
+        lq[s * kResThreads + tid] = a;
+    }
+    // the streamed remainder: q through memory, as k_mgs_pass
+    dx2* q2 = reinterpret_cast<dx2*>(A.q);
+    const dx2* v2 = reinterpret_cast<const dx2*>(A.V[t]);
+    const dx2* w2 = reinterpret_cast<const dx2*>(A.V[next ? t + 1 : t]);
+    int64_t e = lo + (int64_t)(RV + rl) * kResThreads + tid;
+    for (; e + kResThreads < hi; e += 2 * kResThreads) {
+        const int64_t e1 = e + kResThreads;
+        dx2 a0 = q2[e], a1 = q2[e1];
+        const dx2 b0 = __builtin_nontemporal_load(v2 + e), b1 = __builtin_nontemporal_load(v2 + e1);
+        const dx2 c0 = w2[e], c1 = w2[e1];
+        upd(a0, b0, c0);
+        upd(a1, b1, c1);
+        q2[e] = a0;
+        q2[e1] = a1;
+    }
+    if (e < hi) {
+        dx2 a0 = q2[e];
+        const dx2 b0 = __builtin_nontemporal_load(v2 + e);
+        const dx2 c0 = w2[e];
+        upd(a0, b0, c0);
+        q2[e] = a0;
+    }
+    return acc;
+}
+
+template <int RV>
+__global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
+    extern __shared__ dx2 lq[];  // rl x 256 double2
+    __shared__ double sh[kShN];
+    const int tid = threadIdx.x, G = gridDim.x;
+    const int64_t per = ((A.n2 + G - 1) / G + kResThreads - 1) / kResThreads * kResThreads;
+    const int64_t lo = (int64_t)blockIdx.x * per;
+    const int64_t hi = lo + per < A.n2 ? lo + per : A.n2;
+    const dx2* qb = reinterpret_cast<const dx2*>(A.q) + lo + tid;
+    ResState<RV> S;
+#pragma unroll
+    for (int s = 0; s < RV; ++s) S.r[s] = qb[s * kResThreads];
+    for (int s = 0; s < A.rl; ++s) lq[s * kResThreads + tid] = qb[(RV + s) * kResThreads];
+    double h = reduce_input(A.red_in, A.red_len, sh);
+    unsigned budget = A.spin;
+    for (int t = 0; t < A.np; ++t) {
+        if (blockIdx.x == 0 && tid == 0) {
+            A.col[t] = h;
+            if (A.colh) A.colh[t] = h;
+        }
+        const double acc = res_pass<RV>(A, S, lq, t, -h, lo, hi);
+        const double part = block_sum<kResThreads>(acc, sh);
+        h = res_exchange(A, part, t, sh, budget);
+    }
+    if (blockIdx.x == 0 && tid == 0) {
+        const double r = sqrt(h);
+        A.col[A.np] = r;
+        if (A.colh) A.colh[A.np] = r;
+    }
+    dx2* qw = reinterpret_cast<dx2*>(A.q) + lo + tid;
+#pragma unroll
+    for (int s = 0; s < RV; ++s) qw[s * kResThreads] = S.r[s];
+    for (int s = 0; s < A.rl; ++s) qw[(RV + s) * kResThreads] = lq[s * kResThreads + tid];
+}
+
+template <int RV>
+int res_attr(nk_ctx* c, size_t lds) {
+    NK_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+    return NK_OK;
+}
 }  // namespace
+
+// Resident sweep: returns NK_OK after enqueueing, or 1 when the resident path does not apply
+// (caller falls back to one k_mgs_pass launch per pass).
+int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, int k, int np, Red in, double* col,
+                     double* colh, int rv) {
+    if (np < 1 || np > kResMax || (n & 1) || !c->res_ok) return 1;
+    if (c->comm && !c->mb_on) return 1;  // RCCL reductions need the host between passes
+    if (!c->res_gran) {
+        int dev = 0, cus = 0, lds = 0;
+        NK_HIP(c, hipGetDevice(&dev));
+        NK_HIP(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        NK_HIP(c, hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
+        if (cus < 1 || cus > kResThreads) return 1;
+        c->res_blocks = cus;
+        const int avail = lds - (int)(sizeof(double) * kShN) - 256;
+        c->res_rl = std::max(0, avail / (int)(kResThreads * sizeof(dx2)));
+        NK_HIP(c, hipMalloc(&c->res_gran, sizeof(uint64_t) * 4 * kResThreads));
+        NK_HIP(c, hipMemsetAsync(c->res_gran, 0, sizeof(uint64_t) * 4 * kResThreads, c->stream));
+        NK_HIP(c, hipHostMalloc(&c->res_err, sizeof(int), hipHostMallocMapped));
+        *c->res_err = 0;
+        NK_HIP(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->res_err_dev), c->res_err, 0));
+        const size_t lmax = (size_t)c->res_rl * kResThreads * sizeof(dx2);
+        NK_TRY(res_attr<0>(c, lmax));
+        NK_TRY(res_attr<16>(c, lmax));
+        NK_TRY(res_attr<32>(c, lmax));
+        NK_TRY(res_attr<48>(c, lmax));
+        NK_TRY(res_attr<64>(c, lmax));
+        NK_TRY(res_attr<89>(c, lmax));
+    }
+    ResArgs A{};
+    for (int t = 0; t < np; ++t) A.V[t] = V[t % k];
+    A.V[np] = V[(np) % k];
+    A.q = q;
+    A.col = col;
+    A.colh = colh;
+    A.red_in = in.ptr;
+    A.red_len = in.len;
+    A.gran = c->res_gran;
+    A.err = c->res_err_dev;
+    A.n2 = n >> 1;
+    A.np = np;
+    {  // every block's chunk must hold its rv + rl resident slots (the kernel does not predicate them)
+        const int64_t G = c->res_blocks, n2 = n >> 1;
+        const int64_t per = ((n2 + G - 1) / G + kResThreads - 1) / kResThreads * kResThreads;
+        const int64_t last = n2 - (G - 1) * per;  // the shortest chunk
+        if (last < kResThreads) return 1;
+        const int slots = (int)std::min<int64_t>(std::min(per, last) / kResThreads, 1 << 20);
+        static const int rl_env = env_int("NK_RES_RL", -1);
+        static const int rv_env = env_int("NK_RES_RV", -1);
+        int rl = std::min(slots, rl_env >= 0 ? std::min(rl_env, c->res_rl) : c->res_rl);  // LDS first
+        if (rv < 0) rv = rv_env >= 0 ? rv_env : slots - rl;  // registers hold what the LDS cannot
+        static const int kRv[] = {89, 64, 48, 32, 16, 0};  // the instantiated register-slot counts
+        int pick = 0;
+        for (int r : kRv)
+            if (r <= rv && r <= slots) {
+                pick = r;
+                break;
+            }
+        rv = pick;
+        A.rl = std::min(rl, slots - rv);
+    }
+    if (c->res_tag > 0xfffffff0u - (unsigned)kResMax) {  // tag wrap: restart from clean granules
+        NK_HIP(c, hipMemsetAsync(c->res_gran, 0, sizeof(uint64_t) * 4 * kResThreads, c->stream));
+        c->res_tag = 0;
+    }
+    A.tag0 = c->res_tag + 1;
+    c->res_tag += (unsigned)np;
+    A.mb0 = 0;
+    if (c->mb_on) {  // np consecutive mailbox epochs, no 16-bit wrap inside the range
+        if (c->mb_epoch + (unsigned)np > 0xffffu) c->mb_epoch = 0;
+        A.mb0 = c->mb_epoch + 1;
+        c->mb_epoch += (unsigned)np;
+    }
+    A.spin = 1u << 22;  // polls per thread per launch (~1 s): a grid that is not co-resident fails fast
+    const size_t lds = (size_t)A.rl * kResThreads * sizeof(dx2);
+    const double bytes = 16.0 * n + (16.0 * np - 8.0) * n;  // q in + out, V_i (+ V_{i+1}) per pass
+    return launch(c, "mgs_sweep", bytes, [&] {
+        const dim3 g(c->res_blocks), b(kResThreads);
+        switch (rv) {
+        case 0: hipLaunchKernelGGL(k_mgs_res<0>, g, b, lds, c->stream, A); break;
+        case 16: hipLaunchKernelGGL(k_mgs_res<16>, g, b, lds, c->stream, A); break;
+        case 48: hipLaunchKernelGGL(k_mgs_res<48>, g, b, lds, c->stream, A); break;
+        case 64: hipLaunchKernelGGL(k_mgs_res<64>, g, b, lds, c->stream, A); break;
+        case 89: hipLaunchKernelGGL(k_mgs_res<89>, g, b, lds, c->stream, A); break;
+        default: hipLaunchKernelGGL(k_mgs_res<32>, g, b, lds, c->stream, A); break;
+        }
+    });
+}
 
 int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const double* vnext, Red in, double* h_out,
                     double* h_host, Red* out,
@@ -1109,6 +1398,91 @@ extern "C" int nkb_stencil3d(nk_ctx* c, int64_t n, int mode, int epi, int fast, 
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     for (double* q : {u, v, F0, aux, out, un}) nk_vec_free(c, q);
+    return NK_OK;
+}
+
+namespace nk {
+namespace {
+__global__ __launch_bounds__(kBlock) void k_hashfill(int64_t n, double* __restrict__ x, uint64_t seed) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        uint64_t z = (uint64_t)i * 0x9e3779b97f4a7c15ull + seed;
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        z ^= z >> 31;
+        x[i] = (double)(z >> 11) * 0x1.0p-53 - 0.5;
+    }
+}
+}  // namespace
+}  // namespace nk
+
+// The resident MGS sweep (launch_mgs_sweep, register slots rv) against the per-pass chain
+// (launch_mgs_pass) on the same q and basis: us_out / us_ref = microseconds per pass of each;
+// diff_out = max |q_res - q_chain| / max |q_chain| after the sweep, and the largest relative
+// difference of the Hessenberg column in diff_out[1].
+extern "C" int nkb_mgs_res(nk_ctx* c, int64_t n, int k, int rv, int reps, double* us_out, double* us_ref, double* diff_out) {
+    using namespace nk;
+    if (!c || n < 2 || k < 1 || k > kResMax || reps < 1 || !us_out || !us_ref || !diff_out) return NK_E_ARG;
+    std::vector<double*> V(k + 3, nullptr);
+    for (size_t v = 0; v < V.size(); ++v) {
+        NK_HIP(c, hipMalloc(&V[v], sizeof(double) * n));
+        hipLaunchKernelGGL(k_hashfill, dim3(2048), dim3(kBlock), 0, c->stream, n, V[v], (uint64_t)(v + 1) * 7919u);
+    }
+    double* q0 = V[k];
+    double* qa = V[k + 1];
+    double* qb = V[k + 2];
+    double* col = c->scal + 64;
+    double* col2 = c->scal + 64 + 2 * kResMax;
+    hipEvent_t e0, e1;
+    NK_HIP(c, hipEventCreate(&e0));
+    NK_HIP(c, hipEventCreate(&e1));
+    double ms_a = 0.0, ms_b = 0.0;
+    for (int r = 0; r <= reps; ++r) {
+        float ms = 0.f;
+        NK_TRY(launch_copy(c, n, qa, q0));
+        Red red{};
+        NK_TRY(launch_dot(c, n, V[0], qa, &red));
+        NK_HIP(c, hipEventRecord(e0, c->stream));
+        for (int t = 0; t < k; ++t) {
+            Red nxt{};
+            NK_TRY(launch_mgs_pass(c, n, qa, V[t], t + 1 < k ? V[t + 1] : nullptr, red, col + t, nullptr, &nxt, 0));
+            red = nxt;
+        }
+        NK_TRY(launch_finalize(c, red, col + k, 1, nullptr));
+        NK_HIP(c, hipEventRecord(e1, c->stream));
+        NK_HIP(c, hipEventSynchronize(e1));
+        NK_HIP(c, hipEventElapsedTime(&ms, e0, e1));
+        if (r > 0) ms_a += ms;
+        NK_TRY(launch_copy(c, n, qb, q0));
+        NK_TRY(launch_dot(c, n, V[0], qb, &red));
+        NK_HIP(c, hipEventRecord(e0, c->stream));
+        const int rc = launch_mgs_sweep(c, n, qb, V.data(), k, k, red, col2, nullptr, rv);
+        if (rc != NK_OK) return rc == 1 ? fail(c, NK_E_ARG, "resident sweep not applicable") : rc;
+        NK_HIP(c, hipEventRecord(e1, c->stream));
+        NK_HIP(c, hipEventSynchronize(e1));
+        NK_HIP(c, hipEventElapsedTime(&ms, e0, e1));
+        if (r > 0) ms_b += ms;
+        if (*c->res_err) return fail(c, NK_E_HIP, "resident sweep: granule poll timed out");
+    }
+    *us_ref = 1e3 * ms_a / ((double)reps * k);
+    *us_out = 1e3 * ms_b / ((double)reps * k);
+    std::vector<double> a(n), b(n), ca(k + 1), cb(k + 1);
+    NK_HIP(c, hipMemcpy(a.data(), qa, sizeof(double) * n, hipMemcpyDeviceToHost));
+    NK_HIP(c, hipMemcpy(b.data(), qb, sizeof(double) * n, hipMemcpyDeviceToHost));
+    NK_HIP(c, hipMemcpy(ca.data(), col, sizeof(double) * (k + 1), hipMemcpyDeviceToHost));
+    NK_HIP(c, hipMemcpy(cb.data(), col2, sizeof(double) * (k + 1), hipMemcpyDeviceToHost));
+    double m = 0.0, d = 0.0, dh = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+        m = std::max(m, std::fabs(a[i]));
+        d = std::max(d, std::fabs(a[i] - b[i]));
+    }
+    for (int i = 0; i <= k; ++i) dh = std::max(dh, std::fabs(ca[i] - cb[i]) / std::max(1e-300, std::fabs(ca[i])));
+    diff_out[0] = m > 0 ? d / m : d;
+    diff_out[1] = dh;
+    diff_out[2] = (double)c->res_rl;
+    diff_out[3] = (double)c->res_blocks;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    for (auto p : V) (void)hipFree(p);
     return NK_OK;
 }
 

@@ -113,6 +113,12 @@ const int mgs_alt = [] {
     return (e && *e) ? atoi(e) : 0;
 }();
 
+// NK_MGS_RESIDENT=0: one k_mgs_pass launch per MGS pass instead of the resident sweep
+const int mgs_resident = [] {
+    const char* e = getenv("NK_MGS_RESIDENT");
+    return (e && *e) ? atoi(e) : 1;
+}();
+
 // Krylov.jl sym_givens (real case)
 void sym_givens(double a, double b, double* c, double* s, double* rho) {
     if (b == 0.0) {
@@ -312,16 +318,25 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         } else {
             NK_TRY(A.apply(q, qprev, 1.0, EPI_DOT, ws->V[0], &red, hprev, ws->V[k - 1]));
         }
-        for (int t = 0; t < np; ++t) {
-            const double* vi = ws->V[t % k];
-            const double* vnext = (t + 1 < np) ? ws->V[(t + 1) % k] : nullptr;
+        // the whole sweep in one launch with q resident on chip, else one launch per pass
+        int rc = 1;
+        if (mgs_resident) {
             NK_TRY(finish_reduction(c, &red));
-            Red nxt{};
-            NK_TRY(launch_mgs_pass(c, n, q, vi, vnext, red, col + t, colh + t, &nxt, mgs_alt ? (t & 1) : 0));
-            red = nxt;
+            rc = launch_mgs_sweep(c, n, q, ws->V.data(), k, np, red, col, colh, -1);
+            if (rc != NK_OK && rc != 1) return rc;
         }
-        NK_TRY(finish_reduction(c, &red));
-        NK_TRY(launch_finalize(c, red, col + np, 1, colh + np));  // h_{k+1,k} = ||q||
+        if (rc == 1) {
+            for (int t = 0; t < np; ++t) {
+                const double* vi = ws->V[t % k];
+                const double* vnext = (t + 1 < np) ? ws->V[(t + 1) % k] : nullptr;
+                NK_TRY(finish_reduction(c, &red));
+                Red nxt{};
+                NK_TRY(launch_mgs_pass(c, n, q, vi, vnext, red, col + t, colh + t, &nxt, mgs_alt ? (t & 1) : 0));
+                red = nxt;
+            }
+            NK_TRY(finish_reduction(c, &red));
+            NK_TRY(launch_finalize(c, red, col + np, 1, colh + np));  // h_{k+1,k} = ||q||
+        }
         NK_HIP(c, hipEventRecord(ws->col_ready[k & 1], c->stream));  // column complete in pinned memory
         return NK_OK;
     };
