@@ -953,9 +953,10 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     extern __shared__ dx2 lq[];  // rl x 256 double2
     __shared__ double sh[kShN];
     const int tid = threadIdx.x, G = gridDim.x;
-    const int64_t per = ((A.n2 + G - 1) / G + kResThreads - 1) / kResThreads * kResThreads;
-    const int64_t lo = (int64_t)blockIdx.x * per;
-    const int64_t hi = lo + per < A.n2 ? lo + per : A.n2;
+    // balanced partition of the ceil(n2 / 256) 256-wide slots: block b owns slots [b S / G, (b+1) S / G)
+    const int64_t ns = (A.n2 + kResThreads - 1) / kResThreads;
+    const int64_t lo = (int64_t)blockIdx.x * ns / G * kResThreads;
+    const int64_t hi = std::min<int64_t>((int64_t)(blockIdx.x + 1) * ns / G * kResThreads, A.n2);
     const dx2* qb = reinterpret_cast<const dx2*>(A.q) + lo + tid;
     ResState<RV> S;
 #pragma unroll
@@ -1031,15 +1032,16 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
     A.err = c->res_err_dev;
     A.n2 = n >> 1;
     A.np = np;
-    {  // every block's chunk must hold its rv + rl resident slots (the kernel does not predicate them)
+    {  // every block's chunk must hold its rv + rl resident slots in full (the kernel does not predicate them)
         const int64_t G = c->res_blocks, n2 = n >> 1;
-        const int64_t per = ((n2 + G - 1) / G + kResThreads - 1) / kResThreads * kResThreads;
-        const int64_t last = n2 - (G - 1) * per;  // the shortest chunk
-        if (last < kResThreads) return 1;
-        const int slots = (int)std::min<int64_t>(std::min(per, last) / kResThreads, 1 << 20);
+        const int64_t S = (n2 + kResThreads - 1) / kResThreads;
+        const int64_t full = S / G - (n2 % kResThreads != 0 ? 1 : 0);  // the last block's last slot may be partial
+        if (full < 1) return 1;
+        const int slots = (int)std::min<int64_t>(full, 1 << 20);
         static const int rl_env = env_int("NK_RES_RL", -1);
         static const int rv_env = env_int("NK_RES_RV", -1);
         int rl = std::min(slots, rl_env >= 0 ? std::min(rl_env, c->res_rl) : c->res_rl);  // LDS first
+        const bool explicit_rv = rv >= 0 || rv_env >= 0;  // a caller's choice skips the benefit test below
         if (rv < 0) rv = rv_env >= 0 ? rv_env : slots - rl;  // registers hold what the LDS cannot
         static const int kRv[] = {89, 64, 48, 32, 16, 0};  // the instantiated register-slot counts
         int pick = 0;
@@ -1050,6 +1052,12 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
             }
         rv = pick;
         A.rl = std::min(rl, slots - rv);
+        // worth it when q is re-read often enough: a one-pass sweep only adds q's load + store, and a
+        // mostly streamed q gains little over k_mgs_pass (heat 8192^2, 25 % resident: +11-13 % from
+        // k = 8 in tools/kbench_res.py, nothing over the 1-3 Arnoldi steps of a heat time step)
+        const int64_t chunk = std::max<int64_t>(1, S / G);
+        const double f = (double)(rv + A.rl) / (double)chunk;  // resident fraction of q
+        if (!explicit_rv && (np < 2 || (f < 0.5 && !(np >= 4 && f >= 0.2)))) return 1;
     }
     if (c->res_tag > 0xfffffff0u - (unsigned)kResMax) {  // tag wrap: restart from clean granules
         NK_HIP(c, hipMemsetAsync(c->res_gran, 0, sizeof(uint64_t) * 4 * kResThreads, c->stream));

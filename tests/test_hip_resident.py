@@ -1,0 +1,84 @@
+"""GPU tests of the resident MGS sweep (launch_mgs_sweep / k_mgs_res in nk_kernels.hip).
+
+From 512^2 up, every Arnoldi step's MGS sweep runs as ONE launch with q held in registers and LDS
+(one block per CU, partial sums handed between passes as tagged granules).  These solves cover
+its geometries against the CPU oracle -- LDS-only residency (1000^2, whose last 256-wide slot is
+partial), LDS + streamed remainder (2560^2), registers + LDS + a partial streamed remainder
+(2900 x 2901) -- with and without reorthogonalisation (2k passes per launch), run-to-run
+determinism, and the in-kernel peer-mailbox reduction (one rank, self-send) bit for bit against
+the local one.  The full residency of config 2 (4096^2) is covered by test_hip.py's
+test_bratu2d_4096_full_size and by bench.py's CPU/GPU agreement check.
+"""
+import numpy as np
+import pytest
+
+import _nkpath  # noqa: F401
+import ariadne_hip as ah
+from oracle import oracle as oc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = ah.Context(0)
+    ah.set_default_context(c)
+    yield c
+    c.sync()
+
+
+def solve(P, u, b, ctx=None, **kw):
+    g = ah.Grid.full(P.nx, P.ny)
+    ud = ah.DeviceArray.from_numpy(u, g, ctx)
+    bd = ah.DeviceArray.from_numpy(b, g, ctx)
+    res = ud.zero()
+    p = (P.hx, P.hy, P.lam)
+    ah.bratu2d_(res, ud, p)
+    memory = kw.pop("memory", 10)
+    ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=memory))
+    ah.krylov_solve_(ws, ah.JacobianOperator(ah.bratu2d_, res, ud, p, jv="exact"), bd, history=True, **kw)
+    return ws.x.to_numpy(), ws.stats
+
+
+@pytest.mark.parametrize("nx,ny,reorth", [(1000, 1000, False), (2560, 2560, False), (2900, 2901, False),
+                                          (2900, 2901, True)])
+def test_resident_sweep_matches_oracle(ctx, nx, ny, reorth):
+    P = oc.bratu2d(nx, ny)
+    u = oc.sin_ic(P)
+    b = oc.residual(P, u)
+    kw = dict(restart=True, reorthogonalization=reorth, atol=0.0, rtol=0.0, itmax=24)
+    x, st = solve(P, u, b, memory=10, **kw)
+    xo, sto, ho = oc.krylov_solve(P, u, b, jv="exact", memory=10, **kw)
+    assert st.niter == sto["niter"] == 24 and st.n_matvec == sto["n_matvec"]
+    # the same MGS arithmetic per element; only the order of the partial sums differs
+    assert np.allclose(np.array(st.residuals), ho, rtol=1e-9, atol=0)
+    assert np.max(np.abs(x - xo)) <= 1e-9 * np.max(np.abs(xo))
+
+
+def test_resident_sweep_deterministic(ctx):
+    P = oc.bratu2d(2900, 2901)
+    u = oc.sin_ic(P)
+    b = oc.residual(P, u)
+    runs = [solve(P, u, b, restart=True, atol=0.0, rtol=0.0, itmax=12) for _ in range(2)]
+    assert np.array_equal(runs[0][0], runs[1][0])
+    assert runs[0][1].residuals == runs[1][1].residuals
+
+
+def test_resident_sweep_mailbox_one_rank_is_bitwise(monkeypatch):
+    """The sweep's per-pass scalars through the peer mailbox (self-send) equal the local ones bit for bit."""
+    P = oc.bratu2d(1024)
+    u = oc.sin_ic(P)
+    b = oc.residual(P, u)
+    plain = ah.Context(0)
+    ah.set_default_context(plain)
+    x1, s1 = solve(P, u, b, ctx=plain, restart=True, atol=0.0, rtol=0.0, itmax=15)
+    monkeypatch.setenv("NK_DIST_FORCE", "1")
+    monkeypatch.setenv("NK_DIST_MAILBOX", "1")
+    forced = ah.Context(0)
+    forced.init_distributed(0, 1, ah.dist_unique_id())
+    assert forced.mailbox_active
+    ah.set_default_context(forced)
+    x2, s2 = solve(P, u, b, ctx=forced, restart=True, atol=0.0, rtol=0.0, itmax=15)
+    assert s1.niter == s2.niter == 15
+    assert s1.residuals == s2.residuals
+    assert np.array_equal(x1, x2)
