@@ -814,6 +814,8 @@ struct ResArgs {
     const double* red_in;  // partials of h of the first pass (the Jv's <V_1, q>)
     uint64_t* gran;        // 2 parities x G blocks x 2 granules
     int* err;              // pinned host flag: a poll timed out
+    int noxchg;            // kernel-variant bench only (NK_RES_NOXCHG=1): skip the exchange, h stays fixed
+    int poll1;             // one polling wave (NK_RES_POLL1, default 1) instead of every thread polling one partial
     int64_t n2;            // double2 elements
     int np, red_len, rl;
     unsigned tag0, mb0, spin;
@@ -835,6 +837,44 @@ __device__ __forceinline__ double res_exchange(const ResArgs& A, double part, in
                            __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(slot + 2 * blockIdx.x + 1, ((uint64_t)tag << 32) | (bits >> 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (A.poll1) {  // ONE wave polls: lane l sums the partials of blocks l, 64 + l, 128 + l, 192 + l
+        if (tid < 64) {
+            uint64_t w[8];
+            for (;;) {
+                bool ok = true;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int bl = 64 * j + tid;
+                    if (bl < G) {
+                        w[2 * j] = __hip_atomic_load(slot + 2 * bl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        w[2 * j + 1] = __hip_atomic_load(slot + 2 * bl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ok = ok && (unsigned)(w[2 * j] >> 32) == tag && (unsigned)(w[2 * j + 1] >> 32) == tag;
+                    } else {
+                        w[2 * j] = w[2 * j + 1] = 0;
+                    }
+                }
+                if (ok) break;
+                if (budget == 0 || --budget == 0) {
+                    __hip_atomic_store(A.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            double p = 0.0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                p += __longlong_as_double((long long)(((w[2 * j + 1] & 0xffffffffull) << 32) | (w[2 * j] & 0xffffffffull)));
+            p = wave_sum(p);
+            if (tid == 0) sh[kShB] = p;
+        }
+        __syncthreads();
+        const double s1 = sh[kShB];
+        if (A.mb0 == 0) return s1;
+        const unsigned epoch = A.mb0 + (unsigned)t;
+        if (blockIdx.x == 0) mb_send(s1, epoch);
+        __syncthreads();
+        return mb_recv(epoch, sh);
     }
     double v = 0.0;
     if (tid < G) {
@@ -867,7 +907,7 @@ __device__ __forceinline__ double res_exchange(const ResArgs& A, double part, in
 
 // one pass over this block's chunk: q -= h V_i, partial of <V_{i+1}, q> (NEXT) or <q, q>.  The
 // host guarantees every block's chunk covers its RV + rl resident slots (no predicates there).
-template <int RV>
+template <int RV, int B>
 __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx2* lq, int t, double mh, int64_t lo,
                                            int64_t hi) {
     const int tid = threadIdx.x;
@@ -882,7 +922,7 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
         acc = fma(p.x, a.x, acc);
         acc = fma(p.y, a.y, acc);
     };
-    constexpr int B = RV > 64 ? 4 : 8;  // slots per batch: 2 x B 16-B loads in flight per lane
+    // B slots per batch: 2 x B 16-B loads in flight per lane
 #pragma unroll
     for (int s0 = 0; s0 < RV; s0 += B) {
         dx2 bv[B], cv[B];
@@ -948,7 +988,7 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
     return acc;
 }
 
-template <int RV>
+template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8)>
 __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     extern __shared__ dx2 lq[];  // rl x 256 double2
     __shared__ double sh[kShN];
@@ -969,9 +1009,10 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
             A.col[t] = h;
             if (A.colh) A.colh[t] = h;
         }
-        const double acc = res_pass<RV>(A, S, lq, t, -h, lo, hi);
+        const double acc = res_pass<RV, B>(A, S, lq, t, -h, lo, hi);
         const double part = block_sum<kResThreads>(acc, sh);
-        h = res_exchange(A, part, t, sh, budget);
+        if (!A.noxchg) h = res_exchange(A, part, t, sh, budget);
+        else __syncthreads();
     }
     if (blockIdx.x == 0 && tid == 0) {
         const double r = sqrt(h);
@@ -984,9 +1025,9 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     for (int s = 0; s < A.rl; ++s) qw[(RV + s) * kResThreads] = lq[s * kResThreads + tid];
 }
 
-template <int RV>
+template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8)>
 int res_attr(nk_ctx* c, size_t lds) {
-    NK_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV>), hipFuncAttributeMaxDynamicSharedMemorySize,
+    NK_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV, B>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds));
     return NK_OK;
 }
@@ -1019,6 +1060,9 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         NK_TRY(res_attr<48>(c, lmax));
         NK_TRY(res_attr<64>(c, lmax));
         NK_TRY(res_attr<89>(c, lmax));
+        NK_TRY((res_attr<89, 4>(c, lmax)));
+        NK_TRY((res_attr<80, 8>(c, lmax)));
+        NK_TRY((res_attr<72, 8>(c, lmax)));
     }
     ResArgs A{};
     for (int t = 0; t < np; ++t) A.V[t] = V[t % k];
@@ -1032,6 +1076,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
     A.err = c->res_err_dev;
     A.n2 = n >> 1;
     A.np = np;
+    int xv = -1;  // experimental variant (kernel-variant bench)
     {  // every block's chunk must hold its rv + rl resident slots in full (the kernel does not predicate them)
         const int64_t G = c->res_blocks, n2 = n >> 1;
         const int64_t S = (n2 + kResThreads - 1) / kResThreads;
@@ -1042,6 +1087,10 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         static const int rv_env = env_int("NK_RES_RV", -1);
         int rl = std::min(slots, rl_env >= 0 ? std::min(rl_env, c->res_rl) : c->res_rl);  // LDS first
         const bool explicit_rv = rv >= 0 || rv_env >= 0;  // a caller's choice skips the benefit test below
+        if (rv >= 1000) {  // kernel-variant bench: 1000 + {0: 89/B4, 1: 80/B8, 2: 72/B8}
+            xv = rv - 1000;
+            rv = xv == 0 ? 89 : xv == 1 ? 80 : 72;
+        }
         if (rv < 0) rv = rv_env >= 0 ? rv_env : slots - rl;  // registers hold what the LDS cannot
         static const int kRv[] = {89, 64, 48, 32, 16, 0};  // the instantiated register-slot counts
         int pick = 0;
@@ -1050,7 +1099,8 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
                 pick = r;
                 break;
             }
-        rv = pick;
+        if (xv < 0) rv = pick;
+        else if (rv > slots) return 1;
         A.rl = std::min(rl, slots - rv);
         // worth it when q is re-read often enough: a one-pass sweep only adds q's load + store, and a
         // mostly streamed q gains little over k_mgs_pass (heat 8192^2, 25 % resident: +11-13 % from
@@ -1071,6 +1121,10 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         A.mb0 = c->mb_epoch + 1;
         c->mb_epoch += (unsigned)np;
     }
+    static const int noxchg = env_int("NK_RES_NOXCHG", 0);
+    A.noxchg = noxchg;
+    static const int poll1 = env_int("NK_RES_POLL1", 1);
+    A.poll1 = poll1;
     A.spin = 1u << 22;  // polls per thread per launch (~1 s): a grid that is not co-resident fails fast
     const size_t lds = (size_t)A.rl * kResThreads * sizeof(dx2);
     const double bytes = 16.0 * n + (16.0 * np - 8.0) * n;  // q in + out, V_i (+ V_{i+1}) per pass
@@ -1081,7 +1135,12 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         case 16: hipLaunchKernelGGL(k_mgs_res<16>, g, b, lds, c->stream, A); break;
         case 48: hipLaunchKernelGGL(k_mgs_res<48>, g, b, lds, c->stream, A); break;
         case 64: hipLaunchKernelGGL(k_mgs_res<64>, g, b, lds, c->stream, A); break;
-        case 89: hipLaunchKernelGGL(k_mgs_res<89>, g, b, lds, c->stream, A); break;
+        case 89:
+            if (xv == 0) hipLaunchKernelGGL((k_mgs_res<89, 4>), g, b, lds, c->stream, A);
+            else hipLaunchKernelGGL(k_mgs_res<89>, g, b, lds, c->stream, A);
+            break;
+        case 80: hipLaunchKernelGGL((k_mgs_res<80, 8>), g, b, lds, c->stream, A); break;
+        case 72: hipLaunchKernelGGL((k_mgs_res<72, 8>), g, b, lds, c->stream, A); break;
         default: hipLaunchKernelGGL(k_mgs_res<32>, g, b, lds, c->stream, A); break;
         }
     });
