@@ -39,7 +39,7 @@ struct ProfPending {
 };
 struct ProfAcc {
     int64_t launches = 0, timed = 0;
-    double ms = 0.0, bytes = 0.0;
+    double ms = 0.0, bytes = 0.0, bytes_all = 0.0;
 };
 
 struct Comm;  // RCCL state (nk_dist.cpp)
@@ -129,6 +129,7 @@ int launch(nk_ctx* c, const char* name, double bytes, F&& f) {
     bool timed = false;
     if (c->prof) {
         k = kid(c, name);
+        c->acc[k].bytes_all += bytes;
         timed = (c->acc[k].launches++ % c->prof_every) == 0;
         if (timed) NK_TRY(prof_begin(c, &a));
     }

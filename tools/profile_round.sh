@@ -6,7 +6,7 @@
 #   1. rocprofv3 --kernel-trace --stats of the default bench         -> kernel_stats_bench.csv
 #   2. two separate PMC passes (FETCH_SIZE, WRITE_SIZE) per workload  -> pmc_traffic_<workload>.json
 #   3. the bench lines themselves (every workload tag, each with its CPU baseline)
-#   4. in-process kernel-variant A/B (tools/kbench.py)
+#   4. in-process kernel-variant A/B (tools/kbench.py, tools/kbench_res.py)
 set -e -o pipefail
 R=${1:-r01}
 ROOT=$(pwd)
@@ -20,6 +20,11 @@ echo "[profile] kernel trace"
     -- python3 "$ROOT/bench.py" --no-cpu-baseline > "$OUT/bench_traced.log" 2>&1)
 cp "$OUT/trace/run_kernel_stats.csv" "$DST/kernel_stats_bench.csv"
 grep '^{"metric"' "$OUT/bench_traced.log" | tail -n 1 > "$DST/bench_under_rocprof.json"
+
+echo "[profile] roctx ranges"
+(cd /tmp && timeout -k 10 300 rocprofv3 --marker-trace --stats -d "$OUT/marker" -o run --output-format csv \
+    -- python3 "$ROOT/bench.py" --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/bench_marker.log" 2>&1)
+cp "$OUT/marker/run_marker_api_stats.csv" "$DST/marker_stats_bench.csv"
 
 # workload tag -> bench.py arguments
 declare -A WARGS=(
@@ -52,4 +57,5 @@ cp "$DST/bench_bratu2d.json" "$DST/bench.json"
 echo "[profile] kernel variants"
 timeout -k 10 300 python3 tools/kbench.py --rounds 3 --what mgs > "$DST/kbench_mgs.log" 2>&1
 timeout -k 10 300 python3 tools/kbench.py --rounds 3 --what stencil > "$DST/kbench_stencil.log" 2>&1
+timeout -k 10 300 python3 tools/kbench_res.py --ks 8,16,30 --rvs 0,32,48,64,89 > "$DST/kbench_res.log" 2>&1
 echo "[profile] done"
