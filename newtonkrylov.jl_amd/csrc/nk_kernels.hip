@@ -907,9 +907,29 @@ __device__ __forceinline__ double res_exchange(const ResArgs& A, double part, in
 
 // one pass over this block's chunk: q -= h V_i, partial of <V_{i+1}, q> (NEXT) or <q, q>.  The
 // host guarantees every block's chunk covers its RV + rl resident slots (no predicates there).
-template <int RV, int B>
+// the first register batch of a pass, loaded before the previous pass's hand-off completes (its
+// addresses do not depend on h): the load latency hides behind the hand-off
+template <int B>
+struct ResPre {
+    dx2 b[B], c[B];
+};
+template <int RV, int B, bool PRE>
+__device__ __forceinline__ void res_prefetch(const ResArgs& A, ResPre<B>& P, int t, int64_t lo) {
+    if constexpr (PRE && RV >= B) {
+        const int tid = threadIdx.x;
+        const dx2* vb = reinterpret_cast<const dx2*>(A.V[t]) + lo + tid;
+        const dx2* wb = reinterpret_cast<const dx2*>(A.V[t + 1 < A.np ? t + 1 : t]) + lo + tid;
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            P.b[u] = __builtin_nontemporal_load(vb + u * kResThreads);
+            P.c[u] = wb[u * kResThreads];
+        }
+    }
+}
+
+template <int RV, int B, bool PRE>
 __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx2* lq, int t, double mh, int64_t lo,
-                                           int64_t hi) {
+                                           int64_t hi, ResPre<B>& P) {
     const int tid = threadIdx.x;
     const bool next = t + 1 < A.np;  // last pass: <q, q> instead of <V_{i+1}, q>
     const dx2* vb = reinterpret_cast<const dx2*>(A.V[t]) + lo + tid;
@@ -926,11 +946,19 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
 #pragma unroll
     for (int s0 = 0; s0 < RV; s0 += B) {
         dx2 bv[B], cv[B];
+        if (PRE && RV >= B && s0 == 0) {
 #pragma unroll
-        for (int u = 0; u < B; ++u) {
-            if (s0 + u < RV) {
-                bv[u] = __builtin_nontemporal_load(vb + (s0 + u) * kResThreads);
-                cv[u] = wb[(s0 + u) * kResThreads];
+            for (int u = 0; u < B; ++u) {
+                bv[u] = P.b[u];
+                cv[u] = P.c[u];
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < B; ++u) {
+                if (s0 + u < RV) {
+                    bv[u] = __builtin_nontemporal_load(vb + (s0 + u) * kResThreads);
+                    cv[u] = wb[(s0 + u) * kResThreads];
+                }
             }
         }
 #pragma unroll
@@ -988,7 +1016,7 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
     return acc;
 }
 
-template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8)>
+template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false>
 __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     extern __shared__ dx2 lq[];  // rl x 256 double2
     __shared__ double sh[kShN];
@@ -1002,6 +1030,8 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
 #pragma unroll
     for (int s = 0; s < RV; ++s) S.r[s] = qb[s * kResThreads];
     for (int s = 0; s < A.rl; ++s) lq[s * kResThreads + tid] = qb[(RV + s) * kResThreads];
+    ResPre<B> P;
+    res_prefetch<RV, B, PRE>(A, P, 0, lo);
     double h = reduce_input(A.red_in, A.red_len, sh);
     unsigned budget = A.spin;
     for (int t = 0; t < A.np; ++t) {
@@ -1009,7 +1039,8 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
             A.col[t] = h;
             if (A.colh) A.colh[t] = h;
         }
-        const double acc = res_pass<RV, B>(A, S, lq, t, -h, lo, hi);
+        const double acc = res_pass<RV, B, PRE>(A, S, lq, t, -h, lo, hi, P);
+        if (t + 1 < A.np) res_prefetch<RV, B, PRE>(A, P, t + 1, lo);
         const double part = block_sum<kResThreads>(acc, sh);
         if (!A.noxchg) h = res_exchange(A, part, t, sh, budget);
         else __syncthreads();
@@ -1025,9 +1056,9 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     for (int s = 0; s < A.rl; ++s) qw[(RV + s) * kResThreads] = lq[s * kResThreads + tid];
 }
 
-template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8)>
+template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false>
 int res_attr(nk_ctx* c, size_t lds) {
-    NK_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV, B>), hipFuncAttributeMaxDynamicSharedMemorySize,
+    NK_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV, B, PRE>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds));
     return NK_OK;
 }
@@ -1060,9 +1091,8 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         NK_TRY(res_attr<48>(c, lmax));
         NK_TRY(res_attr<64>(c, lmax));
         NK_TRY(res_attr<89>(c, lmax));
+        NK_TRY((res_attr<89, 4, true>(c, lmax)));
         NK_TRY((res_attr<89, 4>(c, lmax)));
-        NK_TRY((res_attr<80, 8>(c, lmax)));
-        NK_TRY((res_attr<72, 8>(c, lmax)));
     }
     ResArgs A{};
     for (int t = 0; t < np; ++t) A.V[t] = V[t % k];
@@ -1087,9 +1117,9 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         static const int rv_env = env_int("NK_RES_RV", -1);
         int rl = std::min(slots, rl_env >= 0 ? std::min(rl_env, c->res_rl) : c->res_rl);  // LDS first
         const bool explicit_rv = rv >= 0 || rv_env >= 0;  // a caller's choice skips the benefit test below
-        if (rv >= 1000) {  // kernel-variant bench: 1000 + {0: 89/B4, 1: 80/B8, 2: 72/B8}
+        if (rv >= 1000) {  // kernel-variant bench: 1000 + {0: 89 slots, batches of 4 + prefetch across the hand-off; 1: same, no prefetch}
             xv = rv - 1000;
-            rv = xv == 0 ? 89 : xv == 1 ? 80 : 72;
+            rv = 89;
         }
         if (rv < 0) rv = rv_env >= 0 ? rv_env : slots - rl;  // registers hold what the LDS cannot
         static const int kRv[] = {89, 64, 48, 32, 16, 0};  // the instantiated register-slot counts
@@ -1136,11 +1166,10 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         case 48: hipLaunchKernelGGL(k_mgs_res<48>, g, b, lds, c->stream, A); break;
         case 64: hipLaunchKernelGGL(k_mgs_res<64>, g, b, lds, c->stream, A); break;
         case 89:
-            if (xv == 0) hipLaunchKernelGGL((k_mgs_res<89, 4>), g, b, lds, c->stream, A);
+            if (xv == 0) hipLaunchKernelGGL((k_mgs_res<89, 4, true>), g, b, lds, c->stream, A);
+            else if (xv == 1) hipLaunchKernelGGL((k_mgs_res<89, 4>), g, b, lds, c->stream, A);
             else hipLaunchKernelGGL(k_mgs_res<89>, g, b, lds, c->stream, A);
             break;
-        case 80: hipLaunchKernelGGL((k_mgs_res<80, 8>), g, b, lds, c->stream, A); break;
-        case 72: hipLaunchKernelGGL((k_mgs_res<72, 8>), g, b, lds, c->stream, A); break;
         default: hipLaunchKernelGGL(k_mgs_res<32>, g, b, lds, c->stream, A); break;
         }
     });
