@@ -157,8 +157,10 @@ int mb_check(nk_ctx* c);                     // after a host sync: did a mailbox
 int red_blocks(int64_t n);                   // grid size of streaming reductions
 // One Arnoldi step's MGS sweep in one launch (np passes over V[t % k], then ||q||) with q resident
 // on chip; returns 1 (nothing enqueued) when the resident path does not apply.
+// *vout (optional): where to store V_{k+1} = q / ||q|| instead of q; reset to null when the sweep
+// stores q (not every slot resident).
 int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, int k, int np, Red in, double* col,
-                     double* colh, int rv);
+                     double* colh, int rv, double** vout);
 constexpr int kMbSlots = 256;                // mailbox ring (epoch % kMbSlots)
 constexpr int kMbRanks = 32;                 // max ranks of the mailbox all-reduce (2 granules each: one wave polls them all)
 constexpr int kHaloBlocks = 64;              // blocks (= flags per side) of the IPC ghost-plane exchange

@@ -809,6 +809,7 @@ constexpr int kResThreads = 256;
 struct ResArgs {
     const double* V[kResMax + 1];  // pass t: V_i = V[t], V_{i+1} = V[t + 1]
     double* q;
+    double* vout;  // non-null (full residency only): store V_{k+1} = q / ||q|| here instead of q
     double* col;   // h of every pass, ||q|| at [np]
     double* colh;  // pinned host mirror
     const double* red_in;  // partials of h of the first pass (the Jv's <V_1, q>)
@@ -1050,6 +1051,17 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
         A.col[A.np] = r;
         if (A.colh) A.colh[A.np] = r;
     }
+    if (A.vout) {  // the next Arnoldi step's kdivcopy!(V_{k+1}, q, h) done here: q never leaves the chip
+        const double hn = sqrt(h);  // == col[np], the h the next Jv would divide by
+        dx2* vw = reinterpret_cast<dx2*>(A.vout) + lo + tid;
+#pragma unroll
+        for (int s = 0; s < RV; ++s) vw[s * kResThreads] = dx2{S.r[s].x / hn, S.r[s].y / hn};
+        for (int s = 0; s < A.rl; ++s) {
+            const dx2 a = lq[s * kResThreads + tid];
+            vw[(RV + s) * kResThreads] = dx2{a.x / hn, a.y / hn};
+        }
+        return;
+    }
     dx2* qw = reinterpret_cast<dx2*>(A.q) + lo + tid;
 #pragma unroll
     for (int s = 0; s < RV; ++s) qw[s * kResThreads] = S.r[s];
@@ -1067,7 +1079,7 @@ int res_attr(nk_ctx* c, size_t lds) {
 // Resident sweep: returns NK_OK after enqueueing, or 1 when the resident path does not apply
 // (caller falls back to one k_mgs_pass launch per pass).
 int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, int k, int np, Red in, double* col,
-                     double* colh, int rv) {
+                     double* colh, int rv, double** vout) {
     if (np < 1 || np > kResMax || (n & 1) || !c->res_ok) return 1;
     if (c->comm && !c->mb_on) return 1;  // RCCL reductions need the host between passes
     if (!c->res_gran) {
@@ -1109,10 +1121,10 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
     int xv = -1;  // experimental variant (kernel-variant bench)
     {  // every block's chunk must hold its rv + rl resident slots in full (the kernel does not predicate them)
         const int64_t G = c->res_blocks, n2 = n >> 1;
-        const int64_t S = (n2 + kResThreads - 1) / kResThreads;
-        const int64_t full = S / G - (n2 % kResThreads != 0 ? 1 : 0);  // the last block's last slot may be partial
-        if (full < 1) return 1;
-        const int slots = (int)std::min<int64_t>(full, 1 << 20);
+        const int64_t ns = (n2 + kResThreads - 1) / kResThreads;
+        const int64_t whole = ns / G - (n2 % kResThreads != 0 ? 1 : 0);  // the last block's last slot may be partial
+        if (whole < 1) return 1;
+        const int slots = (int)std::min<int64_t>(whole, 1 << 20);
         static const int rl_env = env_int("NK_RES_RL", -1);
         static const int rv_env = env_int("NK_RES_RV", -1);
         int rl = std::min(slots, rl_env >= 0 ? std::min(rl_env, c->res_rl) : c->res_rl);  // LDS first
@@ -1135,9 +1147,15 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         // worth it when q is re-read often enough: a one-pass sweep only adds q's load + store, and a
         // mostly streamed q gains little over k_mgs_pass (heat 8192^2, 25 % resident: +11-13 % from
         // k = 8 in tools/kbench_res.py, nothing over the 1-3 Arnoldi steps of a heat time step)
-        const int64_t chunk = std::max<int64_t>(1, S / G);
+        const int64_t chunk = std::max<int64_t>(1, ns / G);
         const double f = (double)(rv + A.rl) / (double)chunk;  // resident fraction of q
         if (!explicit_rv && (np < 2 || (f < 0.5 && !(np >= 4 && f >= 0.2)))) return 1;
+        // V_{k+1} straight from the registers only when all of q is resident (no streamed slot; a
+        // partial last slot is streamed)
+        const bool full = n2 % kResThreads == 0 && (ns + G - 1) / G <= rv + A.rl;
+        static const int vout_env = env_int("NK_RES_VOUT", 1);
+        if (vout && *vout && !(full && vout_env)) *vout = nullptr;
+        A.vout = vout ? *vout : nullptr;
     }
     if (c->res_tag > 0xfffffff0u - (unsigned)kResMax) {  // tag wrap: restart from clean granules
         NK_HIP(c, hipMemsetAsync(c->res_gran, 0, sizeof(uint64_t) * 4 * kResThreads, c->stream));
@@ -1157,7 +1175,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
     A.poll1 = poll1;
     A.spin = 1u << 22;  // polls per thread per launch (~1 s): a grid that is not co-resident fails fast
     const size_t lds = (size_t)A.rl * kResThreads * sizeof(dx2);
-    const double bytes = 16.0 * n + (16.0 * np - 8.0) * n;  // q in + out, V_i (+ V_{i+1}) per pass
+    const double bytes = 16.0 * n + (16.0 * np - 8.0) * n;  // q in, q (or V_{k+1}) out, V_i (+ V_{i+1}) per pass
     return launch(c, "mgs_sweep", bytes, [&] {
         const dim3 g(c->res_blocks), b(kResThreads);
         switch (rv) {
@@ -1551,7 +1569,7 @@ extern "C" int nkb_mgs_res(nk_ctx* c, int64_t n, int k, int rv, int reps, double
         NK_TRY(launch_copy(c, n, qb, q0));
         NK_TRY(launch_dot(c, n, V[0], qb, &red));
         NK_HIP(c, hipEventRecord(e0, c->stream));
-        const int rc = launch_mgs_sweep(c, n, qb, V.data(), k, k, red, col2, nullptr, rv);
+        const int rc = launch_mgs_sweep(c, n, qb, V.data(), k, k, red, col2, nullptr, rv, nullptr);
         if (rc != NK_OK) return rc == 1 ? fail(c, NK_E_ARG, "resident sweep not applicable") : rc;
         NK_HIP(c, hipEventRecord(e1, c->stream));
         NK_HIP(c, hipEventSynchronize(e1));

@@ -296,6 +296,8 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
     const nk_precond* N = (o->N && o->N->kind != NK_PRECOND_NONE) ? o->N : nullptr;
     const bool flex = N && ws->algo == NK_ALGO_FGMRES;
     const bool spec = N == nullptr;
+    // vready[k]: step k's resident sweep stored V_{k+1} itself, so step k+1's Jv reads it as is
+    std::vector<char> vready(mem + 2, 0);
     auto issue = [&](int k) -> int {
         NK_TRY(ws_basis(ws, k));
         NK_TRY(ws_scalars(ws, k + 1));
@@ -315,15 +317,25 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
             NK_TRY(A.apply(q, zk, znorm, EPI_DOT, ws->V[0], &red));
         } else if (k == 1) {  // fused kdivcopy!(V_1, r0, beta) + mul! + <V_1, Jv> (the dot partner is V_1 itself)
             NK_TRY(A.apply(q, v1_src, 1.0, EPI_DOT, nullptr, &red, ws->bdev, ws->V[0]));
+        } else if (vready[k - 1]) {  // V_k is in place: mul! + <V_1, Jv> only
+            NK_TRY(A.apply(q, ws->V[k - 1], 1.0, EPI_DOT, ws->V[0], &red));
         } else {
             NK_TRY(A.apply(q, qprev, 1.0, EPI_DOT, ws->V[0], &red, hprev, ws->V[k - 1]));
         }
+        if ((int)vready.size() < k + 2) vready.resize(k + 2, 0);
+        vready[k] = 0;
         // the whole sweep in one launch with q resident on chip, else one launch per pass
         int rc = 1;
         if (mgs_resident) {
             NK_TRY(finish_reduction(c, &red));
-            rc = launch_mgs_sweep(c, n, q, ws->V.data(), k, np, red, col, colh, -1);
+            double* vnext = nullptr;
+            if (spec) {  // the speculative path's next Jv can take V_{k+1} from the sweep
+                NK_TRY(ws_basis(ws, k + 1));
+                vnext = ws->V[k];
+            }
+            rc = launch_mgs_sweep(c, n, q, ws->V.data(), k, np, red, col, colh, -1, &vnext);
             if (rc != NK_OK && rc != 1) return rc;
+            if (rc == NK_OK && vnext) vready[k] = 1;
         }
         if (rc == 1) {
             for (int t = 0; t < np; ++t) {
