@@ -84,6 +84,7 @@ struct nk_ctx {
     int* res_err_dev = nullptr;
     unsigned res_tag = 0;                  // granule tags handed out so far
     int res_blocks = 0, res_rl = 0;        // grid (= CUs) and LDS double2 slots per thread
+    uint64_t* res_tstamp = nullptr;        // kernel-variant bench only (nkb_mgs_res, NK_RES_TSTAMP)
     // distribution
     int rank = 0, nranks = 1;
     nk::Comm* comm = nullptr;

@@ -817,6 +817,7 @@ struct ResArgs {
     int* err;              // pinned host flag: a poll timed out
     int noxchg;            // kernel-variant bench only (NK_RES_NOXCHG=1): skip the exchange, h stays fixed
     int poll1;             // one polling wave (NK_RES_POLL1, default 1) instead of every thread polling one partial
+    uint64_t* tstamp;      // kernel-variant bench only: per pass and block, wall clock at pass end and after the hand-off
     int64_t n2;            // double2 elements
     int np, red_len, rl;
     unsigned tag0, mb0, spin;
@@ -1043,8 +1044,10 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
         const double acc = res_pass<RV, B, PRE>(A, S, lq, t, -h, lo, hi, P);
         if (t + 1 < A.np) res_prefetch<RV, B, PRE>(A, P, t + 1, lo);
         const double part = block_sum<kResThreads>(acc, sh);
+        if (A.tstamp && tid == 0) A.tstamp[((size_t)t * G + blockIdx.x) * 2] = wall_clock64();
         if (!A.noxchg) h = res_exchange(A, part, t, sh, budget);
         else __syncthreads();
+        if (A.tstamp && tid == 0) A.tstamp[((size_t)t * G + blockIdx.x) * 2 + 1] = wall_clock64();
     }
     if (blockIdx.x == 0 && tid == 0) {
         const double r = sqrt(h);
@@ -1173,6 +1176,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
     A.noxchg = noxchg;
     static const int poll1 = env_int("NK_RES_POLL1", 1);
     A.poll1 = poll1;
+    A.tstamp = c->res_tstamp;
     A.spin = 1u << 22;  // polls per thread per launch (~1 s): a grid that is not co-resident fails fast
     const size_t lds = (size_t)A.rl * kResThreads * sizeof(dx2);
     const double bytes = 16.0 * n + (16.0 * np - 8.0) * n;  // q in, q (or V_{k+1}) out, V_i (+ V_{i+1}) per pass
@@ -1536,6 +1540,9 @@ __global__ __launch_bounds__(kBlock) void k_hashfill(int64_t n, double* __restri
 extern "C" int nkb_mgs_res(nk_ctx* c, int64_t n, int k, int rv, int reps, double* us_out, double* us_ref, double* diff_out) {
     using namespace nk;
     if (!c || n < 2 || k < 1 || k > kResMax || reps < 1 || !us_out || !us_ref || !diff_out) return NK_E_ARG;
+    // NK_RES_TSTAMP=<file>: also dump the per-pass, per-block wall clocks of the last timed sweep
+    const char* tsf = getenv("NK_RES_TSTAMP");
+    if (tsf && *tsf && !c->res_tstamp) NK_HIP(c, hipMalloc(&c->res_tstamp, sizeof(uint64_t) * 2 * kResMax * 1024));
     std::vector<double*> V(k + 3, nullptr);
     for (size_t v = 0; v < V.size(); ++v) {
         NK_HIP(c, hipMalloc(&V[v], sizeof(double) * n));
@@ -1593,6 +1600,16 @@ extern "C" int nkb_mgs_res(nk_ctx* c, int64_t n, int k, int rv, int reps, double
     diff_out[0] = m > 0 ? d / m : d;
     diff_out[1] = dh;
     diff_out[2] = (double)c->res_rl;
+    if (c->res_tstamp && tsf && *tsf) {
+        std::vector<uint64_t> ts((size_t)2 * k * c->res_blocks);
+        NK_HIP(c, hipMemcpy(ts.data(), c->res_tstamp, sizeof(uint64_t) * ts.size(), hipMemcpyDeviceToHost));
+        if (FILE* f = std::fopen(tsf, "wb")) {
+            std::fwrite(ts.data(), sizeof(uint64_t), ts.size(), f);
+            std::fclose(f);
+        }
+        (void)hipFree(c->res_tstamp);
+        c->res_tstamp = nullptr;
+    }
     diff_out[3] = (double)c->res_blocks;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
