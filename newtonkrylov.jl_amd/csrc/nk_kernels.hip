@@ -1106,6 +1106,13 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         NK_TRY(res_attr<48>(c, lmax));
         NK_TRY(res_attr<64>(c, lmax));
         NK_TRY(res_attr<89>(c, lmax));
+        int per_cu = 0;  // residency: at least one block of the largest variant per CU
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_mgs_res<89>),
+                                                         kResThreads, lmax) != hipSuccess || per_cu < 1) {
+            (void)hipGetLastError();
+            c->res_ok = false;
+            return 1;
+        }
         NK_TRY((res_attr<89, 4, true>(c, lmax)));
         NK_TRY((res_attr<89, 4>(c, lmax)));
     }
