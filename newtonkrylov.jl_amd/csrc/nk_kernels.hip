@@ -817,6 +817,7 @@ struct ResArgs {
     int* err;              // pinned host flag: a poll timed out
     int noxchg;            // kernel-variant bench only (NK_RES_NOXCHG=1): skip the exchange, h stays fixed
     int poll1;             // one polling wave (NK_RES_POLL1, default 1) instead of every thread polling one partial
+    int strided;           // slots interleaved across blocks (every block exactly full: no streamed remainder)
     uint64_t* tstamp;      // kernel-variant bench only: per pass and block, wall clock at pass end and after the hand-off
     int64_t n2;            // double2 elements
     int np, red_len, rl;
@@ -916,26 +917,26 @@ struct ResPre {
     dx2 b[B], c[B];
 };
 template <int RV, int B, bool PRE>
-__device__ __forceinline__ void res_prefetch(const ResArgs& A, ResPre<B>& P, int t, int64_t lo) {
+__device__ __forceinline__ void res_prefetch(const ResArgs& A, ResPre<B>& P, int t, int64_t base, int64_t ss) {
     if constexpr (PRE && RV >= B) {
         const int tid = threadIdx.x;
-        const dx2* vb = reinterpret_cast<const dx2*>(A.V[t]) + lo + tid;
-        const dx2* wb = reinterpret_cast<const dx2*>(A.V[t + 1 < A.np ? t + 1 : t]) + lo + tid;
+        const dx2* vb = reinterpret_cast<const dx2*>(A.V[t]) + base + tid;
+        const dx2* wb = reinterpret_cast<const dx2*>(A.V[t + 1 < A.np ? t + 1 : t]) + base + tid;
 #pragma unroll
         for (int u = 0; u < B; ++u) {
-            P.b[u] = __builtin_nontemporal_load(vb + u * kResThreads);
-            P.c[u] = wb[u * kResThreads];
+            P.b[u] = __builtin_nontemporal_load(vb + u * ss);
+            P.c[u] = wb[u * ss];
         }
     }
 }
 
 template <int RV, int B, bool PRE>
 __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx2* lq, int t, double mh, int64_t lo,
-                                           int64_t hi, ResPre<B>& P) {
+                                           int64_t hi, ResPre<B>& P, int64_t base, int64_t ss) {
     const int tid = threadIdx.x;
     const bool next = t + 1 < A.np;  // last pass: <q, q> instead of <V_{i+1}, q>
-    const dx2* vb = reinterpret_cast<const dx2*>(A.V[t]) + lo + tid;
-    const dx2* wb = reinterpret_cast<const dx2*>(A.V[next ? t + 1 : t]) + lo + tid;
+    const dx2* vb = reinterpret_cast<const dx2*>(A.V[t]) + base + tid;
+    const dx2* wb = reinterpret_cast<const dx2*>(A.V[next ? t + 1 : t]) + base + tid;
     double acc = 0.0;
     auto upd = [&](dx2& a, const dx2 b, const dx2 c) {
         a.x = fma(mh, b.x, a.x);
@@ -958,8 +959,8 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
 #pragma unroll
             for (int u = 0; u < B; ++u) {
                 if (s0 + u < RV) {
-                    bv[u] = __builtin_nontemporal_load(vb + (s0 + u) * kResThreads);
-                    cv[u] = wb[(s0 + u) * kResThreads];
+                    bv[u] = __builtin_nontemporal_load(vb + (s0 + u) * ss);
+                    cv[u] = wb[(s0 + u) * ss];
                 }
             }
         }
@@ -968,16 +969,16 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
             if (s0 + u < RV) upd(S.r[s0 + u], bv[u], cv[u]);
         __builtin_amdgcn_sched_barrier(0);  // no hoisting across batches: registers hold q, not loads
     }
-    const dx2* vl = vb + RV * kResThreads;
-    const dx2* wl = wb + RV * kResThreads;
+    const dx2* vl = vb + RV * ss;
+    const dx2* wl = wb + RV * ss;
     const int rl = A.rl;
     int s = 0;
     for (; s + 4 <= rl; s += 4) {
         dx2 bv[4], cv[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            bv[u] = __builtin_nontemporal_load(vl + (s + u) * kResThreads);
-            cv[u] = wl[(s + u) * kResThreads];
+            bv[u] = __builtin_nontemporal_load(vl + (s + u) * ss);
+            cv[u] = wl[(s + u) * ss];
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -987,8 +988,8 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
         }
     }
     for (; s < rl; ++s) {
-        const dx2 b = __builtin_nontemporal_load(vl + s * kResThreads);
-        const dx2 cc = wl[s * kResThreads];
+        const dx2 b = __builtin_nontemporal_load(vl + s * ss);
+        const dx2 cc = wl[s * ss];
         dx2 a = lq[s * kResThreads + tid];
         upd(a, b, cc);
         lq[s * kResThreads + tid] = a;
@@ -1027,13 +1028,18 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     const int64_t ns = (A.n2 + kResThreads - 1) / kResThreads;
     const int64_t lo = (int64_t)blockIdx.x * ns / G * kResThreads;
     const int64_t hi = std::min<int64_t>((int64_t)(blockIdx.x + 1) * ns / G * kResThreads, A.n2);
-    const dx2* qb = reinterpret_cast<const dx2*>(A.q) + lo + tid;
+    // slot s of this block: contiguous chunk (base = lo, stride 256) or, with A.strided (every block
+    // exactly full), interleaved across the blocks (base = 256 b, stride 256 G) so that every block
+    // touches every address region alike
+    const int64_t base = A.strided ? (int64_t)blockIdx.x * kResThreads : lo;
+    const int64_t ss = A.strided ? (int64_t)G * kResThreads : kResThreads;
+    const dx2* qb = reinterpret_cast<const dx2*>(A.q) + base + tid;
     ResState<RV> S;
 #pragma unroll
-    for (int s = 0; s < RV; ++s) S.r[s] = qb[s * kResThreads];
-    for (int s = 0; s < A.rl; ++s) lq[s * kResThreads + tid] = qb[(RV + s) * kResThreads];
+    for (int s = 0; s < RV; ++s) S.r[s] = qb[s * ss];
+    for (int s = 0; s < A.rl; ++s) lq[s * kResThreads + tid] = qb[(RV + s) * ss];
     ResPre<B> P;
-    res_prefetch<RV, B, PRE>(A, P, 0, lo);
+    res_prefetch<RV, B, PRE>(A, P, 0, base, ss);
     double h = reduce_input(A.red_in, A.red_len, sh);
     unsigned budget = A.spin;
     for (int t = 0; t < A.np; ++t) {
@@ -1041,8 +1047,8 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
             A.col[t] = h;
             if (A.colh) A.colh[t] = h;
         }
-        const double acc = res_pass<RV, B, PRE>(A, S, lq, t, -h, lo, hi, P);
-        if (t + 1 < A.np) res_prefetch<RV, B, PRE>(A, P, t + 1, lo);
+        const double acc = res_pass<RV, B, PRE>(A, S, lq, t, -h, lo, hi, P, base, ss);
+        if (t + 1 < A.np) res_prefetch<RV, B, PRE>(A, P, t + 1, base, ss);
         const double part = block_sum<kResThreads>(acc, sh);
         if (A.tstamp && tid == 0) A.tstamp[((size_t)t * G + blockIdx.x) * 2] = wall_clock64();
         if (!A.noxchg) h = res_exchange(A, part, t, sh, budget);
@@ -1056,19 +1062,19 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     }
     if (A.vout) {  // the next Arnoldi step's kdivcopy!(V_{k+1}, q, h) done here: q never leaves the chip
         const double hn = sqrt(h);  // == col[np], the h the next Jv would divide by
-        dx2* vw = reinterpret_cast<dx2*>(A.vout) + lo + tid;
+        dx2* vw = reinterpret_cast<dx2*>(A.vout) + base + tid;
 #pragma unroll
-        for (int s = 0; s < RV; ++s) vw[s * kResThreads] = dx2{S.r[s].x / hn, S.r[s].y / hn};
+        for (int s = 0; s < RV; ++s) vw[s * ss] = dx2{S.r[s].x / hn, S.r[s].y / hn};
         for (int s = 0; s < A.rl; ++s) {
             const dx2 a = lq[s * kResThreads + tid];
-            vw[(RV + s) * kResThreads] = dx2{a.x / hn, a.y / hn};
+            vw[(RV + s) * ss] = dx2{a.x / hn, a.y / hn};
         }
         return;
     }
-    dx2* qw = reinterpret_cast<dx2*>(A.q) + lo + tid;
+    dx2* qw = reinterpret_cast<dx2*>(A.q) + base + tid;
 #pragma unroll
-    for (int s = 0; s < RV; ++s) qw[s * kResThreads] = S.r[s];
-    for (int s = 0; s < A.rl; ++s) qw[(RV + s) * kResThreads] = lq[s * kResThreads + tid];
+    for (int s = 0; s < RV; ++s) qw[s * ss] = S.r[s];
+    for (int s = 0; s < A.rl; ++s) qw[(RV + s) * ss] = lq[s * kResThreads + tid];
 }
 
 template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false>
@@ -1166,6 +1172,8 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         static const int vout_env = env_int("NK_RES_VOUT", 1);
         if (vout && *vout && !(full && vout_env)) *vout = nullptr;
         A.vout = vout ? *vout : nullptr;
+        static const int strided_env = env_int("NK_RES_STRIDED", 0);
+        A.strided = strided_env && n2 % kResThreads == 0 && ns % G == 0 && ns / G == rv + A.rl;
     }
     if (c->res_tag > 0xfffffff0u - (unsigned)kResMax) {  // tag wrap: restart from clean granules
         NK_HIP(c, hipMemsetAsync(c->res_gran, 0, sizeof(uint64_t) * 4 * kResThreads, c->stream));
