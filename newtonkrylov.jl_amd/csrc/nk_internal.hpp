@@ -160,8 +160,15 @@ int red_blocks(int64_t n);                   // grid size of streaming reduction
 // on chip; returns 1 (nothing enqueued) when the resident path does not apply.
 // *vout (optional): where to store V_{k+1} = q / ||q|| instead of q; reset to null when the sweep
 // stores q (not every slot resident).
+// *jin (optional, 2D Bratu FD Jv at full residency only): compute q = J V_k in the launch itself
+// (q never touches memory; `in` is unused) -- returns 1 without enqueueing when it does not apply.
+struct ResJv {
+    const double *u, *v, *F0, *aux;  // u, V_k, F(u), V_1
+    double eps, lam, hx2, hy2;
+    int64_t nx;
+};
 int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, int k, int np, Red in, double* col,
-                     double* colh, int rv, double** vout);
+                     double* colh, int rv, double** vout, const ResJv* jin = nullptr);
 constexpr int kMbSlots = 256;                // mailbox ring (epoch % kMbSlots)
 constexpr int kMbRanks = 32;                 // max ranks of the mailbox all-reduce (2 granules each: one wave polls them all)
 constexpr int kHaloBlocks = 64;              // blocks (= flags per side) of the IPC ghost-plane exchange

@@ -819,6 +819,12 @@ struct ResArgs {
     int poll1;             // one polling wave (NK_RES_POLL1, default 1) instead of every thread polling one partial
     int strided;           // slots interleaved across blocks (every block exactly full: no streamed remainder)
     uint64_t* tstamp;      // kernel-variant bench only: per pass and block, wall clock at pass end and after the hand-off
+    // fused FD Jv (2D Bratu): q = (F(u + eps V_k) - F0) / eps computed into the registers, with the
+    // partials of <V_1, q> -- instead of loading the q a separate Jv kernel wrote
+    const double *ju, *jv, *jf0, *jaux;
+    double jeps, jlam, jhx2, jhy2;
+    int64_t jnx;
+    int jv_on;
     int64_t n2;            // double2 elements
     int np, red_len, rl;
     unsigned tag0, mb0, spin;
@@ -830,6 +836,7 @@ struct ResState {
 };
 
 // `budget`: this thread's remaining polls for the whole launch (a stuck grid drains in bounded time)
+// t: the exchange's index in this launch (tags, parity and mailbox epochs follow it)
 __device__ __forceinline__ double res_exchange(const ResArgs& A, double part, int t, double* sh, unsigned& budget) {
     const int tid = threadIdx.x, G = gridDim.x;
     const unsigned tag = A.tag0 + (unsigned)t;
@@ -910,6 +917,35 @@ __device__ __forceinline__ double res_exchange(const ResArgs& A, double part, in
 
 // one pass over this block's chunk: q -= h V_i, partial of <V_{i+1}, q> (NEXT) or <q, q>.  The
 // host guarantees every block's chunk covers its RV + rl resident slots (no predicates there).
+// The FD Jv of 2D Bratu at the two points (2e, 2e + 1) of one row, exactly as k_st2d<NK_BRATU2D,
+// MODE_JFD> evaluates it (w = u + eps v; ((p - 2c) + m) / h^2 in x, then y; + lam exp(c);
+// (r - F0) / eps), + the two terms of <V_1, Jv>.  Rows j +- 1 come from memory (ghost planes at the
+// slab ends: zero or the neighbour's rows, as in the stencil kernel); x-neighbours outside the row
+// are the zero Dirichlet boundary.
+__device__ __forceinline__ dx2 res_jv_pair(const ResArgs& A, int64_t e, double& acc) {
+    const int64_t p = 2 * e, nx = A.jnx;
+    const int64_t i = p % nx;
+    const dx2 vc = *reinterpret_cast<const dx2*>(A.jv + p), uc = __builtin_nontemporal_load(reinterpret_cast<const dx2*>(A.ju + p));
+    const dx2 vu = *reinterpret_cast<const dx2*>(A.jv + p + nx), uu = *reinterpret_cast<const dx2*>(A.ju + p + nx);
+    const dx2 vd = *reinterpret_cast<const dx2*>(A.jv + p - nx), ud = *reinterpret_cast<const dx2*>(A.ju + p - nx);
+    const double vl = A.jv[p - 1], ul = A.ju[p - 1], vr = A.jv[p + 2], ur = A.ju[p + 2];
+    const dx2 f0 = __builtin_nontemporal_load(reinterpret_cast<const dx2*>(A.jf0 + p));
+    const dx2 ax = *reinterpret_cast<const dx2*>(A.jaux + p);
+    const double eps = A.jeps;
+    const double c0 = uc.x + eps * vc.x, c1 = uc.y + eps * vc.y;
+    const double wl = i > 0 ? ul + eps * vl : 0.0;
+    const double wr = i + 2 < nx ? ur + eps * vr : 0.0;
+    const double u0 = uu.x + eps * vu.x, u1 = uu.y + eps * vu.y;
+    const double d0 = ud.x + eps * vd.x, d1 = ud.y + eps * vd.y;
+    const double l0 = ((c1 - 2.0 * c0) + wl) / A.jhx2 + ((u0 - 2.0 * c0) + d0) / A.jhy2;
+    const double l1 = ((wr - 2.0 * c1) + c0) / A.jhx2 + ((u1 - 2.0 * c1) + d1) / A.jhy2;
+    const double r0 = l0 + A.jlam * exp(c0), r1 = l1 + A.jlam * exp(c1);
+    const dx2 val{(r0 - f0.x) / eps, (r1 - f0.y) / eps};
+    acc = fma(ax.x, val.x, acc);
+    acc = fma(ax.y, val.y, acc);
+    return val;
+}
+
 // the first register batch of a pass, loaded before the previous pass's hand-off completes (its
 // addresses do not depend on h): the load latency hides behind the hand-off
 template <int B>
@@ -1019,7 +1055,7 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
     return acc;
 }
 
-template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false>
+template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false>
 __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     extern __shared__ dx2 lq[];  // rl x 256 double2
     __shared__ double sh[kShN];
@@ -1033,15 +1069,37 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     // touches every address region alike
     const int64_t base = A.strided ? (int64_t)blockIdx.x * kResThreads : lo;
     const int64_t ss = A.strided ? (int64_t)G * kResThreads : kResThreads;
-    const dx2* qb = reinterpret_cast<const dx2*>(A.q) + base + tid;
     ResState<RV> S;
-#pragma unroll
-    for (int s = 0; s < RV; ++s) S.r[s] = qb[s * ss];
-    for (int s = 0; s < A.rl; ++s) lq[s * kResThreads + tid] = qb[(RV + s) * ss];
     ResPre<B> P;
-    res_prefetch<RV, B, PRE>(A, P, 0, base, ss);
-    double h = reduce_input(A.red_in, A.red_len, sh);
+    double h;
     unsigned budget = A.spin;
+    constexpr int xo = JV ? 1 : 0;  // exchange 0 carries <V_1, J V_k> when the Jv is fused
+    if constexpr (JV) {
+        double jacc = 0.0;
+        // register slots in rounds of kJvStage, each computed by a compact (not unrolled) loop into
+        // the LDS and then moved into its registers; the LDS slots last
+        constexpr int kJvStage = 16;  // the host guarantees rl >= kJvStage when RV > 0
+#pragma unroll
+        for (int s0 = 0; s0 < RV; s0 += kJvStage) {
+            const int m = RV - s0 < kJvStage ? RV - s0 : kJvStage;
+#pragma unroll 4
+            for (int u = 0; u < m; ++u) lq[u * kResThreads + tid] = res_jv_pair(A, base + (s0 + u) * ss + tid, jacc);
+#pragma unroll
+            for (int u = 0; u < kJvStage; ++u)
+                if (s0 + u < RV) S.r[s0 + u] = lq[u * kResThreads + tid];
+        }
+#pragma unroll 4
+        for (int s = 0; s < A.rl; ++s) lq[s * kResThreads + tid] = res_jv_pair(A, base + (RV + s) * ss + tid, jacc);
+        res_prefetch<RV, B, PRE>(A, P, 0, base, ss);
+        h = res_exchange(A, block_sum<kResThreads>(jacc, sh), 0, sh, budget);
+    } else {
+        const dx2* qb = reinterpret_cast<const dx2*>(A.q) + base + tid;
+#pragma unroll
+        for (int s = 0; s < RV; ++s) S.r[s] = qb[s * ss];
+        for (int s = 0; s < A.rl; ++s) lq[s * kResThreads + tid] = qb[(RV + s) * ss];
+        res_prefetch<RV, B, PRE>(A, P, 0, base, ss);
+        h = reduce_input(A.red_in, A.red_len, sh);
+    }
     for (int t = 0; t < A.np; ++t) {
         if (blockIdx.x == 0 && tid == 0) {
             A.col[t] = h;
@@ -1051,7 +1109,7 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
         if (t + 1 < A.np) res_prefetch<RV, B, PRE>(A, P, t + 1, base, ss);
         const double part = block_sum<kResThreads>(acc, sh);
         if (A.tstamp && tid == 0) A.tstamp[((size_t)t * G + blockIdx.x) * 2] = wall_clock64();
-        if (!A.noxchg) h = res_exchange(A, part, t, sh, budget);
+        if (!A.noxchg) h = res_exchange(A, part, t + xo, sh, budget);
         else __syncthreads();
         if (A.tstamp && tid == 0) A.tstamp[((size_t)t * G + blockIdx.x) * 2 + 1] = wall_clock64();
     }
@@ -1077,9 +1135,9 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     for (int s = 0; s < A.rl; ++s) qw[(RV + s) * ss] = lq[s * kResThreads + tid];
 }
 
-template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false>
+template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false>
 int res_attr(nk_ctx* c, size_t lds) {
-    NK_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV, B, PRE>), hipFuncAttributeMaxDynamicSharedMemorySize,
+    NK_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV, B, PRE, JV>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds));
     return NK_OK;
 }
@@ -1088,8 +1146,13 @@ int res_attr(nk_ctx* c, size_t lds) {
 // Resident sweep: returns NK_OK after enqueueing, or 1 when the resident path does not apply
 // (caller falls back to one k_mgs_pass launch per pass).
 int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, int k, int np, Red in, double* col,
-                     double* colh, int rv, double** vout) {
+                     double* colh, int rv, double** vout, const ResJv* jin) {
     if (np < 1 || np > kResMax || (n & 1) || !c->res_ok) return 1;
+    // fused Jv phase: off by default -- at one wave per SIMD its ~190 fp64 VALU instructions per point
+    // pair (IEEE divisions, two exp) do not hide behind the loads: 791 us per Arnoldi step vs
+    // 619 + 124 us for the sweep and a separate Jv kernel (-1.7 % end to end, 4096^2)
+    static const int jv_env = env_int("NK_RES_JV", 0);
+    if (jin && (!jv_env || !vout || !*vout || jin->nx % 2 != 0)) return 1;
     if (c->comm && !c->mb_on) return 1;  // RCCL reductions need the host between passes
     if (!c->res_gran) {
         int dev = 0, cus = 0, lds = 0;
@@ -1121,6 +1184,8 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         }
         NK_TRY((res_attr<89, 4, true>(c, lmax)));
         NK_TRY((res_attr<89, 4>(c, lmax)));
+        NK_TRY((res_attr<89, 6, false, true>(c, lmax)));
+        NK_TRY((res_attr<0, 8, false, true>(c, lmax)));
     }
     ResArgs A{};
     for (int t = 0; t < np; ++t) A.V[t] = V[t % k];
@@ -1172,20 +1237,34 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         static const int vout_env = env_int("NK_RES_VOUT", 1);
         if (vout && *vout && !(full && vout_env)) *vout = nullptr;
         A.vout = vout ? *vout : nullptr;
+        if (jin && (!A.vout || (rv != 0 && rv != 89) || (rv > 0 && A.rl < 16))) return 1;  // fused Jv: full residency, instantiated rv, LDS staging
         static const int strided_env = env_int("NK_RES_STRIDED", 0);
         A.strided = strided_env && n2 % kResThreads == 0 && ns % G == 0 && ns / G == rv + A.rl;
     }
-    if (c->res_tag > 0xfffffff0u - (unsigned)kResMax) {  // tag wrap: restart from clean granules
+    if (jin) {
+        A.jv_on = 1;
+        A.ju = jin->u;
+        A.jv = jin->v;
+        A.jf0 = jin->F0;
+        A.jaux = jin->aux;
+        A.jeps = jin->eps;
+        A.jlam = jin->lam;
+        A.jhx2 = jin->hx2;
+        A.jhy2 = jin->hy2;
+        A.jnx = jin->nx;
+    }
+    const unsigned nx_ = (unsigned)np + (jin ? 1u : 0u);  // hand-offs in this launch
+    if (c->res_tag > 0xfffffff0u - (unsigned)(kResMax + 1)) {  // tag wrap: restart from clean granules
         NK_HIP(c, hipMemsetAsync(c->res_gran, 0, sizeof(uint64_t) * 4 * kResThreads, c->stream));
         c->res_tag = 0;
     }
     A.tag0 = c->res_tag + 1;
-    c->res_tag += (unsigned)np;
+    c->res_tag += nx_;
     A.mb0 = 0;
-    if (c->mb_on) {  // np consecutive mailbox epochs, no 16-bit wrap inside the range
-        if (c->mb_epoch + (unsigned)np > 0xffffu) c->mb_epoch = 0;
+    if (c->mb_on) {  // consecutive mailbox epochs, no 16-bit wrap inside the range
+        if (c->mb_epoch + nx_ > 0xffffu) c->mb_epoch = 0;
         A.mb0 = c->mb_epoch + 1;
-        c->mb_epoch += (unsigned)np;
+        c->mb_epoch += nx_;
     }
     static const int noxchg = env_int("NK_RES_NOXCHG", 0);
     A.noxchg = noxchg;
@@ -1194,16 +1273,21 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
     A.tstamp = c->res_tstamp;
     A.spin = 1u << 22;  // polls per thread per launch (~1 s): a grid that is not co-resident fails fast
     const size_t lds = (size_t)A.rl * kResThreads * sizeof(dx2);
-    const double bytes = 16.0 * n + (16.0 * np - 8.0) * n;  // q in, q (or V_{k+1}) out, V_i (+ V_{i+1}) per pass
-    return launch(c, "mgs_sweep", bytes, [&] {
+    // q in (or the fused Jv's u, V_k, F0, V_1), q (or V_{k+1}) out, V_i (+ V_{i+1}) per pass
+    const double bytes = (jin ? 32.0 : 8.0) * n + 8.0 * n + (16.0 * np - 8.0) * n;
+    return launch(c, jin ? "arnoldi_step" : "mgs_sweep", bytes, [&] {
         const dim3 g(c->res_blocks), b(kResThreads);
         switch (rv) {
-        case 0: hipLaunchKernelGGL(k_mgs_res<0>, g, b, lds, c->stream, A); break;
+        case 0:
+            if (jin) hipLaunchKernelGGL((k_mgs_res<0, 8, false, true>), g, b, lds, c->stream, A);
+            else hipLaunchKernelGGL(k_mgs_res<0>, g, b, lds, c->stream, A);
+            break;
         case 16: hipLaunchKernelGGL(k_mgs_res<16>, g, b, lds, c->stream, A); break;
         case 48: hipLaunchKernelGGL(k_mgs_res<48>, g, b, lds, c->stream, A); break;
         case 64: hipLaunchKernelGGL(k_mgs_res<64>, g, b, lds, c->stream, A); break;
         case 89:
-            if (xv == 0) hipLaunchKernelGGL((k_mgs_res<89, 4, true>), g, b, lds, c->stream, A);
+            if (jin) hipLaunchKernelGGL((k_mgs_res<89, 6, false, true>), g, b, lds, c->stream, A);
+            else if (xv == 0) hipLaunchKernelGGL((k_mgs_res<89, 4, true>), g, b, lds, c->stream, A);
             else if (xv == 1) hipLaunchKernelGGL((k_mgs_res<89, 4>), g, b, lds, c->stream, A);
             else hipLaunchKernelGGL(k_mgs_res<89>, g, b, lds, c->stream, A);
             break;
@@ -1591,7 +1675,7 @@ extern "C" int nkb_mgs_res(nk_ctx* c, int64_t n, int k, int rv, int reps, double
         NK_TRY(launch_copy(c, n, qb, q0));
         NK_TRY(launch_dot(c, n, V[0], qb, &red));
         NK_HIP(c, hipEventRecord(e0, c->stream));
-        const int rc = launch_mgs_sweep(c, n, qb, V.data(), k, k, red, col2, nullptr, rv, nullptr);
+        const int rc = launch_mgs_sweep(c, n, qb, V.data(), k, k, red, col2, nullptr, rv, nullptr, nullptr);
         if (rc != NK_OK) return rc == 1 ? fail(c, NK_E_ARG, "resident sweep not applicable") : rc;
         NK_HIP(c, hipEventRecord(e1, c->stream));
         NK_HIP(c, hipEventSynchronize(e1));

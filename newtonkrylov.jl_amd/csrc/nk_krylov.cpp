@@ -183,13 +183,14 @@ struct Op {
                 }
                 return NK_OK;
             }
-            eps = std::sqrt(DBL_EPSILON) * std::fmax(1.0, unorm) / vnorm;
+            eps = fd_eps(vnorm);
         }
         NK_TRY(halo_exchange(c, p, v));
         StencilIn in{p, mode == NK_JV_FD ? MODE_JFD : MODE_JEXACT, epi, out, u, v, F0, aux, eps, vdiv, vout};
         return launch_stencil(c, in, red);
     }
     int64_t ws_n() const { return p->nx * p->ny * p->nz; }
+    double fd_eps(double vnorm) const { return std::sqrt(DBL_EPSILON) * std::fmax(1.0, unorm) / vnorm; }
 };
 
 // z = N v (right preconditioner); *znorm = ||z|| when the FD operator needs it.
@@ -308,6 +309,23 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         Red red{};
         const double* hprev = k > 1 ? slot_dev(k - 1) + npasses_of(k - 1) : ws->bdev;
         const double* qprev = k > 1 ? W[(k - 1) & 1] : v1_src;
+        if ((int)vready.size() < k + 2) vready.resize(k + 2, 0);
+        // 2D Bratu, FD Jv, V_k stored by the previous resident sweep: Jv + MGS sweep in ONE launch
+        // (q = J V_k is computed into the registers that hold it through the sweep)
+        if (spec && k >= 2 && vready[k - 1] && mgs_resident && A.mode == NK_JV_FD && p->kind == NK_BRATU2D) {
+            NK_TRY(ws_basis(ws, k + 1));
+            double* vnext = ws->V[k];
+            const ResJv jin{A.u, ws->V[k - 1], A.F0, ws->V[0], A.fd_eps(1.0), p->lambda, p->hx * p->hx, p->hy * p->hy, p->nx};
+            NK_TRY(halo_exchange(c, p, ws->V[k - 1]));
+            const int rc = launch_mgs_sweep(c, n, q, ws->V.data(), k, np, Red{}, col, colh, -1, &vnext, &jin);
+            if (rc != NK_OK && rc != 1) return rc;
+            if (rc == NK_OK) {
+                ++A.n_matvec;
+                vready[k] = vnext != nullptr;
+                NK_HIP(c, hipEventRecord(ws->col_ready[k & 1], c->stream));
+                return NK_OK;
+            }
+        }
         if (N) {  // V_k = q_{k-1} / h (r0 / beta), Z_k = N V_k, q = J Z_k, <V_1, q>
             NK_TRY(launch_fd_point(c, n, nullptr, nullptr, qprev, hprev, 0.0, ws->V[k - 1]));
             NK_TRY(ws_zbasis(ws, flex ? k : 1));  // gmres!: one p = N V_k buffer; fgmres!: Z_k kept
@@ -322,7 +340,6 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         } else {
             NK_TRY(A.apply(q, qprev, 1.0, EPI_DOT, ws->V[0], &red, hprev, ws->V[k - 1]));
         }
-        if ((int)vready.size() < k + 2) vready.resize(k + 2, 0);
         vready[k] = 0;
         // the whole sweep in one launch with q resident on chip, else one launch per pass
         int rc = 1;
