@@ -6,7 +6,8 @@ its geometries against the CPU oracle -- LDS-only residency (1000^2, whose last 
 partial), LDS + streamed remainder (2560^2), registers + LDS + a partial streamed remainder
 (2900 x 2901) -- with and without reorthogonalisation (2k passes per launch), run-to-run
 determinism, and the in-kernel peer-mailbox reduction (one rank, self-send) bit for bit against
-the local one.  The full residency of config 2 (4096^2) is covered by test_hip.py's
+the local one; and the optional fused FD Jv phase (NK_RES_JV=1, a child process).  The full
+residency of config 2 (4096^2) is covered by test_hip.py's
 test_bratu2d_4096_full_size and by bench.py's CPU/GPU agreement check.
 """
 import numpy as np
@@ -82,3 +83,47 @@ def test_resident_sweep_mailbox_one_rank_is_bitwise(monkeypatch):
     assert s1.niter == s2.niter == 15
     assert s1.residuals == s2.residuals
     assert np.array_equal(x1, x2)
+
+
+_JV_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import _nkpath  # noqa: F401
+import ariadne_hip as ah
+from oracle import oracle as oc
+P = oc.bratu2d(1024)
+u = oc.sin_ic(P)
+b = oc.residual(P, u)
+g = ah.Grid.full(P.nx, P.ny)
+ud, bd = ah.DeviceArray.from_numpy(u, g), ah.DeviceArray.from_numpy(b, g)
+res = ud.zero()
+p = (P.hx, P.hy, P.lam)
+ah.bratu2d_(res, ud, p)
+ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=10))
+ah.krylov_solve_(ws, ah.JacobianOperator(ah.bratu2d_, res, ud, p, jv="fd"), bd, restart=True, atol=0.0, rtol=0.0,
+                 itmax=20, history=True)
+np.savez(sys.argv[2], x=ws.x.to_numpy(), h=np.array(ws.stats.residuals), F0=res.to_numpy(), nm=ws.stats.n_matvec)
+"""
+
+
+def test_fused_jv_sweep_matches_oracle(tmp_path):
+    """NK_RES_JV=1 (off by default): the FD Jv computed inside the resident launch, against the oracle."""
+    import os
+    import subprocess
+    import sys
+
+    out = tmp_path / "jv.npz"
+    env = dict(os.environ, NK_RES_JV="1")
+    tests = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, "-c", _JV_CHILD, tests, str(out)], env=env, capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = np.load(out)
+    P = oc.bratu2d(1024)
+    u = oc.sin_ic(P)
+    b = oc.residual(P, u)
+    kw = dict(restart=True, atol=0.0, rtol=0.0, itmax=20)
+    xo, sto, ho = oc.krylov_solve(P, u, b, jv="fd", F0=d["F0"], memory=10, **kw)
+    assert int(d["nm"]) == sto["n_matvec"]
+    assert np.allclose(d["h"], ho, rtol=1e-8)
+    assert np.max(np.abs(d["x"] - xo)) <= 1e-8 * np.max(np.abs(xo))
