@@ -966,9 +966,13 @@ __device__ __forceinline__ void res_prefetch(const ResArgs& A, ResPre<B>& P, int
     }
 }
 
+// rev (alternate passes, ALT variant): the LDS slots first and in descending order, then the
+// register slots -- so the pass starts on the V_i lines the previous pass loaded last as its V_{i+1}
+// (the LDS slots, ~5 MB per XCD: still in its L2).  The register slots keep one (ascending) order:
+// a second, reversed copy of their unrolled loop costs scratch.
 template <int RV, int B, bool PRE>
 __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx2* lq, int t, double mh, int64_t lo,
-                                           int64_t hi, ResPre<B>& P, int64_t base, int64_t ss) {
+                                           int64_t hi, ResPre<B>& P, int64_t base, int64_t ss, bool rev = false) {
     const int tid = threadIdx.x;
     const bool next = t + 1 < A.np;  // last pass: <q, q> instead of <V_{i+1}, q>
     const dx2* vb = reinterpret_cast<const dx2*>(A.V[t]) + base + tid;
@@ -982,80 +986,100 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
         acc = fma(p.y, a.y, acc);
     };
     // B slots per batch: 2 x B 16-B loads in flight per lane
+    auto regs = [&] {
+        constexpr int NB = (RV + B - 1) / B;
 #pragma unroll
-    for (int s0 = 0; s0 < RV; s0 += B) {
-        dx2 bv[B], cv[B];
-        if (PRE && RV >= B && s0 == 0) {
+        for (int bi = 0; bi < NB; ++bi) {
+            const int s0 = bi * B;
+            dx2 bv[B], cv[B];
+            if (PRE && RV >= B && s0 == 0) {
 #pragma unroll
-            for (int u = 0; u < B; ++u) {
-                bv[u] = P.b[u];
-                cv[u] = P.c[u];
-            }
-        } else {
+                for (int u = 0; u < B; ++u) {
+                    bv[u] = P.b[u];
+                    cv[u] = P.c[u];
+                }
+            } else {
 #pragma unroll
-            for (int u = 0; u < B; ++u) {
-                if (s0 + u < RV) {
-                    bv[u] = __builtin_nontemporal_load(vb + (s0 + u) * ss);
-                    cv[u] = wb[(s0 + u) * ss];
+                for (int u = 0; u < B; ++u) {
+                    if (s0 + u < RV) {
+                        bv[u] = __builtin_nontemporal_load(vb + (s0 + u) * ss);
+                        cv[u] = wb[(s0 + u) * ss];
+                    }
                 }
             }
-        }
 #pragma unroll
-        for (int u = 0; u < B; ++u)
-            if (s0 + u < RV) upd(S.r[s0 + u], bv[u], cv[u]);
-        __builtin_amdgcn_sched_barrier(0);  // no hoisting across batches: registers hold q, not loads
-    }
+            for (int u = 0; u < B; ++u)
+                if (s0 + u < RV) upd(S.r[s0 + u], bv[u], cv[u]);
+            __builtin_amdgcn_sched_barrier(0);  // no hoisting across batches: registers hold q, not loads
+        }
+    };
     const dx2* vl = vb + RV * ss;
     const dx2* wl = wb + RV * ss;
     const int rl = A.rl;
-    int s = 0;
-    for (; s + 4 <= rl; s += 4) {
-        dx2 bv[4], cv[4];
+    auto lds = [&] {
+        auto one4 = [&](int s, bool down) {  // LDS slots s .. s+3 (down: s+3 .. s)
+            dx2 bv[4], cv[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            bv[u] = __builtin_nontemporal_load(vl + (s + u) * ss);
-            cv[u] = wl[(s + u) * ss];
-        }
+            for (int u = 0; u < 4; ++u) {
+                bv[u] = __builtin_nontemporal_load(vl + (s + u) * ss);
+                cv[u] = wl[(s + u) * ss];
+            }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            dx2 a = lq[(s + u) * kResThreads + tid];
-            upd(a, bv[u], cv[u]);
-            lq[(s + u) * kResThreads + tid] = a;
+            for (int u0 = 0; u0 < 4; ++u0) {
+                const int u = down ? 3 - u0 : u0;
+                dx2 a = lq[(s + u) * kResThreads + tid];
+                upd(a, bv[u], cv[u]);
+                lq[(s + u) * kResThreads + tid] = a;
+            }
+        };
+        auto one = [&](int s) {
+            const dx2 b = __builtin_nontemporal_load(vl + s * ss);
+            const dx2 cc = wl[s * ss];
+            dx2 a = lq[s * kResThreads + tid];
+            upd(a, b, cc);
+            lq[s * kResThreads + tid] = a;
+        };
+        const int r4 = rl / 4 * 4;
+        if (!rev) {
+            for (int s = 0; s < r4; s += 4) one4(s, false);
+            for (int s = r4; s < rl; ++s) one(s);
+        } else {
+            for (int s = rl - 1; s >= r4; --s) one(s);
+            for (int s = r4 - 4; s >= 0; s -= 4) one4(s, true);
         }
-    }
-    for (; s < rl; ++s) {
-        const dx2 b = __builtin_nontemporal_load(vl + s * ss);
-        const dx2 cc = wl[s * ss];
-        dx2 a = lq[s * kResThreads + tid];
-        upd(a, b, cc);
-        lq[s * kResThreads + tid] = a;
-    }
-    // the streamed remainder: q through memory, as k_mgs_pass
-    dx2* q2 = reinterpret_cast<dx2*>(A.q);
-    const dx2* v2 = reinterpret_cast<const dx2*>(A.V[t]);
-    const dx2* w2 = reinterpret_cast<const dx2*>(A.V[next ? t + 1 : t]);
-    int64_t e = lo + (int64_t)(RV + rl) * kResThreads + tid;
-    for (; e + kResThreads < hi; e += 2 * kResThreads) {
-        const int64_t e1 = e + kResThreads;
-        dx2 a0 = q2[e], a1 = q2[e1];
-        const dx2 b0 = __builtin_nontemporal_load(v2 + e), b1 = __builtin_nontemporal_load(v2 + e1);
-        const dx2 c0 = w2[e], c1 = w2[e1];
-        upd(a0, b0, c0);
-        upd(a1, b1, c1);
-        q2[e] = a0;
-        q2[e1] = a1;
-    }
-    if (e < hi) {
-        dx2 a0 = q2[e];
-        const dx2 b0 = __builtin_nontemporal_load(v2 + e);
-        const dx2 c0 = w2[e];
-        upd(a0, b0, c0);
-        q2[e] = a0;
-    }
+    };
+    auto stream = [&] {
+        // the streamed remainder: q through memory, as k_mgs_pass
+        dx2* q2 = reinterpret_cast<dx2*>(A.q);
+        const dx2* v2 = reinterpret_cast<const dx2*>(A.V[t]);
+        const dx2* w2 = reinterpret_cast<const dx2*>(A.V[next ? t + 1 : t]);
+        int64_t e = lo + (int64_t)(RV + rl) * kResThreads + tid;
+        for (; e + kResThreads < hi; e += 2 * kResThreads) {
+            const int64_t e1 = e + kResThreads;
+            dx2 a0 = q2[e], a1 = q2[e1];
+            const dx2 b0 = __builtin_nontemporal_load(v2 + e), b1 = __builtin_nontemporal_load(v2 + e1);
+            const dx2 c0 = w2[e], c1 = w2[e1];
+            upd(a0, b0, c0);
+            upd(a1, b1, c1);
+            q2[e] = a0;
+            q2[e1] = a1;
+        }
+        if (e < hi) {
+            dx2 a0 = q2[e];
+            const dx2 b0 = __builtin_nontemporal_load(v2 + e);
+            const dx2 c0 = w2[e];
+            upd(a0, b0, c0);
+            q2[e] = a0;
+        }
+    };
+    if (rev) lds();
+    regs();
+    if (!rev) lds();
+    stream();
     return acc;
 }
 
-template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false>
+template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false, bool ALT = false>
 __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     extern __shared__ dx2 lq[];  // rl x 256 double2
     __shared__ double sh[kShN];
@@ -1105,7 +1129,7 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
             A.col[t] = h;
             if (A.colh) A.colh[t] = h;
         }
-        const double acc = res_pass<RV, B, PRE>(A, S, lq, t, -h, lo, hi, P, base, ss);
+        const double acc = res_pass<RV, B, PRE>(A, S, lq, t, -h, lo, hi, P, base, ss, ALT && (t & 1));
         if (t + 1 < A.np) res_prefetch<RV, B, PRE>(A, P, t + 1, base, ss);
         const double part = block_sum<kResThreads>(acc, sh);
         if (A.tstamp && tid == 0) A.tstamp[((size_t)t * G + blockIdx.x) * 2] = wall_clock64();
@@ -1135,9 +1159,9 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     for (int s = 0; s < A.rl; ++s) qw[(RV + s) * ss] = lq[s * kResThreads + tid];
 }
 
-template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false>
+template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false, bool ALT = false>
 int res_attr(nk_ctx* c, size_t lds) {
-    NK_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV, B, PRE, JV>), hipFuncAttributeMaxDynamicSharedMemorySize,
+    NK_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV, B, PRE, JV, ALT>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds));
     return NK_OK;
 }
@@ -1186,6 +1210,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         NK_TRY((res_attr<89, 4>(c, lmax)));
         NK_TRY((res_attr<89, 6, false, true>(c, lmax)));
         NK_TRY((res_attr<0, 8, false, true>(c, lmax)));
+        NK_TRY((res_attr<89, 6, false, false, true>(c, lmax)));
     }
     ResArgs A{};
     for (int t = 0; t < np; ++t) A.V[t] = V[t % k];
@@ -1210,7 +1235,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         static const int rv_env = env_int("NK_RES_RV", -1);
         int rl = std::min(slots, rl_env >= 0 ? std::min(rl_env, c->res_rl) : c->res_rl);  // LDS first
         const bool explicit_rv = rv >= 0 || rv_env >= 0;  // a caller's choice skips the benefit test below
-        if (rv >= 1000) {  // kernel-variant bench: 1000 + {0: 89 slots, batches of 4 + prefetch across the hand-off; 1: same, no prefetch}
+        if (rv >= 1000) {  // kernel-variant bench: 1000 + {0: 89 slots, batches of 4 + prefetch across the hand-off; 1: same, no prefetch; 2: alternating slot order}
             xv = rv - 1000;
             rv = 89;
         }
@@ -1289,6 +1314,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
             if (jin) hipLaunchKernelGGL((k_mgs_res<89, 6, false, true>), g, b, lds, c->stream, A);
             else if (xv == 0) hipLaunchKernelGGL((k_mgs_res<89, 4, true>), g, b, lds, c->stream, A);
             else if (xv == 1) hipLaunchKernelGGL((k_mgs_res<89, 4>), g, b, lds, c->stream, A);
+            else if (xv == 2) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, true>), g, b, lds, c->stream, A);
             else hipLaunchKernelGGL(k_mgs_res<89>, g, b, lds, c->stream, A);
             break;
         default: hipLaunchKernelGGL(k_mgs_res<32>, g, b, lds, c->stream, A); break;
