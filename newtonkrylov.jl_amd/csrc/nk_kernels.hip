@@ -1160,10 +1160,9 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
 }
 
 template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false, bool ALT = false>
-int res_attr(nk_ctx* c, size_t lds) {
-    NK_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV, B, PRE, JV, ALT>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds));
-    return NK_OK;
+bool res_attr(size_t lds) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV, B, PRE, JV, ALT>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
 }
 }  // namespace
 
@@ -1178,39 +1177,35 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
     static const int jv_env = env_int("NK_RES_JV", 0);
     if (jin && (!jv_env || !vout || !*vout || jin->nx % 2 != 0)) return 1;
     if (c->comm && !c->mb_on) return 1;  // RCCL reductions need the host between passes
-    if (!c->res_gran) {
+    if (!c->res_gran) {  // one-time set-up; anything missing turns the resident path off for good
         int dev = 0, cus = 0, lds = 0;
-        NK_HIP(c, hipGetDevice(&dev));
-        NK_HIP(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        NK_HIP(c, hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
-        if (cus < 1 || cus > kResThreads) return 1;
-        c->res_blocks = cus;
-        const int avail = lds - (int)(sizeof(double) * kShN) - 256;
-        c->res_rl = std::max(0, avail / (int)(kResThreads * sizeof(dx2)));
-        NK_HIP(c, hipMalloc(&c->res_gran, sizeof(uint64_t) * 4 * kResThreads));
-        NK_HIP(c, hipMemsetAsync(c->res_gran, 0, sizeof(uint64_t) * 4 * kResThreads, c->stream));
-        NK_HIP(c, hipHostMalloc(&c->res_err, sizeof(int), hipHostMallocMapped));
-        *c->res_err = 0;
-        NK_HIP(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->res_err_dev), c->res_err, 0));
-        const size_t lmax = (size_t)c->res_rl * kResThreads * sizeof(dx2);
-        NK_TRY(res_attr<0>(c, lmax));
-        NK_TRY(res_attr<16>(c, lmax));
-        NK_TRY(res_attr<32>(c, lmax));
-        NK_TRY(res_attr<48>(c, lmax));
-        NK_TRY(res_attr<64>(c, lmax));
-        NK_TRY(res_attr<89>(c, lmax));
-        int per_cu = 0;  // residency: at least one block of the largest variant per CU
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_mgs_res<89>),
-                                                         kResThreads, lmax) != hipSuccess || per_cu < 1) {
+        bool ok = hipGetDevice(&dev) == hipSuccess &&
+                  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                  hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess &&
+                  cus >= 1 && cus <= kResThreads;
+        if (ok) {
+            c->res_blocks = cus;
+            const int avail = lds - (int)(sizeof(double) * kShN) - 256;
+            c->res_rl = std::max(0, avail / (int)(kResThreads * sizeof(dx2)));
+            const size_t lmax = (size_t)c->res_rl * kResThreads * sizeof(dx2);
+            ok = res_attr<0>(lmax) && res_attr<16>(lmax) && res_attr<32>(lmax) && res_attr<48>(lmax) &&
+                 res_attr<64>(lmax) && res_attr<89>(lmax) && res_attr<89, 4, true>(lmax) && res_attr<89, 4>(lmax) &&
+                 res_attr<89, 6, false, true>(lmax) && res_attr<0, 8, false, true>(lmax) &&
+                 res_attr<89, 6, false, false, true>(lmax);
+            int per_cu = 0;  // residency: at least one block of the largest variant per CU
+            ok = ok && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_mgs_res<89>),
+                                                                    kResThreads, lmax) == hipSuccess && per_cu >= 1;
+        }
+        ok = ok && hipMalloc(&c->res_gran, sizeof(uint64_t) * 4 * kResThreads) == hipSuccess;
+        ok = ok && hipMemsetAsync(c->res_gran, 0, sizeof(uint64_t) * 4 * kResThreads, c->stream) == hipSuccess;
+        ok = ok && hipHostMalloc(&c->res_err, sizeof(int), hipHostMallocMapped) == hipSuccess;
+        if (ok) *c->res_err = 0;
+        ok = ok && hipHostGetDevicePointer(reinterpret_cast<void**>(&c->res_err_dev), c->res_err, 0) == hipSuccess;
+        if (!ok) {
             (void)hipGetLastError();
             c->res_ok = false;
             return 1;
         }
-        NK_TRY((res_attr<89, 4, true>(c, lmax)));
-        NK_TRY((res_attr<89, 4>(c, lmax)));
-        NK_TRY((res_attr<89, 6, false, true>(c, lmax)));
-        NK_TRY((res_attr<0, 8, false, true>(c, lmax)));
-        NK_TRY((res_attr<89, 6, false, false, true>(c, lmax)));
     }
     ResArgs A{};
     for (int t = 0; t < np; ++t) A.V[t] = V[t % k];
