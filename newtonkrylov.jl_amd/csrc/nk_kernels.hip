@@ -1245,12 +1245,13 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         if (xv < 0) rv = pick;
         else if (rv > slots) return 1;
         A.rl = std::min(rl, slots - rv);
-        // worth it when q is re-read often enough: a one-pass sweep only adds q's load + store, and a
-        // mostly streamed q gains little over k_mgs_pass (heat 8192^2, 25 % resident: +11-13 % from
-        // k = 8 in tools/kbench_res.py, nothing over the 1-3 Arnoldi steps of a heat time step)
+        // worth it from two passes on (a one-pass sweep only adds q's load + store) while a fifth of q
+        // or more is resident (tools/kbench_res.py per pass vs the chain: 4096^2 1.28x at k = 2,
+        // 1.8x from k = 16; 2 x 4096^2 (half resident) 1.18-1.48x; 8192^2 (a quarter) 1.08-1.13x;
+        // 512^3 (an eighth) 1.01x)
         const int64_t chunk = std::max<int64_t>(1, ns / G);
         const double f = (double)(rv + A.rl) / (double)chunk;  // resident fraction of q
-        if (!explicit_rv && (np < 2 || (f < 0.5 && !(np >= 4 && f >= 0.2)))) return 1;
+        if (!explicit_rv && (np < 2 || f < 0.2)) return 1;
         // V_{k+1} straight from the registers only when all of q is resident (no streamed slot; a
         // partial last slot is streamed)
         const bool full = n2 % kResThreads == 0 && (ns + G - 1) / G <= rv + A.rl;
