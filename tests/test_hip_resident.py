@@ -6,7 +6,8 @@ its geometries against the CPU oracle -- LDS-only residency (1000^2, whose last 
 partial), LDS + streamed remainder (2560^2), registers + LDS + a partial streamed remainder
 (2900 x 2901) -- with and without reorthogonalisation (2k passes per launch), run-to-run
 determinism, and the in-kernel peer-mailbox reduction (one rank, self-send) bit for bit against
-the local one; and the optional fused FD Jv phase (NK_RES_JV=1, a child process).  The full
+the local one; a heat time step whose sweeps are only partly resident (6144^2); and the optional
+fused FD Jv phase (NK_RES_JV=1, a child process).  The full
 residency of config 2 (4096^2) is covered by test_hip.py's
 test_bratu2d_4096_full_size and by bench.py's CPU/GPU agreement check.
 """
@@ -127,3 +128,21 @@ def test_fused_jv_sweep_matches_oracle(tmp_path):
     assert int(d["nm"]) == sto["n_matvec"]
     assert np.allclose(d["h"], ho, rtol=1e-8)
     assert np.max(np.abs(d["x"] - xo)) <= 1e-8 * np.max(np.abs(xo))
+
+
+def test_heat2d_step_partly_resident_matches_oracle(ctx):
+    """One implicit-Euler heat step at 6144^2 (noisy IC): ~44 % of q resident, the rest streamed
+    through the same launch; Newton/Krylov counts and the new u equal the oracle's."""
+    N = 6144
+    rng = np.random.default_rng(0)
+    P = oc.heat2d_euler(N)
+    u0 = oc.sin_ic(P) + 0.1 * rng.uniform(-1, 1, (N, N))
+    un = ah.DeviceArray.from_numpy(u0)
+    results = []
+    ah.solve(ah.G_Euler_, ah.diffusion_, un, (P.a, P.hx, P.hy, ah.bc_zero_), P.dt, [0.0, P.dt], stats_out=results)
+    Q = oc.heat2d_euler(N, un=u0)
+    ref, so = oc.newton_krylov(Q, u0.copy(), tol_abs=6e-6)
+    r = results[0]
+    assert r.solved and so["solved"]
+    assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
+    assert np.max(np.abs(un.to_numpy() - ref)) <= 1e-10
