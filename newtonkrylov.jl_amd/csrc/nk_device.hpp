@@ -20,6 +20,9 @@ struct MbInfo {
     int* err;            // pinned host flag
     unsigned spin_limit;
 };
+hipError_t resident_bind_mb(const MbInfo& m);  // nk_resident.hip's copy of g_mb
+
+typedef double dx2 __attribute__((ext_vector_type(2)));  // 16-B streaming element
 
 namespace {
 

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <map>
 #include <string>
@@ -91,6 +92,12 @@ struct nk_ctx {
 };
 
 namespace nk {
+
+// integer knob from the environment (unset or empty: dflt)
+inline int env_int(const char* name, int dflt) {
+    const char* s = getenv(name);
+    return (s && *s) ? atoi(s) : dflt;
+}
 
 // ---------------------------------------------------------------- errors
 int fail(nk_ctx* c, int code, const std::string& msg);

@@ -190,7 +190,6 @@ __global__ __launch_bounds__(kBlock) void k_ref(int64_t n, double* __restrict__ 
 // 32 B/point (24 on the last pass) instead of the 40 B of separate kdot + kaxpy!.
 // U independent 16-B loads per stream are issued before any use (memory-level parallelism);
 // NT marks the loads/stores non-temporal (streams that are not re-read soon).
-typedef double dx2 __attribute__((ext_vector_type(2)));
 
 template <bool NT>
 __device__ __forceinline__ dx2 ld2(const dx2* p) {
@@ -453,11 +452,6 @@ __global__ __launch_bounds__(kBlock) void k_jdiag(KArgs A, double* __restrict__ 
     }
 }
 
-int env_int(const char* name, int dflt) {
-    const char* s = getenv(name);
-    return (s && *s) ? atoi(s) : dflt;
-}
-
 }  // namespace
 
 // partial-sum slot of a reduction launch.  With an RCCL communicator the kernel also folds its
@@ -480,7 +474,19 @@ double* red_out(nk_ctx* c, int len, Red* r, int* fin) {
     return part;
 }
 
+// The binding (g_mb, one copy per translation unit and device) is process-wide: several contexts
+// on one device share it.  A context binds its mailbox when it turns it on, and clears the binding
+// only if it is the one bound -- tearing down a context without a mailbox (or another one's) must
+// not unbind a live one.
+namespace {
+constexpr int kMaxDevices = 64;
+nk_ctx* g_mb_owner[kMaxDevices] = {};
+}  // namespace
+
 int mailbox_bind(nk_ctx* c) {
+    const int d = (c->device >= 0 && c->device < kMaxDevices) ? c->device : 0;
+    if (!c->mb_on && g_mb_owner[d] != c) return NK_OK;
+    g_mb_owner[d] = c->mb_on ? c : nullptr;
     MbInfo m{};
     if (c->mb_on) {
         m.self = c->mb_self;
@@ -494,7 +500,7 @@ int mailbox_bind(nk_ctx* c) {
     NK_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(g_mb), &m, sizeof(m)));
     // and the copy in every stencil instantiation unit
     for (auto bind : {stencil_bind_mb_1, stencil_bind_mb_2, stencil_bind_mb_3, stencil_bind_mb_4, stencil_bind_mb_5,
-                      stencil_bind_mb_6, stencil_bind_mb_7, stencil_bind_mb_8})
+                      stencil_bind_mb_6, stencil_bind_mb_7, stencil_bind_mb_8, resident_bind_mb})
         NK_HIP(c, bind(m));
     return NK_OK;
 }
@@ -789,535 +795,7 @@ void mgs_dispatch(int variant, int g, hipStream_t s, int64_t n, double* q, const
     }
 }
 
-// ------------------------------------------------------------------------------ resident MGS sweep
-// One Arnoldi step's whole MGS sweep (np passes + h_{k+1,k} = ||q||) in ONE launch, with q held
-// on chip: one block per CU owns a contiguous chunk of q; its first RV x 256 double2 live in
-// registers, the next rl x 256 in LDS, only the rest streams through memory.  A pass then reads
-// V_i and V_{i+1} (16 B/pt; V_{i+1} is re-read as the next pass's V_i from the Infinity Cache)
-// instead of q, V_i, V_{i+1} and the q write-back (32 B/pt).  Per-element arithmetic is exactly
-// k_mgs_pass's (q = fma(-h, V_i, q); acc = fma(V_{i+1}, q, acc)); only the partition of the
-// partial sums differs, and it is fixed, so results stay run-to-run bit reproducible.
-// Between passes every block needs h = Σ_b partial_b: each block publishes its partial as two
-// self-validating {tag:32 | half:32} granules (cdna_hip_programming.md §6 G16, R2 -- the data is
-// the flag, no fence) into a parity-double-buffered slot, then polls all G partials and sums them
-// in block order -- the same tree in every block, so every block holds the bit-identical h.
-// Double buffering is enough: a block can write pass t+2's granule only after reading everyone's
-// pass t+1 granule, i.e. after everyone finished reading pass t's.  Every spin is bounded.
-// Requires all G blocks co-resident: G = #CUs, 1 block per CU (the LDS share forces it).
-constexpr int kResMax = 64;  // passes per launch (reorthogonalisation: 2k)
-constexpr int kResThreads = 256;
-struct ResArgs {
-    const double* V[kResMax + 1];  // pass t: V_i = V[t], V_{i+1} = V[t + 1]
-    double* q;
-    double* vout;  // non-null (full residency only): store V_{k+1} = q / ||q|| here instead of q
-    double* col;   // h of every pass, ||q|| at [np]
-    double* colh;  // pinned host mirror
-    const double* red_in;  // partials of h of the first pass (the Jv's <V_1, q>)
-    uint64_t* gran;        // 2 parities x G blocks x 2 granules
-    int* err;              // pinned host flag: a poll timed out
-    int noxchg;            // kernel-variant bench only (NK_RES_NOXCHG=1): skip the exchange, h stays fixed
-    int poll1;             // one polling wave (NK_RES_POLL1, default 1) instead of every thread polling one partial
-    int strided;           // slots interleaved across blocks (every block exactly full: no streamed remainder)
-    uint64_t* tstamp;      // kernel-variant bench only: per pass and block, wall clock at pass end and after the hand-off
-    // fused FD Jv (2D Bratu): q = (F(u + eps V_k) - F0) / eps computed into the registers, with the
-    // partials of <V_1, q> -- instead of loading the q a separate Jv kernel wrote
-    const double *ju, *jv, *jf0, *jaux;
-    double jeps, jlam, jhx2, jhy2;
-    int64_t jnx;
-    int jv_on;
-    int64_t n2;            // double2 elements
-    int np, red_len, rl;
-    unsigned tag0, mb0, spin;
-};
-
-template <int RV>
-struct ResState {
-    dx2 r[RV];
-};
-
-// `budget`: this thread's remaining polls for the whole launch (a stuck grid drains in bounded time)
-// t: the exchange's index in this launch (tags, parity and mailbox epochs follow it)
-__device__ __forceinline__ double res_exchange(const ResArgs& A, double part, int t, double* sh, unsigned& budget) {
-    const int tid = threadIdx.x, G = gridDim.x;
-    const unsigned tag = A.tag0 + (unsigned)t;
-    uint64_t* slot = A.gran + (size_t)(t & 1) * G * 2;
-    if (tid == 0) {
-        const uint64_t bits = (uint64_t)__double_as_longlong(part);
-        __hip_atomic_store(slot + 2 * blockIdx.x, ((uint64_t)tag << 32) | (bits & 0xffffffffull), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(slot + 2 * blockIdx.x + 1, ((uint64_t)tag << 32) | (bits >> 32), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (A.poll1) {  // ONE wave polls: lane l sums the partials of blocks l, 64 + l, 128 + l, 192 + l
-        if (tid < 64) {
-            uint64_t w[8];
-            for (;;) {
-                bool ok = true;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int bl = 64 * j + tid;
-                    if (bl < G) {
-                        w[2 * j] = __hip_atomic_load(slot + 2 * bl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        w[2 * j + 1] = __hip_atomic_load(slot + 2 * bl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        ok = ok && (unsigned)(w[2 * j] >> 32) == tag && (unsigned)(w[2 * j + 1] >> 32) == tag;
-                    } else {
-                        w[2 * j] = w[2 * j + 1] = 0;
-                    }
-                }
-                if (ok) break;
-                if (budget == 0 || --budget == 0) {
-                    __hip_atomic_store(A.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-            double p = 0.0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                p += __longlong_as_double((long long)(((w[2 * j + 1] & 0xffffffffull) << 32) | (w[2 * j] & 0xffffffffull)));
-            p = wave_sum(p);
-            if (tid == 0) sh[kShB] = p;
-        }
-        __syncthreads();
-        const double s1 = sh[kShB];
-        if (A.mb0 == 0) return s1;
-        const unsigned epoch = A.mb0 + (unsigned)t;
-        if (blockIdx.x == 0) mb_send(s1, epoch);
-        __syncthreads();
-        return mb_recv(epoch, sh);
-    }
-    double v = 0.0;
-    if (tid < G) {
-        const uint64_t* g = slot + 2 * tid;
-        uint64_t lo = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint64_t hi = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while ((unsigned)(lo >> 32) != tag || (unsigned)(hi >> 32) != tag) {
-            if (budget == 0 || --budget == 0) {
-                __hip_atomic_store(A.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                lo = hi = 0;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            lo = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            hi = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        v = __longlong_as_double((long long)(((hi & 0xffffffffull) << 32) | (lo & 0xffffffffull)));
-    }
-    __syncthreads();  // thread 0 is done with sh[] of the partial's block_sum
-    double s = block_sum<kResThreads>(v, sh);
-    if (tid == 0) sh[kShB] = s;
-    __syncthreads();
-    s = sh[kShB];
-    if (A.mb0 == 0) return s;
-    const unsigned epoch = A.mb0 + (unsigned)t;  // cross-rank: the peer mailbox, as reduce_input does
-    if (blockIdx.x == 0) mb_send(s, epoch);
-    __syncthreads();
-    return mb_recv(epoch, sh);
-}
-
-// one pass over this block's chunk: q -= h V_i, partial of <V_{i+1}, q> (NEXT) or <q, q>.  The
-// host guarantees every block's chunk covers its RV + rl resident slots (no predicates there).
-// The FD Jv of 2D Bratu at the two points (2e, 2e + 1) of one row, exactly as k_st2d<NK_BRATU2D,
-// MODE_JFD> evaluates it (w = u + eps v; ((p - 2c) + m) / h^2 in x, then y; + lam exp(c);
-// (r - F0) / eps), + the two terms of <V_1, Jv>.  Rows j +- 1 come from memory (ghost planes at the
-// slab ends: zero or the neighbour's rows, as in the stencil kernel); x-neighbours outside the row
-// are the zero Dirichlet boundary.
-__device__ __forceinline__ dx2 res_jv_pair(const ResArgs& A, int64_t e, double& acc) {
-    const int64_t p = 2 * e, nx = A.jnx;
-    const int64_t i = p % nx;
-    const dx2 vc = *reinterpret_cast<const dx2*>(A.jv + p), uc = __builtin_nontemporal_load(reinterpret_cast<const dx2*>(A.ju + p));
-    const dx2 vu = *reinterpret_cast<const dx2*>(A.jv + p + nx), uu = *reinterpret_cast<const dx2*>(A.ju + p + nx);
-    const dx2 vd = *reinterpret_cast<const dx2*>(A.jv + p - nx), ud = *reinterpret_cast<const dx2*>(A.ju + p - nx);
-    const double vl = A.jv[p - 1], ul = A.ju[p - 1], vr = A.jv[p + 2], ur = A.ju[p + 2];
-    const dx2 f0 = __builtin_nontemporal_load(reinterpret_cast<const dx2*>(A.jf0 + p));
-    const dx2 ax = *reinterpret_cast<const dx2*>(A.jaux + p);
-    const double eps = A.jeps;
-    const double c0 = uc.x + eps * vc.x, c1 = uc.y + eps * vc.y;
-    const double wl = i > 0 ? ul + eps * vl : 0.0;
-    const double wr = i + 2 < nx ? ur + eps * vr : 0.0;
-    const double u0 = uu.x + eps * vu.x, u1 = uu.y + eps * vu.y;
-    const double d0 = ud.x + eps * vd.x, d1 = ud.y + eps * vd.y;
-    const double l0 = ((c1 - 2.0 * c0) + wl) / A.jhx2 + ((u0 - 2.0 * c0) + d0) / A.jhy2;
-    const double l1 = ((wr - 2.0 * c1) + c0) / A.jhx2 + ((u1 - 2.0 * c1) + d1) / A.jhy2;
-    const double r0 = l0 + A.jlam * exp(c0), r1 = l1 + A.jlam * exp(c1);
-    const dx2 val{(r0 - f0.x) / eps, (r1 - f0.y) / eps};
-    acc = fma(ax.x, val.x, acc);
-    acc = fma(ax.y, val.y, acc);
-    return val;
-}
-
-// the first register batch of a pass, loaded before the previous pass's hand-off completes (its
-// addresses do not depend on h): the load latency hides behind the hand-off
-template <int B>
-struct ResPre {
-    dx2 b[B], c[B];
-};
-template <int RV, int B, bool PRE>
-__device__ __forceinline__ void res_prefetch(const ResArgs& A, ResPre<B>& P, int t, int64_t base, int64_t ss) {
-    if constexpr (PRE && RV >= B) {
-        const int tid = threadIdx.x;
-        const dx2* vb = reinterpret_cast<const dx2*>(A.V[t]) + base + tid;
-        const dx2* wb = reinterpret_cast<const dx2*>(A.V[t + 1 < A.np ? t + 1 : t]) + base + tid;
-#pragma unroll
-        for (int u = 0; u < B; ++u) {
-            P.b[u] = __builtin_nontemporal_load(vb + u * ss);
-            P.c[u] = wb[u * ss];
-        }
-    }
-}
-
-// rev (alternate passes, ALT variant): the LDS slots first and in descending order, then the
-// register slots -- so the pass starts on the V_i lines the previous pass loaded last as its V_{i+1}
-// (the LDS slots, ~5 MB per XCD: still in its L2).  The register slots keep one (ascending) order:
-// a second, reversed copy of their unrolled loop costs scratch.
-template <int RV, int B, bool PRE>
-__device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx2* lq, int t, double mh, int64_t lo,
-                                           int64_t hi, ResPre<B>& P, int64_t base, int64_t ss, bool rev = false) {
-    const int tid = threadIdx.x;
-    const bool next = t + 1 < A.np;  // last pass: <q, q> instead of <V_{i+1}, q>
-    const dx2* vb = reinterpret_cast<const dx2*>(A.V[t]) + base + tid;
-    const dx2* wb = reinterpret_cast<const dx2*>(A.V[next ? t + 1 : t]) + base + tid;
-    double acc = 0.0;
-    auto upd = [&](dx2& a, const dx2 b, const dx2 c) {
-        a.x = fma(mh, b.x, a.x);
-        a.y = fma(mh, b.y, a.y);
-        const dx2 p = next ? c : a;
-        acc = fma(p.x, a.x, acc);
-        acc = fma(p.y, a.y, acc);
-    };
-    // B slots per batch: 2 x B 16-B loads in flight per lane
-    auto regs = [&] {
-        constexpr int NB = (RV + B - 1) / B;
-#pragma unroll
-        for (int bi = 0; bi < NB; ++bi) {
-            const int s0 = bi * B;
-            dx2 bv[B], cv[B];
-            if (PRE && RV >= B && s0 == 0) {
-#pragma unroll
-                for (int u = 0; u < B; ++u) {
-                    bv[u] = P.b[u];
-                    cv[u] = P.c[u];
-                }
-            } else {
-#pragma unroll
-                for (int u = 0; u < B; ++u) {
-                    if (s0 + u < RV) {
-                        bv[u] = __builtin_nontemporal_load(vb + (s0 + u) * ss);
-                        cv[u] = wb[(s0 + u) * ss];
-                    }
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < B; ++u)
-                if (s0 + u < RV) upd(S.r[s0 + u], bv[u], cv[u]);
-            __builtin_amdgcn_sched_barrier(0);  // no hoisting across batches: registers hold q, not loads
-        }
-    };
-    const dx2* vl = vb + RV * ss;
-    const dx2* wl = wb + RV * ss;
-    const int rl = A.rl;
-    auto lds = [&] {
-        auto one4 = [&](int s, bool down) {  // LDS slots s .. s+3 (down: s+3 .. s)
-            dx2 bv[4], cv[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                bv[u] = __builtin_nontemporal_load(vl + (s + u) * ss);
-                cv[u] = wl[(s + u) * ss];
-            }
-#pragma unroll
-            for (int u0 = 0; u0 < 4; ++u0) {
-                const int u = down ? 3 - u0 : u0;
-                dx2 a = lq[(s + u) * kResThreads + tid];
-                upd(a, bv[u], cv[u]);
-                lq[(s + u) * kResThreads + tid] = a;
-            }
-        };
-        auto one = [&](int s) {
-            const dx2 b = __builtin_nontemporal_load(vl + s * ss);
-            const dx2 cc = wl[s * ss];
-            dx2 a = lq[s * kResThreads + tid];
-            upd(a, b, cc);
-            lq[s * kResThreads + tid] = a;
-        };
-        const int r4 = rl / 4 * 4;
-        if (!rev) {
-            for (int s = 0; s < r4; s += 4) one4(s, false);
-            for (int s = r4; s < rl; ++s) one(s);
-        } else {
-            for (int s = rl - 1; s >= r4; --s) one(s);
-            for (int s = r4 - 4; s >= 0; s -= 4) one4(s, true);
-        }
-    };
-    auto stream = [&] {
-        // the streamed remainder: q through memory, as k_mgs_pass
-        dx2* q2 = reinterpret_cast<dx2*>(A.q);
-        const dx2* v2 = reinterpret_cast<const dx2*>(A.V[t]);
-        const dx2* w2 = reinterpret_cast<const dx2*>(A.V[next ? t + 1 : t]);
-        int64_t e = lo + (int64_t)(RV + rl) * kResThreads + tid;
-        for (; e + kResThreads < hi; e += 2 * kResThreads) {
-            const int64_t e1 = e + kResThreads;
-            dx2 a0 = q2[e], a1 = q2[e1];
-            const dx2 b0 = __builtin_nontemporal_load(v2 + e), b1 = __builtin_nontemporal_load(v2 + e1);
-            const dx2 c0 = w2[e], c1 = w2[e1];
-            upd(a0, b0, c0);
-            upd(a1, b1, c1);
-            q2[e] = a0;
-            q2[e1] = a1;
-        }
-        if (e < hi) {
-            dx2 a0 = q2[e];
-            const dx2 b0 = __builtin_nontemporal_load(v2 + e);
-            const dx2 c0 = w2[e];
-            upd(a0, b0, c0);
-            q2[e] = a0;
-        }
-    };
-    if (rev) lds();
-    regs();
-    if (!rev) lds();
-    stream();
-    return acc;
-}
-
-template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false, bool ALT = false>
-__global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
-    extern __shared__ dx2 lq[];  // rl x 256 double2
-    __shared__ double sh[kShN];
-    const int tid = threadIdx.x, G = gridDim.x;
-    // balanced partition of the ceil(n2 / 256) 256-wide slots: block b owns slots [b S / G, (b+1) S / G)
-    const int64_t ns = (A.n2 + kResThreads - 1) / kResThreads;
-    const int64_t lo = (int64_t)blockIdx.x * ns / G * kResThreads;
-    const int64_t hi = std::min<int64_t>((int64_t)(blockIdx.x + 1) * ns / G * kResThreads, A.n2);
-    // slot s of this block: contiguous chunk (base = lo, stride 256) or, with A.strided (every block
-    // exactly full), interleaved across the blocks (base = 256 b, stride 256 G) so that every block
-    // touches every address region alike
-    const int64_t base = A.strided ? (int64_t)blockIdx.x * kResThreads : lo;
-    const int64_t ss = A.strided ? (int64_t)G * kResThreads : kResThreads;
-    ResState<RV> S;
-    ResPre<B> P;
-    double h;
-    unsigned budget = A.spin;
-    constexpr int xo = JV ? 1 : 0;  // exchange 0 carries <V_1, J V_k> when the Jv is fused
-    if constexpr (JV) {
-        double jacc = 0.0;
-        // register slots in rounds of kJvStage, each computed by a compact (not unrolled) loop into
-        // the LDS and then moved into its registers; the LDS slots last
-        constexpr int kJvStage = 16;  // the host guarantees rl >= kJvStage when RV > 0
-#pragma unroll
-        for (int s0 = 0; s0 < RV; s0 += kJvStage) {
-            const int m = RV - s0 < kJvStage ? RV - s0 : kJvStage;
-#pragma unroll 4
-            for (int u = 0; u < m; ++u) lq[u * kResThreads + tid] = res_jv_pair(A, base + (s0 + u) * ss + tid, jacc);
-#pragma unroll
-            for (int u = 0; u < kJvStage; ++u)
-                if (s0 + u < RV) S.r[s0 + u] = lq[u * kResThreads + tid];
-        }
-#pragma unroll 4
-        for (int s = 0; s < A.rl; ++s) lq[s * kResThreads + tid] = res_jv_pair(A, base + (RV + s) * ss + tid, jacc);
-        res_prefetch<RV, B, PRE>(A, P, 0, base, ss);
-        h = res_exchange(A, block_sum<kResThreads>(jacc, sh), 0, sh, budget);
-    } else {
-        const dx2* qb = reinterpret_cast<const dx2*>(A.q) + base + tid;
-#pragma unroll
-        for (int s = 0; s < RV; ++s) S.r[s] = qb[s * ss];
-        for (int s = 0; s < A.rl; ++s) lq[s * kResThreads + tid] = qb[(RV + s) * ss];
-        res_prefetch<RV, B, PRE>(A, P, 0, base, ss);
-        h = reduce_input(A.red_in, A.red_len, sh);
-    }
-    for (int t = 0; t < A.np; ++t) {
-        if (blockIdx.x == 0 && tid == 0) {
-            A.col[t] = h;
-            if (A.colh) A.colh[t] = h;
-        }
-        const double acc = res_pass<RV, B, PRE>(A, S, lq, t, -h, lo, hi, P, base, ss, ALT && (t & 1));
-        if (t + 1 < A.np) res_prefetch<RV, B, PRE>(A, P, t + 1, base, ss);
-        const double part = block_sum<kResThreads>(acc, sh);
-        if (A.tstamp && tid == 0) A.tstamp[((size_t)t * G + blockIdx.x) * 2] = wall_clock64();
-        if (!A.noxchg) h = res_exchange(A, part, t + xo, sh, budget);
-        else __syncthreads();
-        if (A.tstamp && tid == 0) A.tstamp[((size_t)t * G + blockIdx.x) * 2 + 1] = wall_clock64();
-    }
-    if (blockIdx.x == 0 && tid == 0) {
-        const double r = sqrt(h);
-        A.col[A.np] = r;
-        if (A.colh) A.colh[A.np] = r;
-    }
-    if (A.vout) {  // the next Arnoldi step's kdivcopy!(V_{k+1}, q, h) done here: q never leaves the chip
-        const double hn = sqrt(h);  // == col[np], the h the next Jv would divide by
-        dx2* vw = reinterpret_cast<dx2*>(A.vout) + base + tid;
-#pragma unroll
-        for (int s = 0; s < RV; ++s) vw[s * ss] = dx2{S.r[s].x / hn, S.r[s].y / hn};
-        for (int s = 0; s < A.rl; ++s) {
-            const dx2 a = lq[s * kResThreads + tid];
-            vw[(RV + s) * ss] = dx2{a.x / hn, a.y / hn};
-        }
-        return;
-    }
-    dx2* qw = reinterpret_cast<dx2*>(A.q) + base + tid;
-#pragma unroll
-    for (int s = 0; s < RV; ++s) qw[s * ss] = S.r[s];
-    for (int s = 0; s < A.rl; ++s) qw[(RV + s) * ss] = lq[s * kResThreads + tid];
-}
-
-template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false, bool ALT = false>
-bool res_attr(size_t lds) {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV, B, PRE, JV, ALT>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
-}
 }  // namespace
-
-// Resident sweep: returns NK_OK after enqueueing, or 1 when the resident path does not apply
-// (caller falls back to one k_mgs_pass launch per pass).
-int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, int k, int np, Red in, double* col,
-                     double* colh, int rv, double** vout, const ResJv* jin) {
-    if (np < 1 || np > kResMax || (n & 1) || !c->res_ok) return 1;
-    // fused Jv phase: off by default -- at one wave per SIMD its ~190 fp64 VALU instructions per point
-    // pair (IEEE divisions, two exp) do not hide behind the loads: 791 us per Arnoldi step vs
-    // 619 + 124 us for the sweep and a separate Jv kernel (-1.7 % end to end, 4096^2)
-    static const int jv_env = env_int("NK_RES_JV", 0);
-    if (jin && (!jv_env || !vout || !*vout || jin->nx % 2 != 0)) return 1;
-    if (c->comm && !c->mb_on) return 1;  // RCCL reductions need the host between passes
-    if (!c->res_gran) {  // one-time set-up; anything missing turns the resident path off for good
-        int dev = 0, cus = 0, lds = 0;
-        bool ok = hipGetDevice(&dev) == hipSuccess &&
-                  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-                  hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess &&
-                  cus >= 1 && cus <= kResThreads;
-        if (ok) {
-            c->res_blocks = cus;
-            const int avail = lds - (int)(sizeof(double) * kShN) - 256;
-            c->res_rl = std::max(0, avail / (int)(kResThreads * sizeof(dx2)));
-            const size_t lmax = (size_t)c->res_rl * kResThreads * sizeof(dx2);
-            ok = res_attr<0>(lmax) && res_attr<16>(lmax) && res_attr<32>(lmax) && res_attr<48>(lmax) &&
-                 res_attr<64>(lmax) && res_attr<89>(lmax) && res_attr<89, 4, true>(lmax) && res_attr<89, 4>(lmax) &&
-                 res_attr<89, 6, false, true>(lmax) && res_attr<0, 8, false, true>(lmax) &&
-                 res_attr<89, 6, false, false, true>(lmax);
-            int per_cu = 0;  // residency: at least one block of the largest variant per CU
-            ok = ok && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_mgs_res<89>),
-                                                                    kResThreads, lmax) == hipSuccess && per_cu >= 1;
-        }
-        ok = ok && hipMalloc(&c->res_gran, sizeof(uint64_t) * 4 * kResThreads) == hipSuccess;
-        ok = ok && hipMemsetAsync(c->res_gran, 0, sizeof(uint64_t) * 4 * kResThreads, c->stream) == hipSuccess;
-        ok = ok && hipHostMalloc(&c->res_err, sizeof(int), hipHostMallocMapped) == hipSuccess;
-        if (ok) *c->res_err = 0;
-        ok = ok && hipHostGetDevicePointer(reinterpret_cast<void**>(&c->res_err_dev), c->res_err, 0) == hipSuccess;
-        if (!ok) {
-            (void)hipGetLastError();
-            c->res_ok = false;
-            return 1;
-        }
-    }
-    ResArgs A{};
-    for (int t = 0; t < np; ++t) A.V[t] = V[t % k];
-    A.V[np] = V[(np) % k];
-    A.q = q;
-    A.col = col;
-    A.colh = colh;
-    A.red_in = in.ptr;
-    A.red_len = in.len;
-    A.gran = c->res_gran;
-    A.err = c->res_err_dev;
-    A.n2 = n >> 1;
-    A.np = np;
-    int xv = -1;  // experimental variant (kernel-variant bench)
-    {  // every block's chunk must hold its rv + rl resident slots in full (the kernel does not predicate them)
-        const int64_t G = c->res_blocks, n2 = n >> 1;
-        const int64_t ns = (n2 + kResThreads - 1) / kResThreads;
-        const int64_t whole = ns / G - (n2 % kResThreads != 0 ? 1 : 0);  // the last block's last slot may be partial
-        if (whole < 1) return 1;
-        const int slots = (int)std::min<int64_t>(whole, 1 << 20);
-        static const int rl_env = env_int("NK_RES_RL", -1);
-        static const int rv_env = env_int("NK_RES_RV", -1);
-        int rl = std::min(slots, rl_env >= 0 ? std::min(rl_env, c->res_rl) : c->res_rl);  // LDS first
-        const bool explicit_rv = rv >= 0 || rv_env >= 0;  // a caller's choice skips the benefit test below
-        if (rv >= 1000) {  // kernel-variant bench: 1000 + {0: 89 slots, batches of 4 + prefetch across the hand-off; 1: same, no prefetch; 2: alternating slot order}
-            xv = rv - 1000;
-            rv = 89;
-        }
-        if (rv < 0) rv = rv_env >= 0 ? rv_env : slots - rl;  // registers hold what the LDS cannot
-        static const int kRv[] = {89, 64, 48, 32, 16, 0};  // the instantiated register-slot counts
-        int pick = 0;
-        for (int r : kRv)
-            if (r <= rv && r <= slots) {
-                pick = r;
-                break;
-            }
-        if (xv < 0) rv = pick;
-        else if (rv > slots) return 1;
-        A.rl = std::min(rl, slots - rv);
-        // worth it from two passes on (a one-pass sweep only adds q's load + store) while a fifth of q
-        // or more is resident (tools/kbench_res.py per pass vs the chain: 4096^2 1.28x at k = 2,
-        // 1.8x from k = 16; 2 x 4096^2 (half resident) 1.18-1.48x; 8192^2 (a quarter) 1.08-1.13x;
-        // 512^3 (an eighth) 1.01x)
-        const int64_t chunk = std::max<int64_t>(1, ns / G);
-        const double f = (double)(rv + A.rl) / (double)chunk;  // resident fraction of q
-        if (!explicit_rv && (np < 2 || f < 0.2)) return 1;
-        // V_{k+1} straight from the registers only when all of q is resident (no streamed slot; a
-        // partial last slot is streamed)
-        const bool full = n2 % kResThreads == 0 && (ns + G - 1) / G <= rv + A.rl;
-        static const int vout_env = env_int("NK_RES_VOUT", 1);
-        if (vout && *vout && !(full && vout_env)) *vout = nullptr;
-        A.vout = vout ? *vout : nullptr;
-        if (jin && (!A.vout || (rv != 0 && rv != 89) || (rv > 0 && A.rl < 16))) return 1;  // fused Jv: full residency, instantiated rv, LDS staging
-        static const int strided_env = env_int("NK_RES_STRIDED", 0);
-        A.strided = strided_env && n2 % kResThreads == 0 && ns % G == 0 && ns / G == rv + A.rl;
-    }
-    if (jin) {
-        A.jv_on = 1;
-        A.ju = jin->u;
-        A.jv = jin->v;
-        A.jf0 = jin->F0;
-        A.jaux = jin->aux;
-        A.jeps = jin->eps;
-        A.jlam = jin->lam;
-        A.jhx2 = jin->hx2;
-        A.jhy2 = jin->hy2;
-        A.jnx = jin->nx;
-    }
-    const unsigned nx_ = (unsigned)np + (jin ? 1u : 0u);  // hand-offs in this launch
-    if (c->res_tag > 0xfffffff0u - (unsigned)(kResMax + 1)) {  // tag wrap: restart from clean granules
-        NK_HIP(c, hipMemsetAsync(c->res_gran, 0, sizeof(uint64_t) * 4 * kResThreads, c->stream));
-        c->res_tag = 0;
-    }
-    A.tag0 = c->res_tag + 1;
-    c->res_tag += nx_;
-    A.mb0 = 0;
-    if (c->mb_on) {  // consecutive mailbox epochs, no 16-bit wrap inside the range
-        if (c->mb_epoch + nx_ > 0xffffu) c->mb_epoch = 0;
-        A.mb0 = c->mb_epoch + 1;
-        c->mb_epoch += nx_;
-    }
-    static const int noxchg = env_int("NK_RES_NOXCHG", 0);
-    A.noxchg = noxchg;
-    static const int poll1 = env_int("NK_RES_POLL1", 1);
-    A.poll1 = poll1;
-    A.tstamp = c->res_tstamp;
-    A.spin = 1u << 22;  // polls per thread per launch (~1 s): a grid that is not co-resident fails fast
-    const size_t lds = (size_t)A.rl * kResThreads * sizeof(dx2);
-    // q in (or the fused Jv's u, V_k, F0, V_1), q (or V_{k+1}) out, V_i (+ V_{i+1}) per pass
-    const double bytes = (jin ? 32.0 : 8.0) * n + 8.0 * n + (16.0 * np - 8.0) * n;
-    return launch(c, jin ? "arnoldi_step" : "mgs_sweep", bytes, [&] {
-        const dim3 g(c->res_blocks), b(kResThreads);
-        switch (rv) {
-        case 0:
-            if (jin) hipLaunchKernelGGL((k_mgs_res<0, 8, false, true>), g, b, lds, c->stream, A);
-            else hipLaunchKernelGGL(k_mgs_res<0>, g, b, lds, c->stream, A);
-            break;
-        case 16: hipLaunchKernelGGL(k_mgs_res<16>, g, b, lds, c->stream, A); break;
-        case 48: hipLaunchKernelGGL(k_mgs_res<48>, g, b, lds, c->stream, A); break;
-        case 64: hipLaunchKernelGGL(k_mgs_res<64>, g, b, lds, c->stream, A); break;
-        case 89:
-            if (jin) hipLaunchKernelGGL((k_mgs_res<89, 6, false, true>), g, b, lds, c->stream, A);
-            else if (xv == 0) hipLaunchKernelGGL((k_mgs_res<89, 4, true>), g, b, lds, c->stream, A);
-            else if (xv == 1) hipLaunchKernelGGL((k_mgs_res<89, 4>), g, b, lds, c->stream, A);
-            else if (xv == 2) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, true>), g, b, lds, c->stream, A);
-            else hipLaunchKernelGGL(k_mgs_res<89>, g, b, lds, c->stream, A);
-            break;
-        default: hipLaunchKernelGGL(k_mgs_res<32>, g, b, lds, c->stream, A); break;
-        }
-    });
-}
-
 int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const double* vnext, Red in, double* h_out,
                     double* h_host, Red* out,
                     int rev) {
@@ -1637,104 +1115,6 @@ extern "C" int nkb_stencil3d(nk_ctx* c, int64_t n, int mode, int epi, int fast, 
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     for (double* q : {u, v, F0, aux, out, un}) nk_vec_free(c, q);
-    return NK_OK;
-}
-
-namespace nk {
-namespace {
-__global__ __launch_bounds__(kBlock) void k_hashfill(int64_t n, double* __restrict__ x, uint64_t seed) {
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-        uint64_t z = (uint64_t)i * 0x9e3779b97f4a7c15ull + seed;
-        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-        z ^= z >> 31;
-        x[i] = (double)(z >> 11) * 0x1.0p-53 - 0.5;
-    }
-}
-}  // namespace
-}  // namespace nk
-
-// The resident MGS sweep (launch_mgs_sweep, register slots rv) against the per-pass chain
-// (launch_mgs_pass) on the same q and basis: us_out / us_ref = microseconds per pass of each;
-// diff_out = max |q_res - q_chain| / max |q_chain| after the sweep, and the largest relative
-// difference of the Hessenberg column in diff_out[1].
-extern "C" int nkb_mgs_res(nk_ctx* c, int64_t n, int k, int rv, int reps, double* us_out, double* us_ref, double* diff_out) {
-    using namespace nk;
-    if (!c || n < 2 || k < 1 || k > kResMax || reps < 1 || !us_out || !us_ref || !diff_out) return NK_E_ARG;
-    // NK_RES_TSTAMP=<file>: also dump the per-pass, per-block wall clocks of the last timed sweep
-    const char* tsf = getenv("NK_RES_TSTAMP");
-    if (tsf && *tsf && !c->res_tstamp) NK_HIP(c, hipMalloc(&c->res_tstamp, sizeof(uint64_t) * 2 * kResMax * 1024));
-    std::vector<double*> V(k + 3, nullptr);
-    for (size_t v = 0; v < V.size(); ++v) {
-        NK_HIP(c, hipMalloc(&V[v], sizeof(double) * n));
-        hipLaunchKernelGGL(k_hashfill, dim3(2048), dim3(kBlock), 0, c->stream, n, V[v], (uint64_t)(v + 1) * 7919u);
-    }
-    double* q0 = V[k];
-    double* qa = V[k + 1];
-    double* qb = V[k + 2];
-    double* col = c->scal + 64;
-    double* col2 = c->scal + 64 + 2 * kResMax;
-    hipEvent_t e0, e1;
-    NK_HIP(c, hipEventCreate(&e0));
-    NK_HIP(c, hipEventCreate(&e1));
-    double ms_a = 0.0, ms_b = 0.0;
-    for (int r = 0; r <= reps; ++r) {
-        float ms = 0.f;
-        NK_TRY(launch_copy(c, n, qa, q0));
-        Red red{};
-        NK_TRY(launch_dot(c, n, V[0], qa, &red));
-        NK_HIP(c, hipEventRecord(e0, c->stream));
-        for (int t = 0; t < k; ++t) {
-            Red nxt{};
-            NK_TRY(launch_mgs_pass(c, n, qa, V[t], t + 1 < k ? V[t + 1] : nullptr, red, col + t, nullptr, &nxt, 0));
-            red = nxt;
-        }
-        NK_TRY(launch_finalize(c, red, col + k, 1, nullptr));
-        NK_HIP(c, hipEventRecord(e1, c->stream));
-        NK_HIP(c, hipEventSynchronize(e1));
-        NK_HIP(c, hipEventElapsedTime(&ms, e0, e1));
-        if (r > 0) ms_a += ms;
-        NK_TRY(launch_copy(c, n, qb, q0));
-        NK_TRY(launch_dot(c, n, V[0], qb, &red));
-        NK_HIP(c, hipEventRecord(e0, c->stream));
-        const int rc = launch_mgs_sweep(c, n, qb, V.data(), k, k, red, col2, nullptr, rv, nullptr, nullptr);
-        if (rc != NK_OK) return rc == 1 ? fail(c, NK_E_ARG, "resident sweep not applicable") : rc;
-        NK_HIP(c, hipEventRecord(e1, c->stream));
-        NK_HIP(c, hipEventSynchronize(e1));
-        NK_HIP(c, hipEventElapsedTime(&ms, e0, e1));
-        if (r > 0) ms_b += ms;
-        if (*c->res_err) return fail(c, NK_E_HIP, "resident sweep: granule poll timed out");
-    }
-    *us_ref = 1e3 * ms_a / ((double)reps * k);
-    *us_out = 1e3 * ms_b / ((double)reps * k);
-    std::vector<double> a(n), b(n), ca(k + 1), cb(k + 1);
-    NK_HIP(c, hipMemcpy(a.data(), qa, sizeof(double) * n, hipMemcpyDeviceToHost));
-    NK_HIP(c, hipMemcpy(b.data(), qb, sizeof(double) * n, hipMemcpyDeviceToHost));
-    NK_HIP(c, hipMemcpy(ca.data(), col, sizeof(double) * (k + 1), hipMemcpyDeviceToHost));
-    NK_HIP(c, hipMemcpy(cb.data(), col2, sizeof(double) * (k + 1), hipMemcpyDeviceToHost));
-    double m = 0.0, d = 0.0, dh = 0.0;
-    for (int64_t i = 0; i < n; ++i) {
-        m = std::max(m, std::fabs(a[i]));
-        d = std::max(d, std::fabs(a[i] - b[i]));
-    }
-    for (int i = 0; i <= k; ++i) dh = std::max(dh, std::fabs(ca[i] - cb[i]) / std::max(1e-300, std::fabs(ca[i])));
-    diff_out[0] = m > 0 ? d / m : d;
-    diff_out[1] = dh;
-    diff_out[2] = (double)c->res_rl;
-    if (c->res_tstamp && tsf && *tsf) {
-        std::vector<uint64_t> ts((size_t)2 * k * c->res_blocks);
-        NK_HIP(c, hipMemcpy(ts.data(), c->res_tstamp, sizeof(uint64_t) * ts.size(), hipMemcpyDeviceToHost));
-        if (FILE* f = std::fopen(tsf, "wb")) {
-            std::fwrite(ts.data(), sizeof(uint64_t), ts.size(), f);
-            std::fclose(f);
-        }
-        (void)hipFree(c->res_tstamp);
-        c->res_tstamp = nullptr;
-    }
-    diff_out[3] = (double)c->res_blocks;
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    for (auto p : V) (void)hipFree(p);
     return NK_OK;
 }
 

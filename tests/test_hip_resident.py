@@ -66,7 +66,7 @@ def test_resident_sweep_deterministic(ctx):
     assert runs[0][1].residuals == runs[1][1].residuals
 
 
-def test_resident_sweep_mailbox_one_rank_is_bitwise(monkeypatch):
+def test_resident_sweep_mailbox_one_rank_is_bitwise(ctx, monkeypatch):
     """The sweep's per-pass scalars through the peer mailbox (self-send) equal the local ones bit for bit."""
     P = oc.bratu2d(1024)
     u = oc.sin_ic(P)
@@ -81,6 +81,7 @@ def test_resident_sweep_mailbox_one_rank_is_bitwise(monkeypatch):
     assert forced.mailbox_active
     ah.set_default_context(forced)
     x2, s2 = solve(P, u, b, ctx=forced, restart=True, atol=0.0, rtol=0.0, itmax=15)
+    ah.set_default_context(ctx)
     assert s1.niter == s2.niter == 15
     assert s1.residuals == s2.residuals
     assert np.array_equal(x1, x2)
@@ -133,6 +134,7 @@ def test_fused_jv_sweep_matches_oracle(tmp_path):
 def test_heat2d_step_partly_resident_matches_oracle(ctx):
     """One implicit-Euler heat step at 6144^2 (noisy IC): ~44 % of q resident, the rest streamed
     through the same launch; Newton/Krylov counts and the new u equal the oracle's."""
+    ah.set_default_context(ctx)
     N = 6144
     rng = np.random.default_rng(0)
     P = oc.heat2d_euler(N)
@@ -146,3 +148,25 @@ def test_heat2d_step_partly_resident_matches_oracle(ctx):
     assert r.solved and so["solved"]
     assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
     assert np.max(np.abs(un.to_numpy() - ref)) <= 1e-10
+
+
+def test_closing_a_context_keeps_another_ones_mailbox(monkeypatch):
+    """The mailbox binding is per process and device: closing a context without a mailbox must not
+    unbind a live one (it used to, and every later reduction of the live context summed 0 ranks)."""
+    P = oc.bratu2d(64)
+    u0 = oc.sin_ic(P)
+    ref = float(np.linalg.norm(oc.residual(P, u0)))
+    monkeypatch.setenv("NK_DIST_FORCE", "1")
+    monkeypatch.setenv("NK_DIST_MAILBOX", "1")
+    forced = ah.Context(0)
+    forced.init_distributed(0, 1, ah.dist_unique_id())
+    assert forced.mailbox_active
+    monkeypatch.delenv("NK_DIST_FORCE")
+    monkeypatch.delenv("NK_DIST_MAILBOX")
+    other = ah.Context(0)
+    other.close()
+    u = ah.DeviceArray.from_numpy(u0, None, forced)
+    res = u.zero()
+    from ariadne_hip import problems as pr
+    n = pr.bratu2d_.residual_norm(res, u, (P.hx, P.hy, P.lam))
+    assert abs(n - ref) <= 1e-12 * ref
