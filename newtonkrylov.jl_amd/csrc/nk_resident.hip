@@ -522,8 +522,12 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
     A.tstamp = c->res_tstamp;
     A.spin = 1u << 22;  // polls per thread per launch (~1 s): a grid that is not co-resident fails fast
     const size_t lds = (size_t)A.rl * kResThreads * sizeof(dx2);
-    // q in (or the fused Jv's u, V_k, F0, V_1), q (or V_{k+1}) out, V_i (+ V_{i+1}) per pass
-    const double bytes = (jin ? 32.0 : 8.0) * n + 8.0 * n + (16.0 * np - 8.0) * n;
+    // algorithmic bytes: the resident fraction f of q is loaded once (or computed by the fused Jv
+    // from u, V_k, F0, V_1), stored once (q or V_{k+1}) and each pass reads V_i (+ V_{i+1}); the
+    // streamed rest reads and writes q in every pass as well (k_mgs_pass's 32 / 24 B/pt)
+    const double f = std::min(1.0, (double)c->res_blocks * (rv + A.rl) * kResThreads / (double)(n >> 1));
+    const double per_res = (jin ? 5.0 : 2.0) + 2.0 * np - 1.0, per_str = 4.0 * np - 1.0;  // doubles per point
+    const double bytes = 8.0 * (double)n * (f * per_res + (1.0 - f) * per_str);
     return launch(c, jin ? "arnoldi_step" : "mgs_sweep", bytes, [&] {
         const dim3 g(c->res_blocks), b(kResThreads);
         switch (rv) {
