@@ -128,7 +128,8 @@ static int mb_open_peers(nk_ctx* c, int rank, int nranks, const char* handles, c
     std::vector<uint64_t*> peers((size_t)nranks);
     // the resident MGS sweep needs every CU of the device to itself: off when a peer may share it
     // (no bus ids: the mailbox-only transport, made for ranks on one GPU)
-    c->res_ok = busids != nullptr || nranks < 2;
+    const bool shared_ok = env_int("NK_RES_SHARED", 0) != 0;  // tests: ranks on one GPU with NK_RES_BLOCKS grids
+    c->res_ok = busids != nullptr || nranks < 2 || shared_ok;
     for (int r = 0; r < nranks; ++r) {
         if (r == rank) {
             peers[r] = c->mb_self;
@@ -143,7 +144,7 @@ static int mb_open_peers(nk_ctx* c, int rank, int nranks, const char* handles, c
                 mb_disable(c);
                 return fail(c, NK_E_HIP, "mailbox: rank " + std::to_string(r) + "'s device is not visible here");
             }
-            if (dev == c->device) c->res_ok = false;
+            if (dev == c->device && !shared_ok) c->res_ok = false;
             if (dev != c->device) {
                 int can = 0;
                 if (hipDeviceCanAccessPeer(&can, c->device, dev) != hipSuccess || !can) {

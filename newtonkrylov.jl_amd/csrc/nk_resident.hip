@@ -412,7 +412,10 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
                   hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess &&
                   cus >= 1 && cus <= kResThreads;
         if (ok) {
-            c->res_blocks = cus;
+            // NK_RES_BLOCKS (tests only): a smaller grid, so that ranks sharing one GPU
+            // (NK_RES_SHARED=1) can each hold their sweep's blocks resident at once
+            const int rb = env_int("NK_RES_BLOCKS", 0);
+            c->res_blocks = (rb > 0 && rb < cus) ? rb : cus;
             const int avail = lds - (int)(sizeof(double) * kShN) - 256;
             c->res_rl = std::max(0, avail / (int)(kResThreads * sizeof(dx2)));
             const size_t lmax = (size_t)c->res_rl * kResThreads * sizeof(dx2);

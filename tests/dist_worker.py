@@ -22,6 +22,9 @@ ap.add_argument("--out", required=True)
 ap.add_argument("--nx", type=int, default=48)
 ap.add_argument("--ny", type=int, default=40)
 ap.add_argument("--jv", default="exact")
+ap.add_argument("--krylov-itmax", type=int, default=0,
+                help="> 0: instead of the Newton solve, one restarted GMRES(10) solve J x = F(u0) with this fixed "
+                     "budget (atol = rtol = 0); rank 0 saves x and the residual history")
 ap.add_argument("--problem", choices=["bratu", "heat_periodic"], default="bratu",
                 help="heat_periodic: G_Trapezoid! ∘ diffusion! with bc_periodic! -- u_n's ghost planes are "
                      "exchanged too and the slabs form a ring (rank 0 <-> rank world-1)")
@@ -86,6 +89,23 @@ ah.mul_(out, ah.JacobianOperator(F_, res, u, p, jv=args.jv), vd)
 jv_loc = out.to_numpy()
 F_loc = res.to_numpy()
 dot = ah.kdot(len(u), u, vd)
+if args.krylov_itmax > 0:
+    ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=10))
+    ctx.prof_enable(1)
+    ah.krylov_solve_(ws, ah.JacobianOperator(F_, res, u, p, jv=args.jv), res, restart=True, atol=0.0, rtol=0.0,
+                     itmax=args.krylov_itmax, history=True)
+    sweeps = ctx.prof_read().get("mgs_sweep", {}).get("launches", 0)  # resident sweeps that ran
+    ctx.prof_enable(0)
+    parts = [None] * world
+    dist.all_gather_object(parts, dict(y0=y0, x=ws.x.to_numpy()))
+    if rank == 0:
+        parts.sort(key=lambda d: d["y0"])
+        np.savez(args.out + ".npz", x=np.concatenate([d["x"] for d in parts]), h=np.array(ws.stats.residuals))
+        json.dump(dict(niter=ws.stats.niter, n_matvec=ws.stats.n_matvec, world=world, sweeps=sweeps),
+                  open(args.out + ".json", "w"))
+    dist.barrier()
+    ctx.sync()
+    sys.exit(0)
 u, r = ah.newton_krylov_(F_, u, p, res, jv=args.jv, **kw)
 parts = [None] * world
 dist.all_gather_object(parts, dict(y0=y0, u=u.to_numpy(), jv=jv_loc, F=F_loc))

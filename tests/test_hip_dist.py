@@ -165,3 +165,34 @@ def test_periodic_trapezoid_ring_matches_oracle(tmp_path, world, transport):
     assert meta["solved"] and so["solved"]
     assert (meta["outer"], meta["inner"]) == (so["outer_iterations"], so["inner_iterations"])
     assert np.max(np.abs(d["u"] - uo)) <= 1e-10
+
+
+def test_resident_sweep_two_ranks_one_gpu(tmp_path):
+    """The resident MGS sweep with its per-pass scalars crossing ranks through the peer mailbox: two
+    ranks share the test box's GPU, each with a 128-block sweep grid (NK_RES_BLOCKS) so that both
+    grids are resident together; 1024^2 global (a 1024 x 512 slab per rank: all of q on chip, the
+    V_{k+1} hand-over to the next Jv included).  20 restarted GMRES(10) steps against the oracle."""
+    out = str(tmp_path / "dist")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
+           "--nx", "1024", "--ny", "1024", "--krylov-itmax", "20"]
+    env = dict(os.environ, NK_WORKER_SHARED_DEVICE="1", NK_RES_SHARED="1", NK_RES_BLOCKS="128")
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
+    try:
+        log, _ = proc.communicate(timeout=180)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, signal.SIGKILL)
+        pytest.fail("distributed worker timed out")
+    assert proc.returncode == 0, log.decode()[-3000:]
+    meta = json.load(open(out + ".json"))
+    d = np.load(out + ".npz")
+    P = oc.bratu2d(1024, 1024)
+    u0 = oc.sin_ic(P)
+    F = oc.residual(P, u0)
+    kw = dict(restart=True, atol=0.0, rtol=0.0, itmax=20)
+    xo, sto, ho = oc.krylov_solve(P, u0, F, jv="exact", memory=10, **kw)
+    assert meta["sweeps"] >= 16  # the resident launches ran (steps 2..10 of both cycles)
+    assert meta["niter"] == sto["niter"] == 20 and meta["n_matvec"] == sto["n_matvec"]
+    assert np.allclose(d["h"], ho, rtol=1e-9, atol=0)
+    assert np.max(np.abs(d["x"] - xo)) <= 1e-9 * np.max(np.abs(xo))
