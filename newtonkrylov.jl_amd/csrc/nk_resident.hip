@@ -170,13 +170,26 @@ __device__ __forceinline__ dx2 res_jv_pair(const ResArgs& A, int64_t e, double& 
     return val;
 }
 
+// V loads of a pass: NTM 0 = V_i non-temporal, V_{i+1} cached (it is the next pass's V_i);
+// 1 = both cached; 2 = both non-temporal (kernel-variant bench)
+template <int NTM>
+__device__ __forceinline__ dx2 ldv(const dx2* p) {
+    if constexpr (NTM == 1) return *p;
+    else return __builtin_nontemporal_load(p);
+}
+template <int NTM>
+__device__ __forceinline__ dx2 ldw(const dx2* p) {
+    if constexpr (NTM == 2) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
 // the first register batch of a pass, loaded before the previous pass's hand-off completes (its
 // addresses do not depend on h): the load latency hides behind the hand-off
 template <int B>
 struct ResPre {
     dx2 b[B], c[B];
 };
-template <int RV, int B, bool PRE>
+template <int RV, int B, bool PRE, int NTM = 0>
 __device__ __forceinline__ void res_prefetch(const ResArgs& A, ResPre<B>& P, int t, int64_t base, int64_t ss) {
     if constexpr (PRE && RV >= B) {
         const int tid = threadIdx.x;
@@ -184,8 +197,8 @@ __device__ __forceinline__ void res_prefetch(const ResArgs& A, ResPre<B>& P, int
         const dx2* wb = reinterpret_cast<const dx2*>(A.V[t + 1 < A.np ? t + 1 : t]) + base + tid;
 #pragma unroll
         for (int u = 0; u < B; ++u) {
-            P.b[u] = __builtin_nontemporal_load(vb + u * ss);
-            P.c[u] = wb[u * ss];
+            P.b[u] = ldv<NTM>(vb + u * ss);
+            P.c[u] = ldw<NTM>(wb + u * ss);
         }
     }
 }
@@ -194,7 +207,7 @@ __device__ __forceinline__ void res_prefetch(const ResArgs& A, ResPre<B>& P, int
 // register slots -- so the pass starts on the V_i lines the previous pass loaded last as its V_{i+1}
 // (the LDS slots, ~5 MB per XCD: still in its L2).  The register slots keep one (ascending) order:
 // a second, reversed copy of their unrolled loop costs scratch.
-template <int RV, int B, bool PRE>
+template <int RV, int B, bool PRE, int NTM = 0>
 __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx2* lq, int t, double mh, int64_t lo,
                                            int64_t hi, ResPre<B>& P, int64_t base, int64_t ss, bool rev = false) {
     const int tid = threadIdx.x;
@@ -226,8 +239,8 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
 #pragma unroll
                 for (int u = 0; u < B; ++u) {
                     if (s0 + u < RV) {
-                        bv[u] = __builtin_nontemporal_load(vb + (s0 + u) * ss);
-                        cv[u] = wb[(s0 + u) * ss];
+                        bv[u] = ldv<NTM>(vb + (s0 + u) * ss);
+                        cv[u] = ldw<NTM>(wb + (s0 + u) * ss);
                     }
                 }
             }
@@ -245,8 +258,8 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
             dx2 bv[4], cv[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                bv[u] = __builtin_nontemporal_load(vl + (s + u) * ss);
-                cv[u] = wl[(s + u) * ss];
+                bv[u] = ldv<NTM>(vl + (s + u) * ss);
+                cv[u] = ldw<NTM>(wl + (s + u) * ss);
             }
 #pragma unroll
             for (int u0 = 0; u0 < 4; ++u0) {
@@ -257,8 +270,8 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
             }
         };
         auto one = [&](int s) {
-            const dx2 b = __builtin_nontemporal_load(vl + s * ss);
-            const dx2 cc = wl[s * ss];
+            const dx2 b = ldv<NTM>(vl + s * ss);
+            const dx2 cc = ldw<NTM>(wl + s * ss);
             dx2 a = lq[s * kResThreads + tid];
             upd(a, b, cc);
             lq[s * kResThreads + tid] = a;
@@ -303,7 +316,8 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
     return acc;
 }
 
-template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false, bool ALT = false>
+template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false, bool ALT = false,
+          int NTM = 0>
 __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     extern __shared__ dx2 lq[];  // rl x 256 double2
     __shared__ double sh[kShN];
@@ -338,14 +352,14 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
         }
 #pragma unroll 4
         for (int s = 0; s < A.rl; ++s) lq[s * kResThreads + tid] = res_jv_pair(A, base + (RV + s) * ss + tid, jacc);
-        res_prefetch<RV, B, PRE>(A, P, 0, base, ss);
+        res_prefetch<RV, B, PRE, NTM>(A, P, 0, base, ss);
         h = res_exchange(A, block_sum<kResThreads>(jacc, sh), 0, sh, budget);
     } else {
         const dx2* qb = reinterpret_cast<const dx2*>(A.q) + base + tid;
 #pragma unroll
         for (int s = 0; s < RV; ++s) S.r[s] = qb[s * ss];
         for (int s = 0; s < A.rl; ++s) lq[s * kResThreads + tid] = qb[(RV + s) * ss];
-        res_prefetch<RV, B, PRE>(A, P, 0, base, ss);
+        res_prefetch<RV, B, PRE, NTM>(A, P, 0, base, ss);
         h = reduce_input(A.red_in, A.red_len, sh);
     }
     for (int t = 0; t < A.np; ++t) {
@@ -353,8 +367,8 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
             A.col[t] = h;
             if (A.colh) A.colh[t] = h;
         }
-        const double acc = res_pass<RV, B, PRE>(A, S, lq, t, -h, lo, hi, P, base, ss, ALT && (t & 1));
-        if (t + 1 < A.np) res_prefetch<RV, B, PRE>(A, P, t + 1, base, ss);
+        const double acc = res_pass<RV, B, PRE, NTM>(A, S, lq, t, -h, lo, hi, P, base, ss, ALT && (t & 1));
+        if (t + 1 < A.np) res_prefetch<RV, B, PRE, NTM>(A, P, t + 1, base, ss);
         const double part = block_sum<kResThreads>(acc, sh);
         if (A.tstamp && tid == 0) A.tstamp[((size_t)t * G + blockIdx.x) * 2] = wall_clock64();
         if (!A.noxchg) h = res_exchange(A, part, t + xo, sh, budget);
@@ -383,9 +397,10 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     for (int s = 0; s < A.rl; ++s) qw[(RV + s) * ss] = lq[s * kResThreads + tid];
 }
 
-template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false, bool ALT = false>
+template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false, bool ALT = false,
+          int NTM = 0>
 bool res_attr(size_t lds) {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV, B, PRE, JV, ALT>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV, B, PRE, JV, ALT, NTM>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
 }
 }  // namespace
@@ -422,7 +437,8 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
             ok = res_attr<0>(lmax) && res_attr<16>(lmax) && res_attr<32>(lmax) && res_attr<48>(lmax) &&
                  res_attr<64>(lmax) && res_attr<89>(lmax) && res_attr<89, 4, true>(lmax) && res_attr<89, 4>(lmax) &&
                  res_attr<89, 6, false, true>(lmax) && res_attr<0, 8, false, true>(lmax) &&
-                 res_attr<89, 6, false, false, true>(lmax);
+                 res_attr<89, 6, false, false, true>(lmax) && res_attr<89, 6, false, false, false, 1>(lmax) &&
+                 res_attr<89, 6, false, false, false, 2>(lmax);
             int per_cu = 0;  // residency: at least one block of the largest variant per CU
             ok = ok && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_mgs_res<89>),
                                                                     kResThreads, lmax) == hipSuccess && per_cu >= 1;
@@ -461,7 +477,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         static const int rv_env = env_int("NK_RES_RV", -1);
         int rl = std::min(slots, rl_env >= 0 ? std::min(rl_env, c->res_rl) : c->res_rl);  // LDS first
         const bool explicit_rv = rv >= 0 || rv_env >= 0;  // a caller's choice skips the benefit test below
-        if (rv >= 1000) {  // kernel-variant bench: 1000 + {0: 89 slots, batches of 4 + prefetch across the hand-off; 1: same, no prefetch; 2: alternating slot order}
+        if (rv >= 1000) {  // kernel-variant bench: 1000 + {0: 89 slots, batches of 4 + prefetch across the hand-off; 1: same, no prefetch; 2: alternating slot order; 3: V_i cached; 4: V_{i+1} non-temporal}
             xv = rv - 1000;
             rv = 89;
         }
@@ -546,6 +562,8 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
             else if (xv == 0) hipLaunchKernelGGL((k_mgs_res<89, 4, true>), g, b, lds, c->stream, A);
             else if (xv == 1) hipLaunchKernelGGL((k_mgs_res<89, 4>), g, b, lds, c->stream, A);
             else if (xv == 2) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, true>), g, b, lds, c->stream, A);
+            else if (xv == 3) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, false, 1>), g, b, lds, c->stream, A);
+            else if (xv == 4) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, false, 2>), g, b, lds, c->stream, A);
             else hipLaunchKernelGGL(k_mgs_res<89>, g, b, lds, c->stream, A);
             break;
         default: hipLaunchKernelGGL(k_mgs_res<32>, g, b, lds, c->stream, A); break;
