@@ -434,7 +434,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
             const int avail = lds - (int)(sizeof(double) * kShN) - 256;
             c->res_rl = std::max(0, avail / (int)(kResThreads * sizeof(dx2)));
             const size_t lmax = (size_t)c->res_rl * kResThreads * sizeof(dx2);
-            ok = res_attr<0>(lmax) && res_attr<16>(lmax) && res_attr<32>(lmax) && res_attr<48>(lmax) &&
+            ok = res_attr<0>(lmax) && res_attr<16>(lmax) && res_attr<25>(lmax) && res_attr<32>(lmax) && res_attr<48>(lmax) &&
                  res_attr<64>(lmax) && res_attr<89>(lmax) && res_attr<89, 4, true>(lmax) && res_attr<89, 4>(lmax) &&
                  res_attr<89, 6, false, true>(lmax) && res_attr<0, 8, false, true>(lmax) &&
                  res_attr<89, 6, false, false, true>(lmax) && res_attr<89, 6, false, false, false, 1>(lmax) &&
@@ -482,7 +482,8 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
             rv = 89;
         }
         if (rv < 0) rv = rv_env >= 0 ? rv_env : slots - rl;  // registers hold what the LDS cannot
-        static const int kRv[] = {89, 64, 48, 32, 16, 0};  // the instantiated register-slot counts
+        // the instantiated register-slot counts (25 + 39 LDS slots = 64: a 4096 x 2048 slab, 4096^2 on two GPUs)
+        static const int kRv[] = {89, 64, 48, 32, 25, 16, 0};
         int pick = 0;
         for (int r : kRv)
             if (r <= rv && r <= slots) {
@@ -555,6 +556,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
             else hipLaunchKernelGGL(k_mgs_res<0>, g, b, lds, c->stream, A);
             break;
         case 16: hipLaunchKernelGGL(k_mgs_res<16>, g, b, lds, c->stream, A); break;
+        case 25: hipLaunchKernelGGL(k_mgs_res<25>, g, b, lds, c->stream, A); break;
         case 48: hipLaunchKernelGGL(k_mgs_res<48>, g, b, lds, c->stream, A); break;
         case 64: hipLaunchKernelGGL(k_mgs_res<64>, g, b, lds, c->stream, A); break;
         case 89:
