@@ -119,6 +119,12 @@ const int mgs_resident = [] {
     return (e && *e) ? atoi(e) : 1;
 }();
 
+// NK_RES_JV=1: the 2D Bratu FD Jv inside the resident sweep's launch (off: slower)
+const int mgs_fused_jv = [] {
+    const char* e = getenv("NK_RES_JV");
+    return (e && *e) ? atoi(e) : 0;
+}();
+
 // Krylov.jl sym_givens (real case)
 void sym_givens(double a, double b, double* c, double* s, double* rho) {
     if (b == 0.0) {
@@ -312,7 +318,8 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         if ((int)vready.size() < k + 2) vready.resize(k + 2, 0);
         // 2D Bratu, FD Jv, V_k stored by the previous resident sweep: Jv + MGS sweep in ONE launch
         // (q = J V_k is computed into the registers that hold it through the sweep)
-        if (spec && k >= 2 && vready[k - 1] && mgs_resident && A.mode == NK_JV_FD && p->kind == NK_BRATU2D) {
+        if (mgs_fused_jv && spec && k >= 2 && vready[k - 1] && mgs_resident && A.mode == NK_JV_FD &&
+            p->kind == NK_BRATU2D) {
             NK_TRY(ws_basis(ws, k + 1));
             double* vnext = ws->V[k];
             const ResJv jin{A.u, ws->V[k - 1], A.F0, ws->V[0], A.fd_eps(1.0), p->lambda, p->hx * p->hx, p->hy * p->hy, p->nx};
