@@ -4,7 +4,8 @@ From 512^2 up, every Arnoldi step's MGS sweep runs as ONE launch with q held in 
 (one block per CU, partial sums handed between passes as tagged granules).  These solves cover
 its geometries against the CPU oracle -- LDS-only residency (1000^2, whose last 256-wide slot is
 partial), LDS + streamed remainder (2560^2), registers + LDS + a partial streamed remainder
-(2900 x 2901) -- with and without reorthogonalisation (2k passes per launch), run-to-run
+(2900 x 2901) -- with and without reorthogonalisation (2k passes per launch; at 1024^2 also with
+V_{k+1} handed to the next Jv), run-to-run
 determinism, and the in-kernel peer-mailbox reduction (one rank, self-send) bit for bit against
 the local one; a heat time step whose sweeps are only partly resident (6144^2); and the optional
 fused FD Jv phase (NK_RES_JV=1, a child process).  The full
@@ -43,7 +44,7 @@ def solve(P, u, b, ctx=None, **kw):
 
 
 @pytest.mark.parametrize("nx,ny,reorth", [(1000, 1000, False), (2560, 2560, False), (2900, 2901, False),
-                                          (2900, 2901, True)])
+                                          (2900, 2901, True), (1024, 1024, True)])
 def test_resident_sweep_matches_oracle(ctx, nx, ny, reorth):
     P = oc.bratu2d(nx, ny)
     u = oc.sin_ic(P)
