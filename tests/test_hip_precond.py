@@ -232,3 +232,19 @@ def test_newton_ilu_bratu2d_matches_oracle(ctx):
     assert r.solved and so["solved"]
     assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
     np.testing.assert_allclose(u.to_numpy(), ref, rtol=0, atol=1e-9 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("algo", ["gmres", "fgmres"])
+def test_jacobi_preconditioned_resident_sweep_matches_oracle(ctx, algo):
+    """The same at 1024^2, where each Arnoldi step's MGS sweep is the resident launch (the
+    preconditioned path hands it q, not V_{k+1}): 24 restarted steps against the oracle."""
+    P, u0, u, res, p = bratu(1024, 1024)
+    J = ah.JacobianOperator(ah.bratu2d_, res, u, p, jv="exact")
+    kw = dict(restart=True, itmax=24, atol=0.0, rtol=0.0, memory=10)
+    x, st = solve(J, res, algo, N=ah.jacobi(J), **kw)
+    b = oc.residual(P, u0)
+    d = oc.jacobian_diag(P, u0, reciprocal=True)
+    xo, so, ho = oc.krylov_solve(P, u0, b, algo=algo, jv="exact", N=("diag", d), **kw)
+    assert st.niter == so["niter"] == 24 and st.n_matvec == so["n_matvec"]
+    np.testing.assert_allclose(st.residuals, ho, rtol=1e-9)
+    assert np.linalg.norm(x - xo) <= 1e-9 * np.linalg.norm(xo)
