@@ -28,6 +28,8 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -90,11 +92,30 @@ def parse():
                          "small slabs only (e.g. --side 1024): a rank's spin-waiting reduction consumers must leave "
                          "the other rank's kernels room on the shared GPU)")
     ap.add_argument("--cpu-itmax", type=int, default=300, help="Arnoldi steps in the CPU-baseline sample (300 = one bench step)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, os.cpu_count())")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0: OMP_NUM_THREADS (the GPU box's per-GPU CPU share), else every core in the affinity "
+                         "mask; the machine's nproc is reported beside it")
     ap.add_argument("--traffic-json", default="",
                     help="per-kernel HBM traffic from separate rocprofv3 --pmc passes (tools/pmc_traffic.py); "
                          "default profiles/r01/pmc_traffic_<workload>.json when present")
+    ap.add_argument("--launch-probe", type=int, default=-1, help=argparse.SUPPRESS)  # CPU test of the launcher
     return ap.parse_args()
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list) -> int:
+    """`bench.py --gpus N` run as a plain process (no torch.distributed.run around it): start the N
+    ranks here, one process per GPU (LOCAL_RANK = device), with this same argument list, and return
+    the launcher's exit status.  Nothing in this parent touches the GPU (the ranks are children, not
+    an exec), so the N = 1 path and the driver's own torchrun launch are unchanged."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + list(argv)
+    return subprocess.run(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")).returncode
 
 
 def noisy(shape_rows, nx, seed_rows):
@@ -274,17 +295,37 @@ class HeatEuler:
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     if args.workload == "bratu2d" and not args.memory:
         args.memory = 30
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)", file=sys.stderr)
+        sys.exit(2)
+    if args.launch_probe >= 0:  # CPU test of the launcher: report what this rank was given, no GPU work
+        print(json.dumps({"rank": rank, "world": world, "local": local, "argv": sys.argv[1:]}), flush=True)
+        sys.exit(args.launch_probe if rank == world - 1 else 0)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    ctx = ah.Context(int(os.environ.get("NK_BENCH_DEVICE", local)))  # NK_BENCH_DEVICE: diagnostic override
+    # one GPU per rank (LOCAL_RANK); a box with fewer GPUs than ranks shares them (a rehearsal only:
+    # RCCL refuses two ranks on one device, so that needs --transport mailbox and small slabs)
+    ndev = ah.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no GPU visible (the HIP path has no CPU fallback)")
+    shared = world > ndev
+    if shared and args.transport == "rccl":
+        raise SystemExit(f"bench.py: {world} ranks on {ndev} GPU(s): RCCL needs one GPU per rank "
+                         "(use --transport mailbox with a small --side to rehearse on fewer GPUs)")
+    device = int(os.environ.get("NK_BENCH_DEVICE", local % ndev))  # NK_BENCH_DEVICE: diagnostic override
+    ctx = ah.Context(device)
     ah.set_default_context(ctx)
     if world > 1 and args.transport == "mailbox":
         handles = [None] * world
@@ -400,6 +441,7 @@ def main():
             "data": "synthetic (see config.workload)",
             "config": {"workload": W.workload, "matvecs_per_step": matvecs // max(1, args.steps),
                        "parallelism": f"slab{world}",
+                       "devices": f"{min(world, ndev)} GPU(s) for {world} rank(s)" + (" (shared: rehearsal)" if shared else ""),
                        "reductions": ("peer mailbox (IPC/xGMI)" if ctx.mailbox_active else
                                       ("ncclAllReduce" if world > 1 else "local"))},
             "hbm_gbs_algorithmic": round(world * total_bytes / elapsed / 1e9, 1) if total_bytes else None,
@@ -410,8 +452,13 @@ def main():
             "newton_n_res": last.stats.n_res if last else None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            # the CPU share this process is given: OMP_NUM_THREADS (the GPU box sets it to its per-GPU share
+            # of the host, 16), else every core in the affinity mask; the machine's full count is reported too
+            affinity = len(os.sched_getaffinity(0))
+            threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
             out["cpu_baseline"] = W.cpu_baseline(threads)
+            out["cpu_baseline"]["host_cpus"] = {"nproc": os.cpu_count(), "affinity": affinity,
+                                                "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
             out["cpu_baseline"]["value"] = round(out["cpu_baseline"]["value"], 4)
             if hasattr(W, "agreement"):
                 out["cpu_gpu_agreement"] = W.agreement()

@@ -270,22 +270,24 @@ int nk_dist_init(nk_ctx* c, int32_t rank, int32_t nranks, const char id[128]) {
         // per rank: 64-byte IPC handle + 32-byte PCI bus id of its device
         constexpr size_t kRec = 96;
         std::vector<char> all(kRec * nranks, 0);
-        char* dbuf = nullptr;
+        // the exchange buffer is the context's reduction scratch (allocated at nk_ctx_create), so no
+        // rank can fail an allocation here and leave the others alone in the collectives below
+        static_assert(kRec * kMbRanks <= sizeof(double) * kRedCap, "handle records fit one reduction slot");
+        char* dbuf = reinterpret_cast<char*>(c->red);
         int rc = nk_dist_mailbox_handle(c, all.data() + kRec * (size_t)rank);
         if (rc == NK_OK && hipDeviceGetPCIBusId(all.data() + kRec * (size_t)rank + 64, 32, c->device) != hipSuccess)
             rc = NK_E_HIP;
-        if (hipMalloc(&dbuf, all.size()) != hipSuccess) {
-            std::fprintf(stderr, "[nkhip] rank %d: no memory for the handle exchange\n", rank);
-            return fail(c, NK_E_NOMEM, "hipMalloc (mailbox handles)");
-        }
         // allgather the IPC handles: collective, every rank takes part whatever its local state
         (void)hipMemcpy(dbuf + kRec * (size_t)rank, all.data() + kRec * (size_t)rank, kRec, hipMemcpyHostToDevice);
         const ncclResult_t ag = ncclAllGather(dbuf + kRec * (size_t)rank, dbuf, kRec, ncclChar, cm->comm, c->stream);
         if (ag != ncclSuccess || hipStreamSynchronize(c->stream) != hipSuccess ||
             hipMemcpy(all.data(), dbuf, all.size(), hipMemcpyDeviceToHost) != hipSuccess)
             rc = NK_E_RCCL;
-        (void)hipFree(dbuf);
-        if (ag != ncclSuccess) return rccl_fail(c, ag, "ncclAllGather (mailbox handles)");
+        if (ag != ncclSuccess) {
+            // still join the verdict's all-reduce (the other ranks are in it), then report the failure
+            (void)mb_verdict(c, false);
+            return rccl_fail(c, ag, "ncclAllGather (mailbox handles)");
+        }
         if (rc == NK_OK) {
             std::vector<char> handles(64 * (size_t)nranks), busids(32 * (size_t)nranks);
             for (int r = 0; r < nranks; ++r) {

@@ -2,8 +2,10 @@
 
 * one rank with a forced RCCL communicator: every reduction goes through finalize -> ncclAllReduce
   -> consumer, which must reproduce the single-GPU run bit for bit (same partials, same order);
-* 2 and 3 ranks (slabs of a 2D Bratu grid; on a one-GPU box all ranks share device 0): halo
-  exchange + all-reduced dots against the CPU oracle on the whole grid.
+* 2 and 3 ranks (slabs of a 2D Bratu grid): halo exchange + all-reduced dots against the CPU
+  oracle on the whole grid.  Each rank gets its own GPU when the box has enough (then the RCCL
+  variants must run: an RCCL error fails the test); on a box with fewer GPUs than ranks they
+  share device 0, where only the mailbox transport can run (RCCL refuses -> skip).
 """
 import json
 import os
@@ -89,6 +91,22 @@ def test_mailbox_two_ranks_one_gpu(tmp_path):
         assert abs(nrm2 - 2 * (y * y).sum()) <= 1e-9 * nrm2  # sqrt then square: a few ulp
 
 
+def worker_env(world, **extra):
+    """One device per rank when there are enough; else every rank on device 0 (NK_WORKER_SHARED_DEVICE)."""
+    env = dict(os.environ, **extra)
+    if ah.device_count() < world:
+        env["NK_WORKER_SHARED_DEVICE"] = "1"
+    else:
+        env.pop("NK_WORKER_SHARED_DEVICE", None)
+    return env
+
+
+def check_meta(meta, world):
+    if "skip" in meta:
+        assert ah.device_count() < world, "RCCL failed although every rank had its own GPU"
+        pytest.skip(meta["skip"])
+
+
 def free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -106,7 +124,7 @@ def test_slabs_match_oracle(tmp_path, world, transport):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", transport]
-    env = dict(os.environ, NK_WORKER_SHARED_DEVICE="1")
+    env = worker_env(world)
     proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
     try:
         log, _ = proc.communicate(timeout=180)
@@ -115,8 +133,7 @@ def test_slabs_match_oracle(tmp_path, world, transport):
         pytest.fail("distributed worker timed out")
     assert proc.returncode == 0, log.decode()[-3000:]
     meta = json.load(open(out + ".json"))
-    if "skip" in meta:
-        pytest.skip(meta["skip"])
+    check_meta(meta, world)
     d = np.load(out + ".npz")
     P = oc.bratu2d(48, 40)
     u0 = oc.sin_ic(P)
@@ -143,7 +160,7 @@ def test_periodic_trapezoid_ring_matches_oracle(tmp_path, world, transport):
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", transport,
            "--problem", "heat_periodic"]
-    env = dict(os.environ, NK_WORKER_SHARED_DEVICE="1")
+    env = worker_env(world)
     proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
     try:
         log, _ = proc.communicate(timeout=180)
@@ -152,8 +169,7 @@ def test_periodic_trapezoid_ring_matches_oracle(tmp_path, world, transport):
         pytest.fail("distributed worker timed out")
     assert proc.returncode == 0, log.decode()[-3000:]
     meta = json.load(open(out + ".json"))
-    if "skip" in meta:
-        pytest.skip(meta["skip"])
+    check_meta(meta, world)
     d = np.load(out + ".npz")
     rng = np.random.default_rng(5)
     un = rng.standard_normal((40, 48))
@@ -177,7 +193,7 @@ def test_resident_sweep_two_ranks_one_gpu(tmp_path):
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
            "--nx", "1024", "--ny", "1024", "--krylov-itmax", "20"]
-    env = dict(os.environ, NK_WORKER_SHARED_DEVICE="1", NK_RES_SHARED="1", NK_RES_BLOCKS="128")
+    env = worker_env(2, NK_RES_SHARED="1", NK_RES_BLOCKS="128")
     proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
     try:
         log, _ = proc.communicate(timeout=180)

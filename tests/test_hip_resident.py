@@ -30,7 +30,16 @@ def ctx():
     c.sync()
 
 
+def sweeps(ctx, name="mgs_sweep"):
+    """Launches of the resident sweep since profiling was enabled: launch_mgs_sweep silently falls back
+    to one launch per pass when it cannot keep q on chip, so every test here checks that it ran."""
+    return ctx.prof_read().get(name, {}).get("launches", 0)
+
+
 def solve(P, u, b, ctx=None, **kw):
+    ctx = ctx or ah.default_context()
+    ctx.prof_reset()
+    ctx.prof_enable(1 << 20)  # count launches (time almost none)
     g = ah.Grid.full(P.nx, P.ny)
     ud = ah.DeviceArray.from_numpy(u, g, ctx)
     bd = ah.DeviceArray.from_numpy(b, g, ctx)
@@ -40,6 +49,9 @@ def solve(P, u, b, ctx=None, **kw):
     memory = kw.pop("memory", 10)
     ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=memory))
     ah.krylov_solve_(ws, ah.JacobianOperator(ah.bratu2d_, res, ud, p, jv="exact"), bd, history=True, **kw)
+    n_sweeps = sweeps(ctx)
+    ctx.prof_enable(0)
+    assert n_sweeps > 0, "the resident MGS sweep did not run"
     return ws.x.to_numpy(), ws.stats
 
 
@@ -103,9 +115,13 @@ res = ud.zero()
 p = (P.hx, P.hy, P.lam)
 ah.bratu2d_(res, ud, p)
 ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=10))
+ctx = ah.default_context()
+ctx.prof_enable(1 << 20)
 ah.krylov_solve_(ws, ah.JacobianOperator(ah.bratu2d_, res, ud, p, jv="fd"), bd, restart=True, atol=0.0, rtol=0.0,
                  itmax=20, history=True)
-np.savez(sys.argv[2], x=ws.x.to_numpy(), h=np.array(ws.stats.residuals), F0=res.to_numpy(), nm=ws.stats.n_matvec)
+steps = ctx.prof_read().get("arnoldi_step", {}).get("launches", 0)  # the fused Jv + sweep launches
+np.savez(sys.argv[2], x=ws.x.to_numpy(), h=np.array(ws.stats.residuals), F0=res.to_numpy(), nm=ws.stats.n_matvec,
+         steps=steps)
 """
 
 
@@ -128,6 +144,7 @@ def test_fused_jv_sweep_matches_oracle(tmp_path):
     kw = dict(restart=True, atol=0.0, rtol=0.0, itmax=20)
     xo, sto, ho = oc.krylov_solve(P, u, b, jv="fd", F0=d["F0"], memory=10, **kw)
     assert int(d["nm"]) == sto["n_matvec"]
+    assert int(d["steps"]) > 0, "the fused Jv + resident sweep launch did not run"
     assert np.allclose(d["h"], ho, rtol=1e-8)
     assert np.max(np.abs(d["x"] - xo)) <= 1e-8 * np.max(np.abs(xo))
 
@@ -142,7 +159,11 @@ def test_heat2d_step_partly_resident_matches_oracle(ctx):
     u0 = oc.sin_ic(P) + 0.1 * rng.uniform(-1, 1, (N, N))
     un = ah.DeviceArray.from_numpy(u0)
     results = []
+    ctx.prof_reset()
+    ctx.prof_enable(1 << 20)
     ah.solve(ah.G_Euler_, ah.diffusion_, un, (P.a, P.hx, P.hy, ah.bc_zero_), P.dt, [0.0, P.dt], stats_out=results)
+    assert sweeps(ctx) > 0, "the partly resident sweep did not run"
+    ctx.prof_enable(0)
     Q = oc.heat2d_euler(N, un=u0)
     ref, so = oc.newton_krylov(Q, u0.copy(), tol_abs=6e-6)
     r = results[0]
