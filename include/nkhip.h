@@ -160,6 +160,26 @@ int nk_ilu0_factor(nk_ctx* ctx, const nk_problem* p, const double* u, double* dt
  * the exact tangent kernel; user problems need user->JT. */
 int nk_jtv(nk_ctx* ctx, const nk_problem* p, double* out, const double* u, const double* v);
 
+/* Batched products: mul!(Out::AbstractMatrix, J, V) (src/Ariadne.jl:67-84, Enzyme BatchDuplicated)
+ * and mul!(Out, transpose(J), V) (:109-138).  out[b] = J(u) v[b] for b < k (host arrays of k device
+ * grid functions).  One launch per 8 columns reads u, F0 (and u_n) once for all of them; each product
+ * is bit-identical to nk_jv / nk_jtv of that column (FD: eps <= 0 picks each column's own step as
+ * nk_jv does).  User residuals: one nk_jv / nk_jtv per column. */
+int nk_jv_batched(nk_ctx* ctx, const nk_problem* p, int32_t k, double* const* out, const double* u,
+                  const double* const* v, const double* F0, int32_t mode, double eps);
+int nk_jtv_batched(nk_ctx* ctx, const nk_problem* p, int32_t k, double* const* out, const double* u,
+                   const double* const* v);
+
+/* collect(J) / collect(transpose(J)) (src/Ariadne.jl:140-162): the exact Jacobian J(u) as the CSC
+ * arrays of the reference's SparseMatrixCSC, 0-based (colptr: n + 1 entries; rowval / nzval: nnz),
+ * entries that are exactly 0 dropped as the reference drops them.  Built-in stencils: 2 dim + 1
+ * coloured probes in one batched launch + device assembly (values identical to unit probing); user
+ * residuals and periodic grids whose extents the colouring does not fit: unit probes (n <= 8192).
+ * cap = capacity of rowval / nzval ((2 dim + 1) n always suffices); if nnz > cap, NK_E_ARG with *nnz
+ * set.  One rank only. */
+int nk_jacobian_collect(nk_ctx* ctx, const nk_problem* p, const double* u, int32_t transpose, int64_t* colptr,
+                        int64_t* rowval, double* nzval, int64_t cap, int64_t* nnz);
+
 /* ---------------------------------------------------------------- Krylov vector primitives
  * Krylov.kdot/knorm/kscal!/kaxpy!/kaxpby!/kcopy!/kfill!/kdivcopy!/kref! -- the overload points
  * examples/halovector.jl:51-147 demonstrates for a custom vector type.  n = interior length. */

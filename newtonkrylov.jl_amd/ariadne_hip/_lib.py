@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "libnkhip.so")
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "nkhip.h")
 
 NK_OK = 0
+NK_E_HIP, NK_E_ARG, NK_E_NOMEM, NK_E_RCCL, NK_E_STATE, NK_E_USER = -1, -2, -3, -4, -5, -6
 NK_BRATU1D, NK_BRATU2D, NK_HEAT2D_EULER, NK_HEAT3D_EULER = 1, 2, 3, 4
 NK_HEAT2D_MIDPOINT, NK_HEAT3D_MIDPOINT, NK_HEAT2D_TRAPEZOID, NK_HEAT3D_TRAPEZOID = 5, 6, 7, 8
 NK_USER1D, NK_USER2D, NK_USER3D = 16, 17, 18
@@ -103,6 +104,10 @@ SIGNATURES = {
     "nk_residual_norm": (C.c_int, [_VP, _PP, _VP, _VP, _PD]),
     "nk_jv": (C.c_int, [_VP, _PP, _VP, _VP, _VP, _VP, _I32, _D]),
     "nk_jtv": (C.c_int, [_VP, _PP, _VP, _VP, _VP]),
+    "nk_jv_batched": (C.c_int, [_VP, _PP, _I32, C.POINTER(_VP), _VP, C.POINTER(_VP), _VP, _I32, _D]),
+    "nk_jtv_batched": (C.c_int, [_VP, _PP, _I32, C.POINTER(_VP), _VP, C.POINTER(_VP)]),
+    "nk_jacobian_collect": (C.c_int, [_VP, _PP, _VP, _I32, C.POINTER(_I64), C.POINTER(_I64), _PD, _I64,
+                                      C.POINTER(_I64)]),
     "nk_jacobian_diag": (C.c_int, [_VP, _PP, _VP, _VP, _I32]),
     "nk_ilu0_factor": (C.c_int, [_VP, _PP, _VP, _VP]),
     "nk_precond_apply": (C.c_int, [_VP, _PP, _VP, _VP, _VP, _I32, _VP, _VP]),

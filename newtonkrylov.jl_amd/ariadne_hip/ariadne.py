@@ -121,13 +121,26 @@ JacobianOperator.T = property(transpose)
 
 def mul_(out, J, v, eps: float = 0.0):
     """mul!(out, J, v) (src/Ariadne.jl:48-57); mul!(out, transpose(J), v) (:87-107).  Unlike Enzyme
-    it does not rewrite J.res.  Lists of vectors are the batched form (:59-85, :109-138): one
-    product per column, each exactly the single-vector result."""
+    it does not rewrite J.res.  Lists of vectors are the batched form mul!(Out, J, V) (:59-85,
+    :109-138): ONE fused launch per 8 columns (nk_jv_batched: u, F(u) read once for all of them),
+    each column bit-identical to the single-vector product."""
     if isinstance(out, (list, tuple)):
         if not isinstance(v, (list, tuple)) or len(out) != len(v):
             raise ValueError("batched mul!: out and v must be lists of equal length")
-        for o, w in zip(out, v):
-            mul_(o, J, w, eps)
+        if not out:
+            return None
+        k = len(out)
+        outs = (C.c_void_p * k)(*[o.ptr for o in out])
+        vs = (C.c_void_p * k)(*[w.ptr for w in v])
+        ctx = out[0].ctx
+        if isinstance(J, TransposeOperator):
+            prob = J.problem()
+            ctx.check(load().nk_jtv_batched(ctx.handle, C.byref(prob), k, outs, J.J.u.ptr, vs), "mul!(Out, J', V)")
+            return None
+        prob = J.problem()
+        F0 = J.res.ptr if J.jv_mode == _lib.NK_JV_FD else None
+        ctx.check(load().nk_jv_batched(ctx.handle, C.byref(prob), k, outs, J.u.ptr, vs, F0, J.jv_mode, float(eps)),
+                  "mul!(Out, J, V)")
         return None
     if isinstance(J, TransposeOperator):
         prob = J.problem()
@@ -140,25 +153,17 @@ def mul_(out, J, v, eps: float = 0.0):
     return None
 
 
-def _stencil_colors(grid):
-    """Distance-2 colouring of the 3/5/7-point stencil graph: colour(i, j, k) = (i + 2j + 3k) mod
-    (2 dim + 1) gives the point and its 2 dim neighbours pairwise different colours."""
-    import numpy as np
-
-    nx, ny, nz = grid.nxyz
-    ncol = 2 * grid.dim + 1
-    k, j, i = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
-    return ((i + 2 * j + 3 * k) % ncol).reshape(grid.np_shape), ncol
-
-
 def collect(J, *, coloring: str | None = None):
-    """collect(J) (src/Ariadne.jl:140-162): the Jacobian as a scipy.sparse CSC matrix, row/column
-    index = interior point in memory order (x fastest).  The reference applies J to the n unit
-    vectors; here the built-in stencils are probed with 2 dim + 1 coloured vectors instead (a
-    distance-2 colouring of the stencil: every probe entry then holds exactly one Jacobian entry,
-    computed by the same kernel from the same operands as the unit-vector probe, so the values are
-    identical).  coloring="dense" (the default for user residuals, whose coupling is unknown)
-    probes the n unit vectors like the reference.  transpose(J) gives the transpose."""
+    """collect(J) (src/Ariadne.jl:140-162): the exact Jacobian J(u) as a scipy.sparse CSC matrix
+    (row/column index = interior point in memory order, x fastest; exact zeros dropped like the
+    reference's `if out[i] != 0`).  Assembled on the device by nk_jacobian_collect: the built-in
+    stencils are probed with 2 dim + 1 coloured vectors in ONE batched launch (a distance-2
+    colouring: every probe entry is exactly one Jacobian entry, computed by the same kernel from the
+    same operands as the unit-vector probe, so the values are identical), and the CSC arrays are
+    written by device kernels; user residuals and periodic grids the colouring does not fit are
+    probed with unit vectors, as the reference does.  transpose(J) gives the transpose.  The entries
+    are the exact tangent's (Enzyme's mul! in the reference) whatever J's jv mode.
+    coloring="dense": unit-vector probing through mul_ from the host (an independent cross-check)."""
     import numpy as np
     import scipy.sparse as sp
 
@@ -167,58 +172,43 @@ def collect(J, *, coloring: str | None = None):
     grid = Jo.u.grid
     if Jo.u.ctx.nranks > 1:
         raise NotImplementedError("collect(J) of a distributed operator: gather the slabs first")
-    user = getattr(Jo.f, "kind", 0) >= _lib.NK_USER1D
-    coloring = coloring or ("dense" if user else "stencil")
     n = grid.n
-    periodic = Jo.problem().bc == _lib.NK_BC_PERIODIC
-    nx, ny, nz = grid.nxyz
-    idx = np.arange(n)
-    i, j, k = idx % nx, (idx // nx) % ny, idx // (nx * ny)
-    offs = [(0, 0, 0), (1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)][: 2 * grid.dim + 1]
-    nbr = []  # (rows, columns) of each stencil offset; bc_periodic! wraps the neighbour index
-    for di, dj, dk in offs:
-        ii, jj, kk = i + di, j + dj, k + dk
-        if periodic:
-            ii, jj, kk = ii % nx, jj % ny, kk % nz
-        ok = (ii >= 0) & (ii < nx) & (jj >= 0) & (jj < ny) & (kk >= 0) & (kk < nz)
-        nbr.append((idx[ok], ((kk * ny + jj) * nx + ii)[ok]))
-    if coloring == "stencil" and periodic:
-        # the colouring stays distance-2 across the wrap only for extents the colour period divides
-        color_chk = _stencil_colors(grid)[0].reshape(-1)
-        seen = np.stack([color_chk[((k + dk) % nz * ny + (j + dj) % ny) * nx + (i + di) % nx] for di, dj, dk in offs])
-        if any(len(set(col)) != len(offs) for col in seen.T):
-            if n > 4096:
-                raise ValueError("collect(J) with bc_periodic!: the stencil colouring needs extents divisible by "
-                                 f"{2 * grid.dim + 1}; this grid has {n} points (too many for unit probing)")
-            coloring = "dense"
-    out = Jo.u.zero()
     if coloring == "dense":
         if n > 4096:
-            raise ValueError(f"dense collect(J) probes n = {n} unit vectors; use coloring='stencil'")
+            raise ValueError(f"dense collect(J) probes n = {n} unit vectors from the host; use the default")
+        Jx = JacobianOperator(Jo.f, Jo.res, Jo.u, Jo.p, jv="exact")
+        Jp = TransposeOperator(Jx) if transposed else Jx
+        out = Jo.u.zero()
         cols = []
         e = np.zeros(n)
         for j in range(n):
             e[j] = 1.0
-            mul_(out, J, DeviceArray.from_numpy(e.reshape(grid.np_shape), grid, Jo.u.ctx))
+            mul_(out, Jp, DeviceArray.from_numpy(e.reshape(grid.np_shape), grid, Jo.u.ctx))
             e[j] = 0.0
             cols.append(sp.csc_matrix(out.to_numpy().reshape(n, 1)))
         return sp.hstack(cols, format="csc")
-    if coloring != "stencil":
-        raise ValueError("coloring must be 'stencil' or 'dense'")
-    color, ncol = _stencil_colors(grid)
-    color = color.reshape(-1)
-    rows, cols, vals = [], [], []
-    probes = []
-    for c in range(ncol):
-        v = DeviceArray.from_numpy((color == c).astype(np.float64).reshape(grid.np_shape), grid, Jo.u.ctx)
-        mul_(out, J, v)
-        probes.append(out.to_numpy().reshape(-1))
-    for p_ok, q_ok in nbr:  # entry (row p, column q = p + offset) sits in the probe of q's colour
-        rows.append(p_ok)
-        cols.append(q_ok)
-        vals.append(np.array([probes[c][r] for c, r in zip(color[q_ok], p_ok)]) if len(p_ok) else np.zeros(0))
-    M = sp.csc_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))), shape=(n, n))
-    return M
+    if coloring not in (None, "stencil"):
+        raise ValueError("coloring must be 'stencil' (default) or 'dense'")
+    prob = Jo.problem()
+    user = getattr(Jo.f, "kind", 0) >= _lib.NK_USER1D
+    # (2 dim + 1) n bounds a stencil's entries; a user residual's coupling is unknown: retry with nnz
+    cap = (2 * grid.dim + 1) * n if not user else min(n * n, 64 * n)
+    colptr = np.zeros(n + 1, dtype=np.int64)
+    P64 = C.POINTER(C.c_int64)
+    nnz = C.c_int64(0)
+    for _ in range(2):
+        rowval = np.zeros(cap, dtype=np.int64)
+        nzval = np.zeros(cap, dtype=np.float64)
+        rc = load().nk_jacobian_collect(Jo.u.ctx.handle, C.byref(prob), Jo.u.ptr, int(transposed),
+                                        colptr.ctypes.data_as(P64), rowval.ctypes.data_as(P64),
+                                        nzval.ctypes.data_as(C.POINTER(C.c_double)), cap, C.byref(nnz))
+        if rc == _lib.NK_E_ARG and nnz.value > cap:
+            cap = nnz.value
+            continue
+        Jo.u.ctx.check(rc, "collect(J)")
+        break
+    m = nnz.value
+    return sp.csc_matrix((nzval[:m].copy(), rowval[:m].copy(), colptr), shape=(n, n))
 
 
 # ----------------------------------------------------------------------------- Newton-Krylov

@@ -9,8 +9,8 @@
 # is what the test-suite exercises.
 module AriadneHIP
 
-using Ariadne, Krylov, LinearAlgebra
-import LinearAlgebra: mul!, norm
+using Ariadne, Krylov, LinearAlgebra, SparseArrays
+import LinearAlgebra: mul!, norm, Adjoint, Transpose
 import Krylov: kdot, knorm, kscal!, kaxpy!, kaxpby!, kcopy!, kfill!, kdivcopy!, kref!
 
 const libnkhip = joinpath(@__DIR__, "..", "lib", "libnkhip.so")
@@ -138,25 +138,39 @@ kref!(n::Integer, x::HipVector, y::HipVector, c::Float64, s::Float64) =
                  x.ctx.ptr, n, x.ptr, y.ptr, c, s), x.ctx, "kref!"); (x, y))
 
 # --------------------------------------------------------------------------- residuals (F!) and mul!
-"""A residual `F!(res, u, p)` with a hand-written HIP stencil (same `p` tuples as the examples)."""
+"""A residual `F!(res, u, p)` with a hand-written HIP stencil (same `p` tuples as the examples).
+`jv` picks the operator behind `mul!`: NK_JV_EXACT (Enzyme parity, default) or NK_JV_FD (the
+north-star FD quotient); `α` is G_Midpoint!'s keyword (implicit.jl:17, default 0.5)."""
 struct HipResidual{K}
-    jv::Int32   # NK_JV_EXACT (Enzyme parity, default) or NK_JV_FD (north-star FD operator)
+    jv::Int32
+    α::Float64
 end
-HipResidual{K}() where {K} = HipResidual{K}(NK_JV_EXACT)
+HipResidual{K}(; jv::Integer = NK_JV_EXACT, α::Real = 0.5) where {K} = HipResidual{K}(Int32(jv), Float64(α))
 const bratu! = HipResidual{:bratu1d}()        # examples/bratu.jl:14-24, p = (Δx, λ)
 const bratu2d! = HipResidual{:bratu2d}()      # p = (Δx, Δy, λ)
-const heat2d_euler! = HipResidual{:heat2d}()  # G_Euler! ∘ diffusion!, p = (uₙ, Δt, du, (a, Δx, Δy, bc!), t)
-const heat2d_midpoint! = HipResidual{:heat2d_midpoint}()    # G_Midpoint! ∘ diffusion! (α = 0.5), implicit.jl:17-25
-const heat2d_trapezoid! = HipResidual{:heat2d_trapezoid}()  # G_Trapezoid! ∘ diffusion!, implicit.jl:29-37
+# G ∘ diffusion! (implicit.jl:8-37 ∘ heat_2D.jl:45-62), p = (uₙ, Δt, du, (a, Δx, Δy, bc!), t); 3D: (a, Δx, Δy, Δz, bc!)
+const heat2d_euler! = HipResidual{:heat2d}()
+const heat2d_midpoint! = HipResidual{:heat2d_midpoint}()    # α = 0.5; HipResidual{:heat2d_midpoint}(α = 0.3)
+const heat2d_trapezoid! = HipResidual{:heat2d_trapezoid}()
+const heat3d_euler! = HipResidual{:heat3d}()
+const heat3d_midpoint! = HipResidual{:heat3d_midpoint}()
+const heat3d_trapezoid! = HipResidual{:heat3d_trapezoid}()
 
 # bc_zero! / bc_periodic! of examples/heat_2D.jl:15-38, recognised by name
 bccode(bc) = nameof(bc) === :bc_periodic! ? NK_BC_PERIODIC : NK_BC_ZERO
-const HEAT_KINDS = (heat2d = NK_HEAT2D_EULER, heat2d_midpoint = NK_HEAT2D_MIDPOINT, heat2d_trapezoid = NK_HEAT2D_TRAPEZOID)
+const HEAT_KINDS = (heat2d = NK_HEAT2D_EULER, heat2d_midpoint = NK_HEAT2D_MIDPOINT, heat2d_trapezoid = NK_HEAT2D_TRAPEZOID,
+                    heat3d = NK_HEAT3D_EULER, heat3d_midpoint = NK_HEAT3D_MIDPOINT, heat3d_trapezoid = NK_HEAT3D_TRAPEZOID)
 
-problem(::HipResidual{:bratu1d}, u::HipVector, (dx, λ)) = NkProblem(NK_BRATU1D, 0, u.grid..., dx, 1, 1, λ, 0, 0, C_NULL, C_NULL, 0.5)
-problem(::HipResidual{:bratu2d}, u::HipVector, (dx, dy, λ)) = NkProblem(NK_BRATU2D, 0, u.grid..., dx, dy, 1, λ, 0, 0, C_NULL, C_NULL, 0.5)
-problem(::HipResidual{K}, u::HipVector, (un, Δt, _, (a, dx, dy, bc), _t)) where {K} =
-    NkProblem(HEAT_KINDS[K], bccode(bc), u.grid..., dx, dy, 1, 0, a, Δt, un.ptr, C_NULL, 0.5)
+problem(F::HipResidual{:bratu1d}, u::HipVector, (dx, λ)) = NkProblem(NK_BRATU1D, 0, u.grid..., dx, 1, 1, λ, 0, 0, C_NULL, C_NULL, F.α)
+problem(F::HipResidual{:bratu2d}, u::HipVector, (dx, dy, λ)) = NkProblem(NK_BRATU2D, 0, u.grid..., dx, dy, 1, λ, 0, 0, C_NULL, C_NULL, F.α)
+function problem(F::HipResidual{K}, u::HipVector, (un, Δt, _, fp, _t)) where {K}
+    kind = HEAT_KINDS[K]
+    three = kind in (NK_HEAT3D_EULER, NK_HEAT3D_MIDPOINT, NK_HEAT3D_TRAPEZOID)
+    (three ? length(fp) == 5 : length(fp) == 4) || error("$(K): p[4] must be (a, Δx, Δy$(three ? ", Δz" : ""), bc!)")
+    a, dx, dy = fp[1], fp[2], fp[3]
+    dz = three ? fp[4] : 1.0
+    return NkProblem(kind, bccode(fp[end]), u.grid..., dx, dy, dz, 0, a, Δt, un.ptr, C_NULL, F.α)
+end
 
 # --------------------------------------------------------------------------- user residuals (NK_USER*)
 # Any F!(res, u, p) the caller evaluates on the device (e.g. an AMDGPU.jl / KernelAbstractions
@@ -204,11 +218,80 @@ function (F::HipResidual)(res::HipVector, u::HipVector, p)
 end
 
 # mul!(out, J, v): more specific than Ariadne's Enzyme method (src/Ariadne.jl:48) by dispatch
-function mul!(out::HipVector, J::Ariadne.JacobianOperator{<:AnyHipResidual, <:HipVector}, v::HipVector)
-    F0 = J.f.jv == NK_JV_FD ? J.res.ptr : Ptr{Float64}(C_NULL)
+const HipJacobian = Ariadne.JacobianOperator{<:AnyHipResidual, <:HipVector}
+const HipJacobianT = Union{Adjoint{<:Any, <:HipJacobian}, Transpose{<:Any, <:HipJacobian}}
+jvmode(J) = J.f.jv  # NK_JV_EXACT or NK_JV_FD (HipResidual and HipUserResidual both carry it)
+function mul!(out::HipVector, J::HipJacobian, v::HipVector)
+    F0 = jvmode(J) == NK_JV_FD ? J.res.ptr : Ptr{Float64}(C_NULL)
     check(ccall((:nk_jv, libnkhip), Cint, (VP, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int32, Float64),
-                out.ctx.ptr, problem(J.f, J.u, J.p), out.ptr, J.u.ptr, v.ptr, F0, J.f.jv, 0.0), out.ctx, "mul!")
+                out.ctx.ptr, problem(J.f, J.u, J.p), out.ptr, J.u.ptr, v.ptr, F0, jvmode(J), 0.0), out.ctx, "mul!")
     return nothing
+end
+
+# mul!(out, transpose(J), v) / adjoint (src/Ariadne.jl:87-107, Enzyme reverse mode): J(u)ᵀ v
+function mul!(out::HipVector, J′::HipJacobianT, v::HipVector)
+    J = parent(J′)
+    check(ccall((:nk_jtv, libnkhip), Cint, (VP, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                out.ctx.ptr, problem(J.f, J.u, J.p), out.ptr, J.u.ptr, v.ptr), out.ctx, "mul!(out, Jᵀ, v)")
+    return nothing
+end
+
+"""k grid functions as the columns of an n × k matrix: the `Out` / `V` of the batched
+mul!(Out::AbstractMatrix, J, V) (src/Ariadne.jl:67-84, :109-138)."""
+struct HipMatrix <: AbstractMatrix{Float64}
+    cols::Vector{HipVector}
+end
+HipMatrix(ctx::HipContext, grid::NTuple{3, Int}, k::Integer) = HipMatrix([HipVector(ctx, grid) for _ in 1:k])
+Base.size(M::HipMatrix) = (length(first(M.cols)), length(M.cols))
+Base.getindex(::HipMatrix, ::Int, ::Int) = error("scalar indexing of a HipMatrix; copy a column with Array(M.cols[j])")
+colptrs(M::HipMatrix) = [c.ptr for c in M.cols]
+
+# one fused launch per 8 columns: u, F(u) read once for all of them (nk_jv_batched)
+function mul!(Out::HipMatrix, J::HipJacobian, V::HipMatrix)
+    @assert size(Out, 2) == size(V, 2)
+    F0 = jvmode(J) == NK_JV_FD ? J.res.ptr : Ptr{Float64}(C_NULL)
+    o, v = colptrs(Out), colptrs(V)
+    GC.@preserve Out V o v begin
+        check(ccall((:nk_jv_batched, libnkhip), Cint,
+                    (VP, Ref{NkProblem}, Int32, Ptr{Ptr{Float64}}, Ptr{Float64}, Ptr{Ptr{Float64}}, Ptr{Float64}, Int32, Float64),
+                    J.u.ctx.ptr, problem(J.f, J.u, J.p), length(o), o, J.u.ptr, v, F0, jvmode(J), 0.0), J.u.ctx, "mul!(Out, J, V)")
+    end
+    return nothing
+end
+function mul!(Out::HipMatrix, J′::HipJacobianT, V::HipMatrix)
+    J = parent(J′)
+    @assert size(Out, 2) == size(V, 2)
+    o, v = colptrs(Out), colptrs(V)
+    GC.@preserve Out V o v begin
+        check(ccall((:nk_jtv_batched, libnkhip), Cint,
+                    (VP, Ref{NkProblem}, Int32, Ptr{Ptr{Float64}}, Ptr{Float64}, Ptr{Ptr{Float64}}),
+                    J.u.ctx.ptr, problem(J.f, J.u, J.p), length(o), o, J.u.ptr, v), J.u.ctx, "mul!(Out, Jᵀ, V)")
+    end
+    return nothing
+end
+
+# collect(J) (src/Ariadne.jl:140-162): the exact Jacobian as a SparseMatrixCSC, assembled on the device
+function Base.collect(JOp::Union{HipJacobian, HipJacobianT})
+    J = JOp isa HipJacobian ? JOp : parent(JOp)
+    n = length(J.u)
+    dim = J.u.grid[3] > 1 ? 3 : (J.u.grid[2] > 1 ? 2 : 1)
+    cap = J.f isa HipUserResidual ? min(n * n, 64 * n) : (2 * dim + 1) * n
+    colptr = Vector{Int64}(undef, n + 1)
+    nnz = Ref{Int64}(0)
+    for attempt in 1:2
+        rowval = Vector{Int64}(undef, cap)
+        nzval = Vector{Float64}(undef, cap)
+        rc = ccall((:nk_jacobian_collect, libnkhip), Cint,
+                   (VP, Ref{NkProblem}, Ptr{Float64}, Int32, Ptr{Int64}, Ptr{Int64}, Ptr{Float64}, Int64, Ref{Int64}),
+                   J.u.ctx.ptr, problem(J.f, J.u, J.p), J.u.ptr, JOp isa HipJacobian ? 0 : 1, colptr, rowval, nzval, cap, nnz)
+        if rc == -2 && nnz[] > cap && attempt == 1
+            cap = nnz[]
+            continue
+        end
+        check(rc, J.u.ctx, "collect(J)")
+        m = nnz[]
+        return SparseMatrixCSC(n, n, colptr .+ 1, rowval[1:m] .+ 1, nzval[1:m])
+    end
 end
 
 # --------------------------------------------------------------------------- optional: device-resident Krylov solve
@@ -305,23 +388,28 @@ function Krylov.krylov_workspace(method::Symbol, kc::KrylovConstructor{<:HipVect
     return ws
 end
 
-function Krylov.krylov_solve!(ws::HipKrylovWorkspace, J::Ariadne.JacobianOperator{<:AnyHipResidual, <:HipVector}, b::HipVector;
+function Krylov.krylov_solve!(ws::HipKrylovWorkspace, J::HipJacobian, b::HipVector;
                               restart::Bool = false, reorthogonalization::Bool = false, itmax::Integer = 0,
                               atol::Real = sqrt(eps(Float64)), rtol::Real = sqrt(eps(Float64)),
-                              N = nothing, ldiv::Bool = false, kwargs...)
+                              M = nothing, N = nothing, ldiv::Bool = false, kwargs...)
+    # Ariadne forwards M = M(J) when the caller gives one (src/Ariadne.jl:327-329): the device GMRES has
+    # no left preconditioner, so refuse it instead of silently solving without it
+    M === nothing || error("AriadneHIP: a left preconditioner M is not supported by the device GMRES (use N)")
+    isempty(kwargs) || error("AriadneHIP: unsupported Krylov keyword(s) $(join(keys(kwargs), ", "))")
     ldiv && !(N isa HipDiagPreconditioner && N.kind == NK_PRECOND_ILU0) &&
         error("ldiv = true: the HIP path takes factorisations (hip_ilu0) for N")
-    Nc = N === nothing ? nothing : Ref(nkprecond(N))
-    opts = NkKrylovOpts(restart, reorthogonalization, itmax, J.f.jv, atol, rtol, 0.0, 0.0, C_NULL,
-                        Nc === nothing ? C_NULL : Ptr{Cvoid}(Base.unsafe_convert(Ptr{NkPrecond}, Nc)))
+    Nc = Ref(N === nothing ? NkPrecond(0, C_NULL, C_NULL, C_NULL, C_NULL, 0) : nkprecond(N))
     st = Ref{NkKrylovStats}()
     hl = Ref{Int64}(0)
-    F0 = J.f.jv == NK_JV_FD ? J.res.ptr : Ptr{Float64}(C_NULL)
-    check(ccall((:nk_krylov_solve, libnkhip), Cint,
-                (Ptr{Cvoid}, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ref{NkKrylovOpts}, Ref{NkKrylovStats},
-                 Ptr{Float64}, Int64, Ref{Int64}),
-                ws.ptr, problem(J.f, J.u, J.p), J.u.ptr, F0, b.ptr, opts, st, C_NULL, 0, hl), ws.ctx, "krylov_solve!")
-    Nc === nothing || GC.@preserve Nc nothing
+    F0 = jvmode(J) == NK_JV_FD ? J.res.ptr : Ptr{Float64}(C_NULL)
+    GC.@preserve Nc N begin   # the raw nk_precond* (and what it points to) stay rooted through the call
+        Np = N === nothing ? Ptr{Cvoid}(C_NULL) : Ptr{Cvoid}(Base.unsafe_convert(Ptr{NkPrecond}, Nc))
+        opts = NkKrylovOpts(restart, reorthogonalization, itmax, jvmode(J), atol, rtol, 0.0, 0.0, C_NULL, Np)
+        check(ccall((:nk_krylov_solve, libnkhip), Cint,
+                    (Ptr{Cvoid}, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ref{NkKrylovOpts}, Ref{NkKrylovStats},
+                     Ptr{Float64}, Int64, Ref{Int64}),
+                    ws.ptr, problem(J.f, J.u, J.p), J.u.ptr, F0, b.ptr, opts, st, C_NULL, 0, hl), ws.ctx, "krylov_solve!")
+    end
     ws.stats.niter = st[].niter
     ws.stats.solved = st[].solved != 0
     return ws

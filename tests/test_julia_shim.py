@@ -33,3 +33,111 @@ def test_shim_struct_matches_header(jl, cstruct):
     got = jl_fields(jl)
     want = [("lambda" if f == "lam" else f, C.sizeof(t)) for f, t in cstruct._fields_]
     assert got == want
+
+
+# ---------------------------------------------------------------------------------------------------
+# Every `ccall((:nk_*, libnkhip), Ret, (Args...), ...)` in the shim against the prototype in nkhip.h:
+# the symbol exists, the argument count matches, and each argument / the return value has the same
+# class (32-bit int, 64-bit int, double, pointer).  A wrong width here would corrupt the call.
+HEADER = os.path.join(os.path.dirname(_lib.PKG_DIR), "include", "nkhip.h")
+
+
+def _split_top(s):
+    out, depth, cur = [], 0, ""
+    for ch in s:
+        if ch in "({[":
+            depth += 1
+        elif ch in ")}]":
+            depth -= 1
+        if ch == "," and depth == 0:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        out.append(cur.strip())
+    return out
+
+
+def _matching(s, i):
+    """index of the parenthesis closing the one at s[i]"""
+    depth = 0
+    for j in range(i, len(s)):
+        depth += s[j] == "("
+        depth -= s[j] == ")"
+        if depth == 0:
+            return j
+    raise ValueError("unbalanced")
+
+
+JL_CLASS = {"Cint": "i32", "Int32": "i32", "Int64": "i64", "Float64": "f64", "Cdouble": "f64", "VP": "ptr",
+            "Cstring": "ptr"}
+
+
+def jl_class(t):
+    t = t.strip()
+    if t.startswith(("Ptr{", "Ref{")) or t == "Ptr":
+        return "ptr"
+    return JL_CLASS[t]
+
+
+def c_class(decl):
+    d = decl.strip()
+    if "*" in d or "[" in d:
+        return "ptr"
+    d = d.replace("const", "").strip()
+    typ = d.rsplit(None, 1)[0] if len(d.split()) > 1 else d
+    return {"int": "i32", "int32_t": "i32", "int64_t": "i64", "double": "f64"}[typ]
+
+
+def header_prototypes():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", " ", src, flags=re.S)
+    protos = {}
+    for m in re.finditer(r"([\w\s\*]+?)\b(nk_\w+)\s*\(([^;{]*?)\)\s*;", src):
+        ret, name, args = m.group(1), m.group(2), m.group(3)
+        if "typedef" in ret or "(*" in m.group(0):
+            continue
+        params = [] if args.strip() in ("", "void") else _split_top(args)
+        protos[name] = (c_class(ret.strip() + " x"), [c_class(p) for p in params])
+    return protos
+
+
+def shim_ccalls():
+    src = open(SHIM).read()
+    calls = []
+    for m in re.finditer(r"ccall\(\(:(nk_\w+),\s*libnkhip\),", src):
+        rest = src[m.end():]
+        ret_end = rest.index(",")
+        ret = rest[:ret_end].strip()
+        i = rest.index("(", ret_end)
+        j = _matching(rest, i)
+        calls.append((m.group(1), ret, _split_top(rest[i + 1:j])))
+    return calls
+
+
+def test_shim_ccalls_match_header():
+    protos = header_prototypes()
+    calls = shim_ccalls()
+    assert len(calls) >= 30
+    for name, ret, args in calls:
+        assert name in protos, f"{name} is not declared in nkhip.h"
+        cret, cargs = protos[name]
+        got = [jl_class(a) for a in args]
+        assert len(got) == len(cargs), f"{name}: {len(got)} ccall arguments, header has {len(cargs)}"
+        assert got == cargs, f"{name}: argument classes {got} != header {cargs}"
+        assert jl_class(ret) == cret, f"{name}: return {ret} vs header class {cret}"
+
+
+def test_shim_binds_the_reference_operator_surface():
+    """The shim's entry points for src/Ariadne.jl:48-162: mul! on J, transpose(J), the batched forms,
+    collect(J) -- and the left preconditioner M is refused, not dropped (:327-329)."""
+    names = {c[0] for c in shim_ccalls()}
+    for sym in ("nk_jv", "nk_jtv", "nk_jv_batched", "nk_jtv_batched", "nk_jacobian_collect", "nk_krylov_solve"):
+        assert sym in names
+    src = open(SHIM).read()
+    assert "M === nothing || error(" in src
+    assert "isempty(kwargs) || error(" in src
+    assert re.search(r"GC\.@preserve Nc N begin.*?ccall\(\(:nk_krylov_solve", src, re.S)
+    for k in ("heat3d", "heat3d_midpoint", "heat3d_trapezoid"):
+        assert f"{k} = NK_HEAT3D" in src
