@@ -79,12 +79,21 @@ def parse():
     ap.add_argument("--global-n", type=int, default=0,
                     help="strong scaling: one global N^dim problem in slabs over the GPUs (--gpus 8 --global-n "
                          "16384 is BASELINE config 4; --workload heat3d --gpus 8 --global-n 512 is config 5)")
+    ap.add_argument("--slab-of", type=int, default=0,
+                    help="with --global-n on ONE GPU: run the slab one rank of a --slab-of-way decomposition owns "
+                         "(rank slab_of // 2, ghost planes zero, no exchange) -- the per-GPU compute of configs 4 / 5 "
+                         "before an 8-GPU node is available (--global-n 16384 --slab-of 8)")
     ap.add_argument("--memory", type=int, default=0, help="Krylov memory (default 30 for bratu2d, 20 for heat)")
     ap.add_argument("--itmax", type=int, default=300)
     ap.add_argument("--jv", choices=["fd", "exact"], default="fd")
+    ap.add_argument("--reorth", choices=["auto", "on", "off"], default="auto",
+                    help="GMRES reorthogonalization; auto = the reference's own run conditions: on for the heat "
+                         "workloads (heat_2D.jl:131 solves with reorthogonalization = true), off for Bratu")
     ap.add_argument("--no-prof", action="store_true", help="do not time kernels with HIP events")
-    ap.add_argument("--prof-every", type=int, default=64,
-                    help="time every k-th launch of each kernel class (HIP events; k > 1 keeps their cost out)")
+    ap.add_argument("--prof-every", type=int, default=0,
+                    help="time every k-th launch of each kernel class (HIP events; k > 1 keeps their cost out); "
+                         "0 = 64 for bratu2d (~6000 launches per class), 1 for the heat workloads (11 matvecs per "
+                         "step: every launch timed, so each class has >= 10 timed launches)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--transport", choices=["rccl", "mailbox"], default="rccl",
                     help="N > 1: rccl = nk_dist_init (RCCL bootstrap; peer mailbox + IPC ghost planes when available); "
@@ -97,7 +106,8 @@ def parse():
                          "mask; the machine's nproc is reported beside it")
     ap.add_argument("--traffic-json", default="",
                     help="per-kernel HBM traffic from separate rocprofv3 --pmc passes (tools/pmc_traffic.py); "
-                         "default profiles/r01/pmc_traffic_<workload>.json when present")
+                         "default profiles/<latest round>/pmc_traffic_<workload>_<side>.json when present (a file "
+                         "of another size is never applied)")
     ap.add_argument("--launch-probe", type=int, default=-1, help=argparse.SUPPRESS)  # CPU test of the launcher
     return ap.parse_args()
 
@@ -128,11 +138,14 @@ class Bratu2D:
     """BASELINE config 2: one inexact-Newton step of 2D Bratu with GMRES(30) and a fixed Krylov budget."""
 
     def __init__(self, args, ctx, rank, world):
+        parts = args.slab_of or world
+        if args.slab_of:  # one rank's slab of a parts-way decomposition, alone on this GPU
+            rank = parts // 2
         if args.global_n:  # strong scaling: one global G x G problem, G / world rows per rank
             G = args.global_n
-            if G % world:
-                raise SystemExit(f"--global-n {G} must be divisible by the number of GPUs {world}")
-            n, ny_glob, rows = G, G, G // world
+            if G % parts:
+                raise SystemExit(f"--global-n {G} must be divisible by the number of slabs {parts}")
+            n, ny_glob, rows = G, G, G // parts
         else:  # weak scaling: an n x n slab per rank
             n = args.n or 4096
             ny_glob, rows = n * world, n
@@ -147,14 +160,18 @@ class Bratu2D:
         self.res = self.u.zero()
         self.ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(self.res, memory=args.memory))
         self.p = (self.hx, self.hy, LAMBDA)
-        self.kw = dict(restart=True, rtol=0.0, atol=0.0, itmax=args.itmax)
+        self.kw = dict(restart=True, rtol=0.0, atol=0.0, itmax=args.itmax, reorthogonalization=args.reorth == "on")
         self.args = args
         self.jv_kernel = "jv_fd_dot_norm" if args.jv == "fd" else "jv_exact_dot_norm"
         self.scaling = "strong" if args.global_n else "weak"
         self.units_per_matvec = 1 if args.global_n else world  # matvecs counted over the whole problem
+        slab = (f"; rank {rank}'s slab of the {parts}-way split ALONE on one GPU (ghost planes zero, no exchange): "
+                f"value = slab matvecs/s = the global matvec rate {parts} GPUs would reach without exchange cost"
+                if args.slab_of else "")
         self.workload = (f"2D Bratu {n}x{ny_glob} ({n}x{rows} per GPU), one inexact-Newton step per step: "
-                         f"GMRES({args.memory}) restart, itmax={args.itmax}, rtol=atol=0, {args.jv.upper()} Jv")
+                         f"GMRES({args.memory}) restart, itmax={args.itmax}, rtol=atol=0, {args.jv.upper()} Jv{slab}")
         self.metric = f"Krylov matvecs/sec + achieved HBM GB/s, 2D Bratu {n}^2"
+        self.side = f"{n}x{rows}" if rows != n else str(n)
 
     def step(self):
         _, r = ah.newton_krylov_(ah.bratu2d_, self.u, self.p, self.res, max_niter=0, tol_rel=0.0, tol_abs=0.0,
@@ -171,7 +188,8 @@ class Bratu2D:
         F0 = oc.residual(P, u0)
         t0 = time.perf_counter()
         x, st, _ = oc.krylov_solve(P, u0, F0, jv=self.args.jv, F0=F0, memory=self.args.memory, restart=True,
-                                   itmax=self.args.cpu_itmax, atol=0.0, rtol=0.0, history=False)
+                                   itmax=self.args.cpu_itmax, atol=0.0, rtol=0.0, history=False,
+                                   reorthogonalization=self.args.reorth == "on")
         dt = time.perf_counter() - t0
         self.x_cpu = x
         return dict(value=st["n_matvec"] / dt, unit="matvecs/s", cores=oc.get_threads(), kind="port",
@@ -189,7 +207,8 @@ class Bratu2D:
         ah.bratu2d_(res, u, self.p)
         J = ah.JacobianOperator(ah.bratu2d_, res, u, self.p, jv=self.args.jv)
         ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=self.args.memory))
-        ah.krylov_solve_(ws, J, res, restart=True, itmax=self.args.cpu_itmax, atol=0.0, rtol=0.0)
+        ah.krylov_solve_(ws, J, res, restart=True, itmax=self.args.cpu_itmax, atol=0.0, rtol=0.0,
+                         reorthogonalization=self.args.reorth == "on")
         x = ws.x.to_numpy()
         ah.kaxpy_(len(u), -1.0, ws.x, u)  # u .-= d (src/Ariadne.jl:344)
         ah.bratu2d_(res, u, self.p)
@@ -214,11 +233,14 @@ class HeatEuler:
     --scheme / --bc: the same loop with G_Midpoint! / G_Trapezoid! and bc_periodic!."""
 
     def __init__(self, args, ctx, rank, world, dim):
+        parts = args.slab_of or world
+        if args.slab_of:
+            rank = parts // 2
         if args.global_n:  # strong scaling: one global G^dim problem, G / world slab planes per rank
             n = args.global_n
-            if n % world:
-                raise SystemExit(f"--global-n {n} must be divisible by the number of GPUs {world}")
-            planes = n // world
+            if n % parts:
+                raise SystemExit(f"--global-n {n} must be divisible by the number of slabs {parts}")
+            planes = n // parts
             glob = (n,) * dim
         else:  # weak scaling: an n^dim block per rank
             n = args.n or (8192 if dim == 2 else 512)
@@ -250,6 +272,7 @@ class HeatEuler:
         self.u = self.un.copy()
         self.res = self.u.zero()
         self.ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(self.res, memory=args.memory or 20))
+        self.reorth = args.reorth != "off"  # heat_2D.jl:131: krylov_kwargs = (; reorthogonalization = true)
         G = {"euler": ah.G_Euler_, "midpoint": ah.G_Midpoint_, "trapezoid": ah.G_Trapezoid_}[args.scheme]
         self.F = G.bind(ah.diffusion_ if dim == 2 else ah.diffusion3d_)
         bc = ah.bc_periodic_ if args.bc == "periodic" else ah.bc_zero_
@@ -260,14 +283,19 @@ class HeatEuler:
         per_gpu = f"{n}^{dim - 1}x{planes} slab per GPU" if args.global_n else f"{n}^{dim} per GPU"
         sname = {"euler": "implicit Euler", "midpoint": "implicit midpoint", "trapezoid": "implicit trapezoid"}[args.scheme]
         bcname = "" if args.bc == "zero" else ", bc_periodic!"
+        slab = (f"; rank {rank}'s slab of the {parts}-way split ALONE on one GPU (ghost planes zero, no exchange)"
+                if args.slab_of else "")
         self.workload = (f"{dim}D heat {sname}{bcname} {shape} ({per_gpu}), one time step per step: "
-                         f"newton_krylov! tol_abs=6e-6, GMRES memory {args.memory or 20} (unrestarted), "
-                         f"{args.jv.upper()} Jv, IC sin*sin + 0.1 U(-1,1)")
+                         f"newton_krylov! tol_abs=6e-6, GMRES memory {args.memory or 20} (unrestarted, "
+                         f"reorthogonalization={'true' if self.reorth else 'false'}), "
+                         f"{args.jv.upper()} Jv, IC sin*sin + 0.1 U(-1,1){slab}")
+        self.side = str(n) if planes == n else f"{n}x{planes}"
         self.metric = f"Krylov matvecs/sec + achieved HBM GB/s, {dim}D heat {sname}{bcname} {n}^{dim}"
 
     def step(self):
         _, r = ah.newton_krylov_(self.F, self.u, self.p, self.res, tol_abs=6.0e-6, memory=self.args.memory or 20,
-                                 jv=self.args.jv, workspace=self.ws)
+                                 jv=self.args.jv, workspace=self.ws,
+                                 krylov_kwargs=dict(reorthogonalization=self.reorth))
         ah.kcopy_(len(self.un), self.un, self.u)  # uₙ .= u  (implicit.jl:75)
         return r.n_matvec, r
 
@@ -282,10 +310,11 @@ class HeatEuler:
         u0 = oc.sin_ic(P) + 0.1 * np.random.default_rng(0).uniform(-1, 1, P.shape)
         P.un = u0
         t0 = time.perf_counter()
-        _, st = oc.newton_krylov(P, u0, tol_abs=6e-6, memory=self.args.memory or 20, jv=self.args.jv)
+        _, st = oc.newton_krylov(P, u0, tol_abs=6e-6, memory=self.args.memory or 20, jv=self.args.jv,
+                                 reorthogonalization=self.reorth)
         dt = time.perf_counter() - t0
         return dict(value=st["n_matvec"] / dt, unit="matvecs/s", cores=oc.get_threads(), kind="port",
-                    sample=f"oracle/nk_oracle.c one {self.args.scheme} time step ({st['outer_iterations']} Newton, "
+                    sample=f"oracle/nk_oracle.c one {self.args.scheme} time step (reorthogonalization={self.reorth}) ({st['outer_iterations']} Newton, "
                            f"{st['n_matvec']} matvecs) of the same {self.dim}D heat problem at {m}^{self.dim} "
                            f"(noise from numpy default_rng(0)), {dt:.2f} s")
 
@@ -304,6 +333,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.slab_of and (world > 1 or not args.global_n):
+        raise SystemExit("--slab-of runs one rank's slab of a --global-n problem on ONE GPU (--gpus 1)")
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)", file=sys.stderr)
         sys.exit(2)
@@ -352,6 +383,8 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
+    if not args.prof_every:
+        args.prof_every = 64 if args.workload == "bratu2d" else 1
     if not args.no_prof:
         ctx.prof_reset()
         ctx.prof_enable(args.prof_every)
@@ -375,19 +408,34 @@ def main():
     prof = ctx.prof_read() if not args.no_prof else {}
     ctx.prof_enable(0)
 
-    # algorithmic bytes of every launch (timed launches carry bytes; scale by launches / timed)
+    # Two byte counts per kernel class (nk_prof_entry): `bytes` = the operand bytes the kernel moves
+    # through the memory hierarchy (every load / store it issues, served by L2, the Infinity Cache or
+    # HBM -- "L2 egress"), `dram` = the unique-DRAM model (each distinct operand byte once: a vector
+    # re-read by the next pass counts once; a lower bound on HBM traffic, since no gfx950 counter
+    # separates Infinity-Cache hits from DRAM reads).  Timed launches carry bytes; scale by launches.
     total_bytes = sum(v.get("bytes_all") or v["bytes"] / max(1, v["timed"]) * v["launches"] for v in prof.values())
+    total_dram = sum(v.get("dram_all") or v.get("bytes_all") or 0.0 for v in prof.values())
+
+    def dram_ratio(v):
+        return (v.get("dram_all") or 0.0) / v["bytes_all"] if v.get("bytes_all") else 1.0
+
     kernels = {k: dict(launches=v["launches"], timed=v["timed"], avg_us=1e3 * v["ms"] / max(1, v["timed"]),
                        gbs=(v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["ms"] > 0 else None,
+                       dram_gbs=(dram_ratio(v) * v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["ms"] > 0 else None,
                        share=v["ms"] / max(1, v["timed"]) * v["launches"]
                        / max(1e-30, sum(x["ms"] / max(1, x["timed"]) * x["launches"] for x in prof.values())))
                for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"] / max(1, kv[1]["timed"]) * kv[1]["launches"])}
 
     pmc = {}
+    tag = args.workload + ("" if args.scheme == "euler" else "_" + args.scheme) + ("" if args.bc == "zero" else "_periodic")
     if not args.traffic_json:
-        tag = args.workload + ("" if args.scheme == "euler" else "_" + args.scheme) + ("" if args.bc == "zero" else "_periodic")
-        args.traffic_json = os.path.join(ROOT, "profiles", "r01", f"pmc_traffic_{tag}.json")
-    if os.path.exists(args.traffic_json):
+        rounds = sorted(d for d in os.listdir(os.path.join(ROOT, "profiles")) if d.startswith("r"))
+        for rd in reversed(rounds):  # the newest PMC pass of exactly this workload and size
+            f = os.path.join(ROOT, "profiles", rd, f"pmc_traffic_{tag}_{W.side}.json")
+            if os.path.exists(f):
+                args.traffic_json = f
+                break
+    if args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             pmc = json.load(f)
 
@@ -407,11 +455,17 @@ def main():
         # timed launches are every 64th one).  PMC traffic comes from a separate run with the same
         # GMRES(30) cycle structure, so traffic / algorithmic bytes per launch is compared as a ratio.
         bpl = v.get("bytes_all", 0.0) / v["launches"] if v.get("bytes_all") else v["bytes"] / v["timed"]
+        dr = dram_ratio(v)
         # avg_us: the mean launch duration over ALL launches at the measured rate (the timed launches
         # of a kernel whose size varies per launch are not a uniform sample of the sizes);
         # avg_us_timed: the plain mean of the timed launches
         return {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4),
+                "bytes_basis": "l2_egress: every operand byte the kernel loads / stores (any cache level; "
+                               "PMC FETCH/WRITE_SIZE count the same, Infinity-Cache hits included)",
+                "dram_model": {"achieved": round(ach * dr, 1), "frac": round(ach * dr / HBM_PEAK_GBS, 4),
+                               "bytes_per_launch": bpl * dr,
+                               "basis": "unique operand bytes (re-reads counted once: a lower bound on DRAM traffic)"},
                 "traffic": round(ach * tb / bpl, 1) if tb else None,
                 "traffic_bytes_per_launch": tb,
                 "traffic_source": os.path.relpath(args.traffic_json, ROOT) if tb else None,
@@ -440,18 +494,21 @@ def main():
             "dtype": "f64",
             "data": "synthetic (see config.workload)",
             "config": {"workload": W.workload, "matvecs_per_step": matvecs // max(1, args.steps),
-                       "parallelism": f"slab{world}",
+                       "parallelism": f"slab{world}" if not args.slab_of else f"slab 1 of {args.slab_of} (one GPU)",
+                       "reorthogonalization": bool(getattr(W, "reorth", args.reorth == "on")),
                        "devices": f"{min(world, ndev)} GPU(s) for {world} rank(s)" + (" (shared: rehearsal)" if shared else ""),
                        "reductions": ("peer mailbox (IPC/xGMI)" if ctx.mailbox_active else
                                       ("ncclAllReduce" if world > 1 else "local"))},
-            "hbm_gbs_algorithmic": round(world * total_bytes / elapsed / 1e9, 1) if total_bytes else None,
+            # whole job: operand bytes through the memory hierarchy, and the unique-DRAM model, per second
+            "gbs_l2_egress_wholejob": round(world * total_bytes / elapsed / 1e9, 1) if total_bytes else None,
+            "gbs_dram_model_wholejob": round(world * total_dram / elapsed / 1e9, 1) if total_dram else None,
             "roofline": roof(dominant) if dominant else None,
             "jv_roofline": roof(jv_kernel),
             "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in list(kernels.items())[:8]},
             "newton_n_res": last.stats.n_res if last else None,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not args.global_n:
             # the CPU share this process is given: OMP_NUM_THREADS (the GPU box sets it to its per-GPU share
             # of the host, 16), else every core in the affinity mask; the machine's full count is reported too
             affinity = len(os.sched_getaffinity(0))

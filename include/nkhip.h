@@ -296,6 +296,8 @@ typedef struct nk_prof_entry {
     double total_ms;       /* sum of the timed launches' event durations                      */
     double bytes;          /* algorithmic bytes (compulsory HBM traffic) of the timed launches */
     double bytes_all;      /* algorithmic bytes of ALL launches (per-launch sizes may vary)   */
+    double dram_bytes_all; /* the unique-DRAM model of ALL launches: each distinct operand byte once
+                              (re-reads counted as Infinity-Cache hits -- a lower bound on DRAM traffic) */
 } nk_prof_entry;
 /* every = 0: off; every = k > 0: time every k-th launch of each kernel class with a pair of HIP
  * events on the context stream (k > 1 keeps the event overhead out of the timed region). */

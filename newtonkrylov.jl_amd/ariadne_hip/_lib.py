@@ -83,7 +83,7 @@ class nk_newton_stats(C.Structure):
 
 class nk_prof_entry(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("timed", C.c_int64), ("total_ms", C.c_double),
-                ("bytes", C.c_double), ("bytes_all", C.c_double)]
+                ("bytes", C.c_double), ("bytes_all", C.c_double), ("dram_bytes_all", C.c_double)]
 
 
 # name -> (restype, argtypes); mirrors include/nkhip.h one to one

@@ -455,6 +455,7 @@ int nk_prof_read(nk_ctx* c, nk_prof_entry* out, int32_t cap, int32_t* count) {
             out[m].total_ms = c->acc[k].ms;
             out[m].bytes = c->acc[k].bytes;
             out[m].bytes_all = c->acc[k].bytes_all;
+            out[m].dram_bytes_all = c->acc[k].dram_all;
         }
         ++m;
     }

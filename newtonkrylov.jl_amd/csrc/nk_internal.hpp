@@ -40,7 +40,7 @@ struct ProfPending {
 };
 struct ProfAcc {
     int64_t launches = 0, timed = 0;
-    double ms = 0.0, bytes = 0.0, bytes_all = 0.0;
+    double ms = 0.0, bytes = 0.0, bytes_all = 0.0, dram_all = 0.0;
 };
 
 struct Comm;  // RCCL state (nk_dist.cpp)
@@ -129,15 +129,18 @@ int prof_begin(nk_ctx* c, hipEvent_t* a);
 int prof_end(nk_ctx* c, int k, hipEvent_t a, double bytes);
 void prof_drain(nk_ctx* c, bool blocking);
 
-// run `launch()` (which enqueues one kernel on c->stream) under optional event timing
+// run `launch()` (which enqueues one kernel on c->stream) under optional event timing.  bytes: the
+// kernel's algorithmic operand bytes (every load / store it must issue, served by any cache level);
+// dram: the unique-DRAM model of the same launch (each distinct operand byte once; < 0: = bytes)
 template <typename F>
-int launch(nk_ctx* c, const char* name, double bytes, F&& f) {
+int launch(nk_ctx* c, const char* name, double bytes, F&& f, double dram = -1.0) {
     hipEvent_t a = nullptr;
     int k = -1;
     bool timed = false;
     if (c->prof) {
         k = kid(c, name);
         c->acc[k].bytes_all += bytes;
+        c->acc[k].dram_all += dram < 0.0 ? bytes : dram;
         timed = (c->acc[k].launches++ % c->prof_every) == 0;
         if (timed) NK_TRY(prof_begin(c, &a));
     }

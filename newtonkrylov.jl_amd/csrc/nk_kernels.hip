@@ -808,9 +808,10 @@ int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const dou
     int fin;
     double* part = red_out(c, g, out, &fin);
     if (vnext)
+        // unique-DRAM model: V_{i+1} is the next pass's V_i (counted there), so q in + q out + V_i
         return launch(c, "mgs_pass", 32.0 * n, [&] {
             mgs_dispatch<true>(variant, g, c->stream, n, q, vi, vnext, in.ptr, in.len, h_out, h_host, part, rev, fin);
-        });
+        }, 24.0 * n);
     return launch(c, "mgs_pass_last", 24.0 * n, [&] {
         mgs_dispatch<false>(variant, g, c->stream, n, q, vi, vnext, in.ptr, in.len, h_out, h_host, part, rev, fin);
     });

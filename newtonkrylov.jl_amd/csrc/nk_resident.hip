@@ -548,6 +548,10 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
     const double f = std::min(1.0, (double)c->res_blocks * (rv + A.rl) * kResThreads / (double)(n >> 1));
     const double per_res = (jin ? 5.0 : 2.0) + 2.0 * np - 1.0, per_str = 4.0 * np - 1.0;  // doubles per point
     const double bytes = 8.0 * (double)n * (f * per_res + (1.0 - f) * per_str);
+    // unique-DRAM model: V_{i+1}, read again as the next pass's V_i, counted once (the Infinity Cache
+    // serves the second read at best): np + 2 doubles per resident point (q in, V_1..V_np, q / V_{k+1}
+    // out), 3 np for a streamed point (q read and written every pass, each V once)
+    const double dram = 8.0 * (double)n * (f * ((jin ? 5.0 : 2.0) + np) + (1.0 - f) * (3.0 * np));
     return launch(c, jin ? "arnoldi_step" : "mgs_sweep", bytes, [&] {
         const dim3 g(c->res_blocks), b(kResThreads);
         switch (rv) {
@@ -570,7 +574,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
             break;
         default: hipLaunchKernelGGL(k_mgs_res<32>, g, b, lds, c->stream, A); break;
         }
-    });
+    }, dram);
 }
 
 }  // namespace nk
