@@ -311,6 +311,59 @@ struct UpdArgs {
 
 // xr = Σ y_i V_i (the kaxpy! chain of gmres!, from xr = 0); on the last chunk x = x + xr
 // (restart) or x = xr; optional partials of ||x||^2.  16-B accesses; V loads non-temporal.
+// U elements (16 B each) per thread and iteration, all their loads issued before any store: with
+// the few streams of a short solve (k = 1..3 in the heat time steps) one element per thread leaves
+// too few bytes in flight per CU.
+template <int U>
+__device__ __forceinline__ void update_elems(const UpdArgs& A, const double* yv, int64_t i, double& acc) {
+    dx2 t[U];
+#pragma unroll
+    for (int e = 0; e < U; ++e) t[e] = A.first ? dx2{0.0, 0.0} : reinterpret_cast<const dx2*>(A.xr)[i + e * kBlock];
+    dx2 x0[U], uv[U];
+    if (A.last) {
+#pragma unroll
+        for (int e = 0; e < U; ++e) {
+            if (A.restart) x0[e] = reinterpret_cast<const dx2*>(A.x)[i + e * kBlock];
+            if (A.u) uv[e] = reinterpret_cast<const dx2*>(A.u)[i + e * kBlock];
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < kMaxUpdateVecs; ++m)  // compile-time indices keep yv in registers
+        if (m < A.k) {
+            dx2 v[U];
+#pragma unroll
+            for (int e = 0; e < U; ++e) v[e] = __builtin_nontemporal_load(reinterpret_cast<const dx2*>(A.V[m]) + i + e * kBlock);
+#pragma unroll
+            for (int e = 0; e < U; ++e) {
+                t[e].x = fma(yv[m], v[e].x, t[e].x);
+                t[e].y = fma(yv[m], v[e].y, t[e].y);
+            }
+        }
+#pragma unroll
+    for (int e = 0; e < U; ++e) {
+        if (A.last) {
+            dx2 xv = t[e];
+            if (A.restart) {
+                xv.x = fma(1.0, t[e].x, x0[e].x);
+                xv.y = fma(1.0, t[e].y, x0[e].y);
+            }
+            if (A.u) {  // u .-= 1 .* d, exactly kaxpy!(n, -1, x, u) on the x that would have been stored
+                uv[e].x = fma(-1.0, xv.x, uv[e].x);
+                uv[e].y = fma(-1.0, xv.y, uv[e].y);
+                reinterpret_cast<dx2*>(A.u)[i + e * kBlock] = uv[e];
+                xv = uv[e];  // the norm below is ||u||
+            } else {
+                reinterpret_cast<dx2*>(A.x)[i + e * kBlock] = xv;
+            }
+            acc = fma(xv.x, xv.x, acc);
+            acc = fma(xv.y, xv.y, acc);
+        } else {
+            reinterpret_cast<dx2*>(A.xr)[i + e * kBlock] = t[e];
+        }
+    }
+}
+
+template <int U>
 __global__ __launch_bounds__(kBlock) void k_update_x(UpdArgs A) {
     __shared__ double sh[kShN];
     const int64_t n = A.n;
@@ -318,37 +371,10 @@ __global__ __launch_bounds__(kBlock) void k_update_x(UpdArgs A) {
 #pragma unroll
     for (int m = 0; m < kMaxUpdateVecs; ++m) yv[m] = m < A.k ? A.y[m] : 0.0;
     double acc = 0.0;
-    NK_CHUNKED(i, n >> 1) {
-        dx2 t = A.first ? dx2{0.0, 0.0} : reinterpret_cast<const dx2*>(A.xr)[i];
-#pragma unroll
-        for (int m = 0; m < kMaxUpdateVecs; ++m)  // compile-time indices keep yv in registers
-            if (m < A.k) {
-                const dx2 v = __builtin_nontemporal_load(reinterpret_cast<const dx2*>(A.V[m]) + i);
-                t.x = fma(yv[m], v.x, t.x);
-                t.y = fma(yv[m], v.y, t.y);
-            }
-        if (A.last) {
-            dx2 xv = t;
-            if (A.restart) {
-                const dx2 x0 = reinterpret_cast<const dx2*>(A.x)[i];
-                xv.x = fma(1.0, t.x, x0.x);
-                xv.y = fma(1.0, t.y, x0.y);
-            }
-            if (A.u) {  // u .-= 1 .* d, exactly kaxpy!(n, -1, x, u) on the x that would have been stored
-                dx2 uv = reinterpret_cast<const dx2*>(A.u)[i];
-                uv.x = fma(-1.0, xv.x, uv.x);
-                uv.y = fma(-1.0, xv.y, uv.y);
-                reinterpret_cast<dx2*>(A.u)[i] = uv;
-                xv = uv;  // the norm below is ||u||
-            } else {
-                reinterpret_cast<dx2*>(A.x)[i] = xv;
-            }
-            acc = fma(xv.x, xv.x, acc);
-            acc = fma(xv.y, xv.y, acc);
-        } else {
-            reinterpret_cast<dx2*>(A.xr)[i] = t;
-        }
-    }
+    const Chunk ck = block_chunk(n >> 1);
+    int64_t i = ck.lo + threadIdx.x;
+    for (; i + (U - 1) * kBlock < ck.hi; i += U * kBlock) update_elems<U>(A, yv, i, acc);
+    for (; i < ck.hi; i += kBlock) update_elems<1>(A, yv, i, acc);
     if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
         const int64_t i = n - 1;
         double t = A.first ? 0.0 : A.xr[i];
@@ -841,8 +867,15 @@ int launch_update_x(nk_ctx* c, int64_t n, double* x, double* xr, const double* c
         if (A.last && xnorm) A.part = red_out(c, g, xnorm, &A.fin);
         // every chunk reads m basis vectors and (after the first) xr; the last writes x (reading it on restart)
         const double bytes = 8.0 * n * (m + (A.first ? 0 : 1) + (A.last ? (restart ? 2 : 1) + (u ? 1 : 0) : 1));
+        // 4 elements per thread and iteration: +10-25 % over 1 for every chain length k = 1..30 at
+        // 4096^2 and 8192^2 (profiles/r02/kbench_upd.log); NK_UPD_U = 1 / 2 / 8 for A/B
+        static const int uenv = env_int("NK_UPD_U", 0);
+        const int U = uenv > 0 ? uenv : 4;
         NK_TRY(launch(c, "update_x", bytes, [&] {
-            hipLaunchKernelGGL(k_update_x, dim3(g), dim3(kBlock), 0, c->stream, A);
+            if (U >= 8) hipLaunchKernelGGL(k_update_x<8>, dim3(g), dim3(kBlock), 0, c->stream, A);
+            else if (U >= 4) hipLaunchKernelGGL(k_update_x<4>, dim3(g), dim3(kBlock), 0, c->stream, A);
+            else if (U == 2) hipLaunchKernelGGL(k_update_x<2>, dim3(g), dim3(kBlock), 0, c->stream, A);
+            else hipLaunchKernelGGL(k_update_x<1>, dim3(g), dim3(kBlock), 0, c->stream, A);
         }));
         done += m;
     }
@@ -1116,6 +1149,49 @@ extern "C" int nkb_stencil3d(nk_ctx* c, int64_t n, int mode, int epi, int fast, 
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     for (double* q : {u, v, F0, aux, out, un}) nk_vec_free(c, q);
+    return NK_OK;
+}
+
+// x update of a GMRES cycle with k basis vectors (xr = 0 start, Newton update fused into u, ||u||
+// partials), with U elements per thread (NK_UPD_U) -- average microseconds per launch
+extern "C" int nkb_update_x(nk_ctx* c, int64_t n, int k, int u_elems, int reps, double* us_out) {
+    using namespace nk;
+    if (!c || n < 2 || k < 1 || k > kMaxUpdateVecs || reps < 1 || !us_out) return NK_E_ARG;
+    std::vector<double*> V(k + 3, nullptr);
+    for (size_t v = 0; v < V.size(); ++v) {
+        NK_HIP(c, hipMalloc(&V[v], sizeof(double) * n));
+        NK_TRY(launch_fill(c, n, V[v], 0.37 + 0.01 * (double)v));
+    }
+    double *x = V[k], *xr = V[k + 1], *u = V[k + 2];
+    double* y = c->scal + 16;
+    std::vector<double> yh(k, 1e-3);
+    NK_HIP(c, hipMemcpy(y, yh.data(), sizeof(double) * k, hipMemcpyHostToDevice));
+    const int g = red_blocks(n);
+    UpdArgs A{};
+    for (int i = 0; i < k; ++i) A.V[i] = V[i];
+    A.x = x; A.xr = xr; A.y = y; A.n = n; A.k = k; A.first = 1; A.last = 1; A.restart = 0; A.u = u;
+    A.part = red_slot(c);
+    A.fin = 0;
+    auto go = [&] {
+        if (u_elems >= 8) hipLaunchKernelGGL(k_update_x<8>, dim3(g), dim3(kBlock), 0, c->stream, A);
+        else if (u_elems >= 4) hipLaunchKernelGGL(k_update_x<4>, dim3(g), dim3(kBlock), 0, c->stream, A);
+        else if (u_elems == 2) hipLaunchKernelGGL(k_update_x<2>, dim3(g), dim3(kBlock), 0, c->stream, A);
+        else hipLaunchKernelGGL(k_update_x<1>, dim3(g), dim3(kBlock), 0, c->stream, A);
+    };
+    hipEvent_t a, b;
+    NK_HIP(c, hipEventCreate(&a));
+    NK_HIP(c, hipEventCreate(&b));
+    go();
+    NK_HIP(c, hipEventRecord(a, c->stream));
+    for (int r = 0; r < reps; ++r) go();
+    NK_HIP(c, hipEventRecord(b, c->stream));
+    NK_HIP(c, hipEventSynchronize(b));
+    float ms = 0.f;
+    NK_HIP(c, hipEventElapsedTime(&ms, a, b));
+    *us_out = 1e3 * ms / reps;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    for (double* v : V) (void)hipFree(v);
     return NK_OK;
 }
 
