@@ -1152,6 +1152,38 @@ extern "C" int nkb_stencil3d(nk_ctx* c, int64_t n, int mode, int epi, int fast, 
     return NK_OK;
 }
 
+// 3D heat stencil of `kind` (4 Euler / 6 midpoint / 8 trapezoid) at n x n x nz with `planes` per
+// z-march (0: the launcher's choice) -- average microseconds per launch
+extern "C" int nkb_stencil3d_ex(nk_ctx* c, int64_t n, int64_t nz, int kind, int mode, int epi, int planes, int reps,
+                                double* us_out) {
+    using namespace nk;
+    if (!c || n < 3 || nz < 1 || reps < 1 || !us_out) return NK_E_ARG;
+    const double h = 1.0 / (n + 1);
+    nk_problem p{kind, NK_BC_ZERO, n, n, nz, h, h, h, 0.0, 0.01, 1e-6, nullptr, nullptr, 0.5};
+    double *u = nullptr, *v = nullptr, *F0 = nullptr, *aux = nullptr, *out = nullptr, *un = nullptr;
+    p.un = reinterpret_cast<const double*>(1);  // geometry only while allocating
+    for (double** q : {&u, &v, &F0, &aux, &out, &un}) NK_TRY(nk_vec_alloc(c, &p, q));
+    for (double* q : {u, v, F0, aux, un}) NK_TRY(launch_fill(c, n * n * nz, q, 0.25));
+    p.un = un;
+    StencilIn in{&p, mode, epi, out, u, v, F0, aux, 1e-6};
+    Red r{};
+    hipEvent_t a, b;
+    NK_HIP(c, hipEventCreate(&a));
+    NK_HIP(c, hipEventCreate(&b));
+    NK_TRY(launch_stencil_ex(c, in, &r, planes, 0));
+    NK_HIP(c, hipEventRecord(a, c->stream));
+    for (int k = 0; k < reps; ++k) NK_TRY(launch_stencil_ex(c, in, &r, planes, 0));
+    NK_HIP(c, hipEventRecord(b, c->stream));
+    NK_HIP(c, hipEventSynchronize(b));
+    float ms = 0.f;
+    NK_HIP(c, hipEventElapsedTime(&ms, a, b));
+    *us_out = 1e3 * ms / reps;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    for (double* q : {u, v, F0, aux, out, un}) nk_vec_free(c, q);
+    return NK_OK;
+}
+
 // x update of a GMRES cycle with k basis vectors (xr = 0 start, Newton update fused into u, ||u||
 // partials), with U elements per thread (NK_UPD_U) -- average microseconds per launch
 extern "C" int nkb_update_x(nk_ctx* c, int64_t n, int k, int u_elems, int reps, double* us_out) {
