@@ -707,12 +707,19 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         grid = A.tiles_x * A.tiles_y;
     } else {
         vec = (p->nx % 2 == 0) ? 2 : 1;
-        A.nw = 4;  // rows per 3D tile (k_st3d's NW)
+        // rows per 3D tile and the y-neighbour path (k_st3d loads, k_st3l LDS); fast bits 8 / 16 select
+        // k_st3l with 4 / 8 rows (kernel-variant bench), NK_ST3_LDS / NK_ST3_NW likewise
+        // k_st3l with 4-row tiles is the default: +6-16 % over k_st3d on every 3D kind / mode at 512^3
+        // and at config 5's 512^2 x 64 slab (profiles/r02/kbench_st3l.log)
+        static const int lds_env = env_int("NK_ST3_LDS", 1);
+        static const int nw_env = env_int("NK_ST3_NW", 4);
+        A.lds3 = (fast & 24) ? 1 : lds_env;
+        A.nw = A.lds3 ? ((fast & 8) ? 4 : ((fast & 16) ? 8 : (nw_env == 4 ? 4 : 8))) : 4;
         A.tiles_x = (int)((p->nx + 64 * vec - 1) / (64 * vec));
         A.tiles_y = (int)((p->ny + A.nw - 1) / A.nw);
         static const int target = env_int("NK_ST3_BLOCKS", 8192);  // shorter z-marches keep y-adjacent tiles in step (L2 reuse of the halo rows)
         int64_t planes = ((int64_t)p->nz * A.tiles_x * A.tiles_y + target - 1) / target;
-        static const int min_planes = env_int("NK_ST_MINPLANES", 8);
+        static const int min_planes = env_int("NK_ST_MINPLANES", 16);  // 16: (16 + 2) / 16 z-halo re-reads
         if (planes < min_planes) planes = min_planes;
         if (rows_override > 0) planes = rows_override;
         if (planes > p->nz) planes = p->nz;
@@ -1154,8 +1161,8 @@ extern "C" int nkb_stencil3d(nk_ctx* c, int64_t n, int mode, int epi, int fast, 
 
 // 3D heat stencil of `kind` (4 Euler / 6 midpoint / 8 trapezoid) at n x n x nz with `planes` per
 // z-march (0: the launcher's choice) -- average microseconds per launch
-extern "C" int nkb_stencil3d_ex(nk_ctx* c, int64_t n, int64_t nz, int kind, int mode, int epi, int planes, int reps,
-                                double* us_out) {
+extern "C" int nkb_stencil3d_ex(nk_ctx* c, int64_t n, int64_t nz, int kind, int mode, int epi, int planes, int fast,
+                                int reps, double* us_out) {
     using namespace nk;
     if (!c || n < 3 || nz < 1 || reps < 1 || !us_out) return NK_E_ARG;
     const double h = 1.0 / (n + 1);
@@ -1170,9 +1177,9 @@ extern "C" int nkb_stencil3d_ex(nk_ctx* c, int64_t n, int64_t nz, int kind, int 
     hipEvent_t a, b;
     NK_HIP(c, hipEventCreate(&a));
     NK_HIP(c, hipEventCreate(&b));
-    NK_TRY(launch_stencil_ex(c, in, &r, planes, 0));
+    NK_TRY(launch_stencil_ex(c, in, &r, planes, fast));
     NK_HIP(c, hipEventRecord(a, c->stream));
-    for (int k = 0; k < reps; ++k) NK_TRY(launch_stencil_ex(c, in, &r, planes, 0));
+    for (int k = 0; k < reps; ++k) NK_TRY(launch_stencil_ex(c, in, &r, planes, fast));
     NK_HIP(c, hipEventRecord(b, c->stream));
     NK_HIP(c, hipEventSynchronize(b));
     float ms = 0.f;

@@ -28,6 +28,7 @@ struct KArgs {
     int fin;             // fold the partials in-kernel (publish)
     double alpha;        // G_Midpoint! α
     int nw;              // 3D: rows (waves) per tile
+    int lds3;            // 3D: y-neighbour rows through LDS (k_st3l) instead of per-wave loads (k_st3d)
 };
 
 // per-kind entry points (nk_stencil_inst.hip): launch one stencil kernel of kind K / bind its g_mb
@@ -685,7 +686,179 @@ __global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
     if constexpr (EPI != EPI_NONE) publish<64 * NW>(acc, A.part, A.fin, sh);
 }
 
+// ------------------------------------------------------------------------------ 3D stencil, LDS rows
+// The same tile and z-march as k_st3d, but the y-neighbour rows come from the adjacent waves of the
+// block through LDS: every wave cooks its own centre row of plane k (it already holds it for the z
+// pipeline), stores it in a parity-double-buffered LDS row, and after one barrier per plane reads
+// rows j +- 1 from there.  Only the tile's edge waves load a halo row (row j0 - 1 or j0 + NW, or the
+// periodic wrap) -- per plane NW + 2 row loads per field instead of 3 NW, so taller tiles (NW = 8)
+// cost no extra load issue and re-fetch (NW + 2) / NW of a plane instead of 1.5x.
+template <int KIND, int MODE, int EPI, int VEC, bool PER = false, int NW = 8>
+__global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
+    __shared__ double sh[kShN];
+    KArgs A = A0;
+    A.hd = A.vdiv ? *A.vdiv : 1.0;
+    constexpr int SCH = scheme_of<KIND>();
+    constexpr bool kG = SCH != 0 && MODE != MODE_JEXACT;
+    constexpr bool kTG = SCH == 2 && kG;  // G_Trapezoid!: u_n's y-neighbours too
+    __shared__ double ly[2][kTG ? 2 : 1][NW][64 * VEC];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int t = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;
+    const int tpl = A.tiles_x * A.tiles_y;
+    const int tz = t / tpl, txy = t % tpl;
+    const int ty = txy / A.tiles_x, tx = txy % A.tiles_x;
+    const int64_t nx = A.nx, ny = A.ny, nz = A.nz, pl = nx * ny;
+    const int64_t x0 = (int64_t)tx * (64 * VEC) + (int64_t)lane * VEC;
+    const int64_t j = (int64_t)ty * NW + wv;
+    const bool act = x0 < nx && j < ny;
+    const int64_t oj = (act ? j * nx + x0 : 0);
+    // y-neighbours: from the adjacent wave's LDS row when it is in this tile, else a halo-row load
+    const bool lds_n = wv + 1 < NW && j + 1 < ny;
+    const bool lds_s = wv >= 1;
+    bool has_n, has_s;
+    int64_t dn, ds;
+    if constexpr (PER) {
+        has_n = act;
+        has_s = act;
+        dn = !act ? 0 : (j + 1 < ny ? nx : -(ny - 1) * nx);
+        ds = !act ? 0 : (j >= 1 ? -nx : (ny - 1) * nx);
+    } else {
+        has_n = act && j + 1 < ny;
+        has_s = act && j >= 1;
+        dn = has_n ? nx : 0;
+        ds = has_s ? -nx : 0;
+    }
+    const bool ld_n = !lds_n && has_n, ld_s = !lds_s && has_s;  // wave-uniform
+    const XEdge xe = x_edge<VEC, PER>(lane, act, x0, nx);
+    const int64_t de = xe.de, de2 = xe.de2;
+    const bool edge_ok = xe.ok, edge_ok2 = xe.ok2;
+    const int64_t z0 = (int64_t)tz * A.rows;
+    const int64_t z1 = z0 + A.rows < nz ? z0 + A.rows : nz;
+    constexpr bool kUn = SCH == 0 && MODE != MODE_JEXACT;
+    constexpr bool kF0 = MODE == MODE_JFD;
+    constexpr bool kAx = EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID;
+    constexpr bool vout = MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS);
+    double acc = 0.0;
+    if (z0 < nz) {
+        const int64_t o0 = z0 * pl + oj;
+        Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(A, load_raw<MODE, VEC, false, kG, PER>(A, o0 - pl, 0), act, false);
+        Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, load_raw<MODE, VEC, true, kG, PER>(A, o0, o0 + de, o0 + de2), act,
+                                                      edge_ok, edge_ok2);
+        RawRow<MODE, VEC> rp = load_raw<MODE, VEC, true, kG, PER>(A, o0 + pl, o0 + pl + de, o0 + pl + de2);
+        RawRow<MODE, VEC> rn{}, rs{};
+        if (ld_n) rn = load_raw<MODE, VEC, false, kG, PER>(A, o0 + dn, 0);
+        if (ld_s) rs = load_raw<MODE, VEC, false, kG, PER>(A, o0 + ds, 0);
+        Row<VEC> unc{}, f0c{}, ax{};
+        if constexpr (kUn) unc = data_row<VEC, NK_ST_NTN>(A.un, o0, true);
+        if constexpr (kF0) f0c = data_row<VEC, NK_ST_NT>(A.F0, o0, true);
+        if constexpr (kAx) ax = data_row<VEC>(A.aux, o0, true);
+        for (int64_t k = z0; k < z1; ++k) {
+            const int64_t o = k * pl + oj;
+            const int par = (int)(k & 1);
+            // ---- publish this wave's cooked centre row of plane k for its y-neighbours
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) {
+                ly[par][0][wv][lane * VEC + q] = fc.c[q];
+                if constexpr (kTG) ly[par][kTG ? 1 : 0][wv][lane * VEC + q] = fc.g[q];
+            }
+            // ---- issue: centre row of plane k+2, halo rows and centre data of plane k+1
+            const bool more = k + 1 < z1;
+            const int64_t o2 = more ? o + 2 * pl : o + pl;
+            const int64_t o1 = more ? o + pl : o;
+            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2);
+            RawRow<MODE, VEC> rnn{}, rss{};
+            if (ld_n) rnn = load_raw<MODE, VEC, false, kG, PER>(A, o1 + dn, 0);
+            if (ld_s) rss = load_raw<MODE, VEC, false, kG, PER>(A, o1 + ds, 0);
+            Row<VEC> uncn{}, f0cn{}, axn{};
+            if constexpr (kUn) uncn = data_row<VEC, NK_ST_NTN>(A.un, o1, true);
+            if constexpr (kF0) f0cn = data_row<VEC, NK_ST_NT>(A.F0, o1, true);
+            if constexpr (kAx) axn = data_row<VEC>(A.aux, o1, true);
+            // ---- cook what was issued one iteration ago
+            const Field<VEC> fp = cook<MODE, VEC, SCH, kG, PER>(A, rp, act, edge_ok, edge_ok2);
+            Field<VEC> fn{}, fs{};
+            if (ld_n) fn = cook<MODE, VEC, SCH, kG, PER>(A, rn, has_n, false);
+            if (ld_s) fs = cook<MODE, VEC, SCH, kG, PER>(A, rs, has_s, false);
+            __syncthreads();  // plane k's rows are in LDS (parity: the next plane's writes go to the other buffer)
+            double cn[VEC], cs[VEC], gn[VEC], gs[VEC];
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) {
+                cn[q] = lds_n ? ly[par][0][wv + (lds_n ? 1 : 0)][lane * VEC + q] : fn.c[q];
+                cs[q] = lds_s ? ly[par][0][wv - (lds_s ? 1 : 0)][lane * VEC + q] : fs.c[q];
+                if constexpr (kTG) {
+                    gn[q] = lds_n ? ly[par][1][wv + (lds_n ? 1 : 0)][lane * VEC + q] : fn.g[q];
+                    gs[q] = lds_s ? ly[par][1][wv - (lds_s ? 1 : 0)][lane * VEC + q] : fs.g[q];
+                } else {
+                    gn[q] = gs[q] = 0.0;
+                }
+                if (!has_n) { cn[q] = 0.0; gn[q] = 0.0; }  // bc_zero! beyond the last row
+                if (!has_s) { cs[q] = 0.0; gs[q] = 0.0; }
+            }
+            // ---- compute plane k
+            const LR xn = x_nbrs<PER>(fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
+            const double lft = xn.l, rgt = xn.r;
+            double glft = 0.0, grgt = 0.0;
+            if constexpr (SCH == 2 && kG) {
+                const LR g2 = x_nbrs<PER>(fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
+                glft = g2.l;
+                grgt = g2.r;
+            }
+            if (act) {
+                Row<VEC> val;
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) {
+                    const double w = (q == 0) ? lft : fc.c[q == 0 ? 0 : q - 1];
+                    const double e = (q == VEC - 1) ? rgt : fc.c[q == VEC - 1 ? q : q + 1];
+                    const double c = fc.c[q];
+                    const double lsum = (lapk(A, c, e, w, A.hx2, A.ihx2) + lapk(A, c, cn[q], cs[q], A.hy2, A.ihy2)) +
+                                        lapk(A, c, fp.c[q], fm.c[q], A.hz2, A.ihz2);
+                    double lsumg = 0.0;
+                    if constexpr (SCH == 2 && kG) {
+                        const double g = fc.g[q];
+                        const double gw = (q == 0) ? glft : fc.g[q == 0 ? 0 : q - 1];
+                        const double ge = (q == VEC - 1) ? grgt : fc.g[q == VEC - 1 ? q : q + 1];
+                        lsumg = (lapk(A, g, ge, gw, A.hx2, A.ihx2) + lapk(A, g, gn[q], gs[q], A.hy2, A.ihy2)) +
+                                lapk(A, g, fp.g[q], fm.g[q], A.hz2, A.ihz2);
+                    }
+                    const double unq = kG ? fc.g[q] : unc.v[q];
+                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0c.v[q], SCH == 1 ? fc.x[q] : c, lsumg);
+                    acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[q] : ax.v[q], acc);
+                    val.v[q] = r;
+                }
+                store_row<VEC>(A.out, o, val);
+                if (vout) {
+                    Row<VEC> vn;
+#pragma unroll
+                    for (int q = 0; q < VEC; ++q) vn.v[q] = fc.vn[q];
+                    store_row<VEC, NK_ST_NT>(A.vout, o, vn);
+                }
+            }
+            fm = fc;
+            fc = fp;
+            rp = rpp;
+            rn = rnn;
+            rs = rss;
+            unc = uncn;
+            f0c = f0cn;
+            ax = axn;
+        }
+    }
+    if constexpr (EPI != EPI_NONE) publish<64 * NW>(acc, A.part, A.fin, sh);
+}
+
 // ------------------------------------------------------------------------------ stencil dispatch
+template <int KIND, int MODE, int EPI, int NW>
+void go_st3l(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
+    if (per) {
+        if (vec == 2) hipLaunchKernelGGL((k_st3l<KIND, MODE, EPI, 2, true, NW>), dim3(grid), dim3(64 * NW), 0, s, A);
+        else hipLaunchKernelGGL((k_st3l<KIND, MODE, EPI, 1, true, NW>), dim3(grid), dim3(64 * NW), 0, s, A);
+        return;
+    }
+    if (vec == 2) hipLaunchKernelGGL((k_st3l<KIND, MODE, EPI, 2, false, NW>), dim3(grid), dim3(64 * NW), 0, s, A);
+    else hipLaunchKernelGGL((k_st3l<KIND, MODE, EPI, 1, false, NW>), dim3(grid), dim3(64 * NW), 0, s, A);
+}
+
 template <int KIND, int MODE, int EPI, int NW>
 void go_st3d(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
     if (per) {
@@ -715,9 +888,14 @@ void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
         else if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
         else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1>), dim3(grid), dim3(kBlock), 0, s, A);
     } else {
-        // 4-row tiles: 8- and 16-row tiles (fewer y-halo re-reads) measured 2-9 % slower at 512^3
-        // (profiles/r01/kbench_stencil3d.log), so only NW = 4 is instantiated
-        go_st3d<KIND, MODE, EPI, 4>(A, vec, grid, s, per);
+        // k_st3d: 4-row tiles, every wave loads its y-neighbour rows (8- and 16-row tiles measured 2-9 %
+        // slower, profiles/r01/kbench_stencil3d.log); k_st3l: y-neighbours through LDS, 4- or 8-row tiles
+        if (A.lds3) {
+            if (A.nw == 8) go_st3l<KIND, MODE, EPI, 8>(A, vec, grid, s, per);
+            else go_st3l<KIND, MODE, EPI, 4>(A, vec, grid, s, per);
+        } else {
+            go_st3d<KIND, MODE, EPI, 4>(A, vec, grid, s, per);
+        }
     }
 }
 
