@@ -80,6 +80,11 @@ int mb_check(nk_ctx* c) {
         c->res_ok = false;  // later solves use one launch per MGS pass
         return fail(c, NK_E_HIP, "resident MGS sweep: a block's partial sum never arrived (timeout); resident sweep disabled");
     }
+    if (c->ilu_err && *(volatile int*)c->ilu_err) {  // a strip of the pipelined ILU(0) sweep never advanced
+        *c->ilu_err = 0;
+        c->ilu_pipe_ok = false;  // later sweeps use the one-work-group level sweep
+        return fail(c, NK_E_HIP, "pipelined ILU(0) sweep: a strip's progress never arrived (timeout); pipelined sweep disabled");
+    }
     return NK_OK;
 }
 
@@ -219,6 +224,8 @@ int nk_ctx_destroy(nk_ctx* c) {
     (void)hipHostFree(c->hpin);
     if (c->res_gran) (void)hipFree(c->res_gran);
     if (c->res_err) (void)hipHostFree(c->res_err);
+    if (c->ilu_prog) (void)hipFree(c->ilu_prog);
+    if (c->ilu_err) (void)hipHostFree(c->ilu_err);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return NK_OK;

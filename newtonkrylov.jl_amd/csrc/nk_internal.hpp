@@ -86,6 +86,12 @@ struct nk_ctx {
     unsigned res_tag = 0;                  // granule tags handed out so far
     int res_blocks = 0, res_rl = 0;        // grid (= CUs) and LDS double2 slots per thread
     uint64_t* res_tstamp = nullptr;        // kernel-variant bench only (nkb_mgs_res, NK_RES_TSTAMP)
+    // pipelined ILU(0) sweeps (launch_ilu0_*): per-strip progress counters + a pinned timeout flag
+    int64_t* ilu_prog = nullptr;
+    int64_t ilu_prog_cap = 0;
+    int* ilu_err = nullptr;
+    int* ilu_err_dev = nullptr;
+    bool ilu_pipe_ok = true;               // false after a progress poll timed out: the one-work-group sweep
     // distribution
     int rank = 0, nranks = 1;
     nk::Comm* comm = nullptr;

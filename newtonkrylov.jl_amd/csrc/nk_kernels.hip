@@ -1019,6 +1019,162 @@ __global__ __launch_bounds__(1024) void k_ilu0_solve(IluArgs I, const double* __
     });
 }
 
+// ---- pipelined wavefront sweeps: one wave per 64-row strip, lanes skewed by one column --------
+// Rows r = z ny + y of length nx (x fastest) are processed in order; point (x, r) needs (x - 1, r)
+// (west: the lane's own previous step), (x, r - 1) (south: the lane above, one step earlier -- a
+// shuffle; lane 0 reads the previous strip's last row) and (x, r - ny) (below: an earlier strip).
+// At step t lane l handles column t - l, so a wave advances its 64 rows together, one column per
+// step.  Strips hand over through per-strip progress counters (columns complete in every row):
+// results are stored write-through (sc1), the wave drains its stores, then lane 0 publishes the
+// counter (sc1); a consumer polls the counter (sc1) before its sc1 loads of those results
+// (cdna_hip_programming.md §6 G16, the flag form).  Same arithmetic, in the same order per point, as
+// the level sweep above and the oracle's loop: bit-identical.  The backward sweep is the forward
+// one on reversed indices.  3D needs ny >= 64 (the plane below then lies in an earlier strip).
+constexpr int kIluCh = 16;  // columns per chunk: loads issued together, progress checked / published once
+struct IluPipe {
+    IluArgs I;
+    double* d;        // pivots (OP 0: diag(J) in, D~ out; else read-only)
+    double* z;        // OP 1: y = L^-1 v out; OP 2: y in, z = U^-1 y out (in place)
+    const double* v;  // OP 1: right-hand side
+    int64_t* prog;    // per strip: leading columns complete in every row of the strip
+    int* err;         // pinned host flag: a progress poll timed out
+    int64_t R, S;     // rows (ny nz) and strips (ceil(R / 64))
+    unsigned spin;    // polls per wave before giving up (~1 s)
+};
+
+__device__ __forceinline__ double ld_sc1(const double* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_sc1(double* p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// wait until strip q has completed `need` leading columns (q < 0: nothing to wait for)
+__device__ __forceinline__ bool ilu_wait(const IluPipe& P, int64_t q, int64_t need, unsigned& spins) {
+    if (q < 0) return true;
+    while (__hip_atomic_load(P.prog + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+        if (++spins > P.spin) {
+            __hip_atomic_store(P.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
+}
+
+template <int OP>  // 0: factor D~ in place; 1: forward y = L^-1 v; 2: backward z = U^-1 y
+__global__ __launch_bounds__(64) void k_ilu0_pipe(IluPipe P) {
+    const int l = threadIdx.x;
+    const int64_t nx = P.I.nx, ny = P.I.ny, nz = P.I.nz, nxny = nx * ny, R = P.R;
+    const double cx = P.I.cx, cy = P.I.cy, cz = P.I.cz;
+    // memory offsets of the processing-order neighbours (the backward sweep walks every axis reversed)
+    const int64_t dS = OP == 2 ? nx : -nx, dB = OP == 2 ? nxny : -nxny;
+    unsigned spins = 0;
+    bool ok = true;
+    for (int64_t s = blockIdx.x; s < P.S && ok; s += gridDim.x) {
+        const int64_t rr = 64 * s + l;  // this lane's row in processing order
+        const bool row_ok = rr < R;
+        const int64_t r = OP == 2 ? R - 1 - rr : rr;
+        const int64_t yy = row_ok ? r % ny : 0, zz = row_ok ? r / ny : 0;
+        const bool has_s = row_ok && (OP == 2 ? yy + 1 < ny : yy > 0);
+        const bool has_b = row_ok && (OP == 2 ? zz + 1 < nz : zz > 0);
+        const int64_t last = (R - 1 - 64 * s) < 63 ? (R - 1 - 64 * s) : 63;  // last active lane
+        // the earliest strip holding a "below" row of this strip (rows 64 s - ny ...); its successors
+        // up to s - 1 have progressed at least as far (each strip waits for its predecessor)
+        const int64_t sb = (nz > 1 && 64 * s - ny >= 0) ? (64 * s - ny) / 64 : -1;
+        const int64_t sb2 = (nz > 1 && 64 * s + last - ny >= 0) ? (64 * s + last - ny) / 64 : -1;  // the last one
+        const int64_t steps = nx + last;
+        double prev = 0.0, prevd = 0.0;  // the lane's value (and OP 1: pivot) at its previous column
+        for (int64_t t0 = 0; t0 < steps && ok; t0 += kIluCh) {
+            const int64_t need = (t0 + kIluCh < nx) ? t0 + kIluCh : nx;
+            ok = ilu_wait(P, s - 1, need, spins) && ilu_wait(P, sb, need, spins) &&
+                 (sb2 == sb || sb2 == s - 1 || ilu_wait(P, sb2, need, spins));
+            if (!ok) break;
+            // every operand of the chunk's steps is independent of the recurrence: issue all loads
+            // first (one memory round trip per chunk, not one per step), then run the chain
+            // qa: own operand (D / v / y), qc: own pivot (OP 1, 2), qs: lane 0's south value (previous
+            // strip), qb: south pivot (OP 1) or the below value (OP 0: pivot, OP 2: z), qd / qe: OP 1's
+            // below pivot and below value
+            double qa[kIluCh], qb[kIluCh], qc[kIluCh], qs[kIluCh], qd[kIluCh], qe[kIluCh];
+#pragma unroll
+            for (int k = 0; k < kIluCh; ++k) {
+                const int64_t xp = t0 + k - l;
+                const bool on = row_ok && xp >= 0 && xp < nx;
+                const int64_t i = on ? r * nx + (OP == 2 ? nx - 1 - xp : xp) : 0;
+                qa[k] = qb[k] = qc[k] = qs[k] = qd[k] = qe[k] = 0.0;
+                if (on) {
+                    if (l == 0 && has_s) qs[k] = ld_sc1((OP == 0 ? P.d : P.z) + i + dS);
+                    if constexpr (OP == 0) {
+                        qa[k] = P.d[i];
+                        if (has_b) qb[k] = ld_sc1(P.d + i + dB);
+                    } else if constexpr (OP == 1) {
+                        qa[k] = P.v[i];
+                        qc[k] = P.d[i];
+                        if (has_s) qb[k] = P.d[i + dS];
+                        if (has_b) {
+                            qd[k] = P.d[i + dB];
+                            qe[k] = ld_sc1(P.z + i + dB);
+                        }
+                    } else {
+                        qa[k] = P.z[i];
+                        qc[k] = P.d[i];
+                        if (has_b) qb[k] = ld_sc1(P.z + i + dB);
+                    }
+                }
+            }
+            // OP 1: the L factors (c / pivot) do not depend on the recurrence: divide off the chain
+            // (the same quotients, so the same rounding)
+            double fb[kIluCh], fs[kIluCh], fw[kIluCh];
+#pragma unroll
+            for (int k = 0; k < kIluCh; ++k) {
+                fb[k] = fs[k] = fw[k] = 0.0;
+                if constexpr (OP == 1) {
+                    const int64_t xp = t0 + k - l;
+                    if (row_ok && xp >= 0 && xp < nx) {
+                        if (has_b) fb[k] = cz / qd[k];
+                        if (has_s) fs[k] = cy / qb[k];
+                        if (xp > 0) fw[k] = cx / (k == 0 ? prevd : qc[k - 1]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kIluCh; ++k) {
+                const int64_t xp = t0 + k - l;
+                const bool on = row_ok && xp >= 0 && xp < nx;
+                const int64_t i = on ? r * nx + (OP == 2 ? nx - 1 - xp : xp) : 0;
+                // south: lane l - 1's value of the previous step (same column, row rr - 1)
+                double sv = __shfl_up(prev, 1, 64);
+                if (l == 0) sv = qs[k];
+                double a = 0.0, dcur = 0.0;
+                if (on) {
+                    if constexpr (OP == 0) {
+                        a = qa[k];
+                        if (has_b) a = a - (cz / qb[k]) * cz;
+                        if (has_s) a = a - (cy / sv) * cy;
+                        if (xp > 0) a = a - (cx / prev) * cx;
+                    } else if constexpr (OP == 1) {
+                        a = qa[k];
+                        dcur = qc[k];
+                        if (has_b) a = a - fb[k] * qe[k];
+                        if (has_s) a = a - fs[k] * sv;
+                        if (xp > 0) a = a - fw[k] * prev;
+                    } else {
+                        a = qa[k];
+                        if (xp > 0) a = a - cx * prev;
+                        if (has_s) a = a - cy * sv;
+                        if (has_b) a = a - cz * qb[k];
+                        a = a / qc[k];
+                    }
+                    st_sc1((OP == 0 ? P.d : P.z) + i, a);
+                }
+                prev = a;
+                prevd = dcur;
+            }
+            // publish: every store of this chunk drained, then the strip's progress
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            int64_t done = t0 + kIluCh - last;
+            done = done < 0 ? 0 : (done > nx ? nx : done);
+            if (l == 0) __hip_atomic_store(P.prog + s, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 // off-diagonal entry of J along one axis: the exact tangent at point i of the unit vector on its
 // neighbour (the entry collect(J) holds): lap = f / h^2 with f = 1 ((1 - α) for G_Midpoint!), the
 // other axes add +0, Bratu adds λ (e^u · 0) = +0, heat: (Δt or Δt/2) (a lap) - 0
@@ -1039,16 +1195,76 @@ IluArgs ilu_args(const nk_problem* p, int dim) {
     return I;
 }
 
+// the pipelined sweeps: rows of at least 64 columns... any 2D / 1D grid; 3D with ny >= 64 (the plane
+// below a strip's rows must lie in an earlier strip); NK_ILU_PIPE=0 forces the level sweeps
+static bool ilu_pipe_applies(nk_ctx* c, const nk_problem* p) {
+    static const int env = env_int("NK_ILU_PIPE", 1);
+    return env && c->ilu_pipe_ok && (p->nz == 1 || p->ny >= 64);
+}
+
+static int ilu_pipe_setup(nk_ctx* c, const nk_problem* p, int dim, IluPipe* P, int* grid) {
+    P->I = ilu_args(p, dim);
+    P->R = p->ny * p->nz;
+    P->S = (P->R + 63) / 64;
+    if (P->S > c->ilu_prog_cap) {
+        if (c->ilu_prog) (void)hipFree(c->ilu_prog);
+        c->ilu_prog = nullptr;
+        c->ilu_prog_cap = 0;
+        NK_HIP(c, hipMalloc(&c->ilu_prog, sizeof(int64_t) * (size_t)P->S));
+        c->ilu_prog_cap = P->S;
+    }
+    if (!c->ilu_err) {
+        NK_HIP(c, hipHostMalloc(&c->ilu_err, sizeof(int), hipHostMallocMapped));
+        *c->ilu_err = 0;
+        NK_HIP(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->ilu_err_dev), c->ilu_err, 0));
+    }
+    P->prog = c->ilu_prog;
+    P->err = c->ilu_err_dev;
+    P->spin = 1u << 22;
+    int dev = 0, cus = 0;
+    NK_HIP(c, hipGetDevice(&dev));
+    NK_HIP(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    // at most one wave per CU: every strip's predecessor is always running (no waiting wave can
+    // keep it from being scheduled), and the sc1 hand-off stays in its measured form
+    *grid = (int)std::min<int64_t>(P->S, std::max(1, cus));
+    return NK_OK;
+}
+
+template <int OP>
+static int ilu_pipe_launch(nk_ctx* c, const IluPipe& P, int grid, const char* name, double bytes) {
+    NK_HIP(c, hipMemsetAsync(P.prog, 0, sizeof(int64_t) * (size_t)P.S, c->stream));
+    return launch(c, name, bytes, [&] { hipLaunchKernelGGL(k_ilu0_pipe<OP>, dim3(grid), dim3(64), 0, c->stream, P); });
+}
+
 int launch_ilu0_factor(nk_ctx* c, const nk_problem* p, int dim, double* d) {
+    const double bytes = 16.0 * (double)(p->nx * p->ny * p->nz);
+    if (ilu_pipe_applies(c, p)) {
+        IluPipe P{};
+        int grid = 1;
+        NK_TRY(ilu_pipe_setup(c, p, dim, &P, &grid));
+        P.d = d;
+        return ilu_pipe_launch<0>(c, P, grid, "ilu0_factor", bytes);
+    }
     const IluArgs I = ilu_args(p, dim);
-    return launch(c, "ilu0_factor", 16.0 * (double)(p->nx * p->ny * p->nz), [&] {
+    return launch(c, "ilu0_factor_levels", bytes, [&] {
         hipLaunchKernelGGL(k_ilu0_factor, dim3(1), dim3(1024), 0, c->stream, I, d);
     });
 }
 
 int launch_ilu0_solve(nk_ctx* c, const nk_problem* p, int dim, const double* d, double* z, const double* v) {
+    const double n = (double)(p->nx * p->ny * p->nz);
+    if (ilu_pipe_applies(c, p)) {
+        IluPipe P{};
+        int grid = 1;
+        NK_TRY(ilu_pipe_setup(c, p, dim, &P, &grid));
+        P.d = const_cast<double*>(d);
+        P.z = z;
+        P.v = v;
+        NK_TRY(ilu_pipe_launch<1>(c, P, grid, "ilu0_forward", 24.0 * n));  // v, d in; y out
+        return ilu_pipe_launch<2>(c, P, grid, "ilu0_backward", 24.0 * n);  // y, d in; z out
+    }
     const IluArgs I = ilu_args(p, dim);
-    return launch(c, "ilu0_solve", 48.0 * (double)(p->nx * p->ny * p->nz), [&] {
+    return launch(c, "ilu0_solve_levels", 48.0 * n, [&] {
         hipLaunchKernelGGL(k_ilu0_solve, dim3(1), dim3(1024), 0, c->stream, I, d, z, v);
     });
 }
