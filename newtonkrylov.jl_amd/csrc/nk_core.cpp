@@ -325,8 +325,8 @@ int nk_jv(nk_ctx* c, const nk_problem* p, double* out, const double* u, const do
     }
     NK_TRY(halo_exchange(c, p, u));
     NK_TRY(exchange_un(c, p));
-    NK_TRY(halo_exchange(c, p, v));
     StencilIn in{p, mode == NK_JV_FD ? MODE_JFD : MODE_JEXACT, EPI_NONE, out, u, v, F0, nullptr, eps};
+    in.xchg_v = true;
     Red r{};
     return launch_stencil(c, in, &r);
 }

@@ -190,5 +190,68 @@ __device__ __forceinline__ void publish(double acc, double* part, int fin, doubl
 
 __device__ __forceinline__ double lap(double c, double p, double m, double h2) { return ((p - 2.0 * c) + m) / h2; }
 
+// ------------------------------------------------------------------------------ peer ghost planes
+__device__ __forceinline__ uint64_t* halo_flags(uint64_t* base) { return base + kMbWords; }
+__device__ __forceinline__ uint64_t* halo_tile_flags(uint64_t* base, int par, int side) {
+    return base + kMbWords + (size_t)2 * 2 * kHaloBlocks + (size_t)(par * 2 + side) * kHaloTileFlags;
+}
+__device__ __forceinline__ uint64_t* halo_inbox(uint64_t* base, int par, int side, int64_t cap) {
+    return base + kMbWords + kHaloFlagWords + (size_t)(par * 2 + side) * (size_t)cap;
+}
+__device__ __forceinline__ double ld_inbox(const uint64_t* p) {
+    return __longlong_as_double((long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+
+// Ghost patch of one stencil tile through the peers' inboxes, inside the stencil launch (no
+// separate exchange kernel): a tile whose rows reach the slab's lower (upper) end pushes its patch
+// of my first (last) plane of v -- rows [ra, rb) x columns [ca, cb) of the plane -- into that
+// neighbour's inbox (system-scope stores, drained), raises its tile flag there, then waits for the
+// neighbour's flag of the same tile; its ghost loads then read the neighbour's patch from my inbox.
+// Every other tile never waits, so the exchange overlaps the interior of the stencil.
+struct HaloTile {
+    int lo, hi;          // this tile needs the lower / upper neighbour's patch
+};
+__device__ __forceinline__ bool halo_tile_exchange(const double* __restrict__ v, int64_t plane, int64_t nplanes,
+                                                   int64_t nx, int64_t ra, int64_t rb, int64_t ca, int64_t cb, int tile,
+                                                   HaloTile t, uint64_t epoch, int64_t cap, int nthreads) {
+    __shared__ int hx_ok;
+    const int rank = g_mb.rank, nr = g_mb.nranks;
+    const int par = (int)(epoch & 1);
+    const int64_t w = cb - ca, cnt = (rb - ra) * w;
+    for (int side = 0; side < 2; ++side) {  // side 0: my first plane -> the lower rank's "from upper" inbox
+        if ((side == 0 && !t.lo) || (side == 1 && !t.hi)) continue;
+        const int peer = side == 0 ? rank - 1 : rank + 1;
+        const double* src = side == 0 ? v : v + (nplanes - 1) * plane;
+        uint64_t* dst = halo_inbox(g_mb.peers[peer], par, side == 0 ? 1 : 0, cap);
+        for (int64_t q = threadIdx.x; q < cnt; q += nthreads) {
+            const int64_t pos = (ra + q / w) * nx + ca + q % w;
+            __hip_atomic_store(dst + pos, (uint64_t)__double_as_longlong(src[pos]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every thread drains its stores before the flag
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (t.lo) __hip_atomic_store(halo_tile_flags(g_mb.peers[rank - 1], par, 1) + tile, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (t.hi) __hip_atomic_store(halo_tile_flags(g_mb.peers[rank + 1], par, 0) + tile, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        hx_ok = 1;
+        for (int side = 0; side < 2; ++side) {
+            if ((side == 0 && !t.lo) || (side == 1 && !t.hi)) continue;
+            const uint64_t* f = halo_tile_flags(g_mb.self, par, side) + tile;
+            unsigned spins = 0;
+            while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+                if (++spins > g_mb.spin_limit) {
+                    __hip_atomic_store(g_mb.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    hx_ok = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+    }
+    __syncthreads();
+    (void)nr;
+    return hx_ok != 0;
+}
+
 }  // namespace
 }  // namespace nk

@@ -188,11 +188,13 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
 constexpr int kMbSlots = 256;                // mailbox ring (epoch % kMbSlots)
 constexpr int kMbRanks = 32;                 // max ranks of the mailbox all-reduce (2 granules each: one wave polls them all)
 constexpr int kHaloBlocks = 64;              // blocks (= flags per side) of the IPC ghost-plane exchange
+constexpr int kHaloTileFlags = 4096;         // stencil tiles per plane whose ghost patch travels in the stencil itself
 // one fine-grained region per rank, IPC-mapped by every other rank:
 //   [mailbox: kMbSlots x kMbRanks x 2 u64][halo flags: 2 parity x 2 sides x kHaloBlocks u64]
+//   [tile flags: 2 parity x 2 sides x kHaloTileFlags u64]
 //   [halo inbox: 2 parity x 2 sides x halo_cap doubles]   (side 0: from the lower rank, 1: from the upper)
 constexpr size_t kMbWords = (size_t)2 * kMbSlots * kMbRanks;
-constexpr size_t kHaloFlagWords = (size_t)2 * 2 * kHaloBlocks;
+constexpr size_t kHaloFlagWords = (size_t)2 * 2 * (kHaloBlocks + kHaloTileFlags);
 int mailbox_bind(nk_ctx* c);                 // make c's mailbox the one the kernels use (nk_kernels.hip)
 int mailbox_selftest(nk_ctx* c, bool* ok);   // a few epochs through the mailbox vs the expected sums
 // ghost planes of v (interior pointer, `plane` doubles per plane, `nplanes` planes) through the peer
@@ -213,6 +215,8 @@ struct StencilIn {
     double eps;
     const double* vdiv = nullptr;  // device scalar h: the operator is applied to v / h ...
     double* vout = nullptr;        // ... and v / h is stored here (fused kdivcopy!)
+    bool xchg_v = false;           // v's ghost planes are stale: exchange them (in the stencil itself when
+                                   // the peer mailbox is up, else halo_exchange before the launch)
 };
 // returns the partial sums (when epi != EPI_NONE) in *red
 int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red);

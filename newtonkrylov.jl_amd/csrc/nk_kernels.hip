@@ -541,10 +541,6 @@ __global__ void k_mb_test(unsigned epoch, double value, double* out) {
 }  // namespace
 
 namespace {
-__device__ __forceinline__ uint64_t* halo_flags(uint64_t* base) { return base + kMbWords; }
-__device__ __forceinline__ uint64_t* halo_inbox(uint64_t* base, int par, int side, int64_t cap) {
-    return base + kMbWords + kHaloFlagWords + (size_t)(par * 2 + side) * (size_t)cap;
-}
 
 // Ghost planes through the peers' inboxes (IPC-mapped fine-grained memory over xGMI).  Block b
 // owns chunk b of the plane: it pushes my boundary-plane chunks into the lower / upper
@@ -668,7 +664,10 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
 }
 
 int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red) {
-    if (in.p && nk_is_user(in.p->kind)) return launch_user(c, in, red);
+    if (in.p && nk_is_user(in.p->kind)) {
+        if (in.xchg_v) NK_TRY(halo_exchange(c, in.p, in.v));
+        return launch_user(c, in, red);
+    }
     return launch_stencil_ex(c, in, red, 0, 0);
 }
 
@@ -725,6 +724,23 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         if (planes > p->nz) planes = p->nz;
         A.rows = (int)planes;
         grid = A.tiles_x * A.tiles_y * (int)((p->nz + planes - 1) / planes);
+    }
+    if (in.xchg_v) {
+        // v's ghost planes: through the peers' inboxes inside this launch (halo_tile_exchange: only the
+        // tiles at the slab's ends fetch, the rest of the grid never waits) when the peer mailbox is up,
+        // the slab axis is not periodic and every tile of a plane has a flag; else exchanged first
+        static const int fuse_env = env_int("NK_HALO_FUSE", 1);
+        const int64_t tiles_pl = g.dim == 2 ? A.tiles_x : (int64_t)A.tiles_x * A.tiles_y;
+        const bool fuse = fuse_env && c->mb_on && c->nranks > 1 && !per && in.mode != MODE_RES &&
+                          (g.dim == 2 || (g.dim == 3 && A.lds3)) && g.plane <= c->halo_cap && tiles_pl <= kHaloTileFlags;
+        if (fuse) {
+            A.hx_lo = c->rank > 0;
+            A.hx_hi = c->rank + 1 < c->nranks;
+            A.hx_epoch = ++c->halo_epoch;
+            A.hx_cap = c->halo_cap;
+        } else {
+            NK_TRY(halo_exchange(c, p, in.v));
+        }
     }
     if (in.epi != EPI_NONE) {
         if (grid > kRedCap - 2) return fail(c, NK_E_ARG, "stencil grid exceeds reduction capacity");

@@ -191,8 +191,8 @@ struct Op {
             }
             eps = fd_eps(vnorm);
         }
-        NK_TRY(halo_exchange(c, p, v));
         StencilIn in{p, mode == NK_JV_FD ? MODE_JFD : MODE_JEXACT, epi, out, u, v, F0, aux, eps, vdiv, vout};
+        in.xchg_v = true;  // v's ghost planes: exchanged by the stencil launch itself where it can
         return launch_stencil(c, in, red);
     }
     int64_t ws_n() const { return p->nx * p->ny * p->nz; }

@@ -29,6 +29,11 @@ struct KArgs {
     double alpha;        // G_Midpoint! α
     int nw;              // 3D: rows (waves) per tile
     int lds3;            // 3D: y-neighbour rows through LDS (k_st3l) instead of per-wave loads (k_st3d)
+    // ghost planes of v through the peers' inboxes inside this launch (halo_tile_exchange): the rank
+    // has a lower / upper neighbour whose boundary patch this launch fetches itself
+    int hx_lo, hx_hi;
+    uint64_t hx_epoch;
+    int64_t hx_cap;
 };
 
 // per-kind entry points (nk_stencil_inst.hip): launch one stencil kernel of kind K / bind its g_mb
@@ -334,6 +339,25 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o,
     return r;
 }
 
+// the same for a ghost row / plane whose v values are in my inbox (ib, indexed by the in-plane
+// position p) while u and u_n stay in memory (o); only centres are read -- a ghost row / plane is
+// only ever a y / z neighbour, its x-edges are never used
+template <int MODE, int VEC, bool G = false>
+__device__ __forceinline__ RawRow<MODE, VEC> load_raw_ib(const KArgs& A, const uint64_t* ib, int64_t o, int64_t p) {
+    RawRow<MODE, VEC> r;
+#pragma unroll
+    for (int h = 0; h < VEC; ++h) {
+        if constexpr (MODE == MODE_JEXACT) r.a[h] = ld_inbox(ib + p + h);
+        else r.a[h] = A.u[o + h];
+        if constexpr (MODE == MODE_JFD) r.b[h] = ld_inbox(ib + p + h);
+        if constexpr (G) r.g[h] = A.un[o + h];
+    }
+    r.ae = r.ae2 = 0.0;
+    r.be = r.be2 = 0.0;
+    r.ge = r.ge2 = 0.0;
+    return r;
+}
+
 // cooked stencil field of a row: centres, the lane's edge value(s), and (fused normalisation) v / h
 template <int VEC>
 struct Field {
@@ -469,6 +493,20 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     const bool edge_ok = xe.ok, edge_ok2 = xe.ok2;
     const int64_t y0 = (int64_t)ty * A.rows;
     const int64_t y1 = y0 + A.rows < ny ? y0 + A.rows : ny;
+    // ghost rows of v from the neighbours' patches, fetched by this launch (tiles at the slab's ends)
+    const uint64_t* ib_lo = nullptr;
+    const uint64_t* ib_hi = nullptr;
+    if constexpr (MODE != MODE_RES && !PER) {
+        const HaloTile ht{A.hx_lo && y0 == 0 && y0 < ny, A.hx_hi && y1 == ny && y0 < ny};
+        if (ht.lo || ht.hi) {  // block-uniform
+            const int64_t ca = (int64_t)tx * (kBlock * VEC), cb = ca + kBlock * VEC < nx ? ca + kBlock * VEC : nx;
+            if (halo_tile_exchange(A.v, nx, ny, nx, 0, 1, ca, cb, tx, ht, A.hx_epoch, A.hx_cap, kBlock)) {
+                const int par = (int)(A.hx_epoch & 1);
+                if (ht.lo) ib_lo = halo_inbox(g_mb.self, par, 0, A.hx_cap);
+                if (ht.hi) ib_hi = halo_inbox(g_mb.self, par, 1, A.hx_cap);
+            }
+        }
+    }
     constexpr bool kU = MODE == MODE_JEXACT && KIND == NK_BRATU2D;
     constexpr bool kUn = KIND == NK_HEAT2D_EULER && MODE != MODE_JEXACT;
     constexpr bool kF0 = MODE == MODE_JFD;
@@ -478,13 +516,15 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     if (y0 < ny) {
         // rows y0-1 (ghost plane when y0 = 0) and y0 cooked up front; row y0+1 raw in flight
         Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(
-            A, load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 - 1) * nx + xc, (y0 - 1) * nx + xc + de, (y0 - 1) * nx + xc + de2),
+            A, ib_lo ? load_raw_ib<MODE, VEC, kG>(A, ib_lo, (y0 - 1) * nx + xc, xc)
+                     : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 - 1) * nx + xc, (y0 - 1) * nx + xc + de, (y0 - 1) * nx + xc + de2),
             act, false, false);
         Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(
             A, load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, y0 * nx + xc, y0 * nx + xc + de, y0 * nx + xc + de2), act, edge_ok,
             edge_ok2);
         RawRow<MODE, VEC> rp =
-            load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 + 1) * nx + xc, (y0 + 1) * nx + xc + de, (y0 + 1) * nx + xc + de2);
+            (ib_hi && y0 + 1 == ny) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, (y0 + 1) * nx + xc, xc)
+                                    : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 + 1) * nx + xc, (y0 + 1) * nx + xc + de, (y0 + 1) * nx + xc + de2);
         Row<VEC> uc{}, unc{}, f0c{}, ax{};
         {
             const int64_t o = y0 * nx + xc;
@@ -498,7 +538,9 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
             // ---- issue: raw row j+2 (rows up to ny are the ghost plane; y1 <= ny keeps j+2 <= ny+1
             //      in range only when j+1 < y1, so clamp to row j+1 otherwise)
             const int64_t o2 = (j + 1 < y1) ? o + 2 * nx : o + nx;
-            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, o2, o2 + de, o2 + de2);
+            const int64_t r2 = (j + 1 < y1) ? j + 2 : j + 1;  // the row o2 is in (ny: the upper ghost row)
+            const RawRow<MODE, VEC> rpp = (ib_hi && r2 == ny) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, o2, xc)
+                                                              : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, o2, o2 + de, o2 + de2);
             Row<VEC> ucn{}, uncn{}, f0cn{}, axn{};
             const int64_t o1 = (j + 1 < y1) ? o + nx : o;
             if constexpr (kU) ucn = data_row<VEC>(A.u, o1, true);
@@ -740,13 +782,31 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
     constexpr bool kF0 = MODE == MODE_JFD;
     constexpr bool kAx = EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID;
     constexpr bool vout = MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS);
+    // ghost planes of v from the neighbours' patches, fetched by this launch (z-tiles at the slab's ends)
+    const uint64_t* ib_lo = nullptr;
+    const uint64_t* ib_hi = nullptr;
+    if constexpr (MODE != MODE_RES && !PER) {
+        const HaloTile ht{A.hx_lo && z0 == 0 && z0 < nz, A.hx_hi && z1 == nz && z0 < nz};
+        if (ht.lo || ht.hi) {  // block-uniform
+            const int64_t ra = (int64_t)ty * NW, rb = ra + NW < ny ? ra + NW : ny;
+            const int64_t ca = (int64_t)tx * (64 * VEC), cb = ca + 64 * VEC < nx ? ca + 64 * VEC : nx;
+            if (halo_tile_exchange(A.v, pl, nz, nx, ra, rb, ca, cb, txy, ht, A.hx_epoch, A.hx_cap, 64 * NW)) {
+                const int par = (int)(A.hx_epoch & 1);
+                if (ht.lo) ib_lo = halo_inbox(g_mb.self, par, 0, A.hx_cap);
+                if (ht.hi) ib_hi = halo_inbox(g_mb.self, par, 1, A.hx_cap);
+            }
+        }
+    }
     double acc = 0.0;
     if (z0 < nz) {
         const int64_t o0 = z0 * pl + oj;
-        Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(A, load_raw<MODE, VEC, false, kG, PER>(A, o0 - pl, 0), act, false);
+        Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(
+            A, ib_lo ? load_raw_ib<MODE, VEC, kG>(A, ib_lo, o0 - pl, oj) : load_raw<MODE, VEC, false, kG, PER>(A, o0 - pl, 0), act,
+            false);
         Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, load_raw<MODE, VEC, true, kG, PER>(A, o0, o0 + de, o0 + de2), act,
                                                       edge_ok, edge_ok2);
-        RawRow<MODE, VEC> rp = load_raw<MODE, VEC, true, kG, PER>(A, o0 + pl, o0 + pl + de, o0 + pl + de2);
+        RawRow<MODE, VEC> rp = (ib_hi && z0 + 1 == nz) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, o0 + pl, oj)
+                                                       : load_raw<MODE, VEC, true, kG, PER>(A, o0 + pl, o0 + pl + de, o0 + pl + de2);
         RawRow<MODE, VEC> rn{}, rs{};
         if (ld_n) rn = load_raw<MODE, VEC, false, kG, PER>(A, o0 + dn, 0);
         if (ld_s) rs = load_raw<MODE, VEC, false, kG, PER>(A, o0 + ds, 0);
@@ -767,7 +827,9 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
             const bool more = k + 1 < z1;
             const int64_t o2 = more ? o + 2 * pl : o + pl;
             const int64_t o1 = more ? o + pl : o;
-            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2);
+            const int64_t k2 = more ? k + 2 : k + 1;  // the plane o2 is in (nz: the upper ghost plane)
+            const RawRow<MODE, VEC> rpp = (ib_hi && k2 == nz) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, o2, oj)
+                                                              : load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2);
             RawRow<MODE, VEC> rnn{}, rss{};
             if (ld_n) rnn = load_raw<MODE, VEC, false, kG, PER>(A, o1 + dn, 0);
             if (ld_s) rss = load_raw<MODE, VEC, false, kG, PER>(A, o1 + ds, 0);
