@@ -27,7 +27,7 @@ ap.add_argument("--jv", default="exact")
 ap.add_argument("--krylov-itmax", type=int, default=0,
                 help="> 0: instead of the Newton solve, one restarted GMRES(10) solve J x = F(u0) with this fixed "
                      "budget (atol = rtol = 0); rank 0 saves x and the residual history")
-ap.add_argument("--problem", choices=["bratu", "heat_periodic"], default="bratu",
+ap.add_argument("--problem", choices=["bratu", "heat_periodic", "heat3d"], default="bratu",
                 help="heat_periodic: G_Trapezoid! ∘ diffusion! with bc_periodic! -- u_n's ghost planes are "
                      "exchanged too and the slabs form a ring (rank 0 <-> rank world-1)")
 ap.add_argument("--transport", choices=["rccl", "mailbox"], default="rccl",
@@ -63,6 +63,40 @@ else:
         sys.exit(0)
 
 nx, ny = args.nx, args.ny
+if args.problem == "heat3d":  # 3D heat, implicit midpoint, z-slabs (k_st3l: the ghost planes travel in the stencil)
+    nz = 24
+    grid = ah.slab((nx, ny, nz), rank, world)
+    z0, nzl = grid.offset, grid.shape_xyz[2]
+    rng = np.random.default_rng(9)
+    un_glob = rng.standard_normal((nz, ny, nx))
+    u_glob = un_glob + 0.01 * rng.standard_normal((nz, ny, nx))
+    v_glob = rng.standard_normal((nz, ny, nx))
+    hx, hy, hz, a = 1.0 / (nx + 1), 1.0 / (ny + 1), 1.0 / (nz + 1), 0.01
+    dt = 1.0 / (2.0 * a * (1 / hx ** 2 + 1 / hy ** 2 + 1 / hz ** 2))
+    und = ah.DeviceArray.from_numpy(np.ascontiguousarray(un_glob[z0:z0 + nzl]), grid, ctx)
+    F_, p = ah.G_Midpoint_(alpha=0.3).bind(ah.diffusion3d_), (und, dt, None, (a, hx, hy, hz, ah.bc_zero_), 0.0)
+    u = ah.DeviceArray.from_numpy(np.ascontiguousarray(u_glob[z0:z0 + nzl]), grid, ctx)
+    res = u.zero()
+    vd = ah.DeviceArray.from_numpy(np.ascontiguousarray(v_glob[z0:z0 + nzl]), grid, ctx)
+    out = u.zero()
+    F_(res, u, p)
+    ah.mul_(out, ah.JacobianOperator(F_, res, u, p, jv="exact"), vd)
+    jv_ex = out.to_numpy()
+    ah.mul_(out, ah.JacobianOperator(F_, res, u, p, jv="fd"), vd, eps=1e-6)
+    jv_fd = out.to_numpy()
+    F_loc = res.to_numpy()
+    u, r = ah.newton_krylov_(F_, u, p, res, tol_abs=6e-6, jv="fd")
+    parts = [None] * world
+    dist.all_gather_object(parts, dict(z0=z0, u=u.to_numpy(), jv=jv_ex, jvfd=jv_fd, F=F_loc))
+    if rank == 0:
+        parts.sort(key=lambda d: d["z0"])
+        cat = lambda key: np.concatenate([d[key] for d in parts])  # noqa: E731
+        np.savez(args.out + ".npz", u=cat("u"), jv=cat("jv"), jvfd=cat("jvfd"), F=cat("F"))
+        json.dump(dict(solved=bool(r.solved), outer=r.stats.outer_iterations, inner=r.stats.inner_iterations,
+                       world=world, mailbox=ctx.mailbox_active), open(args.out + ".json", "w"))
+    dist.barrier()
+    ctx.sync()
+    sys.exit(0)
 grid = ah.slab((nx, ny), rank, world)
 hx, hy, lam = 1.0 / (nx + 1), 1.0 / (ny + 1), 3.51382
 xs = np.arange(1, nx + 1) * hx

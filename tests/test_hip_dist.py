@@ -113,8 +113,8 @@ def free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("transport", ["mailbox", "rccl"])
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("transport,world", [("mailbox", 2), ("rccl", 2), ("mailbox", 3), ("rccl", 3), ("mailbox", 4),
+                                             ("rccl", 4)])
 def test_slabs_match_oracle(tmp_path, world, transport):
     """Slabs of one 2D Bratu grid on `world` ranks: residual, Jv (ghost rows from the neighbours),
     a dot, and a whole Newton-GMRES solve against the oracle on the full grid.  transport=mailbox
@@ -212,3 +212,40 @@ def test_resident_sweep_two_ranks_one_gpu(tmp_path):
     assert meta["niter"] == sto["niter"] == 20 and meta["n_matvec"] == sto["n_matvec"]
     assert np.allclose(d["h"], ho, rtol=1e-9, atol=0)
     assert np.max(np.abs(d["x"] - xo)) <= 1e-9 * np.max(np.abs(xo))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_heat3d_midpoint_zslabs_match_oracle(tmp_path, world):
+    """3D heat (G_Midpoint!, alpha 0.3) on z-slabs, mailbox transport: the Jv's ghost planes of v travel
+    inside the 3D stencil launch (k_st3l's tiles at the slab ends fetch the neighbours' patches).
+    Residual, exact and FD JVP bit-identical to the oracle on the whole grid; one implicit step
+    with the FD operator: equal Newton / Krylov counts."""
+    out = str(tmp_path / "h3")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
+           "--problem", "heat3d", "--nx", "40", "--ny", "20"]
+    proc = subprocess.Popen(cmd, env=worker_env(world), stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                            start_new_session=True)
+    try:
+        log, _ = proc.communicate(timeout=180)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, signal.SIGKILL)
+        pytest.fail("distributed worker timed out")
+    assert proc.returncode == 0, log.decode()[-3000:]
+    meta = json.load(open(out + ".json"))
+    assert meta["mailbox"]
+    d = np.load(out + ".npz")
+    nx, ny, nz = 40, 20, 24
+    rng = np.random.default_rng(9)
+    un = rng.standard_normal((nz, ny, nx))
+    u0 = un + 0.01 * rng.standard_normal((nz, ny, nx))
+    v = rng.standard_normal((nz, ny, nx))
+    P = oc.heat3d_euler(nx, ny, nz, un=un, scheme="midpoint", alpha=0.3)
+    np.testing.assert_array_equal(d["F"], oc.residual(P, u0))
+    np.testing.assert_array_equal(d["jv"], oc.jv_exact(P, u0, v))
+    np.testing.assert_array_equal(d["jvfd"], oc.jv_fd(P, u0, v, F0=d["F"], eps=1e-6))
+    uo, so = oc.newton_krylov(P, u0, tol_abs=6e-6, jv="fd")
+    assert meta["solved"] and so["solved"]
+    assert (meta["outer"], meta["inner"]) == (so["outer_iterations"], so["inner_iterations"])
+    assert np.max(np.abs(d["u"] - uo)) <= 1e-10
