@@ -218,6 +218,10 @@ typedef struct nk_krylov_opts {
     double* u_update;             /* non-null: the Newton update u .-= x is fused into the solve's last pass;
                                      x is then NOT stored and stats.u_norm = ||u|| afterwards                */
     const nk_precond* N;          /* right preconditioner (null: none)                                      */
+    const nk_precond* M;          /* left preconditioner (null: none): Krylov.jl's `M` (ldiv = false), the
+                                     `M = M(J)` Ariadne forwards (src/Ariadne.jl:327-329).  gmres!/fgmres!:
+                                     r0 = M (b - A x), q = M A N V_k, the stopping test on ||M r||;
+                                     cg!: the SPD preconditioner (z = M r, gamma = <r, z>)                   */
 } nk_krylov_opts;
 
 typedef struct nk_krylov_stats {

@@ -237,15 +237,14 @@ def newton_krylov_(F_: DeviceResidual, u: DeviceArray, p=None, res: DeviceArray 
                    jv: str = "exact", workspace=None):
     """newton_krylov!(F!, u, p, res; kwargs...) -- src/Ariadne.jl:288-372 (and the 3-arg form :259-263).
 
-    `N` (right preconditioner) is a preconditioner object or a factory `N(J)` called per Newton
-    step (ariadne_hip.precond: `jacobi`, DiagonalPreconditioner, UserPreconditioner); left `M` is
-    not implemented.
+    `N` (right) and `M` (left preconditioner) are preconditioner objects or factories `N(J)` /
+    `M(J)` called per Newton step (ariadne_hip.precond: `jacobi`, `ilu0`, `gmres_preconditioner`,
+    DiagonalPreconditioner, UserPreconditioner), forwarded as Krylov.jl's `N` / `M` (:323-329);
+    an `N` or `M` inside krylov_kwargs wins over the factory, as the reference's kwarg merge does.
     Additions of the HIP path: `memory` (Krylov workspace memory = GMRES restart length),
     `jv` ("exact" | "fd") and `workspace` (re-use a Krylov workspace across calls -- the
     reference's own TODO at :316); everything else keeps the reference's meaning and default.
     """
-    if M is not None:
-        raise NotImplementedError("left preconditioner factories M: the HIP path implements right preconditioning (N)")
     callback = callback or (lambda *a: None)
     krylov_kwargs = dict(krylov_kwargs or {})
     t0 = time.perf_counter_ns()
@@ -279,9 +278,13 @@ def newton_krylov_(F_: DeviceResidual, u: DeviceArray, p=None, res: DeviceArray 
         # mul!; the device operator never writes res, so res itself is the right-hand side.
         # u .-= 1 .* d (Newton step s = 1, :341-344) is fused into the solve's last pass (d =
         # workspace.x is consumed there, not stored), which also returns ||u|| for the next FD step
-        # N: a preconditioner, or a factory called with this step's operator (e.g. N=jacobi)
-        Nop = None if N is None else (N if hasattr(N, "as_c") else N(J))
-        krylov_solve_(workspace, J, res, _b_norm=n_res, _u_norm=u_norm, _u_update=u, N=Nop, **kwargs)
+        # N / M: a preconditioner, or a factory called with this step's operator (e.g. N=jacobi);
+        # (; N = N(J), kwargs...), (; M = M(J), kwargs...): the user's krylov_kwargs win (:323-329)
+        if N is not None and "N" not in kwargs:
+            kwargs["N"] = N if hasattr(N, "as_c") else N(J)
+        if M is not None and "M" not in kwargs:
+            kwargs["M"] = M if hasattr(M, "as_c") else M(J)
+        krylov_solve_(workspace, J, res, _b_norm=n_res, _u_norm=u_norm, _u_update=u, **kwargs)
         n_matvec += workspace.stats.n_matvec
         u_norm = workspace.stats.u_norm
         n_res_prior = n_res

@@ -164,21 +164,23 @@ def krylov_solve_(ws: KrylovWorkspace, J, b: DeviceArray, *, restart=False, reor
     u .-= x is fused into the last pass; ws.x is then not stored and ws.stats.u_norm = ||u||.)"""
     if unknown:
         raise TypeError(f"unsupported Krylov keyword(s): {sorted(unknown)}")
-    if M is not None:
-        raise NotImplementedError("left preconditioner M: the HIP path implements right preconditioning (N) only")
-    if ldiv and not getattr(N, "ldiv", False):
-        raise NotImplementedError("ldiv = true: give N as the operator that approximates J^{-1} (ldiv = false), "
-                                  "or a factorisation (ilu0)")
-    if N is not None and not hasattr(N, "as_c"):
-        raise TypeError("N must be an ariadne_hip preconditioner (DiagonalPreconditioner, UserPreconditioner, "
-                        "GmresPreconditioner, jacobi(J))")
+    for name, P in (("N", N), ("M", M)):
+        if ldiv and P is not None and not getattr(P, "ldiv", False):
+            raise NotImplementedError(f"ldiv = true: give {name} as the operator that approximates J^{{-1}} "
+                                      "(ldiv = false), or a factorisation (ilu0)")
+        if P is not None and not hasattr(P, "as_c"):
+            raise TypeError(f"{name} must be an ariadne_hip preconditioner (DiagonalPreconditioner, "
+                            "UserPreconditioner, GmresPreconditioner, jacobi(J), ilu0(J))")
+    if ws.algo == "cg" and N is not None:
+        raise TypeError("cg! takes its preconditioner as M (Krylov.jl has no right preconditioner for CG)")
     if ws.algo == "cg" and (restart or reorthogonalization):
         raise TypeError("restart / reorthogonalization are GMRES keywords")
     prob = J.problem()
     opts = _lib.nk_krylov_opts(int(bool(restart)), int(bool(reorthogonalization)), int(itmax), J.jv_mode,
                                float(atol), float(rtol), float(_b_norm), float(_u_norm),
                                _u_update.ptr if _u_update is not None else None,
-                               C.cast(C.pointer(N.as_c()), C.c_void_p) if N is not None else None)
+                               C.cast(C.pointer(N.as_c()), C.c_void_p) if N is not None else None,
+                               C.cast(C.pointer(M.as_c()), C.c_void_p) if M is not None else None)
     st = _lib.nk_krylov_stats()
     cap = ((int(itmax) or 4096) + 64) if history else 0
     hist = (C.c_double * max(cap, 1))()

@@ -1,9 +1,10 @@
-"""Right preconditioners for the device GMRES / FGMRES (Krylov.jl's `N`, ldiv = false: z = N v
-approximates J^{-1} v).  SURVEY.md §8f rank 3: a device Jacobi preconditioner built from the
-Jacobian's diagonal; any other preconditioner can be supplied as device code (UserPreconditioner).
+"""Preconditioners for the device GMRES / FGMRES / CG: Krylov.jl's right `N` and left `M` (ldiv =
+false: z = P v approximates J^{-1} v; for CG, M is the SPD preconditioner).  SURVEY.md §8f rank 3:
+device Jacobi and ILU(0) preconditioners built from the Jacobian, an inner GMRES, and any other
+preconditioner supplied as device code (UserPreconditioner).
 
-`newton_krylov_(…, N=factory)`: a factory is called as `factory(J)` once per Newton step (the
-JacobianOperator of that step) and returns one of these (e.g. `N=jacobi`).
+`newton_krylov_(…, N=factory, M=factory)`: a factory is called as `factory(J)` once per Newton step
+(the JacobianOperator of that step) and returns one of these (e.g. `N=jacobi`, `M=ilu0`).
 """
 from __future__ import annotations
 

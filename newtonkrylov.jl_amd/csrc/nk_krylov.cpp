@@ -1,4 +1,5 @@
-// nk_krylov.cpp -- device-resident Krylov.jl 0.10 gmres!/cg! (M = N = I) for the Jacobian operator.
+// nk_krylov.cpp -- device-resident Krylov.jl 0.10 gmres!/fgmres!/cg! for the Jacobian operator, with
+// Krylov.jl's right (N) and left (M) preconditioners.
 //
 // Restates krylov_workspace(algo, KrylovConstructor(res)) + krylov_solve!(workspace, J, b; kwargs)
 // as called by Ariadne (src/Ariadne.jl:317-318, :338, :340, :367) -- SURVEY.md Appendix A.
@@ -37,6 +38,8 @@ struct nk_workspace {
     double* p = nullptr;   // cg: search direction
     std::vector<double*> V;
     std::vector<double*> Z;  // flexible form: Z_k = N V_k (right preconditioner)
+    double* mr = nullptr;    // left preconditioner: r0 = M w (gmres) / z = M r (cg)
+    double* mw = nullptr;    // left preconditioner: w = A N V_k before q = M w (gmres)
     double* hdev = nullptr;  // device Hessenberg columns: 2 slots of (2*cap + 2) doubles (steps k, k+1 in flight)
     double* ydev = nullptr;  // device y (cap doubles)
     double* bdev = nullptr;  // device beta of the current cycle (V_1 = r0 / beta is fused into step 1)
@@ -92,6 +95,12 @@ int ws_basis(nk_workspace* ws, int need) {
         NK_TRY(nk_vec_alloc(ws->c, &ws->prob, &v));
         ws->V.push_back(v);
     }
+    return NK_OK;
+}
+
+// a lazily allocated workspace vector (the left preconditioner's buffers)
+int ws_vec(nk_workspace* ws, double** v) {
+    if (!*v) NK_TRY(nk_vec_alloc(ws->c, &ws->prob, v));
     return NK_OK;
 }
 
@@ -265,11 +274,22 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
 
     NK_TRY(ws_basis(ws, mem));
     NK_TRY(ws_scalars(ws, mem + 1));
+    // left preconditioner M (ldiv = false): r0 = M (b - A x), q = M A (N V_k); beta and the stopping
+    // test measure the preconditioned residual (Krylov.jl 0.10 gmres!)
+    const nk_precond* Mp = (o->M && o->M->kind != NK_PRECOND_NONE) ? o->M : nullptr;
+    if (Mp) {
+        NK_TRY(ws_vec(ws, &ws->mr));
+        NK_TRY(ws_vec(ws, &ws->mw));
+    }
     // x .= 0 ; r0 = b - A*0 = b.  x is only materialised when no cycle runs: the first cycle's
     // update writes x = Σ y_i V_i directly (bit-identical to 0 + Σ y_i V_i), saving a pass over x.
     Red rb{};
     double beta = o->b_norm;  // the caller may know ||b|| already (Newton: b = F(u), ||F(u)|| just computed)
-    if (!(beta > 0.0)) {
+    const double* r0 = b;
+    if (Mp) {  // r0 = M b, beta = ||M b||
+        NK_TRY(apply_precond(c, p, Mp, A, n, ws->mr, b, true, &beta));
+        r0 = ws->mr;
+    } else if (!(beta > 0.0)) {
         NK_TRY(launch_sumsq(c, n, b, &rb));
         NK_TRY(host_scalar(c, rb, 1, &beta));
     }
@@ -296,13 +316,13 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
     auto slot_pin = [&](int k) { return ws->hpin + (size_t)(k & 1) * (2 * ws->cap + 2); };
     auto slot_pin_dev = [&](int k) { return ws->hpin_dev + (size_t)(k & 1) * (2 * ws->cap + 2); };
     auto npasses_of = [&](int k) { return reorth ? 2 * k : k; };
-    const double* v1_src = b;  // r0 of the current cycle; step 1 applies J to r0 / beta and stores V_1
+    const double* v1_src = r0;  // r0 of the current cycle; step 1 applies J to r0 / beta and stores V_1
     // right preconditioner, without the one-step-ahead issue (the FD step size needs ||N V_k|| on
     // the host): fgmres! stores Z_k = N V_k and updates x += Z y; gmres! applies N to p = N V_k
     // only for the product and updates x += N (V y) (Krylov.jl 0.10 gmres! / fgmres!)
     const nk_precond* N = (o->N && o->N->kind != NK_PRECOND_NONE) ? o->N : nullptr;
     const bool flex = N && ws->algo == NK_ALGO_FGMRES;
-    const bool spec = N == nullptr;
+    const bool spec = N == nullptr && Mp == nullptr;
     // vready[k]: step k's resident sweep stored V_{k+1} itself, so step k+1's Jv reads it as is
     std::vector<char> vready(mem + 2, 0);
     auto issue = [&](int k) -> int {
@@ -333,13 +353,24 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
                 return NK_OK;
             }
         }
-        if (N) {  // V_k = q_{k-1} / h (r0 / beta), Z_k = N V_k, q = J Z_k, <V_1, q>
+        if (N || Mp) {  // V_k = q_{k-1} / h (r0 / beta), Z_k = N V_k, q = M J Z_k, <V_1, q>
             NK_TRY(launch_fd_point(c, n, nullptr, nullptr, qprev, hprev, 0.0, ws->V[k - 1]));
-            NK_TRY(ws_zbasis(ws, flex ? k : 1));  // gmres!: one p = N V_k buffer; fgmres!: Z_k kept
-            double* zk = ws->Z[flex ? k - 1 : 0];
+            const double* zk = ws->V[k - 1];
             double znorm = 1.0;
-            NK_TRY(apply_precond(c, p, N, A, n, zk, ws->V[k - 1], A.mode == NK_JV_FD, &znorm));
-            NK_TRY(A.apply(q, zk, znorm, EPI_DOT, ws->V[0], &red));
+            if (N) {
+                NK_TRY(ws_zbasis(ws, flex ? k : 1));  // gmres!: one p = N V_k buffer; fgmres!: Z_k kept
+                double* z = ws->Z[flex ? k - 1 : 0];
+                NK_TRY(apply_precond(c, p, N, A, n, z, ws->V[k - 1], A.mode == NK_JV_FD, &znorm));
+                zk = z;
+            }
+            if (Mp) {  // w = J Z_k; q = M w
+                NK_TRY(A.apply(ws->mw, zk, znorm, EPI_NONE, nullptr, nullptr));
+                double unused = 0.0;
+                NK_TRY(apply_precond(c, p, Mp, A, n, q, ws->mw, false, &unused));
+                NK_TRY(launch_dot(c, n, ws->V[0], q, &red));
+            } else {
+                NK_TRY(A.apply(q, zk, znorm, EPI_DOT, ws->V[0], &red));
+            }
         } else if (k == 1) {  // fused kdivcopy!(V_1, r0, beta) + mul! + <V_1, Jv> (the dot partner is V_1 itself)
             NK_TRY(A.apply(q, v1_src, 1.0, EPI_DOT, nullptr, &red, ws->bdev, ws->V[0]));
         } else if (vready[k - 1]) {  // V_k is in place: mul! + <V_1, Jv> only
@@ -390,12 +421,16 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         std::fill(sn.begin(), sn.end(), 0.0);
         std::fill(z.begin(), z.end(), 0.0);
         std::fill(R.begin(), R.end(), 0.0);
-        const double* src = b;
+        const double* src = r0;
         if (restart && npass >= 1) {
             Red rr{};
             NK_TRY(A.apply(W[0], x, xnorm, EPI_RESID, b, &rr));  // w = b - A x, fused ||w||^2 partials
             NK_TRY(host_scalar(c, rr, 1, &beta));
             src = W[0];
+            if (Mp) {  // r0 = M w, beta = ||r0||
+                NK_TRY(apply_precond(c, p, Mp, A, n, ws->mr, W[0], true, &beta));
+                src = ws->mr;
+            }
         }
         Range cycle_range("gmres_cycle");
         z[0] = beta;
@@ -510,11 +545,21 @@ int cg(nk_workspace* ws, Op& A, const double* b, const nk_krylov_opts* o, nk_kry
     const int64_t n = ws->n;
     int64_t nh = 0;
     double *x = ws->x, *r = ws->xr, *p = ws->p, *Ap = ws->w;
+    // preconditioner M (Krylov.jl cg!: z = M r, gamma = <r, z>, p = z + beta p); M = I: z === r
+    const nk_precond* Mp = (o->M && o->M->kind != NK_PRECOND_NONE) ? o->M : nullptr;
+    double* zr = r;
+    if (Mp) {
+        NK_TRY(ws_vec(ws, &ws->mr));
+        zr = ws->mr;
+    }
+    double unused = 0.0;
     NK_TRY(launch_fill(c, n, x, 0.0));
     NK_TRY(launch_copy(c, n, r, b));
-    NK_TRY(launch_copy(c, n, p, r));
+    if (Mp) NK_TRY(apply_precond(c, A.p, Mp, A, n, zr, r, false, &unused));
+    NK_TRY(launch_copy(c, n, p, zr));
     Red rg{};
-    NK_TRY(launch_sumsq(c, n, r, &rg));
+    if (Mp) NK_TRY(launch_dot(c, n, r, zr, &rg));
+    else NK_TRY(launch_sumsq(c, n, r, &rg));
     double gamma = 0.0;
     NK_TRY(host_scalar(c, rg, 0, &gamma));
     double rNorm = std::sqrt(gamma);
@@ -553,6 +598,11 @@ int cg(nk_workspace* ws, Op& A, const double* b, const nk_krylov_opts* o, nk_kry
         const double alpha = gamma / pAp;
         Red rn{};
         NK_TRY(launch_cg_update(c, n, alpha, x, r, p, Ap, &rn));  // x += a p ; r -= a Ap ; <r,r>
+        if (Mp) {  // z = M r ; <r, z> (the update's <r,r> partials are not used)
+            rn = Red{};
+            NK_TRY(apply_precond(c, A.p, Mp, A, n, zr, r, false, &unused));
+            NK_TRY(launch_dot(c, n, r, zr, &rn));
+        }
         double gamma_next = 0.0;
         NK_TRY(host_scalar(c, rn, 0, &gamma_next));
         rNorm = std::sqrt(gamma_next);
@@ -563,7 +613,7 @@ int cg(nk_workspace* ws, Op& A, const double* b, const nk_krylov_opts* o, nk_kry
             const double beta = gamma_next / gamma;
             pNorm2 = gamma_next + beta * beta * pNorm2;
             gamma = gamma_next;
-            NK_TRY(launch_cg_direction(c, n, beta, p, r));  // p = r + beta p
+            NK_TRY(launch_cg_direction(c, n, beta, p, zr));  // p = z + beta p
         }
         iter++;
         tired = iter >= itmax;
@@ -651,7 +701,7 @@ int nk_workspace_destroy(nk_workspace* ws) {
     nk_ctx* c = ws->c;
     for (double* v : ws->V) nk_vec_free(c, v);
     for (double* v : ws->Z) nk_vec_free(c, v);
-    for (double* v : {ws->x, ws->w, ws->w2, ws->xr, ws->p})
+    for (double* v : {ws->x, ws->w, ws->w2, ws->xr, ws->p, ws->mr, ws->mw})
         if (v) nk_vec_free(c, v);
     for (hipEvent_t e : ws->col_ready)
         if (e) (void)hipEventDestroy(e);

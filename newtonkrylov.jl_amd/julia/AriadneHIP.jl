@@ -322,6 +322,7 @@ struct NkKrylovOpts
     u_norm::Float64   # 0: computed by the solve
     u_update::Ptr{Float64}  # C_NULL: workspace.x holds the step (Ariadne applies u .-= d itself)
     N::Ptr{Cvoid}           # nk_precond* right preconditioner, C_NULL: none
+    M::Ptr{Cvoid}           # nk_precond* left preconditioner, C_NULL: none
 end
 struct NkKrylovStats
     niter::Int64
@@ -333,9 +334,9 @@ struct NkKrylovStats
     u_norm::Float64
 end
 
-# --------------------------------------------------------------------------- right preconditioners (N)
-# Ariadne passes `N` (a factory called with the step's JacobianOperator, src/Ariadne.jl:318-333) to
-# krylov_solve!.  The device counterparts of examples/bratu.jl:119-157:
+# --------------------------------------------------------------------------- preconditioners (N, M)
+# Ariadne passes `N` and `M` (factories called with the step's JacobianOperator, src/Ariadne.jl:318-333)
+# to krylov_solve!.  The device counterparts of examples/bratu.jl:119-157 (usable as N or as M):
 #   N = hip_jacobi                           1 ./ diag(J)
 #   N = hip_ilu0, krylov_kwargs = (; ldiv = true)   for  N = (J) -> ilu(collect(J))
 #   N = (J) -> HipGmresPreconditioner(J, 5)  the GmresPreconditioner (algo = :fgmres)
@@ -392,19 +393,25 @@ function Krylov.krylov_solve!(ws::HipKrylovWorkspace, J::HipJacobian, b::HipVect
                               restart::Bool = false, reorthogonalization::Bool = false, itmax::Integer = 0,
                               atol::Real = sqrt(eps(Float64)), rtol::Real = sqrt(eps(Float64)),
                               M = nothing, N = nothing, ldiv::Bool = false, kwargs...)
-    # Ariadne forwards M = M(J) when the caller gives one (src/Ariadne.jl:327-329): the device GMRES has
-    # no left preconditioner, so refuse it instead of silently solving without it
-    M === nothing || error("AriadneHIP: a left preconditioner M is not supported by the device GMRES (use N)")
+    # Ariadne forwards N = N(J) and M = M(J) when the caller gives them (src/Ariadne.jl:323-329): the
+    # device GMRES / FGMRES applies both (right N, left M); the device CG takes M only
     isempty(kwargs) || error("AriadneHIP: unsupported Krylov keyword(s) $(join(keys(kwargs), ", "))")
-    ldiv && !(N isa HipDiagPreconditioner && N.kind == NK_PRECOND_ILU0) &&
-        error("ldiv = true: the HIP path takes factorisations (hip_ilu0) for N")
-    Nc = Ref(N === nothing ? NkPrecond(0, C_NULL, C_NULL, C_NULL, C_NULL, 0) : nkprecond(N))
+    for P in (N, M)
+        P === nothing || P isa HipPreconditioner ||
+            error("AriadneHIP: preconditioners are device objects (hip_jacobi, hip_ilu0, HipGmresPreconditioner)")
+        ldiv && P !== nothing && !(P isa HipDiagPreconditioner && P.kind == NK_PRECOND_ILU0) &&
+            error("ldiv = true: the HIP path takes factorisations (hip_ilu0) for N and M")
+    end
+    nullprec = NkPrecond(0, C_NULL, C_NULL, C_NULL, C_NULL, 0)
+    Nc = Ref(N === nothing ? nullprec : nkprecond(N))
+    Mc = Ref(M === nothing ? nullprec : nkprecond(M))
     st = Ref{NkKrylovStats}()
     hl = Ref{Int64}(0)
     F0 = jvmode(J) == NK_JV_FD ? J.res.ptr : Ptr{Float64}(C_NULL)
-    GC.@preserve Nc N begin   # the raw nk_precond* (and what it points to) stay rooted through the call
+    GC.@preserve Nc N Mc M begin   # the raw nk_precond* (and what they point to) stay rooted through the call
         Np = N === nothing ? Ptr{Cvoid}(C_NULL) : Ptr{Cvoid}(Base.unsafe_convert(Ptr{NkPrecond}, Nc))
-        opts = NkKrylovOpts(restart, reorthogonalization, itmax, jvmode(J), atol, rtol, 0.0, 0.0, C_NULL, Np)
+        Mp = M === nothing ? Ptr{Cvoid}(C_NULL) : Ptr{Cvoid}(Base.unsafe_convert(Ptr{NkPrecond}, Mc))
+        opts = NkKrylovOpts(restart, reorthogonalization, itmax, jvmode(J), atol, rtol, 0.0, 0.0, C_NULL, Np, Mp)
         check(ccall((:nk_krylov_solve, libnkhip), Cint,
                     (Ptr{Cvoid}, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ref{NkKrylovOpts}, Ref{NkKrylovStats},
                      Ptr{Float64}, Int64, Ref{Int64}),

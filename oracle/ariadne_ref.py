@@ -142,8 +142,9 @@ class KrylovStats:
 
 
 def gmres(A, b, *, memory=20, restart=False, reorthogonalization=False, atol=SQRT_EPS, rtol=SQRT_EPS, itmax=0,
-          dot=None, n=None):
-    """Krylov.jl gmres! with M = N = I. A: callable v -> A v.
+          dot=None, n=None, M=None):
+    """Krylov.jl gmres! with N = I. A: callable v -> A v; M: the left
+    preconditioner as a callable v -> M v (ldiv = false; None = I): r0 = M w, q = M A V_k.
 
     `dot` (default numpy) lets a caller supply a distributed inner product (all-reduced over
     ranks) and `n` the global length -- the multi-rank protocol test uses both."""
@@ -151,7 +152,8 @@ def gmres(A, b, *, memory=20, restart=False, reorthogonalization=False, atol=SQR
     n = b.size if n is None else n  # global length (itmax = 2n); arrays are this rank's b.size
     x = np.zeros(b.size)
     xr = np.zeros(b.size) if restart else x
-    w = b.copy()
+    Mf = M or (lambda v: v)
+    w = Mf(b.copy())  # r0 = M (b - A 0)
     beta = math.sqrt(dot(w, w))
     rNorm = beta
     hist = [rNorm]
@@ -174,7 +176,7 @@ def gmres(A, b, *, memory=20, restart=False, reorthogonalization=False, atol=SQR
         if restart:
             xr[:] = 0.0
             if npass >= 1:
-                w = b - A(x)
+                w = Mf(b - A(x))
                 nmv += 1
         beta = math.sqrt(dot(w, w))
         z[0] = beta
@@ -184,7 +186,7 @@ def gmres(A, b, *, memory=20, restart=False, reorthogonalization=False, atol=SQR
         inner_tired = False
         while not (solved or inner_tired or breakdown):
             k += 1
-            w = A(V[k - 1])
+            w = Mf(A(V[k - 1]))
             nmv += 1
             col = []
             for i in range(k):
@@ -236,13 +238,16 @@ def gmres(A, b, *, memory=20, restart=False, reorthogonalization=False, atol=SQR
     return x, st, hist
 
 
-def cg(A, b, *, atol=SQRT_EPS, rtol=SQRT_EPS, itmax=0):
-    """Krylov.jl cg! with M = I, radius = 0, linesearch = false."""
+def cg(A, b, *, atol=SQRT_EPS, rtol=SQRT_EPS, itmax=0, M=None):
+    """Krylov.jl cg! with radius = 0, linesearch = false; M: the (SPD) preconditioner as a callable
+    (None = I): z = M r, gamma = <r, z>, p = z + beta p."""
+    Mf = M or (lambda v: v)
     n = b.size
     x = np.zeros(n)
     r = b.copy()
-    p = r.copy()
-    gamma = float(np.dot(r, r))
+    z = Mf(r)
+    p = z.copy()
+    gamma = float(np.dot(r, z))
     rNorm = math.sqrt(gamma)
     hist = [rNorm]
     st = KrylovStats()
@@ -263,7 +268,8 @@ def cg(A, b, *, atol=SQRT_EPS, rtol=SQRT_EPS, itmax=0):
         alpha = gamma / pAp
         x += alpha * p
         r -= alpha * Ap
-        gn = float(np.dot(r, r))
+        z = Mf(r)
+        gn = float(np.dot(r, z))
         rNorm = math.sqrt(gn)
         hist.append(rNorm)
         solved = rNorm <= eps_ or rNorm + 1.0 <= 1.0
@@ -271,7 +277,7 @@ def cg(A, b, *, atol=SQRT_EPS, rtol=SQRT_EPS, itmax=0):
             beta = gn / gamma
             pN2 = gn + beta * beta * pN2
             gamma = gn
-            p = r + beta * p
+            p = z + beta * p
         it += 1
         tired = it >= itmax
     st.niter, st.solved = it, solved

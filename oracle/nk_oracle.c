@@ -74,6 +74,7 @@ typedef struct {
     double atol, rtol;
     int32_t flexible;       /* fgmres! (Z_k = N V_k stored, x += Z y) instead of gmres! (x += N (V y)) */
     const oc_precond* N;    /* right preconditioner or NULL */
+    const oc_precond* M;    /* left preconditioner (Krylov.jl's `M`, ldiv = false) or NULL */
 } oc_krylov_opts;
 
 typedef struct {
@@ -93,6 +94,8 @@ typedef struct {
     int32_t rtol_user;      /* krylov_kwargs carries rtol: it wins over the forcing (Ariadne.jl:330-333) */
     int32_t precond;        /* N factory called per Newton step: OC_PRECOND_NONE / _JACOBI / _GMRES */
     int32_t precond_itmax;  /* OC_PRECOND_GMRES: GmresPreconditioner(J, itmax) */
+    int32_t mprecond;       /* M factory called per Newton step (Ariadne.jl:327-329): same kinds as `precond` */
+    int32_t mprecond_itmax;
 } oc_newton_opts;
 
 typedef struct {
@@ -454,14 +457,16 @@ static void prec_apply(oc_op* A, const oc_precond* N, double* z, const double* v
         oc_ilu0_solve(N->P ? N->P : A->P, N->diag, z, v);
     } else { /* mul!(y, P::GmresPreconditioner, x): sol, _ = gmres(P.J, x; P.itmax); copyto!(y, sol) -- Krylov's
                 gmres defaults: memory 20, no restart, atol = rtol = √eps, x0 = 0 */
-        oc_krylov_opts io = {20, 0, 0, N->itmax, sqrt(DBL_EPSILON), sqrt(DBL_EPSILON), 0, NULL};
+        oc_krylov_opts io = {20, 0, 0, N->itmax, sqrt(DBL_EPSILON), sqrt(DBL_EPSILON), 0, NULL, NULL};
         oc_krylov_stats is;
         memset(&is, 0, sizeof is);
         oc_gmres(A, v, z, &io, &is, NULL, 0, NULL);
     }
 }
 
-/* ------------------------------------------------------------------ GMRES / FGMRES (Krylov.jl 0.10 gmres! / fgmres!, M = I) */
+/* ------------------------------------------------------------------ GMRES / FGMRES (Krylov.jl 0.10 gmres! / fgmres!)
+ * Left preconditioner M (ldiv = false): r0 = M (b - A x), the Arnoldi vector q = M A (N V_k), and
+ * beta / the stopping test measure the preconditioned residual; with M = I, r0 === w and q === w. */
 static void* xrealloc(void* p, size_t sz) { void* q = realloc(p, sz); if (!q) abort(); return q; }
 
 int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_krylov_stats* st,
@@ -477,6 +482,9 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
     double* w = (double*)malloc(sizeof(double) * n);
     double* xr = restart ? (double*)malloc(sizeof(double) * n) : x;
     const oc_precond* N = (o->N && o->N->kind != OC_PRECOND_NONE) ? o->N : NULL;
+    const oc_precond* M = (o->M && o->M->kind != OC_PRECOND_NONE) ? o->M : NULL;
+    double* r0 = M ? (double*)malloc(sizeof(double) * n) : w; /* r0 = M w */
+    double* q = M ? (double*)malloc(sizeof(double) * n) : w;  /* q = M A p */
     const int flex = N && o->flexible;
     double* pv = N ? (double*)malloc(sizeof(double) * n) : NULL; /* gmres!: p = N V_k, and N (V y) */
     int vcap = mem;
@@ -492,8 +500,9 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
     double* R = (double*)calloc((size_t)cap * (cap + 1) / 2, sizeof(double));
 
     oc_fill(n, x, 0.0);
-    oc_copy(n, w, b); /* r0 = b - A*0 */
-    double beta = oc_norm(n, w);
+    oc_copy(n, w, b); /* w = b - A*0 */
+    if (M) prec_apply(A, M, r0, w); /* r0 = M w */
+    double beta = oc_norm(n, r0);
     double rNorm = beta;
     PUSH_HIST(rNorm);
     const double eps_ = o->atol + o->rtol * rNorm;
@@ -520,11 +529,12 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
                 if (npass >= 1) {
                     op_apply(A, w, x, -1.0);
                     oc_axpby(n, 1.0, b, -1.0, w);
+                    if (M) prec_apply(A, M, r0, w);
                 }
             }
-            beta = oc_norm(n, w);
+            beta = oc_norm(n, r0);
             z[0] = beta;
-            oc_divcopy(n, V[0], w, beta);
+            oc_divcopy(n, V[0], r0, beta);
             npass++;
             inner_iter = 0;
             int inner_tired = 0;
@@ -549,18 +559,19 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
                 } else {
                     op_apply(A, w, V[k - 1], 1.0);
                 }
+                if (M) prec_apply(A, M, q, w);
                 for (int i = 1; i <= k; ++i) {
-                    R[nr + i - 1] = oc_dot(n, V[i - 1], w);
-                    oc_axpy(n, -R[nr + i - 1], V[i - 1], w);
+                    R[nr + i - 1] = oc_dot(n, V[i - 1], q);
+                    oc_axpy(n, -R[nr + i - 1], V[i - 1], q);
                 }
                 if (reorth) {
                     for (int i = 1; i <= k; ++i) {
-                        double htmp = oc_dot(n, V[i - 1], w);
+                        double htmp = oc_dot(n, V[i - 1], q);
                         R[nr + i - 1] += htmp;
-                        oc_axpy(n, -htmp, V[i - 1], w);
+                        oc_axpy(n, -htmp, V[i - 1], q);
                     }
                 }
-                double Hbis = oc_norm(n, w);
+                double Hbis = oc_norm(n, q);
                 for (int i = 1; i <= k - 1; ++i) {
                     double Rtmp = c[i - 1] * R[nr + i - 1] + s[i - 1] * R[nr + i];
                     R[nr + i] = s[i - 1] * R[nr + i - 1] - c[i - 1] * R[nr + i];
@@ -587,7 +598,7 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
                         }
                         vcap = nv;
                     }
-                    oc_divcopy(n, V[k], w, Hbis);
+                    oc_divcopy(n, V[k], q, Hbis);
                     z[k] = zeta; /* cap >= k+1 guaranteed by the growth above */
                 }
             }
@@ -622,6 +633,7 @@ done:
     st->n_matvec = A->n_matvec - nmv0;
     if (hist_len) *hist_len = nh;
     free(w);
+    if (M) { free(r0); free(q); }
     if (restart) free(xr);
     for (int i = 0; i < vcap; ++i) free(V[i]);
     if (flex) {
@@ -634,7 +646,8 @@ done:
 #undef PUSH_HIST
 }
 
-/* ------------------------------------------------------------------ CG (Krylov.jl 0.10 cg!, M = I, radius = 0, linesearch = false) */
+/* ------------------------------------------------------------------ CG (Krylov.jl 0.10 cg!, radius = 0, linesearch = false)
+ * Left (= the SPD) preconditioner M: z = M r, gamma = <r, z>, p = z + beta p; M = I: z === r. */
 int oc_cg(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_krylov_stats* st,
           double* hist, int64_t hist_cap, int64_t* hist_len) {
     const int64_t n = oc_n(A->P);
@@ -644,10 +657,13 @@ int oc_cg(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_kryl
     double* r = (double*)malloc(sizeof(double) * n);
     double* p = (double*)malloc(sizeof(double) * n);
     double* Ap = (double*)malloc(sizeof(double) * n);
+    const oc_precond* M = (o->M && o->M->kind != OC_PRECOND_NONE) ? o->M : NULL;
+    double* zr = M ? (double*)malloc(sizeof(double) * n) : r;
     oc_fill(n, x, 0.0);
     oc_copy(n, r, b);
-    oc_copy(n, p, r);
-    double gamma = oc_dot(n, r, r);
+    if (M) prec_apply(A, M, zr, r);
+    oc_copy(n, p, zr);
+    double gamma = oc_dot(n, r, zr);
     double rNorm = sqrt(gamma);
     PUSH_HIST(rNorm);
     st->inconsistent = 0; st->breakdown = 0;
@@ -668,7 +684,8 @@ int oc_cg(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_kryl
             double alpha = gamma / pAp;
             oc_axpy(n, alpha, p, x);
             oc_axpy(n, -alpha, Ap, r);
-            double gamma_next = oc_dot(n, r, r);
+            if (M) prec_apply(A, M, zr, r);
+            double gamma_next = oc_dot(n, r, zr);
             rNorm = sqrt(gamma_next);
             PUSH_HIST(rNorm);
             int mach = (rNorm + 1.0 <= 1.0);
@@ -677,7 +694,7 @@ int oc_cg(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_kryl
                 double beta = gamma_next / gamma;
                 pNorm2 = gamma_next + beta * beta * pNorm2;
                 gamma = gamma_next;
-                oc_axpby(n, 1.0, r, beta, p);
+                oc_axpby(n, 1.0, zr, beta, p);
             }
             iter++;
             tired = iter >= itmax;
@@ -687,6 +704,7 @@ int oc_cg(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_kryl
     }
     st->n_matvec = A->n_matvec - nmv0;
     if (hist_len) *hist_len = nh;
+    if (M) free(zr);
     free(r); free(p); free(Ap);
     return 0;
 #undef PUSH_HIST
@@ -709,6 +727,7 @@ int oc_newton_krylov(const oc_problem* P, double* u, const oc_newton_opts* o, oc
     double* res = (double*)malloc(sizeof(double) * n);
     double* d = (double*)malloc(sizeof(double) * n);
     double* dinv = (o->precond == OC_PRECOND_JACOBI || o->precond == OC_PRECOND_ILU) ? (double*)malloc(sizeof(double) * n) : NULL;
+    double* minv = (o->mprecond == OC_PRECOND_JACOBI || o->mprecond == OC_PRECOND_ILU) ? (double*)malloc(sizeof(double) * n) : NULL;
     oc_op A = {P, o->jv_mode, u, res, 0.0, 0};
     int64_t nres_count = 0;
     oc_residual(P, res, u);
@@ -742,6 +761,20 @@ int oc_newton_krylov(const oc_problem* P, double* u, const oc_newton_opts* o, oc
             Np.kind = OC_PRECOND_GMRES;
         }
         ko.N = Np.kind != OC_PRECOND_NONE ? &Np : NULL;
+        /* M = M(J) (Ariadne.jl:327-329), the same factories */
+        oc_precond Mp = {OC_PRECOND_NONE, o->mprecond_itmax, NULL, P};
+        if (o->mprecond == OC_PRECOND_JACOBI) {
+            oc_jacobian_diag(P, minv, u, 1);
+            Mp.kind = OC_PRECOND_DIAG;
+            Mp.diag = minv;
+        } else if (o->mprecond == OC_PRECOND_ILU) {
+            oc_ilu0_factor(P, u, minv);
+            Mp.kind = OC_PRECOND_ILU0;
+            Mp.diag = minv;
+        } else if (o->mprecond == OC_PRECOND_GMRES) {
+            Mp.kind = OC_PRECOND_GMRES;
+        }
+        ko.M = Mp.kind != OC_PRECOND_NONE ? &Mp : NULL;
         ko.flexible = o->algo == OC_ALGO_FGMRES;
         /* b = copy(res) (Ariadne.jl:338): res is not overwritten by our operator, so pass it directly */
         if (o->algo == OC_ALGO_CG) oc_cg(&A, res, d, &ko, &ks, NULL, 0, NULL);
@@ -766,7 +799,7 @@ int oc_newton_krylov(const oc_problem* P, double* u, const oc_newton_opts* o, oc
     st->n_matvec = A.n_matvec;
     st->n_residual = nres_count;
     st->tol = tol;
-    free(res); free(d); free(dinv);
+    free(res); free(d); free(dinv); free(minv);
     return 0;
 }
 

@@ -53,7 +53,7 @@ class _Precond(C.Structure):
 class _KrylovOpts(C.Structure):
     _fields_ = [("memory", C.c_int32), ("restart", C.c_int32), ("reorthogonalization", C.c_int32),
                 ("itmax", C.c_int32), ("atol", C.c_double), ("rtol", C.c_double), ("flexible", C.c_int32),
-                ("N", C.POINTER(_Precond))]
+                ("N", C.POINTER(_Precond)), ("M", C.POINTER(_Precond))]
 
 
 class _KrylovStats(C.Structure):
@@ -66,7 +66,7 @@ class _NewtonOpts(C.Structure):
                 ("forcing", C.c_int32), ("eta_fixed", C.c_double), ("eta_max", C.c_double),
                 ("gamma", C.c_double), ("algo", C.c_int32), ("jv_mode", C.c_int32),
                 ("krylov", _KrylovOpts), ("rtol_user", C.c_int32), ("precond", C.c_int32),
-                ("precond_itmax", C.c_int32)]
+                ("precond_itmax", C.c_int32), ("mprecond", C.c_int32), ("mprecond_itmax", C.c_int32)]
 
 
 class _NewtonStats(C.Structure):
@@ -320,9 +320,10 @@ def get_threads() -> int:
 
 
 def krylov_solve(P: Problem, u, b, *, algo="gmres", jv="exact", F0=None, memory=20, restart=False,
-                 reorthogonalization=False, itmax=0, atol=SQRT_EPS, rtol=SQRT_EPS, history=True, N=None):
+                 reorthogonalization=False, itmax=0, atol=SQRT_EPS, rtol=SQRT_EPS, history=True, N=None, M=None):
     """One Krylov.jl-style solve of J(u) x = b; returns (x, stats dict, residual-norm history).
-    algo: gmres | fgmres | cg; N: right preconditioner ("diag", d) or ("gmres", itmax)."""
+    algo: gmres | fgmres | cg; N: right preconditioner ("diag", d), ("ilu0", D~) or ("gmres", itmax);
+    M: left preconditioner, the same forms (cg: M is the SPD preconditioner)."""
     u = np.ascontiguousarray(u, dtype=np.float64)
     b = np.ascontiguousarray(b, dtype=np.float64)
     if jv == "fd" and F0 is None:
@@ -330,8 +331,9 @@ def krylov_solve(P: Problem, u, b, *, algo="gmres", jv="exact", F0=None, memory=
     F0 = np.ascontiguousarray(F0 if F0 is not None else u, dtype=np.float64)
     x = np.empty_like(u)
     Np, _keep = _precond(N)
+    Mp, _keepm = _precond(M)
     o = _KrylovOpts(memory, int(restart), int(reorthogonalization), itmax, atol, rtol, int(algo == "fgmres"),
-                    C.pointer(Np) if Np is not None else None)
+                    C.pointer(Np) if Np is not None else None, C.pointer(Mp) if Mp is not None else None)
     st = _KrylovStats()
     cap = (itmax if itmax else 2 * P.n) + 16 if history else 0
     cap = min(cap, 1 << 22)
@@ -347,23 +349,27 @@ def krylov_solve(P: Problem, u, b, *, algo="gmres", jv="exact", F0=None, memory=
 
 def newton_krylov(P: Problem, u0, *, tol_rel=1e-6, tol_abs=1e-12, max_niter=50, forcing="ew", eta=0.1,
                   eta_max=0.999, gamma=0.9, algo="gmres", jv="exact", memory=20, restart=False,
-                  reorthogonalization=False, itmax=0, atol=SQRT_EPS, rtol=None, N=None):
+                  reorthogonalization=False, itmax=0, atol=SQRT_EPS, rtol=None, N=None, M=None):
     """Ariadne newton_krylov! restated (src/Ariadne.jl:288-372). rtol given => krylov_kwargs rtol wins.
     N: a factory called per Newton step -- "jacobi" (1 ./ diag(J(u))) or ("gmres", itmax), the
-    GmresPreconditioner of examples/bratu.jl:139-157."""
+    GmresPreconditioner of examples/bratu.jl:139-157; M: the same factories for the left preconditioner
+    (Ariadne.jl:327-329)."""
     u = np.array(u0, dtype=np.float64, order="C", copy=True)
     fk = {"none": FORCING_NONE, None: FORCING_NONE, "fixed": FORCING_FIXED, "ew": FORCING_EW}[forcing]
     ko = _KrylovOpts(memory, int(restart), int(reorthogonalization), itmax, atol, 0.0 if rtol is None else rtol)
-    pk, pit = PRECOND_NONE, 0
-    if N == "jacobi":
-        pk = PRECOND_JACOBI
-    elif N == "ilu":
-        pk = PRECOND_ILU
-    elif N is not None:
-        pk, pit = PRECOND_GMRES, int(N[1])
+    def factory(F):
+        if F is None:
+            return PRECOND_NONE, 0
+        if F == "jacobi":
+            return PRECOND_JACOBI, 0
+        if F == "ilu":
+            return PRECOND_ILU, 0
+        return PRECOND_GMRES, int(F[1])
+    pk, pit = factory(N)
+    mk, mit = factory(M)
     o = _NewtonOpts(tol_rel, tol_abs, max_niter, fk, eta, eta_max, gamma,
                     _ALGO[algo], JV_FD if jv == "fd" else JV_EXACT, ko,
-                    0 if rtol is None else 1, pk, pit)
+                    0 if rtol is None else 1, pk, pit, mk, mit)
     st = _NewtonStats()
     cap = max_niter + 4
     hist = np.zeros(cap)

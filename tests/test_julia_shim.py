@@ -131,13 +131,13 @@ def test_shim_ccalls_match_header():
 
 def test_shim_binds_the_reference_operator_surface():
     """The shim's entry points for src/Ariadne.jl:48-162: mul! on J, transpose(J), the batched forms,
-    collect(J) -- and the left preconditioner M is refused, not dropped (:327-329)."""
+    collect(J) -- and the left preconditioner M is passed to the solve, not dropped (:327-329)."""
     names = {c[0] for c in shim_ccalls()}
     for sym in ("nk_jv", "nk_jtv", "nk_jv_batched", "nk_jtv_batched", "nk_jacobian_collect", "nk_krylov_solve"):
         assert sym in names
     src = open(SHIM).read()
-    assert "M === nothing || error(" in src
     assert "isempty(kwargs) || error(" in src
-    assert re.search(r"GC\.@preserve Nc N begin.*?ccall\(\(:nk_krylov_solve", src, re.S)
+    assert re.search(r"GC\.@preserve Nc N Mc M begin.*?NkKrylovOpts\(.*?, Np, Mp\).*?ccall\(\(:nk_krylov_solve",
+                     src, re.S)
     for k in ("heat3d", "heat3d_midpoint", "heat3d_trapezoid"):
         assert f"{k} = NK_HEAT3D" in src

@@ -394,3 +394,64 @@ def test_preconditioned_gmres_restatements():
     assert s5["solved"] and s5["niter"] < s0["niter"]
     xs, ss, _ = oc.krylov_solve(P, u0, b, memory=100, itmax=1000, atol=0.0, rtol=1e-13)
     assert ss["solved"] and np.linalg.norm(x5 - xs) <= 1e-8 * np.linalg.norm(xs)
+
+
+# ----------------------------------------------------------------------------- left preconditioner M
+@pytest.mark.parametrize("restart,memory,reorth", [(False, 20, False), (True, 10, False), (True, 8, True)])
+def test_left_preconditioned_gmres_c_matches_python(restart, memory, reorth):
+    """gmres! with M (src/Ariadne.jl:327-329 forwards M = M(J)): r0 = M b, q = M A V_k, the history is
+    the preconditioned residual -- C and numpy restatements agree (Jacobi M)."""
+    P = oc.bratu2d(12, 10)
+    u = oc.sin_ic(P)
+    b = oc.residual(P, u)
+    d = oc.jacobian_diag(P, u, reciprocal=True)
+    kw = dict(memory=memory, restart=restart, reorthogonalization=reorth, atol=1e-12, rtol=1e-10, itmax=120)
+    x_c, st_c, h_c = oc.krylov_solve(P, u, b, M=("diag", d), **kw)
+    A = lambda v: oc.jv_exact(P, u, v.reshape(P.shape)).ravel()
+    x_p, st_p, h_p = ar.gmres(A, b.ravel(), M=lambda v: d.ravel() * v, **kw)
+    assert st_c["niter"] == st_p.niter and st_c["solved"] == st_p.solved
+    assert np.allclose(h_c[: memory + 1], h_p[: memory + 1], rtol=1e-8, atol=0)
+    assert h_c[0] == pytest.approx(np.linalg.norm(d * b), rel=1e-14)  # beta = ||M b||
+    assert _rel(x_c.ravel(), x_p) < 1e-8
+    # M only changes the Krylov space: x still solves J x = b
+    assert _rel(oc.jv_exact(P, u, x_c).ravel(), b.ravel()) < 1e-7
+
+
+def test_left_ilu_is_exact_for_bratu1d():
+    """For the tridiagonal 1D J, ILU(0) is the exact LU: M = J^-1, so M A = I and left-preconditioned
+    GMRES converges in one Arnoldi step to x = J^-1 b (known answer)."""
+    P = oc.bratu1d(400)
+    u = oc.sin_ic(P)
+    b = oc.residual(P, u)
+    D = oc.ilu0_factor(P, u)
+    x, st, h = oc.krylov_solve(P, u, b, M=("ilu0", D), atol=0.0, rtol=1e-10)
+    assert st["solved"] and st["niter"] == 1
+    assert _rel(oc.jv_exact(P, u, x), b) < 1e-8
+    xn, stn, _ = oc.krylov_solve(P, u, b, N=("ilu0", D), atol=0.0, rtol=1e-10)
+    assert stn["niter"] == 1 and _rel(x, xn) < 1e-8
+
+
+def test_preconditioned_cg_c_matches_python():
+    """cg! with M: z = M r, gamma = <r, z>.  The Bratu J is negative definite, so the SPD M is
+    -1 ./ diag(J); the Jacobi M cuts the iterations on a variable-diagonal problem."""
+    P = oc.bratu1d(300)
+    u = 3.0 * oc.sin_ic(P)
+    b = oc.residual(P, u)
+    m = -oc.jacobian_diag(P, u, reciprocal=True)
+    assert np.all(m > 0)
+    x_c, st_c, h_c = oc.krylov_solve(P, u, b, algo="cg", atol=1e-12, rtol=1e-10, M=("diag", m))
+    A = lambda v: oc.jv_exact(P, u, v)
+    x_p, st_p, h_p = ar.cg(A, b.copy(), atol=1e-12, rtol=1e-10, M=lambda v: m * v)
+    assert st_c["niter"] == st_p.niter and st_c["solved"]
+    np.testing.assert_allclose(h_c[:20], h_p[:20], rtol=1e-8)
+    assert _rel(x_c, x_p) < 1e-6
+    assert _rel(oc.jv_exact(P, u, x_c), b) < 1e-6
+
+
+def test_newton_left_preconditioned_bratu1d(golden_dir):
+    """newton_krylov!(…; M = ilu) on config 1: every Krylov solve takes one step (M = J^-1)."""
+    g = np.load(os.path.join(golden_dir, "bratu1d_n1000.npz"))
+    P = oc.bratu1d(1000)
+    u, st = oc.newton_krylov(P, oc.sin_ic(P), M="ilu")
+    assert st["solved"] and st["inner_iterations"] == st["outer_iterations"]
+    assert np.max(np.abs(u - g["true_sol"])) < 3e-4
