@@ -112,6 +112,19 @@ def parse():
     return ap.parse_args()
 
 
+def copy_calibration(ctx, n=1 << 27, reps=5):
+    """Achievable HBM streaming rate on this GPU: the library's plain copy kernel (nkb_copy) over two
+    1 GiB vectors, run after the timed region (GB/s on 16 B per element)."""
+    import ctypes as C
+
+    lib = ah.load()
+    lib.nkb_copy.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.POINTER(C.c_double)]
+    us = C.c_double()
+    if lib.nkb_copy(ctx.handle, n, reps, C.byref(us)) != 0 or us.value <= 0:
+        return None
+    return 16.0 * n / (us.value * 1e-6) / 1e9
+
+
 def free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -414,6 +427,7 @@ def main():
         elapsed = float(tt.item())
     prof = ctx.prof_read() if not args.no_prof else {}
     ctx.prof_enable(0)
+    copy_gbs = copy_calibration(ctx) if rank == 0 else None
 
     # Two byte counts per kernel class (nk_prof_entry): `bytes` = the operand bytes the kernel moves
     # through the memory hierarchy (every load / store it issues, served by L2, the Infinity Cache or
@@ -476,6 +490,7 @@ def main():
                 "traffic": round(ach * tb / bpl, 1) if tb else None,
                 "traffic_bytes_per_launch": tb,
                 "traffic_source": os.path.relpath(args.traffic_json, ROOT) if tb else None,
+                "frac_of_copy": round(ach / copy_gbs, 4) if copy_gbs else None,
                 "bytes_per_launch": bpl, "avg_us": round(1e6 * bpl / (ach * 1e9), 3),
                 "avg_us_timed": 1e3 * v["ms"] / v["timed"], "timed_launches": v["timed"]}
 
@@ -514,6 +529,11 @@ def main():
             "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in list(kernels.items())[:8]},
             "newton_n_res": last.stats.n_res if last else None,
+            # what plain streaming reaches on this GPU (roofline.frac_of_copy divides by it): the spec
+            # 8 TB/s is not reachable by any access pattern (MI355X_MICROARCH.md: 6.29 TB/s best measured)
+            "calibration": {"copy_gbs": round(copy_gbs, 1) if copy_gbs else None,
+                            "what": "y = x over 2 x 1 GiB (HBM, beyond the Infinity Cache), 16 B per lane, "
+                                    "mean of 5 launches, after the timed region"},
         }
         if world == 1 and not args.no_cpu_baseline and not args.global_n:
             # the CPU share this process is given: OMP_NUM_THREADS (the GPU box sets it to its per-GPU share

@@ -1423,6 +1423,39 @@ extern "C" int nkb_stencil3d_ex(nk_ctx* c, int64_t n, int64_t nz, int kind, int 
     return NK_OK;
 }
 
+// any stencil kind at nx x ny x nz (nz = 1 for the 2D kinds): mode / epi, rows (2D: rows per tile;
+// 3D: planes per z-march; 0: the launcher's choice), variant bits `fast` -- microseconds per launch
+extern "C" int nkb_stencil_kind(nk_ctx* c, int kind, int64_t nx, int64_t ny, int64_t nz, int mode, int epi, int rows,
+                                int fast, int reps, double* us_out) {
+    using namespace nk;
+    if (!c || nx < 3 || ny < 3 || nz < 1 || reps < 1 || !us_out || kind < NK_BRATU2D || kind > NK_HEAT3D_TRAPEZOID)
+        return NK_E_ARG;
+    const double h = 1.0 / (nx + 1);
+    nk_problem p{kind, NK_BC_ZERO, nx, ny, nz, h, h, h, 3.51382, 0.01, 1e-6, nullptr, nullptr, 0.5};
+    double *u = nullptr, *v = nullptr, *F0 = nullptr, *aux = nullptr, *out = nullptr, *un = nullptr;
+    p.un = reinterpret_cast<const double*>(1);  // geometry only while allocating
+    for (double** q : {&u, &v, &F0, &aux, &out, &un}) NK_TRY(nk_vec_alloc(c, &p, q));
+    for (double* q : {u, v, F0, aux, un}) NK_TRY(launch_fill(c, nx * ny * nz, q, 0.25));
+    p.un = un;
+    StencilIn in{&p, mode, epi, out, u, v, F0, aux, 1e-6};
+    Red r{};
+    hipEvent_t a, b;
+    NK_HIP(c, hipEventCreate(&a));
+    NK_HIP(c, hipEventCreate(&b));
+    NK_TRY(launch_stencil_ex(c, in, &r, rows, fast));
+    NK_HIP(c, hipEventRecord(a, c->stream));
+    for (int k = 0; k < reps; ++k) NK_TRY(launch_stencil_ex(c, in, &r, rows, fast));
+    NK_HIP(c, hipEventRecord(b, c->stream));
+    NK_HIP(c, hipEventSynchronize(b));
+    float ms = 0.f;
+    NK_HIP(c, hipEventElapsedTime(&ms, a, b));
+    *us_out = 1e3 * ms / reps;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    for (double* q : {u, v, F0, aux, out, un}) nk_vec_free(c, q);
+    return NK_OK;
+}
+
 // x update of a GMRES cycle with k basis vectors (xr = 0 start, Newton update fused into u, ||u||
 // partials), with U elements per thread (NK_UPD_U) -- average microseconds per launch
 extern "C" int nkb_update_x(nk_ctx* c, int64_t n, int k, int u_elems, int reps, double* us_out) {

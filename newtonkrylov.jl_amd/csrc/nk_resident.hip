@@ -207,7 +207,9 @@ __device__ __forceinline__ void res_prefetch(const ResArgs& A, ResPre<B>& P, int
 // register slots -- so the pass starts on the V_i lines the previous pass loaded last as its V_{i+1}
 // (the LDS slots, ~5 MB per XCD: still in its L2).  The register slots keep one (ascending) order:
 // a second, reversed copy of their unrolled loop costs scratch.
-template <int RV, int B, bool PRE, int NTM = 0>
+// NTS: the streamed remainder's q and V_{i+1} go non-temporal too (V_i always is), so the Infinity
+// Cache keeps only the resident part's V_{i+1} for its re-read as the next pass's V_i
+template <int RV, int B, bool PRE, int NTM = 0, bool NTS = false>
 __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx2* lq, int t, double mh, int64_t lo,
                                            int64_t hi, ResPre<B>& P, int64_t base, int64_t ss, bool rev = false) {
     const int tid = threadIdx.x;
@@ -290,23 +292,31 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
         dx2* q2 = reinterpret_cast<dx2*>(A.q);
         const dx2* v2 = reinterpret_cast<const dx2*>(A.V[t]);
         const dx2* w2 = reinterpret_cast<const dx2*>(A.V[next ? t + 1 : t]);
+        auto ld = [](const dx2* p) {
+            if constexpr (NTS) return __builtin_nontemporal_load(p);
+            else return *p;
+        };
+        auto st = [](dx2* p, const dx2 v) {
+            if constexpr (NTS) __builtin_nontemporal_store(v, p);
+            else *p = v;
+        };
         int64_t e = lo + (int64_t)(RV + rl) * kResThreads + tid;
         for (; e + kResThreads < hi; e += 2 * kResThreads) {
             const int64_t e1 = e + kResThreads;
-            dx2 a0 = q2[e], a1 = q2[e1];
+            dx2 a0 = ld(q2 + e), a1 = ld(q2 + e1);
             const dx2 b0 = __builtin_nontemporal_load(v2 + e), b1 = __builtin_nontemporal_load(v2 + e1);
-            const dx2 c0 = w2[e], c1 = w2[e1];
+            const dx2 c0 = ld(w2 + e), c1 = ld(w2 + e1);
             upd(a0, b0, c0);
             upd(a1, b1, c1);
-            q2[e] = a0;
-            q2[e1] = a1;
+            st(q2 + e, a0);
+            st(q2 + e1, a1);
         }
         if (e < hi) {
-            dx2 a0 = q2[e];
+            dx2 a0 = ld(q2 + e);
             const dx2 b0 = __builtin_nontemporal_load(v2 + e);
-            const dx2 c0 = w2[e];
+            const dx2 c0 = ld(w2 + e);
             upd(a0, b0, c0);
-            q2[e] = a0;
+            st(q2 + e, a0);
         }
     };
     if (rev) lds();
@@ -317,7 +327,7 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
 }
 
 template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false, bool ALT = false,
-          int NTM = 0>
+          int NTM = 0, bool NTS = false>
 __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     extern __shared__ dx2 lq[];  // rl x 256 double2
     __shared__ double sh[kShN];
@@ -367,7 +377,7 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
             A.col[t] = h;
             if (A.colh) A.colh[t] = h;
         }
-        const double acc = res_pass<RV, B, PRE, NTM>(A, S, lq, t, -h, lo, hi, P, base, ss, ALT && (t & 1));
+        const double acc = res_pass<RV, B, PRE, NTM, NTS>(A, S, lq, t, -h, lo, hi, P, base, ss, ALT && (t & 1));
         if (t + 1 < A.np) res_prefetch<RV, B, PRE, NTM>(A, P, t + 1, base, ss);
         const double part = block_sum<kResThreads>(acc, sh);
         if (A.tstamp && tid == 0) A.tstamp[((size_t)t * G + blockIdx.x) * 2] = wall_clock64();
@@ -398,9 +408,9 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
 }
 
 template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false, bool ALT = false,
-          int NTM = 0>
+          int NTM = 0, bool NTS = false>
 bool res_attr(size_t lds) {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV, B, PRE, JV, ALT, NTM>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV, B, PRE, JV, ALT, NTM, NTS>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
 }
 }  // namespace
@@ -438,7 +448,8 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
                  res_attr<64>(lmax) && res_attr<89>(lmax) && res_attr<89, 4, true>(lmax) && res_attr<89, 4>(lmax) &&
                  res_attr<89, 6, false, true>(lmax) && res_attr<0, 8, false, true>(lmax) &&
                  res_attr<89, 6, false, false, true>(lmax) && res_attr<89, 6, false, false, false, 1>(lmax) &&
-                 res_attr<89, 6, false, false, false, 2>(lmax);
+                 res_attr<89, 6, false, false, false, 2>(lmax) && res_attr<89, 6, false, false, false, 0, true>(lmax) &&
+                 res_attr<89, 4, true, false, false, 0, true>(lmax);
             int per_cu = 0;  // residency: at least one block of the largest variant per CU
             ok = ok && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_mgs_res<89>),
                                                                     kResThreads, lmax) == hipSuccess && per_cu >= 1;
@@ -467,6 +478,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
     A.n2 = n >> 1;
     A.np = np;
     int xv = -1;  // experimental variant (kernel-variant bench)
+    bool streamed = false;  // part of q streams through memory (partial residency)
     {  // every block's chunk must hold its rv + rl resident slots in full (the kernel does not predicate them)
         const int64_t G = c->res_blocks, n2 = n >> 1;
         const int64_t ns = (n2 + kResThreads - 1) / kResThreads;
@@ -477,7 +489,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         static const int rv_env = env_int("NK_RES_RV", -1);
         int rl = std::min(slots, rl_env >= 0 ? std::min(rl_env, c->res_rl) : c->res_rl);  // LDS first
         const bool explicit_rv = rv >= 0 || rv_env >= 0;  // a caller's choice skips the benefit test below
-        if (rv >= 1000) {  // kernel-variant bench: 1000 + {0: 89 slots, batches of 4 + prefetch across the hand-off; 1: same, no prefetch; 2: alternating slot order; 3: V_i cached; 4: V_{i+1} non-temporal}
+        if (rv >= 1000) {  // kernel-variant bench: 1000 + {0: 89 slots, batches of 4 + prefetch across the hand-off; 1: same, no prefetch; 2: alternating slot order; 3: V_i cached; 4: V_{i+1} non-temporal; 5: streamed remainder non-temporal (NTS); 6: 0 + 5}
             xv = rv - 1000;
             rv = 89;
         }
@@ -503,6 +515,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         // V_{k+1} straight from the registers only when all of q is resident (no streamed slot; a
         // partial last slot is streamed)
         const bool full = n2 % kResThreads == 0 && (ns + G - 1) / G <= rv + A.rl;
+        streamed = !full;
         static const int vout_env = env_int("NK_RES_VOUT", 1);
         if (vout && *vout && !(full && vout_env)) *vout = nullptr;
         A.vout = vout ? *vout : nullptr;
@@ -535,6 +548,14 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         A.mb0 = c->mb_epoch + 1;
         c->mb_epoch += nx_;
     }
+    // NK_RES_NTS (default on): with a streamed remainder its q and V_{i+1} go non-temporal, so the
+    // Infinity Cache keeps the resident part's V_{i+1} for the next pass (kbench_res: -2..3 % per pass at
+    // half residency, -2..7 % at a quarter; config-4 slab bench +2.4 %, heat 8192^2 +3.9 %); NK_RES_PRE
+    // (default on): batches of 4 with the first one loaded across the hand-off (-1.5 % per pass at
+    // k = 30, full residency; 4096^2 bench +0.6 %).  Same per-element arithmetic and accumulation order
+    // in every variant: bit-identical results.
+    static const int nts_env = env_int("NK_RES_NTS", 1);
+    static const int pre_env = env_int("NK_RES_PRE", 1);
     static const int noxchg = env_int("NK_RES_NOXCHG", 0);
     A.noxchg = noxchg;
     static const int poll1 = env_int("NK_RES_POLL1", 1);
@@ -570,6 +591,12 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
             else if (xv == 2) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, true>), g, b, lds, c->stream, A);
             else if (xv == 3) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, false, 1>), g, b, lds, c->stream, A);
             else if (xv == 4) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, false, 2>), g, b, lds, c->stream, A);
+            else if (xv == 5) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, false, 0, true>), g, b, lds, c->stream, A);
+            else if (xv == 6) hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, false, 0, true>), g, b, lds, c->stream, A);
+            else if (streamed && nts_env && pre_env)
+                hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, false, 0, true>), g, b, lds, c->stream, A);
+            else if (streamed && nts_env) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, false, 0, true>), g, b, lds, c->stream, A);
+            else if (pre_env) hipLaunchKernelGGL((k_mgs_res<89, 4, true>), g, b, lds, c->stream, A);
             else hipLaunchKernelGGL(k_mgs_res<89>, g, b, lds, c->stream, A);
             break;
         default: hipLaunchKernelGGL(k_mgs_res<32>, g, b, lds, c->stream, A); break;

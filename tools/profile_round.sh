@@ -8,6 +8,8 @@
 #      (bench.py applies a PMC file only to the workload AND size it was measured on)
 #   3. the bench lines themselves (every workload tag; CPU baseline on the default sizes)
 #   4. (not with "quick") in-process kernel-variant A/B (tools/kbench.py, tools/kbench_res.py)
+# PROFILE_PARTS="trace pmc bench" and PROFILE_TAGS="bratu2d heat2d ..." select a subset (one gpurun
+# call stays well inside its time limit).
 set -e -o pipefail
 R=${1:-r02}
 MODE=${2:-full}
@@ -17,11 +19,14 @@ DST=$OUT/profiles  # only gpurun_out/ comes back from the box: copy to profiles/
 mkdir -p "$OUT" "$DST"
 export TMPDIR=/tmp
 
+PARTS=${PROFILE_PARTS:-trace pmc bench}
+if [[ " $PARTS " == *" trace "* ]]; then
 echo "[profile] kernel trace"
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
     -- python3 "$ROOT/bench.py" --no-cpu-baseline > "$OUT/bench_traced.log" 2>&1)
 cp "$OUT/trace/run_kernel_stats.csv" "$DST/kernel_stats_bench.csv"
 grep '^{"metric"' "$OUT/bench_traced.log" | tail -n 1 > "$DST/bench_under_rocprof.json"
+fi
 
 # workload tag -> bench.py arguments, and the size part of its PMC file name (W.side in bench.py)
 declare -A WARGS=(
@@ -38,8 +43,9 @@ declare -A WFILE=(
     [heat2d_trapezoid_periodic]="heat2d_trapezoid_periodic_8192" [heat3d_midpoint]="heat3d_midpoint_512"
     [bratu2d_slab]="bratu2d_16384x2048" [heat3d_slab]="heat3d_512x64"
 )
-TAGS="bratu2d heat2d heat3d heat2d_trapezoid_periodic heat3d_midpoint bratu2d_slab heat3d_slab"
+TAGS=${PROFILE_TAGS:-bratu2d heat2d heat3d heat2d_trapezoid_periodic heat3d_midpoint bratu2d_slab heat3d_slab}
 
+if [[ " $PARTS " == *" pmc "* ]]; then
 for w in $TAGS; do
     for ctr in FETCH_SIZE WRITE_SIZE; do
         echo "[profile] $w $ctr"
@@ -50,14 +56,19 @@ for w in $TAGS; do
     python3 tools/pmc_traffic.py "$OUT/pmc_${w}_FETCH_SIZE/run_counter_collection.csv" \
         "$OUT/pmc_${w}_WRITE_SIZE/run_counter_collection.csv" "$DST/pmc_traffic_${WFILE[$w]}.json"
 done
+fi
 
+if [[ " $PARTS " == *" bench "* ]]; then
 echo "[profile] bench lines"
 for w in $TAGS; do
-    timeout -k 10 300 python3 bench.py ${WARGS[$w]} --traffic-json "$DST/pmc_traffic_${WFILE[$w]}.json" \
+    TJ="$DST/pmc_traffic_${WFILE[$w]}.json"
+    [ -f "$TJ" ] || TJ="profiles/$R/pmc_traffic_${WFILE[$w]}.json"  # PMC passes of an earlier call
+    timeout -k 10 300 python3 bench.py ${WARGS[$w]} --traffic-json "$TJ" \
         > "$OUT/bench_$w.log" 2>&1
     tail -n 1 "$OUT/bench_$w.log" > "$DST/bench_$w.json"
 done
-cp "$DST/bench_bratu2d.json" "$DST/bench.json"
+[ -f "$DST/bench_bratu2d.json" ] && cp "$DST/bench_bratu2d.json" "$DST/bench.json"
+fi
 
 if [ "$MODE" = full ]; then
     echo "[profile] kernel variants"
