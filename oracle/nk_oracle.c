@@ -109,7 +109,10 @@ typedef struct {
 static inline int64_t oc_n(const oc_problem* P) { return P->nx * P->ny * P->nz; }
 
 /* ------------------------------------------------------------------ BLAS-1 (Krylov k* primitives) */
-#define OC_CHUNK 8192
+/* reduction chunk (fixed-order partial sums; oc_set_chunk changes the order to measure how much a
+ * different summation order alone moves a result -- the GPU's reduction tree differs from this one) */
+static int64_t OC_CHUNK = 8192;
+void oc_set_chunk(int64_t c) { OC_CHUNK = c > 0 ? c : 8192; }
 
 double oc_dot(int64_t n, const double* x, const double* y) {
     int64_t nch = (n + OC_CHUNK - 1) / OC_CHUNK;

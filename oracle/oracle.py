@@ -110,6 +110,7 @@ def lib():
         L.oc_ilu0_factor.argtypes = [C.POINTER(_Problem), P, P]
         L.oc_ilu0_solve.argtypes = [C.POINTER(_Problem), P, P, P]
         L.oc_set_threads.argtypes = [C.c_int]
+        L.oc_set_chunk.argtypes = [C.c_int64]
         L.oc_get_threads.restype = C.c_int
         for name in ("oc_axpy",):
             getattr(L, name).argtypes = [I64, D, P, P]
@@ -309,6 +310,11 @@ def sym_givens(a: float, b: float):
 
 def ew_forcing(eta, tol, n_res, n_res_prior, eta_max=0.999, gamma=0.9):
     return lib().oc_ew_forcing(eta_max, gamma, eta, tol, n_res, n_res_prior)
+
+
+def set_chunk(c: int):
+    """Reduction chunk of the oracle's dot / norm (default 8192): another summation order."""
+    lib().oc_set_chunk(int(c))
 
 
 def set_threads(t: int):

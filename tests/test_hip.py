@@ -195,12 +195,38 @@ def test_gmres_matches_oracle(ctx, restart, memory, reorth, jv):
         assert np.allclose(h[m], ho[m], rtol=1e-5)
         assert np.max(np.abs(x - xo)) <= 1e-7 * np.max(np.abs(xo))
     else:
-        # the FD operator carries O(sqrt(eps)) truncation + O(eps/eps_fd) rounding noise, so two
-        # implementations drift apart once restarts feed the noise back (eps itself differs by an
-        # ulp: ||u|| is reduced in a different order)
-        assert np.allclose(h[: memory + 1], ho[: memory + 1], rtol=1e-6, atol=0)
-        assert np.allclose(h, ho, rtol=1e-2)
-        assert np.max(np.abs(x - xo)) <= 1e-2 * np.max(np.abs(xo))
+        # The FD quotient divides rounding differences by eps_fd ~ 1e-8: ocml's exp vs glibc's (<= 1 ulp
+        # of F) reaches the operator at ~1e-8 relative and restarts feed it back.  The oracle against
+        # itself with F0 perturbed by <= 1 ulp moves this history by ~1e-2 where ||r|| > 1e-4 ||r0||
+        # (tests/test_oracle.py::test_fd_gmres_sensitivity); the GPU sits at 3.7e-3, x at 6.5e-8
+        # (tools/fd_probe.py).  The heat FD solve (no exp) matches to 1e-13: test_heat_fd_gmres_matches_oracle.
+        assert np.allclose(h[: memory + 1], ho[: memory + 1], rtol=1e-7, atol=0)
+        k = ho > 1e-2 * ho[0]
+        assert np.allclose(h[k], ho[k], rtol=1e-4, atol=0)
+        k = ho > 1e-6 * ho[0]
+        assert np.allclose(h[k], ho[k], rtol=2e-2, atol=0)
+        assert np.max(np.abs(x - xo)) <= 2e-6 * np.max(np.abs(xo))
+
+
+@pytest.mark.parametrize("restart,memory", [(True, 10), (False, 20)])
+def test_heat_fd_gmres_matches_oracle(ctx, restart, memory):
+    """FD-GMRES on a heat residual (G_Euler! of heat_2D.jl: no exp, so F agrees bit for bit): only the
+    reductions' summation order separates the GPU from the oracle -- histories to 1e-9, x to 1e-11."""
+    n = 24
+    u0 = oc.sin_ic(oc.bratu2d(n)) + 0.1 * np.random.default_rng(1).standard_normal((n, n))
+    un = u0.copy()
+    P = oc.heat2d_euler(n, un=un)
+    u = u0 + 0.01
+    b = oc.residual(P, u)
+    kw = dict(restart=restart, atol=1e-12, rtol=1e-9, itmax=150)
+    x, st, F0 = device_solve(P, u, b, memory=memory, jv="fd", **kw)
+    np.testing.assert_array_equal(F0, b)  # the heat residual is bit-identical
+    xo, so, ho = oc.krylov_solve(P, u, b, jv="fd", F0=F0, memory=memory, **kw)
+    assert st.niter == so["niter"] and st.n_matvec == so["n_matvec"]
+    h = np.array(st.residuals)
+    k = ho > 1e-6 * ho[0]
+    assert np.allclose(h[k], ho[k], rtol=1e-9, atol=0)
+    assert np.max(np.abs(x - xo)) <= 1e-11 * np.max(np.abs(xo))
 
 
 def test_cg_matches_oracle(ctx):

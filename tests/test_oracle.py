@@ -455,3 +455,31 @@ def test_newton_left_preconditioned_bratu1d(golden_dir):
     u, st = oc.newton_krylov(P, oc.sin_ic(P), M="ilu")
     assert st["solved"] and st["inner_iterations"] == st["outer_iterations"]
     assert np.max(np.abs(u - g["true_sol"])) < 3e-4
+
+
+def test_fd_gmres_sensitivity():
+    """Why Bratu FD-GMRES parity is a tolerance, not bits: the oracle against ITSELF.  Changing only the
+    summation order of its reductions (chunk 7 instead of 8192) moves a restarted FD-GMRES(10) history
+    on 2D Bratu 24^2 by ~1e-9; perturbing F0 = F(u) by at most 1 ulp per element -- what ocml's exp vs
+    glibc's does to the GPU's F -- moves it by ~1e-2 where ||r|| > 1e-4 ||r0|| (the FD quotient divides
+    the perturbation by eps_fd ~ 1e-8 and the restarts feed it back).  The GPU run of the same solve
+    sits at 3.7e-3 (tests/test_hip.py::test_gmres_matches_oracle, tools/fd_probe.py)."""
+    P = oc.bratu2d(24)
+    u = oc.sin_ic(P)
+    b = oc.residual(P, u)
+    kw = dict(restart=True, memory=10, atol=1e-12, rtol=1e-9, itmax=150)
+    F0p = b + np.random.default_rng(0).choice([-1.0, 0.0, 1.0], b.shape) * np.spacing(np.abs(b))
+    try:
+        x1, s1, h1 = oc.krylov_solve(P, u, b, jv="fd", F0=b, **kw)
+        oc.set_chunk(7)
+        x2, s2, h2 = oc.krylov_solve(P, u, b, jv="fd", F0=b, **kw)
+    finally:
+        oc.set_chunk(8192)
+    x3, s3, h3 = oc.krylov_solve(P, u, b, jv="fd", F0=F0p, **kw)
+    assert s1["niter"] == s2["niter"] == s3["niter"] == 150
+    k = h1 > 1e-4 * h1[0]
+    d_order = np.max(np.abs(h2[k] - h1[k]) / h1[k])
+    d_ulp = np.max(np.abs(h3[k] - h1[k]) / h1[k])
+    assert 0 < d_order < 1e-7, d_order
+    assert d_ulp > 1e-4, d_ulp
+    np.testing.assert_allclose(h3[:11], h1[:11], rtol=1e-7)  # the first cycle is still tight
