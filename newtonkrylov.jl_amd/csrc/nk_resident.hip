@@ -477,6 +477,14 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
     A.err = c->res_err_dev;
     A.n2 = n >> 1;
     A.np = np;
+    // NK_RES_NTS (default on): with a streamed remainder its q and V_{i+1} go non-temporal, so the
+    // Infinity Cache keeps the resident part's V_{i+1} for the next pass (kbench_res: -2..3 % per pass at
+    // half residency, -2..7 % at a quarter; config-4 slab bench +2.4 %, heat 8192^2 +3.9 %); NK_RES_PRE
+    // (default on): batches of 4 with the first one loaded across the hand-off (-1.5 % per pass at
+    // k = 30, full residency; 4096^2 bench +0.6 %).  Same per-element arithmetic and accumulation order
+    // in every variant: bit-identical results.
+    static const int nts_env = env_int("NK_RES_NTS", 1);
+    static const int pre_env = env_int("NK_RES_PRE", 1);
     int xv = -1;  // experimental variant (kernel-variant bench)
     bool streamed = false;  // part of q streams through memory (partial residency)
     {  // every block's chunk must hold its rv + rl resident slots in full (the kernel does not predicate them)
@@ -505,13 +513,14 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         if (xv < 0) rv = pick;
         else if (rv > slots) return 1;
         A.rl = std::min(rl, slots - rv);
-        // worth it from two passes on (a one-pass sweep only adds q's load + store) while a fifth of q
+        // worth it from two passes on (a one-pass sweep only adds q's load + store) while a tenth of q
         // or more is resident (tools/kbench_res.py per pass vs the chain: 4096^2 1.28x at k = 2,
-        // 1.8x from k = 16; 2 x 4096^2 (half resident) 1.18-1.48x; 8192^2 (a quarter) 1.08-1.13x;
-        // 512^3 (an eighth) 1.01x)
+        // 1.8x from k = 16; 2 x 4096^2 (half resident) 1.40-1.52x; 8192^2 (a quarter) 1.16-1.18x;
+        // 512^3 (an eighth) 1.06-1.09x -- with the streamed remainder non-temporal, NK_RES_NTS; 1.01x
+        // at 512^3 without it, hence a fifth then)
         const int64_t chunk = std::max<int64_t>(1, ns / G);
         const double f = (double)(rv + A.rl) / (double)chunk;  // resident fraction of q
-        if (!explicit_rv && (np < 2 || f < 0.2)) return 1;
+        if (!explicit_rv && (np < 2 || f < (nts_env ? 0.1 : 0.2))) return 1;
         // V_{k+1} straight from the registers only when all of q is resident (no streamed slot; a
         // partial last slot is streamed)
         const bool full = n2 % kResThreads == 0 && (ns + G - 1) / G <= rv + A.rl;
@@ -548,14 +557,6 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         A.mb0 = c->mb_epoch + 1;
         c->mb_epoch += nx_;
     }
-    // NK_RES_NTS (default on): with a streamed remainder its q and V_{i+1} go non-temporal, so the
-    // Infinity Cache keeps the resident part's V_{i+1} for the next pass (kbench_res: -2..3 % per pass at
-    // half residency, -2..7 % at a quarter; config-4 slab bench +2.4 %, heat 8192^2 +3.9 %); NK_RES_PRE
-    // (default on): batches of 4 with the first one loaded across the hand-off (-1.5 % per pass at
-    // k = 30, full residency; 4096^2 bench +0.6 %).  Same per-element arithmetic and accumulation order
-    // in every variant: bit-identical results.
-    static const int nts_env = env_int("NK_RES_NTS", 1);
-    static const int pre_env = env_int("NK_RES_PRE", 1);
     static const int noxchg = env_int("NK_RES_NOXCHG", 0);
     A.noxchg = noxchg;
     static const int poll1 = env_int("NK_RES_POLL1", 1);
