@@ -1,4 +1,4 @@
-"""Multi-rank protocol of the slab decomposition, on CPU with gloo (world_size 2 and 3).
+"""Multi-rank protocol of the slab decomposition, on CPU with gloo (world_size 2, 3 and 8: the driver's node size).
 
 libnkhip.so's distributed path (nk_dist.cpp) does exactly two things beyond the single-GPU code:
 before every stencil application it fills the two ghost planes of the input vector with the
@@ -120,7 +120,7 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_slab_protocol_matches_single_domain(tmp_path, world):
     out = str(tmp_path / "dist.npz")
     mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
