@@ -1,5 +1,5 @@
-"""CPU tests of bench.py's rank launcher (no GPU work: --launch-probe makes every rank report what it
-was given and exit before any device call).
+"""Tests of bench.py's rank launcher: on CPU with --launch-probe (every rank reports what it was given
+and exits before any device call), and one end-to-end two-rank run on the GPU.
 
 `python bench.py --gpus N` without a torch.distributed.run environment must start N ranks itself
 (one process per GPU, LOCAL_RANK = device), pass every argument through, and return the ranks'
@@ -9,6 +9,8 @@ import json
 import os
 import subprocess
 import sys
+
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BENCH = os.path.join(ROOT, "bench.py")
@@ -53,3 +55,23 @@ def test_world_size_mismatch_is_an_error():
     p = run(["--gpus", "2", "--launch-probe", "0"], env={"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode == 2
     assert "--gpus 2" in p.stderr
+
+
+@pytest.mark.gpu
+def test_two_rank_bench_runs_end_to_end():
+    """`bench.py --gpus 2` from one command, on the GPU: two ranks (one GPU each when the box has two,
+    else sharing the one GPU over the IPC mailbox with a small slab), the whole distributed path
+    (slab ghost rows, reductions across ranks), one JSON line with n_gpus 2."""
+    import _nkpath  # noqa: F401
+    import ariadne_hip as ah
+
+    args = ["--gpus", "2", "--side", "512", "--steps", "1", "--warmup", "1", "--no-prof", "--no-cpu-baseline"]
+    if ah.device_count() < 2:
+        args += ["--transport", "mailbox"]
+    p = run(args, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(line) == 1
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["matvecs_per_step"] == 309
+    assert d["config"]["reductions"] in ("peer mailbox (IPC/xGMI)", "ncclAllReduce")
