@@ -42,7 +42,7 @@ struct nk_workspace {
     double* mw = nullptr;    // left preconditioner: w = A N V_k before q = M w (gmres)
     double* hdev = nullptr;  // device Hessenberg columns: 2 slots of (2*cap + 2) doubles (steps k, k+1 in flight)
     double* ydev = nullptr;  // device y (cap doubles)
-    double* bdev = nullptr;  // device beta of the current cycle (V_1 = r0 / beta is fused into step 1)
+    double* bdev = nullptr;  // device divisor of V_1 = r0 / rNorm (fused into step 1)
     bool u_fused = false;    // the last solve applied opts.u_update inside its final x update
     double* hpin = nullptr;  // pinned host mirror of hdev (2 slots), written by the kernels themselves
     double* hpin_dev = nullptr;  // hpin's device address
@@ -434,7 +434,9 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         }
         Range cycle_range("gmres_cycle");
         z[0] = beta;
-        NK_TRY(launch_fill(c, 1, ws->bdev, beta));  // V1 = r0 / beta happens inside step 1's Jv
+        // kdivcopy!(n, V[1], r0, rNorm) inside step 1's Jv: Krylov.jl divides by rNorm, which is beta on
+        // the first pass and, after a restart, the previous cycle's estimate |zeta| (z[1] = beta regardless)
+        NK_TRY(launch_fill(c, 1, ws->bdev, rNorm));
         v1_src = src;
         npass++;
         inner_iter = 0;

@@ -180,7 +180,7 @@ def gmres(A, b, *, memory=20, restart=False, reorthogonalization=False, atol=SQR
                 nmv += 1
         beta = math.sqrt(dot(w, w))
         z[0] = beta
-        V.append(w / beta)
+        V.append(w / rNorm)  # kdivcopy!(n, V[1], r0, rNorm): after a restart, the previous cycle's estimate
         npass += 1
         k = 0
         inner_tired = False

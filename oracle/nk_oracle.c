@@ -537,7 +537,9 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
             }
             beta = oc_norm(n, r0);
             z[0] = beta;
-            oc_divcopy(n, V[0], r0, beta);
+            /* kdivcopy!(n, V[1], r0, rNorm): Krylov.jl divides by rNorm -- beta on the first pass, after a
+             * restart the previous cycle's estimate |zeta|, not the beta just computed */
+            oc_divcopy(n, V[0], r0, rNorm);
             npass++;
             inner_iter = 0;
             int inner_tired = 0;

@@ -154,7 +154,11 @@ def test_user_heat_gmres_matches_builtin(ctx, jv):
     assert hists[0][0] == hists[1][0]
     # late entries sit ~1e-10 below ||b||: there the two reduction orders show at ~1e-16 of ||b||
     np.testing.assert_allclose(hists[0][1], hists[1][1], rtol=1e-12, atol=1e-14 * hists[1][1][0])
-    np.testing.assert_allclose(xs[0], xs[1], rtol=1e-11, atol=1e-14 * np.abs(xs[1]).max())
+    # the two paths sum their dot partials in different block orders (fused stencil epilogue vs
+    # k_user_epi); restarted FD-GMRES amplifies such 1e-16 differences (tests/test_oracle.py::
+    # test_fd_gmres_sensitivity), so x agrees to 3e-11 there, to 1e-11 with the exact tangent
+    tol = (1e-11, 1e-14) if jv == "exact" else (1e-9, 1e-12)
+    np.testing.assert_allclose(xs[0], xs[1], rtol=tol[0], atol=tol[1] * np.abs(xs[1]).max())
 
 
 def test_user_bratu_newton_matches_oracle(ctx):
