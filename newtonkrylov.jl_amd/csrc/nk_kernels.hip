@@ -695,10 +695,18 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         vec = (p->nx % 2 == 0) ? 2 : 1;
         if (((fast & 4) || vec_pref == 4) && p->nx % 4 == 0 && !per) vec = 4;
         A.tiles_x = (int)((p->nx + kBlock * vec - 1) / (kBlock * vec));
-        static const int target = env_int("NK_ST_BLOCKS", 2048);
+        // rows per tile: about 1024 tiles, between 8 and 32 rows (4096^2: 32-row tiles, FD Jv 121.3 ->
+        // 114.8 us and +0.6 % on the bench, profiles/r02/ab_st_blocks.log; 8192^2 heat: 32 rows are
+        // as fast as 64 for the FD Jv and 3 % faster for the residual, kbench_st2d_8192.log), and
+        // never more tiles than the reduction slot holds partials
+        static const int target = env_int("NK_ST_BLOCKS", 1024);
         int64_t rows = (p->ny * A.tiles_x + target - 1) / target;
         static const int min_rows = env_int("NK_ST_MINROWS", 8);
+        static const int max_rows = env_int("NK_ST_MAXROWS", 32);
+        if (rows > max_rows) rows = max_rows;
         if (rows < min_rows) rows = min_rows;
+        const int64_t cap_rows = (p->ny * A.tiles_x + (kRedCap - 3)) / (kRedCap - 2);
+        if (rows < cap_rows) rows = cap_rows;
         if (rows_override > 0) rows = rows_override;
         if (rows > p->ny) rows = p->ny;
         A.rows = (int)rows;
