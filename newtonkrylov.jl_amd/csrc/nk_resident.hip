@@ -209,7 +209,7 @@ __device__ __forceinline__ void res_prefetch(const ResArgs& A, ResPre<B>& P, int
 // a second, reversed copy of their unrolled loop costs scratch.
 // NTS: the streamed remainder's q and V_{i+1} go non-temporal too (V_i always is), so the Infinity
 // Cache keeps only the resident part's V_{i+1} for its re-read as the next pass's V_i
-template <int RV, int B, bool PRE, int NTM = 0, bool NTS = false>
+template <int RV, int B, bool PRE, int NTM = 0, bool NTS = false, int LB = 4>
 __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx2* lq, int t, double mh, int64_t lo,
                                            int64_t hi, ResPre<B>& P, int64_t base, int64_t ss, bool rev = false) {
     const int tid = threadIdx.x;
@@ -278,8 +278,27 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
             upd(a, b, cc);
             lq[s * kResThreads + tid] = a;
         };
+        auto oneB = [&](int s) {  // LDS slots s .. s+LB-1, all their loads issued first
+            dx2 bv[LB], cv[LB];
+#pragma unroll
+            for (int u = 0; u < LB; ++u) {
+                bv[u] = ldv<NTM>(vl + (s + u) * ss);
+                cv[u] = ldw<NTM>(wl + (s + u) * ss);
+            }
+#pragma unroll
+            for (int u = 0; u < LB; ++u) {
+                dx2 a = lq[(s + u) * kResThreads + tid];
+                upd(a, bv[u], cv[u]);
+                lq[(s + u) * kResThreads + tid] = a;
+            }
+        };
         const int r4 = rl / 4 * 4;
-        if (!rev) {
+        if (!rev && LB != 4) {
+            const int rb = rl / LB * LB;
+            for (int s = 0; s < rb; s += LB) oneB(s);
+            for (int s = rb; s < r4; s += 4) one4(s, false);
+            for (int s = r4; s < rl; ++s) one(s);
+        } else if (!rev) {
             for (int s = 0; s < r4; s += 4) one4(s, false);
             for (int s = r4; s < rl; ++s) one(s);
         } else {
@@ -327,7 +346,7 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
 }
 
 template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false, bool ALT = false,
-          int NTM = 0, bool NTS = false>
+          int NTM = 0, bool NTS = false, int LB = 4>
 __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     extern __shared__ dx2 lq[];  // rl x 256 double2
     __shared__ double sh[kShN];
@@ -377,7 +396,7 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
             A.col[t] = h;
             if (A.colh) A.colh[t] = h;
         }
-        const double acc = res_pass<RV, B, PRE, NTM, NTS>(A, S, lq, t, -h, lo, hi, P, base, ss, ALT && (t & 1));
+        const double acc = res_pass<RV, B, PRE, NTM, NTS, LB>(A, S, lq, t, -h, lo, hi, P, base, ss, ALT && (t & 1));
         if (t + 1 < A.np) res_prefetch<RV, B, PRE, NTM>(A, P, t + 1, base, ss);
         const double part = block_sum<kResThreads>(acc, sh);
         if (A.tstamp && tid == 0) A.tstamp[((size_t)t * G + blockIdx.x) * 2] = wall_clock64();
@@ -408,9 +427,9 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
 }
 
 template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false, bool ALT = false,
-          int NTM = 0, bool NTS = false>
+          int NTM = 0, bool NTS = false, int LB = 4>
 bool res_attr(size_t lds) {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV, B, PRE, JV, ALT, NTM, NTS>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mgs_res<RV, B, PRE, JV, ALT, NTM, NTS, LB>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
 }
 }  // namespace
@@ -449,7 +468,8 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
                  res_attr<89, 6, false, true>(lmax) && res_attr<0, 8, false, true>(lmax) &&
                  res_attr<89, 6, false, false, true>(lmax) && res_attr<89, 6, false, false, false, 1>(lmax) &&
                  res_attr<89, 6, false, false, false, 2>(lmax) && res_attr<89, 6, false, false, false, 0, true>(lmax) &&
-                 res_attr<89, 4, true, false, false, 0, true>(lmax);
+                 res_attr<89, 4, true, false, false, 0, true>(lmax) && res_attr<89, 2, true>(lmax) &&
+                 res_attr<89, 4, true, false, false, 0, false, 8>(lmax) && res_attr<89, 4, true, false, false, 0, false, 6>(lmax);
             int per_cu = 0;  // residency: at least one block of the largest variant per CU
             ok = ok && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_mgs_res<89>),
                                                                     kResThreads, lmax) == hipSuccess && per_cu >= 1;
@@ -497,7 +517,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         static const int rv_env = env_int("NK_RES_RV", -1);
         int rl = std::min(slots, rl_env >= 0 ? std::min(rl_env, c->res_rl) : c->res_rl);  // LDS first
         const bool explicit_rv = rv >= 0 || rv_env >= 0;  // a caller's choice skips the benefit test below
-        if (rv >= 1000) {  // kernel-variant bench: 1000 + {0: 89 slots, batches of 4 + prefetch across the hand-off; 1: same, no prefetch; 2: alternating slot order; 3: V_i cached; 4: V_{i+1} non-temporal; 5: streamed remainder non-temporal (NTS); 6: 0 + 5}
+        if (rv >= 1000) {  // kernel-variant bench: 1000 + {0: 89 slots, batches of 4 + prefetch across the hand-off; 1: same, no prefetch; 2: alternating slot order; 3: V_i cached; 4: V_{i+1} non-temporal; 5: streamed remainder non-temporal (NTS); 6: 0 + 5; 8: batches of 2 + prefetch (batches of 6 + prefetch spill); 9 / 10: 0 with LDS slots in batches of 8 / 6}
             xv = rv - 1000;
             rv = 89;
         }
@@ -594,6 +614,9 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
             else if (xv == 4) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, false, 2>), g, b, lds, c->stream, A);
             else if (xv == 5) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, false, 0, true>), g, b, lds, c->stream, A);
             else if (xv == 6) hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, false, 0, true>), g, b, lds, c->stream, A);
+            else if (xv == 8) hipLaunchKernelGGL((k_mgs_res<89, 2, true>), g, b, lds, c->stream, A);
+            else if (xv == 9) hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, false, 0, false, 8>), g, b, lds, c->stream, A);
+            else if (xv == 10) hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, false, 0, false, 6>), g, b, lds, c->stream, A);
             else if (streamed && nts_env && pre_env)
                 hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, false, 0, true>), g, b, lds, c->stream, A);
             else if (streamed && nts_env) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, false, 0, true>), g, b, lds, c->stream, A);
