@@ -222,6 +222,10 @@ typedef struct nk_krylov_opts {
                                      `M = M(J)` Ariadne forwards (src/Ariadne.jl:327-329).  gmres!/fgmres!:
                                      r0 = M (b - A x), q = M A N V_k, the stopping test on ||M r||;
                                      cg!: the SPD preconditioner (z = M r, gamma = <r, z>)                   */
+    int32_t f0_is_residual;       /* 1: F0 is exactly F(u) as nk_residual / nk_residual_norm computed it for this
+                                     u and problem (the Newton loop's res): the 2D FD operator recomputes F(u)
+                                     from the u it loads anyway instead of reading F0 -- bit-identical, 8 B/pt
+                                     less traffic.  0 (the default): F0 is read                           */
 } nk_krylov_opts;
 
 typedef struct nk_krylov_stats {

@@ -60,7 +60,7 @@ class nk_krylov_opts(C.Structure):
     _fields_ = [("restart", C.c_int32), ("reorthogonalization", C.c_int32), ("itmax", C.c_int32),
                 ("jv_mode", C.c_int32), ("atol", C.c_double), ("rtol", C.c_double), ("b_norm", C.c_double),
                 ("u_norm", C.c_double), ("u_update", C.c_void_p), ("N", C.c_void_p),
-                ("M", C.c_void_p)]
+                ("M", C.c_void_p), ("f0_is_residual", C.c_int32)]
 
 
 class nk_krylov_stats(C.Structure):

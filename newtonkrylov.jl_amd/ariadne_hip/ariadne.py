@@ -284,7 +284,7 @@ def newton_krylov_(F_: DeviceResidual, u: DeviceArray, p=None, res: DeviceArray 
             kwargs["N"] = N if hasattr(N, "as_c") else N(J)
         if M is not None and "M" not in kwargs:
             kwargs["M"] = M if hasattr(M, "as_c") else M(J)
-        krylov_solve_(workspace, J, res, _b_norm=n_res, _u_norm=u_norm, _u_update=u, **kwargs)
+        krylov_solve_(workspace, J, res, _b_norm=n_res, _u_norm=u_norm, _u_update=u, _f0_is_residual=True, **kwargs)
         n_matvec += workspace.stats.n_matvec
         u_norm = workspace.stats.u_norm
         n_res_prior = n_res

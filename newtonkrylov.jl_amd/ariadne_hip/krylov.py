@@ -157,11 +157,13 @@ def krylov_workspace(algo, kc: KrylovConstructor) -> KrylovWorkspace:
 
 def krylov_solve_(ws: KrylovWorkspace, J, b: DeviceArray, *, restart=False, reorthogonalization=False,
                   atol=SQRT_EPS, rtol=SQRT_EPS, itmax=0, history=False, verbose=0, M=None, N=None, ldiv=False,
-                  _b_norm=0.0, _u_norm=0.0, _u_update=None, **unknown):
+                  _b_norm=0.0, _u_norm=0.0, _u_update=None, _f0_is_residual=False, **unknown):
     """krylov_solve!(workspace, J, b; kwargs...) for a JacobianOperator J on device vectors.
     (_b_norm / _u_norm: norms the Newton loop already holds -- ||F(u)|| and ||u|| -- so the solve
     does not stream b and u once more just to recompute them.  _u_update = u: the Newton update
-    u .-= x is fused into the last pass; ws.x is then not stored and ws.stats.u_norm = ||u||.)"""
+    u .-= x is fused into the last pass; ws.x is then not stored and ws.stats.u_norm = ||u||.
+    _f0_is_residual: J.res is exactly F(u) as the device residual computed it -- the Newton loop's res
+    -- so the 2D FD stencils recompute it instead of loading it; bit-identical.)"""
     if unknown:
         raise TypeError(f"unsupported Krylov keyword(s): {sorted(unknown)}")
     for name, P in (("N", N), ("M", M)):
@@ -180,7 +182,8 @@ def krylov_solve_(ws: KrylovWorkspace, J, b: DeviceArray, *, restart=False, reor
                                float(atol), float(rtol), float(_b_norm), float(_u_norm),
                                _u_update.ptr if _u_update is not None else None,
                                C.cast(C.pointer(N.as_c()), C.c_void_p) if N is not None else None,
-                               C.cast(C.pointer(M.as_c()), C.c_void_p) if M is not None else None)
+                               C.cast(C.pointer(M.as_c()), C.c_void_p) if M is not None else None,
+                               int(bool(_f0_is_residual)))
     st = _lib.nk_krylov_stats()
     cap = ((int(itmax) or 4096) + 64) if history else 0
     hist = (C.c_double * max(cap, 1))()

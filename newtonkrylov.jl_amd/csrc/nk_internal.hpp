@@ -217,6 +217,8 @@ struct StencilIn {
     double* vout = nullptr;        // ... and v / h is stored here (fused kdivcopy!)
     bool xchg_v = false;           // v's ghost planes are stale: exchange them (in the stencil itself when
                                    // the peer mailbox is up, else halo_exchange before the launch)
+    bool f0r = false;              // FD: F0 is exactly F(u) as this library's residual kernel computed it, so
+                                   // the 2D kernels recompute it in registers instead of loading it
 };
 // returns the partial sums (when epi != EPI_NONE) in *red
 int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red);

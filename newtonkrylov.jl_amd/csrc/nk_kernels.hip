@@ -733,6 +733,15 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         A.rows = (int)planes;
         grid = A.tiles_x * A.tiles_y * (int)((p->nz + planes - 1) / planes);
     }
+    // FD with F0 recomputed from u (2D, VEC <= 2: k_st2d<..., F0R>); never with the `fast` reciprocals,
+    // which would change F(u) against the residual kernel that stored F0.  NK_F0R: 1 (default) for the
+    // heat kinds, whose F(u) costs a few flops (8192^2 FD Jv 728 -> 612 us, bench +3.3 %); 2 for Bratu
+    // too, where the second exp per point makes the kernel compute-bound (4096^2: the Arnoldi-step Jv
+    // unchanged, the restart residual 108 -> 126 us: profiles/r02/ab_f0r.log); 0 never
+    static const int f0r_env = env_int("NK_F0R", 1);
+    const bool f0r = f0r_env && in.f0r && g.dim == 2 && in.mode == MODE_JFD && vec <= 2 && !(fast & 1) &&
+                     (f0r_env >= 2 || nk_is_heat(p->kind));
+    A.f0r = f0r ? 1 : 0;
     if (in.xchg_v) {
         // v's ghost planes: through the peers' inboxes inside this launch (halo_tile_exchange: only the
         // tiles at the slab's ends fetch, the rest of the grid never waits) when the peer mailbox is up,
@@ -759,7 +768,7 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     int words = 1;  // out
     if (in.mode == MODE_RES) words += 1 + (heat ? 1 : 0);
     else if (in.mode == MODE_JEXACT) words += 1 + (heat ? 0 : 1);
-    else words += 3 + (heat ? 1 : 0);
+    else words += 3 + (heat ? 1 : 0) - (f0r ? 1 : 0);
     if (in.epi == EPI_RESID || (in.epi == EPI_DOT && in.aux)) words += 1;
     if (in.vout) words += 1;  // fused kdivcopy!: V_k is written
     const double bytes = 8.0 * words * (double)g.n;

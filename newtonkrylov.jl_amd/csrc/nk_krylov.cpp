@@ -181,6 +181,7 @@ struct Op {
     const double* F0;
     double unorm;
     int64_t n_matvec = 0;
+    bool f0r = false;  // F0 is this library's F(u): the 2D FD stencils recompute it instead of loading it
 
     // out = J v  (+ epilogue).  vnorm: ||v|| for the FD step (1 for Arnoldi basis vectors).
     // With vdiv/vout the operator is applied to v / *vdiv, which is also stored to vout.
@@ -202,6 +203,7 @@ struct Op {
         }
         StencilIn in{p, mode == NK_JV_FD ? MODE_JFD : MODE_JEXACT, epi, out, u, v, F0, aux, eps, vdiv, vout};
         in.xchg_v = true;  // v's ghost planes: exchanged by the stencil launch itself where it can
+        in.f0r = f0r;
         return launch_stencil(c, in, red);
     }
     int64_t ws_n() const { return p->nx * p->ny * p->nz; }
@@ -729,6 +731,7 @@ int nk_krylov_solve(nk_workspace* ws, const nk_problem* p, const double* u, cons
     *st = nk_krylov_stats{};
     Range solve_range(ws->algo == NK_ALGO_CG ? "cg_solve" : "gmres_solve");
     Op A{c, p, o->jv_mode, u, F0, 0.0};
+    A.f0r = o->f0_is_residual != 0 && o->jv_mode == NK_JV_FD;
     NK_TRY(halo_exchange(c, p, u));  // u (and u_n) are constant during the solve: one exchange
     NK_TRY(exchange_un(c, p));
     if (o->jv_mode == NK_JV_FD) {

@@ -75,6 +75,7 @@ int nk_newton_krylov(nk_ctx* c, const nk_problem* p, double* u, double* res, con
         ko.b_norm = n_res;  // b = F(u): its norm is the n_res just computed
         ko.u_norm = u_norm;
         ko.u_update = u;    // u .-= d fused into the solve's last pass (d = workspace.x is not stored)
+        ko.f0_is_residual = 1;  // res = F(u) was just computed by nk_residual_norm
         nk_krylov_stats ks{};
         const double* F0 = ko.jv_mode == NK_JV_FD ? res : nullptr;
         if ((rc = nk_krylov_solve(ws, p, u, F0, res, &ko, &ks, nullptr, 0, nullptr)) != NK_OK) break;

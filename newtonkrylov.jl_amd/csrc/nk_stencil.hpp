@@ -29,6 +29,7 @@ struct KArgs {
     double alpha;        // G_Midpoint! α
     int nw;              // 3D: rows (waves) per tile
     int lds3;            // 3D: y-neighbour rows through LDS (k_st3l) instead of per-wave loads (k_st3d)
+    int f0r;             // 2D FD: F0 = F(u) recomputed from the u rows already loaded (k_st2d<..., F0R>)
     // ghost planes of v through the peers' inboxes inside this launch (halo_tile_exchange): the rank
     // has a lower / upper neighbour whose boundary patch this launch fetches itself
     int hx_lo, hx_hi;
@@ -473,7 +474,11 @@ __device__ __forceinline__ LR x_nbrs(double cfirst, double clast, double e, doub
 // Block = 256 threads x VEC columns (one row segment), marching A.rows rows in y.  Pipeline: at
 // iteration j the raw loads of row j+2 and the centre operands of row j+1 are issued, row j+1's
 // raw data (issued one iteration earlier) is cooked, and row j is computed from registers.
-template <int KIND, int MODE, int EPI, int VEC, bool PER = false>
+// F0R (FD only): F0 = F(u) is recomputed here -- the u rows are loaded for w = u + eps v anyway -- with
+// exactly the residual kernel's arithmetic (the u field cooked as MODE_RES, the same Laplacian and
+// point_value), so (F(w) - F(u)) / eps is bit-identical to loading the F0 that kernel stored, and
+// 8 B/pt less is read.  Valid only when F0 IS that residual of this u (the Newton loop's res).
+template <int KIND, int MODE, int EPI, int VEC, bool PER = false, bool F0R = false>
 __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     __shared__ double sh[kShN];
     KArgs A = A0;
@@ -509,19 +514,38 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     }
     constexpr bool kU = MODE == MODE_JEXACT && KIND == NK_BRATU2D;
     constexpr bool kUn = KIND == NK_HEAT2D_EULER && MODE != MODE_JEXACT;
-    constexpr bool kF0 = MODE == MODE_JFD;
+    constexpr bool kF0 = MODE == MODE_JFD && !F0R;
+    constexpr bool kR = MODE == MODE_JFD && F0R;  // the u field, cooked as the residual kernel cooks it
     constexpr bool kAx = EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID;
+    auto as_res = [](const RawRow<MODE, VEC>& r) {  // the u part of a raw FD row, as a residual row
+        RawRow<MODE_RES, VEC> q;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            q.a[k] = r.a[k];
+            q.g[k] = r.g[k];
+        }
+        q.ae = r.ae;
+        q.ae2 = r.ae2;
+        q.ge = r.ge;
+        q.ge2 = r.ge2;
+        return q;
+    };
     constexpr bool vout = MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS);  // fused kdivcopy!: V_k stored
     double acc = 0.0;
     if (y0 < ny) {
         // rows y0-1 (ghost plane when y0 = 0) and y0 cooked up front; row y0+1 raw in flight
-        Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(
-            A, ib_lo ? load_raw_ib<MODE, VEC, kG>(A, ib_lo, (y0 - 1) * nx + xc, xc)
-                     : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 - 1) * nx + xc, (y0 - 1) * nx + xc + de, (y0 - 1) * nx + xc + de2),
-            act, false, false);
-        Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(
-            A, load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, y0 * nx + xc, y0 * nx + xc + de, y0 * nx + xc + de2), act, edge_ok,
-            edge_ok2);
+        const RawRow<MODE, VEC> rm0 =
+            ib_lo ? load_raw_ib<MODE, VEC, kG>(A, ib_lo, (y0 - 1) * nx + xc, xc)
+                  : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 - 1) * nx + xc, (y0 - 1) * nx + xc + de, (y0 - 1) * nx + xc + de2);
+        const RawRow<MODE, VEC> rc0 =
+            load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, y0 * nx + xc, y0 * nx + xc + de, y0 * nx + xc + de2);
+        Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(A, rm0, act, false, false);
+        Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, rc0, act, edge_ok, edge_ok2);
+        Field<VEC> um{}, uc_{};  // F0R: the u field of rows j-1, j
+        if constexpr (kR) {
+            um = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res(rm0), act, false, false);
+            uc_ = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res(rc0), act, edge_ok, edge_ok2);
+        }
         RawRow<MODE, VEC> rp =
             (ib_hi && y0 + 1 == ny) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, (y0 + 1) * nx + xc, xc)
                                     : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 + 1) * nx + xc, (y0 + 1) * nx + xc + de, (y0 + 1) * nx + xc + de2);
@@ -549,6 +573,12 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
             if constexpr (kAx) axn = data_row<VEC>(A.aux, o1, true);
             // ---- cook row j+1 (its loads were issued one iteration ago)
             const Field<VEC> fp = cook<MODE, VEC, SCH, kG, PER>(A, rp, act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
+            Field<VEC> up{};
+            LR un_{};
+            if constexpr (kR) {
+                up = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res(rp), act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
+                un_ = x_nbrs<PER>(uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
+            }
             // ---- compute row j from registers
             const LR xn = x_nbrs<PER>(fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
             const double lft = xn.l, rgt = xn.r;
@@ -573,7 +603,15 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
                         lsumg = lapk(A, fc.g[k], ge, gw, A.hx2, A.ihx2) + lapk(A, fc.g[k], fp.g[k], fm.g[k], A.hy2, A.ihy2);
                     }
                     const double unk = kG ? fc.g[k] : unc.v[k];
-                    double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unk, f0c.v[k], SCH == 1 ? fc.x[k] : c, lsumg);
+                    double f0 = f0c.v[k];
+                    if constexpr (kR) {  // F(u) at this point, as the residual kernel evaluates it
+                        const double uw = (k == 0) ? un_.l : uc_.c[k == 0 ? 0 : k - 1];
+                        const double ue = (k == VEC - 1) ? un_.r : uc_.c[k == VEC - 1 ? k : k + 1];
+                        const double ucc = uc_.c[k];
+                        const double lsu = lapk(A, ucc, ue, uw, A.hx2, A.ihx2) + lapk(A, ucc, up.c[k], um.c[k], A.hy2, A.ihy2);
+                        f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unk, 0.0, SCH == 1 ? uc_.x[k] : ucc, lsumg);
+                    }
+                    double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unk, f0, SCH == 1 ? fc.x[k] : c, lsumg);
                     acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[k] : ax.v[k], acc);
                     val.v[k] = r;
                 }
@@ -587,6 +625,10 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
             }
             fm = fc;
             fc = fp;
+            if constexpr (kR) {
+                um = uc_;
+                uc_ = up;
+            }
             rp = rpp;
             uc = ucn;
             unc = uncn;
@@ -943,6 +985,20 @@ void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
             if (per) {
                 if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2, true>), dim3(grid), dim3(kBlock), 0, s, A);
                 else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1, true>), dim3(grid), dim3(kBlock), 0, s, A);
+                return;
+            }
+        }
+        if constexpr (MODE == MODE_JFD) {  // F0 recomputed from u (KArgs::f0r), VEC <= 2
+            if (A.f0r && vec <= 2) {
+                if constexpr (heat_kind<KIND>()) {
+                    if (per) {
+                        if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2, true, true>), dim3(grid), dim3(kBlock), 0, s, A);
+                        else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1, true, true>), dim3(grid), dim3(kBlock), 0, s, A);
+                        return;
+                    }
+                }
+                if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2, false, true>), dim3(grid), dim3(kBlock), 0, s, A);
+                else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1, false, true>), dim3(grid), dim3(kBlock), 0, s, A);
                 return;
             }
         }

@@ -323,6 +323,7 @@ struct NkKrylovOpts
     u_update::Ptr{Float64}  # C_NULL: workspace.x holds the step (Ariadne applies u .-= d itself)
     N::Ptr{Cvoid}           # nk_precond* right preconditioner, C_NULL: none
     M::Ptr{Cvoid}           # nk_precond* left preconditioner, C_NULL: none
+    f0_is_residual::Int32   # 1: J.res is F(J.u) as the device residual computed it (Ariadne's loop: F! just ran)
 end
 struct NkKrylovStats
     niter::Int64
@@ -411,7 +412,10 @@ function Krylov.krylov_solve!(ws::HipKrylovWorkspace, J::HipJacobian, b::HipVect
     GC.@preserve Nc N Mc M begin   # the raw nk_precond* (and what they point to) stay rooted through the call
         Np = N === nothing ? Ptr{Cvoid}(C_NULL) : Ptr{Cvoid}(Base.unsafe_convert(Ptr{NkPrecond}, Nc))
         Mp = M === nothing ? Ptr{Cvoid}(C_NULL) : Ptr{Cvoid}(Base.unsafe_convert(Ptr{NkPrecond}, Mc))
-        opts = NkKrylovOpts(restart, reorthogonalization, itmax, jvmode(J), atol, rtol, 0.0, 0.0, C_NULL, Np, Mp)
+        # Ariadne calls krylov_solve! right after F!(res, u, p): J.res is F(u) from the device residual
+        # (and the FD operator's F(u) is J.res by definition), so the 2D FD stencils may recompute it
+        opts = NkKrylovOpts(restart, reorthogonalization, itmax, jvmode(J), atol, rtol, 0.0, 0.0, C_NULL, Np, Mp,
+                            Int32(J.f isa HipResidual ? 1 : 0))
         check(ccall((:nk_krylov_solve, libnkhip), Cint,
                     (Ptr{Cvoid}, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ref{NkKrylovOpts}, Ref{NkKrylovStats},
                      Ptr{Float64}, Int64, Ref{Int64}),

@@ -1,0 +1,135 @@
+"""GPU tests of the FD operator with F0 recomputed (nk_krylov_opts.f0_is_residual): in the Newton loop
+F0 = res is exactly F(u) as the device residual kernel computed it, so the 2D FD stencils evaluate
+F(u) again from the u rows they load anyway -- the same cooked field, Laplacian and point formula as
+the residual kernel -- instead of reading F0 (8 B/pt less).  The bar is bits: whole restarted
+FD-GMRES solves (Arnoldi steps with the fused V_k = q / h, the restart residual b - J x, the k = 1
+and reorthogonalised steps) with and without the flag give identical histories and iterates, for
+every heat scheme, zero and periodic boundaries, VEC 2 and VEC 1 (odd nx) tiles -- and Bratu, whose
+kernel has the same path but uses it only under NK_F0R=2 (a second exp per point makes it slower)."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import _nkpath  # noqa: F401
+import ariadne_hip as ah
+from oracle import oracle as oc
+
+pytestmark = pytest.mark.gpu
+
+GNAME = {"euler": ah.G_Euler_, "midpoint": ah.G_Midpoint_, "trapezoid": ah.G_Trapezoid_}
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = ah.Context(0)
+    ah.set_default_context(c)
+    yield c
+    c.sync()
+
+
+def case(name, nx, ny, bc="zero"):
+    rng = np.random.default_rng(nx * 7 + ny)
+    if name == "bratu2d":
+        P = oc.bratu2d(nx, ny)
+        u0 = oc.sin_ic(P) + 0.05 * rng.standard_normal(P.shape)
+        return ah.bratu2d_, (P.hx, P.hy, P.lam), u0
+    un = rng.standard_normal((ny, nx))
+    scheme, alpha = (name.split(":") + ["0.5"])[:2]
+    P = oc.heat2d_euler(nx, ny, un=un, scheme=scheme, bc=oc.BC_PERIODIC if bc == "periodic" else oc.BC_ZERO,
+                        alpha=float(alpha))
+    G = GNAME[scheme]
+    if scheme == "midpoint":
+        G = G(alpha=float(alpha))
+    F = G.bind(ah.diffusion_)
+    p = (ah.DeviceArray.from_numpy(un), P.dt, None,
+         (P.a, P.hx, P.hy, ah.bc_periodic_ if bc == "periodic" else ah.bc_zero_), 0.0)
+    return F, p, un + 0.01 * rng.standard_normal(un.shape)
+
+
+def solve(F, p, u0, flag, **kw):
+    u = ah.DeviceArray.from_numpy(u0)
+    res = u.zero()
+    F(res, u, p)
+    ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=kw.pop("memory", 10)))
+    J = ah.JacobianOperator(F, res, u, p, jv="fd")
+    u.ctx.prof_reset()
+    u.ctx.prof_enable(1)
+    ah.krylov_solve_(ws, J, res, history=True, _f0_is_residual=flag, **kw)
+    prof = u.ctx.prof_read()
+    u.ctx.prof_enable(0)
+    out = ws.x.to_numpy(), list(ws.stats.residuals), ws.stats.niter, prof
+    ws.free()
+    return out
+
+
+CASES = [("euler", 130, 67, "zero"), ("euler", 201, 37, "zero"),
+         ("midpoint:0.3", 130, 67, "zero"), ("trapezoid", 129, 40, "zero"), ("euler", 64, 64, "periodic"),
+         ("midpoint", 96, 40, "periodic"), ("trapezoid", 65, 33, "periodic")]
+
+
+@pytest.mark.parametrize("name,nx,ny,bc", CASES)
+@pytest.mark.parametrize("reorth", [False, True])
+def test_f0_recomputed_is_bitwise(ctx, name, nx, ny, bc, reorth):
+    F, p, u0 = case(name, nx, ny, bc)
+    kw = dict(restart=True, memory=10, itmax=35, atol=0.0, rtol=0.0, reorthogonalization=reorth)
+    x0, h0, n0, p0 = solve(F, p, u0, False, **kw)
+    x1, h1, n1, p1 = solve(F, p, u0, True, **kw)
+    assert n0 == n1 == 35
+    assert h0 == h1
+    np.testing.assert_array_equal(x0, x1)
+    # the flag reached the stencils: the FD Jv launches moved 8 B/pt less
+    jv = [k for k in p0 if k.startswith("jv_fd")]
+    assert jv
+    b0 = sum(p0[k]["bytes"] / p0[k]["timed"] * p0[k]["launches"] for k in jv)
+    b1 = sum(p1[k]["bytes"] / p1[k]["timed"] * p1[k]["launches"] for k in jv)
+    launches = sum(p0[k]["launches"] for k in jv)
+    assert b0 - b1 == pytest.approx(8.0 * nx * ny * launches, rel=1e-12)
+
+
+def test_newton_uses_it_and_matches_oracle(ctx):
+    """newton_krylov_ passes the flag (res is F(u)); the FD Newton solve still matches the oracle."""
+    P = oc.bratu2d(48, 40)
+    u0 = oc.sin_ic(P)
+    ref, so = oc.newton_krylov(P, u0, jv="fd", memory=20)
+    u, r = ah.newton_krylov_(ah.bratu2d_, ah.DeviceArray.from_numpy(u0), (P.hx, P.hy, P.lam), jv="fd", memory=20)
+    assert r.solved and so["solved"]
+    assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
+    np.testing.assert_allclose(u.to_numpy(), ref, rtol=0, atol=1e-8 * np.abs(ref).max())
+
+
+BRATU_CHILD = r"""
+import json, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + "/tests")
+import _nkpath
+import ariadne_hip as ah
+from oracle import oracle as oc
+import test_hip_f0r as t
+ctx = ah.Context(0); ah.set_default_context(ctx)
+out = []
+for nx, ny in ((200, 150), (201, 37)):
+    F, p, u0 = t.case("bratu2d", nx, ny)
+    kw = dict(restart=True, memory=10, itmax=35, atol=0.0, rtol=0.0)
+    x0, h0, n0, p0 = t.solve(F, p, u0, False, **kw)
+    x1, h1, n1, p1 = t.solve(F, p, u0, True, **kw)
+    jv = [k for k in p0 if k.startswith("jv_fd")]
+    db = sum(p0[k]["bytes"] / p0[k]["timed"] * p0[k]["launches"] - p1[k]["bytes"] / p1[k]["timed"] * p1[k]["launches"] for k in jv)
+    out.append(dict(same=bool(h0 == h1 and np.array_equal(x0, x1)), n=int(n1),
+                    db=db / (8.0 * nx * ny * sum(p0[k]["launches"] for k in jv))))
+print(json.dumps(out))
+"""
+
+
+def test_f0_recomputed_bratu_bitwise_when_forced():
+    """The Bratu kernel's F0R path (NK_F0R=2, in a child process: the knob is read once per process)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", BRATU_CHILD, root], env=dict(os.environ, NK_F0R="2"),
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    for r in res:
+        assert r["same"] and r["n"] == 35 and r["db"] == pytest.approx(1.0, rel=1e-12)

@@ -137,7 +137,7 @@ def test_shim_binds_the_reference_operator_surface():
         assert sym in names
     src = open(SHIM).read()
     assert "isempty(kwargs) || error(" in src
-    assert re.search(r"GC\.@preserve Nc N Mc M begin.*?NkKrylovOpts\(.*?, Np, Mp\).*?ccall\(\(:nk_krylov_solve",
+    assert re.search(r"GC\.@preserve Nc N Mc M begin.*?NkKrylovOpts\(.*?, Np, Mp,.*?ccall\(\(:nk_krylov_solve",
                      src, re.S)
     for k in ("heat3d", "heat3d_midpoint", "heat3d_trapezoid"):
         assert f"{k} = NK_HEAT3D" in src
