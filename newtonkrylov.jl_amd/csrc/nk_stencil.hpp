@@ -359,6 +359,23 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw_ib(const KArgs& A, const u
     return r;
 }
 
+// the u part of a raw FD row (u centres, edges, u_n) as a residual row: cooked as MODE_RES it is the
+// stencil field the residual kernel evaluates F(u) on (the F0R kernels recompute F0 from it)
+template <int MODE, int VEC>
+__device__ __forceinline__ RawRow<MODE_RES, VEC> as_res_row(const RawRow<MODE, VEC>& r) {
+    RawRow<MODE_RES, VEC> q;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+        q.a[k] = r.a[k];
+        q.g[k] = r.g[k];
+    }
+    q.ae = r.ae;
+    q.ae2 = r.ae2;
+    q.ge = r.ge;
+    q.ge2 = r.ge2;
+    return q;
+}
+
 // cooked stencil field of a row: centres, the lane's edge value(s), and (fused normalisation) v / h
 template <int VEC>
 struct Field {
@@ -517,19 +534,7 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     constexpr bool kF0 = MODE == MODE_JFD && !F0R;
     constexpr bool kR = MODE == MODE_JFD && F0R;  // the u field, cooked as the residual kernel cooks it
     constexpr bool kAx = EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID;
-    auto as_res = [](const RawRow<MODE, VEC>& r) {  // the u part of a raw FD row, as a residual row
-        RawRow<MODE_RES, VEC> q;
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            q.a[k] = r.a[k];
-            q.g[k] = r.g[k];
-        }
-        q.ae = r.ae;
-        q.ae2 = r.ae2;
-        q.ge = r.ge;
-        q.ge2 = r.ge2;
-        return q;
-    };
+    auto as_res = [](const RawRow<MODE, VEC>& r) { return as_res_row<MODE, VEC>(r); };
     constexpr bool vout = MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS);  // fused kdivcopy!: V_k stored
     double acc = 0.0;
     if (y0 < ny) {
@@ -777,7 +782,9 @@ __global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
 // rows j +- 1 from there.  Only the tile's edge waves load a halo row (row j0 - 1 or j0 + NW, or the
 // periodic wrap) -- per plane NW + 2 row loads per field instead of 3 NW, so taller tiles (NW = 8)
 // cost no extra load issue and re-fetch (NW + 2) / NW of a plane instead of 1.5x.
-template <int KIND, int MODE, int EPI, int VEC, bool PER = false, int NW = 8>
+// F0R: as k_st2d's -- F(u) recomputed from the u rows (and a second LDS row for the u field's
+// y-neighbours) with the residual kernel's arithmetic instead of loading F0
+template <int KIND, int MODE, int EPI, int VEC, bool PER = false, int NW = 8, bool F0R = false>
 __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
     __shared__ double sh[kShN];
     KArgs A = A0;
@@ -785,7 +792,9 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
     constexpr int SCH = scheme_of<KIND>();
     constexpr bool kG = SCH != 0 && MODE != MODE_JEXACT;
     constexpr bool kTG = SCH == 2 && kG;  // G_Trapezoid!: u_n's y-neighbours too
+    constexpr bool kR = MODE == MODE_JFD && F0R;
     __shared__ double ly[2][kTG ? 2 : 1][NW][64 * VEC];
+    __shared__ double lyu[2][kR ? NW : 1][kR ? 64 * VEC : 1];  // F0R: the cooked u field's centre rows
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const int nb = gridDim.x, b = blockIdx.x;
@@ -821,7 +830,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
     const int64_t z0 = (int64_t)tz * A.rows;
     const int64_t z1 = z0 + A.rows < nz ? z0 + A.rows : nz;
     constexpr bool kUn = SCH == 0 && MODE != MODE_JEXACT;
-    constexpr bool kF0 = MODE == MODE_JFD;
+    constexpr bool kF0 = MODE == MODE_JFD && !kR;
     constexpr bool kAx = EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID;
     constexpr bool vout = MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS);
     // ghost planes of v from the neighbours' patches, fetched by this launch (z-tiles at the slab's ends)
@@ -842,11 +851,16 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
     double acc = 0.0;
     if (z0 < nz) {
         const int64_t o0 = z0 * pl + oj;
-        Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(
-            A, ib_lo ? load_raw_ib<MODE, VEC, kG>(A, ib_lo, o0 - pl, oj) : load_raw<MODE, VEC, false, kG, PER>(A, o0 - pl, 0), act,
-            false);
-        Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, load_raw<MODE, VEC, true, kG, PER>(A, o0, o0 + de, o0 + de2), act,
-                                                      edge_ok, edge_ok2);
+        const RawRow<MODE, VEC> rm0 =
+            ib_lo ? load_raw_ib<MODE, VEC, kG>(A, ib_lo, o0 - pl, oj) : load_raw<MODE, VEC, false, kG, PER>(A, o0 - pl, 0);
+        const RawRow<MODE, VEC> rc0 = load_raw<MODE, VEC, true, kG, PER>(A, o0, o0 + de, o0 + de2);
+        Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(A, rm0, act, false);
+        Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, rc0, act, edge_ok, edge_ok2);
+        Field<VEC> um{}, uc_{};  // F0R: the u field of planes k-1, k
+        if constexpr (kR) {
+            um = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rm0), act, false);
+            uc_ = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rc0), act, edge_ok, edge_ok2);
+        }
         RawRow<MODE, VEC> rp = (ib_hi && z0 + 1 == nz) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, o0 + pl, oj)
                                                        : load_raw<MODE, VEC, true, kG, PER>(A, o0 + pl, o0 + pl + de, o0 + pl + de2);
         RawRow<MODE, VEC> rn{}, rs{};
@@ -864,6 +878,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
             for (int q = 0; q < VEC; ++q) {
                 ly[par][0][wv][lane * VEC + q] = fc.c[q];
                 if constexpr (kTG) ly[par][kTG ? 1 : 0][wv][lane * VEC + q] = fc.g[q];
+                if constexpr (kR) lyu[par][kR ? wv : 0][kR ? lane * VEC + q : 0] = uc_.c[q];
             }
             // ---- issue: centre row of plane k+2, halo rows and centre data of plane k+1
             const bool more = k + 1 < z1;
@@ -884,6 +899,12 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
             Field<VEC> fn{}, fs{};
             if (ld_n) fn = cook<MODE, VEC, SCH, kG, PER>(A, rn, has_n, false);
             if (ld_s) fs = cook<MODE, VEC, SCH, kG, PER>(A, rs, has_s, false);
+            Field<VEC> up{}, fnu{}, fsu{};
+            if constexpr (kR) {
+                up = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rp), act, edge_ok, edge_ok2);
+                if (ld_n) fnu = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rn), has_n, false);
+                if (ld_s) fsu = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rs), has_s, false);
+            }
             __syncthreads();  // plane k's rows are in LDS (parity: the next plane's writes go to the other buffer)
             double cn[VEC], cs[VEC], gn[VEC], gs[VEC];
 #pragma unroll
@@ -898,6 +919,18 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
                 }
                 if (!has_n) { cn[q] = 0.0; gn[q] = 0.0; }  // bc_zero! beyond the last row
                 if (!has_s) { cs[q] = 0.0; gs[q] = 0.0; }
+            }
+            double cnu[VEC], csu[VEC];  // F0R: the u field's y-neighbours
+            LR xu{};
+            if constexpr (kR) {
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) {
+                    cnu[q] = lds_n ? lyu[par][kR ? wv + (lds_n ? 1 : 0) : 0][kR ? lane * VEC + q : 0] : fnu.c[q];
+                    csu[q] = lds_s ? lyu[par][kR ? wv - (lds_s ? 1 : 0) : 0][kR ? lane * VEC + q : 0] : fsu.c[q];
+                    if (!has_n) cnu[q] = 0.0;
+                    if (!has_s) csu[q] = 0.0;
+                }
+                xu = x_nbrs<PER>(uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
             }
             // ---- compute plane k
             const LR xn = x_nbrs<PER>(fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
@@ -926,7 +959,16 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
                                 lapk(A, g, fp.g[q], fm.g[q], A.hz2, A.ihz2);
                     }
                     const double unq = kG ? fc.g[q] : unc.v[q];
-                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0c.v[q], SCH == 1 ? fc.x[q] : c, lsumg);
+                    double f0 = f0c.v[q];
+                    if constexpr (kR) {  // F(u) at this point, as the residual kernel evaluates it
+                        const double uw = (q == 0) ? xu.l : uc_.c[q == 0 ? 0 : q - 1];
+                        const double ue = (q == VEC - 1) ? xu.r : uc_.c[q == VEC - 1 ? q : q + 1];
+                        const double ucc = uc_.c[q];
+                        const double lsu = (lapk(A, ucc, ue, uw, A.hx2, A.ihx2) + lapk(A, ucc, cnu[q], csu[q], A.hy2, A.ihy2)) +
+                                           lapk(A, ucc, up.c[q], um.c[q], A.hz2, A.ihz2);
+                        f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unq, 0.0, SCH == 1 ? uc_.x[q] : ucc, lsumg);
+                    }
+                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0, SCH == 1 ? fc.x[q] : c, lsumg);
                     acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[q] : ax.v[q], acc);
                     val.v[q] = r;
                 }
@@ -940,6 +982,10 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
             }
             fm = fc;
             fc = fp;
+            if constexpr (kR) {
+                um = uc_;
+                uc_ = up;
+            }
             rp = rpp;
             rn = rnn;
             rs = rss;
@@ -954,6 +1000,18 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
 // ------------------------------------------------------------------------------ stencil dispatch
 template <int KIND, int MODE, int EPI, int NW>
 void go_st3l(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
+    if constexpr (MODE == MODE_JFD && heat_kind<KIND>()) {  // F0 recomputed from u (KArgs::f0r)
+        if (A.f0r) {
+            if (per) {
+                if (vec == 2) hipLaunchKernelGGL((k_st3l<KIND, MODE, EPI, 2, true, NW, true>), dim3(grid), dim3(64 * NW), 0, s, A);
+                else hipLaunchKernelGGL((k_st3l<KIND, MODE, EPI, 1, true, NW, true>), dim3(grid), dim3(64 * NW), 0, s, A);
+                return;
+            }
+            if (vec == 2) hipLaunchKernelGGL((k_st3l<KIND, MODE, EPI, 2, false, NW, true>), dim3(grid), dim3(64 * NW), 0, s, A);
+            else hipLaunchKernelGGL((k_st3l<KIND, MODE, EPI, 1, false, NW, true>), dim3(grid), dim3(64 * NW), 0, s, A);
+            return;
+        }
+    }
     if (per) {
         if (vec == 2) hipLaunchKernelGGL((k_st3l<KIND, MODE, EPI, 2, true, NW>), dim3(grid), dim3(64 * NW), 0, s, A);
         else hipLaunchKernelGGL((k_st3l<KIND, MODE, EPI, 1, true, NW>), dim3(grid), dim3(64 * NW), 0, s, A);

@@ -4,8 +4,10 @@ F(u) again from the u rows they load anyway -- the same cooked field, Laplacian 
 the residual kernel -- instead of reading F0 (8 B/pt less).  The bar is bits: whole restarted
 FD-GMRES solves (Arnoldi steps with the fused V_k = q / h, the restart residual b - J x, the k = 1
 and reorthogonalised steps) with and without the flag give identical histories and iterates, for
-every heat scheme, zero and periodic boundaries, VEC 2 and VEC 1 (odd nx) tiles -- and Bratu, whose
-kernel has the same path but uses it only under NK_F0R=2 (a second exp per point makes it slower)."""
+every heat scheme in 2D and 3D (k_st2d, k_st3l), zero and periodic boundaries, VEC 2 and VEC 1 (odd
+nx) tiles, tiles with and without LDS y-neighbours and halo rows -- under the default policy (2D heat,
+3D G_Euler!) and forced everywhere (NK_F0R=2: Bratu, whose second exp per point makes it slower, and
+the 3D kernels that lose a wave per SIMD)."""
 import json
 import os
 import subprocess
@@ -31,8 +33,20 @@ def ctx():
     c.sync()
 
 
-def case(name, nx, ny, bc="zero"):
+def case(name, nx, ny, bc="zero", nz=0):
     rng = np.random.default_rng(nx * 7 + ny)
+    if nz:  # 3D heat (k_st3l)
+        un = rng.standard_normal((nz, ny, nx))
+        scheme, alpha = (name.split(":") + ["0.5"])[:2]
+        P = oc.heat3d_euler(nx, ny, nz, un=un, scheme=scheme, bc=oc.BC_PERIODIC if bc == "periodic" else oc.BC_ZERO,
+                            alpha=float(alpha))
+        G = GNAME[scheme]
+        if scheme == "midpoint":
+            G = G(alpha=float(alpha))
+        F = G.bind(ah.diffusion3d_)
+        p = (ah.DeviceArray.from_numpy(un), P.dt, None,
+             (P.a, P.hx, P.hy, P.hz, ah.bc_periodic_ if bc == "periodic" else ah.bc_zero_), 0.0)
+        return F, p, un + 0.01 * rng.standard_normal(un.shape)
     if name == "bratu2d":
         P = oc.bratu2d(nx, ny)
         u0 = oc.sin_ic(P) + 0.05 * rng.standard_normal(P.shape)
@@ -71,23 +85,28 @@ CASES = [("euler", 130, 67, "zero"), ("euler", 201, 37, "zero"),
          ("midpoint", 96, 40, "periodic"), ("trapezoid", 65, 33, "periodic")]
 
 
-@pytest.mark.parametrize("name,nx,ny,bc", CASES)
+CASES3 = [("euler", 40, 33, "zero", 20), ("midpoint:0.3", 33, 17, "zero", 9), ("trapezoid", 65, 7, "zero", 5),
+          ("euler", 24, 24, "periodic", 24), ("trapezoid", 33, 17, "periodic", 9)]
+
+
+@pytest.mark.parametrize("name,nx,ny,bc,nz", [c + (0,) for c in CASES] + CASES3)
 @pytest.mark.parametrize("reorth", [False, True])
-def test_f0_recomputed_is_bitwise(ctx, name, nx, ny, bc, reorth):
-    F, p, u0 = case(name, nx, ny, bc)
+def test_f0_recomputed_is_bitwise(ctx, name, nx, ny, bc, nz, reorth):
+    F, p, u0 = case(name, nx, ny, bc, nz)
     kw = dict(restart=True, memory=10, itmax=35, atol=0.0, rtol=0.0, reorthogonalization=reorth)
     x0, h0, n0, p0 = solve(F, p, u0, False, **kw)
     x1, h1, n1, p1 = solve(F, p, u0, True, **kw)
     assert n0 == n1 == 35
     assert h0 == h1
     np.testing.assert_array_equal(x0, x1)
-    # the flag reached the stencils: the FD Jv launches moved 8 B/pt less
+    # the flag reached the stencils the policy picks (2D heat; 3D G_Euler! except the V_1 step): those
+    # FD Jv launches moved 8 B/pt less
     jv = [k for k in p0 if k.startswith("jv_fd")]
     assert jv
-    b0 = sum(p0[k]["bytes"] / p0[k]["timed"] * p0[k]["launches"] for k in jv)
-    b1 = sum(p1[k]["bytes"] / p1[k]["timed"] * p1[k]["launches"] for k in jv)
-    launches = sum(p0[k]["launches"] for k in jv)
-    assert b0 - b1 == pytest.approx(8.0 * nx * ny * launches, rel=1e-12)
+    saved = {k: (p0[k]["bytes"] - p1[k]["bytes"]) / p0[k]["timed"] / (8.0 * nx * ny * max(nz, 1)) for k in jv}
+    uses = (lambda k: True) if not nz else (lambda k: name == "euler" and k != "jv_fd_dot_v1")
+    for k in jv:
+        assert saved[k] == pytest.approx(1.0 if uses(k) else 0.0, abs=1e-12), (k, saved[k])
 
 
 def test_newton_uses_it_and_matches_oracle(ctx):
@@ -111,21 +130,22 @@ from oracle import oracle as oc
 import test_hip_f0r as t
 ctx = ah.Context(0); ah.set_default_context(ctx)
 out = []
-for nx, ny in ((200, 150), (201, 37)):
-    F, p, u0 = t.case("bratu2d", nx, ny)
+for name, nx, ny, bc, nz in [("bratu2d", 200, 150, "zero", 0), ("bratu2d", 201, 37, "zero", 0)] + t.CASES3:
+    F, p, u0 = t.case(name, nx, ny, bc, nz)
     kw = dict(restart=True, memory=10, itmax=35, atol=0.0, rtol=0.0)
     x0, h0, n0, p0 = t.solve(F, p, u0, False, **kw)
     x1, h1, n1, p1 = t.solve(F, p, u0, True, **kw)
     jv = [k for k in p0 if k.startswith("jv_fd")]
     db = sum(p0[k]["bytes"] / p0[k]["timed"] * p0[k]["launches"] - p1[k]["bytes"] / p1[k]["timed"] * p1[k]["launches"] for k in jv)
     out.append(dict(same=bool(h0 == h1 and np.array_equal(x0, x1)), n=int(n1),
-                    db=db / (8.0 * nx * ny * sum(p0[k]["launches"] for k in jv))))
+                    db=db / (8.0 * nx * ny * max(nz, 1) * sum(p0[k]["launches"] for k in jv))))
 print(json.dumps(out))
 """
 
 
-def test_f0_recomputed_bratu_bitwise_when_forced():
-    """The Bratu kernel's F0R path (NK_F0R=2, in a child process: the knob is read once per process)."""
+def test_f0_recomputed_bitwise_when_forced():
+    """Every F0R kernel the default policy does not pick -- Bratu 2D, the 3D midpoint / trapezoid and
+    V_1 steps -- forced with NK_F0R=2 (in a child process: the knob is read once per process)."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     p = subprocess.run([sys.executable, "-c", BRATU_CHILD, root], env=dict(os.environ, NK_F0R="2"),
                        capture_output=True, text=True, timeout=240)
