@@ -1462,6 +1462,7 @@ extern "C" int nkb_stencil_kind(nk_ctx* c, int kind, int64_t nx, int64_t ny, int
     for (double* q : {u, v, F0, aux, un}) NK_TRY(launch_fill(c, nx * ny * nz, q, 0.25));
     p.un = un;
     StencilIn in{&p, mode, epi, out, u, v, F0, aux, 1e-6};
+    in.f0r = (fast & 32) != 0;  // variant bit 32: F0 recomputed (the F0R kernels, where the policy allows)
     Red r{};
     hipEvent_t a, b;
     NK_HIP(c, hipEventCreate(&a));

@@ -19,7 +19,7 @@ ap.add_argument("--side", type=int, default=8192)
 ap.add_argument("--nz", type=int, default=0, help="3D kinds: planes (default side)")
 ap.add_argument("--modes", default="0:1,2:2", help="mode:epi pairs (0:1 residual+norm, 2:2 FD Jv+dot)")
 ap.add_argument("--rows", default="0,16,32,64,128")
-ap.add_argument("--fast", default="0,4")
+ap.add_argument("--fast", default="0,4", help="variant bits: 4 VEC=4 (2D), 8/16 LDS tiles of 4/8 rows (3D), 32 F0 recomputed")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=10)
 args = ap.parse_args()
@@ -32,11 +32,12 @@ NAME = {2: "bratu2d", 3: "heat2d euler", 4: "heat3d euler", 5: "heat2d midpoint"
 MODE = {(0, 1): "residual+norm", (2, 2): "FD Jv+dot", (1, 2): "exact Jv+dot"}
 
 
-def words(kind, mode, epi):  # the launcher's algorithmic count
+def words(kind, mode, epi, fast=0):  # the launcher's algorithmic count (fast bit 32: F0 recomputed)
     heat = kind >= 3
     w = 1
     w += (1 + heat) if mode == 0 else ((1 + (not heat)) if mode == 1 else (3 + heat))
-    return w + (1 if epi == 2 else 0)
+    f0r = mode == 2 and fast & 32 and (kind in (3, 5, 7) or kind == 4)
+    return w + (1 if epi == 2 else 0) - (1 if f0r else 0)
 
 
 res = {}
@@ -56,6 +57,6 @@ for _ in range(args.rounds):
 print(f"stencils at {args.side}^2 (x nz): median us per launch over {args.rounds} interleaved rounds")
 for (kind, mode, epi, rows, fast, nz), v in res.items():
     us = statistics.median(v)
-    gb = 8.0 * words(kind, mode, epi) * args.side * args.side * nz / us / 1e3
+    gb = 8.0 * words(kind, mode, epi, fast) * args.side * args.side * nz / us / 1e3
     print(f"{NAME[kind]:17s} {MODE.get((mode, epi), f'{mode}:{epi}'):14s} rows={rows:4d} fast={fast:2d}"
           f"  {us:9.1f} us  {gb:7.1f} GB/s  ({gb / 80:5.1f}% of 8 TB/s)")
