@@ -244,6 +244,9 @@ int nk_precond_apply(nk_ctx* ctx, const nk_problem* p, const nk_precond* N, cons
 int nk_workspace_create(nk_ctx* ctx, int32_t algo, const nk_problem* p, int32_t memory, nk_workspace** out);
 int nk_workspace_destroy(nk_workspace* ws);
 double* nk_workspace_x(nk_workspace* ws);  /* workspace.x (device interior pointer) */
+/* workspace.V[i + 1] (0-based i) of the last Arnoldi cycle, or null past the allocated basis: the
+ * orthonormal basis the last solve built (Krylov.jl keeps it in the workspace too) */
+double* nk_workspace_basis(nk_workspace* ws, int32_t i);
 /* Solve J(u) x = b; F0 = F(u) (FD mode only).  hist (optional, host) receives the residual-norm
  * estimates (Krylov `history`); *hist_len the number produced (may exceed hist_cap). */
 int nk_krylov_solve(nk_workspace* ws, const nk_problem* p, const double* u, const double* F0, const double* b,

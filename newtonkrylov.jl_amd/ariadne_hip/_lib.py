@@ -126,6 +126,7 @@ SIGNATURES = {
     "nk_workspace_create": (C.c_int, [_VP, _I32, _PP, _I32, C.POINTER(_VP)]),
     "nk_workspace_destroy": (C.c_int, [_VP]),
     "nk_workspace_x": (_VP, [_VP]),
+    "nk_workspace_basis": (_VP, [_VP, _I32]),
     "nk_krylov_solve": (C.c_int, [_VP, _PP, _VP, _VP, _VP, C.POINTER(nk_krylov_opts), C.POINTER(nk_krylov_stats),
                                   _PD, _I64, C.POINTER(_I64)]),
     "nk_newton_defaults": (C.c_int, [C.POINTER(nk_newton_opts)]),

@@ -139,6 +139,11 @@ class KrylovWorkspace:
         self.x = DeviceArray(self.grid, self.ctx, _ptr=load().nk_workspace_x(h))
         self.stats = KrylovStats()
 
+    def basis(self, i: int) -> DeviceArray | None:
+        """workspace.V[i + 1] of the last Arnoldi cycle (a device view; None past the allocated basis)."""
+        p = load().nk_workspace_basis(self.handle, int(i))
+        return DeviceArray(self.grid, self.ctx, _ptr=p) if p else None
+
     def free(self):
         if getattr(self, "handle", None) and self.ctx.handle:
             load().nk_workspace_destroy(self.handle)

@@ -720,6 +720,10 @@ int nk_workspace_destroy(nk_workspace* ws) {
 
 double* nk_workspace_x(nk_workspace* ws) { return ws ? ws->x : nullptr; }
 
+double* nk_workspace_basis(nk_workspace* ws, int32_t i) {
+    return (ws && i >= 0 && i < (int32_t)ws->V.size()) ? ws->V[(size_t)i] : nullptr;
+}
+
 int nk_krylov_solve(nk_workspace* ws, const nk_problem* p, const double* u, const double* F0, const double* b,
                     const nk_krylov_opts* o, nk_krylov_stats* st, double* hist, int64_t hist_cap, int64_t* hist_len) {
     if (!ws || !p || !u || !b || !o || !st) return NK_E_ARG;
