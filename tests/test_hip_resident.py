@@ -229,3 +229,48 @@ def test_full_size_cycle_properties(ctx, jv, reorth, orth_tol, res_tol):
     est = ws.stats.residuals[-1]
     assert abs(ah.knorm(N, r) - est) <= res_tol * est
     ws.free()
+
+
+@pytest.mark.parametrize("case", ["bratu_16384x2048", "heat_8192"])
+def test_partly_resident_cycle_properties(ctx, case):
+    """The same properties where only part of q fits on chip and the rest streams (non-temporal):
+    config 4's 16384 x 2048 slab (half resident) and config 3's 8192^2 heat step (a quarter, with
+    reorthogonalization as heat_2D.jl:131 runs it) -- a full GMRES(30) cycle for Bratu, 12 Arnoldi
+    steps for the well-conditioned heat Jacobian (cond <= 3: 30 steps would reach the rounding floor),
+    exact Jv."""
+    if case.startswith("bratu"):
+        nx, ny = 16384, 2048
+        hx, hy = 1.0 / (nx + 1), 1.0 / (ny + 1)
+        u0 = np.sin(np.pi * np.arange(1, ny + 1) * hy)[:, None] * np.sin(np.pi * np.arange(1, nx + 1) * hx)[None, :]
+        F, p, reorth, k = ah.bratu2d_, (hx, hy, 3.51382), False, 30
+    else:
+        n = 8192
+        P = oc.heat2d_euler(n, un=np.zeros((1, 1)))
+        un = np.sin(np.pi * np.arange(1, n + 1) * P.hy)[:, None] * np.sin(np.pi * np.arange(1, n + 1) * P.hx)[None, :]
+        un += 0.1 * np.random.default_rng(0).uniform(-1.0, 1.0, un.shape)
+        u0 = un + 0.01
+        F = ah.heat2d_euler_
+        p, reorth, k = (ah.DeviceArray.from_numpy(un), P.dt, None, (P.a, P.hx, P.hy, ah.bc_zero_), 0.0), True, 12
+    u = ah.DeviceArray.from_numpy(np.ascontiguousarray(u0))
+    res = u.zero()
+    F(res, u, p)
+    J = ah.JacobianOperator(F, res, u, p, jv="exact")
+    ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=30))
+    ctx.prof_reset()
+    ctx.prof_enable(1)
+    ah.krylov_solve_(ws, J, res, restart=True, itmax=k, atol=0.0, rtol=0.0, history=True, reorthogonalization=reorth)
+    prof = ctx.prof_read()
+    ctx.prof_enable(0)
+    assert ws.stats.niter == k and prof.get("mgs_sweep", {}).get("launches", 0) >= k - 2
+    N = len(u)
+    V = [ws.basis(i) for i in range(k)]
+    G = np.array([[ah.kdot(N, V[i], V[j]) for j in range(i + 1)] + [0.0] * (k - 1 - i) for i in range(k)])
+    G = G + np.tril(G, -1).T
+    assert np.max(np.abs(G - np.eye(k))) <= 1e-12
+    Jx = u.zero()
+    ah.mul_(Jx, J, ws.x)
+    r = res.copy()
+    ah.kaxpy_(N, -1.0, Jx, r)
+    est = ws.stats.residuals[-1]
+    assert abs(ah.knorm(N, r) - est) <= 1e-10 * est
+    ws.free()
