@@ -40,9 +40,10 @@ struct ResArgs {
     uint64_t* gran;        // 2 parities x G blocks x 2 granules
     int* err;              // pinned host flag: a poll timed out
     int noxchg;            // kernel-variant bench only (NK_RES_NOXCHG=1): skip the exchange, h stays fixed
-    int poll1;             // one polling wave (NK_RES_POLL1, default 1) instead of every thread polling one partial
+    int poll1;             // 1: one polling wave (NK_RES_POLL1, default 1), 2: four staggered polling waves, 0: every thread polls one partial
     int strided;           // slots interleaved across blocks (every block exactly full: no streamed remainder)
     uint64_t* tstamp;      // kernel-variant bench only: per pass and block, wall clock at pass end and after the hand-off
+    int senders;           // cross-rank: blocks [0, senders) each send this rank's sum to every rank (identical bits)
     // fused FD Jv (2D Bratu): q = (F(u + eps V_k) - F0) / eps computed into the registers, with the
     // partials of <V_1, q> -- instead of loading the q a separate Jv kernel wrote
     const double *ju, *jv, *jf0, *jaux;
@@ -61,7 +62,8 @@ struct ResState {
 
 // `budget`: this thread's remaining polls for the whole launch (a stuck grid drains in bounded time)
 // t: the exchange's index in this launch (tags, parity and mailbox epochs follow it)
-__device__ __forceinline__ double res_exchange(const ResArgs& A, double part, int t, double* sh, unsigned& budget) {
+__device__ __forceinline__ double res_exchange(const ResArgs& A, double part, int t, double* sh, unsigned& budget,
+                                              unsigned* xdone) {
     const int tid = threadIdx.x, G = gridDim.x;
     const unsigned tag = A.tag0 + (unsigned)t;
     uint64_t* slot = A.gran + (size_t)(t & 1) * G * 2;
@@ -72,41 +74,59 @@ __device__ __forceinline__ double res_exchange(const ResArgs& A, double part, in
         __hip_atomic_store(slot + 2 * blockIdx.x + 1, ((uint64_t)tag << 32) | (bits >> 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (A.poll1) {  // ONE wave polls: lane l sums the partials of blocks l, 64 + l, 128 + l, 192 + l
-        if (tid < 64) {
-            uint64_t w[8];
+    if (A.poll1) {  // ONE wave polls: lane l sums the partials of blocks l, 64 + l, 128 + l, 192 + l.
+        // poll1 >= 2: every wave polls the same way, wave w starting w quarter round trips later, so a
+        // late granule is seen a quarter of a poll round after it lands instead of half a round on
+        // average; the first wave to see all of them publishes the (bit-identical) sum, the others
+        // stop at its flag
+        const int w = tid >> 6, nw = A.poll1 >= 2 ? kResThreads / 64 : 1;
+        if (w < nw) {
+            for (int i = 0; i < w; ++i) __builtin_amdgcn_s_sleep(8);
+            const int l = tid & 63;
+            uint64_t w8[8];
+            bool mine = false;  // this wave saw every granule
             for (;;) {
+                if (nw > 1 && __hip_atomic_load(xdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == tag) break;
                 bool ok = true;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const int bl = 64 * j + tid;
+                    const int bl = 64 * j + l;
                     if (bl < G) {
-                        w[2 * j] = __hip_atomic_load(slot + 2 * bl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        w[2 * j + 1] = __hip_atomic_load(slot + 2 * bl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        ok = ok && (unsigned)(w[2 * j] >> 32) == tag && (unsigned)(w[2 * j + 1] >> 32) == tag;
+                        w8[2 * j] = __hip_atomic_load(slot + 2 * bl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        w8[2 * j + 1] = __hip_atomic_load(slot + 2 * bl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ok = ok && (unsigned)(w8[2 * j] >> 32) == tag && (unsigned)(w8[2 * j + 1] >> 32) == tag;
                     } else {
-                        w[2 * j] = w[2 * j + 1] = 0;
+                        w8[2 * j] = w8[2 * j + 1] = 0;
                     }
                 }
-                if (ok) break;
+                if (__all(ok)) {
+                    mine = true;
+                    break;
+                }
                 if (budget == 0 || --budget == 0) {
                     __hip_atomic_store(A.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    mine = true;  // a timed-out grid still drains: publish whatever arrived
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
-            double p = 0.0;
+            if (mine) {
+                double p = 0.0;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                p += __longlong_as_double((long long)(((w[2 * j + 1] & 0xffffffffull) << 32) | (w[2 * j] & 0xffffffffull)));
-            p = wave_sum(p);
-            if (tid == 0) sh[kShB] = p;
+                for (int j = 0; j < 4; ++j)
+                    p += __longlong_as_double((long long)(((w8[2 * j + 1] & 0xffffffffull) << 32) | (w8[2 * j] & 0xffffffffull)));
+                p = wave_sum(p);
+                if (l == 0) {
+                    sh[kShB] = p;
+                    if (nw > 1) __hip_atomic_store(xdone, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
         }
         __syncthreads();
         const double s1 = sh[kShB];
         if (A.mb0 == 0) return s1;
         const unsigned epoch = A.mb0 + (unsigned)t;
-        if (blockIdx.x == 0) mb_send(s1, epoch);
+        if ((int)blockIdx.x < A.senders) mb_send(s1, epoch);
         __syncthreads();
         return mb_recv(epoch, sh);
     }
@@ -134,7 +154,7 @@ __device__ __forceinline__ double res_exchange(const ResArgs& A, double part, in
     s = sh[kShB];
     if (A.mb0 == 0) return s;
     const unsigned epoch = A.mb0 + (unsigned)t;  // cross-rank: the peer mailbox, as reduce_input does
-    if (blockIdx.x == 0) mb_send(s, epoch);
+    if ((int)blockIdx.x < A.senders) mb_send(s, epoch);
     __syncthreads();
     return mb_recv(epoch, sh);
 }
@@ -350,7 +370,9 @@ template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, boo
 __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     extern __shared__ dx2 lq[];  // rl x 256 double2
     __shared__ double sh[kShN];
+    __shared__ unsigned xdone;  // tag of the last exchange a polling wave completed (poll1 >= 2)
     const int tid = threadIdx.x, G = gridDim.x;
+    if (tid == 0) xdone = 0;  // tags start at 1; the first exchange follows a __syncthreads
     // balanced partition of the ceil(n2 / 256) 256-wide slots: block b owns slots [b S / G, (b+1) S / G)
     const int64_t ns = (A.n2 + kResThreads - 1) / kResThreads;
     const int64_t lo = (int64_t)blockIdx.x * ns / G * kResThreads;
@@ -382,7 +404,7 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
 #pragma unroll 4
         for (int s = 0; s < A.rl; ++s) lq[s * kResThreads + tid] = res_jv_pair(A, base + (RV + s) * ss + tid, jacc);
         res_prefetch<RV, B, PRE, NTM>(A, P, 0, base, ss);
-        h = res_exchange(A, block_sum<kResThreads>(jacc, sh), 0, sh, budget);
+        h = res_exchange(A, block_sum<kResThreads>(jacc, sh), 0, sh, budget, &xdone);
     } else {
         const dx2* qb = reinterpret_cast<const dx2*>(A.q) + base + tid;
 #pragma unroll
@@ -400,7 +422,7 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
         if (t + 1 < A.np) res_prefetch<RV, B, PRE, NTM>(A, P, t + 1, base, ss);
         const double part = block_sum<kResThreads>(acc, sh);
         if (A.tstamp && tid == 0) A.tstamp[((size_t)t * G + blockIdx.x) * 2] = wall_clock64();
-        if (!A.noxchg) h = res_exchange(A, part, t + xo, sh, budget);
+        if (!A.noxchg) h = res_exchange(A, part, t + xo, sh, budget, &xdone);
         else __syncthreads();
         if (A.tstamp && tid == 0) A.tstamp[((size_t)t * G + blockIdx.x) * 2 + 1] = wall_clock64();
     }
@@ -582,6 +604,11 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
     static const int poll1 = env_int("NK_RES_POLL1", 1);
     A.poll1 = poll1;
     A.tstamp = c->res_tstamp;
+    // cross-rank hand-off: the first `senders` blocks (one per XCD at 8) all send the rank's sum -- the
+    // same bits into the same cells -- so the peers see it as soon as the EARLIEST of them has it,
+    // not when block 0 happens to finish its local poll
+    static const int senders = env_int("NK_MB_SENDERS", 8);
+    A.senders = std::max(1, std::min(senders, c->res_blocks));
     A.spin = 1u << 22;  // polls per thread per launch (~1 s): a grid that is not co-resident fails fast
     const size_t lds = (size_t)A.rl * kResThreads * sizeof(dx2);
     // algorithmic bytes: the resident fraction f of q is loaded once (or computed by the fused Jv
