@@ -736,17 +736,20 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     // FD with F0 recomputed from u (2D, VEC <= 2: k_st2d<..., F0R>; 3D heat: k_st3l<..., F0R>, not
     // with NK_F0R=3 (A/B)); never with the `fast` reciprocals,
     // which would change F(u) against the residual kernel that stored F0.  NK_F0R: 1 (default) for the
-    // heat kinds, whose F(u) costs a few flops (8192^2 FD Jv 728 -> 612 us, bench +3.3 %); 2 for Bratu
-    // too, where the second exp per point makes the kernel compute-bound (4096^2: the Arnoldi-step Jv
-    // unchanged, the restart residual 108 -> 126 us: profiles/r02/ab_f0r.log); 0 never
+    // heat kinds, whose F(u) costs a few flops (8192^2 FD Jv 728 -> 612 us, bench +3.3 %), and for
+    // Bratu's Jv launches that also store V_k (fused normalisation): they move enough bytes to hide the
+    // second exp per point (config-4 slab Jv 277 -> 246 us, V_1 step 248 -> 227 us, bench +1.2 %),
+    // while the plain Jv + dot (116 -> 122 us) and the restart residual (110 -> 126 us) do not
+    // (profiles/r02/ab_f0r_bratu.log); 2 for every Bratu launch too; 0 never
     static const int f0r_env = env_int("NK_F0R", 1);
     // 3D: the F0R kernel needs 145 VGPRs (3 waves per SIMD instead of 4), which pays only where the
     // field is cheap and the kernel moves the most bytes: G_Euler!'s Jv with a dot partner (512^3
     // FD Jv + V_k store 1400 -> 1198 us), not the V_1 = r0 / beta step, not midpoint / trapezoid
     // (profiles/r02/ab_f0r3.log)
     const bool dotvs = in.vout && in.epi == EPI_DOT && !in.aux;
+    const bool vfused = in.vout && in.epi == EPI_DOT;
     const bool f0r = f0r_env && in.f0r && in.mode == MODE_JFD && vec <= 2 && !(fast & 1) &&
-                     ((g.dim == 2 && (f0r_env >= 2 || nk_is_heat(p->kind))) ||
+                     ((g.dim == 2 && (f0r_env >= 2 || nk_is_heat(p->kind) || vfused)) ||
                       (g.dim == 3 && A.lds3 && f0r_env != 3 && (f0r_env >= 2 || (p->kind == NK_HEAT3D_EULER && !dotvs))));
     A.f0r = f0r ? 1 : 0;
     if (in.xchg_v) {

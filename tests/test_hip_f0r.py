@@ -6,8 +6,9 @@ FD-GMRES solves (Arnoldi steps with the fused V_k = q / h, the restart residual 
 and reorthogonalised steps) with and without the flag give identical histories and iterates, for
 every heat scheme in 2D and 3D (k_st2d, k_st3l), zero and periodic boundaries, VEC 2 and VEC 1 (odd
 nx) tiles, tiles with and without LDS y-neighbours and halo rows -- under the default policy (2D heat,
-3D G_Euler!) and forced everywhere (NK_F0R=2: Bratu, whose second exp per point makes it slower, and
-the 3D kernels that lose a wave per SIMD)."""
+2D Bratu's Jv launches that also store V_k, 3D G_Euler!) and forced everywhere (NK_F0R=2: Bratu's
+plain Jv and restart residual, whose second exp per point makes them slower, and the 3D kernels that
+lose a wave per SIMD)."""
 import json
 import os
 import subprocess
@@ -80,7 +81,7 @@ def solve(F, p, u0, flag, **kw):
     return out
 
 
-CASES = [("euler", 130, 67, "zero"), ("euler", 201, 37, "zero"),
+CASES = [("euler", 130, 67, "zero"), ("euler", 201, 37, "zero"), ("bratu2d", 200, 150, "zero"),
          ("midpoint:0.3", 130, 67, "zero"), ("trapezoid", 129, 40, "zero"), ("euler", 64, 64, "periodic"),
          ("midpoint", 96, 40, "periodic"), ("trapezoid", 65, 33, "periodic")]
 
@@ -99,12 +100,18 @@ def test_f0_recomputed_is_bitwise(ctx, name, nx, ny, bc, nz, reorth):
     assert n0 == n1 == 35
     assert h0 == h1
     np.testing.assert_array_equal(x0, x1)
-    # the flag reached the stencils the policy picks (2D heat; 3D G_Euler! except the V_1 step): those
+    # the flag reached the stencils the policy picks (2D heat; Bratu's V_k-storing launches; 3D
+    # G_Euler! except the V_1 step): those
     # FD Jv launches moved 8 B/pt less
     jv = [k for k in p0 if k.startswith("jv_fd")]
     assert jv
     saved = {k: (p0[k]["bytes"] - p1[k]["bytes"]) / p0[k]["timed"] / (8.0 * nx * ny * max(nz, 1)) for k in jv}
-    uses = (lambda k: True) if not nz else (lambda k: name == "euler" and k != "jv_fd_dot_v1")
+    if nz:
+        uses = lambda k: name == "euler" and k != "jv_fd_dot_v1"  # noqa: E731
+    elif name == "bratu2d":  # the V_k-storing launches only
+        uses = lambda k: k in ("jv_fd_dot_norm", "jv_fd_dot_v1")  # noqa: E731
+    else:
+        uses = lambda k: True  # noqa: E731
     for k in jv:
         assert saved[k] == pytest.approx(1.0 if uses(k) else 0.0, abs=1e-12), (k, saved[k])
 
