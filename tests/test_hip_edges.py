@@ -1,0 +1,112 @@
+"""GPU tests of the Krylov / Newton edge cases Krylov.jl 0.10 and Ariadne define (restated in the
+oracle: SURVEY.md Appendix A, `src/Ariadne.jl:290-372`): a zero right-hand side (x = 0, no iteration,
+solved), an iteration cap below convergence (stopped at itmax, not solved), GMRES's breakdown on a
+grid smaller than its memory (the Krylov space exhausted: the exact solution), and a Newton start that
+is already a root (no Newton step).  Flags and counts equal the oracle's; histories to 1e-9 relative;
+solutions to the tolerance stated per test."""
+import numpy as np
+import pytest
+
+import _nkpath  # noqa: F401
+import ariadne_hip as ah
+from oracle import oracle as oc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = ah.Context(0)
+    ah.set_default_context(c)
+    yield c
+    c.sync()
+
+
+def setup(P, u0):
+    u = ah.DeviceArray.from_numpy(u0)
+    res = u.zero()
+    if P.kind == oc.BRATU1D:
+        F, p = ah.bratu_, (P.hx, P.lam)
+    else:
+        F, p = ah.bratu2d_, (P.hx, P.hy, P.lam)
+    F(res, u, p)
+    return ah.JacobianOperator(F, res, u, p, jv="exact"), res
+
+
+def solve(ws, J, b, **kw):
+    ah.krylov_solve_(ws, J, b, history=True, **kw)
+    return ws.x.to_numpy(), ws.stats
+
+
+@pytest.mark.parametrize("algo", ["gmres", "fgmres", "cg"])
+def test_zero_rhs(ctx, algo):
+    """Krylov.jl: b = 0 -> x = 0 is a zero-residual solution: niter = 0, solved, no matvec, history
+    [0] -- and the workspace's x from an earlier solve is overwritten with zeros."""
+    P = oc.bratu1d(300) if algo == "cg" else oc.bratu2d(33, 20)
+    u0 = oc.sin_ic(P)
+    J, res = setup(P, u0)
+    ws = ah.krylov_workspace(algo, ah.KrylovConstructor(res, memory=10))
+    solve(ws, J, res, itmax=5, atol=0.0, rtol=0.0)  # leaves a non-zero x behind
+    assert np.any(ws.x.to_numpy() != 0.0)
+    x, st = solve(ws, J, res.zero(), itmax=50)
+    xo, so, ho = oc.krylov_solve(P, u0, np.zeros(P.shape), algo=algo, jv="exact", memory=10, itmax=50)
+    assert st.niter == so["niter"] == 0 and st.solved and so["solved"]
+    assert st.n_matvec == so["n_matvec"] == 0
+    assert st.residuals == list(ho) == [0.0]
+    assert not np.any(x) and not np.any(xo)
+
+
+@pytest.mark.parametrize("algo", ["gmres", "fgmres", "cg"])
+def test_itmax_cap(ctx, algo):
+    """An unreachable tolerance: the solve stops after itmax iterations, not solved, status
+    'maximum number of iterations exceeded' -- the oracle's counts, its history to 1e-9."""
+    P = oc.bratu1d(300) if algo == "cg" else oc.bratu2d(48, 40)
+    u0 = oc.sin_ic(P)
+    J, res = setup(P, u0)
+    kw = dict(itmax=7, atol=1e-300, rtol=1e-15)
+    if algo != "cg":
+        kw["restart"] = True
+    ws = ah.krylov_workspace(algo, ah.KrylovConstructor(res, memory=5))
+    x, st = solve(ws, J, res, **kw)
+    xo, so, ho = oc.krylov_solve(P, u0, res.to_numpy(), algo=algo, jv="exact", memory=5, **kw)
+    assert st.niter == so["niter"] == 7 and not st.solved and not so["solved"]
+    assert st.status == "maximum number of iterations exceeded"
+    assert st.n_matvec == so["n_matvec"]
+    np.testing.assert_allclose(st.residuals, ho, rtol=1e-9)
+    assert np.linalg.norm(x - xo) <= 1e-9 * np.linalg.norm(xo)
+
+
+@pytest.mark.parametrize("nx,ny", [(3, 3), (5, 2), (4, 4)])
+def test_gmres_exhausts_krylov_space(ctx, nx, ny):
+    """GMRES with memory > n and no tolerance: the Arnoldi process runs out of directions (h_{k+1,k}
+    at the rounding level -> Krylov.jl's breakdown exit) within n steps; the iterate is the exact
+    solution of the dense system, and the step count and flags are the oracle's."""
+    P = oc.bratu2d(nx, ny)
+    u0 = oc.sin_ic(P) + 0.1
+    J, res = setup(P, u0)
+    n = nx * ny
+    ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=20))
+    x, st = solve(ws, J, res, itmax=40, atol=0.0, rtol=0.0)
+    xo, so, ho = oc.krylov_solve(P, u0, res.to_numpy(), jv="exact", memory=20, itmax=40, atol=0.0, rtol=0.0)
+    assert st.niter == so["niter"] <= n and st.solved == so["solved"]
+    assert so["breakdown"] and st.status == "breakdown"
+    Jd = np.column_stack([oc.jv_exact(P, u0, e.reshape(P.shape)).reshape(-1) for e in np.eye(n)])
+    exact = np.linalg.solve(Jd, res.to_numpy().reshape(-1))
+    assert np.max(np.abs(x.reshape(-1) - exact)) <= 1e-10 * np.max(np.abs(exact))
+    assert np.max(np.abs(x - xo)) <= 1e-10 * np.max(np.abs(xo))
+
+
+def test_newton_start_at_root(ctx):
+    """newton_krylov! from a root (implicit Euler on a zero field: F(0) = 0): the loop's first check
+    ||F|| <= tol holds, no Newton step is taken -- as in the oracle."""
+    n = 32
+    P = oc.heat2d_euler(n, un=np.zeros((n, n)))
+    u0 = np.zeros((n, n))
+    ref, so = oc.newton_krylov(P, u0)
+    un = ah.DeviceArray.from_numpy(P.un)
+    u, r = ah.newton_krylov_(ah.heat2d_euler_, ah.DeviceArray.from_numpy(u0),
+                             (un, P.dt, None, (P.a, P.hx, P.hy, ah.bc_zero_), 0.0))
+    assert r.solved and so["solved"]
+    assert r.stats.outer_iterations == so["outer_iterations"] == 0
+    assert r.stats.inner_iterations == so["inner_iterations"] == 0
+    assert not np.any(u.to_numpy()) and not np.any(ref)
