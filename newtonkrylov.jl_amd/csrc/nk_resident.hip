@@ -40,6 +40,7 @@ struct ResArgs {
     uint64_t* gran;        // 2 parities x G blocks x 2 granules
     int* err;              // pinned host flag: a poll timed out
     int noxchg;            // kernel-variant bench only (NK_RES_NOXCHG=1): skip the exchange, h stays fixed
+    int ntc;               // NTS: the first ntc streamed slots of a block load V_{i+1} cached (Infinity Cache room)
     int poll1;             // 1: one polling wave (NK_RES_POLL1, default 1), 2: four staggered polling waves, 0: every thread polls one partial
     int strided;           // slots interleaved across blocks (every block exactly full: no streamed remainder)
     uint64_t* tstamp;      // kernel-variant bench only: per pass and block, wall clock at pass end and after the hand-off
@@ -340,6 +341,19 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
             else *p = v;
         };
         int64_t e = lo + (int64_t)(RV + rl) * kResThreads + tid;
+        if constexpr (NTS) {  // the first ntc slots: V_{i+1} cached, re-read from the Infinity Cache next pass
+            const int64_t hc = std::min<int64_t>(hi, e - tid + (int64_t)A.ntc * kResThreads);
+            for (; e + kResThreads < hc; e += 2 * kResThreads) {
+                const int64_t e1 = e + kResThreads;
+                dx2 a0 = ld(q2 + e), a1 = ld(q2 + e1);
+                const dx2 b0 = __builtin_nontemporal_load(v2 + e), b1 = __builtin_nontemporal_load(v2 + e1);
+                const dx2 c0 = w2[e], c1 = w2[e1];
+                upd(a0, b0, c0);
+                upd(a1, b1, c1);
+                st(q2 + e, a0);
+                st(q2 + e1, a1);
+            }
+        }
         for (; e + kResThreads < hi; e += 2 * kResThreads) {
             const int64_t e1 = e + kResThreads;
             dx2 a0 = ld(q2 + e), a1 = ld(q2 + e1);
@@ -601,6 +615,18 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
     }
     static const int noxchg = env_int("NK_RES_NOXCHG", 0);
     A.noxchg = noxchg;
+    // NTS: the Infinity Cache (256 MB) keeps the resident part's V_{i+1} (4 KB per block and slot) for
+    // its re-read as the next pass's V_i; the room left (NK_RES_MALL_MB, default 244 MB of it) goes to
+    // the first streamed slots of every block, whose V_{i+1} then loads cached (NK_RES_NTC overrides
+    // the count): half resident 129.3 -> 120.2 us per pass, a quarter 313.1 -> 300.1
+    // (profiles/r02/ab_ntc.log; 128 slots, past the room, thrash)
+    static const int ntc_env = env_int("NK_RES_NTC", -1);
+    static const int mall_mb = env_int("NK_RES_MALL_MB", 244);
+    {
+        const double slot = 4096.0 * c->res_blocks;  // one slot of V across the grid, bytes
+        const double room = 1e6 * mall_mb - slot * (rv + A.rl);
+        A.ntc = ntc_env >= 0 ? ntc_env : (room > 0 ? (int)(room / slot) : 0);
+    }
     static const int poll1 = env_int("NK_RES_POLL1", 1);
     A.poll1 = poll1;
     A.tstamp = c->res_tstamp;
