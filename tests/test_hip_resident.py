@@ -274,3 +274,52 @@ def test_partly_resident_cycle_properties(ctx, case):
     est = ws.stats.residuals[-1]
     assert abs(ah.knorm(N, r) - est) <= 1e-10 * est
     ws.free()
+
+
+_FLAVOUR_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import _nkpath  # noqa: F401
+import ariadne_hip as ah
+from oracle import oracle as oc
+nx, ny = 4096, 6144  # 1.5x the register + LDS capacity: a third of q streams
+P = oc.bratu2d(nx, ny)
+u = oc.sin_ic(P)
+ud = ah.DeviceArray.from_numpy(u)
+res = ud.zero()
+p = (P.hx, P.hy, P.lam)
+ah.bratu2d_(res, ud, p)
+ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=8))
+ctx = ah.default_context()
+ctx.prof_enable(1 << 20)
+ah.krylov_solve_(ws, ah.JacobianOperator(ah.bratu2d_, res, ud, p, jv="exact"), res, restart=True, atol=0.0, rtol=0.0,
+                 itmax=12, history=True, reorthogonalization=True)
+sweeps = ctx.prof_read().get("mgs_sweep", {}).get("launches", 0)
+np.savez(sys.argv[2], x=ws.x.to_numpy(), h=np.array(ws.stats.residuals), sweeps=sweeps)
+"""
+
+
+def test_sweep_load_flavours_are_bitwise(tmp_path):
+    """The partly resident sweep's cache-policy choices change only how loads and stores are issued
+    -- the Infinity-Cache room given to the first streamed slots (NK_RES_NTC), the non-temporal
+    streamed remainder (NK_RES_NTS), the first batch loaded across the hand-off (NK_RES_PRE) -- never
+    the arithmetic or its order: restarted GMRES with reorthogonalisation, bit for bit."""
+    import os
+    import subprocess
+    import sys
+
+    tests = os.path.dirname(os.path.abspath(__file__))
+    runs = {}
+    for name, extra in [("default", {}), ("ntc0", {"NK_RES_NTC": "0"}), ("ntc_all", {"NK_RES_NTC": "100000"}),
+                        ("nts0", {"NK_RES_NTS": "0"}), ("pre0", {"NK_RES_PRE": "0"})]:
+        out = tmp_path / f"{name}.npz"
+        r = subprocess.run([sys.executable, "-c", _FLAVOUR_CHILD, tests, str(out)], env=dict(os.environ, **extra),
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, (name, r.stderr[-2000:])
+        runs[name] = np.load(out)
+    ref = runs["default"]
+    assert int(ref["sweeps"]) > 0 and len(ref["h"]) == 13  # r0 and the 12 Arnoldi steps
+    for name, d in runs.items():
+        assert int(d["sweeps"]) == int(ref["sweeps"]), name
+        assert np.array_equal(d["h"], ref["h"]), name
+        assert np.array_equal(d["x"], ref["x"]), name
