@@ -79,9 +79,11 @@ def test_resident_sweep_deterministic(ctx):
     assert runs[0][1].residuals == runs[1][1].residuals
 
 
-def test_resident_sweep_mailbox_one_rank_is_bitwise(ctx, monkeypatch):
-    """The sweep's per-pass scalars through the peer mailbox (self-send) equal the local ones bit for bit."""
-    P = oc.bratu2d(1024)
+@pytest.mark.parametrize("nx,ny", [(1024, 1024), (4096, 6144)])
+def test_resident_sweep_mailbox_one_rank_is_bitwise(ctx, monkeypatch, nx, ny):
+    """The sweep's per-pass scalars through the peer mailbox (self-send) equal the local ones bit for
+    bit -- all of q on chip (1024^2) and two thirds of it (4096 x 6144, config 4's per-rank regime)."""
+    P = oc.bratu2d(nx, ny)
     u = oc.sin_ic(P)
     b = oc.residual(P, u)
     plain = ah.Context(0)
