@@ -289,6 +289,35 @@ def test_newton_bratu2d_gmres30_golden(ctx, golden_dir):
     assert abs(F2 - r2.stats.n_res) <= 1e-10 * F2
 
 
+def test_newton_bratu2d_256_scipy_root(ctx):
+    """SURVEY §8c's independent root oracle at 256^2: a scipy sparse-direct Newton iteration
+    (tests/golden/make_golden.py's numpy residual and assembled Jacobian, computed here rather than
+    stored) against the device Newton-Krylov root -- ILU(0)-preconditioned GMRES(30), restarted, as
+    examples/bratu.jl:119-137 preconditions -- to 1e-8 of max |u| (||F|| <= 1e-11 ||F(u0)||, cond(J)
+    ~ 1e4), and ||F|| of the device root (on the oracle's residual) at the solve's tolerance."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_golden as mg
+    import scipy.sparse as sp
+
+    n = 256
+    P = oc.bratu2d(n)
+    u0 = oc.sin_ic(P)
+    h = P.hx
+    F = lambda u: (mg.d2(u, 1, h) + mg.d2(u, 0, h)) + mg.LAM * np.exp(u)  # noqa: E731
+    L = sp.kronsum(mg.lap1d(n, h), mg.lap1d(n, h))
+    ustar, hist = mg.newton_sparse(F, lambda u: L + sp.diags(mg.LAM * np.exp(u.ravel())), u0.copy(), tol=1e-9)
+    assert hist[-1] < 1e-9
+    u, r = ah.newton_krylov_(ah.bratu2d_, dev(u0), (P.hx, P.hy, P.lam), N=ah.ilu0, memory=30, tol_rel=1e-11,
+                             krylov_kwargs={"restart": True, "ldiv": True, "atol": 1e-15})
+    # (Krylov.jl's default atol = sqrt(eps) would stop every inner solve once ||F|| < 1.5e-8)
+    assert r.solved, (r.stats, r.n_res_history if hasattr(r, "n_res_history") else None)
+    got = u.to_numpy()
+    assert np.max(np.abs(got - ustar)) <= 1e-8 * np.max(np.abs(ustar))
+    assert oc.norm(oc.residual(P, got)) <= 2e-11 * oc.norm(oc.residual(P, u0))
+
+
 def test_newton_fd_vs_exact(ctx):
     P = oc.bratu2d(32)
     u0 = oc.sin_ic(P)
