@@ -3,7 +3,8 @@ oracle: SURVEY.md Appendix A, `src/Ariadne.jl:290-372`): a zero right-hand side 
 solved), an iteration cap below convergence (stopped at itmax, not solved), GMRES's breakdown on a
 grid smaller than its memory (the Krylov space exhausted: the exact solution), and a Newton start that
 is already a root (no Newton step).  Flags and counts equal the oracle's; histories to 1e-9 relative;
-solutions to the tolerance stated per test."""
+solutions to the tolerance stated per test.  Plus an oracle-independent check: one implicit heat step
+of every scheme, 2D and 3D, against scipy's sparse LU of the same linear system."""
 import numpy as np
 import pytest
 
@@ -110,3 +111,53 @@ def test_newton_start_at_root(ctx):
     assert r.stats.outer_iterations == so["outer_iterations"] == 0
     assert r.stats.inner_iterations == so["inner_iterations"] == 0
     assert not np.any(u.to_numpy()) and not np.any(ref)
+
+
+# ----------------------------------------------------------------------------- direct-solve oracle
+def _lap(shape, hs):
+    """The zero-Dirichlet Laplacian of a C-ordered (z,) y, x grid as a scipy sparse matrix (x fastest)."""
+    import scipy.sparse as sp
+
+    def d1(n, h):
+        return sp.diags([np.ones(n - 1), -2.0 * np.ones(n), np.ones(n - 1)], [-1, 0, 1]) / (h * h)
+
+    L = None
+    for n, h in zip(shape, hs):  # slowest axis first: kronsum(A, B) = A (x) I + I (x) B, B the faster axis
+        L = d1(n, h) if L is None else sp.kronsum(d1(n, h), L)
+    return L.tocsc()
+
+
+@pytest.mark.parametrize("dim,scheme", [(2, "euler"), (2, "midpoint"), (2, "trapezoid"), (3, "euler"),
+                                        (3, "midpoint"), (3, "trapezoid")])
+def test_implicit_step_matches_direct_solve(ctx, dim, scheme):
+    """One implicit time step (implicit.jl:8-37: G_Euler!, G_Midpoint! with alpha 0.3, G_Trapezoid!)
+    is a linear solve -- (I - dt a c L) u = u_n + dt a d L u_n with (c, d) = (1, 0), (1 - alpha, alpha),
+    (1/2, 1/2) -- so scipy's sparse LU gives the exact step independently of the oracle: the device
+    Newton-Krylov step, solved to ||G|| <= 1e-11, agrees to 1e-10 of max |u|."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+
+    rng = np.random.default_rng(21)
+    alpha = 0.3
+    if dim == 2:
+        n = 160
+        un = rng.standard_normal((n, n))
+        P = oc.heat2d_euler(n, un=un, scheme=scheme, alpha=alpha)
+        hs, diff, bcp = (P.hy, P.hx), ah.diffusion_, (P.a, P.hx, P.hy, ah.bc_zero_)
+    else:
+        n = 36
+        un = rng.standard_normal((n, n, n))
+        P = oc.heat3d_euler(n, un=un, scheme=scheme, alpha=alpha)
+        hs, diff, bcp = (P.hz, P.hy, P.hx), ah.diffusion3d_, (P.a, P.hx, P.hy, P.hz, ah.bc_zero_)
+    c, d = {"euler": (1.0, 0.0), "midpoint": (1.0 - alpha, alpha), "trapezoid": (0.5, 0.5)}[scheme]
+    L = _lap(un.shape, hs)
+    A = sp.identity(un.size, format="csc") - (P.dt * P.a * c) * L
+    rhs = un.ravel() + (P.dt * P.a * d) * (L @ un.ravel())
+    exact = spla.spsolve(A, rhs).reshape(un.shape)
+    G = {"euler": ah.G_Euler_, "midpoint": ah.G_Midpoint_(alpha=alpha), "trapezoid": ah.G_Trapezoid_}[scheme]
+    F = G.bind(diff)
+    und = ah.DeviceArray.from_numpy(un)
+    u, r = ah.newton_krylov_(F, und.copy(), (und, P.dt, None, bcp, 0.0), tol_abs=1e-11, tol_rel=0.0,
+                             krylov_kwargs={"atol": 1e-15})
+    assert r.solved
+    assert np.max(np.abs(u.to_numpy() - exact)) <= 1e-10 * np.max(np.abs(exact))
