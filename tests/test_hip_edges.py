@@ -114,12 +114,17 @@ def test_newton_start_at_root(ctx):
 
 
 # ----------------------------------------------------------------------------- direct-solve oracle
-def _lap(shape, hs):
-    """The zero-Dirichlet Laplacian of a C-ordered (z,) y, x grid as a scipy sparse matrix (x fastest)."""
+def _lap(shape, hs, periodic=False):
+    """The Laplacian of a C-ordered (z,) y, x grid as a scipy sparse matrix (x fastest): zero Dirichlet
+    (bc_zero!) or wrapped (bc_periodic!, heat_2D.jl:15-26)."""
     import scipy.sparse as sp
 
     def d1(n, h):
-        return sp.diags([np.ones(n - 1), -2.0 * np.ones(n), np.ones(n - 1)], [-1, 0, 1]) / (h * h)
+        m = sp.diags([np.ones(n - 1), -2.0 * np.ones(n), np.ones(n - 1)], [-1, 0, 1]).tolil()
+        if periodic:
+            m[0, n - 1] += 1.0
+            m[n - 1, 0] += 1.0
+        return m.tocsr() / (h * h)
 
     L = None
     for n, h in zip(shape, hs):  # slowest axis first: kronsum(A, B) = A (x) I + I (x) B, B the faster axis
@@ -127,10 +132,12 @@ def _lap(shape, hs):
     return L.tocsc()
 
 
+@pytest.mark.parametrize("bc", ["zero", "periodic"])
 @pytest.mark.parametrize("dim,scheme", [(2, "euler"), (2, "midpoint"), (2, "trapezoid"), (3, "euler"),
                                         (3, "midpoint"), (3, "trapezoid")])
-def test_implicit_step_matches_direct_solve(ctx, dim, scheme):
-    """One implicit time step (implicit.jl:8-37: G_Euler!, G_Midpoint! with alpha 0.3, G_Trapezoid!)
+def test_implicit_step_matches_direct_solve(ctx, dim, scheme, bc):
+    """One implicit time step (implicit.jl:8-37: G_Euler!, G_Midpoint! with alpha 0.3, G_Trapezoid!;
+    bc_zero! and bc_periodic!)
     is a linear solve -- (I - dt a c L) u = u_n + dt a d L u_n with (c, d) = (1, 0), (1 - alpha, alpha),
     (1/2, 1/2) -- so scipy's sparse LU gives the exact step independently of the oracle: the device
     Newton-Krylov step, solved to ||G|| <= 1e-11, agrees to 1e-10 of max |u|."""
@@ -139,18 +146,20 @@ def test_implicit_step_matches_direct_solve(ctx, dim, scheme):
 
     rng = np.random.default_rng(21)
     alpha = 0.3
+    per = bc == "periodic"
+    obc, dbc = (oc.BC_PERIODIC, ah.bc_periodic_) if per else (oc.BC_ZERO, ah.bc_zero_)
     if dim == 2:
         n = 160
         un = rng.standard_normal((n, n))
-        P = oc.heat2d_euler(n, un=un, scheme=scheme, alpha=alpha)
-        hs, diff, bcp = (P.hy, P.hx), ah.diffusion_, (P.a, P.hx, P.hy, ah.bc_zero_)
+        P = oc.heat2d_euler(n, un=un, scheme=scheme, alpha=alpha, bc=obc)
+        hs, diff, bcp = (P.hy, P.hx), ah.diffusion_, (P.a, P.hx, P.hy, dbc)
     else:
-        n = 36
+        n = 28  # scipy's LU of a 3D 7-point matrix fills in: 28^3 takes ~1 s, 36^3 ~7 s
         un = rng.standard_normal((n, n, n))
-        P = oc.heat3d_euler(n, un=un, scheme=scheme, alpha=alpha)
-        hs, diff, bcp = (P.hz, P.hy, P.hx), ah.diffusion3d_, (P.a, P.hx, P.hy, P.hz, ah.bc_zero_)
+        P = oc.heat3d_euler(n, un=un, scheme=scheme, alpha=alpha, bc=obc)
+        hs, diff, bcp = (P.hz, P.hy, P.hx), ah.diffusion3d_, (P.a, P.hx, P.hy, P.hz, dbc)
     c, d = {"euler": (1.0, 0.0), "midpoint": (1.0 - alpha, alpha), "trapezoid": (0.5, 0.5)}[scheme]
-    L = _lap(un.shape, hs)
+    L = _lap(un.shape, hs, per)
     A = sp.identity(un.size, format="csc") - (P.dt * P.a * c) * L
     rhs = un.ravel() + (P.dt * P.a * d) * (L @ un.ravel())
     exact = spla.spsolve(A, rhs).reshape(un.shape)
