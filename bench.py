@@ -359,7 +359,9 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)", file=sys.stderr)
         sys.exit(2)
     if args.launch_probe >= 0:  # CPU test of the launcher: report what this rank was given, no GPU work
-        print(json.dumps({"rank": rank, "world": world, "local": local, "argv": sys.argv[1:]}), flush=True)
+        # one write per line (text + newline together): the ranks share the pipe, and print()'s
+        # separate write of the newline lets another rank's line land in between when unbuffered
+        os.write(1, (json.dumps({"rank": rank, "world": world, "local": local, "argv": sys.argv[1:]}) + "\n").encode())
         sys.exit(args.launch_probe if rank == world - 1 else 0)
     dist = None
     if world > 1:
@@ -548,7 +550,8 @@ def main():
                 out["cpu_gpu_agreement"] = W.agreement()
         else:
             out["cpu_baseline"] = None
-        print(json.dumps(out), flush=True)
+        sys.stdout.write(json.dumps(out) + "\n")
+        sys.stdout.flush()
     W.free()
     if dist is not None:
         dist.destroy_process_group()

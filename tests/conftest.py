@@ -4,6 +4,11 @@ import sys
 
 import pytest
 
+# Under pytest-xdist every worker would start a full OpenMP team for the C oracle: 8 workers x 8
+# spinning threads on 8 cores turns a 1 s oracle test into ~10 min.  One worker = one thread.
+if os.environ.get("PYTEST_XDIST_WORKER") and "OMP_NUM_THREADS" not in os.environ:
+    os.environ["OMP_NUM_THREADS"] = "1"
+
 try:  # torch first: libnkhip.so must bind the same HIP runtime torch uses (user residuals run torch code)
     import torch  # noqa: F401
 except ImportError:  # pragma: no cover
