@@ -534,7 +534,8 @@ def main():
             # what plain streaming reaches on this GPU (roofline.frac_of_copy divides by it): the spec
             # 8 TB/s is not reachable by any access pattern (MI355X_MICROARCH.md: 6.29 TB/s best measured)
             "calibration": {"copy_gbs": round(copy_gbs, 1) if copy_gbs else None,
-                            "what": "y = x over 2 x 1 GiB (HBM, beyond the Infinity Cache), 16 B per lane, "
+                            "what": "y = x over 2 x 1 GiB (HBM, beyond the Infinity Cache), one 16-B element per "
+                                    "thread, non-temporal load + store (the fastest copy of tools/stream_probe.py), "
                                     "mean of 5 launches, after the timed region"},
         }
         if world == 1 and not args.no_cpu_baseline and not args.global_n:

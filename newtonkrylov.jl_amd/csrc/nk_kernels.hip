@@ -659,6 +659,20 @@ int red_blocks(int64_t n) {
     return (int)g;
 }
 
+// Grid of the streaming kernels whose partials (if any) only a one-block finaliser reads: up to
+// kRedCap - 2 blocks, >= 2 double2 per thread.  Many short-lived blocks stream faster than a
+// grid of 8 per CU looping over block chunks (tools/stream_probe.py: a plain copy 5.0 -> 6.2 TB/s;
+// k_update_x -9 % on heat 8192^2, profiles/r02/ab_redblocks.log).  Reductions consumed by every
+// block of the next kernel (dot, sumsq, the MGS chain) keep red_blocks: each consumer block sums
+// all the partials.
+int wide_blocks(int64_t n) {
+    static const int cap = std::max(1, std::min(kRedCap - 2, env_int("NK_WIDE_BLOCKS", kRedCap - 2)));
+    int64_t g = (n + 2LL * kBlock * 2 - 1) / (2LL * kBlock * 2);
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
 namespace {
 int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_override, int fast);
 }
@@ -831,7 +845,7 @@ int launch_finalize(nk_ctx* c, Red r, double* dst, int sqrt_it, double* mirror) 
 }
 
 #define NK_STREAM_LAUNCH(name, bytes_per, kern, ...)                                              \
-    const int g = red_blocks(n);                                                                   \
+    const int g = wide_blocks(n);                                                                  \
     return launch(c, name, (bytes_per) * (double)n,                                                \
                   [&] { hipLaunchKernelGGL(kern, dim3(g), dim3(kBlock), 0, c->stream, __VA_ARGS__); })
 
@@ -895,7 +909,7 @@ int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const dou
 
 int launch_update_x(nk_ctx* c, int64_t n, double* x, double* xr, const double* const* V, int k, const double* y_dev,
                     int restart, Red* xnorm, double* u) {
-    const int g = red_blocks(n);
+    const int g = wide_blocks(n);  // its ||x|| / ||u|| partials go to the finaliser only
     int done = 0;
     if (k == 0) {  // nothing to add: x unchanged (restart) or x = 0
         if (!restart) NK_TRY(launch_fill(c, n, x, 0.0));
@@ -1527,7 +1541,19 @@ extern "C" int nkb_update_x(nk_ctx* c, int64_t n, int k, int u_elems, int reps, 
     return NK_OK;
 }
 
-// plain streaming copy (y = x, 16 B per lane) as the achievable-bandwidth calibration point
+// The achievable-bandwidth calibration point: the fastest plain copy the stream probe found
+// (tools/stream_probe.py, profiles/r02/stream_probe.log): one 16-B element per thread, one block
+// per 256 elements, non-temporal load and store -- 6.2-6.5 TB/s, against 5.0 for a grid of 8
+// blocks per CU looping over block chunks (the calibration of the earlier round-2 bench lines).
+namespace nk {
+namespace {
+__global__ __launch_bounds__(kBlock) void k_copy_cal(int64_t n2, dx2* __restrict__ y, const dx2* __restrict__ x) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n2) __builtin_nontemporal_store(__builtin_nontemporal_load(x + i), y + i);
+}
+}  // namespace
+}  // namespace nk
+
 extern "C" int nkb_copy(nk_ctx* c, int64_t n, int reps, double* us_out) {
     using namespace nk;
     if (!c || n < 2 || reps < 1 || !us_out) return NK_E_ARG;
@@ -1538,9 +1564,16 @@ extern "C" int nkb_copy(nk_ctx* c, int64_t n, int reps, double* us_out) {
     hipEvent_t a, b;
     NK_HIP(c, hipEventCreate(&a));
     NK_HIP(c, hipEventCreate(&b));
-    NK_TRY(launch_copy(c, n, y, x));
+    const int64_t n2 = n / 2;  // the calibration counts 16 B per element pair moved: n even
+    const int64_t g = (n2 + kBlock - 1) / kBlock;
+    if (g > INT32_MAX) return NK_E_ARG;
+    auto go = [&] {
+        hipLaunchKernelGGL(k_copy_cal, dim3((unsigned)g), dim3(kBlock), 0, c->stream, n2, reinterpret_cast<dx2*>(y),
+                           reinterpret_cast<const dx2*>(x));
+    };
+    go();
     NK_HIP(c, hipEventRecord(a, c->stream));
-    for (int r = 0; r < reps; ++r) NK_TRY(launch_copy(c, n, y, x));
+    for (int r = 0; r < reps; ++r) go();
     NK_HIP(c, hipEventRecord(b, c->stream));
     NK_HIP(c, hipEventSynchronize(b));
     float ms = 0.f;
@@ -1560,7 +1593,7 @@ extern "C" int nkb_copy(nk_ctx* c, int64_t n, int reps, double* us_out) {
 // contiguous chunks, ORD 2 grid-stride with each block's U loads on consecutive 4 KB pieces.
 namespace nk {
 namespace {
-template <int U, int ORD, int R, bool NTL>
+template <int U, int ORD, int R, bool NTL, bool NTS = false>
 __global__ __launch_bounds__(kBlock) void k_stream_probe(int64_t n2, dx2* __restrict__ q, const dx2* __restrict__ v,
                                                         const dx2* __restrict__ w, double* __restrict__ part) {
     const int64_t nthr = (int64_t)gridDim.x * kBlock;
@@ -1603,7 +1636,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_probe(int64_t n2, dx2* __rest
                 acc = fma(c[u].x, a[u].x, acc);
                 acc = fma(c[u].y, a[u].y, acc);
             }
-            st2<false>(q + i + u * st, a[u]);
+            st2<NTS>(q + i + u * st, a[u]);
         }
     }
     if (acc == 12345.0) part[0] = acc;  // keeps the dot live
@@ -1628,6 +1661,7 @@ extern "C" int nkb_stream(nk_ctx* c, int64_t n, int variant, int grid, int reps,
     const dx2* ws = reinterpret_cast<const dx2*>(w);
     double* part = red_slot(c);
 #define NKB_S(U, O, R, NT) hipLaunchKernelGGL((k_stream_probe<U, O, R, NT>), dim3(g), dim3(kBlock), 0, c->stream, n2, qs, vs, ws, part)
+#define NKB_SN(U, O, NL) hipLaunchKernelGGL((k_stream_probe<U, O, 1, NL, true>), dim3(g), dim3(kBlock), 0, c->stream, n2, qs, vs, ws, part)
     auto go = [&] {
         switch (variant) {  // R=1: y(q) = x(v)    R=3: MGS pattern
         case 0: NKB_S(1, 0, 1, false); break;
@@ -1643,10 +1677,16 @@ extern "C" int nkb_stream(nk_ctx* c, int64_t n, int variant, int grid, int reps,
         case 10: NKB_S(4, 1, 3, true); break;
         case 11: NKB_S(2, 2, 3, true); break;
         case 12: NKB_S(4, 2, 3, true); break;
+        case 14: NKB_S(1, 0, 1, true); break;    // copy, non-temporal load
+        case 15: NKB_SN(1, 0, true); break;      // copy, non-temporal load and store
+        case 16: NKB_SN(1, 0, false); break;     // copy, non-temporal store
+        case 17: NKB_SN(4, 1, true); break;      // copy U4 chunk, non-temporal load and store
+        case 18: NKB_SN(2, 0, true); break;      // copy U2 grid-stride, non-temporal load and store
         default: NKB_S(1, 1, 3, true); break;
         }
     };
 #undef NKB_S
+#undef NKB_SN
     hipEvent_t a, b;
     NK_HIP(c, hipEventCreate(&a));
     NK_HIP(c, hipEventCreate(&b));

@@ -23,9 +23,13 @@ lib = ah.load()
 lib.nkb_stream.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]
 NAMES = {0: "copy U1 gs", 1: "copy U2 gs", 2: "copy U4 gs", 3: "copy U2 chunk", 4: "copy U4 chunk",
          5: "copy U2 gs-blk", 6: "copy U4 gs-blk", 7: "mgs U1 gs", 8: "mgs U2 gs", 9: "mgs U2 chunk",
-         10: "mgs U4 chunk", 11: "mgs U2 gs-blk", 12: "mgs U4 gs-blk", 13: "mgs U1 chunk"}
-BYTES = {v: (16.0 if v < 7 else 32.0) for v in NAMES}
-configs = [(v, g) for v in NAMES for g in (512, 1024, 1536, 2048, 4096)]
+         10: "mgs U4 chunk", 11: "mgs U2 gs-blk", 12: "mgs U4 gs-blk", 13: "mgs U1 chunk",
+         14: "copy U1 gs ntl", 15: "copy U1 gs ntl+nts", 16: "copy U1 gs nts", 17: "copy U4 chunk ntl+nts",
+         18: "copy U2 gs ntl+nts"}
+BYTES = {v: (16.0 if (v < 7 or v >= 14) else 32.0) for v in NAMES}
+ap2 = [int(x) for x in os.environ.get("NK_PROBE_VARIANTS", ",".join(map(str, NAMES))).split(",")]
+grids = [int(x) for x in os.environ.get("NK_PROBE_GRIDS", "512,1024,1536,2048,4096,8192,32768").split(",")]
+configs = [(v, g) for v in ap2 for g in grids]
 res = {k: [] for k in configs}
 us = C.c_double()
 for _ in range(args.rounds):
