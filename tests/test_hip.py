@@ -132,7 +132,9 @@ def test_jv_fd_parity(ctx, P, u):
     assert np.max(np.abs(out.to_numpy() - exact)) <= 1e-5 * np.max(np.abs(exact))
 
 
-@pytest.mark.parametrize("n", [1, 2, 7, 1000, 4097, 1 << 20])
+# (1 << 24) + 3 and (1 << 25) + 1: the wide streaming grid (kRedCap - 2 blocks) with blocks past the
+# last chunk and an odd tail element
+@pytest.mark.parametrize("n", [1, 2, 7, 1000, 4097, 1 << 20, (1 << 24) + 3, (1 << 25) + 1])
 def test_blas1_parity(ctx, n):
     rng = np.random.default_rng(n)
     x, y = rng.standard_normal(n), rng.standard_normal(n)
