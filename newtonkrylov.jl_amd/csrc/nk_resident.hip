@@ -210,12 +210,15 @@ template <int B>
 struct ResPre {
     dx2 b[B], c[B];
 };
+// rev (ALT with PRE, B = 4): the pass starts on the top LDS group, slots RV + rl - 4 .. RV + rl - 1
 template <int RV, int B, bool PRE, int NTM = 0>
-__device__ __forceinline__ void res_prefetch(const ResArgs& A, ResPre<B>& P, int t, int64_t base, int64_t ss) {
+__device__ __forceinline__ void res_prefetch(const ResArgs& A, ResPre<B>& P, int t, int64_t base, int64_t ss,
+                                             bool rev = false) {
     if constexpr (PRE && RV >= B) {
         const int tid = threadIdx.x;
-        const dx2* vb = reinterpret_cast<const dx2*>(A.V[t]) + base + tid;
-        const dx2* wb = reinterpret_cast<const dx2*>(A.V[t + 1 < A.np ? t + 1 : t]) + base + tid;
+        const int s0 = (B == 4 && rev) ? RV + A.rl - 4 : 0;
+        const dx2* vb = reinterpret_cast<const dx2*>(A.V[t]) + base + tid + s0 * ss;
+        const dx2* wb = reinterpret_cast<const dx2*>(A.V[t + 1 < A.np ? t + 1 : t]) + base + tid + s0 * ss;
 #pragma unroll
         for (int u = 0; u < B; ++u) {
             P.b[u] = ldv<NTM>(vb + u * ss);
@@ -252,7 +255,7 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
         for (int bi = 0; bi < NB; ++bi) {
             const int s0 = bi * B;
             dx2 bv[B], cv[B];
-            if (PRE && RV >= B && s0 == 0) {
+            if (PRE && RV >= B && s0 == 0 && !(B == 4 && rev)) {
 #pragma unroll
                 for (int u = 0; u < B; ++u) {
                     bv[u] = P.b[u];
@@ -322,6 +325,22 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
         } else if (!rev) {
             for (int s = 0; s < r4; s += 4) one4(s, false);
             for (int s = r4; s < rl; ++s) one(s);
+        } else if (PRE && B == 4 && RV >= B) {
+            // ALT with PRE: groups of 4 from the top (the first one preloaded across the hand-off,
+            // the previous pass's last V_{i+1} lines), then the rl % 4 lowest slots
+            {
+                const int s = rl - 4;
+#pragma unroll
+                for (int u0 = 0; u0 < 4; ++u0) {
+                    const int u = 3 - u0;
+                    dx2 a = lq[(s + u) * kResThreads + tid];
+                    upd(a, P.b[u], P.c[u]);
+                    lq[(s + u) * kResThreads + tid] = a;
+                }
+            }
+            int s = rl - 8;
+            for (; s >= 0; s -= 4) one4(s, true);
+            for (s += 3; s >= 0; --s) one(s);
         } else {
             for (int s = rl - 1; s >= r4; --s) one(s);
             for (int s = r4 - 4; s >= 0; s -= 4) one4(s, true);
@@ -433,7 +452,7 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
             if (A.colh) A.colh[t] = h;
         }
         const double acc = res_pass<RV, B, PRE, NTM, NTS, LB>(A, S, lq, t, -h, lo, hi, P, base, ss, ALT && (t & 1));
-        if (t + 1 < A.np) res_prefetch<RV, B, PRE, NTM>(A, P, t + 1, base, ss);
+        if (t + 1 < A.np) res_prefetch<RV, B, PRE, NTM>(A, P, t + 1, base, ss, ALT && ((t + 1) & 1));
         const double part = block_sum<kResThreads>(acc, sh);
         if (A.tstamp && tid == 0) A.tstamp[((size_t)t * G + blockIdx.x) * 2] = wall_clock64();
         if (!A.noxchg) h = res_exchange(A, part, t + xo, sh, budget, &xdone);
@@ -505,7 +524,8 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
                  res_attr<89, 6, false, false, true>(lmax) && res_attr<89, 6, false, false, false, 1>(lmax) &&
                  res_attr<89, 6, false, false, false, 2>(lmax) && res_attr<89, 6, false, false, false, 0, true>(lmax) &&
                  res_attr<89, 4, true, false, false, 0, true>(lmax) && res_attr<89, 2, true>(lmax) &&
-                 res_attr<89, 4, true, false, false, 0, false, 8>(lmax) && res_attr<89, 4, true, false, false, 0, false, 6>(lmax);
+                 res_attr<89, 4, true, false, false, 0, false, 8>(lmax) && res_attr<89, 4, true, false, false, 0, false, 6>(lmax) &&
+                 res_attr<89, 4, true, false, true>(lmax);
             int per_cu = 0;  // residency: at least one block of the largest variant per CU
             ok = ok && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_mgs_res<89>),
                                                                     kResThreads, lmax) == hipSuccess && per_cu >= 1;
@@ -553,7 +573,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         static const int rv_env = env_int("NK_RES_RV", -1);
         int rl = std::min(slots, rl_env >= 0 ? std::min(rl_env, c->res_rl) : c->res_rl);  // LDS first
         const bool explicit_rv = rv >= 0 || rv_env >= 0;  // a caller's choice skips the benefit test below
-        if (rv >= 1000) {  // kernel-variant bench: 1000 + {0: 89 slots, batches of 4 + prefetch across the hand-off; 1: same, no prefetch; 2: alternating slot order; 3: V_i cached; 4: V_{i+1} non-temporal; 5: streamed remainder non-temporal (NTS); 6: 0 + 5; 8: batches of 2 + prefetch (batches of 6 + prefetch spill); 9 / 10: 0 with LDS slots in batches of 8 / 6}
+        if (rv >= 1000) {  // kernel-variant bench: 1000 + {0: 89 slots, batches of 4 + prefetch across the hand-off; 1: same, no prefetch; 2: alternating slot order; 3: V_i cached; 4: V_{i+1} non-temporal; 5: streamed remainder non-temporal (NTS); 6: 0 + 5; 8: batches of 2 + prefetch (batches of 6 + prefetch spill); 9 / 10: 0 with LDS slots in batches of 8 / 6; 11: 0 with alternate passes starting on the top LDS group (prefetched across the hand-off)}
             xv = rv - 1000;
             rv = 89;
         }
@@ -569,6 +589,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         if (xv < 0) rv = pick;
         else if (rv > slots) return 1;
         A.rl = std::min(rl, slots - rv);
+        if (xv == 11 && A.rl < 4) xv = 0;  // ALT + prefetch starts on the top LDS group of 4
         // worth it from two passes on (a one-pass sweep only adds q's load + store) while a tenth of q
         // or more is resident (tools/kbench_res.py per pass vs the chain: 4096^2 1.28x at k = 2,
         // 1.8x from k = 16; 2 x 4096^2 (half resident) 1.40-1.52x; 8192^2 (a quarter) 1.16-1.18x;
@@ -670,6 +691,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
             else if (xv == 8) hipLaunchKernelGGL((k_mgs_res<89, 2, true>), g, b, lds, c->stream, A);
             else if (xv == 9) hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, false, 0, false, 8>), g, b, lds, c->stream, A);
             else if (xv == 10) hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, false, 0, false, 6>), g, b, lds, c->stream, A);
+            else if (xv == 11) hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, true>), g, b, lds, c->stream, A);
             else if (streamed && nts_env && pre_env)
                 hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, false, 0, true>), g, b, lds, c->stream, A);
             else if (streamed && nts_env) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, false, 0, true>), g, b, lds, c->stream, A);
