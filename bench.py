@@ -373,11 +373,19 @@ def main():
     ndev = ah.device_count()
     if ndev < 1:
         raise SystemExit("bench.py: no GPU visible (the HIP path has no CPU fallback)")
-    shared = world > ndev
+    device = int(os.environ.get("NK_BENCH_DEVICE", local % ndev))  # NK_BENCH_DEVICE: diagnostic override
+    shared = False
+    if dist is not None:
+        # ranks share a GPU only if two of them name the same device: a launcher that gives every
+        # rank its own GPU through a visibility variable (each rank then sees ONE device) is not sharing
+        vis = tuple(os.environ.get(k, "") for k in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES",
+                                                     "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL"))
+        keys = [None] * world
+        dist.all_gather_object(keys, (vis, device))
+        shared = len(set(keys)) < world
     if shared and args.transport == "rccl":
         raise SystemExit(f"bench.py: {world} ranks on {ndev} GPU(s): RCCL needs one GPU per rank "
                          "(use --transport mailbox with a small --side to rehearse on fewer GPUs)")
-    device = int(os.environ.get("NK_BENCH_DEVICE", local % ndev))  # NK_BENCH_DEVICE: diagnostic override
     ctx = ah.Context(device)
     ah.set_default_context(ctx)
     if world > 1 and args.transport == "mailbox":
@@ -520,7 +528,8 @@ def main():
             "config": {"workload": W.workload, "matvecs_per_step": matvecs // max(1, args.steps),
                        "parallelism": f"slab{world}" if not args.slab_of else f"slab 1 of {args.slab_of} (one GPU)",
                        "reorthogonalization": bool(getattr(W, "reorth", args.reorth == "on")),
-                       "devices": f"{min(world, ndev)} GPU(s) for {world} rank(s)" + (" (shared: rehearsal)" if shared else ""),
+                       "devices": (f"{min(world, ndev)} GPU(s) for {world} rank(s) (shared: rehearsal)" if shared
+                                   else f"{world} GPU(s), one per rank"),
                        "reductions": ("peer mailbox (IPC/xGMI)" if ctx.mailbox_active else
                                       ("ncclAllReduce" if world > 1 else "local"))},
             # whole job: operand bytes through the memory hierarchy, and the unique-DRAM model, per second
