@@ -726,6 +726,9 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         A.rows = (int)rows;
         A.tiles_y = (int)((p->ny + rows - 1) / rows);
         grid = A.tiles_x * A.tiles_y;
+        // raw stencil rows three ahead (fast bit 64 / NK_ST_D3; periodic kinds keep two)
+        static const int d3_env = env_int("NK_ST_D3", 0);
+        A.d3 = ((fast & 64) || d3_env) && !per ? 1 : 0;
     } else {
         vec = (p->nx % 2 == 0) ? 2 : 1;
         // rows per 3D tile and the y-neighbour path (k_st3d loads, k_st3l LDS); fast bits 8 / 16 select

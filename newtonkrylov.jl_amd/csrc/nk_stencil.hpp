@@ -30,6 +30,7 @@ struct KArgs {
     int nw;              // 3D: rows (waves) per tile
     int lds3;            // 3D: y-neighbour rows through LDS (k_st3l) instead of per-wave loads (k_st3d)
     int f0r;             // 2D FD: F0 = F(u) recomputed from the u rows already loaded (k_st2d<..., F0R>)
+    int d3;              // 2D, VEC 2, not periodic: raw stencil rows three ahead in flight (k_st2d<..., D3>)
     // ghost planes of v through the peers' inboxes inside this launch (halo_tile_exchange): the rank
     // has a lower / upper neighbour whose boundary patch this launch fetches itself
     int hx_lo, hx_hi;
@@ -495,7 +496,9 @@ __device__ __forceinline__ LR x_nbrs(double cfirst, double clast, double e, doub
 // exactly the residual kernel's arithmetic (the u field cooked as MODE_RES, the same Laplacian and
 // point_value), so (F(w) - F(u)) / eps is bit-identical to loading the F0 that kernel stored, and
 // 8 B/pt less is read.  Valid only when F0 IS that residual of this u (the Newton loop's res).
-template <int KIND, int MODE, int EPI, int VEC, bool PER = false, bool F0R = false>
+// D3: the raw rows of the stencil field are issued three rows ahead instead of two (one more raw
+// row in registers), so more loads are in flight per wave; loads only -- bit-identical results.
+template <int KIND, int MODE, int EPI, int VEC, bool PER = false, bool F0R = false, bool D3 = false>
 __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     __shared__ double sh[kShN];
     KArgs A = A0;
@@ -554,6 +557,13 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
         RawRow<MODE, VEC> rp =
             (ib_hi && y0 + 1 == ny) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, (y0 + 1) * nx + xc, xc)
                                     : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 + 1) * nx + xc, (y0 + 1) * nx + xc + de, (y0 + 1) * nx + xc + de2);
+        RawRow<MODE, VEC> rq{};  // D3: row y0 + 2 (clamped to y1, the last row the tile reads)
+        if constexpr (D3) {
+            const int64_t r = y0 + 2 < y1 ? y0 + 2 : y1;
+            const int64_t oq = r * nx + xc;
+            rq = (ib_hi && r == ny) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, oq, xc)
+                                    : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, oq, oq + de, oq + de2);
+        }
         Row<VEC> uc{}, unc{}, f0c{}, ax{};
         {
             const int64_t o = y0 * nx + xc;
@@ -566,8 +576,8 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
             const int64_t o = j * nx + xc;
             // ---- issue: raw row j+2 (rows up to ny are the ghost plane; y1 <= ny keeps j+2 <= ny+1
             //      in range only when j+1 < y1, so clamp to row j+1 otherwise)
-            const int64_t o2 = (j + 1 < y1) ? o + 2 * nx : o + nx;
-            const int64_t r2 = (j + 1 < y1) ? j + 2 : j + 1;  // the row o2 is in (ny: the upper ghost row)
+            const int64_t r2 = D3 ? (j + 3 < y1 ? j + 3 : y1) : ((j + 1 < y1) ? j + 2 : j + 1);  // (ny: the upper ghost row)
+            const int64_t o2 = r2 * nx + xc;
             const RawRow<MODE, VEC> rpp = (ib_hi && r2 == ny) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, o2, xc)
                                                               : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, o2, o2 + de, o2 + de2);
             Row<VEC> ucn{}, uncn{}, f0cn{}, axn{};
@@ -634,7 +644,12 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
                 um = uc_;
                 uc_ = up;
             }
-            rp = rpp;
+            if constexpr (D3) {
+                rp = rq;
+                rq = rpp;
+            } else {
+                rp = rpp;
+            }
             uc = ucn;
             unc = uncn;
             f0c = f0cn;
@@ -1055,12 +1070,14 @@ void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
                         return;
                     }
                 }
-                if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2, false, true>), dim3(grid), dim3(kBlock), 0, s, A);
+                if (vec == 2 && A.d3) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2, false, true, true>), dim3(grid), dim3(kBlock), 0, s, A);
+                else if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2, false, true>), dim3(grid), dim3(kBlock), 0, s, A);
                 else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1, false, true>), dim3(grid), dim3(kBlock), 0, s, A);
                 return;
             }
         }
         if (vec == 4) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 4>), dim3(grid), dim3(kBlock), 0, s, A);
+        else if (vec == 2 && A.d3) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2, false, false, true>), dim3(grid), dim3(kBlock), 0, s, A);
         else if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
         else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1>), dim3(grid), dim3(kBlock), 0, s, A);
     } else {
