@@ -91,9 +91,9 @@ def parse():
                          "workloads (heat_2D.jl:131 solves with reorthogonalization = true), off for Bratu")
     ap.add_argument("--no-prof", action="store_true", help="do not time kernels with HIP events")
     ap.add_argument("--prof-every", type=int, default=0,
-                    help="time every k-th launch of each kernel class (HIP events; k > 1 keeps their cost out); "
-                         "0 = 64 for bratu2d (~6000 launches per class), 1 for the heat workloads (11 matvecs per "
-                         "step: every launch timed, so each class has >= 10 timed launches)")
+                    help="time every k-th launch of each kernel class (HIP events; k > 1 keeps their cost out of "
+                         "the timed region); 0 = 64 for bratu2d (~6000 launches per class), 8 for the heat "
+                         "workloads (11 matvecs per step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--transport", choices=["rccl", "mailbox"], default="rccl",
                     help="N > 1: rccl = nk_dist_init (RCCL bootstrap; peer mailbox + IPC ghost planes when available); "
@@ -102,8 +102,8 @@ def parse():
                          "the other rank's kernels room on the shared GPU)")
     ap.add_argument("--cpu-itmax", type=int, default=300, help="Arnoldi steps in the CPU-baseline sample (300 = one bench step)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="0: OMP_NUM_THREADS (the GPU box's per-GPU CPU share), else every core in the affinity "
-                         "mask; the machine's nproc is reported beside it")
+                    help="threads of the headline CPU sample (0: every core in the affinity mask); the per-GPU "
+                         "share (OMP_NUM_THREADS) is timed beside it and the machine's nproc reported")
     ap.add_argument("--traffic-json", default="",
                     help="per-kernel HBM traffic from separate rocprofv3 --pmc passes (tools/pmc_traffic.py); "
                          "default profiles/<latest round>/pmc_traffic_<workload>_<side>.json when present (a file "
@@ -112,15 +112,28 @@ def parse():
     return ap.parse_args()
 
 
-def copy_calibration(ctx, n=1 << 27, reps=5):
-    """Achievable HBM streaming rate on this GPU: the library's plain copy kernel (nkb_copy) over two
-    1 GiB vectors, run after the timed region (GB/s on 16 B per element)."""
+def copy_calibration(device, n=1 << 27, reps=5):
+    """Achievable HBM streaming rate on this GPU: a plain copy over two 1 GiB vectors (nkb_copy, one 16-B
+    element per thread, non-temporal), run after the timed region (GB/s on 16 B per element).  The copy
+    is a timing hook of the kernel-variant bench build (lib/libnkhip_kbench.so, its own context): the
+    product library carries no timing hooks."""
     import ctypes as C
 
-    lib = ah.load()
-    lib.nkb_copy.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.POINTER(C.c_double)]
+    from ariadne_hip import _lib
+
+    if not os.path.exists(_lib.KBENCH_LIB):
+        return None
+    kb = C.CDLL(_lib.KBENCH_LIB)
+    kb.nk_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+    kb.nk_ctx_destroy.argtypes = [C.c_void_p]
+    kb.nkb_copy.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.POINTER(C.c_double)]
+    h = C.c_void_p()
+    if kb.nk_ctx_create(device, C.byref(h)) != 0:
+        return None
     us = C.c_double()
-    if lib.nkb_copy(ctx.handle, n, reps, C.byref(us)) != 0 or us.value <= 0:
+    rc = kb.nkb_copy(h, n, reps, C.byref(us))
+    kb.nk_ctx_destroy(h)
+    if rc != 0 or us.value <= 0:
         return None
     return 16.0 * n / (us.value * 1e-6) / 1e9
 
@@ -331,12 +344,39 @@ class HeatEuler:
             u, st = oc.newton_krylov(P, u, tol_abs=6e-6, memory=self.args.memory or 20, jv=self.args.jv,
                                      reorthogonalization=self.reorth)
             dt += time.perf_counter() - t0
+            if steps == 0:  # the first time step, for the CPU/GPU agreement check
+                self.cpu_step = (u0, u.copy(), st)
             P.un = u
             steps, newton, matvecs = steps + 1, newton + st["outer_iterations"], matvecs + st["n_matvec"]
         return dict(value=matvecs / dt, unit="matvecs/s", cores=oc.get_threads(), kind="port",
                     sample=f"oracle/nk_oracle.c: {steps} {self.args.scheme} time steps (reorthogonalization="
                            f"{self.reorth}; {newton} Newton, {matvecs} matvecs) of the same {self.dim}D heat problem "
                            f"at {m}^{self.dim} (noise from numpy default_rng(0)), {dt:.2f} s")
+
+    def agreement(self):
+        """The CPU sample's first time step repeated on the GPU from the same u0 (same seed, same grid):
+        a converged implicit step, so the comparable quantity is the new state u_{n+1} itself (its
+        ||F|| sits at the solver tolerance, where it is solve noise) -- GPU vs CPU to 1e-10 relative,
+        with the Newton / Krylov counts and both final ||F|| reported."""
+        u0, u_cpu, st = self.cpu_step
+        g = ah.Grid.full(*u0.shape[::-1])
+        un = ah.DeviceArray.from_numpy(u0, g, self.un.ctx)
+        u = un.copy()
+        res = u.zero()
+        p = (un,) + tuple(self.p[1:])
+        ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=self.args.memory or 20))
+        _, r = ah.newton_krylov_(self.F, u, p, res, tol_abs=6.0e-6, memory=self.args.memory or 20,
+                                 jv=self.args.jv, workspace=ws, krylov_kwargs=dict(reorthogonalization=self.reorth))
+        u_gpu = u.to_numpy()
+        ws.free()
+        d = float(np.linalg.norm(u_gpu - u_cpu) / np.linalg.norm(u_cpu))
+        same = (r.stats.outer_iterations, r.stats.inner_iterations) == (st["outer_iterations"], st["inner_iterations"])
+        return {"quantity": f"u after one implicit {self.args.scheme} time step (converged newton_krylov!, "
+                            f"tol_abs=6e-6), GPU vs CPU, relative 2-norm",
+                "value": d, "tolerance": 1e-10, "ok": bool(d <= 1e-10 and same),
+                "counts_gpu": [r.stats.outer_iterations, r.stats.inner_iterations],
+                "counts_cpu": [st["outer_iterations"], st["inner_iterations"]],
+                "n_res_gpu": r.stats.n_res, "n_res_cpu": st["n_res"]}
 
     def free(self):
         self.ws.free()
@@ -374,20 +414,18 @@ def main():
     if ndev < 1:
         raise SystemExit("bench.py: no GPU visible (the HIP path has no CPU fallback)")
     device = int(os.environ.get("NK_BENCH_DEVICE", local % ndev))  # NK_BENCH_DEVICE: diagnostic override
+    ctx = ah.Context(device)
+    ah.set_default_context(ctx)
     shared = False
     if dist is not None:
-        # ranks share a GPU only if two of them name the same device: a launcher that gives every
-        # rank its own GPU through a visibility variable (each rank then sees ONE device) is not sharing
-        vis = tuple(os.environ.get(k, "") for k in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES",
-                                                     "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL"))
+        # ranks share a GPU only if two of them hold the same physical device: (host, PCI bus id of the
+        # device this rank opened) -- independent of how a launcher spells visibility (ordinals, UUIDs)
         keys = [None] * world
-        dist.all_gather_object(keys, (vis, device))
+        dist.all_gather_object(keys, (socket.gethostname(), ctx.path_info()["pci_bus_id"]))
         shared = len(set(keys)) < world
     if shared and args.transport == "rccl":
         raise SystemExit(f"bench.py: {world} ranks on {ndev} GPU(s): RCCL needs one GPU per rank "
                          "(use --transport mailbox with a small --side to rehearse on fewer GPUs)")
-    ctx = ah.Context(device)
-    ah.set_default_context(ctx)
     if world > 1 and args.transport == "mailbox":
         handles = [None] * world
         dist.all_gather_object(handles, ctx.mailbox_handle())
@@ -414,15 +452,23 @@ def main():
         step()
     barrier()
     if not args.prof_every:
-        args.prof_every = 64 if args.workload == "bratu2d" else 1
+        args.prof_every = 64 if args.workload == "bratu2d" else 8
     if not args.no_prof:
         ctx.prof_reset()
         ctx.prof_enable(args.prof_every)
+    # failure-path rehearsal (tests/test_hip_dist.py): this rank stops taking part -- it hangs before its
+    # first timed step, as a stuck peer would; the other ranks' mailbox waits must time out into an
+    # NK_E_* error and the whole launch exit non-zero instead of hanging
+    fault_rank = int(os.environ.get("NK_BENCH_FAULT_RANK", "-1"))
     barrier()
     t0 = time.perf_counter()
     matvecs = 0
     last = None
     for _ in range(args.steps):
+        if rank == fault_rank and world > 1:
+            print(f"bench.py: rank {rank}: NK_BENCH_FAULT_RANK -- hanging instead of stepping", file=sys.stderr,
+                  flush=True)
+            time.sleep(3600)
         mv, last = step()
         matvecs += mv
     ctx.sync()
@@ -437,7 +483,17 @@ def main():
         elapsed = float(tt.item())
     prof = ctx.prof_read() if not args.no_prof else {}
     ctx.prof_enable(0)
-    copy_gbs = copy_calibration(ctx) if rank == 0 else None
+    # the path every rank actually ran (transport, resident sweep, in-launch ghost planes, sharing) and
+    # the launch counts that prove it: a multi-GPU line names its own path
+    path = ctx.path_info()
+    path["host"] = socket.gethostname()
+    path["launches"] = {k: prof.get(k, {}).get("launches", 0)
+                        for k in ("mgs_sweep", "mgs_pass", "mgs_pass_last", "halo_ipc", "halo_rccl", "allreduce")}
+    paths = [path]
+    if dist is not None:
+        paths = [None] * world
+        dist.all_gather_object(paths, path)
+    copy_gbs = copy_calibration(device) if rank == 0 else None
 
     # Two byte counts per kernel class (nk_prof_entry): `bytes` = the operand bytes the kernel moves
     # through the memory hierarchy (every load / store it issues, served by L2, the Infinity Cache or
@@ -531,7 +587,12 @@ def main():
                        "devices": (f"{min(world, ndev)} GPU(s) for {world} rank(s) (shared: rehearsal)" if shared
                                    else f"{world} GPU(s), one per rank"),
                        "reductions": ("peer mailbox (IPC/xGMI)" if ctx.mailbox_active else
-                                      ("ncclAllReduce" if world > 1 else "local"))},
+                                      ("ncclAllReduce" if world > 1 else "local")),
+                       "path": {"mailbox_all_ranks": all(q["mailbox"] for q in paths),
+                                "resident_sweep_all_ranks": all(q["launches"]["mgs_sweep"] > 0 for q in paths),
+                                "halo_in_launch_all_ranks": all(q["halo_in_launch"] for q in paths) if world > 1
+                                else None,
+                                "mailbox_errors": sum(1 for q in paths if q["mailbox_error"])}},
             # whole job: operand bytes through the memory hierarchy, and the unique-DRAM model, per second
             "gbs_l2_egress_wholejob": round(world * total_bytes / elapsed / 1e9, 1) if total_bytes else None,
             "gbs_dram_model_wholejob": round(world * total_dram / elapsed / 1e9, 1) if total_dram else None,
@@ -547,15 +608,24 @@ def main():
                                     "thread, non-temporal load + store (the fastest copy of tools/stream_probe.py), "
                                     "mean of 5 launches, after the timed region"},
         }
+        if world > 1:
+            out["ranks"] = paths  # per rank: transport, resident sweep, in-launch ghost planes, launch counts
         if world == 1 and not args.no_cpu_baseline and not args.global_n:
-            # the CPU share this process is given: OMP_NUM_THREADS (the GPU box sets it to its per-GPU share
-            # of the host, 16), else every core in the affinity mask; the machine's full count is reported too
+            # the node's host cores: every core in this process's affinity mask (the headline figure), and
+            # the per-GPU share the box gives one GPU (OMP_NUM_THREADS, 16 there) beside it; nproc is the
+            # machine's full count
             affinity = len(os.sched_getaffinity(0))
-            threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
-            out["cpu_baseline"] = W.cpu_baseline(threads)
-            out["cpu_baseline"]["host_cpus"] = {"nproc": os.cpu_count(), "affinity": affinity,
-                                                "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
-            out["cpu_baseline"]["value"] = round(out["cpu_baseline"]["value"], 4)
+            share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+            threads = args.cpu_threads or affinity
+            cb = W.cpu_baseline(threads)
+            cb["value"] = round(cb["value"], 4)
+            cb["host_cpus"] = {"nproc": os.cpu_count(), "affinity": affinity,
+                               "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+            if share and share != threads:
+                sh = W.cpu_baseline(share)
+                cb["per_gpu_share"] = {"value": round(sh["value"], 4), "unit": sh["unit"], "cores": sh["cores"],
+                                       "sample": sh["sample"]}
+            out["cpu_baseline"] = cb
             if hasattr(W, "agreement"):
                 out["cpu_gpu_agreement"] = W.agreement()
         else:

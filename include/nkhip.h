@@ -297,6 +297,22 @@ int nk_halo_exchange(nk_ctx* ctx, const nk_problem* p, double* v);
 int nk_dist_mailbox_handle(nk_ctx* ctx, char out[64]);
 int nk_dist_mailbox_open(nk_ctx* ctx, int32_t rank, int32_t nranks, const char* handles /* nranks x 64 */);
 int nk_dist_mailbox_active(nk_ctx* ctx);  /* 1: reductions use the peer mailbox, 0: RCCL / single rank */
+/* Which distributed path this context runs (diagnostics: bench.py prints it for every rank, so a
+ * multi-GPU run names the transport it actually used).  No reference counterpart: the reference
+ * has no distributed path (its ghost-cell pattern is examples/halovector.jl:1-45). */
+typedef struct nk_path_info {
+    int32_t rank, nranks, device;
+    int32_t ranks_on_device;  /* ranks sharing this GPU, this one included (1: one GPU per rank)        */
+    int32_t rccl;             /* an RCCL communicator exists (bootstrap; fallback transport)            */
+    int32_t mailbox;          /* reductions and ghost planes through the IPC peer mailbox (xGMI)        */
+    int32_t resident_sweep;   /* the one-launch resident MGS sweep may run (0: one launch per MGS pass)  */
+    int32_t resident_blocks;  /* its grid once set up (0: not run yet)                                 */
+    int32_t halo_in_launch;   /* a Krylov Jv's ghost planes travel inside the stencil launch           */
+    int32_t mailbox_error;    /* a mailbox wait timed out (a peer never arrived): sticky                */
+    int64_t halo_cap;         /* doubles per IPC inbox plane (larger planes: RCCL send/recv)            */
+    char pci_bus_id[32];      /* this rank's device                                                    */
+} nk_path_info;
+int nk_dist_path(nk_ctx* ctx, nk_path_info* out);
 
 /* ---------------------------------------------------------------- profiling (HIP events, per kernel class) */
 #define NK_PROF_NAME 32

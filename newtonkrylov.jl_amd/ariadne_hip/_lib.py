@@ -11,7 +11,11 @@ import os
 import sys
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libnkhip.so")
+PRODUCT_LIB = os.path.join(PKG_DIR, "lib", "libnkhip.so")
+# the kernel-variant bench build of the same sources (tuning knobs from the environment, nkb_* hooks);
+# NK_KBENCH_LIB=1 loads it instead -- tools/ and the variant-equivalence tests only
+KBENCH_LIB = os.path.join(PKG_DIR, "lib", "libnkhip_kbench.so")
+LIB_PATH = KBENCH_LIB if os.environ.get("NK_KBENCH_LIB") == "1" else PRODUCT_LIB
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "nkhip.h")
 
 NK_OK = 0
@@ -82,6 +86,13 @@ class nk_newton_stats(C.Structure):
                 ("tol", C.c_double), ("solved", C.c_int32), ("n_matvec", C.c_int64), ("n_residual", C.c_int64)]
 
 
+class nk_path_info(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("nranks", C.c_int32), ("device", C.c_int32), ("ranks_on_device", C.c_int32),
+                ("rccl", C.c_int32), ("mailbox", C.c_int32), ("resident_sweep", C.c_int32),
+                ("resident_blocks", C.c_int32), ("halo_in_launch", C.c_int32), ("mailbox_error", C.c_int32),
+                ("halo_cap", C.c_int64), ("pci_bus_id", C.c_char * 32)]
+
+
 class nk_prof_entry(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("timed", C.c_int64), ("total_ms", C.c_double),
                 ("bytes", C.c_double), ("bytes_all", C.c_double), ("dram_bytes_all", C.c_double)]
@@ -139,6 +150,7 @@ SIGNATURES = {
     "nk_dist_mailbox_handle": (C.c_int, [_VP, C.c_char_p]),
     "nk_dist_mailbox_open": (C.c_int, [_VP, _I32, _I32, C.c_char_p]),
     "nk_dist_mailbox_active": (C.c_int, [_VP]),
+    "nk_dist_path": (C.c_int, [_VP, C.POINTER(nk_path_info)]),
     "nk_prof_enable": (C.c_int, [_VP, _I32]),
     "nk_prof_reset": (C.c_int, [_VP]),
     "nk_prof_read": (C.c_int, [_VP, C.POINTER(nk_prof_entry), _I32, C.POINTER(_I32)]),
@@ -149,7 +161,8 @@ TORCH_FIRST = False
 
 
 def load():
-    """Load libnkhip.so (built in-tree by __graft_entry__.build() / `make -C newtonkrylov.jl_amd`)."""
+    """Load libnkhip.so (built in-tree by __graft_entry__.build() / `make -C newtonkrylov.jl_amd`), or the
+    kbench build when NK_KBENCH_LIB=1."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):

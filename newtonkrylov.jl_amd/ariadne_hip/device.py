@@ -70,6 +70,17 @@ class Context:
     def mailbox_active(self) -> bool:
         return bool(load().nk_dist_mailbox_active(self.handle))
 
+    def path_info(self) -> dict:
+        """The distributed path this context runs (nk_dist_path): transport, resident sweep, in-launch
+        ghost planes, ranks sharing the GPU, the device's PCI bus id."""
+        info = _lib.nk_path_info()
+        self.check(load().nk_dist_path(self.handle, C.byref(info)), "nk_dist_path")
+        out = {name: getattr(info, name) for name, _ in _lib.nk_path_info._fields_}
+        out["pci_bus_id"] = info.pci_bus_id.decode(errors="replace")
+        for k in ("rccl", "mailbox", "resident_sweep", "halo_in_launch", "mailbox_error"):
+            out[k] = bool(out[k])
+        return out
+
     def mailbox_handle(self) -> bytes:
         """64-byte IPC handle of this context's peer mailbox (nk_dist_mailbox_handle)."""
         buf = C.create_string_buffer(64)

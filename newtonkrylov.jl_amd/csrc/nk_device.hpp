@@ -92,7 +92,11 @@ __device__ double mb_recv(unsigned epoch, double* sh) {
             uint64_t x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             unsigned spins = 0;
             while ((unsigned)(x >> 32) != epoch) {
-                if (++spins > g_mb.spin_limit) {
+                // bounded: past spin_limit polls raise the error flag; and once ANY wait of this rank
+                // has timed out (a dead peer), every later one gives up within 256 polls -- so a failed
+                // rank costs its peers one timeout per host sync, not one per consuming kernel
+                if (++spins > g_mb.spin_limit ||
+                    ((spins & 255) == 0 && __hip_atomic_load(g_mb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
                     __hip_atomic_store(g_mb.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     x = 0;
                     break;
@@ -239,7 +243,8 @@ __device__ __forceinline__ bool halo_tile_exchange(const double* __restrict__ v,
             const uint64_t* f = halo_tile_flags(g_mb.self, par, side) + tile;
             unsigned spins = 0;
             while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
-                if (++spins > g_mb.spin_limit) {
+                if (++spins > g_mb.spin_limit ||
+                    ((spins & 255) == 0 && __hip_atomic_load(g_mb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
                     __hip_atomic_store(g_mb.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     hx_ok = 0;
                     break;

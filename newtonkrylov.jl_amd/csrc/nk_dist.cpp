@@ -47,7 +47,7 @@ int halo_exchange(nk_ctx* c, const nk_problem* p, const double* v) {
     // Posting order matters when both neighbours are the same rank (a ring of two): sends go up
     // then down, receives come from below then above, so the FIFO matching per peer pairs my
     // lower ghost with the neighbour's last plane and my upper ghost with its first.
-    NK_TRY(launch(c, "halo", 16.0 * pl * ((dn >= 0) + (up >= 0)), [&] {
+    NK_TRY(launch(c, "halo_rccl", 16.0 * pl * ((dn >= 0) + (up >= 0)), [&] {
         chk(ncclGroupStart());
         if (up >= 0) chk(ncclSend(vv + (size_t)(g.nplanes - 1) * pl, pl, ncclFloat64, up, comm, c->stream));
         if (dn >= 0) chk(ncclSend(vv, pl, ncclFloat64, dn, comm, c->stream));
@@ -126,10 +126,11 @@ static int mb_open_peers(nk_ctx* c, int rank, int nranks, const char* handles, c
     NK_TRY(mb_alloc(c));
     mb_disable(c);
     std::vector<uint64_t*> peers((size_t)nranks);
-    // the resident MGS sweep needs every CU of the device to itself: off when a peer may share it
-    // (no bus ids: the mailbox-only transport, made for ranks on one GPU)
-    const bool shared_ok = env_int("NK_RES_SHARED", 0) != 0;  // tests: ranks on one GPU with NK_RES_BLOCKS grids
-    c->res_ok = busids != nullptr || nranks < 2 || shared_ok;
+    // the resident MGS sweep needs every CU of its grid co-resident: with peers on the same device
+    // (no bus ids: the mailbox-only transport, made for ranks on one GPU -- all of them count) it is
+    // off, unless NK_RES_SHARED=1 (test rigs) gives every rank's sweep grid CUs / (ranks on the GPU)
+    const bool shared_ok = env_cfg("NK_RES_SHARED", 0) != 0;
+    int share = busids ? 1 : nranks;
     for (int r = 0; r < nranks; ++r) {
         if (r == rank) {
             peers[r] = c->mb_self;
@@ -144,7 +145,7 @@ static int mb_open_peers(nk_ctx* c, int rank, int nranks, const char* handles, c
                 mb_disable(c);
                 return fail(c, NK_E_HIP, "mailbox: rank " + std::to_string(r) + "'s device is not visible here");
             }
-            if (dev == c->device && !shared_ok) c->res_ok = false;
+            if (dev == c->device) ++share;
             if (dev != c->device) {
                 int can = 0;
                 if (hipDeviceCanAccessPeer(&can, c->device, dev) != hipSuccess || !can) {
@@ -169,6 +170,8 @@ static int mb_open_peers(nk_ctx* c, int rank, int nranks, const char* handles, c
         }
         peers[r] = static_cast<uint64_t*>(p);
     }
+    c->res_share = share;
+    c->res_ok = share < 2 || shared_ok;
     NK_HIP(c, hipMalloc(reinterpret_cast<void**>(&c->mb_peers_dev), sizeof(uint64_t*) * nranks));
     NK_HIP(c, hipMemcpy(c->mb_peers_dev, peers.data(), sizeof(uint64_t*) * nranks, hipMemcpyHostToDevice));
     *c->mb_err = 0;
@@ -325,6 +328,28 @@ int nk_dist_mailbox_open(nk_ctx* c, int32_t rank, int32_t nranks, const char* ha
 }
 
 int nk_dist_mailbox_active(nk_ctx* c) { return (c && c->mb_on) ? 1 : 0; }
+
+int nk_dist_path(nk_ctx* c, nk_path_info* out) {
+    if (!c || !out) return NK_E_ARG;
+    std::memset(out, 0, sizeof(*out));
+    out->rank = c->rank;
+    out->nranks = c->nranks;
+    out->device = c->device;
+    out->ranks_on_device = c->res_share;
+    out->rccl = c->comm ? 1 : 0;
+    out->mailbox = c->mb_on ? 1 : 0;
+    // the resident sweep also needs the mailbox when ranks cross (RCCL reductions need the host between passes)
+    out->resident_sweep = (c->res_ok && (!c->comm || c->mb_on)) ? 1 : 0;
+    out->resident_blocks = c->res_gran ? c->res_blocks : 0;
+    out->halo_in_launch = (halo_fuse_knob() && c->mb_on && c->nranks > 1 && c->halo_cap > 0) ? 1 : 0;
+    out->mailbox_error = (c->mb_err && *(volatile int*)c->mb_err) ? 1 : 0;
+    out->halo_cap = c->halo_cap;
+    if (hipDeviceGetPCIBusId(out->pci_bus_id, (int)sizeof(out->pci_bus_id), c->device) != hipSuccess) {
+        (void)hipGetLastError();
+        out->pci_bus_id[0] = 0;
+    }
+    return NK_OK;
+}
 
 int nk_dist_free(nk_ctx* c) {
     if (c) mb_free(c);

@@ -85,6 +85,7 @@ struct nk_ctx {
     int* res_err_dev = nullptr;
     unsigned res_tag = 0;                  // granule tags handed out so far
     int res_blocks = 0, res_rl = 0;        // grid (= CUs) and LDS double2 slots per thread
+    int res_share = 1;                     // ranks on this GPU (NK_RES_SHARED: each sweep grid gets CUs / res_share)
     uint64_t* res_tstamp = nullptr;        // kernel-variant bench only (nkb_mgs_res, NK_RES_TSTAMP)
     // pipelined ILU(0) sweeps (launch_ilu0_*): per-strip progress counters + a pinned timeout flag
     int64_t* ilu_prog = nullptr;
@@ -99,11 +100,21 @@ struct nk_ctx {
 
 namespace nk {
 
-// integer knob from the environment (unset or empty: dflt)
-inline int env_int(const char* name, int dflt) {
+// Operational configuration from the environment (unset or empty: dflt): the transport of the
+// distributed path, timeouts, shared-GPU test rigs.  None of them changes a kernel's arithmetic;
+// DESIGN.md §5 lists them.
+inline int env_cfg(const char* name, int dflt) {
     const char* s = getenv(name);
     return (s && *s) ? atoi(s) : dflt;
 }
+// Kernel-variant tuning knobs (tile shapes, grid sizes, load flavours, experimental variants): read
+// from the environment only in the kernel-variant bench build (lib/libnkhip_kbench.so, -DNK_KBENCH,
+// driven by tools/); the product library compiles the default in and reads nothing.
+#ifdef NK_KBENCH
+#define NK_TUNE(name, dflt) ::nk::env_cfg(name, dflt)
+#else
+#define NK_TUNE(name, dflt) (dflt)
+#endif
 
 // ---------------------------------------------------------------- errors
 int fail(nk_ctx* c, int code, const std::string& msg);
@@ -172,6 +183,7 @@ double* red_out(nk_ctx* c, int len, Red* r, int* fin);  // slot for a reduction 
 int finish_reduction(nk_ctx* c, Red* r);     // multi-rank: collapse + RCCL all-reduce
 int mb_check(nk_ctx* c);                     // after a host sync: did a mailbox wait time out?
 int red_blocks(int64_t n);                   // grid size of streaming reductions
+int halo_fuse_knob();                        // 1: a Krylov Jv's ghost planes travel in the stencil launch (mailbox up)
 // One Arnoldi step's MGS sweep in one launch (np passes over V[t % k], then ||q||) with q resident
 // on chip; returns 1 (nothing enqueued) when the resident path does not apply.
 // *vout (optional): where to store V_{k+1} = q / ||q|| instead of q; reset to null when the sweep

@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <vector>
 
 #include "nk_stencil.hpp"
 
@@ -520,8 +521,10 @@ int mailbox_bind(nk_ctx* c) {
         m.rank = c->rank;
         m.nranks = c->nranks;
         m.err = c->mb_err_dev;
+        // polls before a mailbox wait gives up with an error (a few s: ranks may drift apart at start-up;
+        // NK_MB_SPIN_LIMIT shortens it for the failure-path tests)
         const char* e = getenv("NK_MB_SPIN_LIMIT");
-        m.spin_limit = (e && *e) ? (unsigned)atoll(e) : (1u << 26);  // a few s of polling: ranks may drift apart at start-up
+        m.spin_limit = (e && *e) ? (unsigned)atoll(e) : (1u << 26);
     }
     NK_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(g_mb), &m, sizeof(m)));
     // and the copy in every stencil instantiation unit
@@ -582,7 +585,8 @@ __global__ __launch_bounds__(kBlock) void k_halo_ipc(double* __restrict__ v, int
             const uint64_t* f = halo_flags(g_mb.self) + (par * 2 + side) * kHaloBlocks + b;
             unsigned spins = 0;
             while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
-                if (++spins > g_mb.spin_limit) {
+                if (++spins > g_mb.spin_limit ||
+                    ((spins & 255) == 0 && __hip_atomic_load(g_mb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
                     __hip_atomic_store(g_mb.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     ready = 0;
                     break;
@@ -623,7 +627,7 @@ int launch_halo_ipc(nk_ctx* c, double* v, int64_t plane, int64_t nplanes, bool r
     if (nb > kHaloBlocks) nb = kHaloBlocks;
     if (nb < 1) nb = 1;
     const int nbrs = ring ? 2 : (c->rank > 0) + (c->rank + 1 < c->nranks);
-    return launch(c, "halo", 16.0 * plane * nbrs, [&] {
+    return launch(c, "halo_ipc", 16.0 * plane * nbrs, [&] {
         hipLaunchKernelGGL(k_halo_ipc, dim3(nb), dim3(kBlock), 0, c->stream, v, plane, nplanes, epoch, c->halo_cap,
                            ring ? 1 : 0);
     });
@@ -651,8 +655,15 @@ int mailbox_selftest(nk_ctx* c, bool* ok) {
     return NK_OK;
 }
 
+// ghost planes of a Krylov Jv inside the stencil launch when the peer mailbox is up (kbench: NK_HALO_FUSE=0
+// forces the separate exchange kernel)
+int halo_fuse_knob() {
+    static const int fuse = NK_TUNE("NK_HALO_FUSE", 1);
+    return fuse;
+}
+
 int red_blocks(int64_t n) {
-    static const int cap = env_int("NK_RED_BLOCKS", kMaxRedBlocks);
+    static const int cap = NK_TUNE("NK_RED_BLOCKS", kMaxRedBlocks);
     int64_t g = (n + 2LL * kBlock * 4 - 1) / (2LL * kBlock * 4);  // >= 4 double2 per thread
     if (g < 1) g = 1;
     if (g > cap) g = cap;
@@ -666,7 +677,7 @@ int red_blocks(int64_t n) {
 // block of the next kernel (dot, sumsq, the MGS chain) keep red_blocks: each consumer block sums
 // all the partials.
 int wide_blocks(int64_t n) {
-    static const int cap = std::max(1, std::min(kRedCap - 2, env_int("NK_WIDE_BLOCKS", kRedCap - 2)));
+    static const int cap = std::max(1, std::min(kRedCap - 2, NK_TUNE("NK_WIDE_BLOCKS", kRedCap - 2)));
     int64_t g = (n + 2LL * kBlock * 2 - 1) / (2LL * kBlock * 2);
     if (g < 1) g = 1;
     if (g > cap) g = cap;
@@ -700,12 +711,13 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     A.vout = in.vout;
     A.ihx2 = 1.0 / A.hx2; A.ihy2 = 1.0 / A.hy2; A.ihz2 = 1.0 / A.hz2; A.ieps = in.eps != 0.0 ? 1.0 / in.eps : 0.0;
     A.alpha = p->alpha;
+    A.eall = (fast & 4096) ? 1 : 0;  // kbench: x-edge loads by every lane
     const bool per = p->bc == NK_BC_PERIODIC;
     int vec = 1, grid = 1;
     if (g.dim == 1) {
         grid = (int)((p->nx + kBlock - 1) / kBlock);
     } else if (g.dim == 2) {
-        static const int vec_pref = env_int("NK_ST_VEC", 2);
+        static const int vec_pref = NK_TUNE("NK_ST_VEC", 2);
         vec = (p->nx % 2 == 0) ? 2 : 1;
         if (((fast & 4) || vec_pref == 4) && p->nx % 4 == 0 && !per) vec = 4;
         A.tiles_x = (int)((p->nx + kBlock * vec - 1) / (kBlock * vec));
@@ -713,10 +725,10 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         // 114.8 us and +0.6 % on the bench, profiles/r02/ab_st_blocks.log; 8192^2 heat: 32 rows are
         // as fast as 64 for the FD Jv and 3 % faster for the residual, kbench_st2d_8192.log), and
         // never more tiles than the reduction slot holds partials
-        static const int target = env_int("NK_ST_BLOCKS", 1024);
+        static const int target = NK_TUNE("NK_ST_BLOCKS", 1024);
         int64_t rows = (p->ny * A.tiles_x + target - 1) / target;
-        static const int min_rows = env_int("NK_ST_MINROWS", 8);
-        static const int max_rows = env_int("NK_ST_MAXROWS", 32);
+        static const int min_rows = NK_TUNE("NK_ST_MINROWS", 8);
+        static const int max_rows = NK_TUNE("NK_ST_MAXROWS", 32);
         if (rows > max_rows) rows = max_rows;
         if (rows < min_rows) rows = min_rows;
         const int64_t cap_rows = (p->ny * A.tiles_x + (kRedCap - 3)) / (kRedCap - 2);
@@ -726,24 +738,29 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         A.rows = (int)rows;
         A.tiles_y = (int)((p->ny + rows - 1) / rows);
         grid = A.tiles_x * A.tiles_y;
-        // raw stencil rows three ahead (fast bit 64 / NK_ST_D3; periodic kinds keep two)
-        static const int d3_env = env_int("NK_ST_D3", 0);
-        A.d3 = ((fast & 64) || d3_env) && !per ? 1 : 0;
+        A.lin = (fast & 2048) ? 1 : 0;  // kbench: tiles in address order
+        // kbench: one-shot LDS tiles (k_st2t) of 8 / 4 / 16 rows x 128 columns (fast bits 8192 / 16384 / 32768)
+        A.tile2 = (fast & 8192) ? 8 : ((fast & 16384) ? 4 : ((fast & 32768) ? 16 : 0));
+        if (A.tile2 && vec == 2) {
+            A.tiles_x = (int)((p->nx + 127) / 128);
+            A.tiles_y = (int)((p->ny + A.tile2 - 1) / A.tile2);
+            grid = A.tiles_x * A.tiles_y;
+        }
     } else {
         vec = (p->nx % 2 == 0) ? 2 : 1;
         // rows per 3D tile and the y-neighbour path (k_st3d loads, k_st3l LDS); fast bits 8 / 16 select
         // k_st3l with 4 / 8 rows (kernel-variant bench), NK_ST3_LDS / NK_ST3_NW likewise
         // k_st3l with 4-row tiles is the default: +6-16 % over k_st3d on every 3D kind / mode at 512^3
         // and at config 5's 512^2 x 64 slab (profiles/r02/kbench_st3l.log)
-        static const int lds_env = env_int("NK_ST3_LDS", 1);
-        static const int nw_env = env_int("NK_ST3_NW", 4);
+        static const int lds_env = NK_TUNE("NK_ST3_LDS", 1);
+        static const int nw_env = NK_TUNE("NK_ST3_NW", 4);
         A.lds3 = (fast & 24) ? 1 : lds_env;
         A.nw = A.lds3 ? ((fast & 8) ? 4 : ((fast & 16) ? 8 : (nw_env == 4 ? 4 : 8))) : 4;
         A.tiles_x = (int)((p->nx + 64 * vec - 1) / (64 * vec));
         A.tiles_y = (int)((p->ny + A.nw - 1) / A.nw);
-        static const int target = env_int("NK_ST3_BLOCKS", 8192);  // shorter z-marches keep y-adjacent tiles in step (L2 reuse of the halo rows)
+        static const int target = NK_TUNE("NK_ST3_BLOCKS", 8192);  // shorter z-marches keep y-adjacent tiles in step (L2 reuse of the halo rows)
         int64_t planes = ((int64_t)p->nz * A.tiles_x * A.tiles_y + target - 1) / target;
-        static const int min_planes = env_int("NK_ST_MINPLANES", 16);  // 16: (16 + 2) / 16 z-halo re-reads
+        static const int min_planes = NK_TUNE("NK_ST_MINPLANES", 16);  // 16: (16 + 2) / 16 z-halo re-reads
         if (planes < min_planes) planes = min_planes;
         if (rows_override > 0) planes = rows_override;
         if (planes > p->nz) planes = p->nz;
@@ -758,7 +775,7 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     // second exp per point (config-4 slab Jv 277 -> 246 us, V_1 step 248 -> 227 us, bench +1.2 %),
     // while the plain Jv + dot (116 -> 122 us) and the restart residual (110 -> 126 us) do not
     // (profiles/r02/ab_f0r_bratu.log); 2 for every Bratu launch too; 0 never
-    static const int f0r_env = env_int("NK_F0R", 1);
+    static const int f0r_env = NK_TUNE("NK_F0R", 1);
     // 3D: the F0R kernel needs 145 VGPRs (3 waves per SIMD instead of 4), which pays only where the
     // field is cheap and the kernel moves the most bytes: G_Euler!'s Jv with a dot partner (512^3
     // FD Jv + V_k store 1400 -> 1198 us), not the V_1 = r0 / beta step, not midpoint / trapezoid
@@ -773,7 +790,7 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         // v's ghost planes: through the peers' inboxes inside this launch (halo_tile_exchange: only the
         // tiles at the slab's ends fetch, the rest of the grid never waits) when the peer mailbox is up,
         // the slab axis is not periodic and every tile of a plane has a flag; else exchanged first
-        static const int fuse_env = env_int("NK_HALO_FUSE", 1);
+        const int fuse_env = halo_fuse_knob();
         const int64_t tiles_pl = g.dim == 2 ? A.tiles_x : (int64_t)A.tiles_x * A.tiles_y;
         const bool fuse = fuse_env && c->mb_on && c->nranks > 1 && !per && in.mode != MODE_RES &&
                           (g.dim == 2 || (g.dim == 3 && A.lds3)) && g.plane <= c->halo_cap && tiles_pl <= kHaloTileFlags;
@@ -876,14 +893,16 @@ template <bool HAS_NEXT>
 void mgs_dispatch(int variant, int g, hipStream_t s, int64_t n, double* q, const double* vi, const double* vn,
                   const double* red, int len, double* h, double* hm, double* part, int rev, int fin) {
     switch (variant) {  // unroll depth x non-temporal V_i loads (tools/kbench.py measures them)
+#ifdef NK_KBENCH
     case 0: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, false>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
     case 1: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
     case 2: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
     case 3: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
     case 4: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
-    case 5: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, false, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
     case 6: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 4, true, false, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
     case 7: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
+#endif
+    case 5: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, false, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
     default: hipLaunchKernelGGL((k_mgs_pass<HAS_NEXT, 2, true, true, true, true>), dim3(g), dim3(kBlock), 0, s, n, q, vi, vn, red, len, h, hm, part, rev, fin); break;
     }
 }
@@ -895,7 +914,7 @@ int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const dou
     // vectors that fit the 256 MB Infinity Cache twice over (q + V_{i+1} re-read by the next pass):
     // cached q / V_{i+1} (variant 5); larger ones stream every operand non-temporally (variant 8:
     // +1.8 % heat 8192^2, +2.3 % heat 512^3; it costs 16 % at 4096^2)
-    static const int forced = env_int("NK_MGS_VARIANT", -1);
+    static const int forced = NK_TUNE("NK_MGS_VARIANT", -1);
     const int variant = forced >= 0 ? forced : (8.0 * (double)n > 256.0 * (1 << 20) ? 8 : kMgsVariant);
     const int g = red_blocks(n);
     int fin;
@@ -922,7 +941,7 @@ int launch_update_x(nk_ctx* c, int64_t n, double* x, double* xr, const double* c
     }
     while (done < k) {
         UpdArgs A{};
-        static const int cap = std::max(1, std::min(kMaxUpdateVecs, env_int("NK_UPD_VECS", kMaxUpdateVecs)));
+        static const int cap = std::max(1, std::min(kMaxUpdateVecs, NK_TUNE("NK_UPD_VECS", kMaxUpdateVecs)));
         const int m = (k - done) < cap ? (k - done) : cap;
         for (int i = 0; i < m; ++i) A.V[i] = V[done + i];
         A.x = x; A.xr = xr; A.y = y_dev + done; A.n = n; A.k = m;
@@ -936,13 +955,18 @@ int launch_update_x(nk_ctx* c, int64_t n, double* x, double* xr, const double* c
         const double bytes = 8.0 * n * (m + (A.first ? 0 : 1) + (A.last ? (restart ? 2 : 1) + (u ? 1 : 0) : 1));
         // 4 elements per thread and iteration: +10-25 % over 1 for every chain length k = 1..30 at
         // 4096^2 and 8192^2 (profiles/r02/kbench_upd.log); NK_UPD_U = 1 / 2 / 8 for A/B
-        static const int uenv = env_int("NK_UPD_U", 0);
+#ifdef NK_KBENCH
+        static const int uenv = NK_TUNE("NK_UPD_U", 0);
         const int U = uenv > 0 ? uenv : 4;
+#endif
         NK_TRY(launch(c, "update_x", bytes, [&] {
+#ifdef NK_KBENCH
             if (U >= 8) hipLaunchKernelGGL(k_update_x<8>, dim3(g), dim3(kBlock), 0, c->stream, A);
-            else if (U >= 4) hipLaunchKernelGGL(k_update_x<4>, dim3(g), dim3(kBlock), 0, c->stream, A);
             else if (U == 2) hipLaunchKernelGGL(k_update_x<2>, dim3(g), dim3(kBlock), 0, c->stream, A);
-            else hipLaunchKernelGGL(k_update_x<1>, dim3(g), dim3(kBlock), 0, c->stream, A);
+            else if (U == 1) hipLaunchKernelGGL(k_update_x<1>, dim3(g), dim3(kBlock), 0, c->stream, A);
+            else
+#endif
+                hipLaunchKernelGGL(k_update_x<4>, dim3(g), dim3(kBlock), 0, c->stream, A);
         }));
         done += m;
     }
@@ -1258,8 +1282,8 @@ IluArgs ilu_args(const nk_problem* p, int dim) {
 // the pipelined sweeps: rows of at least 64 columns... any 2D / 1D grid; 3D with ny >= 64 (the plane
 // below a strip's rows must lie in an earlier strip); NK_ILU_PIPE=0 forces the level sweeps
 static bool ilu_pipe_applies(nk_ctx* c, const nk_problem* p) {
-    static const int env = env_int("NK_ILU_PIPE", 1);
-    return env && c->ilu_pipe_ok && (p->nz == 1 || p->ny >= 64);
+    static const int pipe = NK_TUNE("NK_ILU_PIPE", 1);
+    return pipe && c->ilu_pipe_ok && (p->nz == 1 || p->ny >= 64);
 }
 
 static int ilu_pipe_setup(nk_ctx* c, const nk_problem* p, int dim, IluPipe* P, int* grid) {
@@ -1335,8 +1359,10 @@ int launch_cg_direction(nk_ctx* c, int64_t n, double beta, double* p, const doub
 
 // ------------------------------------------------------------------------------ variant bench hook
 // Times kernel variants in ONE process (interleaved A/B, MI355X_MICROARCH methodology rule 24).
-// Not part of the public ABI (exported as nkb_*; used by tools/kbench.py only).
+// Not part of the public ABI: exported as nkb_* by the kbench build only (tools/kbench*.py).
 }  // namespace nk
+
+#ifdef NK_KBENCH  // the nkb_* hooks: lib/libnkhip_kbench.so only (tools/, bench.py calibration)
 
 // One Arnoldi step's MGS sweep at basis size k, as GMRES runs it: passes i = 1..k read q, V_i,
 // V_{i+1} (the last one q, V_k) over a real basis of k+1 distinct vectors.  alt = alternate the
@@ -1475,14 +1501,22 @@ extern "C" int nkb_stencil_kind(nk_ctx* c, int kind, int64_t nx, int64_t ny, int
     if (!c || nx < 3 || ny < 3 || nz < 1 || reps < 1 || !us_out || kind < NK_BRATU2D || kind > NK_HEAT3D_TRAPEZOID)
         return NK_E_ARG;
     const double h = 1.0 / (nx + 1);
-    nk_problem p{kind, NK_BC_ZERO, nx, ny, nz, h, h, h, 3.51382, 0.01, 1e-6, nullptr, nullptr, 0.5};
-    double *u = nullptr, *v = nullptr, *F0 = nullptr, *aux = nullptr, *out = nullptr, *un = nullptr;
+    // hook-only bits: 128 bc_periodic!, 256 the fused normalisation (v / h stored as V_k: the Arnoldi Jv)
+    const bool per = (fast & 128) != 0, vfuse = (fast & 256) != 0;
+    fast &= ~(128 | 256);
+    nk_problem p{kind, per ? NK_BC_PERIODIC : NK_BC_ZERO, nx, ny, nz, h, h, h, 3.51382, 0.01, 1e-6, nullptr, nullptr, 0.5};
+    double *u = nullptr, *v = nullptr, *F0 = nullptr, *aux = nullptr, *out = nullptr, *un = nullptr, *vk = nullptr;
     p.un = reinterpret_cast<const double*>(1);  // geometry only while allocating
-    for (double** q : {&u, &v, &F0, &aux, &out, &un}) NK_TRY(nk_vec_alloc(c, &p, q));
+    for (double** q : {&u, &v, &F0, &aux, &out, &un, &vk}) NK_TRY(nk_vec_alloc(c, &p, q));
     for (double* q : {u, v, F0, aux, un}) NK_TRY(launch_fill(c, nx * ny * nz, q, 0.25));
     p.un = un;
     StencilIn in{&p, mode, epi, out, u, v, F0, aux, 1e-6};
     in.f0r = (fast & 32) != 0;  // variant bit 32: F0 recomputed (the F0R kernels, where the policy allows)
+    if (vfuse && mode != MODE_RES && epi == EPI_DOT) {
+        NK_TRY(launch_fill(c, 1, c->scal + 32, 2.0));
+        in.vdiv = c->scal + 32;
+        in.vout = vk;
+    }
     Red r{};
     hipEvent_t a, b;
     NK_HIP(c, hipEventCreate(&a));
@@ -1497,7 +1531,89 @@ extern "C" int nkb_stencil_kind(nk_ctx* c, int kind, int64_t nx, int64_t ny, int
     *us_out = 1e3 * ms / reps;
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
-    for (double* q : {u, v, F0, aux, out, un}) nk_vec_free(c, q);
+    for (double* q : {u, v, F0, aux, out, un, vk}) nk_vec_free(c, q);
+    return NK_OK;
+}
+
+// Two stencil variants (fast bits fa / fb, incl. the hook-only bits 128 periodic / 256 fused
+// normalisation) on the same pseudo-random operands: diff[0] = max |out_a - out_b|, diff[1] = the same
+// for the stored V_k, diff[2] / diff[3] = the two reductions' sums (epi != none), diff[4] = max |out_a|
+namespace nk {
+namespace {
+__global__ __launch_bounds__(kBlock) void k_hashfill2(int64_t n, double* __restrict__ x, uint64_t seed, double lo, double hi) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        uint64_t z = (uint64_t)i * 0x9e3779b97f4a7c15ull + seed;
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        z ^= z >> 31;
+        x[i] = lo + (hi - lo) * ((double)(z >> 11) * 0x1.0p-53);
+    }
+}
+}  // namespace
+}  // namespace nk
+
+extern "C" int nkb_stencil_cmp(nk_ctx* c, int kind, int64_t nx, int64_t ny, int64_t nz, int mode, int epi, int fa, int fb,
+                               double* diff) {
+    using namespace nk;
+    if (!c || nx < 3 || ny < 3 || nz < 1 || !diff || kind < NK_BRATU2D || kind > NK_HEAT3D_TRAPEZOID) return NK_E_ARG;
+    const double h = 1.0 / (nx + 1);
+    const bool per = (fa & 128) != 0, vfuse = (fa & 256) != 0;
+    nk_problem p{kind, per ? NK_BC_PERIODIC : NK_BC_ZERO, nx, ny, nz, h, h, h, 3.51382, 0.01, 1e-6, nullptr, nullptr, 0.3};
+    double *u = nullptr, *v = nullptr, *F0 = nullptr, *aux = nullptr, *un = nullptr, *oa = nullptr, *ob = nullptr,
+           *va = nullptr, *vb = nullptr;
+    p.un = reinterpret_cast<const double*>(1);
+    for (double** q : {&u, &v, &F0, &aux, &un, &oa, &ob, &va, &vb}) NK_TRY(nk_vec_alloc(c, &p, q));
+    const int64_t n = nx * ny * nz;
+    uint64_t seed = 17;
+    for (double* q : {u, v, F0, aux, un}) {
+        hipLaunchKernelGGL(k_hashfill2, dim3(2048), dim3(kBlock), 0, c->stream, n, q, seed, -1.0, 1.0);
+        seed += 7919;
+    }
+    p.un = un;
+    NK_TRY(launch_fill(c, 1, c->scal + 32, 1.7));
+    // F0 as the residual kernel computes it (the F0R kernels rely on it)
+    {
+        StencilIn r{&p, MODE_RES, EPI_NONE, F0, u, nullptr, nullptr, nullptr, 0.0};
+        Red rr{};
+        NK_TRY(launch_stencil_ex(c, r, &rr, 0, 0));
+    }
+    double sums[2] = {0.0, 0.0};
+    for (int which = 0; which < 2; ++which) {
+        int f = which ? fb : fa;
+        f &= ~(128 | 256);
+        StencilIn in{&p, mode, epi, which ? ob : oa, u, v, F0, aux, 1e-6};
+        in.f0r = (f & 32) != 0;
+        if (vfuse && mode != MODE_RES && epi == EPI_DOT) {
+            in.vdiv = c->scal + 32;
+            in.vout = which ? vb : va;
+        }
+        Red r{};
+        NK_TRY(launch_stencil_ex(c, in, &r, 0, f));
+        if (epi != EPI_NONE) {
+            NK_TRY(launch_finalize(c, r, c->scal + 40 + which, 0, nullptr));
+        }
+    }
+    NK_HIP(c, hipStreamSynchronize(c->stream));
+    if (epi != EPI_NONE) NK_HIP(c, hipMemcpy(sums, c->scal + 40, 2 * sizeof(double), hipMemcpyDeviceToHost));
+    std::vector<double> a(n), b(n);
+    double d0 = 0.0, d1 = 0.0, m = 0.0;
+    NK_HIP(c, hipMemcpy(a.data(), oa, sizeof(double) * n, hipMemcpyDeviceToHost));
+    NK_HIP(c, hipMemcpy(b.data(), ob, sizeof(double) * n, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n; ++i) {
+        d0 = std::max(d0, std::fabs(a[i] - b[i]));
+        m = std::max(m, std::fabs(a[i]));
+    }
+    if (vfuse) {
+        NK_HIP(c, hipMemcpy(a.data(), va, sizeof(double) * n, hipMemcpyDeviceToHost));
+        NK_HIP(c, hipMemcpy(b.data(), vb, sizeof(double) * n, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < n; ++i) d1 = std::max(d1, std::fabs(a[i] - b[i]));
+    }
+    diff[0] = d0;
+    diff[1] = d1;
+    diff[2] = sums[0];
+    diff[3] = sums[1];
+    diff[4] = m;
+    for (double* q : {u, v, F0, aux, un, oa, ob, va, vb}) nk_vec_free(c, q);
     return NK_OK;
 }
 
@@ -1708,3 +1824,4 @@ extern "C" int nkb_stream(nk_ctx* c, int64_t n, int variant, int grid, int reps,
     (void)hipFree(w);
     return NK_OK;
 }
+#endif  // NK_KBENCH

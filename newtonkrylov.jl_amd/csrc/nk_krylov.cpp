@@ -116,23 +116,13 @@ int ws_zbasis(nk_workspace* ws, int need) {
 
 inline double sgn(double x) { return (double)((x > 0) - (x < 0)); }
 
-// NK_MGS_ALT=1: alternate the sweep direction of consecutive MGS passes (see k_mgs_pass)
-const int mgs_alt = [] {
-    const char* e = getenv("NK_MGS_ALT");
-    return (e && *e) ? atoi(e) : 0;
-}();
-
-// NK_MGS_RESIDENT=0: one k_mgs_pass launch per MGS pass instead of the resident sweep
-const int mgs_resident = [] {
-    const char* e = getenv("NK_MGS_RESIDENT");
-    return (e && *e) ? atoi(e) : 1;
-}();
-
-// NK_RES_JV=1: the 2D Bratu FD Jv inside the resident sweep's launch (off: slower)
-const int mgs_fused_jv = [] {
-    const char* e = getenv("NK_RES_JV");
-    return (e && *e) ? atoi(e) : 0;
-}();
+// kbench knobs: NK_MGS_ALT=1 alternates the sweep direction of consecutive MGS passes (see
+// k_mgs_pass); NK_MGS_RESIDENT=0 runs one k_mgs_pass launch per MGS pass instead of the resident
+// sweep; NK_RES_JV=1 computes the 2D Bratu FD Jv inside the resident sweep's launch (slower,
+// DESIGN.md §4)
+const int mgs_alt = NK_TUNE("NK_MGS_ALT", 0);
+const int mgs_resident = NK_TUNE("NK_MGS_RESIDENT", 1);
+const int mgs_fused_jv = NK_TUNE("NK_RES_JV", 0);
 
 // Krylov.jl sym_givens (real case)
 void sym_givens(double a, double b, double* c, double* s, double* rho) {

@@ -39,7 +39,7 @@ struct ResArgs {
     const double* red_in;  // partials of h of the first pass (the Jv's <V_1, q>)
     uint64_t* gran;        // 2 parities x G blocks x 2 granules
     int* err;              // pinned host flag: a poll timed out
-    int noxchg;            // kernel-variant bench only (NK_RES_NOXCHG=1): skip the exchange, h stays fixed
+    int noxchg;            // kbench build only (NK_RES_NOXCHG=1, timing probe): skip the exchange -- WRONG results
     int ntc;               // NTS: the first ntc streamed slots of a block load V_{i+1} cached (Infinity Cache room)
     int poll1;             // 1: one polling wave (NK_RES_POLL1, default 1), 2: four staggered polling waves, 0: every thread polls one partial
     int strided;           // slots interleaved across blocks (every block exactly full: no streamed remainder)
@@ -454,10 +454,14 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
         const double acc = res_pass<RV, B, PRE, NTM, NTS, LB>(A, S, lq, t, -h, lo, hi, P, base, ss, ALT && (t & 1));
         if (t + 1 < A.np) res_prefetch<RV, B, PRE, NTM>(A, P, t + 1, base, ss, ALT && ((t + 1) & 1));
         const double part = block_sum<kResThreads>(acc, sh);
+#ifdef NK_KBENCH
         if (A.tstamp && tid == 0) A.tstamp[((size_t)t * G + blockIdx.x) * 2] = wall_clock64();
         if (!A.noxchg) h = res_exchange(A, part, t + xo, sh, budget, &xdone);
         else __syncthreads();
         if (A.tstamp && tid == 0) A.tstamp[((size_t)t * G + blockIdx.x) * 2 + 1] = wall_clock64();
+#else
+        h = res_exchange(A, part, t + xo, sh, budget, &xdone);
+#endif
     }
     if (blockIdx.x == 0 && tid == 0) {
         const double r = sqrt(h);
@@ -498,11 +502,15 @@ hipError_t resident_bind_mb(const MbInfo& m) { return hipMemcpyToSymbol(HIP_SYMB
 int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, int k, int np, Red in, double* col,
                      double* colh, int rv, double** vout, const ResJv* jin) {
     if (np < 1 || np > kResMax || (n & 1) || !c->res_ok) return 1;
-    // fused Jv phase: off by default -- at one wave per SIMD its ~190 fp64 VALU instructions per point
-    // pair (IEEE divisions, two exp) do not hide behind the loads: 791 us per Arnoldi step vs
+#ifdef NK_KBENCH
+    // fused Jv phase (kbench build only): at one wave per SIMD its ~190 fp64 VALU instructions per
+    // point pair (IEEE divisions, two exp) do not hide behind the loads: 791 us per Arnoldi step vs
     // 619 + 124 us for the sweep and a separate Jv kernel (-1.7 % end to end, 4096^2)
-    static const int jv_env = env_int("NK_RES_JV", 0);
+    static const int jv_env = NK_TUNE("NK_RES_JV", 0);
     if (jin && (!jv_env || !vout || !*vout || jin->nx % 2 != 0)) return 1;
+#else
+    if (jin) return 1;
+#endif
     if (c->comm && !c->mb_on) return 1;  // RCCL reductions need the host between passes
     if (!c->res_gran) {  // one-time set-up; anything missing turns the resident path off for good
         int dev = 0, cus = 0, lds = 0;
@@ -511,24 +519,26 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
                   hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess &&
                   cus >= 1 && cus <= kResThreads;
         if (ok) {
-            // NK_RES_BLOCKS (tests only): a smaller grid, so that ranks sharing one GPU
-            // (NK_RES_SHARED=1) can each hold their sweep's blocks resident at once
-            const int rb = env_int("NK_RES_BLOCKS", 0);
-            c->res_blocks = (rb > 0 && rb < cus) ? rb : cus;
+            // ranks sharing this GPU (NK_RES_SHARED test rigs): each sweep grid gets its share of the CUs,
+            // so that all the ranks' grids are resident at once
+            c->res_blocks = std::max(1, cus / std::max(1, c->res_share));
             const int avail = lds - (int)(sizeof(double) * kShN) - 256;
             c->res_rl = std::max(0, avail / (int)(kResThreads * sizeof(dx2)));
             const size_t lmax = (size_t)c->res_rl * kResThreads * sizeof(dx2);
             ok = res_attr<0>(lmax) && res_attr<16>(lmax) && res_attr<25>(lmax) && res_attr<32>(lmax) && res_attr<48>(lmax) &&
-                 res_attr<64>(lmax) && res_attr<89>(lmax) && res_attr<89, 4, true>(lmax) && res_attr<89, 4>(lmax) &&
-                 res_attr<89, 6, false, true>(lmax) && res_attr<0, 8, false, true>(lmax) &&
-                 res_attr<89, 6, false, false, true>(lmax) && res_attr<89, 6, false, false, false, 1>(lmax) &&
-                 res_attr<89, 6, false, false, false, 2>(lmax) && res_attr<89, 6, false, false, false, 0, true>(lmax) &&
-                 res_attr<89, 4, true, false, false, 0, true>(lmax) && res_attr<89, 2, true>(lmax) &&
-                 res_attr<89, 4, true, false, false, 0, false, 8>(lmax) && res_attr<89, 4, true, false, false, 0, false, 6>(lmax) &&
-                 res_attr<89, 4, true, false, true>(lmax);
+                 res_attr<64>(lmax) && res_attr<89, 4, true>(lmax) && res_attr<89, 4, true, false, false, 0, true>(lmax);
+#ifdef NK_KBENCH
+            ok = ok && res_attr<89>(lmax) && res_attr<89, 4>(lmax) && res_attr<89, 6, false, true>(lmax) &&
+                 res_attr<0, 8, false, true>(lmax) && res_attr<89, 6, false, false, true>(lmax) &&
+                 res_attr<89, 6, false, false, false, 1>(lmax) && res_attr<89, 6, false, false, false, 2>(lmax) &&
+                 res_attr<89, 6, false, false, false, 0, true>(lmax) && res_attr<89, 2, true>(lmax) &&
+                 res_attr<89, 4, true, false, false, 0, false, 8>(lmax) &&
+                 res_attr<89, 4, true, false, false, 0, false, 6>(lmax) && res_attr<89, 4, true, false, true>(lmax);
+#endif
             int per_cu = 0;  // residency: at least one block of the largest variant per CU
-            ok = ok && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_mgs_res<89>),
-                                                                    kResThreads, lmax) == hipSuccess && per_cu >= 1;
+            ok = ok && hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                           &per_cu, reinterpret_cast<const void*>(&k_mgs_res<89, 4, true>), kResThreads, lmax) == hipSuccess &&
+                 per_cu >= 1;
         }
         ok = ok && hipMalloc(&c->res_gran, sizeof(uint64_t) * 4 * kResThreads) == hipSuccess;
         ok = ok && hipMemsetAsync(c->res_gran, 0, sizeof(uint64_t) * 4 * kResThreads, c->stream) == hipSuccess;
@@ -553,15 +563,15 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
     A.err = c->res_err_dev;
     A.n2 = n >> 1;
     A.np = np;
-    // NK_RES_NTS (default on): with a streamed remainder its q and V_{i+1} go non-temporal, so the
-    // Infinity Cache keeps the resident part's V_{i+1} for the next pass (kbench_res: -2..3 % per pass at
-    // half residency, -2..7 % at a quarter; config-4 slab bench +2.4 %, heat 8192^2 +3.9 %); NK_RES_PRE
-    // (default on): batches of 4 with the first one loaded across the hand-off (-1.5 % per pass at
-    // k = 30, full residency; 4096^2 bench +0.6 %).  Same per-element arithmetic and accumulation order
-    // in every variant: bit-identical results.
-    static const int nts_env = env_int("NK_RES_NTS", 1);
-    static const int pre_env = env_int("NK_RES_PRE", 1);
-    int xv = -1;  // experimental variant (kernel-variant bench)
+    // load policy (kbench: NK_RES_NTS / NK_RES_PRE): with a streamed remainder its q and V_{i+1} go
+    // non-temporal, so the Infinity Cache keeps the resident part's V_{i+1} for the next pass (kbench_res:
+    // -2..3 % per pass at half residency, -2..7 % at a quarter; config-4 slab bench +2.4 %, heat 8192^2
+    // +3.9 %); batches of 4 with the first one loaded across the hand-off (-1.5 % per pass at k = 30,
+    // full residency; 4096^2 bench +0.6 %).  Same per-element arithmetic and accumulation order in every
+    // variant: bit-identical results.
+    static const int nts_env = NK_TUNE("NK_RES_NTS", 1);
+    static const int pre_env = NK_TUNE("NK_RES_PRE", 1);
+    int xv = -1;  // experimental variant (kbench build)
     bool streamed = false;  // part of q streams through memory (partial residency)
     {  // every block's chunk must hold its rv + rl resident slots in full (the kernel does not predicate them)
         const int64_t G = c->res_blocks, n2 = n >> 1;
@@ -569,14 +579,16 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         const int64_t whole = ns / G - (n2 % kResThreads != 0 ? 1 : 0);  // the last block's last slot may be partial
         if (whole < 1) return 1;
         const int slots = (int)std::min<int64_t>(whole, 1 << 20);
-        static const int rl_env = env_int("NK_RES_RL", -1);
-        static const int rv_env = env_int("NK_RES_RV", -1);
+        static const int rl_env = NK_TUNE("NK_RES_RL", -1);
+        static const int rv_env = NK_TUNE("NK_RES_RV", -1);
         int rl = std::min(slots, rl_env >= 0 ? std::min(rl_env, c->res_rl) : c->res_rl);  // LDS first
         const bool explicit_rv = rv >= 0 || rv_env >= 0;  // a caller's choice skips the benefit test below
+#ifdef NK_KBENCH
         if (rv >= 1000) {  // kernel-variant bench: 1000 + {0: 89 slots, batches of 4 + prefetch across the hand-off; 1: same, no prefetch; 2: alternating slot order; 3: V_i cached; 4: V_{i+1} non-temporal; 5: streamed remainder non-temporal (NTS); 6: 0 + 5; 8: batches of 2 + prefetch (batches of 6 + prefetch spill); 9 / 10: 0 with LDS slots in batches of 8 / 6; 11: 0 with alternate passes starting on the top LDS group (prefetched across the hand-off)}
             xv = rv - 1000;
             rv = 89;
         }
+#endif
         if (rv < 0) rv = rv_env >= 0 ? rv_env : slots - rl;  // registers hold what the LDS cannot
         // the instantiated register-slot counts (25 + 39 LDS slots = 64: a 4096 x 2048 slab, 4096^2 on two GPUs)
         static const int kRv[] = {89, 64, 48, 32, 25, 16, 0};
@@ -593,8 +605,8 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         // worth it from two passes on (a one-pass sweep only adds q's load + store) while a tenth of q
         // or more is resident (tools/kbench_res.py per pass vs the chain: 4096^2 1.28x at k = 2,
         // 1.8x from k = 16; 2 x 4096^2 (half resident) 1.40-1.52x; 8192^2 (a quarter) 1.16-1.18x;
-        // 512^3 (an eighth) 1.06-1.09x -- with the streamed remainder non-temporal, NK_RES_NTS; 1.01x
-        // at 512^3 without it, hence a fifth then)
+        // 512^3 (an eighth) 1.06-1.09x -- with the streamed remainder non-temporal; 1.01x at 512^3
+        // without it, hence a fifth then)
         const int64_t chunk = std::max<int64_t>(1, ns / G);
         const double f = (double)(rv + A.rl) / (double)chunk;  // resident fraction of q
         if (!explicit_rv && (np < 2 || f < (nts_env ? 0.1 : 0.2))) return 1;
@@ -602,13 +614,15 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         // partial last slot is streamed)
         const bool full = n2 % kResThreads == 0 && (ns + G - 1) / G <= rv + A.rl;
         streamed = !full;
-        static const int vout_env = env_int("NK_RES_VOUT", 1);
+        static const int vout_env = NK_TUNE("NK_RES_VOUT", 1);
         if (vout && *vout && !(full && vout_env)) *vout = nullptr;
         A.vout = vout ? *vout : nullptr;
         if (jin && (!A.vout || (rv != 0 && rv != 89) || (rv > 0 && A.rl < 16))) return 1;  // fused Jv: full residency, instantiated rv, LDS staging
-        static const int strided_env = env_int("NK_RES_STRIDED", 0);
+        // slots interleaved across the blocks (kbench): a different partition of the partial sums
+        static const int strided_env = NK_TUNE("NK_RES_STRIDED", 0);
         A.strided = strided_env && n2 % kResThreads == 0 && ns % G == 0 && ns / G == rv + A.rl;
     }
+#ifdef NK_KBENCH
     if (jin) {
         A.jv_on = 1;
         A.ju = jin->u;
@@ -621,6 +635,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         A.jhy2 = jin->hy2;
         A.jnx = jin->nx;
     }
+#endif
     const unsigned nx_ = (unsigned)np + (jin ? 1u : 0u);  // hand-offs in this launch
     if (c->res_tag > 0xfffffff0u - (unsigned)(kResMax + 1)) {  // tag wrap: restart from clean granules
         NK_HIP(c, hipMemsetAsync(c->res_gran, 0, sizeof(uint64_t) * 4 * kResThreads, c->stream));
@@ -634,27 +649,26 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         A.mb0 = c->mb_epoch + 1;
         c->mb_epoch += nx_;
     }
-    static const int noxchg = env_int("NK_RES_NOXCHG", 0);
-    A.noxchg = noxchg;
+#ifdef NK_KBENCH
+    A.noxchg = NK_TUNE("NK_RES_NOXCHG", 0);  // timing probe only: the h exchange skipped (wrong results)
+#endif
     // NTS: the Infinity Cache (256 MB) keeps the resident part's V_{i+1} (4 KB per block and slot) for
-    // its re-read as the next pass's V_i; the room left (NK_RES_MALL_MB, default 244 MB of it) goes to
-    // the first streamed slots of every block, whose V_{i+1} then loads cached (NK_RES_NTC overrides
-    // the count): half resident 129.3 -> 120.2 us per pass, a quarter 313.1 -> 300.1
-    // (profiles/r02/ab_ntc.log; 128 slots, past the room, thrash)
-    static const int ntc_env = env_int("NK_RES_NTC", -1);
-    static const int mall_mb = env_int("NK_RES_MALL_MB", 244);
+    // its re-read as the next pass's V_i; the room left (244 MB of it) goes to the first streamed slots
+    // of every block, whose V_{i+1} then loads cached: half resident 129.3 -> 120.2 us per pass, a
+    // quarter 313.1 -> 300.1 (profiles/r02/ab_ntc.log; 128 slots, past the room, thrash)
+    static const int ntc_env = NK_TUNE("NK_RES_NTC", -1);
+    static const int mall_mb = NK_TUNE("NK_RES_MALL_MB", 244);
     {
         const double slot = 4096.0 * c->res_blocks;  // one slot of V across the grid, bytes
         const double room = 1e6 * mall_mb - slot * (rv + A.rl);
         A.ntc = ntc_env >= 0 ? ntc_env : (room > 0 ? (int)(room / slot) : 0);
     }
-    static const int poll1 = env_int("NK_RES_POLL1", 1);
-    A.poll1 = poll1;
+    A.poll1 = NK_TUNE("NK_RES_POLL1", 1);
     A.tstamp = c->res_tstamp;
     // cross-rank hand-off: the first `senders` blocks (one per XCD at 8) all send the rank's sum -- the
     // same bits into the same cells -- so the peers see it as soon as the EARLIEST of them has it,
     // not when block 0 happens to finish its local poll
-    static const int senders = env_int("NK_MB_SENDERS", 8);
+    static const int senders = NK_TUNE("NK_MB_SENDERS", 8);
     A.senders = std::max(1, std::min(senders, c->res_blocks));
     A.spin = 1u << 22;  // polls per thread per launch (~1 s): a grid that is not co-resident fails fast
     const size_t lds = (size_t)A.rl * kResThreads * sizeof(dx2);
@@ -672,14 +686,18 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         const dim3 g(c->res_blocks), b(kResThreads);
         switch (rv) {
         case 0:
+#ifdef NK_KBENCH
             if (jin) hipLaunchKernelGGL((k_mgs_res<0, 8, false, true>), g, b, lds, c->stream, A);
-            else hipLaunchKernelGGL(k_mgs_res<0>, g, b, lds, c->stream, A);
+            else
+#endif
+                hipLaunchKernelGGL(k_mgs_res<0>, g, b, lds, c->stream, A);
             break;
         case 16: hipLaunchKernelGGL(k_mgs_res<16>, g, b, lds, c->stream, A); break;
         case 25: hipLaunchKernelGGL(k_mgs_res<25>, g, b, lds, c->stream, A); break;
         case 48: hipLaunchKernelGGL(k_mgs_res<48>, g, b, lds, c->stream, A); break;
         case 64: hipLaunchKernelGGL(k_mgs_res<64>, g, b, lds, c->stream, A); break;
         case 89:
+#ifdef NK_KBENCH
             if (jin) hipLaunchKernelGGL((k_mgs_res<89, 6, false, true>), g, b, lds, c->stream, A);
             else if (xv == 0) hipLaunchKernelGGL((k_mgs_res<89, 4, true>), g, b, lds, c->stream, A);
             else if (xv == 1) hipLaunchKernelGGL((k_mgs_res<89, 4>), g, b, lds, c->stream, A);
@@ -697,6 +715,12 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
             else if (streamed && nts_env) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, false, 0, true>), g, b, lds, c->stream, A);
             else if (pre_env) hipLaunchKernelGGL((k_mgs_res<89, 4, true>), g, b, lds, c->stream, A);
             else hipLaunchKernelGGL(k_mgs_res<89>, g, b, lds, c->stream, A);
+#else
+            (void)xv;
+            (void)pre_env;
+            if (streamed) hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, false, 0, true>), g, b, lds, c->stream, A);
+            else hipLaunchKernelGGL((k_mgs_res<89, 4, true>), g, b, lds, c->stream, A);
+#endif
             break;
         default: hipLaunchKernelGGL(k_mgs_res<32>, g, b, lds, c->stream, A); break;
         }
@@ -705,6 +729,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
 
 }  // namespace nk
 
+#ifdef NK_KBENCH  // kernel-variant bench hooks: lib/libnkhip_kbench.so only
 namespace nk {
 namespace {
 __global__ __launch_bounds__(kBlock) void k_hashfill(int64_t n, double* __restrict__ x, uint64_t seed) {
@@ -802,4 +827,4 @@ extern "C" int nkb_mgs_res(nk_ctx* c, int64_t n, int k, int rv, int reps, double
     for (auto p : V) (void)hipFree(p);
     return NK_OK;
 }
-
+#endif  // NK_KBENCH

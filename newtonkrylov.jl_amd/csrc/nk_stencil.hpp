@@ -3,6 +3,8 @@
 // translation unit (nk_stencil_inst.hip, compiled once per NK_ST_KIND) so the build parallelises;
 // nk_kernels.hip reaches them through stencil_kind_launch().
 #pragma once
+#include <type_traits>
+
 #include "nk_device.hpp"
 
 namespace nk {
@@ -18,7 +20,7 @@ struct KArgs {
     int64_t nx, ny, nz;
     double hx2, hy2, hz2, lam, a, dt, eps;
     int tiles_x, tiles_y, rows;
-    int fast;            // 1: multiply by reciprocals instead of dividing (measurement variant, not bit-faithful)
+    int fast;            // kbench build only: bit 1 multiplies by reciprocals instead of dividing (not bit-faithful)
     double ihx2, ihy2, ihz2, ieps;
     // fused Arnoldi normalisation: the stencil input is v = src / *vdiv (kdivcopy!, bit-identical),
     // and the block's own points of v are stored to vout (V_k) -- saves the separate divcopy pass
@@ -29,8 +31,10 @@ struct KArgs {
     double alpha;        // G_Midpoint! α
     int nw;              // 3D: rows (waves) per tile
     int lds3;            // 3D: y-neighbour rows through LDS (k_st3l) instead of per-wave loads (k_st3d)
+    int lin;             // tiles in dispatch (= address) order instead of XCD-contiguous bands
+    int eall;            // kbench: every lane issues the x-edge loads (round 2's form) instead of the edge lanes only
+    int tile2;           // kbench: 2D one-shot LDS tiles of tile2 rows (k_st2t) instead of the march
     int f0r;             // 2D FD: F0 = F(u) recomputed from the u rows already loaded (k_st2d<..., F0R>)
-    int d3;              // 2D, VEC 2, not periodic: raw stencil rows three ahead in flight (k_st2d<..., D3>)
     // ghost planes of v through the peers' inboxes inside this launch (halo_tile_exchange): the rank
     // has a lower / upper neighbour whose boundary patch this launch fetches itself
     int hx_lo, hx_hi;
@@ -71,10 +75,21 @@ __device__ __forceinline__ double vin(const KArgs& A, int64_t o) {
     return A.vdiv ? v / A.hd : v;
 }
 
-// ((p - 2c) + m) / h^2 exactly as the reference writes it; `fast` multiplies by 1/h^2 instead
+// ((p - 2c) + m) / h^2 exactly as the reference writes it; the kbench build's `fast` variant multiplies
+// by 1/h^2 instead (not bit-faithful; < 2 % faster)
 __device__ __forceinline__ double lapk(const KArgs& A, double c, double p, double m, double h2, double ih2) {
     const double s = (p - 2.0 * c) + m;
-    return (A.fast & 1) ? s * ih2 : s / h2;
+#ifdef NK_KBENCH
+    if (A.fast & 1) return s * ih2;
+#endif
+    return s / h2;
+}
+// (r - F0) / eps, the FD quotient (kbench `fast`: times 1/eps)
+__device__ __forceinline__ double fdq(const KArgs& A, double r, double f0c) {
+#ifdef NK_KBENCH
+    if (A.fast & 1) return (r - f0c) * A.ieps;
+#endif
+    return (r - f0c) / A.eps;
 }
 
 template <int MODE>
@@ -136,13 +151,13 @@ __device__ __forceinline__ double point_value(const KArgs& A, double c, double l
     if constexpr (KIND == NK_BRATU1D || KIND == NK_BRATU2D) {
         if (MODE == MODE_JEXACT) return lsum + A.lam * (exp(uc) * c);  // Enzyme tangent of λ exp(u)
         const double r = lsum + A.lam * exp(c);
-        return MODE == MODE_JFD ? ((A.fast & 1) ? (r - f0c) * A.ieps : (r - f0c) / A.eps) : r;
+        return MODE == MODE_JFD ? fdq(A, r, f0c) : r;
     } else {  // implicit.jl:8-37
         constexpr int SCH = scheme_of<KIND>();
         if (MODE == MODE_JEXACT) return (SCH == 2 ? A.dt / 2.0 : A.dt) * (A.a * lsum) - xc;
         const double r = SCH == 2 ? (unc + (A.dt / 2.0) * (A.a * lsumg + A.a * lsum)) - xc
                                   : (unc + A.dt * (A.a * lsum)) - xc;
-        return MODE == MODE_JFD ? ((A.fast & 1) ? (r - f0c) * A.ieps : (r - f0c) / A.eps) : r;
+        return MODE == MODE_JFD ? fdq(A, r, f0c) : r;
     }
 }
 
@@ -290,7 +305,8 @@ struct RawRow {
 };
 
 template <int MODE, int VEC, bool EDGE = true, bool G = false, bool PER = false, bool NTU = false>
-__device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o, int64_t oe, int64_t oe2 = 0) {
+__device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o, int64_t oe, int64_t oe2 = 0,
+                                                      bool need1 = true, bool need2 = true) {
     RawRow<MODE, VEC> r;
     const double* __restrict__ pa = (MODE == MODE_JEXACT) ? A.v : A.u;
     if constexpr (VEC % 2 == 0) {
@@ -307,9 +323,17 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o,
     } else {
         r.a[0] = pa[o];
     }
-    if constexpr (EDGE) r.ae = pa[oe];
-    else r.ae = 0.0;
-    if constexpr (EDGE && PER) r.ae2 = pa[oe2];
+    // x-edge values: only the lanes that use them issue the load (need1 / need2: the lane's XEdge flags;
+    // the others' offset is a dummy whose value the cook discards) -- an edge load by all 64 lanes costs the address path a
+    // whole row's worth of work for 2 useful values
+    const bool e1 = EDGE && (A.eall || need1), e2 = EDGE && PER && (A.eall || need2);
+    r.ae = r.ae2 = 0.0;
+    if constexpr (EDGE) {
+        if (e1) r.ae = pa[oe];
+        if constexpr (PER) {
+            if (e2) r.ae2 = pa[oe2];
+        }
+    }
     if constexpr (MODE == MODE_JFD) {
         if constexpr (VEC % 2 == 0) {
 #pragma unroll
@@ -320,9 +344,13 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o,
         } else {
             r.b[0] = A.v[o];
         }
-        if constexpr (EDGE) r.be = A.v[oe];
-        else r.be = 0.0;
-        if constexpr (EDGE && PER) r.be2 = A.v[oe2];
+        r.be = r.be2 = 0.0;
+        if constexpr (EDGE) {
+            if (e1) r.be = A.v[oe];
+            if constexpr (PER) {
+                if (e2) r.be2 = A.v[oe2];
+            }
+        }
     }
     if constexpr (G) {
         if constexpr (VEC % 2 == 0) {
@@ -334,9 +362,13 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o,
         } else {
             r.g[0] = A.un[o];
         }
-        if constexpr (EDGE) r.ge = A.un[oe];
-        else r.ge = 0.0;
-        if constexpr (EDGE && PER) r.ge2 = A.un[oe2];
+        r.ge = r.ge2 = 0.0;
+        if constexpr (EDGE) {
+            if (e1) r.ge = A.un[oe];
+            if constexpr (PER) {
+                if (e2) r.ge2 = A.un[oe2];
+            }
+        }
     }
     return r;
 }
@@ -358,6 +390,18 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw_ib(const KArgs& A, const u
     r.be = r.be2 = 0.0;
     r.ge = r.ge2 = 0.0;
     return r;
+}
+
+// the same, as an override of a row load_raw already issued for that ghost row: only the v values
+// (the stencil field of JEXACT, the tangent part of JFD) come from the inbox.  One load per register
+// whatever the branch, so the march's ping-pong slots never need a copy (nor the vmcnt(0) it costs)
+template <int MODE, int VEC>
+__device__ __forceinline__ void ib_patch(RawRow<MODE, VEC>& r, const uint64_t* ib, int64_t p) {
+#pragma unroll
+    for (int h = 0; h < VEC; ++h) {
+        if constexpr (MODE == MODE_JEXACT) r.a[h] = ld_inbox(ib + p + h);
+        if constexpr (MODE == MODE_JFD) r.b[h] = ld_inbox(ib + p + h);
+    }
 }
 
 // the u part of a raw FD row (u centres, edges, u_n) as a residual row: cooked as MODE_RES it is the
@@ -496,9 +540,7 @@ __device__ __forceinline__ LR x_nbrs(double cfirst, double clast, double e, doub
 // exactly the residual kernel's arithmetic (the u field cooked as MODE_RES, the same Laplacian and
 // point_value), so (F(w) - F(u)) / eps is bit-identical to loading the F0 that kernel stored, and
 // 8 B/pt less is read.  Valid only when F0 IS that residual of this u (the Newton loop's res).
-// D3: the raw rows of the stencil field are issued three rows ahead instead of two (one more raw
-// row in registers), so more loads are in flight per wave; loads only -- bit-identical results.
-template <int KIND, int MODE, int EPI, int VEC, bool PER = false, bool F0R = false, bool D3 = false>
+template <int KIND, int MODE, int EPI, int VEC, bool PER = false, bool F0R = false>
 __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     __shared__ double sh[kShN];
     KArgs A = A0;
@@ -507,7 +549,8 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     constexpr bool kG = SCH != 0 && MODE != MODE_JEXACT;  // u_n rows with the stencil field
     const int lane = threadIdx.x & 63;
     const int nb = gridDim.x, b = blockIdx.x;
-    const int t = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;  // XCD-contiguous tile bands
+    // XCD-contiguous tile bands (lin: tiles in dispatch order, address order)
+    const int t = ((nb & 7) == 0 && !A.lin) ? (b & 7) * (nb >> 3) + (b >> 3) : b;
     const int tx = t % A.tiles_x, ty = t / A.tiles_x;
     const int64_t nx = A.nx, ny = A.ny;
     const int64_t x0 = (int64_t)tx * (kBlock * VEC) + (int64_t)threadIdx.x * VEC;
@@ -544,9 +587,9 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
         // rows y0-1 (ghost plane when y0 = 0) and y0 cooked up front; row y0+1 raw in flight
         const RawRow<MODE, VEC> rm0 =
             ib_lo ? load_raw_ib<MODE, VEC, kG>(A, ib_lo, (y0 - 1) * nx + xc, xc)
-                  : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 - 1) * nx + xc, (y0 - 1) * nx + xc + de, (y0 - 1) * nx + xc + de2);
+                  : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 - 1) * nx + xc, (y0 - 1) * nx + xc + de, (y0 - 1) * nx + xc + de2, edge_ok, edge_ok2);
         const RawRow<MODE, VEC> rc0 =
-            load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, y0 * nx + xc, y0 * nx + xc + de, y0 * nx + xc + de2);
+            load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, y0 * nx + xc, y0 * nx + xc + de, y0 * nx + xc + de2, edge_ok, edge_ok2);
         Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(A, rm0, act, false, false);
         Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, rc0, act, edge_ok, edge_ok2);
         Field<VEC> um{}, uc_{};  // F0R: the u field of rows j-1, j
@@ -554,44 +597,47 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
             um = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res(rm0), act, false, false);
             uc_ = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res(rc0), act, edge_ok, edge_ok2);
         }
-        RawRow<MODE, VEC> rp =
-            (ib_hi && y0 + 1 == ny) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, (y0 + 1) * nx + xc, xc)
-                                    : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 + 1) * nx + xc, (y0 + 1) * nx + xc + de, (y0 + 1) * nx + xc + de2);
-        RawRow<MODE, VEC> rq{};  // D3: row y0 + 2 (clamped to y1, the last row the tile reads)
-        if constexpr (D3) {
-            const int64_t r = y0 + 2 < y1 ? y0 + 2 : y1;
-            const int64_t oq = r * nx + xc;
-            rq = (ib_hi && r == ny) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, oq, xc)
-                                    : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, oq, oq + de, oq + de2);
-        }
-        Row<VEC> uc{}, unc{}, f0c{}, ax{};
-        {
-            const int64_t o = y0 * nx + xc;
-            if constexpr (kU) uc = data_row<VEC>(A.u, o, true);
-            if constexpr (kUn) unc = data_row<VEC, NK_ST_NTN>(A.un, o, true);
-            if constexpr (kF0) f0c = data_row<VEC, NK_ST_NT>(A.F0, o, true);
-            if constexpr (kAx) ax = data_row<VEC>(A.aux, o, true);
-        }
-        for (int64_t j = y0; j < y1; ++j) {
+        // Ping-pong march, unrolled by two: the raw row in flight and the next row's centre operands
+        // alternate between the A and B slots, so nothing loaded is ever copied at the loop's back edge
+        // (a copy of a register whose load is still in flight makes the compiler drain vmcnt(0) there:
+        // one row in flight per wave instead of the pipeline -- measured as the stencils' 0.55-0.65 of
+        // 8 TB/s in round 2)
+        RawRow<MODE, VEC> rA =
+            load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 + 1) * nx + xc, (y0 + 1) * nx + xc + de, (y0 + 1) * nx + xc + de2, edge_ok, edge_ok2);
+        if (ib_hi && y0 + 1 == ny) ib_patch<MODE, VEC>(rA, ib_hi, xc);
+        RawRow<MODE, VEC> rB{};
+        // centre operands of one row: u (Bratu's exact tangent), u_n (G_Euler!), F0, the dot partner
+        struct Ctr {
+            Row<VEC> u, un, f0, ax;
+        };
+        auto load_ctr = [&](int64_t o) {
+            Ctr q{};
+            if constexpr (kU) q.u = data_row<VEC>(A.u, o, true);
+            if constexpr (kUn) q.un = data_row<VEC, NK_ST_NTN>(A.un, o, true);
+            if constexpr (kF0) q.f0 = data_row<VEC, NK_ST_NT>(A.F0, o, true);
+            if constexpr (kAx) q.ax = data_row<VEC>(A.aux, o, true);
+            return q;
+        };
+        Ctr cA = load_ctr(y0 * nx + xc), cB{};
+        // row j: issue raw row j+2 into rn and row j+1's centre operands into cn; cook row j+1 (rc, issued
+        // one row earlier); compute row j from registers with row j's centre operands cc
+        auto step = [&](int64_t j, RawRow<MODE, VEC>& rn, const RawRow<MODE, VEC>& rc, Ctr& cn, const Ctr& cc) {
             const int64_t o = j * nx + xc;
-            // ---- issue: raw row j+2 (rows up to ny are the ghost plane; y1 <= ny keeps j+2 <= ny+1
-            //      in range only when j+1 < y1, so clamp to row j+1 otherwise)
-            const int64_t r2 = D3 ? (j + 3 < y1 ? j + 3 : y1) : ((j + 1 < y1) ? j + 2 : j + 1);  // (ny: the upper ghost row)
-            const int64_t o2 = r2 * nx + xc;
-            const RawRow<MODE, VEC> rpp = (ib_hi && r2 == ny) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, o2, xc)
-                                                              : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, o2, o2 + de, o2 + de2);
-            Row<VEC> ucn{}, uncn{}, f0cn{}, axn{};
-            const int64_t o1 = (j + 1 < y1) ? o + nx : o;
-            if constexpr (kU) ucn = data_row<VEC>(A.u, o1, true);
-            if constexpr (kUn) uncn = data_row<VEC, NK_ST_NTN>(A.un, o1, true);
-            if constexpr (kF0) f0cn = data_row<VEC, NK_ST_NT>(A.F0, o1, true);
-            if constexpr (kAx) axn = data_row<VEC>(A.aux, o1, true);
-            // ---- cook row j+1 (its loads were issued one iteration ago)
-            const Field<VEC> fp = cook<MODE, VEC, SCH, kG, PER>(A, rp, act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
+            // raw row j+2 (rows up to ny are the ghost plane; y1 <= ny keeps j+2 <= ny+1 in range only
+            // when j+1 < y1, so clamp to row j+1 otherwise)
+            if (j + 1 < y1) {  // (the tile's last row needs no further row)
+                const int64_t r2 = j + 2;  // (ny: the upper ghost row)
+                const int64_t o2 = r2 * nx + xc;
+                rn = load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, o2, o2 + de, o2 + de2, edge_ok, edge_ok2);
+                if (ib_hi && r2 == ny) ib_patch<MODE, VEC>(rn, ib_hi, xc);
+                cn = load_ctr(o + nx);
+            }
+            // ---- cook row j+1 (its loads were issued one row ago)
+            const Field<VEC> fp = cook<MODE, VEC, SCH, kG, PER>(A, rc, act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
             Field<VEC> up{};
             LR un_{};
             if constexpr (kR) {
-                up = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res(rp), act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
+                up = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res(rc), act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
                 un_ = x_nbrs<PER>(uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
             }
             // ---- compute row j from registers
@@ -617,8 +663,8 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
                         const double ge = (k == VEC - 1) ? grgt : fc.g[k == VEC - 1 ? k : k + 1];
                         lsumg = lapk(A, fc.g[k], ge, gw, A.hx2, A.ihx2) + lapk(A, fc.g[k], fp.g[k], fm.g[k], A.hy2, A.ihy2);
                     }
-                    const double unk = kG ? fc.g[k] : unc.v[k];
-                    double f0 = f0c.v[k];
+                    const double unk = kG ? fc.g[k] : cc.un.v[k];
+                    double f0 = cc.f0.v[k];
                     if constexpr (kR) {  // F(u) at this point, as the residual kernel evaluates it
                         const double uw = (k == 0) ? un_.l : uc_.c[k == 0 ? 0 : k - 1];
                         const double ue = (k == VEC - 1) ? un_.r : uc_.c[k == VEC - 1 ? k : k + 1];
@@ -626,8 +672,8 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
                         const double lsu = lapk(A, ucc, ue, uw, A.hx2, A.ihx2) + lapk(A, ucc, up.c[k], um.c[k], A.hy2, A.ihy2);
                         f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unk, 0.0, SCH == 1 ? uc_.x[k] : ucc, lsumg);
                     }
-                    double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unk, f0, SCH == 1 ? fc.x[k] : c, lsumg);
-                    acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[k] : ax.v[k], acc);
+                    double r = point_value<KIND, MODE>(A, c, lsum, cc.u.v[k], unk, f0, SCH == 1 ? fc.x[k] : c, lsumg);
+                    acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[k] : cc.ax.v[k], acc);
                     val.v[k] = r;
                 }
                 store_row<VEC>(A.out, o, val);
@@ -638,25 +684,148 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
                     store_row<VEC, NK_ST_NT>(A.vout, o, vn);
                 }
             }
-            fm = fc;
+            fm = fc;  // cooked values (no load in flight): plain moves
             fc = fp;
             if constexpr (kR) {
                 um = uc_;
                 uc_ = up;
             }
-            if constexpr (D3) {
-                rp = rq;
-                rq = rpp;
-            } else {
-                rp = rpp;
-            }
-            uc = ucn;
-            unc = uncn;
-            f0c = f0cn;
-            ax = axn;
+        };
+        int64_t j = y0;
+        for (; j + 1 < y1; j += 2) {
+            step(j, rB, rA, cB, cA);
+            __builtin_amdgcn_sched_barrier(0);  // keep each step's loads in its own half (the slots stay put)
+            step(j + 1, rA, rB, cA, cB);
+            __builtin_amdgcn_sched_barrier(0);
         }
+        if (j < y1) step(j, rB, rA, cB, cA);
     }
     if constexpr (EPI != EPI_NONE) publish(acc, A.part, A.fin, sh);
+}
+
+// ------------------------------------------------------------------------------ 2D stencil, one-shot LDS tile
+// Block = NW waves = NW rows x 64*VEC columns, no march: every wave loads and cooks ITS row once (the
+// first / last wave also the tile's halo rows), publishes the cooked stencil field to LDS, and after
+// one barrier computes its row with the y-neighbours from LDS, the x-neighbours by shuffles.  Tiles in
+// address order: the grid sweeps the arrays front to back like a one-shot copy (the access shape the
+// march lacks: 128 row bands streaming 2 MB apart), with (NW + 2) / NW loads and cooks per row.
+template <int KIND, int MODE, int EPI, int VEC, bool PER = false, bool F0R = false, int NW = 8>
+__global__ __launch_bounds__(64 * NW) void k_st2t(KArgs A0) {
+    __shared__ double sh[kShN];
+    KArgs A = A0;
+    A.hd = A.vdiv ? *A.vdiv : 1.0;
+    constexpr int SCH = scheme_of<KIND>();
+    constexpr bool kG = SCH != 0 && MODE != MODE_JEXACT;
+    constexpr bool kTG = SCH == 2 && kG;              // G_Trapezoid!: u_n's Laplacian
+    constexpr bool kR = MODE == MODE_JFD && F0R;       // F0R: the u field as the residual kernel cooks it
+    constexpr int W = 64 * VEC;
+    __shared__ double lc[NW + 2][W];
+    __shared__ double lg[kTG ? NW + 2 : 1][kTG ? W : 1];
+    __shared__ double lu[kR ? NW + 2 : 1][kR ? W : 1];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int t = blockIdx.x;
+    const int tx = t % A.tiles_x, ty = t / A.tiles_x;
+    const int64_t nx = A.nx, ny = A.ny;
+    const int64_t x0 = (int64_t)tx * W + (int64_t)lane * VEC;
+    const bool act = x0 < nx;
+    const int64_t xc = act ? x0 : 0;
+    const XEdge xe = x_edge<VEC, PER>(lane, act, x0, nx);
+    const int64_t de = xe.de, de2 = xe.de2;
+    const bool edge_ok = xe.ok, edge_ok2 = xe.ok2;
+    const int64_t y0 = (int64_t)ty * NW;
+    const int64_t j = y0 + wv;                          // this wave's row
+    constexpr bool kU = MODE == MODE_JEXACT && KIND == NK_BRATU2D;
+    constexpr bool kUn = KIND == NK_HEAT2D_EULER && MODE != MODE_JEXACT;
+    constexpr bool kF0 = MODE == MODE_JFD && !F0R;
+    constexpr bool kAx = EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID;
+    constexpr bool vout = MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS);
+    // the rows this block's LDS holds: y0 - 1 .. y0 + NW (capped at ny, the upper ghost row)
+    const bool own = j <= ny;                           // row ny (ghost) only as a neighbour
+    const bool lo_halo = wv == 0, hi_halo = wv == NW - 1 && y0 + NW <= ny;
+    auto raw_of = [&](int64_t r) {
+        const int64_t o = r * nx + xc;
+        return load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, o, o + de, o + de2, edge_ok, edge_ok2);
+    };
+    auto put = [&](int i, const RawRow<MODE, VEC>& r, bool eok, bool eok2, Field<VEC>* keep, Field<VEC>* keepu) {
+        const Field<VEC> f = cook<MODE, VEC, SCH, kG, PER>(A, r, act, eok, eok2);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            lc[i][lane * VEC + k] = f.c[k];
+            if constexpr (kTG) lg[kTG ? i : 0][kTG ? lane * VEC + k : 0] = f.g[k];
+        }
+        if (keep) *keep = f;
+        if constexpr (kR) {
+            const Field<VEC> fu = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(r), act, eok, eok2);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) lu[kR ? i : 0][kR ? lane * VEC + k : 0] = fu.c[k];
+            if (keepu) *keepu = fu;
+        }
+    };
+    // ---- issue every load of this wave up front
+    RawRow<MODE, VEC> rown{}, rlo{}, rhi{};
+    if (own) rown = raw_of(j);
+    if (lo_halo) rlo = raw_of(y0 - 1);
+    if (hi_halo) rhi = raw_of(y0 + NW);
+    Row<VEC> uc{}, unc{}, f0c{}, ax{};
+    const bool comp = j < ny;
+    if (comp) {
+        const int64_t o = j * nx + xc;
+        if constexpr (kU) uc = data_row<VEC>(A.u, o, true);
+        if constexpr (kUn) unc = data_row<VEC, NK_ST_NTN>(A.un, o, true);
+        if constexpr (kF0) f0c = data_row<VEC, NK_ST_NT>(A.F0, o, true);
+        if constexpr (kAx) ax = data_row<VEC>(A.aux, o, true);
+    }
+    // ---- cook into LDS
+    Field<VEC> fc{}, uc_{};
+    if (own) put(wv + 1, rown, edge_ok && comp, edge_ok2 && comp, &fc, &uc_);
+    if (lo_halo) put(0, rlo, false, false, nullptr, nullptr);
+    if (hi_halo) put(NW + 1, rhi, false, false, nullptr, nullptr);
+    __syncthreads();
+    double acc = 0.0;
+    if (comp && act) {
+        const LR xn = x_nbrs<PER>(fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
+        LR gn{}, un_{};
+        if constexpr (kTG) gn = x_nbrs<PER>(fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
+        if constexpr (kR) un_ = x_nbrs<PER>(uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
+        Row<VEC> val;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const int q = lane * VEC + k;
+            const double w = (k == 0) ? xn.l : fc.c[k == 0 ? 0 : k - 1];
+            const double e = (k == VEC - 1) ? xn.r : fc.c[k == VEC - 1 ? k : k + 1];
+            const double c = fc.c[k];
+            const double lsum = lapk(A, c, e, w, A.hx2, A.ihx2) + lapk(A, c, lc[wv + 2][q], lc[wv][q], A.hy2, A.ihy2);
+            double lsumg = 0.0;
+            if constexpr (kTG) {
+                const double gw = (k == 0) ? gn.l : fc.g[k == 0 ? 0 : k - 1];
+                const double ge = (k == VEC - 1) ? gn.r : fc.g[k == VEC - 1 ? k : k + 1];
+                lsumg = lapk(A, fc.g[k], ge, gw, A.hx2, A.ihx2) +
+                        lapk(A, fc.g[k], lg[kTG ? wv + 2 : 0][kTG ? q : 0], lg[kTG ? wv : 0][kTG ? q : 0], A.hy2, A.ihy2);
+            }
+            const double unk = kG ? fc.g[k] : unc.v[k];
+            double f0 = f0c.v[k];
+            if constexpr (kR) {
+                const double uw = (k == 0) ? un_.l : uc_.c[k == 0 ? 0 : k - 1];
+                const double ue = (k == VEC - 1) ? un_.r : uc_.c[k == VEC - 1 ? k : k + 1];
+                const double ucc = uc_.c[k];
+                const double lsu = lapk(A, ucc, ue, uw, A.hx2, A.ihx2) +
+                                   lapk(A, ucc, lu[kR ? wv + 2 : 0][kR ? q : 0], lu[kR ? wv : 0][kR ? q : 0], A.hy2, A.ihy2);
+                f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unk, 0.0, SCH == 1 ? uc_.x[k] : ucc, lsumg);
+            }
+            double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unk, f0, SCH == 1 ? fc.x[k] : c, lsumg);
+            acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[k] : ax.v[k], acc);
+            val.v[k] = r;
+        }
+        const int64_t o = j * nx + xc;
+        store_row<VEC>(A.out, o, val);
+        if (vout) {
+            Row<VEC> vn;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) vn.v[k] = fc.vn[k];
+            store_row<VEC, NK_ST_NT>(A.vout, o, vn);
+        }
+    }
+    if constexpr (EPI != EPI_NONE) publish<64 * NW>(acc, A.part, A.fin, sh);
 }
 
 // ------------------------------------------------------------------------------ 3D stencil
@@ -712,9 +881,9 @@ __global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
     if (z0 < nz) {
         const int64_t o0 = z0 * pl + oj;
         Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(A, load_raw<MODE, VEC, false, kG, PER>(A, o0 - pl, 0), act, false);  // plane -1: ghost
-        Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, load_raw<MODE, VEC, true, kG, PER>(A, o0, o0 + de, o0 + de2), act,
+        Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, load_raw<MODE, VEC, true, kG, PER>(A, o0, o0 + de, o0 + de2, edge_ok, edge_ok2), act,
                                                       edge_ok, edge_ok2);
-        RawRow<MODE, VEC> rp = load_raw<MODE, VEC, true, kG, PER>(A, o0 + pl, o0 + pl + de, o0 + pl + de2);  // plane nz: ghost
+        RawRow<MODE, VEC> rp = load_raw<MODE, VEC, true, kG, PER>(A, o0 + pl, o0 + pl + de, o0 + pl + de2, edge_ok, edge_ok2);  // plane nz: ghost
         RawRow<MODE, VEC> rn = load_raw<MODE, VEC, false, kG, PER>(A, o0 + dn, 0);
         RawRow<MODE, VEC> rs = load_raw<MODE, VEC, false, kG, PER>(A, o0 + ds, 0);
         Row<VEC> unc{}, f0c{}, ax{};
@@ -727,7 +896,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
             const bool more = k + 1 < z1;
             const int64_t o2 = more ? o + 2 * pl : o + pl;
             const int64_t o1 = more ? o + pl : o;
-            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2);
+            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2, edge_ok, edge_ok2);
             const RawRow<MODE, VEC> rnn = load_raw<MODE, VEC, false, kG, PER>(A, o1 + dn, 0);
             const RawRow<MODE, VEC> rss = load_raw<MODE, VEC, false, kG, PER>(A, o1 + ds, 0);
             Row<VEC> uncn{}, f0cn{}, axn{};
@@ -868,7 +1037,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
         const int64_t o0 = z0 * pl + oj;
         const RawRow<MODE, VEC> rm0 =
             ib_lo ? load_raw_ib<MODE, VEC, kG>(A, ib_lo, o0 - pl, oj) : load_raw<MODE, VEC, false, kG, PER>(A, o0 - pl, 0);
-        const RawRow<MODE, VEC> rc0 = load_raw<MODE, VEC, true, kG, PER>(A, o0, o0 + de, o0 + de2);
+        const RawRow<MODE, VEC> rc0 = load_raw<MODE, VEC, true, kG, PER>(A, o0, o0 + de, o0 + de2, edge_ok, edge_ok2);
         Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(A, rm0, act, false);
         Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, rc0, act, edge_ok, edge_ok2);
         Field<VEC> um{}, uc_{};  // F0R: the u field of planes k-1, k
@@ -877,7 +1046,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
             uc_ = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rc0), act, edge_ok, edge_ok2);
         }
         RawRow<MODE, VEC> rp = (ib_hi && z0 + 1 == nz) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, o0 + pl, oj)
-                                                       : load_raw<MODE, VEC, true, kG, PER>(A, o0 + pl, o0 + pl + de, o0 + pl + de2);
+                                                       : load_raw<MODE, VEC, true, kG, PER>(A, o0 + pl, o0 + pl + de, o0 + pl + de2, edge_ok, edge_ok2);
         RawRow<MODE, VEC> rn{}, rs{};
         if (ld_n) rn = load_raw<MODE, VEC, false, kG, PER>(A, o0 + dn, 0);
         if (ld_s) rs = load_raw<MODE, VEC, false, kG, PER>(A, o0 + ds, 0);
@@ -901,7 +1070,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
             const int64_t o1 = more ? o + pl : o;
             const int64_t k2 = more ? k + 2 : k + 1;  // the plane o2 is in (nz: the upper ghost plane)
             const RawRow<MODE, VEC> rpp = (ib_hi && k2 == nz) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, o2, oj)
-                                                              : load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2);
+                                                              : load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2, edge_ok, edge_ok2);
             RawRow<MODE, VEC> rnn{}, rss{};
             if (ld_n) rnn = load_raw<MODE, VEC, false, kG, PER>(A, o1 + dn, 0);
             if (ld_s) rss = load_raw<MODE, VEC, false, kG, PER>(A, o1 + ds, 0);
@@ -1015,7 +1184,12 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
 // ------------------------------------------------------------------------------ stencil dispatch
 template <int KIND, int MODE, int EPI, int NW>
 void go_st3l(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
-    if constexpr (MODE == MODE_JFD && heat_kind<KIND>()) {  // F0 recomputed from u (KArgs::f0r)
+#ifdef NK_KBENCH
+    constexpr bool kF0R = MODE == MODE_JFD && heat_kind<KIND>();
+#else
+    constexpr bool kF0R = MODE == MODE_JFD && KIND == NK_HEAT3D_EULER;  // the only 3D F0R kind the launcher picks
+#endif
+    if constexpr (kF0R) {  // F0 recomputed from u (KArgs::f0r)
         if (A.f0r) {
             if (per) {
                 if (vec == 2) hipLaunchKernelGGL((k_st3l<KIND, MODE, EPI, 2, true, NW, true>), dim3(grid), dim3(64 * NW), 0, s, A);
@@ -1054,6 +1228,28 @@ void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
     if constexpr (KIND == NK_BRATU1D) {
         hipLaunchKernelGGL((k_st1d<MODE, EPI>), dim3(grid), dim3(kBlock), 0, s, A);
     } else if constexpr (k2d) {
+#ifdef NK_KBENCH
+        if (A.tile2 && vec == 2) {  // kbench prototype: one-shot LDS tiles of A.tile2 rows
+            const bool f0r = MODE == MODE_JFD && A.f0r;
+            auto go = [&](auto nwc) {
+                constexpr int NWc = decltype(nwc)::value;
+                if (per) {
+                    if constexpr (heat_kind<KIND>()) {
+                        if (f0r) hipLaunchKernelGGL((k_st2t<KIND, MODE, EPI, 2, true, true, NWc>), dim3(grid), dim3(64 * NWc), 0, s, A);
+                        else hipLaunchKernelGGL((k_st2t<KIND, MODE, EPI, 2, true, false, NWc>), dim3(grid), dim3(64 * NWc), 0, s, A);
+                    }
+                } else if (f0r) {
+                    hipLaunchKernelGGL((k_st2t<KIND, MODE, EPI, 2, false, true, NWc>), dim3(grid), dim3(64 * NWc), 0, s, A);
+                } else {
+                    hipLaunchKernelGGL((k_st2t<KIND, MODE, EPI, 2, false, false, NWc>), dim3(grid), dim3(64 * NWc), 0, s, A);
+                }
+            };
+            if (A.tile2 == 16) go(std::integral_constant<int, 16>{});
+            else if (A.tile2 == 4) go(std::integral_constant<int, 4>{});
+            else go(std::integral_constant<int, 8>{});
+            return;
+        }
+#endif
         if constexpr (heat_kind<KIND>()) {  // bc_periodic! instantiations: heat only, VEC <= 2
             if (per) {
                 if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2, true>), dim3(grid), dim3(kBlock), 0, s, A);
@@ -1070,25 +1266,26 @@ void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
                         return;
                     }
                 }
-                if (vec == 2 && A.d3) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2, false, true, true>), dim3(grid), dim3(kBlock), 0, s, A);
-                else if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2, false, true>), dim3(grid), dim3(kBlock), 0, s, A);
+                if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2, false, true>), dim3(grid), dim3(kBlock), 0, s, A);
                 else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1, false, true>), dim3(grid), dim3(kBlock), 0, s, A);
                 return;
             }
         }
+#ifdef NK_KBENCH
         if (vec == 4) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 4>), dim3(grid), dim3(kBlock), 0, s, A);
-        else if (vec == 2 && A.d3) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2, false, false, true>), dim3(grid), dim3(kBlock), 0, s, A);
-        else if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
+        else
+#endif
+        if (vec == 2) hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 2>), dim3(grid), dim3(kBlock), 0, s, A);
         else hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, 1>), dim3(grid), dim3(kBlock), 0, s, A);
     } else {
         // k_st3d: 4-row tiles, every wave loads its y-neighbour rows (8- and 16-row tiles measured 2-9 %
         // slower, profiles/r01/kbench_stencil3d.log); k_st3l: y-neighbours through LDS, 4- or 8-row tiles
-        if (A.lds3) {
-            if (A.nw == 8) go_st3l<KIND, MODE, EPI, 8>(A, vec, grid, s, per);
-            else go_st3l<KIND, MODE, EPI, 4>(A, vec, grid, s, per);
-        } else {
-            go_st3d<KIND, MODE, EPI, 4>(A, vec, grid, s, per);
-        }
+#ifdef NK_KBENCH
+        if (!A.lds3) go_st3d<KIND, MODE, EPI, 4>(A, vec, grid, s, per);
+        else if (A.nw == 8) go_st3l<KIND, MODE, EPI, 8>(A, vec, grid, s, per);
+        else
+#endif
+            go_st3l<KIND, MODE, EPI, 4>(A, vec, grid, s, per);
     }
 }
 

@@ -30,6 +30,10 @@ ap.add_argument("--krylov-itmax", type=int, default=0,
 ap.add_argument("--problem", choices=["bratu", "heat_periodic", "heat3d"], default="bratu",
                 help="heat_periodic: G_Trapezoid! ∘ diffusion! with bc_periodic! -- u_n's ghost planes are "
                      "exchanged too and the slabs form a ring (rank 0 <-> rank world-1)")
+ap.add_argument("--fault-rank", type=int, default=-1,
+                help=">= 0: failure path -- after the first reductions this rank stops taking part (it waits at a "
+                     "gloo barrier, its context alive), the others reduce again and must get an NK_E_* error in "
+                     "bounded time; rank 0 records each rank's outcome")
 ap.add_argument("--transport", choices=["rccl", "mailbox"], default="rccl",
                 help="rccl: nk_dist_init (RCCL bootstrap, then the peer mailbox / RCCL fallback); mailbox: "
                      "IPC handles exchanged over gloo, no RCCL at all (works with every rank on one GPU)")
@@ -127,6 +131,25 @@ ah.mul_(out, ah.JacobianOperator(F_, res, u, p, jv=args.jv), vd)
 jv_loc = out.to_numpy()
 F_loc = res.to_numpy()
 dot = ah.kdot(len(u), u, vd)
+if args.fault_rank >= 0:
+    import time
+
+    outcome = dict(rank=rank, skipped=rank == args.fault_rank)
+    if rank != args.fault_rank:
+        t0 = time.perf_counter()
+        try:
+            ah.kdot(len(u), u, vd)  # a reduction the faulty rank never contributes to
+            outcome["error"] = None
+        except ah.NKError as e:
+            outcome["error"] = str(e)
+        outcome["seconds"] = time.perf_counter() - t0
+        outcome["path"] = ctx.path_info()
+    outs = [None] * world
+    dist.all_gather_object(outs, outcome)  # the faulty rank joins here: its context stayed alive meanwhile
+    if rank == 0:
+        json.dump(dict(fault=outs, world=world, first_dot=dot), open(args.out + ".json", "w"))
+    dist.barrier()
+    sys.exit(0)  # no ctx.sync(): the mailbox error is sticky on the ranks that timed out
 if args.krylov_itmax > 0:
     ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=10))
     ctx.prof_enable(1)

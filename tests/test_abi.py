@@ -25,6 +25,29 @@ def test_library_built_in_tree():
     assert _lib.LIB_PATH.startswith(os.path.dirname(os.path.dirname(__file__)))
 
 
+KNOBS = ["NK_RES_NOXCHG", "NK_RES_JV", "NK_RES_STRIDED", "NK_RES_NTC", "NK_RES_PRE", "NK_F0R",
+         "NK_ST_BLOCKS", "NK_MGS_VARIANT", "NK_HALO_FUSE", "NK_RED_BLOCKS", "NK_UPD_U"]
+
+
+def test_product_library_has_no_kbench_hooks_or_knobs():
+    """The product library (what the Julia shim and the Python mirror load) carries no timing hooks,
+    no tuning knob and no wrong-answer probe (NK_RES_NOXCHG): those live in the kernel-variant bench
+    build only, lib/libnkhip_kbench.so, which exports the nkb_* hooks and reads the knobs."""
+    prod = open(_lib.PRODUCT_LIB, "rb").read()
+    kb = open(_lib.KBENCH_LIB, "rb").read()
+    for sym in (b"nkb_copy", b"nkb_stencil_kind", b"nkb_mgs_res", b"nkb_update_x"):
+        assert sym not in prod, sym
+        assert sym in kb, sym
+    for k in KNOBS:
+        assert k.encode() not in prod, k
+        assert k.encode() in kb, k
+    # the product is the smaller build: variant instantiations pruned
+    assert len(prod) < 0.7 * len(kb)
+    # operational configuration stays readable in the product (transport, timeouts, shared-GPU rigs)
+    for k in (b"NK_DIST_MAILBOX", b"NK_MB_SPIN_LIMIT", b"NK_RES_SHARED"):
+        assert k in prod, k
+
+
 def test_every_header_symbol_exported_and_bound():
     lib = ah.load()
     names = header_functions()

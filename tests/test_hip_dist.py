@@ -2,8 +2,11 @@
 
 * one rank with a forced RCCL communicator: every reduction goes through finalize -> ncclAllReduce
   -> consumer, which must reproduce the single-GPU run bit for bit (same partials, same order);
-* 2 and 3 ranks (slabs of a 2D Bratu grid): halo exchange + all-reduced dots against the CPU
-  oracle on the whole grid.  Each rank gets its own GPU when the box has enough (then the RCCL
+* 2, 3, 4 and 8 ranks (slabs of a 2D Bratu grid, z-slabs of a 3D heat grid, a periodic ring): halo
+  exchange + all-reduced dots against the CPU oracle on the whole grid -- 8 ranks is the decomposition
+  of BASELINE configs 4 and 5;
+* the failure path: a rank that stops taking part makes every other rank's next reduction return an
+  NK_E_* error in bounded time, and `bench.py --gpus N` then exits non-zero instead of hanging.  Each rank gets its own GPU when the box has enough (then the RCCL
   variants must run: an RCCL error fails the test); on a box with fewer GPUs than ranks they
   share device 0, where only the mailbox transport can run (RCCL refuses -> skip).
 """
@@ -114,7 +117,7 @@ def free_port():
 
 
 @pytest.mark.parametrize("transport,world", [("mailbox", 2), ("rccl", 2), ("mailbox", 3), ("rccl", 3), ("mailbox", 4),
-                                             ("rccl", 4)])
+                                             ("rccl", 4), ("mailbox", 8), ("rccl", 8)])
 def test_slabs_match_oracle(tmp_path, world, transport):
     """Slabs of one 2D Bratu grid on `world` ranks: residual, Jv (ghost rows from the neighbours),
     a dot, and a whole Newton-GMRES solve against the oracle on the full grid.  transport=mailbox
@@ -149,7 +152,7 @@ def test_slabs_match_oracle(tmp_path, world, transport):
 
 
 @pytest.mark.parametrize("transport", ["mailbox", "rccl"])
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_periodic_trapezoid_ring_matches_oracle(tmp_path, world, transport):
     """G_Trapezoid! ∘ diffusion! with bc_periodic! on `world` slabs: u_n's ghost planes are exchanged
     as well, and the slabs form a ring (rank 0's lower ghost is rank world-1's last plane; with two
@@ -185,15 +188,15 @@ def test_periodic_trapezoid_ring_matches_oracle(tmp_path, world, transport):
 
 def test_resident_sweep_two_ranks_one_gpu(tmp_path):
     """The resident MGS sweep with its per-pass scalars crossing ranks through the peer mailbox: two
-    ranks share the test box's GPU, each with a 128-block sweep grid (NK_RES_BLOCKS) so that both
-    grids are resident together; 1024^2 global (a 1024 x 512 slab per rank: all of q on chip, the
+    ranks share the test box's GPU, each with a 128-block sweep grid (NK_RES_SHARED: CUs / ranks on
+    the GPU) so that both grids are resident together; 1024^2 global (a 1024 x 512 slab per rank: all of q on chip, the
     V_{k+1} hand-over to the next Jv included).  20 restarted GMRES(10) steps against the oracle."""
     out = str(tmp_path / "dist")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
            "--nx", "1024", "--ny", "1024", "--krylov-itmax", "20"]
-    env = worker_env(2, NK_RES_SHARED="1", NK_RES_BLOCKS="128")
+    env = worker_env(2, NK_RES_SHARED="1")
     proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
     try:
         log, _ = proc.communicate(timeout=180)
@@ -214,7 +217,7 @@ def test_resident_sweep_two_ranks_one_gpu(tmp_path):
     assert np.max(np.abs(d["x"] - xo)) <= 1e-9 * np.max(np.abs(xo))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_heat3d_midpoint_zslabs_match_oracle(tmp_path, world):
     """3D heat (G_Midpoint!, alpha 0.3) on z-slabs, mailbox transport: the Jv's ghost planes of v travel
     inside the 3D stencil launch (k_st3l's tiles at the slab ends fetch the neighbours' patches).
@@ -249,3 +252,79 @@ def test_heat3d_midpoint_zslabs_match_oracle(tmp_path, world):
     assert meta["solved"] and so["solved"]
     assert (meta["outer"], meta["inner"]) == (so["outer_iterations"], so["inner_iterations"])
     assert np.max(np.abs(d["u"] - uo)) <= 1e-10
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_dead_rank_reduction_errors_in_bounded_time(tmp_path, world):
+    """A rank that never contributes to a reduction (it stops after the first dot, its context alive):
+    every other rank's next kdot must return an NK_E_* error ("a rank's value never arrived") within
+    the mailbox spin limit -- never a hang -- and the path report must show the sticky mailbox error."""
+    out = str(tmp_path / "fault")
+    fault = world - 1
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
+           "--fault-rank", str(fault)]
+    env = worker_env(world, NK_MB_SPIN_LIMIT=str(1 << 18))
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
+    try:
+        log, _ = proc.communicate(timeout=180)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, signal.SIGKILL)
+        pytest.fail("a rank hung on a dead peer")
+    assert proc.returncode == 0, log.decode()[-3000:]
+    meta = json.load(open(out + ".json"))
+    P = oc.bratu2d(48, 40)
+    v = np.random.default_rng(7).standard_normal((40, 48))
+    assert abs(meta["first_dot"] - float(np.sum(oc.sin_ic(P) * v))) <= 1e-12 * np.sqrt(v.size)  # healthy before
+    for o in meta["fault"]:
+        if o["rank"] == fault:
+            assert o["skipped"]
+            continue
+        assert o["error"] and "never arrived" in o["error"], o
+        assert o["seconds"] < 60.0, o
+        assert o["path"]["mailbox"] and o["path"]["mailbox_error"], o
+
+
+def test_bench_exits_nonzero_on_a_stuck_rank(tmp_path):
+    """`bench.py --gpus 2` whose rank 1 hangs before its first timed step (NK_BENCH_FAULT_RANK=1): rank 0's
+    mailbox waits time out into an error, it exits non-zero, the launcher tears the job down -- the bench
+    ends with a non-zero status in bounded time instead of hanging."""
+    env = worker_env(2, NK_BENCH_FAULT_RANK="1", NK_MB_SPIN_LIMIT=str(1 << 18))
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--transport", "mailbox", "--side", "256",
+           "--steps", "2", "--warmup", "1", "--itmax", "30", "--no-cpu-baseline"]
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
+    try:
+        log, _ = proc.communicate(timeout=240)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, signal.SIGKILL)
+        pytest.fail("bench.py hung on a stuck rank")
+    text = log.decode(errors="replace")
+    assert proc.returncode != 0, text[-3000:]
+    assert "never arrived" in text, text[-3000:]
+
+
+def test_bench_reports_every_ranks_path(tmp_path):
+    """The N > 1 bench line carries one path record per rank (transport, resident sweep, in-launch ghost
+    planes, launch counts): 8 ranks rehearsed on the box's GPU(s) with the mailbox transport."""
+    world = 8
+    env = worker_env(world)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--transport", "mailbox",
+           "--side", "256", "--steps", "2", "--warmup", "1", "--itmax", "30", "--no-cpu-baseline"]
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, start_new_session=True)
+    try:
+        out, err = proc.communicate(timeout=240)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, signal.SIGKILL)
+        pytest.fail("8-rank bench rehearsal timed out")
+    assert proc.returncode == 0, err.decode()[-3000:]
+    line = json.loads([ln for ln in out.decode().splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == world and len(line["ranks"]) == world
+    assert sorted(r["rank"] for r in line["ranks"]) == list(range(world))
+    for r in line["ranks"]:
+        assert r["mailbox"] and r["nranks"] == world and not r["mailbox_error"]
+        assert r["halo_in_launch"]
+        assert r["launches"]["halo_rccl"] == 0 and r["launches"]["allreduce"] == 0
+    assert line["config"]["path"]["mailbox_all_ranks"]

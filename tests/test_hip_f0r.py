@@ -152,9 +152,10 @@ print(json.dumps(out))
 
 def test_f0_recomputed_bitwise_when_forced():
     """Every F0R kernel the default policy does not pick -- Bratu 2D, the 3D midpoint / trapezoid and
-    V_1 steps -- forced with NK_F0R=2 (in a child process: the knob is read once per process)."""
+    V_1 steps -- forced with NK_F0R=2 (a tuning knob of the kernel-variant bench build,
+    lib/libnkhip_kbench.so, in a child process: the knob is read once per process)."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    p = subprocess.run([sys.executable, "-c", BRATU_CHILD, root], env=dict(os.environ, NK_F0R="2"),
+    p = subprocess.run([sys.executable, "-c", BRATU_CHILD, root], env=dict(os.environ, NK_F0R="2", NK_KBENCH_LIB="1"),
                        capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-2000:]
     res = json.loads(p.stdout.strip().splitlines()[-1])

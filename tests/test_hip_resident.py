@@ -128,13 +128,14 @@ np.savez(sys.argv[2], x=ws.x.to_numpy(), h=np.array(ws.stats.residuals), F0=res.
 
 
 def test_fused_jv_sweep_matches_oracle(tmp_path):
-    """NK_RES_JV=1 (off by default): the FD Jv computed inside the resident launch, against the oracle."""
+    """NK_RES_JV=1 (the kernel-variant bench build only; not shipped): the FD Jv computed inside the
+    resident launch, against the oracle."""
     import os
     import subprocess
     import sys
 
     out = tmp_path / "jv.npz"
-    env = dict(os.environ, NK_RES_JV="1")
+    env = dict(os.environ, NK_RES_JV="1", NK_KBENCH_LIB="1")  # a variant of the kbench build only
     tests = os.path.dirname(os.path.abspath(__file__))
     r = subprocess.run([sys.executable, "-c", _JV_CHILD, tests, str(out)], env=env, capture_output=True, text=True,
                        timeout=180)
@@ -305,15 +306,18 @@ def test_sweep_load_flavours_are_bitwise(tmp_path):
     """The partly resident sweep's cache-policy choices change only how loads and stores are issued
     -- the Infinity-Cache room given to the first streamed slots (NK_RES_NTC), the non-temporal
     streamed remainder (NK_RES_NTS), the first batch loaded across the hand-off (NK_RES_PRE) -- never
-    the arithmetic or its order: restarted GMRES with reorthogonalisation, bit for bit."""
+    the arithmetic or its order: restarted GMRES with reorthogonalisation, bit for bit -- the product
+    library against the kernel-variant bench build (lib/libnkhip_kbench.so) with each knob flipped."""
     import os
     import subprocess
     import sys
 
     tests = os.path.dirname(os.path.abspath(__file__))
     runs = {}
-    for name, extra in [("default", {}), ("ntc0", {"NK_RES_NTC": "0"}), ("ntc_all", {"NK_RES_NTC": "100000"}),
-                        ("nts0", {"NK_RES_NTS": "0"}), ("pre0", {"NK_RES_PRE": "0"})]:
+    kb = {"NK_KBENCH_LIB": "1"}  # the knobs are read by the kernel-variant bench build only
+    for name, extra in [("default", {}), ("kbench", kb), ("ntc0", dict(kb, NK_RES_NTC="0")),
+                        ("ntc_all", dict(kb, NK_RES_NTC="100000")), ("nts0", dict(kb, NK_RES_NTS="0")),
+                        ("pre0", dict(kb, NK_RES_PRE="0"))]:
         out = tmp_path / f"{name}.npz"
         r = subprocess.run([sys.executable, "-c", _FLAVOUR_CHILD, tests, str(out)], env=dict(os.environ, **extra),
                            capture_output=True, text=True, timeout=240)

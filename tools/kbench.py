@@ -1,7 +1,7 @@
 """In-process A/B of kernel variants (interleaved rounds, median reported).
 
 Usage (GPU box): python tools/kbench.py [--n 16777216] [--rounds 5]
-Not part of the product; drives the nkb_* hooks compiled into libnkhip.so.
+Not part of the product; drives the nkb_* hooks compiled into libnkhip_kbench.so.
 """
 import argparse
 import ctypes as C
@@ -10,6 +10,7 @@ import statistics
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("NK_KBENCH_LIB", "1")  # the nkb_* hooks live in lib/libnkhip_kbench.so
 import _nkpath  # noqa: F401,E402
 import ariadne_hip as ah  # noqa: E402
 

@@ -10,6 +10,7 @@ import statistics
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("NK_KBENCH_LIB", "1")  # the nkb_* hooks live in lib/libnkhip_kbench.so
 import _nkpath  # noqa: F401,E402
 import ariadne_hip as ah  # noqa: E402
 
@@ -19,7 +20,9 @@ ap.add_argument("--side", type=int, default=8192)
 ap.add_argument("--nz", type=int, default=0, help="3D kinds: planes (default side)")
 ap.add_argument("--modes", default="0:1,2:2", help="mode:epi pairs (0:1 residual+norm, 2:2 FD Jv+dot)")
 ap.add_argument("--rows", default="0,16,32,64,128")
-ap.add_argument("--fast", default="0,4", help="variant bits: 4 VEC=4 (2D), 8/16 LDS tiles of 4/8 rows (3D), 32 F0 recomputed")
+ap.add_argument("--fast", default="0,4", help="variant bits: 1 reciprocals for the divisions (not bit-faithful), "
+                "4 VEC=4 (2D), 8/16 LDS tiles of 4/8 rows (3D), 32 F0 recomputed, 64 raw rows three ahead, "
+                "128 bc_periodic!, 256 fused normalisation (V_k = v / h stored)")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=10)
 args = ap.parse_args()
@@ -36,8 +39,9 @@ def words(kind, mode, epi, fast=0):  # the launcher's algorithmic count (fast bi
     heat = kind >= 3
     w = 1
     w += (1 + heat) if mode == 0 else ((1 + (not heat)) if mode == 1 else (3 + heat))
-    f0r = mode == 2 and fast & 32 and (kind in (3, 5, 7) or kind == 4)
-    return w + (1 if epi == 2 else 0) - (1 if f0r else 0)
+    f0r = mode == 2 and fast & 32 and (kind in (2, 3, 5, 7) or kind == 4)
+    vout = mode != 0 and epi == 2 and fast & 256  # fused normalisation: V_k stored
+    return w + (1 if epi == 2 else 0) - (1 if f0r else 0) + (1 if vout else 0)
 
 
 res = {}

@@ -3,7 +3,7 @@
 Every tile re-reads the two planes around its z-range, so a tile of P planes loads (P + 2) / P of
 the compulsory bytes; longer marches cut that but leave fewer blocks.  Usage (GPU box):
     python tools/kbench_st3d.py [--n 512] [--nz 512,64] [--rounds 5]
-Not part of the product; drives the nkb_stencil3d_ex hook compiled into libnkhip.so.
+Not part of the product; drives the nkb_stencil3d_ex hook compiled into libnkhip_kbench.so.
 """
 import argparse
 import ctypes as C
@@ -12,6 +12,7 @@ import statistics
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("NK_KBENCH_LIB", "1")  # the nkb_* hooks live in lib/libnkhip_kbench.so
 import _nkpath  # noqa: F401,E402
 import ariadne_hip as ah  # noqa: E402
 

@@ -1,4 +1,4 @@
-"""HBM streaming-rate probe (copy kernel variants x grid sizes), drives nkb_stream in libnkhip.so.
+"""HBM streaming-rate probe (copy kernel variants x grid sizes), drives nkb_stream in libnkhip_kbench.so.
 
 Usage (GPU box): python tools/stream_probe.py [--n 134217728] [--rounds 3]
 Vectors of n doubles (default 1 GiB each: far beyond the 256 MB Infinity Cache).
@@ -10,6 +10,7 @@ import statistics
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("NK_KBENCH_LIB", "1")  # the nkb_* hooks live in lib/libnkhip_kbench.so
 import _nkpath  # noqa: F401,E402
 import ariadne_hip as ah  # noqa: E402
 
