@@ -346,7 +346,17 @@ int nk_ilu0_factor(nk_ctx* c, const nk_problem* p, const double* u, double* dtil
     if (nk_is_user(p->kind)) return fail(c, NK_E_ARG, "ILU(0) of a user residual: assemble it with collect(J)");
     if (p->bc == NK_BC_PERIODIC) return fail(c, NK_E_ARG, "ILU(0) is implemented for bc_zero! (the wrap breaks the banded pattern)");
     NK_TRY(launch_jdiag(c, p, dtilde, u, 0));
-    return launch_ilu0_factor(c, p, g.dim, dtilde);
+    NK_TRY(launch_ilu0_factor(c, p, g.dim, dtilde));
+    // the factor is kept by the preconditioner and reused by later solves: make sure it is whole.  A
+    // pipelined sweep that timed out left D~ partly factored -- start again from diag(J) on the level sweep
+    const int bad = ilu_pipe_failed(c);
+    if (bad < 0) return bad;
+    if (bad == 1) {
+        NK_TRY(launch_jdiag(c, p, dtilde, u, 0));
+        NK_TRY(launch_ilu0_factor(c, p, g.dim, dtilde));
+        NK_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    return NK_OK;
 }
 
 int nk_jtv(nk_ctx* c, const nk_problem* p, double* out, const double* u, const double* v) {

@@ -264,6 +264,9 @@ int launch_diag_apply(nk_ctx* c, int64_t n, double* z, const double* d, const do
 int launch_jdiag(nk_ctx* c, const nk_problem* p, double* out, const double* u, int recip);        // diag(J(u)) or 1 ./ diag
 int launch_ilu0_factor(nk_ctx* c, const nk_problem* p, int dim, double* d);                       // diag(J) -> D~ (in place)
 int launch_ilu0_solve(nk_ctx* c, const nk_problem* p, int dim, const double* d, double* z, const double* v);  // z = (LU)^-1 v
+// after a pipelined ILU(0) launch: 1 if its progress poll timed out (output partial; the pipelined path
+// is now off for this context), 0 if it completed, < 0 on a HIP error
+int ilu_pipe_failed(nk_ctx* c);
 // NK_USER pieces: w = u + eps (v / *vdiv) (w may be null) and vout = v / *vdiv (vout may be null);
 // and the epilogue pass after a user F / J: out = (out - F0) / eps when fd, + the `epi` partials.
 int launch_fd_point(nk_ctx* c, int64_t n, double* w, const double* u, const double* v, const double* vdiv,

@@ -711,7 +711,6 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     A.vout = in.vout;
     A.ihx2 = 1.0 / A.hx2; A.ihy2 = 1.0 / A.hy2; A.ihz2 = 1.0 / A.hz2; A.ieps = in.eps != 0.0 ? 1.0 / in.eps : 0.0;
     A.alpha = p->alpha;
-    A.eall = (fast & 4096) ? 1 : 0;  // kbench: x-edge loads by every lane
     const bool per = p->bc == NK_BC_PERIODIC;
     int vec = 1, grid = 1;
     if (g.dim == 1) {
@@ -1335,6 +1334,19 @@ int launch_ilu0_factor(nk_ctx* c, const nk_problem* p, int dim, double* d) {
     });
 }
 
+// a pipelined sweep whose strip-progress poll timed out (ilu_err) left its output partial: wait for it,
+// and if so turn the pipelined path off for this context and return 1 (the caller redoes the work on
+// the one-work-group level sweep) -- the error never reaches a later call or a reused factor
+int ilu_pipe_failed(nk_ctx* c) {
+    if (!c->ilu_err) return 0;
+    NK_HIP(c, hipStreamSynchronize(c->stream));
+    if (!*(volatile int*)c->ilu_err) return 0;
+    *c->ilu_err = 0;
+    c->ilu_pipe_ok = false;
+    std::fprintf(stderr, "[nkhip] pipelined ILU(0) sweep timed out; redone with the level sweep, which is used from now on\n");
+    return 1;
+}
+
 int launch_ilu0_solve(nk_ctx* c, const nk_problem* p, int dim, const double* d, double* z, const double* v) {
     const double n = (double)(p->nx * p->ny * p->nz);
     if (ilu_pipe_applies(c, p)) {
@@ -1345,7 +1357,10 @@ int launch_ilu0_solve(nk_ctx* c, const nk_problem* p, int dim, const double* d, 
         P.z = z;
         P.v = v;
         NK_TRY(ilu_pipe_launch<1>(c, P, grid, "ilu0_forward", 24.0 * n));  // v, d in; y out
-        return ilu_pipe_launch<2>(c, P, grid, "ilu0_backward", 24.0 * n);  // y, d in; z out
+        NK_TRY(ilu_pipe_launch<2>(c, P, grid, "ilu0_backward", 24.0 * n));  // y, d in; z out
+        const int bad = ilu_pipe_failed(c);
+        if (bad < 0) return bad;
+        if (bad == 0) return NK_OK;  // else: z is partial -- the level sweep below recomputes it from v
     }
     const IluArgs I = ilu_args(p, dim);
     return launch(c, "ilu0_solve_levels", 48.0 * n, [&] {

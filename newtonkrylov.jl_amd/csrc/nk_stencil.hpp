@@ -32,7 +32,6 @@ struct KArgs {
     int nw;              // 3D: rows (waves) per tile
     int lds3;            // 3D: y-neighbour rows through LDS (k_st3l) instead of per-wave loads (k_st3d)
     int lin;             // tiles in dispatch (= address) order instead of XCD-contiguous bands
-    int eall;            // kbench: every lane issues the x-edge loads (round 2's form) instead of the edge lanes only
     int tile2;           // kbench: 2D one-shot LDS tiles of tile2 rows (k_st2t) instead of the march
     int f0r;             // 2D FD: F0 = F(u) recomputed from the u rows already loaded (k_st2d<..., F0R>)
     // ghost planes of v through the peers' inboxes inside this launch (halo_tile_exchange): the rank
@@ -305,8 +304,7 @@ struct RawRow {
 };
 
 template <int MODE, int VEC, bool EDGE = true, bool G = false, bool PER = false, bool NTU = false>
-__device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o, int64_t oe, int64_t oe2 = 0,
-                                                      bool need1 = true, bool need2 = true) {
+__device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o, int64_t oe, int64_t oe2 = 0) {
     RawRow<MODE, VEC> r;
     const double* __restrict__ pa = (MODE == MODE_JEXACT) ? A.v : A.u;
     if constexpr (VEC % 2 == 0) {
@@ -323,17 +321,9 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o,
     } else {
         r.a[0] = pa[o];
     }
-    // x-edge values: only the lanes that use them issue the load (need1 / need2: the lane's XEdge flags;
-    // the others' offset is a dummy whose value the cook discards) -- an edge load by all 64 lanes costs the address path a
-    // whole row's worth of work for 2 useful values
-    const bool e1 = EDGE && (A.eall || need1), e2 = EDGE && PER && (A.eall || need2);
-    r.ae = r.ae2 = 0.0;
-    if constexpr (EDGE) {
-        if (e1) r.ae = pa[oe];
-        if constexpr (PER) {
-            if (e2) r.ae2 = pa[oe2];
-        }
-    }
+    if constexpr (EDGE) r.ae = pa[oe];
+    else r.ae = 0.0;
+    if constexpr (EDGE && PER) r.ae2 = pa[oe2];
     if constexpr (MODE == MODE_JFD) {
         if constexpr (VEC % 2 == 0) {
 #pragma unroll
@@ -344,13 +334,9 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o,
         } else {
             r.b[0] = A.v[o];
         }
-        r.be = r.be2 = 0.0;
-        if constexpr (EDGE) {
-            if (e1) r.be = A.v[oe];
-            if constexpr (PER) {
-                if (e2) r.be2 = A.v[oe2];
-            }
-        }
+        if constexpr (EDGE) r.be = A.v[oe];
+        else r.be = 0.0;
+        if constexpr (EDGE && PER) r.be2 = A.v[oe2];
     }
     if constexpr (G) {
         if constexpr (VEC % 2 == 0) {
@@ -362,13 +348,9 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o,
         } else {
             r.g[0] = A.un[o];
         }
-        r.ge = r.ge2 = 0.0;
-        if constexpr (EDGE) {
-            if (e1) r.ge = A.un[oe];
-            if constexpr (PER) {
-                if (e2) r.ge2 = A.un[oe2];
-            }
-        }
+        if constexpr (EDGE) r.ge = A.un[oe];
+        else r.ge = 0.0;
+        if constexpr (EDGE && PER) r.ge2 = A.un[oe2];
     }
     return r;
 }
@@ -390,18 +372,6 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw_ib(const KArgs& A, const u
     r.be = r.be2 = 0.0;
     r.ge = r.ge2 = 0.0;
     return r;
-}
-
-// the same, as an override of a row load_raw already issued for that ghost row: only the v values
-// (the stencil field of JEXACT, the tangent part of JFD) come from the inbox.  One load per register
-// whatever the branch, so the march's ping-pong slots never need a copy (nor the vmcnt(0) it costs)
-template <int MODE, int VEC>
-__device__ __forceinline__ void ib_patch(RawRow<MODE, VEC>& r, const uint64_t* ib, int64_t p) {
-#pragma unroll
-    for (int h = 0; h < VEC; ++h) {
-        if constexpr (MODE == MODE_JEXACT) r.a[h] = ld_inbox(ib + p + h);
-        if constexpr (MODE == MODE_JFD) r.b[h] = ld_inbox(ib + p + h);
-    }
 }
 
 // the u part of a raw FD row (u centres, edges, u_n) as a residual row: cooked as MODE_RES it is the
@@ -515,6 +485,22 @@ __device__ __forceinline__ XEdge x_edge(int lane, bool act, int64_t x0, int64_t 
     return x;
 }
 
+// Block -> tile.  Tiles go to the 8 XCDs in contiguous bands (b % 8 is the XCD a block lands on), so
+// vertically adjacent tiles share an L2.  With ghost planes exchanged inside the launch (hx_lo / hx_hi)
+// the tiles at the slab's ends come first -- the lower band, then the upper band: they push this rank's
+// boundary patch at once and wait for the neighbour's, which the neighbour's launch also issues first.
+// Dispatched last (in address order), a lower tile would wait on a neighbour whose upper tiles start
+// only when most of ITS launch is done -- a chain along the ranks whenever a launch has more tiles than
+// the GPU holds at once.  `band` = tiles per plane / row band, `nband` = bands.
+__device__ __forceinline__ int tile_of(int b, int nb, int band, int nband, int lo, int hi, int lin) {
+    auto xcd = [lin](int i, int n) { return ((n & 7) == 0 && !lin) ? (i & 7) * (n >> 3) + (i >> 3) : i; };
+    const int nl = lo ? band : 0, nh = (hi && nband > 1) ? band : 0;
+    if (nl + nh == 0) return xcd(b, nb);
+    if (b < nl) return b;
+    if (b < nl + nh) return (nband - 1) * band + (b - nl);
+    return xcd(b - nl - nh, nb - nl - nh) + nl;
+}
+
 // west / east neighbours of the VEC points of a lane: lane shuffles, the wave-edge lanes' edge values
 struct LR {
     double l, r;
@@ -549,8 +535,7 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     constexpr bool kG = SCH != 0 && MODE != MODE_JEXACT;  // u_n rows with the stencil field
     const int lane = threadIdx.x & 63;
     const int nb = gridDim.x, b = blockIdx.x;
-    // XCD-contiguous tile bands (lin: tiles in dispatch order, address order)
-    const int t = ((nb & 7) == 0 && !A.lin) ? (b & 7) * (nb >> 3) + (b >> 3) : b;
+    const int t = tile_of(b, nb, A.tiles_x, A.tiles_y, A.hx_lo, A.hx_hi, A.lin);  // (lin: address order)
     const int tx = t % A.tiles_x, ty = t / A.tiles_x;
     const int64_t nx = A.nx, ny = A.ny;
     const int64_t x0 = (int64_t)tx * (kBlock * VEC) + (int64_t)threadIdx.x * VEC;
@@ -587,9 +572,9 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
         // rows y0-1 (ghost plane when y0 = 0) and y0 cooked up front; row y0+1 raw in flight
         const RawRow<MODE, VEC> rm0 =
             ib_lo ? load_raw_ib<MODE, VEC, kG>(A, ib_lo, (y0 - 1) * nx + xc, xc)
-                  : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 - 1) * nx + xc, (y0 - 1) * nx + xc + de, (y0 - 1) * nx + xc + de2, edge_ok, edge_ok2);
+                  : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 - 1) * nx + xc, (y0 - 1) * nx + xc + de, (y0 - 1) * nx + xc + de2);
         const RawRow<MODE, VEC> rc0 =
-            load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, y0 * nx + xc, y0 * nx + xc + de, y0 * nx + xc + de2, edge_ok, edge_ok2);
+            load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, y0 * nx + xc, y0 * nx + xc + de, y0 * nx + xc + de2);
         Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(A, rm0, act, false, false);
         Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, rc0, act, edge_ok, edge_ok2);
         Field<VEC> um{}, uc_{};  // F0R: the u field of rows j-1, j
@@ -597,47 +582,37 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
             um = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res(rm0), act, false, false);
             uc_ = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res(rc0), act, edge_ok, edge_ok2);
         }
-        // Ping-pong march, unrolled by two: the raw row in flight and the next row's centre operands
-        // alternate between the A and B slots, so nothing loaded is ever copied at the loop's back edge
-        // (a copy of a register whose load is still in flight makes the compiler drain vmcnt(0) there:
-        // one row in flight per wave instead of the pipeline -- measured as the stencils' 0.55-0.65 of
-        // 8 TB/s in round 2)
-        RawRow<MODE, VEC> rA =
-            load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 + 1) * nx + xc, (y0 + 1) * nx + xc + de, (y0 + 1) * nx + xc + de2, edge_ok, edge_ok2);
-        if (ib_hi && y0 + 1 == ny) ib_patch<MODE, VEC>(rA, ib_hi, xc);
-        RawRow<MODE, VEC> rB{};
-        // centre operands of one row: u (Bratu's exact tangent), u_n (G_Euler!), F0, the dot partner
-        struct Ctr {
-            Row<VEC> u, un, f0, ax;
-        };
-        auto load_ctr = [&](int64_t o) {
-            Ctr q{};
-            if constexpr (kU) q.u = data_row<VEC>(A.u, o, true);
-            if constexpr (kUn) q.un = data_row<VEC, NK_ST_NTN>(A.un, o, true);
-            if constexpr (kF0) q.f0 = data_row<VEC, NK_ST_NT>(A.F0, o, true);
-            if constexpr (kAx) q.ax = data_row<VEC>(A.aux, o, true);
-            return q;
-        };
-        Ctr cA = load_ctr(y0 * nx + xc), cB{};
-        // row j: issue raw row j+2 into rn and row j+1's centre operands into cn; cook row j+1 (rc, issued
-        // one row earlier); compute row j from registers with row j's centre operands cc
-        auto step = [&](int64_t j, RawRow<MODE, VEC>& rn, const RawRow<MODE, VEC>& rc, Ctr& cn, const Ctr& cc) {
+        RawRow<MODE, VEC> rp =
+            (ib_hi && y0 + 1 == ny) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, (y0 + 1) * nx + xc, xc)
+                                    : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 + 1) * nx + xc, (y0 + 1) * nx + xc + de, (y0 + 1) * nx + xc + de2);
+        Row<VEC> uc{}, unc{}, f0c{}, ax{};
+        {
+            const int64_t o = y0 * nx + xc;
+            if constexpr (kU) uc = data_row<VEC>(A.u, o, true);
+            if constexpr (kUn) unc = data_row<VEC, NK_ST_NTN>(A.un, o, true);
+            if constexpr (kF0) f0c = data_row<VEC, NK_ST_NT>(A.F0, o, true);
+            if constexpr (kAx) ax = data_row<VEC>(A.aux, o, true);
+        }
+        for (int64_t j = y0; j < y1; ++j) {
             const int64_t o = j * nx + xc;
-            // raw row j+2 (rows up to ny are the ghost plane; y1 <= ny keeps j+2 <= ny+1 in range only
-            // when j+1 < y1, so clamp to row j+1 otherwise)
-            if (j + 1 < y1) {  // (the tile's last row needs no further row)
-                const int64_t r2 = j + 2;  // (ny: the upper ghost row)
-                const int64_t o2 = r2 * nx + xc;
-                rn = load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, o2, o2 + de, o2 + de2, edge_ok, edge_ok2);
-                if (ib_hi && r2 == ny) ib_patch<MODE, VEC>(rn, ib_hi, xc);
-                cn = load_ctr(o + nx);
-            }
-            // ---- cook row j+1 (its loads were issued one row ago)
-            const Field<VEC> fp = cook<MODE, VEC, SCH, kG, PER>(A, rc, act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
+            // ---- issue: raw row j+2 (rows up to ny are the ghost plane; y1 <= ny keeps j+2 <= ny+1
+            //      in range only when j+1 < y1, so clamp to row j+1 otherwise)
+            const int64_t r2 = (j + 1 < y1) ? j + 2 : j + 1;  // (ny: the upper ghost row)
+            const int64_t o2 = r2 * nx + xc;
+            const RawRow<MODE, VEC> rpp = (ib_hi && r2 == ny) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, o2, xc)
+                                                              : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, o2, o2 + de, o2 + de2);
+            Row<VEC> ucn{}, uncn{}, f0cn{}, axn{};
+            const int64_t o1 = (j + 1 < y1) ? o + nx : o;
+            if constexpr (kU) ucn = data_row<VEC>(A.u, o1, true);
+            if constexpr (kUn) uncn = data_row<VEC, NK_ST_NTN>(A.un, o1, true);
+            if constexpr (kF0) f0cn = data_row<VEC, NK_ST_NT>(A.F0, o1, true);
+            if constexpr (kAx) axn = data_row<VEC>(A.aux, o1, true);
+            // ---- cook row j+1 (its loads were issued one iteration ago)
+            const Field<VEC> fp = cook<MODE, VEC, SCH, kG, PER>(A, rp, act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
             Field<VEC> up{};
             LR un_{};
             if constexpr (kR) {
-                up = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res(rc), act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
+                up = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res(rp), act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
                 un_ = x_nbrs<PER>(uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
             }
             // ---- compute row j from registers
@@ -663,8 +638,8 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
                         const double ge = (k == VEC - 1) ? grgt : fc.g[k == VEC - 1 ? k : k + 1];
                         lsumg = lapk(A, fc.g[k], ge, gw, A.hx2, A.ihx2) + lapk(A, fc.g[k], fp.g[k], fm.g[k], A.hy2, A.ihy2);
                     }
-                    const double unk = kG ? fc.g[k] : cc.un.v[k];
-                    double f0 = cc.f0.v[k];
+                    const double unk = kG ? fc.g[k] : unc.v[k];
+                    double f0 = f0c.v[k];
                     if constexpr (kR) {  // F(u) at this point, as the residual kernel evaluates it
                         const double uw = (k == 0) ? un_.l : uc_.c[k == 0 ? 0 : k - 1];
                         const double ue = (k == VEC - 1) ? un_.r : uc_.c[k == VEC - 1 ? k : k + 1];
@@ -672,8 +647,8 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
                         const double lsu = lapk(A, ucc, ue, uw, A.hx2, A.ihx2) + lapk(A, ucc, up.c[k], um.c[k], A.hy2, A.ihy2);
                         f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unk, 0.0, SCH == 1 ? uc_.x[k] : ucc, lsumg);
                     }
-                    double r = point_value<KIND, MODE>(A, c, lsum, cc.u.v[k], unk, f0, SCH == 1 ? fc.x[k] : c, lsumg);
-                    acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[k] : cc.ax.v[k], acc);
+                    double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unk, f0, SCH == 1 ? fc.x[k] : c, lsumg);
+                    acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[k] : ax.v[k], acc);
                     val.v[k] = r;
                 }
                 store_row<VEC>(A.out, o, val);
@@ -684,21 +659,18 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
                     store_row<VEC, NK_ST_NT>(A.vout, o, vn);
                 }
             }
-            fm = fc;  // cooked values (no load in flight): plain moves
+            fm = fc;
             fc = fp;
             if constexpr (kR) {
                 um = uc_;
                 uc_ = up;
             }
-        };
-        int64_t j = y0;
-        for (; j + 1 < y1; j += 2) {
-            step(j, rB, rA, cB, cA);
-            __builtin_amdgcn_sched_barrier(0);  // keep each step's loads in its own half (the slots stay put)
-            step(j + 1, rA, rB, cA, cB);
-            __builtin_amdgcn_sched_barrier(0);
+            rp = rpp;
+            uc = ucn;
+            unc = uncn;
+            f0c = f0cn;
+            ax = axn;
         }
-        if (j < y1) step(j, rB, rA, cB, cA);
     }
     if constexpr (EPI != EPI_NONE) publish(acc, A.part, A.fin, sh);
 }
@@ -744,7 +716,7 @@ __global__ __launch_bounds__(64 * NW) void k_st2t(KArgs A0) {
     const bool lo_halo = wv == 0, hi_halo = wv == NW - 1 && y0 + NW <= ny;
     auto raw_of = [&](int64_t r) {
         const int64_t o = r * nx + xc;
-        return load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, o, o + de, o + de2, edge_ok, edge_ok2);
+        return load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, o, o + de, o + de2);
     };
     auto put = [&](int i, const RawRow<MODE, VEC>& r, bool eok, bool eok2, Field<VEC>* keep, Field<VEC>* keepu) {
         const Field<VEC> f = cook<MODE, VEC, SCH, kG, PER>(A, r, act, eok, eok2);
@@ -881,9 +853,9 @@ __global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
     if (z0 < nz) {
         const int64_t o0 = z0 * pl + oj;
         Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(A, load_raw<MODE, VEC, false, kG, PER>(A, o0 - pl, 0), act, false);  // plane -1: ghost
-        Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, load_raw<MODE, VEC, true, kG, PER>(A, o0, o0 + de, o0 + de2, edge_ok, edge_ok2), act,
+        Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, load_raw<MODE, VEC, true, kG, PER>(A, o0, o0 + de, o0 + de2), act,
                                                       edge_ok, edge_ok2);
-        RawRow<MODE, VEC> rp = load_raw<MODE, VEC, true, kG, PER>(A, o0 + pl, o0 + pl + de, o0 + pl + de2, edge_ok, edge_ok2);  // plane nz: ghost
+        RawRow<MODE, VEC> rp = load_raw<MODE, VEC, true, kG, PER>(A, o0 + pl, o0 + pl + de, o0 + pl + de2);  // plane nz: ghost
         RawRow<MODE, VEC> rn = load_raw<MODE, VEC, false, kG, PER>(A, o0 + dn, 0);
         RawRow<MODE, VEC> rs = load_raw<MODE, VEC, false, kG, PER>(A, o0 + ds, 0);
         Row<VEC> unc{}, f0c{}, ax{};
@@ -896,7 +868,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
             const bool more = k + 1 < z1;
             const int64_t o2 = more ? o + 2 * pl : o + pl;
             const int64_t o1 = more ? o + pl : o;
-            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2, edge_ok, edge_ok2);
+            const RawRow<MODE, VEC> rpp = load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2);
             const RawRow<MODE, VEC> rnn = load_raw<MODE, VEC, false, kG, PER>(A, o1 + dn, 0);
             const RawRow<MODE, VEC> rss = load_raw<MODE, VEC, false, kG, PER>(A, o1 + ds, 0);
             Row<VEC> uncn{}, f0cn{}, axn{};
@@ -982,8 +954,8 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const int nb = gridDim.x, b = blockIdx.x;
-    const int t = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;
     const int tpl = A.tiles_x * A.tiles_y;
+    const int t = tile_of(b, nb, tpl, (int)((A.nz + A.rows - 1) / A.rows), A.hx_lo, A.hx_hi, 0);
     const int tz = t / tpl, txy = t % tpl;
     const int ty = txy / A.tiles_x, tx = txy % A.tiles_x;
     const int64_t nx = A.nx, ny = A.ny, nz = A.nz, pl = nx * ny;
@@ -1037,7 +1009,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
         const int64_t o0 = z0 * pl + oj;
         const RawRow<MODE, VEC> rm0 =
             ib_lo ? load_raw_ib<MODE, VEC, kG>(A, ib_lo, o0 - pl, oj) : load_raw<MODE, VEC, false, kG, PER>(A, o0 - pl, 0);
-        const RawRow<MODE, VEC> rc0 = load_raw<MODE, VEC, true, kG, PER>(A, o0, o0 + de, o0 + de2, edge_ok, edge_ok2);
+        const RawRow<MODE, VEC> rc0 = load_raw<MODE, VEC, true, kG, PER>(A, o0, o0 + de, o0 + de2);
         Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(A, rm0, act, false);
         Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, rc0, act, edge_ok, edge_ok2);
         Field<VEC> um{}, uc_{};  // F0R: the u field of planes k-1, k
@@ -1046,7 +1018,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
             uc_ = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rc0), act, edge_ok, edge_ok2);
         }
         RawRow<MODE, VEC> rp = (ib_hi && z0 + 1 == nz) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, o0 + pl, oj)
-                                                       : load_raw<MODE, VEC, true, kG, PER>(A, o0 + pl, o0 + pl + de, o0 + pl + de2, edge_ok, edge_ok2);
+                                                       : load_raw<MODE, VEC, true, kG, PER>(A, o0 + pl, o0 + pl + de, o0 + pl + de2);
         RawRow<MODE, VEC> rn{}, rs{};
         if (ld_n) rn = load_raw<MODE, VEC, false, kG, PER>(A, o0 + dn, 0);
         if (ld_s) rs = load_raw<MODE, VEC, false, kG, PER>(A, o0 + ds, 0);
@@ -1070,7 +1042,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
             const int64_t o1 = more ? o + pl : o;
             const int64_t k2 = more ? k + 2 : k + 1;  // the plane o2 is in (nz: the upper ghost plane)
             const RawRow<MODE, VEC> rpp = (ib_hi && k2 == nz) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, o2, oj)
-                                                              : load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2, edge_ok, edge_ok2);
+                                                              : load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2);
             RawRow<MODE, VEC> rnn{}, rss{};
             if (ld_n) rnn = load_raw<MODE, VEC, false, kG, PER>(A, o1 + dn, 0);
             if (ld_s) rss = load_raw<MODE, VEC, false, kG, PER>(A, o1 + ds, 0);

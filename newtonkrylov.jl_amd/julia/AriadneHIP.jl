@@ -64,17 +64,26 @@ mutable struct HipVector <: AbstractVector{Float64}
     ctx::HipContext
     ptr::Ptr{Float64}
     grid::NTuple{3, Int}
+    gen::Int     # bumped by every write this shim makes (touch!)
+    f0of::Any    # set by a built-in residual F!(res, u, p): (u, u.gen, p) it was evaluated at; `nothing` once rewritten
     function HipVector(ctx::HipContext, grid::NTuple{3, Int})
         r = Ref{Ptr{Float64}}(C_NULL)
         p = geometry(grid)
         check(ccall((:nk_vec_alloc, libnkhip), Cint, (Ptr{Cvoid}, Ref{NkProblem}, Ref{Ptr{Float64}}), ctx.ptr, p, r),
               ctx, "nk_vec_alloc")
-        v = new(ctx, r[], grid)
+        v = new(ctx, r[], grid, 0, nothing)
         finalizer(x -> ccall((:nk_vec_free, libnkhip), Cint, (Ptr{Cvoid}, Ptr{Float64}), x.ctx.ptr, x.ptr), v)
     end
     # non-owning view of library-owned storage (e.g. the Krylov workspace's x)
-    HipVector(ctx::HipContext, ptr::Ptr{Float64}, grid::NTuple{3, Int}) = new(ctx, ptr, grid)
+    HipVector(ctx::HipContext, ptr::Ptr{Float64}, grid::NTuple{3, Int}) = new(ctx, ptr, grid, 0, nothing)
 end
+touch!(v::HipVector) = (v.gen += 1; v.f0of = nothing; v)
+# the state a residual was evaluated at: u and every device vector in p (u_n of the heat problems) by
+# identity and write generation, the scalars by value
+stampof(x::HipVector) = (objectid(x), x.gen)
+stampof(x::Tuple) = map(stampof, x)
+stampof(x) = x
+f0stamp(u::HipVector, p) = (stampof(u), stampof(p))
 Base.size(v::HipVector) = (prod(v.grid),)
 Base.similar(v::HipVector) = HipVector(v.ctx, v.grid)          # zero-filled, ghosts included
 Base.zero(v::HipVector) = HipVector(v.ctx, v.grid)
@@ -99,7 +108,7 @@ end
 function Base.Broadcast.materialize!(u::HipVector, bc::Base.Broadcast.Broadcasted)
     if bc.f === (-) && bc.args[1] === u && bc.args[2] isa Base.Broadcast.Broadcasted && bc.args[2].f === (*)
         s, d = bc.args[2].args
-        return kaxpy!(length(u), -Float64(s), d::HipVector, u)
+        return kaxpy!(length(u), -Float64(s), d::HipVector, u)  # (kaxpy! touches u)
     end
     error("unsupported broadcast on HipVector: $(bc.f)")
 end
@@ -119,23 +128,23 @@ function knorm(n::Integer, x::HipVector)
     return r[]
 end
 kscal!(n::Integer, s::Float64, x::HipVector) =
-    (check(ccall((:nk_scal, libnkhip), Cint, (VP, Int64, Float64, Ptr{Float64}), x.ctx.ptr, n, s, x.ptr), x.ctx, "kscal!"); x)
+    (check(ccall((:nk_scal, libnkhip), Cint, (VP, Int64, Float64, Ptr{Float64}), x.ctx.ptr, n, s, x.ptr), x.ctx, "kscal!"); touch!(x))
 kaxpy!(n::Integer, s::Float64, x::HipVector, y::HipVector) =
     (check(ccall((:nk_axpy, libnkhip), Cint, (VP, Int64, Float64, Ptr{Float64}, Ptr{Float64}), y.ctx.ptr, n, s, x.ptr, y.ptr),
-           y.ctx, "kaxpy!"); y)
+           y.ctx, "kaxpy!"); touch!(y))
 kaxpby!(n::Integer, s::Float64, x::HipVector, t::Float64, y::HipVector) =
     (check(ccall((:nk_axpby, libnkhip), Cint, (VP, Int64, Float64, Ptr{Float64}, Float64, Ptr{Float64}),
-                 y.ctx.ptr, n, s, x.ptr, t, y.ptr), y.ctx, "kaxpby!"); y)
+                 y.ctx.ptr, n, s, x.ptr, t, y.ptr), y.ctx, "kaxpby!"); touch!(y))
 kcopy!(n::Integer, y::HipVector, x::HipVector) =
-    (check(ccall((:nk_copy, libnkhip), Cint, (VP, Int64, Ptr{Float64}, Ptr{Float64}), y.ctx.ptr, n, y.ptr, x.ptr), y.ctx, "kcopy!"); y)
+    (check(ccall((:nk_copy, libnkhip), Cint, (VP, Int64, Ptr{Float64}, Ptr{Float64}), y.ctx.ptr, n, y.ptr, x.ptr), y.ctx, "kcopy!"); touch!(y))
 kfill!(x::HipVector, v::Float64) =
-    (check(ccall((:nk_fill, libnkhip), Cint, (VP, Int64, Ptr{Float64}, Float64), x.ctx.ptr, length(x), x.ptr, v), x.ctx, "kfill!"); x)
+    (check(ccall((:nk_fill, libnkhip), Cint, (VP, Int64, Ptr{Float64}, Float64), x.ctx.ptr, length(x), x.ptr, v), x.ctx, "kfill!"); touch!(x))
 kdivcopy!(n::Integer, y::HipVector, x::HipVector, s::Float64) =
     (check(ccall((:nk_divcopy, libnkhip), Cint, (VP, Int64, Ptr{Float64}, Ptr{Float64}, Float64), y.ctx.ptr, n, y.ptr, x.ptr, s),
-           y.ctx, "kdivcopy!"); y)
+           y.ctx, "kdivcopy!"); touch!(y))
 kref!(n::Integer, x::HipVector, y::HipVector, c::Float64, s::Float64) =
     (check(ccall((:nk_ref, libnkhip), Cint, (VP, Int64, Ptr{Float64}, Ptr{Float64}, Float64, Float64),
-                 x.ctx.ptr, n, x.ptr, y.ptr, c, s), x.ctx, "kref!"); (x, y))
+                 x.ctx.ptr, n, x.ptr, y.ptr, c, s), x.ctx, "kref!"); (touch!(x), touch!(y)))
 
 # --------------------------------------------------------------------------- residuals (F!) and mul!
 """A residual `F!(res, u, p)` with a hand-written HIP stencil (same `p` tuples as the examples).
@@ -207,6 +216,7 @@ end
 function (F::HipUserResidual)(res::HipVector, u::HipVector, p)
     check(ccall((:nk_residual, libnkhip), Cint, (VP, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}),
                 u.ctx.ptr, problem(F, u, p), res.ptr, u.ptr), u.ctx, "F!")
+    touch!(res)
     return nothing
 end
 const AnyHipResidual = Union{HipResidual, HipUserResidual}
@@ -214,6 +224,7 @@ const AnyHipResidual = Union{HipResidual, HipUserResidual}
 function (F::HipResidual)(res::HipVector, u::HipVector, p)
     check(ccall((:nk_residual, libnkhip), Cint, (VP, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}),
                 u.ctx.ptr, problem(F, u, p), res.ptr, u.ptr), u.ctx, "F!")
+    touch!(res).f0of = f0stamp(u, p)  # res holds F(u, p) exactly as the device residual kernel computes it
     return nothing
 end
 
@@ -225,6 +236,7 @@ function mul!(out::HipVector, J::HipJacobian, v::HipVector)
     F0 = jvmode(J) == NK_JV_FD ? J.res.ptr : Ptr{Float64}(C_NULL)
     check(ccall((:nk_jv, libnkhip), Cint, (VP, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int32, Float64),
                 out.ctx.ptr, problem(J.f, J.u, J.p), out.ptr, J.u.ptr, v.ptr, F0, jvmode(J), 0.0), out.ctx, "mul!")
+    touch!(out)
     return nothing
 end
 
@@ -233,6 +245,7 @@ function mul!(out::HipVector, J′::HipJacobianT, v::HipVector)
     J = parent(J′)
     check(ccall((:nk_jtv, libnkhip), Cint, (VP, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
                 out.ctx.ptr, problem(J.f, J.u, J.p), out.ptr, J.u.ptr, v.ptr), out.ctx, "mul!(out, Jᵀ, v)")
+    touch!(out)
     return nothing
 end
 
@@ -256,6 +269,7 @@ function mul!(Out::HipMatrix, J::HipJacobian, V::HipMatrix)
                     (VP, Ref{NkProblem}, Int32, Ptr{Ptr{Float64}}, Ptr{Float64}, Ptr{Ptr{Float64}}, Ptr{Float64}, Int32, Float64),
                     J.u.ctx.ptr, problem(J.f, J.u, J.p), length(o), o, J.u.ptr, v, F0, jvmode(J), 0.0), J.u.ctx, "mul!(Out, J, V)")
     end
+    foreach(touch!, Out.cols)
     return nothing
 end
 function mul!(Out::HipMatrix, J′::HipJacobianT, V::HipMatrix)
@@ -267,6 +281,7 @@ function mul!(Out::HipMatrix, J′::HipJacobianT, V::HipMatrix)
                     (VP, Ref{NkProblem}, Int32, Ptr{Ptr{Float64}}, Ptr{Float64}, Ptr{Ptr{Float64}}),
                     J.u.ctx.ptr, problem(J.f, J.u, J.p), length(o), o, J.u.ptr, v), J.u.ctx, "mul!(Out, Jᵀ, V)")
     end
+    foreach(touch!, Out.cols)
     return nothing
 end
 
@@ -412,15 +427,19 @@ function Krylov.krylov_solve!(ws::HipKrylovWorkspace, J::HipJacobian, b::HipVect
     GC.@preserve Nc N Mc M begin   # the raw nk_precond* (and what they point to) stay rooted through the call
         Np = N === nothing ? Ptr{Cvoid}(C_NULL) : Ptr{Cvoid}(Base.unsafe_convert(Ptr{NkPrecond}, Nc))
         Mp = M === nothing ? Ptr{Cvoid}(C_NULL) : Ptr{Cvoid}(Base.unsafe_convert(Ptr{NkPrecond}, Mc))
-        # Ariadne calls krylov_solve! right after F!(res, u, p): J.res is F(u) from the device residual
-        # (and the FD operator's F(u) is J.res by definition), so the 2D FD stencils may recompute it
+        # The FD stencils may recompute F(u) from the u rows they load instead of reading J.res -- only when
+        # J.res provably IS that: written by the built-in residual at this very u and p, untouched since
+        # (Ariadne's loop: F!(res, u, p) just ran).  A J whose res was rewritten, or whose u / u_n changed
+        # after F!, reads J.res as the FD operator's F0 (src/Ariadne.jl:48-57 semantics, mul!'s result)
+        f0r = J.f isa HipResidual && J.res.f0of !== nothing && J.res.f0of == f0stamp(J.u, J.p)
         opts = NkKrylovOpts(restart, reorthogonalization, itmax, jvmode(J), atol, rtol, 0.0, 0.0, C_NULL, Np, Mp,
-                            Int32(J.f isa HipResidual ? 1 : 0))
+                            Int32(f0r ? 1 : 0))
         check(ccall((:nk_krylov_solve, libnkhip), Cint,
                     (Ptr{Cvoid}, Ref{NkProblem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ref{NkKrylovOpts}, Ref{NkKrylovStats},
                      Ptr{Float64}, Int64, Ref{Int64}),
                     ws.ptr, problem(J.f, J.u, J.p), J.u.ptr, F0, b.ptr, opts, st, C_NULL, 0, hl), ws.ctx, "krylov_solve!")
     end
+    touch!(ws.x)
     ws.stats.niter = st[].niter
     ws.stats.solved = st[].solved != 0
     return ws

@@ -24,6 +24,7 @@ ap.add_argument("--out", required=True)
 ap.add_argument("--nx", type=int, default=48)
 ap.add_argument("--ny", type=int, default=40)
 ap.add_argument("--jv", default="exact")
+ap.add_argument("--tol-rel", type=float, default=1e-9, help="Newton tol_rel of the Bratu solve")
 ap.add_argument("--krylov-itmax", type=int, default=0,
                 help="> 0: instead of the Newton solve, one restarted GMRES(10) solve J x = F(u0) with this fixed "
                      "budget (atol = rtol = 0); rank 0 saves x and the residual history")
@@ -110,7 +111,7 @@ v_glob = np.random.default_rng(7).standard_normal((ny, nx))
 if args.problem == "bratu":
     u0 = np.sin(np.pi * ys)[:, None] * np.sin(np.pi * xs)[None, :]
     F_, p = ah.bratu2d_, (hx, hy, lam)
-    kw = dict(memory=10, tol_rel=1e-9, krylov_kwargs=dict(restart=True))
+    kw = dict(memory=10, tol_rel=args.tol_rel, krylov_kwargs=dict(restart=True))
 else:
     rng = np.random.default_rng(5)
     un_glob = rng.standard_normal((ny, nx))

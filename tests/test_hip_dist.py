@@ -16,6 +16,8 @@ import signal
 import socket
 import subprocess
 import sys
+import tempfile
+import time
 
 import numpy as np
 import pytest
@@ -76,16 +78,8 @@ def test_forced_one_rank_mailbox_is_bitwise(monkeypatch):
 def test_mailbox_two_ranks_one_gpu(tmp_path):
     """Two processes on one GPU reduce through each other's mailboxes (IPC, no RCCL)."""
     out = str(tmp_path / "mb")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(ROOT, "tests", "mailbox_worker.py"), "--out", out]
-    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
-    try:
-        log, _ = proc.communicate(timeout=180)
-    except subprocess.TimeoutExpired:
-        os.killpg(proc.pid, signal.SIGKILL)
-        pytest.fail("mailbox worker timed out")
-    assert proc.returncode == 0, log.decode()[-3000:]
+    rc, log = run_ranks(2, [os.path.join(ROOT, "tests", "mailbox_worker.py"), "--out", out], dict(os.environ))
+    assert rc == 0, log[-3000:]
     meta = json.load(open(out + ".json"))
     n = meta["n"]
     y = np.arange(n, dtype=np.float64) % 7
@@ -94,11 +88,78 @@ def test_mailbox_two_ranks_one_gpu(tmp_path):
         assert abs(nrm2 - 2 * (y * y).sum()) <= 1e-9 * nrm2  # sqrt then square: a few ulp
 
 
+def gpu_holders():
+    """Other processes that hold the GPU open (/dev/kfd): ranks of a finished multi-rank test linger
+    for a moment while the driver tears their contexts down, and the GPU box allows 16 at once."""
+    me, out = os.getpid(), []
+    for pid in os.listdir("/proc"):
+        if not pid.isdigit() or int(pid) == me:
+            continue
+        try:
+            if any(os.readlink(f"/proc/{pid}/fd/{fd}") == "/dev/kfd" for fd in os.listdir(f"/proc/{pid}/fd")):
+                out.append(int(pid))
+        except OSError:
+            continue
+    return out
+
+
+def wait_gpu_released(timeout=60.0):
+    deadline = time.time() + timeout
+    while gpu_holders() and time.time() < deadline:
+        time.sleep(0.5)
+
+
+def run_ranks(world, args, env, timeout=180):
+    """Start `world` ranks of a worker script directly (no torch.distributed.run agent: one GPU process
+    fewer), after the previous test's ranks have released the GPU; a rank that fails takes the others
+    down at once.  Returns (rc, log)."""
+    wait_gpu_released()
+    port = str(free_port())
+    logs = [tempfile.TemporaryFile() for _ in range(world)]
+    procs = []
+    for r in range(world):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable] + args, env=e, stdout=logs[r], stderr=subprocess.STDOUT,
+                                      start_new_session=True))
+
+    def kill_all():
+        for q in procs:
+            if q.poll() is None:
+                try:
+                    os.killpg(q.pid, signal.SIGKILL)
+                except OSError:
+                    pass
+        for q in procs:
+            q.wait()
+
+    end, rc = time.time() + timeout, 0
+    while any(q.poll() is None for q in procs):
+        failed = [q.returncode for q in procs if q.poll() is not None and q.returncode != 0]
+        if failed or time.time() > end:
+            rc = failed[0] if failed else -9
+            kill_all()
+            break
+        time.sleep(0.2)
+    rc = rc or next((q.returncode for q in procs if q.returncode), 0)
+    text = []
+    for r, f in enumerate(logs):
+        f.seek(0)
+        text.append(f"--- rank {r} (rc {procs[r].returncode})\n" + f.read().decode(errors="replace")[-4000:])
+        f.close()
+    if rc == -9 and time.time() > end:
+        pytest.fail(f"{world}-rank worker timed out\n" + "\n".join(text)[-3000:])
+    return rc, "\n".join(text)
+
+
 def worker_env(world, **extra):
     """One device per rank when there are enough; else every rank on device 0 (NK_WORKER_SHARED_DEVICE)."""
     env = dict(os.environ, **extra)
     if ah.device_count() < world:
         env["NK_WORKER_SHARED_DEVICE"] = "1"
+        # one hardware queue per rank process: 8 ranks x the default 4 would oversubscribe the GPU's
+        # queues, which then time-slice -- and every cross-rank reduction waits for a queue to come round
+        env["GPU_MAX_HW_QUEUES"] = "1"
     else:
         env.pop("NK_WORKER_SHARED_DEVICE", None)
     return env
@@ -124,17 +185,13 @@ def test_slabs_match_oracle(tmp_path, world, transport):
     runs ghost planes and reductions through the IPC-mapped peer regions only (no RCCL), so all
     ranks can share the one GPU of the test box; transport=rccl needs one GPU per rank."""
     out = str(tmp_path / "dist")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", transport]
     env = worker_env(world)
-    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
-    try:
-        log, _ = proc.communicate(timeout=180)
-    except subprocess.TimeoutExpired:
-        os.killpg(proc.pid, signal.SIGKILL)
-        pytest.fail("distributed worker timed out")
-    assert proc.returncode == 0, log.decode()[-3000:]
+    # 8 ranks on the test box's one GPU: a looser Newton tolerance (fewer cross-rank reductions); the
+    # oracle solves to the same one
+    tol = 1e-9 if world <= 4 else 1e-6
+    rc, log = run_ranks(world, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", transport,
+                                "--tol-rel", str(tol)], env)
+    assert rc == 0, log[-3000:]
     meta = json.load(open(out + ".json"))
     check_meta(meta, world)
     d = np.load(out + ".npz")
@@ -145,7 +202,7 @@ def test_slabs_match_oracle(tmp_path, world, transport):
     ref = oc.jv_exact(P, u0, d["v"])
     assert np.max(np.abs(d["jv"] - ref)) <= 1e-12 * np.max(np.abs(ref))  # halo rows came from the neighbours
     assert abs(meta["dot"] - float(np.sum(u0 * d["v"]))) <= 1e-12 * np.sqrt(u0.size)
-    uo, so = oc.newton_krylov(P, u0, memory=10, restart=True, tol_rel=1e-9)
+    uo, so = oc.newton_krylov(P, u0, memory=10, restart=True, tol_rel=tol)
     assert meta["solved"] and so["solved"]
     assert (meta["outer"], meta["inner"]) == (so["outer_iterations"], so["inner_iterations"])
     assert np.max(np.abs(d["u"] - uo)) <= 1e-8 * np.max(np.abs(uo))
@@ -159,18 +216,10 @@ def test_periodic_trapezoid_ring_matches_oracle(tmp_path, world, transport):
     ranks both neighbours are the same rank).  Residual and exact JVP bit-identical to the oracle on
     the whole grid; one implicit step with equal Newton/Krylov counts."""
     out = str(tmp_path / "ring")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", transport,
-           "--problem", "heat_periodic"]
     env = worker_env(world)
-    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
-    try:
-        log, _ = proc.communicate(timeout=180)
-    except subprocess.TimeoutExpired:
-        os.killpg(proc.pid, signal.SIGKILL)
-        pytest.fail("distributed worker timed out")
-    assert proc.returncode == 0, log.decode()[-3000:]
+    rc, log = run_ranks(world, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", transport,
+                                "--problem", "heat_periodic"], env)
+    assert rc == 0, log[-3000:]
     meta = json.load(open(out + ".json"))
     check_meta(meta, world)
     d = np.load(out + ".npz")
@@ -192,18 +241,10 @@ def test_resident_sweep_two_ranks_one_gpu(tmp_path):
     the GPU) so that both grids are resident together; 1024^2 global (a 1024 x 512 slab per rank: all of q on chip, the
     V_{k+1} hand-over to the next Jv included).  20 restarted GMRES(10) steps against the oracle."""
     out = str(tmp_path / "dist")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
-           "--nx", "1024", "--ny", "1024", "--krylov-itmax", "20"]
     env = worker_env(2, NK_RES_SHARED="1")
-    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
-    try:
-        log, _ = proc.communicate(timeout=180)
-    except subprocess.TimeoutExpired:
-        os.killpg(proc.pid, signal.SIGKILL)
-        pytest.fail("distributed worker timed out")
-    assert proc.returncode == 0, log.decode()[-3000:]
+    rc, log = run_ranks(2, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
+                            "--nx", "1024", "--ny", "1024", "--krylov-itmax", "20"], env)
+    assert rc == 0, log[-3000:]
     meta = json.load(open(out + ".json"))
     d = np.load(out + ".npz")
     P = oc.bratu2d(1024, 1024)
@@ -224,18 +265,9 @@ def test_heat3d_midpoint_zslabs_match_oracle(tmp_path, world):
     Residual, exact and FD JVP bit-identical to the oracle on the whole grid; one implicit step
     with the FD operator: equal Newton / Krylov counts."""
     out = str(tmp_path / "h3")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
-           "--problem", "heat3d", "--nx", "40", "--ny", "20"]
-    proc = subprocess.Popen(cmd, env=worker_env(world), stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
-                            start_new_session=True)
-    try:
-        log, _ = proc.communicate(timeout=180)
-    except subprocess.TimeoutExpired:
-        os.killpg(proc.pid, signal.SIGKILL)
-        pytest.fail("distributed worker timed out")
-    assert proc.returncode == 0, log.decode()[-3000:]
+    rc, log = run_ranks(world, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
+                                "--problem", "heat3d", "--nx", "40", "--ny", "20"], worker_env(world))
+    assert rc == 0, log[-3000:]
     meta = json.load(open(out + ".json"))
     assert meta["mailbox"]
     d = np.load(out + ".npz")
@@ -261,18 +293,10 @@ def test_dead_rank_reduction_errors_in_bounded_time(tmp_path, world):
     the mailbox spin limit -- never a hang -- and the path report must show the sticky mailbox error."""
     out = str(tmp_path / "fault")
     fault = world - 1
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
-           "--fault-rank", str(fault)]
     env = worker_env(world, NK_MB_SPIN_LIMIT=str(1 << 18))
-    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
-    try:
-        log, _ = proc.communicate(timeout=180)
-    except subprocess.TimeoutExpired:
-        os.killpg(proc.pid, signal.SIGKILL)
-        pytest.fail("a rank hung on a dead peer")
-    assert proc.returncode == 0, log.decode()[-3000:]
+    rc, log = run_ranks(world, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
+                                "--fault-rank", str(fault)], env)
+    assert rc == 0, log[-3000:]
     meta = json.load(open(out + ".json"))
     P = oc.bratu2d(48, 40)
     v = np.random.default_rng(7).standard_normal((40, 48))
@@ -292,6 +316,7 @@ def test_bench_exits_nonzero_on_a_stuck_rank(tmp_path):
     ends with a non-zero status in bounded time instead of hanging."""
     env = worker_env(2, NK_BENCH_FAULT_RANK="1", NK_MB_SPIN_LIMIT=str(1 << 18))
     env.pop("WORLD_SIZE", None)
+    wait_gpu_released()
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--transport", "mailbox", "--side", "256",
            "--steps", "2", "--warmup", "1", "--itmax", "30", "--no-cpu-baseline"]
     proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
@@ -311,6 +336,7 @@ def test_bench_reports_every_ranks_path(tmp_path):
     world = 8
     env = worker_env(world)
     env.pop("WORLD_SIZE", None)
+    wait_gpu_released()
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--transport", "mailbox",
            "--side", "256", "--steps", "2", "--warmup", "1", "--itmax", "30", "--no-cpu-baseline"]
     proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, start_new_session=True)
