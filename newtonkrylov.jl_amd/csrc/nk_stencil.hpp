@@ -32,6 +32,7 @@ struct KArgs {
     int nw;              // 3D: rows (waves) per tile
     int lds3;            // 3D: y-neighbour rows through LDS (k_st3l) instead of per-wave loads (k_st3d)
     int lin;             // tiles in dispatch (= address) order instead of XCD-contiguous bands
+    int zalt;            // 3D: z-chunks of one tile column dispatched together, odd chunks marching down
     int tile2;           // kbench: 2D one-shot LDS tiles of tile2 rows (k_st2t) instead of the march
     int f0r;             // 2D FD: F0 = F(u) recomputed from the u rows already loaded (k_st2d<..., F0R>)
     // ghost planes of v through the peers' inboxes inside this launch (halo_tile_exchange): the rank
@@ -492,13 +493,64 @@ __device__ __forceinline__ XEdge x_edge(int lane, bool act, int64_t x0, int64_t 
 // Dispatched last (in address order), a lower tile would wait on a neighbour whose upper tiles start
 // only when most of ITS launch is done -- a chain along the ranks whenever a launch has more tiles than
 // the GPU holds at once.  `band` = tiles per plane / row band, `nband` = bands.
+// XCD band of dispatch index i of n: block i lands on XCD i % 8 and takes the (i / 8)-th tile of that
+// XCD's contiguous band (the last n % 8 blocks in dispatch order)
+__device__ __forceinline__ int xcd_band(int i, int n) {
+    const int n8 = n & ~7;
+    return i < n8 ? (i & 7) * (n8 >> 3) + (i >> 3) : i;
+}
 __device__ __forceinline__ int tile_of(int b, int nb, int band, int nband, int lo, int hi, int lin) {
-    auto xcd = [lin](int i, int n) { return ((n & 7) == 0 && !lin) ? (i & 7) * (n >> 3) + (i >> 3) : i; };
+    auto xcd = [lin](int i, int n) { return lin ? i : xcd_band(i, n); };
     const int nl = lo ? band : 0, nh = (hi && nband > 1) ? band : 0;
     if (nl + nh == 0) return xcd(b, nb);
     if (b < nl) return b;
     if (b < nl + nh) return (nband - 1) * band + (b - nl);
     return xcd(b - nl - nh, nb - nl - nh) + nl;
+}
+// 3D block -> (z-chunk tz, tile txy of the plane).  zcol: an XCD's band holds whole tile columns -- all
+// z-chunks of one column at consecutive band positions, the columns in y order -- so the chunks of a
+// column run at the same time on one L2.  With odd chunks marching downwards (k_st3l, A.zalt) every
+// chunk boundary is then read by both of its chunks at the same step (both at their start or both at
+// their end), and the z-halo planes come from L2 instead of a second trip to memory; y-adjacent
+// columns sit next to each other in the band, so the y-halo rows stay shared as well.  The slab-end
+// chunks of the in-launch ghost-plane exchange still come first (tile_of).
+__device__ __forceinline__ void tile3_of(int b, int nb, int tiles_x, int tiles_y, int nzc, int lo, int hi, int zcol,
+                                         int& tz, int& txy) {
+    const int tpl = tiles_x * tiles_y;
+    if (zcol == 0 || zcol == 2) {  // plane-major (2: with the odd chunks marching down)
+        const int t = tile_of(b, nb, tpl, nzc, lo, hi, 0);
+        tz = t / tpl;
+        txy = t % tpl;
+        return;
+    }
+    const int nl = lo ? tpl : 0, nh = (hi && nzc > 1) ? tpl : 0;
+    if (b < nl) {
+        tz = 0;
+        txy = b;
+        return;
+    }
+    if (b < nl + nh) {
+        tz = nzc - 1;
+        txy = b - nl;
+        return;
+    }
+    const int zl = nl ? 1 : 0, nzi = nzc - zl - (nh ? 1 : 0);  // > 0 here
+    const int L = xcd_band(b - nl - nh, nb - nl - nh);
+    if (zcol == 3) {  // pairs of chunks (2m, 2m + 1) of one tile at consecutive band positions, plane-major otherwise
+        const int full = nzi / 2 * 2 * tpl;  // band positions of the full pairs
+        if (L >= full) {  // an odd chunk count: the last chunk has no partner
+            tz = zl + nzi - 1;
+            txy = L - full;
+            return;
+        }
+        const int pr = L >> 1;
+        tz = zl + 2 * (pr / tpl) + (L & 1);
+        txy = pr % tpl;
+        return;
+    }
+    tz = zl + L % nzi;
+    const int col = L / nzi;
+    txy = (col % tiles_y) * tiles_x + col / tiles_y;
 }
 
 // west / east neighbours of the VEC points of a lane: lane shuffles, the wave-edge lanes' edge values
@@ -954,9 +1006,8 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const int nb = gridDim.x, b = blockIdx.x;
-    const int tpl = A.tiles_x * A.tiles_y;
-    const int t = tile_of(b, nb, tpl, (int)((A.nz + A.rows - 1) / A.rows), A.hx_lo, A.hx_hi, 0);
-    const int tz = t / tpl, txy = t % tpl;
+    int tz, txy;
+    tile3_of(b, nb, A.tiles_x, A.tiles_y, (int)((A.nz + A.rows - 1) / A.rows), A.hx_lo, A.hx_hi, A.zalt, tz, txy);
     const int ty = txy / A.tiles_x, tx = txy % A.tiles_x;
     const int64_t nx = A.nx, ny = A.ny, nz = A.nz, pl = nx * ny;
     const int64_t x0 = (int64_t)tx * (64 * VEC) + (int64_t)lane * VEC;
@@ -967,16 +1018,16 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
     const bool lds_n = wv + 1 < NW && j + 1 < ny;
     const bool lds_s = wv >= 1;
     bool has_n, has_s;
-    int64_t dn, ds;
+    int64_t dn_, ds;
     if constexpr (PER) {
         has_n = act;
         has_s = act;
-        dn = !act ? 0 : (j + 1 < ny ? nx : -(ny - 1) * nx);
+        dn_ = !act ? 0 : (j + 1 < ny ? nx : -(ny - 1) * nx);
         ds = !act ? 0 : (j >= 1 ? -nx : (ny - 1) * nx);
     } else {
         has_n = act && j + 1 < ny;
         has_s = act && j >= 1;
-        dn = has_n ? nx : 0;
+        dn_ = has_n ? nx : 0;
         ds = has_s ? -nx : 0;
     }
     const bool ld_n = !lds_n && has_n, ld_s = !lds_s && has_s;  // wave-uniform
@@ -985,6 +1036,11 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
     const bool edge_ok = xe.ok, edge_ok2 = xe.ok2;
     const int64_t z0 = (int64_t)tz * A.rows;
     const int64_t z1 = z0 + A.rows < nz ? z0 + A.rows : nz;
+    // march direction: odd chunks (zalt) from z1 - 1 down to z0 -- fm / fp are then the planes above /
+    // below, and the z-Laplacian takes them in the reference's order ((p - 2c) + m) all the same
+    const bool dn = A.zalt && (tz & 1);
+    const int64_t st = dn ? -pl : pl, dz = dn ? -1 : 1;
+    const int64_t zs = dn ? z1 - 1 : z0;
     constexpr bool kUn = SCH == 0 && MODE != MODE_JEXACT;
     constexpr bool kF0 = MODE == MODE_JFD && !kR;
     constexpr bool kAx = EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID;
@@ -1005,10 +1061,18 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
         }
     }
     double acc = 0.0;
+    // a plane ahead of the march (plane kk at offset o): the neighbour's patch from the inbox for a
+    // ghost plane fetched in this launch, else memory
+    auto ahead = [&](int64_t kk, int64_t o) {
+        const uint64_t* ib = (ib_hi && kk == nz) ? ib_hi : ((ib_lo && kk == -1) ? ib_lo : nullptr);
+        return ib ? load_raw_ib<MODE, VEC, kG>(A, ib, o, oj) : load_raw<MODE, VEC, true, kG, PER>(A, o, o + de, o + de2);
+    };
     if (z0 < nz) {
-        const int64_t o0 = z0 * pl + oj;
+        const int64_t o0 = zs * pl + oj;
+        const int64_t kb = zs - dz;  // the plane behind the first
+        const uint64_t* ibb = (ib_lo && kb == -1) ? ib_lo : ((ib_hi && kb == nz) ? ib_hi : nullptr);
         const RawRow<MODE, VEC> rm0 =
-            ib_lo ? load_raw_ib<MODE, VEC, kG>(A, ib_lo, o0 - pl, oj) : load_raw<MODE, VEC, false, kG, PER>(A, o0 - pl, 0);
+            ibb ? load_raw_ib<MODE, VEC, kG>(A, ibb, o0 - st, oj) : load_raw<MODE, VEC, false, kG, PER>(A, o0 - st, 0);
         const RawRow<MODE, VEC> rc0 = load_raw<MODE, VEC, true, kG, PER>(A, o0, o0 + de, o0 + de2);
         Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(A, rm0, act, false);
         Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, rc0, act, edge_ok, edge_ok2);
@@ -1017,18 +1081,19 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
             um = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rm0), act, false);
             uc_ = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rc0), act, edge_ok, edge_ok2);
         }
-        RawRow<MODE, VEC> rp = (ib_hi && z0 + 1 == nz) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, o0 + pl, oj)
-                                                       : load_raw<MODE, VEC, true, kG, PER>(A, o0 + pl, o0 + pl + de, o0 + pl + de2);
+        RawRow<MODE, VEC> rp = ahead(zs + dz, o0 + st);
         RawRow<MODE, VEC> rn{}, rs{};
-        if (ld_n) rn = load_raw<MODE, VEC, false, kG, PER>(A, o0 + dn, 0);
+        if (ld_n) rn = load_raw<MODE, VEC, false, kG, PER>(A, o0 + dn_, 0);
         if (ld_s) rs = load_raw<MODE, VEC, false, kG, PER>(A, o0 + ds, 0);
         Row<VEC> unc{}, f0c{}, ax{};
         if constexpr (kUn) unc = data_row<VEC, NK_ST_NTN>(A.un, o0, true);
         if constexpr (kF0) f0c = data_row<VEC, NK_ST_NT>(A.F0, o0, true);
         if constexpr (kAx) ax = data_row<VEC>(A.aux, o0, true);
-        for (int64_t k = z0; k < z1; ++k) {
+        const int cnt = (int)(z1 - z0);
+        for (int it = 0; it < cnt; ++it) {
+            const int64_t k = zs + it * dz;
             const int64_t o = k * pl + oj;
-            const int par = (int)(k & 1);
+            const int par = it & 1;
             // ---- publish this wave's cooked centre row of plane k for its y-neighbours
 #pragma unroll
             for (int q = 0; q < VEC; ++q) {
@@ -1037,14 +1102,13 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
                 if constexpr (kR) lyu[par][kR ? wv : 0][kR ? lane * VEC + q : 0] = uc_.c[q];
             }
             // ---- issue: centre row of plane k+2, halo rows and centre data of plane k+1
-            const bool more = k + 1 < z1;
-            const int64_t o2 = more ? o + 2 * pl : o + pl;
-            const int64_t o1 = more ? o + pl : o;
-            const int64_t k2 = more ? k + 2 : k + 1;  // the plane o2 is in (nz: the upper ghost plane)
-            const RawRow<MODE, VEC> rpp = (ib_hi && k2 == nz) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, o2, oj)
-                                                              : load_raw<MODE, VEC, true, kG, PER>(A, o2, o2 + de, o2 + de2);
+            const bool more = it + 1 < cnt;
+            const int64_t o2 = more ? o + 2 * st : o + st;
+            const int64_t o1 = more ? o + st : o;
+            const int64_t k2 = more ? k + 2 * dz : k + dz;  // the plane o2 is in (-1 / nz: a ghost plane)
+            const RawRow<MODE, VEC> rpp = ahead(k2, o2);
             RawRow<MODE, VEC> rnn{}, rss{};
-            if (ld_n) rnn = load_raw<MODE, VEC, false, kG, PER>(A, o1 + dn, 0);
+            if (ld_n) rnn = load_raw<MODE, VEC, false, kG, PER>(A, o1 + dn_, 0);
             if (ld_s) rss = load_raw<MODE, VEC, false, kG, PER>(A, o1 + ds, 0);
             Row<VEC> uncn{}, f0cn{}, axn{};
             if constexpr (kUn) uncn = data_row<VEC, NK_ST_NTN>(A.un, o1, true);
@@ -1105,14 +1169,14 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
                     const double e = (q == VEC - 1) ? rgt : fc.c[q == VEC - 1 ? q : q + 1];
                     const double c = fc.c[q];
                     const double lsum = (lapk(A, c, e, w, A.hx2, A.ihx2) + lapk(A, c, cn[q], cs[q], A.hy2, A.ihy2)) +
-                                        lapk(A, c, fp.c[q], fm.c[q], A.hz2, A.ihz2);
+                                        lapk(A, c, dn ? fm.c[q] : fp.c[q], dn ? fp.c[q] : fm.c[q], A.hz2, A.ihz2);
                     double lsumg = 0.0;
                     if constexpr (SCH == 2 && kG) {
                         const double g = fc.g[q];
                         const double gw = (q == 0) ? glft : fc.g[q == 0 ? 0 : q - 1];
                         const double ge = (q == VEC - 1) ? grgt : fc.g[q == VEC - 1 ? q : q + 1];
                         lsumg = (lapk(A, g, ge, gw, A.hx2, A.ihx2) + lapk(A, g, gn[q], gs[q], A.hy2, A.ihy2)) +
-                                lapk(A, g, fp.g[q], fm.g[q], A.hz2, A.ihz2);
+                                lapk(A, g, dn ? fm.g[q] : fp.g[q], dn ? fp.g[q] : fm.g[q], A.hz2, A.ihz2);
                     }
                     const double unq = kG ? fc.g[q] : unc.v[q];
                     double f0 = f0c.v[q];
@@ -1121,7 +1185,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
                         const double ue = (q == VEC - 1) ? xu.r : uc_.c[q == VEC - 1 ? q : q + 1];
                         const double ucc = uc_.c[q];
                         const double lsu = (lapk(A, ucc, ue, uw, A.hx2, A.ihx2) + lapk(A, ucc, cnu[q], csu[q], A.hy2, A.ihy2)) +
-                                           lapk(A, ucc, up.c[q], um.c[q], A.hz2, A.ihz2);
+                                           lapk(A, ucc, dn ? um.c[q] : up.c[q], dn ? up.c[q] : um.c[q], A.hz2, A.ihz2);
                         f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unq, 0.0, SCH == 1 ? uc_.x[q] : ucc, lsumg);
                     }
                     double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0, SCH == 1 ? fc.x[q] : c, lsumg);

@@ -23,6 +23,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--out", required=True)
 ap.add_argument("--nx", type=int, default=48)
 ap.add_argument("--ny", type=int, default=40)
+ap.add_argument("--nz", type=int, default=24, help="heat3d: planes of the global grid")
 ap.add_argument("--jv", default="exact")
 ap.add_argument("--tol-rel", type=float, default=1e-9, help="Newton tol_rel of the Bratu solve")
 ap.add_argument("--krylov-itmax", type=int, default=0,
@@ -69,7 +70,7 @@ else:
 
 nx, ny = args.nx, args.ny
 if args.problem == "heat3d":  # 3D heat, implicit midpoint, z-slabs (k_st3l: the ghost planes travel in the stencil)
-    nz = 24
+    nz = args.nz
     grid = ah.slab((nx, ny, nz), rank, world)
     z0, nzl = grid.offset, grid.shape_xyz[2]
     rng = np.random.default_rng(9)

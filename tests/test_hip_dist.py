@@ -258,20 +258,21 @@ def test_resident_sweep_two_ranks_one_gpu(tmp_path):
     assert np.max(np.abs(d["x"] - xo)) <= 1e-9 * np.max(np.abs(xo))
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
-def test_heat3d_midpoint_zslabs_match_oracle(tmp_path, world):
+@pytest.mark.parametrize("world,nz", [(2, 24), (3, 24), (8, 24), (2, 64), (3, 72)])
+def test_heat3d_midpoint_zslabs_match_oracle(tmp_path, world, nz):
     """3D heat (G_Midpoint!, alpha 0.3) on z-slabs, mailbox transport: the Jv's ghost planes of v travel
     inside the 3D stencil launch (k_st3l's tiles at the slab ends fetch the neighbours' patches).
     Residual, exact and FD JVP bit-identical to the oracle on the whole grid; one implicit step
-    with the FD operator: equal Newton / Krylov counts."""
+    with the FD operator: equal Newton / Krylov counts.  nz 64 / 72: two 16-plane z-chunks per slab
+    (32 / 24 planes), the second marching down -- it starts on the upper ghost plane from the inbox."""
     out = str(tmp_path / "h3")
     rc, log = run_ranks(world, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
-                                "--problem", "heat3d", "--nx", "40", "--ny", "20"], worker_env(world))
+                                "--problem", "heat3d", "--nx", "40", "--ny", "20", "--nz", str(nz)], worker_env(world))
     assert rc == 0, log[-3000:]
     meta = json.load(open(out + ".json"))
     assert meta["mailbox"]
     d = np.load(out + ".npz")
-    nx, ny, nz = 40, 20, 24
+    nx, ny = 40, 20
     rng = np.random.default_rng(9)
     un = rng.standard_normal((nz, ny, nx))
     u0 = un + 0.01 * rng.standard_normal((nz, ny, nx))
