@@ -765,8 +765,10 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         if (planes > p->nz) planes = p->nz;
         A.rows = (int)planes;
         grid = A.tiles_x * A.tiles_y * (int)((p->nz + planes - 1) / planes);
-        // k_st3l: whole tile columns per XCD band, odd z-chunks marching down (tile3_of)
-        static const int zalt_env = NK_TUNE("NK_ST3_ZALT", 1);
+        // k_st3l tile order / march direction (tile3_of; kbench only: 1 whole tile columns per XCD band with
+        // odd z-chunks marching down, 2 plane-major + odd chunks down, 3 chunk pairs): within +-3 % of the
+        // plane-major order, upward marches (0, the product) -- profiles/r03/ab_zalt*.log
+        static const int zalt_env = NK_TUNE("NK_ST3_ZALT", 0);
         A.zalt = (A.lds3 && !(fast & 65536)) ? zalt_env : 0;  // kbench fast bit 65536: the plane-major order
     }
     // FD with F0 recomputed from u (2D, VEC <= 2: k_st2d<..., F0R>; 3D heat: k_st3l<..., F0R>, not

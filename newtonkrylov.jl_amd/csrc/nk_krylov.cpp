@@ -308,7 +308,8 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
     auto slot_pin = [&](int k) { return ws->hpin + (size_t)(k & 1) * (2 * ws->cap + 2); };
     auto slot_pin_dev = [&](int k) { return ws->hpin_dev + (size_t)(k & 1) * (2 * ws->cap + 2); };
     auto npasses_of = [&](int k) { return reorth ? 2 * k : k; };
-    const double* v1_src = r0;  // r0 of the current cycle; step 1 applies J to r0 / beta and stores V_1
+    const double* v1_src = r0;  // r0 of the current cycle; step 1 applies J to r0 / rNorm and stores V_1
+    double v1norm = 1.0;        // ||V_1|| = beta / rNorm
     // right preconditioner, without the one-step-ahead issue (the FD step size needs ||N V_k|| on
     // the host): fgmres! stores Z_k = N V_k and updates x += Z y; gmres! applies N to p = N V_k
     // only for the product and updates x += N (V y) (Krylov.jl 0.10 gmres! / fgmres!)
@@ -348,7 +349,7 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         if (N || Mp) {  // V_k = q_{k-1} / h (r0 / beta), Z_k = N V_k, q = M J Z_k, <V_1, q>
             NK_TRY(launch_fd_point(c, n, nullptr, nullptr, qprev, hprev, 0.0, ws->V[k - 1]));
             const double* zk = ws->V[k - 1];
-            double znorm = 1.0;
+            double znorm = k == 1 ? v1norm : 1.0;
             if (N) {
                 NK_TRY(ws_zbasis(ws, flex ? k : 1));  // gmres!: one p = N V_k buffer; fgmres!: Z_k kept
                 double* z = ws->Z[flex ? k - 1 : 0];
@@ -363,8 +364,9 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
             } else {
                 NK_TRY(A.apply(q, zk, znorm, EPI_DOT, ws->V[0], &red));
             }
-        } else if (k == 1) {  // fused kdivcopy!(V_1, r0, beta) + mul! + <V_1, Jv> (the dot partner is V_1 itself)
-            NK_TRY(A.apply(q, v1_src, 1.0, EPI_DOT, nullptr, &red, ws->bdev, ws->V[0]));
+        } else if (k == 1) {  // fused kdivcopy!(V_1, r0, rNorm) + mul! + <V_1, Jv> (the dot partner is V_1 itself)
+            // ||V_1|| = beta / rNorm: 1 on the first cycle, |r0| / |zeta| after a restart (the FD step's ||v||)
+            NK_TRY(A.apply(q, v1_src, v1norm, EPI_DOT, nullptr, &red, ws->bdev, ws->V[0]));
         } else if (vready[k - 1]) {  // V_k is in place: mul! + <V_1, Jv> only
             NK_TRY(A.apply(q, ws->V[k - 1], 1.0, EPI_DOT, ws->V[0], &red));
         } else {
@@ -430,6 +432,7 @@ int gmres(nk_workspace* ws, const nk_problem* p, Op& A, const double* b, const n
         // the first pass and, after a restart, the previous cycle's estimate |zeta| (z[1] = beta regardless)
         NK_TRY(launch_fill(c, 1, ws->bdev, rNorm));
         v1_src = src;
+        v1norm = beta / rNorm;
         npass++;
         inner_iter = 0;
         bool inner_tired = false;

@@ -1038,7 +1038,11 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
     const int64_t z1 = z0 + A.rows < nz ? z0 + A.rows : nz;
     // march direction: odd chunks (zalt) from z1 - 1 down to z0 -- fm / fp are then the planes above /
     // below, and the z-Laplacian takes them in the reference's order ((p - 2c) + m) all the same
+#ifdef NK_KBENCH
     const bool dn = A.zalt && (tz & 1);
+#else
+    constexpr bool dn = false;  // the product keeps the plane-major order, upward marches (profiles/r03/ab_zalt2.log)
+#endif
     const int64_t st = dn ? -pl : pl, dz = dn ? -1 : 1;
     const int64_t zs = dn ? z1 - 1 : z0;
     constexpr bool kUn = SCH == 0 && MODE != MODE_JEXACT;

@@ -562,7 +562,8 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
                     prec_apply(A, N, pv, V[k - 1]);
                     op_apply(A, w, pv, -1.0);
                 } else {
-                    op_apply(A, w, V[k - 1], 1.0);
+                    /* ||V_1|| = beta / rNorm (1 on the first cycle, |r0| / |zeta| after a restart) */
+                    op_apply(A, w, V[k - 1], k == 1 ? beta / rNorm : 1.0);
                 }
                 if (M) prec_apply(A, M, q, w);
                 for (int i = 1; i <= k; ++i) {

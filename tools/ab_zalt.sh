@@ -1,6 +1,6 @@
 #!/bin/bash
-# 3D stencils: whole tile columns per XCD band with odd z-chunks marching down (A.zalt, the default)
-# vs the plane-major order (kbench fast bit 65536): bitwise check of out / V_k first, then timing
+# 3D stencils: whole tile columns per XCD band with odd z-chunks marching down (A.zalt = 1; run with
+# NK_ST3_ZALT=1 -- the default was 1 when this log was taken, it is 0 now) vs the plane-major order (kbench fast bit 65536): bitwise check of out / V_k first, then timing
 # (profiles/r03/ab_zalt.log).  The reductions differ in the last bits (another block -> tile map and
 # accumulation order), every point value must not.
 set -e

@@ -1,7 +1,8 @@
 """Cost of the ghost-plane exchange on config 5's slab shape, measured on ONE GPU.
 
 Two processes share the GPU, each owning a 512 x 512 x 64 z-slab of 3D heat (G_Euler! ∘ diffusion!,
-FD Jv), and time (a) a loop of Jv products and (b) a fixed-budget GMRES(20) solve, in three modes:
+FD and exact Jv), and time a loop of Jv products (optionally also a fixed-budget GMRES(20) solve, --itmax),
+in three modes:
 
   alone   no communicator: two independent slabs, ghost planes zero -- no exchange at all
   fused   peer mailbox; v's ghost planes travel inside the Jv launch (halo_tile_exchange, the default)
@@ -10,7 +11,7 @@ FD Jv), and time (a) a loop of Jv products and (b) a fixed-budget GMRES(20) solv
 Both processes run their kernels concurrently on the one GPU, so absolute times are those of a shared
 device; the differences between the modes are the exchange's cost.  Not part of the product.
 
-Usage (GPU box): python tools/halo_cost.py [--nx 512 --ny 512 --nzl 64] [--reps 40] [--itmax 40]
+Usage (GPU box): python tools/halo_cost.py [--nx 512 --ny 512 --nzl 64] [--reps 40] [--itmax 0]
 """
 import argparse
 import json
