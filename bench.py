@@ -61,6 +61,12 @@ def pmc_name(workload, kernel, scheme="euler"):
 LAMBDA = 3.51382       # examples/bratu.jl:41
 
 
+def log(msg):
+    """Progress on stderr (the JSON line alone goes to stdout): the phases after the timed region -- copy
+    calibration, CPU baseline, agreement -- take tens of seconds and a silent run looks hung."""
+    print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -205,22 +211,35 @@ class Bratu2D:
         return r.n_matvec, r
 
     def cpu_baseline(self, threads):
-        """The C oracle (test infrastructure) on one GMRES restart cycle of the same problem."""
+        """The C oracle (test infrastructure) on the Krylov solve of one bench step of the same problem --
+        bounded: one restart cycle is timed first and the sample shortened to about 20 s of CPU work if the
+        whole step would take longer (a host whose cores are busy with other work)."""
         from oracle import oracle as oc
 
         oc.set_threads(threads)
         P = oc.bratu2d(self.n)
         u0 = oc.sin_ic(P)
         F0 = oc.residual(P, u0)
-        t0 = time.perf_counter()
-        x, st, _ = oc.krylov_solve(P, u0, F0, jv=self.args.jv, F0=F0, memory=self.args.memory, restart=True,
-                                   itmax=self.args.cpu_itmax, atol=0.0, rtol=0.0, history=False,
-                                   reorthogonalization=self.args.reorth == "on")
-        dt = time.perf_counter() - t0
-        self.x_cpu = x
+
+        def solve(itmax):
+            t0 = time.perf_counter()
+            x, st, _ = oc.krylov_solve(P, u0, F0, jv=self.args.jv, F0=F0, memory=self.args.memory, restart=True,
+                                       itmax=itmax, atol=0.0, rtol=0.0, history=False,
+                                       reorthogonalization=self.args.reorth == "on")
+            return x, st, time.perf_counter() - t0
+
+        m = self.args.memory
+        _, st1, dt1 = solve(m)  # one restart cycle: the per-step cost on these cores
+        per_step = dt1 / max(1, st1["niter"])
+        itmax = self.args.cpu_itmax
+        if per_step * itmax > 20.0:
+            itmax = max(m, min(itmax, int(20.0 / per_step) // m * m))
+        log(f"cpu baseline: {threads} threads, {dt1:.1f} s per restart cycle -> itmax {itmax}")
+        x, st, dt = solve(itmax)
+        self.x_cpu, self.cpu_itmax = x, itmax
         return dict(value=st["n_matvec"] / dt, unit="matvecs/s", cores=oc.get_threads(), kind="port",
                     sample=f"oracle/nk_oracle.c: the Krylov solve of one bench step -- GMRES({self.args.memory}) with "
-                           f"restarts, itmax={self.args.cpu_itmax}, {st['n_matvec']} {self.args.jv.upper()} matvecs "
+                           f"restarts, itmax={itmax}, {st['n_matvec']} {self.args.jv.upper()} matvecs "
                            f"(MGS, same schedule) on the same {self.n}x{self.n} Bratu problem, {dt:.2f} s")
 
     def agreement(self):
@@ -233,7 +252,7 @@ class Bratu2D:
         ah.bratu2d_(res, u, self.p)
         J = ah.JacobianOperator(ah.bratu2d_, res, u, self.p, jv=self.args.jv)
         ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=self.args.memory))
-        ah.krylov_solve_(ws, J, res, restart=True, itmax=self.args.cpu_itmax, atol=0.0, rtol=0.0,
+        ah.krylov_solve_(ws, J, res, restart=True, itmax=self.cpu_itmax, atol=0.0, rtol=0.0,
                          reorthogonalization=self.args.reorth == "on")
         x = ws.x.to_numpy()
         ah.kaxpy_(len(u), -1.0, ws.x, u)  # u .-= d (src/Ariadne.jl:344)
@@ -245,7 +264,7 @@ class Bratu2D:
         d = abs(n_gpu - n_cpu) / n_cpu
         dx = float(np.linalg.norm(x - self.x_cpu) / np.linalg.norm(self.x_cpu))
         return {"quantity": f"||F(u0 - x)|| after one Newton step (GMRES({self.args.memory}), "
-                            f"{self.args.cpu_itmax} Arnoldi steps), GPU vs CPU, relative",
+                            f"{self.cpu_itmax} Arnoldi steps), GPU vs CPU, relative",
                 "value": d, "tolerance": 1e-10, "ok": d <= 1e-10, "n_res_gpu": n_gpu, "n_res_cpu": n_cpu,
                 "x_rel_diff": dx}
 
@@ -344,6 +363,7 @@ class HeatEuler:
             u, st = oc.newton_krylov(P, u, tol_abs=6e-6, memory=self.args.memory or 20, jv=self.args.jv,
                                      reorthogonalization=self.reorth)
             dt += time.perf_counter() - t0
+            log(f"cpu baseline: time step {steps + 1}, {dt:.1f} s so far")
             if steps == 0:  # the first time step, for the CPU/GPU agreement check
                 self.cpu_step = (u0, u.copy(), st)
             P.un = u
@@ -493,6 +513,8 @@ def main():
     if dist is not None:
         paths = [None] * world
         dist.all_gather_object(paths, path)
+    if rank == 0:
+        log("timed steps done; copy calibration")
     copy_gbs = copy_calibration(device) if rank == 0 else None
 
     # Two byte counts per kernel class (nk_prof_entry): `bytes` = the operand bytes the kernel moves
@@ -617,16 +639,19 @@ def main():
             affinity = len(os.sched_getaffinity(0))
             share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
             threads = args.cpu_threads or affinity
+            log(f"cpu baseline on {threads} threads (the affinity mask)")
             cb = W.cpu_baseline(threads)
             cb["value"] = round(cb["value"], 4)
             cb["host_cpus"] = {"nproc": os.cpu_count(), "affinity": affinity,
                                "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
             if share and share != threads:
+                log(f"cpu baseline on the per-GPU share, {share} threads")
                 sh = W.cpu_baseline(share)
                 cb["per_gpu_share"] = {"value": round(sh["value"], 4), "unit": sh["unit"], "cores": sh["cores"],
                                        "sample": sh["sample"]}
             out["cpu_baseline"] = cb
             if hasattr(W, "agreement"):
+                log("cpu/gpu agreement")
                 out["cpu_gpu_agreement"] = W.agreement()
         else:
             out["cpu_baseline"] = None
