@@ -108,7 +108,7 @@ def parse():
                          "the other rank's kernels room on the shared GPU)")
     ap.add_argument("--cpu-itmax", type=int, default=300, help="Arnoldi steps in the CPU-baseline sample (300 = one bench step)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="threads of the headline CPU sample (0: every core in the affinity mask); the per-GPU "
+                    help="threads of the headline CPU sample (0: the fastest count up to the affinity mask, probed); the per-GPU "
                          "share (OMP_NUM_THREADS) is timed beside it and the machine's nproc reported")
     ap.add_argument("--traffic-json", default="",
                     help="per-kernel HBM traffic from separate rocprofv3 --pmc passes (tools/pmc_traffic.py); "
@@ -116,6 +116,35 @@ def parse():
                          "of another size is never applied)")
     ap.add_argument("--launch-probe", type=int, default=-1, help=argparse.SUPPRESS)  # CPU test of the launcher
     return ap.parse_args()
+
+
+def cpu_thread_probe(affinity, share):
+    """Seconds of a short oracle sample (3 x FD Jv + dot + norm on the 4096^2 Bratu grid) per OpenMP thread
+    count -- the per-GPU share, then doubling up to the affinity mask, stopping once a count is clearly
+    slower than the best (on a GPU box the mask spans the whole machine while other jobs own most of it:
+    256 threads took 135 s for a GMRES cycle that 16 do in 1.5 s).  Returns (fastest count, {count: s})."""
+    from oracle import oracle as oc
+
+    P = oc.bratu2d(4096)
+    u = oc.sin_ic(P)
+    v = np.random.default_rng(1).standard_normal(P.shape)
+    F0 = oc.residual(P, u)
+    counts = sorted({t for t in (share, 8, 16, 32, 64, 128, 256, 512, affinity) if 0 < t <= affinity})
+    probe, best = {}, None
+    for t in counts:
+        oc.set_threads(t)
+        oc.jv_fd(P, u, v, F0)  # warm-up (thread pool)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            w = oc.jv_fd(P, u, v, F0)
+            oc.dot(w, v)
+            oc.norm(w)
+        probe[t] = round(time.perf_counter() - t0, 4)
+        if best is None or probe[t] < probe[best]:
+            best = t
+        elif probe[t] > 1.5 * probe[best] or probe[t] > 10.0:
+            break
+    return best, probe
 
 
 def copy_calibration(device, n=1 << 27, reps=5):
@@ -633,17 +662,24 @@ def main():
         if world > 1:
             out["ranks"] = paths  # per rank: transport, resident sweep, in-launch ghost planes, launch counts
         if world == 1 and not args.no_cpu_baseline and not args.global_n:
-            # the node's host cores: every core in this process's affinity mask (the headline figure), and
-            # the per-GPU share the box gives one GPU (OMP_NUM_THREADS, 16 there) beside it; nproc is the
-            # machine's full count
+            # the node's host cores: the fastest thread count the process's affinity mask offers (the
+            # headline figure), and the per-GPU share the box gives one GPU (OMP_NUM_THREADS, 16 there)
+            # beside it; nproc is the machine's full count
             affinity = len(os.sched_getaffinity(0))
             share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-            threads = args.cpu_threads or affinity
-            log(f"cpu baseline on {threads} threads (the affinity mask)")
+            probe = {}
+            if args.cpu_threads:
+                threads = args.cpu_threads
+            else:  # the fastest thread count the affinity mask offers (on a shared host, more is not faster)
+                threads, probe = cpu_thread_probe(affinity, share)
+            log(f"cpu baseline on {threads} threads (affinity mask {affinity}, probe {probe})")
             cb = W.cpu_baseline(threads)
             cb["value"] = round(cb["value"], 4)
             cb["host_cpus"] = {"nproc": os.cpu_count(), "affinity": affinity,
-                               "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+                               "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+                               "thread_probe_s": probe,
+                               "threads_rule": "the fastest of the probed thread counts up to the affinity mask "
+                                               "(a Bratu 4096^2 FD Jv + dot + norm, 3x, per count)"}
             if share and share != threads:
                 log(f"cpu baseline on the per-GPU share, {share} threads")
                 sh = W.cpu_baseline(share)

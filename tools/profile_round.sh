@@ -1,6 +1,6 @@
 #!/bin/bash
 # Regenerate one round's profiles on the GPU box (run from the repo root):
-#     bash tools/profile_round.sh r02 [quick]
+#     bash tools/profile_round.sh r03 [quick]
 # Results land in gpurun_out/prof_<round>/profiles/ (copy them to profiles/<round>/).
 # Every GPU step has its own time limit; the script stops at the first failure.
 #   1. rocprofv3 --kernel-trace --stats of the default bench         -> kernel_stats_bench.csv
@@ -11,7 +11,7 @@
 # PROFILE_PARTS="trace pmc bench" and PROFILE_TAGS="bratu2d heat2d ..." select a subset (one gpurun
 # call stays well inside its time limit).
 set -e -o pipefail
-R=${1:-r02}
+R=${1:-r03}
 MODE=${2:-full}
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/prof_$R
