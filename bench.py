@@ -678,13 +678,18 @@ def main():
             cb["host_cpus"] = {"nproc": os.cpu_count(), "affinity": affinity,
                                "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
                                "thread_probe_s": probe,
-                               "threads_rule": "the fastest of the probed thread counts up to the affinity mask "
-                                               "(a Bratu 4096^2 FD Jv + dot + norm, 3x, per count)"}
+                               "threads_rule": "the faster of two samples: the per-GPU share (OMP_NUM_THREADS) and "
+                                               "the fastest count of a short probe up to the affinity mask (a Bratu "
+                                               "4096^2 FD Jv + dot + norm, 3x, per count)"}
             if share and share != threads:
                 log(f"cpu baseline on the per-GPU share, {share} threads")
                 sh = W.cpu_baseline(share)
-                cb["per_gpu_share"] = {"value": round(sh["value"], 4), "unit": sh["unit"], "cores": sh["cores"],
-                                       "sample": sh["sample"]}
+                sh["value"] = round(sh["value"], 4)
+                if sh["value"] > cb["value"]:  # the headline is the faster of the two measured samples
+                    sh["host_cpus"] = cb.pop("host_cpus")
+                    cb, sh = sh, cb
+                cb["other_sample"] = {"value": sh["value"], "unit": sh["unit"], "cores": sh["cores"],
+                                      "sample": sh["sample"]}
             out["cpu_baseline"] = cb
             if hasattr(W, "agreement"):
                 log("cpu/gpu agreement")
