@@ -224,7 +224,7 @@ __device__ __forceinline__ bool halo_tile_exchange(const double* __restrict__ v,
     const int64_t w = cb - ca, cnt = (rb - ra) * w;
     for (int side = 0; side < 2; ++side) {  // side 0: my first plane -> the lower rank's "from upper" inbox
         if ((side == 0 && !t.lo) || (side == 1 && !t.hi)) continue;
-        const int peer = side == 0 ? rank - 1 : rank + 1;
+        const int peer = side == 0 ? (rank + nr - 1) % nr : (rank + 1) % nr;  // (modular: a one-rank self ring, kbench)
         const double* src = side == 0 ? v : v + (nplanes - 1) * plane;
         uint64_t* dst = halo_inbox(g_mb.peers[peer], par, side == 0 ? 1 : 0, cap);
         for (int64_t q = threadIdx.x; q < cnt; q += nthreads) {
@@ -235,8 +235,8 @@ __device__ __forceinline__ bool halo_tile_exchange(const double* __restrict__ v,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every thread drains its stores before the flag
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (t.lo) __hip_atomic_store(halo_tile_flags(g_mb.peers[rank - 1], par, 1) + tile, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (t.hi) __hip_atomic_store(halo_tile_flags(g_mb.peers[rank + 1], par, 0) + tile, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (t.lo) __hip_atomic_store(halo_tile_flags(g_mb.peers[(rank + nr - 1) % nr], par, 1) + tile, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (t.hi) __hip_atomic_store(halo_tile_flags(g_mb.peers[(rank + 1) % nr], par, 0) + tile, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         hx_ok = 1;
         for (int side = 0; side < 2; ++side) {
             if ((side == 0 && !t.lo) || (side == 1 && !t.hi)) continue;
@@ -254,7 +254,6 @@ __device__ __forceinline__ bool halo_tile_exchange(const double* __restrict__ v,
         }
     }
     __syncthreads();
-    (void)nr;
     return hx_ok != 0;
 }
 

@@ -183,6 +183,7 @@ double* red_out(nk_ctx* c, int len, Red* r, int* fin);  // slot for a reduction 
 int finish_reduction(nk_ctx* c, Red* r);     // multi-rank: collapse + RCCL all-reduce
 int mb_check(nk_ctx* c);                     // after a host sync: did a mailbox wait time out?
 int red_blocks(int64_t n);                   // grid size of streaming reductions
+bool halo_self_ring(const nk_ctx* c);        // kbench: a one-rank mailbox exchanges ghost planes with itself
 int halo_fuse_knob();                        // 1: a Krylov Jv's ghost planes travel in the stencil launch (mailbox up)
 // One Arnoldi step's MGS sweep in one launch (np passes over V[t % k], then ||q||) with q resident
 // on chip; returns 1 (nothing enqueued) when the resident path does not apply.

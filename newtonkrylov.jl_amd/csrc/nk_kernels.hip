@@ -621,7 +621,8 @@ __global__ __launch_bounds__(kBlock) void k_periodic_fill(double* __restrict__ v
 }  // namespace
 
 int launch_halo_ipc(nk_ctx* c, double* v, int64_t plane, int64_t nplanes, bool ring) {
-    if (c->nranks < 2) return NK_OK;
+    if (halo_self_ring(c)) ring = true;
+    else if (c->nranks < 2) return NK_OK;
     const uint64_t epoch = ++c->halo_epoch;
     int nb = (int)((plane + 1023) / 1024);
     if (nb > kHaloBlocks) nb = kHaloBlocks;
@@ -660,6 +661,13 @@ int mailbox_selftest(nk_ctx* c, bool* ok) {
 int halo_fuse_knob() {
     static const int fuse = NK_TUNE("NK_HALO_FUSE", 1);
     return fuse;
+}
+
+// kbench only (NK_HALO_SELF=1, with a forced one-rank mailbox): the lone rank is its own lower and upper
+// neighbour -- a self ring that runs the whole ghost-plane exchange on one GPU (tools/halo_self.py)
+bool halo_self_ring(const nk_ctx* c) {
+    static const int self = NK_TUNE("NK_HALO_SELF", 0);
+    return self && c->mb_on && c->nranks == 1;
 }
 
 int red_blocks(int64_t n) {
@@ -796,11 +804,12 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         // the slab axis is not periodic and every tile of a plane has a flag; else exchanged first
         const int fuse_env = halo_fuse_knob();
         const int64_t tiles_pl = g.dim == 2 ? A.tiles_x : (int64_t)A.tiles_x * A.tiles_y;
-        const bool fuse = fuse_env && c->mb_on && c->nranks > 1 && !per && in.mode != MODE_RES &&
+        const bool self = halo_self_ring(c);
+        const bool fuse = fuse_env && c->mb_on && (c->nranks > 1 || self) && !per && in.mode != MODE_RES &&
                           (g.dim == 2 || (g.dim == 3 && A.lds3)) && g.plane <= c->halo_cap && tiles_pl <= kHaloTileFlags;
         if (fuse) {
-            A.hx_lo = c->rank > 0;
-            A.hx_hi = c->rank + 1 < c->nranks;
+            A.hx_lo = c->rank > 0 || self;
+            A.hx_hi = c->rank + 1 < c->nranks || self;
             A.hx_epoch = ++c->halo_epoch;
             A.hx_cap = c->halo_cap;
         } else {
