@@ -168,17 +168,22 @@ __device__ __forceinline__ double reduce_input(const double* __restrict__ in, in
 // stored write-through (agent-scope atomic store = sc1) and drained before the ticket; the last
 // block reads the partials with sc1 loads.  An agent-scope RELEASE fence here would write back the
 // XCD's whole L2 -- full of this kernel's streamed output -- once per block (measured: 2x slower).
+// slot: where the partial goes (default: blockIdx.x).  The stencils pass their TILE index, so the
+// fixed-order sum runs over tiles in address order whatever block a tile was dispatched on (the XCD
+// bands, the slab-end tiles first when ghost planes travel in the launch): the same operator gives the
+// same bits on every path.
 template <int NT = kBlock>
-__device__ __forceinline__ void publish(double acc, double* part, int fin, double* sh) {
+__device__ __forceinline__ void publish(double acc, double* part, int fin, double* sh, int slot = -1) {
     __shared__ unsigned ticket;
     const double s = block_sum<NT>(acc, sh);
+    if (slot < 0) slot = (int)blockIdx.x;
     if (!fin) {
-        if (threadIdx.x == 0) part[blockIdx.x] = s;
+        if (threadIdx.x == 0) part[slot] = s;
         return;
     }
     unsigned* cnt = reinterpret_cast<unsigned*>(part + kRedCap - 2);
     if (threadIdx.x == 0) {  // the partial's only writer is this lane
-        __hip_atomic_store(part + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(part + slot, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         ticket = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

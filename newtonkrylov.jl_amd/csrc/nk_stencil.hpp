@@ -724,7 +724,7 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
             ax = axn;
         }
     }
-    if constexpr (EPI != EPI_NONE) publish(acc, A.part, A.fin, sh);
+    if constexpr (EPI != EPI_NONE) publish(acc, A.part, A.fin, sh, t);
 }
 
 // ------------------------------------------------------------------------------ 2D stencil, one-shot LDS tile
@@ -1218,7 +1218,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
             ax = axn;
         }
     }
-    if constexpr (EPI != EPI_NONE) publish<64 * NW>(acc, A.part, A.fin, sh);
+    if constexpr (EPI != EPI_NONE) publish<64 * NW>(acc, A.part, A.fin, sh, tz * A.tiles_x * A.tiles_y + txy);
 }
 
 // ------------------------------------------------------------------------------ stencil dispatch
