@@ -355,3 +355,22 @@ def test_bench_reports_every_ranks_path(tmp_path):
         assert r["halo_in_launch"]
         assert r["launches"]["halo_rccl"] == 0 and r["launches"]["allreduce"] == 0
     assert line["config"]["path"]["mailbox_all_ranks"]
+
+
+@pytest.mark.parametrize("dims", [("64", "48", "40"), ("96", "70", "0")])
+def test_self_ring_exchange_forms_are_bitwise(dims):
+    """One process, a forced one-rank mailbox whose rank is its own lower and upper neighbour (kernel-variant
+    build, NK_HALO_SELF): a restarted FD-GMRES solve with the ghost planes (3D) / rows (2D) inside the Jv
+    launch gives bit for bit the solution of the separate exchange kernel -- the slab-end-first dispatch of
+    the in-launch form changes no sum (stencil partials are indexed by tile) -- and the one-rank mailbox
+    without exchange reproduces the plain context."""
+    nx, ny, nz = dims
+    wait_gpu_released()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "halo_self.py"), "--nx", nx, "--ny", ny, "--nz", nz,
+                        "--itmax", "25", "--modes", "plain,mbox,fused,kernel"], capture_output=True, text=True,
+                       timeout=240, env=dict(os.environ))
+    assert p.returncode == 0, (p.stdout + p.stderr)[-3000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("fused vs kernel")][-1]
+    assert "(bitwise: True)" in line and "plain vs mbox bitwise: True" in line, p.stdout[-3000:]
+    fused = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith('{"mode": "fused"')][-1]
+    assert "halo_ipc" not in fused["classes"] or fused["classes"]["halo_ipc"]["launches"] <= 1  # v's planes in-launch

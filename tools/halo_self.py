@@ -30,7 +30,8 @@ ROOT = os.path.dirname(HERE)
 ap = argparse.ArgumentParser()
 ap.add_argument("--nx", type=int, default=512)
 ap.add_argument("--ny", type=int, default=512)
-ap.add_argument("--nz", type=int, default=64, help="planes of the slab (config 5: 512 / 8)")
+ap.add_argument("--nz", type=int, default=64, help="planes of the slab (config 5: 512 / 8); 0: a 2D Bratu slab "
+                                                   "of nx x ny (ghost rows in k_st2d's launch)")
 ap.add_argument("--itmax", type=int, default=60)
 ap.add_argument("--modes", default="plain,mbox,fused,kernel,plain,mbox,fused,kernel")
 ap.add_argument("--child", default="")
@@ -57,14 +58,21 @@ def child(mode):
     if mode != "plain":
         ctx.init_distributed(0, 1, ah.dist_unique_id())
     nx, ny, nz = args.nx, args.ny, args.nz
-    grid = ah.Grid.full(nx, ny, nz)
     rng = np.random.default_rng(11)
-    un = rng.standard_normal(grid.np_shape)
-    hx, hy, hz, a = 1.0 / (nx + 1), 1.0 / (ny + 1), 1.0 / (8 * nz + 1), 0.01
-    dt = 1.0 / (2.0 * a * (1 / hx ** 2 + 1 / hy ** 2 + 1 / hz ** 2))
-    und = ah.DeviceArray.from_numpy(un, grid, ctx)
-    F_, p = ah.G_Euler_.bind(ah.diffusion3d_), (und, dt, None, (a, hx, hy, hz, ah.bc_zero_), 0.0)
-    u = ah.DeviceArray.from_numpy(un + 0.01 * rng.standard_normal(grid.np_shape), grid, ctx)
+    if nz == 0:  # 2D Bratu slab: the ghost rows travel in k_st2d's launch
+        grid = ah.Grid.full(nx, ny)
+        hx, hy = 1.0 / (nx + 1), 1.0 / (8 * ny + 1)
+        F_, p = ah.bratu2d_, (hx, hy, 3.51382)
+        xs, ys = np.arange(1, nx + 1) * hx, np.arange(1, ny + 1) * hy
+        u = ah.DeviceArray.from_numpy(np.sin(np.pi * ys)[:, None] * np.sin(np.pi * xs)[None, :], grid, ctx)
+    else:
+        grid = ah.Grid.full(nx, ny, nz)
+        un = rng.standard_normal(grid.np_shape)
+        hx, hy, hz, a = 1.0 / (nx + 1), 1.0 / (ny + 1), 1.0 / (8 * nz + 1), 0.01
+        dt = 1.0 / (2.0 * a * (1 / hx ** 2 + 1 / hy ** 2 + 1 / hz ** 2))
+        und = ah.DeviceArray.from_numpy(un, grid, ctx)
+        F_, p = ah.G_Euler_.bind(ah.diffusion3d_), (und, dt, None, (a, hx, hy, hz, ah.bc_zero_), 0.0)
+        u = ah.DeviceArray.from_numpy(un + 0.01 * rng.standard_normal(grid.np_shape), grid, ctx)
     res = u.zero()
     F_(res, u, p)
     J = ah.JacobianOperator(F_, res, u, p, jv="fd")
@@ -92,8 +100,9 @@ if args.child:
     child(args.child)
     sys.exit(0)
 
-print(f"halo self ring: one process, {args.nx} x {args.ny} x {args.nz} slab of 3D heat (G_Euler!, FD Jv), "
-      f"GMRES(20) restarted, {args.itmax} Arnoldi steps", flush=True)
+what = (f"{args.nx} x {args.ny} slab of 2D Bratu" if args.nz == 0 else
+        f"{args.nx} x {args.ny} x {args.nz} slab of 3D heat (G_Euler!)")
+print(f"halo self ring: one process, {what}, FD Jv, GMRES(20) restarted, {args.itmax} Arnoldi steps", flush=True)
 rows = []
 for mode in args.modes.split(","):
     env = dict(os.environ, NK_KBENCH_LIB="1", **ENV[mode])
