@@ -116,12 +116,13 @@ int ws_zbasis(nk_workspace* ws, int need) {
 
 inline double sgn(double x) { return (double)((x > 0) - (x < 0)); }
 
-// kbench knobs: NK_MGS_ALT=1 alternates the sweep direction of consecutive MGS passes (see
-// k_mgs_pass); NK_MGS_RESIDENT=0 runs one k_mgs_pass launch per MGS pass instead of the resident
-// sweep; NK_RES_JV=1 computes the 2D Bratu FD Jv inside the resident sweep's launch (slower,
+// NK_MGS_RESIDENT=0 (operational) runs one k_mgs_pass launch per MGS pass instead
+// of the resident sweep, which needs every CU of the device at once: for a GPU shared with unrelated
+// work.  kbench knobs: NK_MGS_ALT=1 alternates the sweep direction of consecutive MGS passes (see
+// k_mgs_pass); NK_RES_JV=1 computes the 2D Bratu FD Jv inside the resident sweep's launch (slower,
 // DESIGN.md §4)
 const int mgs_alt = NK_TUNE("NK_MGS_ALT", 0);
-const int mgs_resident = NK_TUNE("NK_MGS_RESIDENT", 1);
+const int mgs_resident = env_cfg("NK_MGS_RESIDENT", 1);
 const int mgs_fused_jv = NK_TUNE("NK_RES_JV", 0);
 
 // Krylov.jl sym_givens (real case)

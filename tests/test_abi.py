@@ -44,7 +44,8 @@ def test_product_library_has_no_kbench_hooks_or_knobs():
     # the product is the smaller build: variant instantiations pruned
     assert len(prod) < 0.7 * len(kb)
     # operational configuration stays readable in the product (transport, timeouts, shared-GPU rigs)
-    for k in (b"NK_DIST_MAILBOX", b"NK_MB_SPIN_LIMIT", b"NK_RES_SHARED"):
+    for k in (b"NK_DIST_MAILBOX", b"NK_MB_SPIN_LIMIT", b"NK_RES_SHARED", b"NK_MGS_RESIDENT", b"NK_HALO_CAP",
+              b"NK_DIST_FORCE"):
         assert k in prod, k
 
 
