@@ -264,7 +264,8 @@ def test_heat3d_midpoint_zslabs_match_oracle(tmp_path, world, nz):
     inside the 3D stencil launch (k_st3l's tiles at the slab ends fetch the neighbours' patches).
     Residual, exact and FD JVP bit-identical to the oracle on the whole grid; one implicit step
     with the FD operator: equal Newton / Krylov counts.  nz 64 / 72: two 16-plane z-chunks per slab
-    (32 / 24 planes), the second marching down -- it starts on the upper ghost plane from the inbox."""
+    (32 / 24 planes): the lower chunk's tiles fetch the lower ghost plane, the upper chunk's the upper
+    one, each from its own inbox in the same launch."""
     out = str(tmp_path / "h3")
     rc, log = run_ranks(world, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
                                 "--problem", "heat3d", "--nx", "40", "--ny", "20", "--nz", str(nz)], worker_env(world))
