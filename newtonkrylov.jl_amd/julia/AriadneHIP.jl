@@ -36,6 +36,32 @@ mutable struct HipContext
     end
 end
 
+"""What a context's distributed path runs (nk_dist_path, nkhip.h): transport, resident sweep, ghost
+planes inside the Jv launch, ranks sharing its GPU, its PCI bus id, a sticky mailbox error."""
+struct NkPathInfo
+    rank::Int32
+    nranks::Int32
+    device::Int32
+    ranks_on_device::Int32
+    rccl::Int32
+    mailbox::Int32
+    resident_sweep::Int32
+    resident_blocks::Int32
+    halo_in_launch::Int32
+    mailbox_error::Int32
+    halo_cap::Int64
+    pci_bus_id::NTuple{32, UInt8}
+end
+function path_info(ctx::HipContext)
+    r = Ref{NkPathInfo}()
+    check(ccall((:nk_dist_path, libnkhip), Cint, (Ptr{Cvoid}, Ref{NkPathInfo}), ctx.ptr, r), ctx, "nk_dist_path")
+    p = r[]
+    (rank = p.rank, nranks = p.nranks, device = p.device, ranks_on_device = p.ranks_on_device, rccl = p.rccl != 0,
+     mailbox = p.mailbox != 0, resident_sweep = p.resident_sweep != 0, resident_blocks = p.resident_blocks,
+     halo_in_launch = p.halo_in_launch != 0, mailbox_error = p.mailbox_error != 0, halo_cap = p.halo_cap,
+     pci_bus_id = String(UInt8[c for c in p.pci_bus_id if c != 0x00]))
+end
+
 # --------------------------------------------------------------------------- nk_problem (C layout)
 struct NkProblem
     kind::Int32

@@ -11,9 +11,10 @@ import _nkpath  # noqa: F401
 from ariadne_hip import _lib
 
 SHIM = os.path.join(os.path.dirname(_lib.PKG_DIR), "newtonkrylov.jl_amd", "julia", "AriadneHIP.jl")
-JL_SIZE = {"Int32": 4, "Int64": 8, "Float64": 8, "Bool": 1}
+JL_SIZE = {"Int32": 4, "Int64": 8, "Float64": 8, "Bool": 1, "UInt8": 1}
 PAIRS = [("NkProblem", _lib.nk_problem), ("NkKrylovOpts", _lib.nk_krylov_opts),
-         ("NkKrylovStats", _lib.nk_krylov_stats), ("NkUserOps", _lib.nk_user_ops), ("NkPrecond", _lib.nk_precond)]
+         ("NkKrylovStats", _lib.nk_krylov_stats), ("NkUserOps", _lib.nk_user_ops), ("NkPrecond", _lib.nk_precond),
+         ("NkPathInfo", _lib.nk_path_info)]
 
 
 def jl_fields(name):
@@ -21,10 +22,12 @@ def jl_fields(name):
     body = re.search(rf"^struct {name}\n(.*?)^end", src, re.S | re.M).group(1)
     out = []
     for line in body.splitlines():
-        m = re.match(r"\s*(\w+)::([\w{}]+)", line)
+        m = re.match(r"\s*(\w+)::(NTuple\{\d+, ?\w+\}|[\w{}]+)", line)
         if m:
             t = m.group(2)
-            out.append((m.group(1), 8 if t.startswith("Ptr") else JL_SIZE[t]))
+            tup = re.match(r"NTuple\{(\d+), ?(\w+)\}", t)
+            size = int(tup.group(1)) * JL_SIZE[tup.group(2)] if tup else (8 if t.startswith("Ptr") else JL_SIZE[t])
+            out.append((m.group(1), size))
     return out
 
 
