@@ -748,7 +748,13 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         A.lin = (fast & 2048) ? 1 : 0;  // kbench: tiles in address order
         // kbench: one-shot LDS tiles (k_st2t) of 8 / 4 / 16 rows x 128 columns (fast bits 8192 / 16384 / 32768)
         A.tile2 = (fast & 8192) ? 8 : ((fast & 16384) ? 4 : ((fast & 32768) ? 16 : 0));
-        if (A.tile2 && vec == 2) {
+        // fast bit 131072 with a one-shot tile: 256 columns wide (VEC 4), 8 or 4 rows
+        if (A.tile2 && (fast & 131072) && p->nx % 4 == 0 && !per && !(A.tile2 == 16)) {
+            vec = 4;
+            A.tiles_x = (int)((p->nx + 255) / 256);
+            A.tiles_y = (int)((p->ny + A.tile2 - 1) / A.tile2);
+            grid = A.tiles_x * A.tiles_y;
+        } else if (A.tile2 && vec == 2) {
             A.tiles_x = (int)((p->nx + 127) / 128);
             A.tiles_y = (int)((p->ny + A.tile2 - 1) / A.tile2);
             grid = A.tiles_x * A.tiles_y;

@@ -1269,6 +1269,11 @@ void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
         hipLaunchKernelGGL((k_st1d<MODE, EPI>), dim3(grid), dim3(kBlock), 0, s, A);
     } else if constexpr (k2d) {
 #ifdef NK_KBENCH
+        if (A.tile2 && vec == 4) {  // kbench prototype: one-shot LDS tiles 256 columns wide (no F0R / periodic)
+            if (A.tile2 == 4) hipLaunchKernelGGL((k_st2t<KIND, MODE, EPI, 4, false, false, 4>), dim3(grid), dim3(256), 0, s, A);
+            else hipLaunchKernelGGL((k_st2t<KIND, MODE, EPI, 4, false, false, 8>), dim3(grid), dim3(512), 0, s, A);
+            return;
+        }
         if (A.tile2 && vec == 2) {  // kbench prototype: one-shot LDS tiles of A.tile2 rows
             const bool f0r = MODE == MODE_JFD && A.f0r;
             auto go = [&](auto nwc) {
