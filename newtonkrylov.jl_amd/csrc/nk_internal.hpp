@@ -22,6 +22,8 @@ constexpr int kBlock = 256;          // threads per block for every streaming ke
 constexpr int kMaxRedBlocks = 2048;  // partial sums per reduction (8 blocks per CU on 256 CUs)
 constexpr int kRedSlots = 4;         // ring of partial-sum slots
 constexpr int kRedCap = 16384;       // doubles per slot (a stencil launch may have more blocks)
+constexpr int kTileCap = 1 << 19;    // one-shot stencil tiles per launch (per-tile partials before the group fold)
+constexpr int kTileParts = 1024;     // partials a one-shot stencil launch hands on (tiles folded in groups)
 constexpr int kScalCap = 8192;       // device scalar area (Hessenberg column, y, norms)
 constexpr int kMaxUpdateVecs = 32;   // basis vectors folded per x-update launch
 constexpr int kMgsVariant = 5;       // MGS-pass variant (unroll x non-temporal V_i), see mgs_dispatch
@@ -54,6 +56,11 @@ struct nk_ctx {
     std::unordered_map<double*, void*> allocs;  // interior pointer -> allocation base
     double* red = nullptr;                      // kRedSlots * kRedCap partial sums
     double* scal = nullptr;                     // kScalCap device scalars
+    uint64_t* tgran = nullptr;                  // 2 x kTileCap partial granules of a one-shot stencil launch
+    unsigned tile_tag = 0;                      // their tag: one per grouped launch (re-zeroed on wrap)
+    int* tile_err = nullptr;                    // pinned host flag: a group fold's poll timed out
+    int* tile_err_dev = nullptr;
+    bool oneshot_ok = true;                     // false after such a timeout: the row march from then on
     double* hpin = nullptr;                     // kScalCap pinned host scalars
     int red_next = 0;
     // profiling

@@ -746,8 +746,16 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         A.tiles_y = (int)((p->ny + rows - 1) / rows);
         grid = A.tiles_x * A.tiles_y;
         A.lin = (fast & 2048) ? 1 : 0;  // kbench: tiles in address order
-        // kbench: one-shot LDS tiles (k_st2t) of 8 / 4 / 16 rows x 128 columns (fast bits 8192 / 16384 / 32768)
+        // The FD operator runs on one-shot LDS tiles (k_st2t: 8 rows x 128 columns, no march, tiles in
+        // address order; their block partials folded in groups, publish_grouped): 6-12 % faster than the
+        // row march on the Bratu and heat FD Jv + dot (profiles/r03/ab_tile8.log).  The residual and the
+        // exact tangent keep the march.  kbench: fast bits 8192 / 16384 / 32768 force 8 / 4 / 16-row
+        // one-shot tiles for any mode, 262144 forces the march, NK_ST_ONESHOT=0 turns them off.
+        static const int oneshot_env = NK_TUNE("NK_ST_ONESHOT", 0);
         A.tile2 = (fast & 8192) ? 8 : ((fast & 16384) ? 4 : ((fast & 32768) ? 16 : 0));
+        if (!A.tile2 && oneshot_env && c->oneshot_ok && in.mode == MODE_JFD && vec == 2 && !(fast & (262144 | 4 | 2048)) &&
+            rows_override <= 0 && !(oneshot_env == 2 && nk_scheme(p->kind) == 2))
+            A.tile2 = 8;
         // fast bit 131072 with a one-shot tile: 256 columns wide (VEC 4), 8 or 4 rows
         if (A.tile2 && (fast & 131072) && p->nx % 4 == 0 && !per && !(A.tile2 == 16)) {
             vec = 4;
@@ -755,9 +763,16 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
             A.tiles_y = (int)((p->ny + A.tile2 - 1) / A.tile2);
             grid = A.tiles_x * A.tiles_y;
         } else if (A.tile2 && vec == 2) {
-            A.tiles_x = (int)((p->nx + 127) / 128);
-            A.tiles_y = (int)((p->ny + A.tile2 - 1) / A.tile2);
-            grid = A.tiles_x * A.tiles_y;
+            const int tx1 = (int)((p->nx + 127) / 128), ty1 = (int)((p->ny + A.tile2 - 1) / A.tile2);
+            if ((int64_t)tx1 * ty1 <= kTileCap) {
+                A.tiles_x = tx1;
+                A.tiles_y = ty1;
+                grid = A.tiles_x * A.tiles_y;
+            } else {
+                A.tile2 = 0;  // beyond the per-tile partial buffer: the row march
+            }
+        } else {
+            A.tile2 = 0;
         }
     } else {
         vec = (p->nx % 2 == 0) ? 2 : 1;
@@ -823,8 +838,31 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         }
     }
     if (in.epi != EPI_NONE) {
-        if (grid > kRedCap - 2) return fail(c, NK_E_ARG, "stencil grid exceeds reduction capacity");
-        A.part = red_out(c, grid, red, &A.fin);
+        int nparts = grid;
+        A.group = 1;
+        A.ntiles = grid;
+        static const int tile_parts = std::max(1, std::min(kRedCap - 2, NK_TUNE("NK_TILE_PARTS", kTileParts)));
+        if (A.tile2 && grid > tile_parts) {  // one-shot tiles: about kTileParts group partials handed on
+            int G = (grid + tile_parts - 1) / tile_parts;
+            // band-aligned groups (a divisor or a multiple of the tiles per row band): a group's folder
+            // only waits for tiles dispatched before it, also with the slab-end bands dispatched first
+            if (G <= A.tiles_x) {
+                while (A.tiles_x % G) ++G;
+            } else {
+                G = (G + A.tiles_x - 1) / A.tiles_x * A.tiles_x;
+            }
+            A.group = G;
+            nparts = (grid + G - 1) / G;
+            A.tgran = c->tgran;
+            A.terr = c->tile_err_dev;
+            if (++c->tile_tag == 0) {  // wrapped: no granule may carry a live tag
+                NK_HIP(c, hipMemsetAsync(c->tgran, 0, sizeof(uint64_t) * 2 * (size_t)kTileCap, c->stream));
+                c->tile_tag = 1;
+            }
+            A.ttag = c->tile_tag;
+        }
+        if (nparts > kRedCap - 2) return fail(c, NK_E_ARG, "stencil grid exceeds reduction capacity");
+        A.part = red_out(c, nparts, red, &A.fin);
     }
     // algorithmic (compulsory) bytes per launch
     const bool heat = nk_is_heat(p->kind);

@@ -33,7 +33,11 @@ struct KArgs {
     int lds3;            // 3D: y-neighbour rows through LDS (k_st3l) instead of per-wave loads (k_st3d)
     int lin;             // tiles in dispatch (= address) order instead of XCD-contiguous bands
     int zalt;            // 3D: z-chunks of one tile column dispatched together, odd chunks marching down
-    int tile2;           // kbench: 2D one-shot LDS tiles of tile2 rows (k_st2t) instead of the march
+    int tile2;           // 2D one-shot LDS tiles of tile2 rows (k_st2t) instead of the row march (0: march)
+    uint64_t* tgran;     // one-shot tiles: per-tile partial granules, folded in groups of `group` tiles
+    int* terr;           //   (publish_grouped): tag of this launch, pinned timeout flag
+    unsigned ttag;
+    int group, ntiles;
     int f0r;             // 2D FD: F0 = F(u) recomputed from the u rows already loaded (k_st2d<..., F0R>)
     // ghost planes of v through the peers' inboxes inside this launch (halo_tile_exchange): the rank
     // has a lower / upper neighbour whose boundary patch this launch fetches itself
@@ -747,7 +751,8 @@ __global__ __launch_bounds__(64 * NW) void k_st2t(KArgs A0) {
     __shared__ double lg[kTG ? NW + 2 : 1][kTG ? W : 1];
     __shared__ double lu[kR ? NW + 2 : 1][kR ? W : 1];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int t = blockIdx.x;
+    // tiles in address order; with ghost rows inside the launch the slab-end row bands first (tile_of)
+    const int t = tile_of(blockIdx.x, gridDim.x, A.tiles_x, A.tiles_y, A.hx_lo, A.hx_hi, 1);
     const int tx = t % A.tiles_x, ty = t / A.tiles_x;
     const int64_t nx = A.nx, ny = A.ny;
     const int64_t x0 = (int64_t)tx * W + (int64_t)lane * VEC;
@@ -766,6 +771,20 @@ __global__ __launch_bounds__(64 * NW) void k_st2t(KArgs A0) {
     // the rows this block's LDS holds: y0 - 1 .. y0 + NW (capped at ny, the upper ghost row)
     const bool own = j <= ny;                           // row ny (ghost) only as a neighbour
     const bool lo_halo = wv == 0, hi_halo = wv == NW - 1 && y0 + NW <= ny;
+    // ghost rows of v from the neighbours' patches, fetched by this launch (row bands at the slab's ends)
+    const uint64_t* ib_lo = nullptr;
+    const uint64_t* ib_hi = nullptr;
+    if constexpr (MODE != MODE_RES && !PER) {
+        const HaloTile ht{A.hx_lo && y0 == 0, A.hx_hi && y0 + NW >= ny && y0 < ny};
+        if (ht.lo || ht.hi) {  // block-uniform
+            const int64_t ca = (int64_t)tx * W, cb = ca + W < nx ? ca + W : nx;
+            if (halo_tile_exchange(A.v, nx, ny, nx, 0, 1, ca, cb, tx, ht, A.hx_epoch, A.hx_cap, 64 * NW)) {
+                const int par = (int)(A.hx_epoch & 1);
+                if (ht.lo) ib_lo = halo_inbox(g_mb.self, par, 0, A.hx_cap);
+                if (ht.hi) ib_hi = halo_inbox(g_mb.self, par, 1, A.hx_cap);
+            }
+        }
+    }
     auto raw_of = [&](int64_t r) {
         const int64_t o = r * nx + xc;
         return load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, o, o + de, o + de2);
@@ -790,6 +809,13 @@ __global__ __launch_bounds__(64 * NW) void k_st2t(KArgs A0) {
     if (own) rown = raw_of(j);
     if (lo_halo) rlo = raw_of(y0 - 1);
     if (hi_halo) rhi = raw_of(y0 + NW);
+    // the slab-end tiles of an in-launch exchange: the ghost row (-1 / ny) comes from the inbox instead
+    // (kept out of the loads above: a per-load branch there serialises their issue)
+    if (ib_lo && lo_halo) rlo = load_raw_ib<MODE, VEC, kG>(A, ib_lo, -nx + xc, xc);
+    if (ib_hi) {
+        if (own && j == ny) rown = load_raw_ib<MODE, VEC, kG>(A, ib_hi, ny * nx + xc, xc);
+        if (hi_halo && y0 + NW == ny) rhi = load_raw_ib<MODE, VEC, kG>(A, ib_hi, ny * nx + xc, xc);
+    }
     Row<VEC> uc{}, unc{}, f0c{}, ax{};
     const bool comp = j < ny;
     if (comp) {
@@ -849,7 +875,10 @@ __global__ __launch_bounds__(64 * NW) void k_st2t(KArgs A0) {
             store_row<VEC, NK_ST_NT>(A.vout, o, vn);
         }
     }
-    if constexpr (EPI != EPI_NONE) publish<64 * NW>(acc, A.part, A.fin, sh);
+    if constexpr (EPI != EPI_NONE) {
+        if (A.group > 1) publish_grouped<64 * NW>(acc, A.tgran, A.ttag, A.group, A.ntiles, A.part, A.fin, sh, t, A.terr);
+        else publish<64 * NW>(acc, A.part, A.fin, sh, t);
+    }
 }
 
 // ------------------------------------------------------------------------------ 3D stencil
@@ -1268,31 +1297,40 @@ void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
     if constexpr (KIND == NK_BRATU1D) {
         hipLaunchKernelGGL((k_st1d<MODE, EPI>), dim3(grid), dim3(kBlock), 0, s, A);
     } else if constexpr (k2d) {
+        // one-shot LDS tiles (k_st2t): the FD operator's product path, 8 rows x 128 columns (the launcher
+        // decides: A.tile2 = 8); the kernel-variant build also has 4 / 16 rows and 256-column tiles
+        auto go = [&](auto nwc) {
+            constexpr int NWc = decltype(nwc)::value;
+            const bool f0r = MODE == MODE_JFD && A.f0r;
+            if (per) {
+                if constexpr (heat_kind<KIND>()) {
+                    if (f0r) hipLaunchKernelGGL((k_st2t<KIND, MODE, EPI, 2, true, true, NWc>), dim3(grid), dim3(64 * NWc), 0, s, A);
+                    else hipLaunchKernelGGL((k_st2t<KIND, MODE, EPI, 2, true, false, NWc>), dim3(grid), dim3(64 * NWc), 0, s, A);
+                }
+            } else if (f0r) {
+                hipLaunchKernelGGL((k_st2t<KIND, MODE, EPI, 2, false, true, NWc>), dim3(grid), dim3(64 * NWc), 0, s, A);
+            } else {
+                hipLaunchKernelGGL((k_st2t<KIND, MODE, EPI, 2, false, false, NWc>), dim3(grid), dim3(64 * NWc), 0, s, A);
+            }
+        };
 #ifdef NK_KBENCH
         if (A.tile2 && vec == 4) {  // kbench prototype: one-shot LDS tiles 256 columns wide (no F0R / periodic)
             if (A.tile2 == 4) hipLaunchKernelGGL((k_st2t<KIND, MODE, EPI, 4, false, false, 4>), dim3(grid), dim3(256), 0, s, A);
             else hipLaunchKernelGGL((k_st2t<KIND, MODE, EPI, 4, false, false, 8>), dim3(grid), dim3(512), 0, s, A);
             return;
         }
-        if (A.tile2 && vec == 2) {  // kbench prototype: one-shot LDS tiles of A.tile2 rows
-            const bool f0r = MODE == MODE_JFD && A.f0r;
-            auto go = [&](auto nwc) {
-                constexpr int NWc = decltype(nwc)::value;
-                if (per) {
-                    if constexpr (heat_kind<KIND>()) {
-                        if (f0r) hipLaunchKernelGGL((k_st2t<KIND, MODE, EPI, 2, true, true, NWc>), dim3(grid), dim3(64 * NWc), 0, s, A);
-                        else hipLaunchKernelGGL((k_st2t<KIND, MODE, EPI, 2, true, false, NWc>), dim3(grid), dim3(64 * NWc), 0, s, A);
-                    }
-                } else if (f0r) {
-                    hipLaunchKernelGGL((k_st2t<KIND, MODE, EPI, 2, false, true, NWc>), dim3(grid), dim3(64 * NWc), 0, s, A);
-                } else {
-                    hipLaunchKernelGGL((k_st2t<KIND, MODE, EPI, 2, false, false, NWc>), dim3(grid), dim3(64 * NWc), 0, s, A);
-                }
-            };
+        if (A.tile2 && vec == 2) {  // every mode (the launcher picks one-shot tiles for the FD operator only)
             if (A.tile2 == 16) go(std::integral_constant<int, 16>{});
             else if (A.tile2 == 4) go(std::integral_constant<int, 4>{});
             else go(std::integral_constant<int, 8>{});
             return;
+        }
+#else
+        if constexpr (MODE == MODE_JFD) {
+            if (A.tile2 == 8 && vec == 2) {
+                go(std::integral_constant<int, 8>{});
+                return;
+            }
         }
 #endif
         if constexpr (heat_kind<KIND>()) {  // bc_periodic! instantiations: heat only, VEC <= 2

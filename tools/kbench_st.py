@@ -18,6 +18,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--kinds", default="3,5,7")
 ap.add_argument("--side", type=int, default=8192)
 ap.add_argument("--nz", type=int, default=0, help="3D kinds: planes (default side)")
+ap.add_argument("--ny", type=int, default=0, help="rows (default side)")
 ap.add_argument("--modes", default="0:1,2:2", help="mode:epi pairs (0:1 residual+norm, 2:2 FD Jv+dot)")
 ap.add_argument("--rows", default="0,16,32,64,128")
 ap.add_argument("--fast", default="0,4", help="variant bits: 1 reciprocals for the divisions (not bit-faithful), "
@@ -54,13 +55,13 @@ for _ in range(args.rounds):
             for rows in map(int, args.rows.split(",")):
                 for fast in map(int, args.fast.split(",")):
                     t = C.c_double()
-                    rc = lib.nkb_stencil_kind(ctx.handle, kind, args.side, args.side, nz, mode, epi, rows, fast,
+                    rc = lib.nkb_stencil_kind(ctx.handle, kind, args.side, args.ny or args.side, nz, mode, epi, rows, fast,
                                               args.reps, C.byref(t))
                     assert rc == 0, (kind, mode, epi, rows, fast, rc)
                     res.setdefault((kind, mode, epi, rows, fast, nz), []).append(t.value)
 print(f"stencils at {args.side}^2 (x nz): median us per launch over {args.rounds} interleaved rounds")
 for (kind, mode, epi, rows, fast, nz), v in res.items():
     us = statistics.median(v)
-    gb = 8.0 * words(kind, mode, epi, fast) * args.side * args.side * nz / us / 1e3
+    gb = 8.0 * words(kind, mode, epi, fast) * args.side * (args.ny or args.side) * nz / us / 1e3
     print(f"{NAME[kind]:17s} {MODE.get((mode, epi), f'{mode}:{epi}'):14s} rows={rows:4d} fast={fast:2d}"
           f"  {us:9.1f} us  {gb:7.1f} GB/s  ({gb / 80:5.1f}% of 8 TB/s)")
