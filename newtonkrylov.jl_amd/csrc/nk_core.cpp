@@ -80,11 +80,6 @@ int mb_check(nk_ctx* c) {
         c->res_ok = false;  // later solves use one launch per MGS pass
         return fail(c, NK_E_HIP, "resident MGS sweep: a block's partial sum never arrived (timeout); resident sweep disabled");
     }
-    if (c->tile_err && *(volatile int*)c->tile_err) {  // a one-shot stencil's group fold never saw a tile
-        *c->tile_err = 0;
-        c->oneshot_ok = false;  // later launches use the row march
-        return fail(c, NK_E_HIP, "one-shot stencil: a tile's partial sum never arrived (timeout); one-shot tiles disabled");
-    }
     if (c->ilu_err && *(volatile int*)c->ilu_err) {  // a strip of the pipelined ILU(0) sweep never advanced
         *c->ilu_err = 0;
         c->ilu_pipe_ok = false;  // later sweeps use the one-work-group level sweep
@@ -207,13 +202,6 @@ int nk_ctx_create(int device, nk_ctx** out) {
     if (hipHostMalloc(&c->hpin, sizeof(double) * kScalCap, hipHostMallocDefault) != hipSuccess) return bail(NK_E_NOMEM);
     if (hipMemset(c->red, 0, sizeof(double) * (size_t)kRedSlots * kRedCap) != hipSuccess) return bail(NK_E_HIP);
     if (hipMemset(c->scal, 0, sizeof(double) * kScalCap) != hipSuccess) return bail(NK_E_HIP);
-    // one-shot stencil tiles: the partial granules of their group fold (publish_grouped) + its timeout flag
-    if (hipMalloc(&c->tgran, sizeof(uint64_t) * 2 * (size_t)kTileCap) != hipSuccess) return bail(NK_E_NOMEM);
-    if (hipMemset(c->tgran, 0, sizeof(uint64_t) * 2 * (size_t)kTileCap) != hipSuccess) return bail(NK_E_HIP);
-    if (hipHostMalloc(&c->tile_err, sizeof(int), hipHostMallocMapped) != hipSuccess) return bail(NK_E_NOMEM);
-    *c->tile_err = 0;
-    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&c->tile_err_dev), c->tile_err, 0) != hipSuccess)
-        return bail(NK_E_HIP);
     *out = c;
     return NK_OK;
 }
@@ -233,8 +221,7 @@ int nk_ctx_destroy(nk_ctx* c) {
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     (void)hipFree(c->red);
     (void)hipFree(c->scal);
-    (void)hipFree(c->tgran);
-    if (c->tile_err) (void)hipHostFree(c->tile_err);
+    if (c->tpart) (void)hipFree(c->tpart);
     (void)hipHostFree(c->hpin);
     if (c->res_gran) (void)hipFree(c->res_gran);
     if (c->res_err) (void)hipHostFree(c->res_err);

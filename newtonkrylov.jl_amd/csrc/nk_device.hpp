@@ -200,61 +200,6 @@ __device__ __forceinline__ void publish(double acc, double* part, int fin, doubl
     const double s = block_sum<NT>(acc, sh);
     publish_sum<NT>(s, part, fin, sh, slot < 0 ? (int)blockIdx.x : slot, (int)gridDim.x);
 }
-// Tile partials folded in groups of G tiles, for grids with far more tiles than the next kernel should
-// read partials (the one-shot stencil tiles: 16 Ki tiles at 4096^2).  Every tile but the last of its
-// group publishes its block sum as two self-validating {tag:32 | half:32} granules (the resident
-// sweep's hand-off form: the data is the flag, no fence, no returning atomic -- the block retires at
-// once); the group's last tile polls the others' granules and sums the group in tile order (lane l
-// takes tiles l, l + 64, ... then a fixed wave tree) and publishes that as partial g of ngroups.  Its
-// polls only wait for tiles of lower index, i.e. blocks dispatched before it (address order; the
-// host makes groups band-aligned so the slab-end-first dispatch keeps that); every poll is bounded
-// (then *err and the sum of what arrived).  The result does not depend on arrival order.
-template <int NT>
-__device__ __forceinline__ void publish_grouped(double acc, uint64_t* gran, unsigned tag, int G, int ntiles, double* part,
-                                                int fin, double* sh, int tile, int* err) {
-    __shared__ double self;
-    const double s = block_sum<NT>(acc, sh);
-    const int g = tile / G, g0 = g * G, m = (ntiles - g0) < G ? ntiles - g0 : G;
-    if (tile != g0 + m - 1) {  // not the group's folder: publish and retire
-        if (threadIdx.x == 0) {
-            const uint64_t bits = (uint64_t)__double_as_longlong(s);
-            __hip_atomic_store(gran + 2 * (size_t)tile, ((uint64_t)tag << 32) | (bits & 0xffffffffull), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(gran + 2 * (size_t)tile + 1, ((uint64_t)tag << 32) | (bits >> 32), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return;
-    }
-    if (threadIdx.x == 0) self = s;
-    __syncthreads();
-    double v = 0.0;
-    if (threadIdx.x < 64) {
-        for (int i = (int)threadIdx.x; i < m; i += 64) {
-            double x = self;
-            if (i < m - 1) {
-                const uint64_t* gp = gran + 2 * (size_t)(g0 + i);
-                uint64_t lo = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                uint64_t hi = __hip_atomic_load(gp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                unsigned spins = 0;
-                while ((unsigned)(lo >> 32) != tag || (unsigned)(hi >> 32) != tag) {
-                    if (++spins > (1u << 24)) {
-                        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                        lo = hi = 0;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    lo = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    hi = __hip_atomic_load(gp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                x = __longlong_as_double((long long)(((hi & 0xffffffffull) << 32) | (lo & 0xffffffffull)));
-            }
-            v += x;
-        }
-        v = wave_sum(v);
-    }
-    publish_sum<NT>(v, part, fin, sh, g, (ntiles + G - 1) / G);
-}
-
 __device__ __forceinline__ double lap(double c, double p, double m, double h2) { return ((p - 2.0 * c) + m) / h2; }
 
 // ------------------------------------------------------------------------------ peer ghost planes

@@ -56,11 +56,7 @@ struct nk_ctx {
     std::unordered_map<double*, void*> allocs;  // interior pointer -> allocation base
     double* red = nullptr;                      // kRedSlots * kRedCap partial sums
     double* scal = nullptr;                     // kScalCap device scalars
-    uint64_t* tgran = nullptr;                  // 2 x kTileCap partial granules of a one-shot stencil launch
-    unsigned tile_tag = 0;                      // their tag: one per grouped launch (re-zeroed on wrap)
-    int* tile_err = nullptr;                    // pinned host flag: a group fold's poll timed out
-    int* tile_err_dev = nullptr;
-    bool oneshot_ok = true;                     // false after such a timeout: the row march from then on
+    double* tpart = nullptr;                    // kTileCap per-tile partials of a one-shot stencil launch
     double* hpin = nullptr;                     // kScalCap pinned host scalars
     int red_next = 0;
     // profiling

@@ -610,6 +610,20 @@ __global__ __launch_bounds__(kBlock) void k_halo_ipc(double* __restrict__ v, int
     }
 }
 
+// The per-tile partials of a one-shot stencil launch (more tiles than the next kernel should read
+// partials) folded in groups of G tiles: block g sums tiles gG .. gG + G - 1 in tile order (lane l
+// takes l, l + 64, ..., then a fixed wave tree) and hands the sum on as partial g -- with `fin` the
+// last block also folds the partials, as the stencil itself would (publish_sum).  Bit-reproducible.
+__global__ __launch_bounds__(64) void k_tile_fold(const double* __restrict__ tpart, int G, int ntiles, double* part,
+                                                  int fin) {
+    __shared__ double sh[kShN];
+    const int g = blockIdx.x, g0 = g * G, m = (ntiles - g0) < G ? ntiles - g0 : G;
+    double v = 0.0;
+    for (int i = (int)threadIdx.x; i < m; i += 64) v += tpart[g0 + i];
+    v = wave_sum(v);
+    publish_sum<64>(v, part, fin, sh, g, (int)gridDim.x);
+}
+
 // bc_periodic! along the slab axis of a lone slab: ghost plane -1 <- the last interior plane,
 // ghost plane nplanes <- the first (heat_2D.jl:20-21 / 23-24)
 __global__ __launch_bounds__(kBlock) void k_periodic_fill(double* __restrict__ v, int64_t plane, int64_t nplanes) {
@@ -746,14 +760,14 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         A.tiles_y = (int)((p->ny + rows - 1) / rows);
         grid = A.tiles_x * A.tiles_y;
         A.lin = (fast & 2048) ? 1 : 0;  // kbench: tiles in address order
-        // The FD operator runs on one-shot LDS tiles (k_st2t: 8 rows x 128 columns, no march, tiles in
-        // address order; their block partials folded in groups, publish_grouped): 6-12 % faster than the
-        // row march on the Bratu and heat FD Jv + dot (profiles/r03/ab_tile8.log).  The residual and the
-        // exact tangent keep the march.  kbench: fast bits 8192 / 16384 / 32768 force 8 / 4 / 16-row
-        // one-shot tiles for any mode, 262144 forces the march, NK_ST_ONESHOT=0 turns them off.
+        // kbench only: one-shot LDS tiles (k_st2t: 8 rows x 128 columns, no march, tiles in address
+        // order, block partials folded by k_tile_fold) for the FD operator (NK_ST_ONESHOT=1), or for any
+        // mode with fast bits 8192 / 16384 / 32768 (8 / 4 / 16 rows); 262144 forces the march.  8-12 %
+        // faster than the march in isolation (profiles/r03/ab_tile8.log, ab_oneshot_fold2.log), but not in
+        // the bench (ab_oneshot4.log): the product keeps the march.
         static const int oneshot_env = NK_TUNE("NK_ST_ONESHOT", 0);
         A.tile2 = (fast & 8192) ? 8 : ((fast & 16384) ? 4 : ((fast & 32768) ? 16 : 0));
-        if (!A.tile2 && oneshot_env && c->oneshot_ok && in.mode == MODE_JFD && vec == 2 && !(fast & (262144 | 4 | 2048)) &&
+        if (!A.tile2 && oneshot_env && in.mode == MODE_JFD && vec == 2 && !(fast & (262144 | 4 | 2048)) &&
             rows_override <= 0 && !(oneshot_env == 2 && nk_scheme(p->kind) == 2))
             A.tile2 = 8;
         // fast bit 131072 with a one-shot tile: 256 columns wide (VEC 4), 8 or 4 rows
@@ -840,26 +854,13 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     if (in.epi != EPI_NONE) {
         int nparts = grid;
         A.group = 1;
-        A.ntiles = grid;
         static const int tile_parts = std::max(1, std::min(kRedCap - 2, NK_TUNE("NK_TILE_PARTS", kTileParts)));
         if (A.tile2 && grid > tile_parts) {  // one-shot tiles: about kTileParts group partials handed on
-            int G = (grid + tile_parts - 1) / tile_parts;
-            // band-aligned groups (a divisor or a multiple of the tiles per row band): a group's folder
-            // only waits for tiles dispatched before it, also with the slab-end bands dispatched first
-            if (G <= A.tiles_x) {
-                while (A.tiles_x % G) ++G;
-            } else {
-                G = (G + A.tiles_x - 1) / A.tiles_x * A.tiles_x;
-            }
-            A.group = G;
-            nparts = (grid + G - 1) / G;
-            A.tgran = c->tgran;
-            A.terr = c->tile_err_dev;
-            if (++c->tile_tag == 0) {  // wrapped: no granule may carry a live tag
-                NK_HIP(c, hipMemsetAsync(c->tgran, 0, sizeof(uint64_t) * 2 * (size_t)kTileCap, c->stream));
-                c->tile_tag = 1;
-            }
-            A.ttag = c->tile_tag;
+            A.group = (grid + tile_parts - 1) / tile_parts;
+            nparts = (grid + A.group - 1) / A.group;
+            if (!c->tpart && hipMalloc(&c->tpart, sizeof(double) * (size_t)kTileCap) != hipSuccess)
+                return fail(c, NK_E_NOMEM, "one-shot tile partials");
+            A.tpart = c->tpart;
         }
         if (nparts > kRedCap - 2) return fail(c, NK_E_ARG, "stencil grid exceeds reduction capacity");
         A.part = red_out(c, nparts, red, &A.fin);
@@ -897,6 +898,10 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         case NK_HEAT3D_MIDPOINT: stencil_kind_6(A, mode, epi, vec, grid, s, per); break;
         case NK_HEAT2D_TRAPEZOID: stencil_kind_7(A, mode, epi, vec, grid, s, per); break;
         default: stencil_kind_8(A, mode, epi, vec, grid, s, per); break;
+        }
+        if (A.group > 1) {  // one-shot tiles: the group sums in tile order, as the next kernel's partials
+            const int ng = (grid + A.group - 1) / A.group;
+            hipLaunchKernelGGL(k_tile_fold, dim3(ng), dim3(64), 0, s, A.tpart, A.group, grid, A.part, A.fin);
         }
     });
 }

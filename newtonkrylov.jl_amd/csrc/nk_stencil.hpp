@@ -34,10 +34,8 @@ struct KArgs {
     int lin;             // tiles in dispatch (= address) order instead of XCD-contiguous bands
     int zalt;            // 3D: z-chunks of one tile column dispatched together, odd chunks marching down
     int tile2;           // 2D one-shot LDS tiles of tile2 rows (k_st2t) instead of the row march (0: march)
-    uint64_t* tgran;     // one-shot tiles: per-tile partial granules, folded in groups of `group` tiles
-    int* terr;           //   (publish_grouped): tag of this launch, pinned timeout flag
-    unsigned ttag;
-    int group, ntiles;
+    double* tpart;       // one-shot tiles with more tiles than kTileParts: per-tile partials (plain stores),
+    int group;           //   folded in groups of `group` tiles by k_tile_fold right after the stencil launch
     int f0r;             // 2D FD: F0 = F(u) recomputed from the u rows already loaded (k_st2d<..., F0R>)
     // ghost planes of v through the peers' inboxes inside this launch (halo_tile_exchange): the rank
     // has a lower / upper neighbour whose boundary patch this launch fetches itself
@@ -876,8 +874,12 @@ __global__ __launch_bounds__(64 * NW) void k_st2t(KArgs A0) {
         }
     }
     if constexpr (EPI != EPI_NONE) {
-        if (A.group > 1) publish_grouped<64 * NW>(acc, A.tgran, A.ttag, A.group, A.ntiles, A.part, A.fin, sh, t, A.terr);
-        else publish<64 * NW>(acc, A.part, A.fin, sh, t);
+        if (A.group > 1) {  // per-tile partial; k_tile_fold hands on the group sums
+            const double bs = block_sum<64 * NW>(acc, sh);
+            if (threadIdx.x == 0) A.tpart[t] = bs;
+        } else {
+            publish<64 * NW>(acc, A.part, A.fin, sh, t);
+        }
     }
 }
 
@@ -1297,8 +1299,8 @@ void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
     if constexpr (KIND == NK_BRATU1D) {
         hipLaunchKernelGGL((k_st1d<MODE, EPI>), dim3(grid), dim3(kBlock), 0, s, A);
     } else if constexpr (k2d) {
-        // one-shot LDS tiles (k_st2t): the FD operator's product path, 8 rows x 128 columns (the launcher
-        // decides: A.tile2 = 8); the kernel-variant build also has 4 / 16 rows and 256-column tiles
+        // one-shot LDS tiles (k_st2t, kernel-variant build only: NK_ST_ONESHOT / fast bits): 8 rows x 128
+        // columns, also 4 / 16 rows and 256-column tiles -- faster in isolation, not in the bench
         auto go = [&](auto nwc) {
             constexpr int NWc = decltype(nwc)::value;
             const bool f0r = MODE == MODE_JFD && A.f0r;
@@ -1326,12 +1328,7 @@ void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
             return;
         }
 #else
-        if constexpr (MODE == MODE_JFD) {
-            if (A.tile2 == 8 && vec == 2) {
-                go(std::integral_constant<int, 8>{});
-                return;
-            }
-        }
+        (void)go;
 #endif
         if constexpr (heat_kind<KIND>()) {  // bc_periodic! instantiations: heat only, VEC <= 2
             if (per) {
