@@ -140,6 +140,7 @@ def cpu_thread_probe(affinity, share):
             oc.dot(w, v)
             oc.norm(w)
         probe[t] = round(time.perf_counter() - t0, 4)
+        log(f"cpu thread probe: {t} threads {probe[t]:.3f} s")
         if best is None or probe[t] < probe[best]:
             best = t
         elif probe[t] > 1.5 * probe[best] or probe[t] > 10.0:
