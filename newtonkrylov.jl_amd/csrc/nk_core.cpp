@@ -248,12 +248,17 @@ int nk_vec_alloc(nk_ctx* c, const nk_problem* p, double** out) {
     if (!c || !out) return NK_E_ARG;
     Geo g;
     NK_TRY(geometry(c, p, &g));
-    const size_t total = (size_t)(g.front + g.n + g.plane + 32);
+    // start offset: vector j's interior begins (j mod 8) x stagger bytes further into its allocation,
+    // so that the same index of the fields a kernel streams together does not fall on the same
+    // address bits (hipMalloc hands out 2 MB-aligned blocks)
+    static const int stagger = NK_TUNE("NK_ALLOC_STAGGER", 0);
+    const size_t shift = stagger > 0 ? (size_t)(c->alloc_seq++ % 8u) * ((size_t)stagger / 256 * 32) : 0;  // doubles
+    const size_t total = (size_t)(g.front + g.n + g.plane + 32) + shift;
     void* base = nullptr;
     if (hipMalloc(&base, total * sizeof(double)) != hipSuccess) return fail(c, NK_E_NOMEM, "hipMalloc failed (vector)");
     NK_HIP(c, hipMemsetAsync(base, 0, total * sizeof(double), c->stream));
     NK_HIP(c, hipStreamSynchronize(c->stream));
-    double* interior = static_cast<double*>(base) + g.front;
+    double* interior = static_cast<double*>(base) + g.front + shift;
     c->allocs[interior] = base;
     *out = interior;
     return NK_OK;

@@ -54,6 +54,7 @@ struct nk_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     std::unordered_map<double*, void*> allocs;  // interior pointer -> allocation base
+    unsigned alloc_seq = 0;                     // vectors allocated so far (their start offsets, §3)
     double* red = nullptr;                      // kRedSlots * kRedCap partial sums
     double* scal = nullptr;                     // kScalCap device scalars
     double* tpart = nullptr;                    // kTileCap per-tile partials of a one-shot stencil launch

@@ -1756,7 +1756,11 @@ extern "C" int nkb_copy(nk_ctx* c, int64_t n, int reps, double* us_out) {
     if (!c || n < 2 || reps < 1 || !us_out) return NK_E_ARG;
     double *x = nullptr, *y = nullptr;
     NK_HIP(c, hipMalloc(&x, sizeof(double) * n));
-    NK_HIP(c, hipMalloc(&y, sizeof(double) * n));
+    // NK_ALLOC_STAGGER=<bytes>: y starts that far into its allocation (the vector start-offset probe, §3)
+    const size_t ys = (size_t)std::max(0, NK_TUNE("NK_ALLOC_STAGGER", 0)) / 256 * 32;
+    NK_HIP(c, hipMalloc(&y, sizeof(double) * (n + ys)));
+    double* const ybase = y;
+    y += ys;
     NK_HIP(c, hipMemsetAsync(x, 0, sizeof(double) * n, c->stream));
     hipEvent_t a, b;
     NK_HIP(c, hipEventCreate(&a));
@@ -1779,7 +1783,7 @@ extern "C" int nkb_copy(nk_ctx* c, int64_t n, int reps, double* us_out) {
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     (void)hipFree(x);
-    (void)hipFree(y);
+    (void)hipFree(ybase);
     return NK_OK;
 }
 
