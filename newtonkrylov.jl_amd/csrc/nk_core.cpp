@@ -248,10 +248,12 @@ int nk_vec_alloc(nk_ctx* c, const nk_problem* p, double** out) {
     if (!c || !out) return NK_E_ARG;
     Geo g;
     NK_TRY(geometry(c, p, &g));
-    // start offset: vector j's interior begins (j mod 8) x stagger bytes further into its allocation,
-    // so that the same index of the fields a kernel streams together does not fall on the same
-    // address bits (hipMalloc hands out 2 MB-aligned blocks)
-    static const int stagger = NK_TUNE("NK_ALLOC_STAGGER", 0);
+    // start offset: vector j's interior begins (j mod 8) x 128 KB further into its allocation, so that
+    // the same index of the fields a kernel streams together (V_i and V_i+1 of an MGS pass; u, v, F0,
+    // V_1 of the Jv) does not fall on the same address bits 17-19 (hipMalloc hands out 2 MB-aligned
+    // blocks): Bratu 4096^2 +2.1 %, the sweep -2.6 % (profiles/r03/ab_stagger2.log; 256 KB or 1 MB
+    // steps gain nothing).  Addresses only: every result is bit-identical.
+    static const int stagger = NK_TUNE("NK_ALLOC_STAGGER", 131072);
     const size_t shift = stagger > 0 ? (size_t)(c->alloc_seq++ % 8u) * ((size_t)stagger / 256 * 32) : 0;  // doubles
     const size_t total = (size_t)(g.front + g.n + g.plane + 32) + shift;
     void* base = nullptr;
