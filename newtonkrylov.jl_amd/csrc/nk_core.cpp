@@ -2,6 +2,7 @@
 // Jacobian operator and Krylov vector primitives (include/nkhip.h).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstring>
@@ -254,7 +255,8 @@ int nk_vec_alloc(nk_ctx* c, const nk_problem* p, double** out) {
     // blocks): Bratu 4096^2 +2.1 %, the sweep -2.6 % (profiles/r03/ab_stagger2.log; 256 KB or 1 MB
     // steps gain nothing).  Addresses only: every result is bit-identical.
     static const int stagger = NK_TUNE("NK_ALLOC_STAGGER", 131072);
-    const size_t shift = stagger > 0 ? (size_t)(c->alloc_seq++ % 8u) * ((size_t)stagger / 256 * 32) : 0;  // doubles
+    static const unsigned smod = (unsigned)std::max(1, NK_TUNE("NK_ALLOC_STAGGER_MOD", 8));
+    const size_t shift = stagger > 0 ? (size_t)(c->alloc_seq++ % smod) * ((size_t)stagger / 256 * 32) : 0;  // doubles
     const size_t total = (size_t)(g.front + g.n + g.plane + 32) + shift;
     void* base = nullptr;
     if (hipMalloc(&base, total * sizeof(double)) != hipSuccess) return fail(c, NK_E_NOMEM, "hipMalloc failed (vector)");
