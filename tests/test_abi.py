@@ -26,7 +26,8 @@ def test_library_built_in_tree():
 
 
 KNOBS = ["NK_RES_NOXCHG", "NK_RES_JV", "NK_RES_STRIDED", "NK_RES_NTC", "NK_RES_PRE", "NK_F0R",
-         "NK_ST_BLOCKS", "NK_MGS_VARIANT", "NK_HALO_FUSE", "NK_RED_BLOCKS", "NK_UPD_U"]
+         "NK_ST_BLOCKS", "NK_MGS_VARIANT", "NK_HALO_FUSE", "NK_RED_BLOCKS", "NK_UPD_U",
+         "NK_ALLOC_STAGGER", "NK_ALLOC_STAGGER_MOD"]
 
 
 def test_product_library_has_no_kbench_hooks_or_knobs():

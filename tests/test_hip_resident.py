@@ -307,7 +307,9 @@ def test_sweep_load_flavours_are_bitwise(tmp_path):
     -- the Infinity-Cache room given to the first streamed slots (NK_RES_NTC), the non-temporal
     streamed remainder (NK_RES_NTS), the first batch loaded across the hand-off (NK_RES_PRE) -- never
     the arithmetic or its order: restarted GMRES with reorthogonalisation, bit for bit -- the product
-    library against the kernel-variant bench build (lib/libnkhip_kbench.so) with each knob flipped."""
+    library against the kernel-variant bench build (lib/libnkhip_kbench.so) with each knob flipped.
+    The vectors' start offsets likewise move addresses only: off, or cycling over two
+    vectors instead of eight, the same bits."""
     import os
     import subprocess
     import sys
@@ -317,7 +319,8 @@ def test_sweep_load_flavours_are_bitwise(tmp_path):
     kb = {"NK_KBENCH_LIB": "1"}  # the knobs are read by the kernel-variant bench build only
     for name, extra in [("default", {}), ("kbench", kb), ("ntc0", dict(kb, NK_RES_NTC="0")),
                         ("ntc_all", dict(kb, NK_RES_NTC="100000")), ("nts0", dict(kb, NK_RES_NTS="0")),
-                        ("pre0", dict(kb, NK_RES_PRE="0"))]:
+                        ("pre0", dict(kb, NK_RES_PRE="0")), ("offsets0", dict(kb, NK_ALLOC_STAGGER="0")),
+                        ("offsets2", dict(kb, NK_ALLOC_STAGGER_MOD="2"))]:
         out = tmp_path / f"{name}.npz"
         r = subprocess.run([sys.executable, "-c", _FLAVOUR_CHILD, tests, str(out)], env=dict(os.environ, **extra),
                            capture_output=True, text=True, timeout=240)
