@@ -256,7 +256,9 @@ int nk_vec_alloc(nk_ctx* c, const nk_problem* p, double** out) {
     // steps gain nothing).  Addresses only: every result is bit-identical.
     static const int stagger = NK_TUNE("NK_ALLOC_STAGGER", 131072);
     static const unsigned smod = (unsigned)std::max(1, NK_TUNE("NK_ALLOC_STAGGER_MOD", 8));
-    const size_t shift = stagger > 0 ? (size_t)(c->alloc_seq++ % smod) * ((size_t)stagger / 256 * 32) : 0;  // doubles
+    // (vectors under 2 MB live in sub-allocated pools: no offset, no wasted room)
+    const bool big = (size_t)g.n * sizeof(double) >= ((size_t)2 << 20);
+    const size_t shift = stagger > 0 && big ? (size_t)(c->alloc_seq++ % smod) * ((size_t)stagger / 256 * 32) : 0;  // doubles
     const size_t total = (size_t)(g.front + g.n + g.plane + 32) + shift;
     void* base = nullptr;
     if (hipMalloc(&base, total * sizeof(double)) != hipSuccess) return fail(c, NK_E_NOMEM, "hipMalloc failed (vector)");
