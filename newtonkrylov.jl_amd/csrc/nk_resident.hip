@@ -43,6 +43,7 @@ struct ResArgs {
     int ntc;               // NTS: the first ntc streamed slots of a block load V_{i+1} cached (Infinity Cache room)
     int poll1;             // 1: one polling wave (NK_RES_POLL1, default 1), 2: four staggered polling waves, 0: every thread polls one partial
     int strided;           // slots interleaved across blocks (every block exactly full: no streamed remainder)
+    int mirror;            // kbench: odd blocks map slot s to the chunk's slot S-1-s (every block exactly full)
     uint64_t* tstamp;      // kernel-variant bench only: per pass and block, wall clock at pass end and after the hand-off
     int senders;           // cross-rank: blocks [0, senders) each send this rank's sum to every rank (identical bits)
     // fused FD Jv (2D Bratu): q = (F(u + eps V_k) - F0) / eps computed into the registers, with the
@@ -413,8 +414,14 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     // slot s of this block: contiguous chunk (base = lo, stride 256) or, with A.strided (every block
     // exactly full), interleaved across the blocks (base = 256 b, stride 256 G) so that every block
     // touches every address region alike
-    const int64_t base = A.strided ? (int64_t)blockIdx.x * kResThreads : lo;
-    const int64_t ss = A.strided ? (int64_t)G * kResThreads : kResThreads;
+    int64_t base = A.strided ? (int64_t)blockIdx.x * kResThreads : lo;
+    int64_t ss = A.strided ? (int64_t)G * kResThreads : kResThreads;
+#ifdef NK_KBENCH
+    if (A.mirror && (blockIdx.x & 1)) {  // odd blocks walk their chunk from the top: another address phase
+        base = hi - kResThreads;
+        ss = -(int64_t)kResThreads;
+    }
+#endif
     ResState<RV> S;
     ResPre<B> P;
     double h;
@@ -621,6 +628,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         // slots interleaved across the blocks (kbench): a different partition of the partial sums
         static const int strided_env = NK_TUNE("NK_RES_STRIDED", 0);
         A.strided = strided_env && n2 % kResThreads == 0 && ns % G == 0 && ns / G == rv + A.rl;
+        A.mirror = NK_TUNE("NK_RES_MIRROR", 0) && !A.strided && n2 % kResThreads == 0 && ns % G == 0 && ns / G == rv + A.rl;
     }
 #ifdef NK_KBENCH
     if (jin) {
