@@ -4,7 +4,7 @@
   -> consumer, which must reproduce the single-GPU run bit for bit (same partials, same order);
 * 2, 3, 4 and 8 ranks (slabs of a 2D Bratu grid, z-slabs of a 3D heat grid, a periodic ring): halo
   exchange + all-reduced dots against the CPU oracle on the whole grid -- 8 ranks is the decomposition
-  of BASELINE configs 4 and 5;
+  of BASELINE configs 4 and 5 (config 4's finite-difference Jv and the Newton solve it drives too);
 * the failure path: a rank that stops taking part makes every other rank's next reduction return an
   NK_E_* error in bounded time, and `bench.py --gpus N` then exits non-zero instead of hanging.  Each rank gets its own GPU when the box has enough (then the RCCL
   variants must run: an RCCL error fails the test); on a box with fewer GPUs than ranks they
@@ -206,6 +206,35 @@ def test_slabs_match_oracle(tmp_path, world, transport):
     assert meta["solved"] and so["solved"]
     assert (meta["outer"], meta["inner"]) == (so["outer_iterations"], so["inner_iterations"])
     assert np.max(np.abs(d["u"] - uo)) <= 1e-8 * np.max(np.abs(uo))
+
+
+@pytest.mark.parametrize("world,nx,ny,tol", [(2, 48, 40, 1e-9), (4, 64, 96, 1e-8), (8, 48, 40, 1e-6)])
+def test_slabs_fd_jv_match_oracle(tmp_path, world, nx, ny, tol):
+    """BASELINE config 4's operator on slabs: the finite-difference Jv (the north-star kernel, eps from
+    the cross-rank norms of u and v) with its ghost rows from the neighbours, and a Newton-GMRES(10)
+    solve driven by it, over the peer mailbox with every rank on the box's GPU.  The FD quotient
+    against the oracle's (exp differs by <= 1 ulp, divided by eps), the Newton count against the
+    oracle's FD solve (as test_hip.py::test_newton_fd_vs_exact on one GPU), the root against the
+    oracle's exact-JVP root."""
+    out = str(tmp_path / "fd")
+    env = worker_env(world)
+    rc, log = run_ranks(world, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
+                                "--jv", "fd", "--nx", str(nx), "--ny", str(ny), "--tol-rel", str(tol)], env)
+    assert rc == 0, log[-3000:]
+    meta = json.load(open(out + ".json"))
+    d = np.load(out + ".npz")
+    P = oc.bratu2d(nx, ny)
+    u0 = oc.sin_ic(P)
+    F = oc.residual(P, u0)
+    ref = oc.jv_fd(P, u0, d["v"], F)
+    assert np.max(np.abs(d["jv"] - ref)) <= 1e-6 * np.max(np.abs(ref))  # ghost rows came from the neighbours
+    exact = oc.jv_exact(P, u0, d["v"])
+    assert np.max(np.abs(d["jv"] - exact)) <= 1e-5 * np.max(np.abs(exact))
+    _, so = oc.newton_krylov(P, u0, memory=10, restart=True, tol_rel=tol, jv="fd")
+    ue, se = oc.newton_krylov(P, u0, memory=10, restart=True, tol_rel=tol)
+    assert meta["solved"] and so["solved"] and se["solved"]
+    assert meta["outer"] == so["outer_iterations"]
+    assert np.max(np.abs(d["u"] - ue)) <= 1e-6 * np.max(np.abs(ue))
 
 
 @pytest.mark.parametrize("transport", ["mailbox", "rccl"])
