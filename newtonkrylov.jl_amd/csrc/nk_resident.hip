@@ -762,9 +762,14 @@ extern "C" int nkb_mgs_res(nk_ctx* c, int64_t n, int k, int rv, int reps, double
     // NK_RES_TSTAMP=<file>: also dump the per-pass, per-block wall clocks of the last timed sweep
     const char* tsf = getenv("NK_RES_TSTAMP");
     if (tsf && *tsf && !c->res_tstamp) NK_HIP(c, hipMalloc(&c->res_tstamp, sizeof(uint64_t) * 2 * kResMax * 1024));
-    std::vector<double*> V(k + 3, nullptr);
+    std::vector<double*> V(k + 3, nullptr), Vbase(k + 3, nullptr);
+    // the product's vector start offsets (nk_vec_alloc): vector v starts (v mod 8) x
+    // NK_ALLOC_STAGGER bytes (128 KB) into its allocation, so the hook times the layout the solver runs on
+    const size_t stag = (size_t)std::max(0, NK_TUNE("NK_ALLOC_STAGGER", 131072)) / 256 * 32;  // doubles
     for (size_t v = 0; v < V.size(); ++v) {
-        NK_HIP(c, hipMalloc(&V[v], sizeof(double) * n));
+        const size_t sh = (v % 8) * stag;
+        NK_HIP(c, hipMalloc(&Vbase[v], sizeof(double) * (n + sh)));
+        V[v] = Vbase[v] + sh;
         hipLaunchKernelGGL(k_hashfill, dim3(2048), dim3(kBlock), 0, c->stream, n, V[v], (uint64_t)(v + 1) * 7919u);
     }
     double* q0 = V[k];
@@ -832,7 +837,7 @@ extern "C" int nkb_mgs_res(nk_ctx* c, int64_t n, int k, int rv, int reps, double
     diff_out[3] = (double)c->res_blocks;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    for (auto p : V) (void)hipFree(p);
+    for (auto p : Vbase) (void)hipFree(p);
     return NK_OK;
 }
 #endif  // NK_KBENCH
