@@ -195,6 +195,9 @@ int nk_axpy_norm(nk_ctx* ctx, int64_t n, double s, const double* x, double* y, d
 int nk_fill(nk_ctx* ctx, int64_t n, double* x, double v);                              /* x .= v        */
 int nk_divcopy(nk_ctx* ctx, int64_t n, double* y, const double* x, double s);          /* y = x / s     */
 int nk_ref(nk_ctx* ctx, int64_t n, double* x, double* y, double c, double s);          /* Givens        */
+/* y = exp.(x), correctly rounded: the exp of the Bratu stencils (bratu.jl:21), for user residuals
+ * (test/runtests.jl:4-13's exp(x1 - 1)); the CPU oracle compiles the same source (nk_exp.h). */
+int nk_vexp(nk_ctx* ctx, int64_t n, double* y, const double* x);
 
 /* One modified-Gram-Schmidt sweep (Krylov.jl gmres! inner loop), fused
  * as the device GMRES runs it: for i = 1..k  h_i = <V_i, q>; q -= h_i V_i  (reorth: a second sweep

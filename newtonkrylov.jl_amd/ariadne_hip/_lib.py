@@ -134,6 +134,7 @@ SIGNATURES = {
     "nk_fill": (C.c_int, [_VP, _I64, _VP, _D]),
     "nk_divcopy": (C.c_int, [_VP, _I64, _VP, _VP, _D]),
     "nk_ref": (C.c_int, [_VP, _I64, _VP, _VP, _D, _D]),
+    "nk_vexp": (C.c_int, [_VP, _I64, _VP, _VP]),
     "nk_workspace_create": (C.c_int, [_VP, _I32, _PP, _I32, C.POINTER(_VP)]),
     "nk_workspace_destroy": (C.c_int, [_VP]),
     "nk_workspace_x": (_VP, [_VP]),

@@ -27,6 +27,28 @@ def _h(x: DeviceArray):
 
 
 # -------------------------------------------------------------------------- vector primitives
+def exp_(y, x, ctx=None):
+    """y .= exp.(x) with the library's correctly rounded exp (nk_vexp: the exp of the Bratu stencils,
+    csrc/nk_exp.h, which the CPU oracle compiles too) -- for user residuals, so that runtests.jl:4-13's
+    exp(x1 - 1) evaluates exactly as the oracle's.  y, x: DeviceArrays, or contiguous float64 torch
+    tensors on the context's device (enqueued on the library stream, where user callbacks run)."""
+    from .device import default_context
+
+    def ptr_len(a):
+        if isinstance(a, DeviceArray):
+            return a.ptr, a.n
+        if a.dtype != __import__("torch").float64 or not a.is_contiguous():
+            raise ValueError("exp_: contiguous float64 tensors only")
+        return a.data_ptr(), a.numel()
+
+    (py, ny), (px, nx) = ptr_len(y), ptr_len(x)
+    if ny != nx:
+        raise ValueError(f"exp_: lengths differ ({ny} vs {nx})")
+    ctx = ctx or (y.ctx if isinstance(y, DeviceArray) else x.ctx if isinstance(x, DeviceArray) else default_context())
+    ctx.check(load().nk_vexp(ctx.handle, nx, py, px), "nk_vexp")
+    return y
+
+
 def kdot(n: int, x: DeviceArray, y: DeviceArray) -> float:
     out = C.c_double()
     x.ctx.check(load().nk_dot(_h(x), n, x.ptr, y.ptr, C.byref(out)), "kdot")

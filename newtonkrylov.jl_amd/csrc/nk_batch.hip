@@ -18,6 +18,7 @@
 #include <cmath>
 #include <vector>
 
+#include "nk_exp_dev.hpp"
 #include "nk_internal.hpp"
 
 namespace nk {
@@ -120,7 +121,7 @@ __global__ __launch_bounds__(kBlock) void k_jv_batch(BArgs B) {
             uu[q] = (FD && s.ok[q]) ? B.u[s.off[q]] : 0.0;
             gg[q] = (FD && SCH != 0 && s.ok[q]) ? B.un[s.off[q]] : 0.0;
         }
-        const double eu = (!FD && kind_bratu(KIND)) ? exp(B.u[o]) : 0.0;       // Enzyme tangent of λ exp(u)
+        const double eu = (!FD && kind_bratu(KIND)) ? nk_exp(B.u[o]) : 0.0;       // Enzyme tangent of λ exp(u)
         const double unc = (FD && !kind_bratu(KIND)) ? B.un[o] : 0.0;
         const double f0 = FD ? B.F0[o] : 0.0;
         const double lsumg = (FD && SCH == 2) ? lsum_of<DIM>(B, gg) : 0.0;  // G_Trapezoid!'s du(u_n)
@@ -143,7 +144,7 @@ __global__ __launch_bounds__(kBlock) void k_jv_batch(BArgs B) {
             const double lsum = lsum_of<DIM>(B, f);
             double r;
             if constexpr (kind_bratu(KIND)) {
-                if constexpr (FD) r = ((lsum + B.lam * exp(c)) - f0) / eps;
+                if constexpr (FD) r = ((lsum + B.lam * nk_exp(c)) - f0) / eps;
                 else r = lsum + B.lam * (eu * c);
             } else if constexpr (!FD) {
                 r = (SCH == 2 ? B.dt / 2.0 : B.dt) * (B.a * lsum) - xc;

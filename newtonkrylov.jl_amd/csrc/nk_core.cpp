@@ -426,6 +426,7 @@ int nk_copy(nk_ctx* c, int64_t n, double* y, const double* x) { return c ? launc
 int nk_fill(nk_ctx* c, int64_t n, double* x, double v) { return c ? launch_fill(c, n, x, v) : NK_E_ARG; }
 int nk_divcopy(nk_ctx* c, int64_t n, double* y, const double* x, double s) { return c ? launch_divcopy(c, n, y, x, s) : NK_E_ARG; }
 int nk_ref(nk_ctx* c, int64_t n, double* x, double* y, double cc, double ss) { return c ? launch_ref(c, n, x, y, cc, ss) : NK_E_ARG; }
+int nk_vexp(nk_ctx* c, int64_t n, double* y, const double* x) { return c ? (n > 0 ? launch_exp(c, n, y, x) : NK_OK) : NK_E_ARG; }
 
 // One modified-Gram-Schmidt sweep of q against V_1..V_k -- the fused passes the device GMRES runs per
 // Arnoldi step, for callers that drive Krylov.jl's loop themselves (SURVEY §8b nk_mgs_step).

@@ -10,6 +10,8 @@
 
 #include "nk_internal.hpp"
 
+#include "nk_exp_dev.hpp"
+
 namespace nk {
 
 // mailbox binding of one rank (set by mailbox_bind)

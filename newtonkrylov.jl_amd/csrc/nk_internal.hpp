@@ -251,6 +251,7 @@ int launch_copy(nk_ctx* c, int64_t n, double* y, const double* x);
 int launch_fill(nk_ctx* c, int64_t n, double* x, double v);
 int launch_divcopy(nk_ctx* c, int64_t n, double* y, const double* x, double s);
 int launch_ref(nk_ctx* c, int64_t n, double* x, double* y, double cc, double ss);
+int launch_exp(nk_ctx* c, int64_t n, double* y, const double* x);
 // one fused modified-Gram-Schmidt pass: h = Σ in; q -= h vi; partials of <vnext, q> (or <q,q>
 // when vnext == nullptr).  Block 0 stores h at h_out (and at h_host, a mapped host address, if given).
 int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const double* vnext, Red in,

@@ -169,6 +169,12 @@ __global__ __launch_bounds__(kBlock) void k_divcopy(int64_t n, double* __restric
     if (NK_TAIL) y[n - 1] = x[n - 1] / s;
 }
 
+// y = exp.(x) with the stencils' correctly rounded exp (nk_exp.h): the primitive a user residual calls
+// for its transcendental, so it evaluates exactly what the oracle does (no alignment assumed: any views)
+__global__ __launch_bounds__(kBlock) void k_exp(int64_t n, double* __restrict__ y, const double* __restrict__ x) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) y[i] = nk_exp(x[i]);
+}
+
 __global__ __launch_bounds__(kBlock) void k_ref(int64_t n, double* __restrict__ x, double* __restrict__ y, double c, double s) {
     double2* x2 = reinterpret_cast<double2*>(x);
     double2* y2 = reinterpret_cast<double2*>(y);
@@ -474,7 +480,7 @@ __global__ __launch_bounds__(kBlock) void k_jdiag(KArgs A, double* __restrict__ 
         if (DIM >= 2) lsum = lsum + lapk(A, c, 0.0, 0.0, A.hy2, A.ihy2);
         if (DIM == 3) lsum = lsum + lapk(A, c, 0.0, 0.0, A.hz2, A.ihz2);
         const double uc = (KIND == NK_BRATU1D || KIND == NK_BRATU2D) ? A.u[i] : 0.0;
-        const double d = point_value<KIND, MODE_JEXACT>(A, c, lsum, uc, 0.0, 0.0, 1.0, 0.0);
+        const double d = point_value<KIND, MODE_JEXACT>(A, c, lsum, uc, 0.0, 0.0, 1.0, 0.0, &NKX_T[0][0]);
         out[i] = recip ? 1.0 / d : d;
     }
 }
@@ -728,7 +734,7 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     A.nx = p->nx; A.ny = p->ny; A.nz = p->nz;
     A.hx2 = p->hx * p->hx; A.hy2 = p->hy * p->hy; A.hz2 = p->hz * p->hz;
     A.lam = p->lambda; A.a = p->a; A.dt = p->dt; A.eps = in.eps;
-    A.fast = fast;
+    A.fast = fast | (NK_TUNE("NK_EXP_OCML", 0) ? 4 : 0);  // kbench A/B: the platform exp
     A.vdiv = in.vdiv;
     A.vout = in.vout;
     A.ihx2 = 1.0 / A.hx2; A.ihy2 = 1.0 / A.hy2; A.ihz2 = 1.0 / A.hz2; A.ieps = in.eps != 0.0 ? 1.0 / in.eps : 0.0;
@@ -949,6 +955,7 @@ int launch_divcopy(nk_ctx* c, int64_t n, double* y, const double* x, double s) {
     NK_STREAM_LAUNCH("divcopy", 16.0, k_divcopy, n, y, x, s);
 }
 int launch_ref(nk_ctx* c, int64_t n, double* x, double* y, double cc, double ss) { NK_STREAM_LAUNCH("ref", 32.0, k_ref, n, x, y, cc, ss); }
+int launch_exp(nk_ctx* c, int64_t n, double* y, const double* x) { NK_STREAM_LAUNCH("exp", 16.0, k_exp, n, y, x); }
 
 namespace {
 template <bool HAS_NEXT>

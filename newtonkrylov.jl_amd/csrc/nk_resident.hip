@@ -185,7 +185,7 @@ __device__ __forceinline__ dx2 res_jv_pair(const ResArgs& A, int64_t e, double& 
     const double d0 = ud.x + eps * vd.x, d1 = ud.y + eps * vd.y;
     const double l0 = ((c1 - 2.0 * c0) + wl) / A.jhx2 + ((u0 - 2.0 * c0) + d0) / A.jhy2;
     const double l1 = ((wr - 2.0 * c1) + c0) / A.jhx2 + ((u1 - 2.0 * c1) + d1) / A.jhy2;
-    const double r0 = l0 + A.jlam * exp(c0), r1 = l1 + A.jlam * exp(c1);
+    const double r0 = l0 + A.jlam * nk_exp(c0), r1 = l1 + A.jlam * nk_exp(c1);
     const dx2 val{(r0 - f0.x) / eps, (r1 - f0.y) / eps};
     acc = fma(ax.x, val.x, acc);
     acc = fma(ax.y, val.y, acc);

@@ -140,6 +140,19 @@ __device__ __forceinline__ void storevec(double* __restrict__ p, int64_t o, cons
     }
 }
 
+constexpr bool kind_bratu(int k) { return k == NK_BRATU1D || k == NK_BRATU2D; }
+
+// The exp table (NKX_T: 128 double-double entries, 2 KB) copied into LDS once per block for the Bratu
+// kinds, where every point evaluates exp: read with ds_read, its lookups never wait behind the rows the
+// march keeps in flight (a global-memory table would share their in-order vmcnt).  Declares `et`.
+#define NK_EXP_LDS(KIND)                                                                              \
+    __shared__ double et_lds[kind_bratu(KIND) ? 256 : 2];                                             \
+    const double* const et = et_lds;                                                                  \
+    if constexpr (kind_bratu(KIND)) {                                                                 \
+        for (int i_ = threadIdx.x; i_ < 256; i_ += blockDim.x) et_lds[i_] = (&NKX_T[0][0])[i_];        \
+        __syncthreads();                                                                              \
+    }
+
 // residual / JVP value at one point from the stencil field (c + neighbours) and centre data.
 // lsum = Laplacian-like sum of the stencil field in the reference's association order.  Heat kinds:
 // xc = the centre of w = u (+ eps v) -- or of v for the tangent -- before G_Midpoint!'s mixing (the
@@ -147,12 +160,20 @@ __device__ __forceinline__ void storevec(double* __restrict__ p, int64_t o, cons
 //   Euler      (u_n + Δt du(w)) - w                      tangent  Δt (a lap(v)) - v
 //   Midpoint   (u_n + Δt du(α u_n + (1-α) w)) - w        tangent  Δt (a lap((1-α) v)) - v
 //   Trapezoid  (u_n + (Δt/2) (du(u_n) + du(w))) - w      tangent  (Δt/2) (a lap(v)) - v
+// et: the exp table (nk_exp.h's NKX_T) in LDS for the Bratu kinds (NK_EXP_LDS), unused otherwise.
 template <int KIND, int MODE>
 __device__ __forceinline__ double point_value(const KArgs& A, double c, double lsum, double uc, double unc, double f0c,
-                                              double xc, double lsumg) {
+                                              double xc, double lsumg, const double* et) {
     if constexpr (KIND == NK_BRATU1D || KIND == NK_BRATU2D) {
-        if (MODE == MODE_JEXACT) return lsum + A.lam * (exp(uc) * c);  // Enzyme tangent of λ exp(u)
-        const double r = lsum + A.lam * exp(c);
+#ifdef NK_KBENCH
+        if (A.fast & 4) {  // kbench A/B only: the platform (ocml) exp, <= 1 ulp off the correctly rounded one
+            if (MODE == MODE_JEXACT) return lsum + A.lam * (exp(uc) * c);
+            const double r = lsum + A.lam * exp(c);
+            return MODE == MODE_JFD ? fdq(A, r, f0c) : r;
+        }
+#endif
+        if (MODE == MODE_JEXACT) return lsum + A.lam * (nk_exp_t(uc, et) * c);  // Enzyme tangent of λ exp(u)
+        const double r = lsum + A.lam * nk_exp_t(c, et);
         return MODE == MODE_JFD ? fdq(A, r, f0c) : r;
     } else {  // implicit.jl:8-37
         constexpr int SCH = scheme_of<KIND>();
@@ -178,6 +199,7 @@ __device__ __forceinline__ double epilogue(double& val, double ax, double acc) {
 template <int MODE, int EPI>
 __global__ __launch_bounds__(kBlock) void k_st1d(KArgs A0) {
     __shared__ double sh[kShN];
+    NK_EXP_LDS(NK_BRATU1D)
     KArgs A = A0;
     A.hd = A.vdiv ? *A.vdiv : 1.0;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -187,7 +209,7 @@ __global__ __launch_bounds__(kBlock) void k_st1d(KArgs A0) {
         const double c = fieldval<MODE>(A, i), l = fieldval<MODE>(A, i - 1), r = fieldval<MODE>(A, i + 1);
         const double uc = (MODE == MODE_JEXACT) ? A.u[i] : 0.0;
         const double f0 = (MODE == MODE_JFD) ? A.F0[i] : 0.0;
-        double val = point_value<NK_BRATU1D, MODE>(A, c, lap(c, r, l, A.hx2), uc, 0.0, f0, c, 0.0);
+        double val = point_value<NK_BRATU1D, MODE>(A, c, lap(c, r, l, A.hx2), uc, 0.0, f0, c, 0.0, et);
         const double ax = (EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID) ? A.aux[i]
                           : (EPI == EPI_DOTVS ? A.v[i] / A.hd : 0.0);
         acc = epilogue<EPI>(val, ax, acc);
@@ -583,6 +605,7 @@ __device__ __forceinline__ LR x_nbrs(double cfirst, double clast, double e, doub
 template <int KIND, int MODE, int EPI, int VEC, bool PER = false, bool F0R = false>
 __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     __shared__ double sh[kShN];
+    NK_EXP_LDS(KIND)
     KArgs A = A0;
     A.hd = A.vdiv ? *A.vdiv : 1.0;
     constexpr int SCH = scheme_of<KIND>();
@@ -699,9 +722,9 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
                         const double ue = (k == VEC - 1) ? un_.r : uc_.c[k == VEC - 1 ? k : k + 1];
                         const double ucc = uc_.c[k];
                         const double lsu = lapk(A, ucc, ue, uw, A.hx2, A.ihx2) + lapk(A, ucc, up.c[k], um.c[k], A.hy2, A.ihy2);
-                        f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unk, 0.0, SCH == 1 ? uc_.x[k] : ucc, lsumg);
+                        f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unk, 0.0, SCH == 1 ? uc_.x[k] : ucc, lsumg, et);
                     }
-                    double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unk, f0, SCH == 1 ? fc.x[k] : c, lsumg);
+                    double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unk, f0, SCH == 1 ? fc.x[k] : c, lsumg, et);
                     acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[k] : ax.v[k], acc);
                     val.v[k] = r;
                 }
@@ -738,6 +761,7 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
 template <int KIND, int MODE, int EPI, int VEC, bool PER = false, bool F0R = false, int NW = 8>
 __global__ __launch_bounds__(64 * NW) void k_st2t(KArgs A0) {
     __shared__ double sh[kShN];
+    NK_EXP_LDS(KIND)
     KArgs A = A0;
     A.hd = A.vdiv ? *A.vdiv : 1.0;
     constexpr int SCH = scheme_of<KIND>();
@@ -858,9 +882,9 @@ __global__ __launch_bounds__(64 * NW) void k_st2t(KArgs A0) {
                 const double ucc = uc_.c[k];
                 const double lsu = lapk(A, ucc, ue, uw, A.hx2, A.ihx2) +
                                    lapk(A, ucc, lu[kR ? wv + 2 : 0][kR ? q : 0], lu[kR ? wv : 0][kR ? q : 0], A.hy2, A.ihy2);
-                f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unk, 0.0, SCH == 1 ? uc_.x[k] : ucc, lsumg);
+                f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unk, 0.0, SCH == 1 ? uc_.x[k] : ucc, lsumg, et);
             }
-            double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unk, f0, SCH == 1 ? fc.x[k] : c, lsumg);
+            double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unk, f0, SCH == 1 ? fc.x[k] : c, lsumg, et);
             acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[k] : ax.v[k], acc);
             val.v[k] = r;
         }
@@ -894,6 +918,7 @@ __global__ __launch_bounds__(64 * NW) void k_st2t(KArgs A0) {
 template <int KIND, int MODE, int EPI, int VEC, bool PER = false, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
     __shared__ double sh[kShN];
+    const double* const et = nullptr;  // heat kinds: no exp
     KArgs A = A0;
     A.hd = A.vdiv ? *A.vdiv : 1.0;
     constexpr int SCH = scheme_of<KIND>();
@@ -989,7 +1014,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
                                 lapk(A, g, fp.g[q], fm.g[q], A.hz2, A.ihz2);
                     }
                     const double unq = kG ? fc.g[q] : unc.v[q];
-                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0c.v[q], SCH == 1 ? fc.x[q] : c, lsumg);
+                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0c.v[q], SCH == 1 ? fc.x[q] : c, lsumg, et);
                     acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[q] : ax.v[q], acc);
                     val.v[q] = r;
                 }
@@ -1026,6 +1051,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
 template <int KIND, int MODE, int EPI, int VEC, bool PER = false, int NW = 8, bool F0R = false>
 __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
     __shared__ double sh[kShN];
+    const double* const et = nullptr;  // heat kinds: no exp
     KArgs A = A0;
     A.hd = A.vdiv ? *A.vdiv : 1.0;
     constexpr int SCH = scheme_of<KIND>();
@@ -1221,9 +1247,9 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
                         const double ucc = uc_.c[q];
                         const double lsu = (lapk(A, ucc, ue, uw, A.hx2, A.ihx2) + lapk(A, ucc, cnu[q], csu[q], A.hy2, A.ihy2)) +
                                            lapk(A, ucc, dn ? um.c[q] : up.c[q], dn ? up.c[q] : um.c[q], A.hz2, A.ihz2);
-                        f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unq, 0.0, SCH == 1 ? uc_.x[q] : ucc, lsumg);
+                        f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unq, 0.0, SCH == 1 ? uc_.x[q] : ucc, lsumg, et);
                     }
-                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0, SCH == 1 ? fc.x[q] : c, lsumg);
+                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0, SCH == 1 ? fc.x[q] : c, lsumg, et);
                     acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[q] : ax.v[q], acc);
                     val.v[q] = r;
                 }

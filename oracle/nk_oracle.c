@@ -37,6 +37,15 @@
 #include <float.h>
 #include <omp.h>
 
+/* The correctly rounded exp shared with the HIP stencils (newtonkrylov.jl_amd/csrc/nk_exp.h): the
+ * Bratu residual's lam * exp(u) (examples/bratu.jl:21) evaluates to the same double on both sides,
+ * so the Bratu residual / JVP / FD operator are compared bit for bit like the heat kinds.  The exp
+ * itself is pinned independently (tests/test_exp.py: mpmath at 200 bits on >= 10^6 inputs). */
+#define NKX_FN static inline
+#define NKX_SLOW_FN static
+#define NKX_CONST static const
+#include "nk_exp.h"
+
 enum { OC_BRATU1D = 1, OC_BRATU2D = 2, OC_HEAT2D_EULER = 3, OC_HEAT3D_EULER = 4,
        OC_HEAT2D_MIDPOINT = 5, OC_HEAT3D_MIDPOINT = 6, OC_HEAT2D_TRAPEZOID = 7, OC_HEAT3D_TRAPEZOID = 8 };
 enum { OC_BC_ZERO = 0, OC_BC_PERIODIC = 1 };
@@ -246,12 +255,12 @@ static inline double point_residual(const oc_problem* P, const double* u, const 
     switch (P->kind) {
     case OC_BRATU1D: {
         double l = wval(u, v, eps, nx, ny, nz, i - 1, j, k), r = wval(u, v, eps, nx, ny, nz, i + 1, j, k);
-        return lap1(c, r, l, P->hx) + P->lambda * exp(c);
+        return lap1(c, r, l, P->hx) + P->lambda * nk_exp(c);
     }
     case OC_BRATU2D: {
         double e = wval(u, v, eps, nx, ny, nz, i + 1, j, k), w = wval(u, v, eps, nx, ny, nz, i - 1, j, k);
         double n = wval(u, v, eps, nx, ny, nz, i, j + 1, k), s = wval(u, v, eps, nx, ny, nz, i, j - 1, k);
-        return (lap1(c, e, w, P->hx) + lap1(c, n, s, P->hy)) + P->lambda * exp(c);
+        return (lap1(c, e, w, P->hx) + lap1(c, n, s, P->hy)) + P->lambda * nk_exp(c);
     }
     default:
         return heat_point(P, u, v, eps, i, j, k);
@@ -297,11 +306,11 @@ void oc_jv_exact(const oc_problem* P, double* out, const double* u, const double
                 double e = wval(v, NULL, 0, nx, ny, nz, i + 1, j, k), w = wval(v, NULL, 0, nx, ny, nz, i - 1, j, k);
                 switch (P->kind) {
                 case OC_BRATU1D:
-                    r = lap1(c, e, w, P->hx) + P->lambda * (exp(AT(u, i, j, k)) * c);
+                    r = lap1(c, e, w, P->hx) + P->lambda * (nk_exp(AT(u, i, j, k)) * c);
                     break;
                 case OC_BRATU2D: {
                     double n = wval(v, NULL, 0, nx, ny, nz, i, j + 1, k), s = wval(v, NULL, 0, nx, ny, nz, i, j - 1, k);
-                    r = (lap1(c, e, w, P->hx) + lap1(c, n, s, P->hy)) + P->lambda * (exp(AT(u, i, j, k)) * c);
+                    r = (lap1(c, e, w, P->hx) + lap1(c, n, s, P->hy)) + P->lambda * (nk_exp(AT(u, i, j, k)) * c);
                     break;
                 }
                 default:
@@ -382,7 +391,7 @@ void oc_jacobian_diag(const oc_problem* P, double* out, const double* u, int rec
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; ++i) {
         double d;
-        if (!heat) d = lsum + P->lambda * (exp(u[i]) * 1.0);
+        if (!heat) d = lsum + P->lambda * (nk_exp(u[i]) * 1.0);
         else if (sch == 2) d = (P->dt / 2.0) * (P->a * lsum) - 1.0;
         else d = P->dt * (P->a * lsum) - 1.0;
         out[i] = reciprocal ? 1.0 / d : d;
@@ -823,3 +832,23 @@ int oc_krylov_solve(const oc_problem* P, int jv_mode, int algo, const double* u,
 
 void oc_set_threads(int t) { if (t > 0) omp_set_num_threads(t); }
 int oc_get_threads(void) { return omp_get_max_threads(); }
+
+/* the shared exp, exported for tests/test_exp.py (its pinning against mpmath) */
+void oc_exp(int64_t n, const double* x, double* y) {
+    for (int64_t i = 0; i < n; ++i) y[i] = nk_exp(x[i]);
+}
+void oc_exp_slow(int64_t n, const double* x, double* y) {
+    for (int64_t i = 0; i < n; ++i) y[i] = nkx_exp_slow(x[i]);
+}
+/* the fast phase alone: exp(x) ~ (zh + zl) 2^m; returns how many inputs the Ziv test sent to the slow phase */
+int64_t oc_exp_dd(int64_t n, const double* x, double* zh, double* zl, int32_t* m) {
+    int64_t slow = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        int mm;
+        zh[i] = nkx_exp_dd(x[i], &NKX_T[0][0], &zl[i], &mm);
+        m[i] = mm;
+        const double err = zh[i] * 0x1p-72;
+        if (zh[i] + (zl[i] - err) != zh[i] || zh[i] + (zl[i] + err) != zh[i]) ++slow;
+    }
+    return slow;
+}

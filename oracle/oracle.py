@@ -77,6 +77,10 @@ class _NewtonStats(C.Structure):
 _lib = None
 
 
+# the correctly rounded exp the oracle shares with the HIP stencils (compiled into nk_oracle.c)
+EXP_H = os.path.join(os.path.dirname(HERE), "newtonkrylov.jl_amd", "csrc", "nk_exp.h")
+
+
 def build() -> str:
     """Compile the oracle with its Makefile (gcc is part of the image)."""
     subprocess.run(["make", "-s", "-C", HERE], check=True)
@@ -86,7 +90,8 @@ def build() -> str:
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(HERE, "nk_oracle.c")):
+        srcs = (os.path.join(HERE, "nk_oracle.c"), EXP_H)
+        if not os.path.exists(LIB_PATH) or any(os.path.getmtime(LIB_PATH) < os.path.getmtime(f) for f in srcs if os.path.exists(f)):
             build()
         L = C.CDLL(LIB_PATH)
         D, I64, P = C.c_double, C.c_int64, C.POINTER(C.c_double)
@@ -115,6 +120,10 @@ def lib():
         for name in ("oc_axpy",):
             getattr(L, name).argtypes = [I64, D, P, P]
         L.oc_axpby.argtypes = [I64, D, P, D, P]
+        L.oc_exp.argtypes = [I64, P, P]
+        L.oc_exp_slow.argtypes = [I64, P, P]
+        L.oc_exp_dd.argtypes = [I64, P, P, P, C.POINTER(C.c_int32)]
+        L.oc_exp_dd.restype = I64
         _lib = L
     return _lib
 
@@ -408,3 +417,30 @@ def axpby(s, x, t, y):
     y = np.array(y, dtype=np.float64).reshape(-1)
     lib().oc_axpby(x.size, float(s), _p(x), float(t), _p(y))
     return y
+
+
+# ----------------------------------------------------------------------------- the shared exp
+def exp(x) -> np.ndarray:
+    """nk_exp (csrc/nk_exp.h): the correctly rounded exp every Bratu evaluation uses, elementwise."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    lib().oc_exp(x.size, _p(x), _p(y))
+    return y
+
+
+def exp_slow(x) -> np.ndarray:
+    """nk_exp's exact fixed-point phase alone (valid for 2^-54 < |x| < 746)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    lib().oc_exp_slow(x.size, _p(x), _p(y))
+    return y
+
+
+def exp_dd(x):
+    """nk_exp's fast phase alone: (zh, zl, m) with exp(x) ~ (zh + zl) 2^m, and how many inputs its Ziv
+    test would hand to the exact phase."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    zh, zl = np.empty_like(x), np.empty_like(x)
+    m = np.empty(x.shape, dtype=np.int32)
+    slow = lib().oc_exp_dd(x.size, _p(x), _p(zh), _p(zl), m.ctypes.data_as(C.POINTER(C.c_int32)))
+    return zh, zl, m, int(slow)
