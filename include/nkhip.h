@@ -307,13 +307,21 @@ typedef struct nk_path_info {
     int32_t rank, nranks, device;
     int32_t ranks_on_device;  /* ranks sharing this GPU, this one included (1: one GPU per rank)        */
     int32_t rccl;             /* an RCCL communicator exists (bootstrap; fallback transport)            */
-    int32_t mailbox;          /* reductions and ghost planes through the IPC peer mailbox (xGMI)        */
-    int32_t resident_sweep;   /* the one-launch resident MGS sweep may run (0: one launch per MGS pass)  */
+    int32_t mailbox;          /* reductions and ghost planes through the peer mailbox: 1 device memory
+                                 over xGMI (IPC), 2 host shared memory (a peer's device invisible here,
+                                 or NK_DIST_MAILBOX=host; planes beyond its small inbox take RCCL)     */
+    int32_t resident_sweep;   /* the one-launch resident MGS sweep RAN (sweeps_resident > 0)            */
     int32_t resident_blocks;  /* its grid once set up (0: not run yet)                                 */
-    int32_t halo_in_launch;   /* a Krylov Jv's ghost planes travel inside the stencil launch           */
+    int32_t halo_in_launch;   /* every Krylov Jv that needed v's ghost planes carried them inside the
+                                 stencil launch (jv_halo_fused > 0, jv_halo_separate == 0)               */
     int32_t mailbox_error;    /* a mailbox wait timed out (a peer never arrived): sticky                */
     int64_t halo_cap;         /* doubles per IPC inbox plane (larger planes: RCCL send/recv)            */
     char pci_bus_id[32];      /* this rank's device                                                    */
+    /* launch counts since the context was created (what the flags above are derived from) */
+    int64_t jv_halo_fused;    /* Jv launches with v's ghost planes exchanged inside the launch        */
+    int64_t jv_halo_separate; /* Jv launches that exchanged them with a separate launch first        */
+    int64_t sweeps_resident;  /* resident MGS sweeps (one launch per Arnoldi step)                     */
+    int64_t mgs_passes;       /* per-pass MGS launches (the chain)                                     */
 } nk_path_info;
 int nk_dist_path(nk_ctx* ctx, nk_path_info* out);
 

@@ -90,7 +90,8 @@ class nk_path_info(C.Structure):
     _fields_ = [("rank", C.c_int32), ("nranks", C.c_int32), ("device", C.c_int32), ("ranks_on_device", C.c_int32),
                 ("rccl", C.c_int32), ("mailbox", C.c_int32), ("resident_sweep", C.c_int32),
                 ("resident_blocks", C.c_int32), ("halo_in_launch", C.c_int32), ("mailbox_error", C.c_int32),
-                ("halo_cap", C.c_int64), ("pci_bus_id", C.c_char * 32)]
+                ("halo_cap", C.c_int64), ("pci_bus_id", C.c_char * 32), ("jv_halo_fused", C.c_int64),
+                ("jv_halo_separate", C.c_int64), ("sweeps_resident", C.c_int64), ("mgs_passes", C.c_int64)]
 
 
 class nk_prof_entry(C.Structure):

@@ -18,7 +18,7 @@ from . import _lib
 from ._lib import load
 from .device import DeviceArray
 from .krylov import KrylovConstructor, krylov_solve_, krylov_workspace
-from .problems import DeviceResidual
+from .problems import DeviceResidual, UserResidual
 
 log = logging.getLogger("ariadne_hip")
 
@@ -351,7 +351,19 @@ def newton_krylov_native(F_: DeviceResidual, u: DeviceArray, p=None, res: Device
     return u, Result(bool(st.solved), stats, t, int(st.n_matvec))
 
 
-def newton_krylov(F: DeviceResidual, u0: DeviceArray, p=None, **kwargs):
-    """newton_krylov(F, u₀, p; kwargs...) -- out-of-place form (src/Ariadne.jl:245-248).
-    The device residual computes in place; u₀ is not modified."""
+def newton_krylov(F, u0: DeviceArray, p=None, **kwargs):
+    """newton_krylov(F, u₀, p; kwargs...) -- out-of-place form (src/Ariadne.jl:245-248): u₀ is not
+    modified.  F is a device residual (in place, as newton_krylov_ takes), or -- the reference's
+    out-of-place `F(u, p)` that returns the residual -- a plain callable that gets u as a torch view
+    and returns a tensor of u's shape; it is wrapped as F!(res, u, p) = (res .= F(u, p)) (:245-246),
+    a user residual without a tangent, so pass jv="fd"."""
+    if not isinstance(F, DeviceResidual):
+        if not callable(F):
+            raise TypeError("newton_krylov: F must be a device residual or a callable F(u, p)")
+        fn = F
+
+        def F_inplace(res, u, p_):
+            res.torch().copy_(fn(u.torch(), p_).reshape(res.torch().shape))
+
+        F = UserResidual(F_inplace, name=getattr(fn, "__name__", "F") + "!")
     return newton_krylov_(F, u0.copy(), p, **kwargs)

@@ -77,6 +77,7 @@ class Context:
         self.check(load().nk_dist_path(self.handle, C.byref(info)), "nk_dist_path")
         out = {name: getattr(info, name) for name, _ in _lib.nk_path_info._fields_}
         out["pci_bus_id"] = info.pci_bus_id.decode(errors="replace")
+        out["mailbox_host"] = info.mailbox == 2  # the host shared-memory mailbox (nkhip.h nk_path_info)
         for k in ("rccl", "mailbox", "resident_sweep", "halo_in_launch", "mailbox_error"):
             out[k] = bool(out[k])
         return out

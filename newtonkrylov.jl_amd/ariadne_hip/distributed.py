@@ -1,7 +1,13 @@
-"""Multi-GPU setup: one process per GPU, slab decomposition, RCCL inside libnkhip.so.
+"""Multi-GPU setup: one process per GPU, slab decomposition along the slowest axis (nk_dist.cpp).
 
-torch.distributed (gloo) is only the control plane here: it broadcasts RCCL's unique id from
-rank 0; the data path (ghost planes, inner products) is RCCL over xGMI on the library's stream.
+torch.distributed (gloo) is only the control plane here: it broadcasts RCCL's unique id from rank 0.
+RCCL then bootstraps the data path: at nk_dist_init the ranks allgather the IPC handles of each
+other's peer mailboxes (fine-grained device memory), map them over xGMI and self-test them.  From
+then on every inner product is all-reduced through the mailboxes inside the consuming kernel, and
+v's ghost planes travel inside the Krylov Jv launch -- no collective per reduction.
+RCCL send/recv + ncclAllReduce on the library stream remain the fallback when the mailbox cannot
+come up (a peer device invisible to the process, a failed self-test, NK_DIST_MAILBOX=0) and for
+ghost planes larger than the inbox.  ctx.path_info() reports which path ran, from launch counts.
 """
 from __future__ import annotations
 

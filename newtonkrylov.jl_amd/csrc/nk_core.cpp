@@ -94,6 +94,16 @@ int finish_reduction(nk_ctx* c, Red* r) {
         r->len = -(1 + (int)((r->epoch << 15) | (unsigned)r->len));  // = mb_encode (nk_device.hpp)
         r->epoch = 0;
         r->fin = nullptr;
+        if (c->res_share > 1) {
+            // Ranks sharing this GPU (one-GPU rehearsals): a consumer whose every block spins for the
+            // peers' values could hold the CUs a peer's producer needs (two ranks' 512x128x64 GMRES
+            // timed out that way).  A one-block k_finalize does the exchange first -- one wave polls,
+            // with s_sleep -- and the consumer reads the resolved scalar (len 1: the same bits).
+            double* dst = red_slot(c);
+            NK_TRY(launch_finalize(c, *r, dst, 0));
+            r->ptr = dst;
+            r->len = 1;
+        }
         return NK_OK;
     }
     if (!c->comm) return NK_OK;

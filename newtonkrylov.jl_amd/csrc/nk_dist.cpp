@@ -5,8 +5,12 @@
 // neighbour ranks' boundary planes, exchanged with grouped ncclSend/ncclRecv before every stencil
 // application, and every inner product is completed by an 8-byte ncclAllReduce (the Arnoldi
 // scalars are then replicated on all ranks, as the Hessenberg/Givens work is).
+#include <fcntl.h>
 #include <rccl/rccl.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -79,25 +83,96 @@ int allreduce_scalar(nk_ctx* c, double* dev, int64_t count) {
 // xGMI (nk_kernels.hip: mb_send / mb_recv); RCCL keeps the halo exchange.  Set up collectively at
 // nk_dist_init, verified by a self-test whose verdict all ranks agree on; any failure falls back
 // to the RCCL all-reduce.
+static size_t mb_region_bytes(int64_t cap) {
+    return sizeof(uint64_t) * (kMbWords + kHaloFlagWords) + sizeof(double) * 4 * (size_t)cap;
+}
+
+static int mb_alloc_err(nk_ctx* c) {
+    if (c->mb_err) return NK_OK;
+    int* h = nullptr;
+    NK_HIP(c, hipHostMalloc(&h, 4 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+    h[0] = 0;
+    NK_HIP(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->mb_err_dev), h, 0));
+    c->mb_err = h;
+    return NK_OK;
+}
+
+// my device region: fine-grained device memory whose IPC handle the peers map over xGMI
 static int mb_alloc(nk_ctx* c) {
-    if (c->mb_self) return NK_OK;
+    if (c->mb_dev) return NK_OK;
     NK_HIP(c, hipSetDevice(c->device));
     const char* hc = getenv("NK_HALO_CAP");  // doubles per inbox plane (default 1M: a 1024^2 3D plane)
-    c->halo_cap = (hc && *hc) ? atoll(hc) : ((int64_t)1 << 20);
-    const size_t bytes = sizeof(uint64_t) * (kMbWords + kHaloFlagWords) + sizeof(double) * 4 * (size_t)c->halo_cap;
+    c->halo_cap_dev = (hc && *hc) ? atoll(hc) : ((int64_t)1 << 20);
+    const size_t bytes = mb_region_bytes(c->halo_cap_dev);
     void* p = nullptr;
     if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) != hipSuccess)
         return fail(c, NK_E_NOMEM, "mailbox: fine-grained allocation failed");
     NK_HIP(c, hipMemset(p, 0, bytes));
-    c->mb_self = static_cast<uint64_t*>(p);
-    if (!c->mb_err) {
-        int* h = nullptr;
-        NK_HIP(c, hipHostMalloc(&h, 4 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
-        h[0] = 0;
-        NK_HIP(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->mb_err_dev), h, 0));
-        c->mb_err = h;
+    c->mb_dev = static_cast<uint64_t*>(p);
+    return mb_alloc_err(c);
+}
+
+// Host mailbox: the same region layout in a POSIX shared-memory segment, registered with HIP (mapped:
+// kernels store to it and poll it with system-scope atomics over PCIe / Infinity Fabric).  Used when a
+// peer's device is not visible to this process (a launcher that gives each rank one visible GPU), or
+// forced with NK_DIST_MAILBOX=host.  Its ghost-plane inbox is small (NK_HALO_CAP_HOST doubles per plane,
+// default 64 Ki): larger planes take RCCL send/recv, while every reduction scalar -- and with it the
+// resident MGS sweep's per-pass cross-rank stage -- stays on the mailbox.
+struct HostHandle {  // the 64-byte record that stands in for a hipIpcMemHandle_t
+    char magic[8];
+    char name[48];
+    uint64_t bytes;
+};
+static_assert(sizeof(HostHandle) == 64, "host mailbox handle record");
+static const char kHostMagic[8] = {'N', 'K', 'H', 'O', 'S', 'T', 'M', 'B'};
+static bool is_host_handle(const char* h) { return std::memcmp(h, kHostMagic, 8) == 0; }
+static bool mb_force_host() {
+    const char* e = getenv("NK_DIST_MAILBOX");
+    return e && std::strcmp(e, "host") == 0;
+}
+
+static int mb_alloc_host(nk_ctx* c) {
+    if (c->mb_host_base) return NK_OK;
+    NK_HIP(c, hipSetDevice(c->device));
+    const char* hc = getenv("NK_HALO_CAP_HOST");
+    c->halo_cap_host = (hc && *hc) ? atoll(hc) : ((int64_t)1 << 16);
+    const size_t bytes = mb_region_bytes(c->halo_cap_host);
+    static unsigned seq = 0;
+    std::snprintf(c->mb_host_name, sizeof(c->mb_host_name), "/nk_mb_%d_%u_%d", (int)getpid(), seq++, c->device);
+    const int fd = shm_open(c->mb_host_name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd < 0) return fail(c, NK_E_NOMEM, std::string("host mailbox: shm_open failed for ") + c->mb_host_name);
+    void* p = MAP_FAILED;
+    if (ftruncate(fd, (off_t)bytes) == 0) p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) {
+        shm_unlink(c->mb_host_name);
+        return fail(c, NK_E_NOMEM, "host mailbox: mapping the shared segment failed");
     }
-    return NK_OK;
+    std::memset(p, 0, bytes);
+    void* d = nullptr;
+    if (hipHostRegister(p, bytes, hipHostRegisterMapped) != hipSuccess || hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        munmap(p, bytes);
+        shm_unlink(c->mb_host_name);
+        return fail(c, NK_E_HIP, "host mailbox: hipHostRegister of the shared segment failed");
+    }
+    c->mb_host_base = p;
+    c->mb_host_bytes = bytes;
+    c->mb_host_dev = static_cast<uint64_t*>(d);
+    return mb_alloc_err(c);
+}
+
+// my region for the next open: the device one (xGMI peers) or the host one
+static void mb_use(nk_ctx* c, bool host) {
+    c->mb_host = host;
+    c->mb_self = host ? c->mb_host_dev : c->mb_dev;
+    c->halo_cap = host ? c->halo_cap_host : c->halo_cap_dev;
+}
+
+// every peer has mapped my host segment: its name can go (the mappings stay valid)
+static void mb_host_unlink(nk_ctx* c) {
+    if (c->mb_host_name[0]) shm_unlink(c->mb_host_name);
+    c->mb_host_name[0] = 0;
 }
 
 static void mb_disable(nk_ctx* c) {
@@ -105,17 +180,51 @@ static void mb_disable(nk_ctx* c) {
     (void)mailbox_bind(c);
     for (void* p : c->mb_opened) (void)hipIpcCloseMemHandle(p);
     c->mb_opened.clear();
+    for (auto& m : c->mb_host_maps) {
+        (void)hipHostUnregister(m.first);
+        munmap(m.first, m.second);
+    }
+    c->mb_host_maps.clear();
     if (c->mb_peers_dev) (void)hipFree(c->mb_peers_dev);
     c->mb_peers_dev = nullptr;
 }
 
 void mb_free(nk_ctx* c) {
     mb_disable(c);
-    if (c->mb_self) (void)hipFree(c->mb_self);
+    if (c->mb_dev) (void)hipFree(c->mb_dev);
+    c->mb_dev = nullptr;
+    if (c->mb_host_base) {
+        (void)hipHostUnregister(c->mb_host_base);
+        munmap(c->mb_host_base, c->mb_host_bytes);
+        mb_host_unlink(c);
+    }
+    c->mb_host_base = nullptr;
+    c->mb_host_dev = nullptr;
     c->mb_self = nullptr;
     if (c->mb_err) (void)hipHostFree(c->mb_err);
     c->mb_err = nullptr;
     c->mb_err_dev = nullptr;
+}
+
+// map a peer's host segment: its device address for my kernels
+static int mb_map_host_peer(nk_ctx* c, int r, const char* rec, uint64_t** out) {
+    HostHandle h;
+    std::memcpy(&h, rec, sizeof(h));
+    h.name[sizeof(h.name) - 1] = 0;
+    const int fd = shm_open(h.name, O_RDWR, 0600);
+    if (fd < 0) return fail(c, NK_E_HIP, "host mailbox: rank " + std::to_string(r) + "'s segment cannot be opened");
+    void* p = mmap(nullptr, h.bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) return fail(c, NK_E_HIP, "host mailbox: rank " + std::to_string(r) + "'s segment cannot be mapped");
+    void* d = nullptr;
+    if (hipHostRegister(p, h.bytes, hipHostRegisterMapped) != hipSuccess || hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        munmap(p, h.bytes);
+        return fail(c, NK_E_HIP, "host mailbox: rank " + std::to_string(r) + "'s segment cannot be registered");
+    }
+    c->mb_host_maps.emplace_back(p, (size_t)h.bytes);
+    *out = static_cast<uint64_t*>(d);
+    return NK_OK;
 }
 
 // open the peers' mailboxes (local: IPC mappings + device table + kernel binding).  busids (optional,
@@ -123,8 +232,10 @@ void mb_free(nk_ctx* c) {
 // peer access (xGMI), and every mapping is probed by a host-initiated copy before any kernel
 // dereferences it, so a bad mapping disables the mailbox (RCCL fallback) instead of faulting a kernel.
 static int mb_open_peers(nk_ctx* c, int rank, int nranks, const char* handles, const char* busids = nullptr) {
-    NK_TRY(mb_alloc(c));
+    const bool host = is_host_handle(handles + 64 * (size_t)rank);  // my own record names the mode
+    NK_TRY(host ? mb_alloc_host(c) : mb_alloc(c));
     mb_disable(c);
+    mb_use(c, host);
     std::vector<uint64_t*> peers((size_t)nranks);
     // the resident MGS sweep needs every CU of its grid co-resident: with peers on the same device
     // (no bus ids: the mailbox-only transport, made for ranks on one GPU -- all of them count) it is
@@ -134,6 +245,27 @@ static int mb_open_peers(nk_ctx* c, int rank, int nranks, const char* handles, c
     for (int r = 0; r < nranks; ++r) {
         if (r == rank) {
             peers[r] = c->mb_self;
+            continue;
+        }
+        if (host) {  // host shared memory: reachable from any device, no peer access needed
+            if (busids) {
+                char bus[33];
+                std::memcpy(bus, busids + 32 * (size_t)r, 32);
+                bus[32] = 0;
+                int dev = -1;
+                if (hipDeviceGetByPCIBusId(&dev, bus) == hipSuccess && dev == c->device) ++share;
+                else (void)hipGetLastError();
+            }
+            if (!is_host_handle(handles + 64 * (size_t)r)) {
+                mb_disable(c);
+                return fail(c, NK_E_ARG, "mailbox: ranks disagree on host / device mailboxes");
+            }
+            uint64_t* p = nullptr;
+            if (mb_map_host_peer(c, r, handles + 64 * (size_t)r, &p) != NK_OK) {
+                mb_disable(c);
+                return NK_E_HIP;
+            }
+            peers[r] = p;
             continue;
         }
         if (busids) {
@@ -203,6 +335,18 @@ static bool halo_selftest(nk_ctx* c) {
     return ok;
 }
 
+// min over ranks of a local success flag (RCCL; a context without a communicator decides alone)
+static bool all_ranks_ok(nk_ctx* c, bool local_ok) {
+    if (!c->comm) return local_ok;
+    double v = local_ok ? 1.0 : 0.0;
+    if (hipMemcpy(c->scal, &v, sizeof(double), hipMemcpyHostToDevice) != hipSuccess) return false;
+    if (ncclAllReduce(c->scal, c->scal, 1, ncclFloat64, ncclMin, c->comm->comm, c->stream) != ncclSuccess) return false;
+    if (hipMemcpyAsync(c->hpin, c->scal, sizeof(double), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return false;
+    return c->hpin[0] == 1.0;
+}
+
 static int mb_verdict(nk_ctx* c, bool local_ok) {
     bool ok = local_ok;
     if (c->mb_on) {
@@ -270,16 +414,27 @@ int nk_dist_init(nk_ctx* c, int32_t rank, int32_t nranks, const char id[128]) {
     // also turns it on for a forced 1-rank communicator (exercises the path on one GPU), =0 off
     const bool mb_want = (mbe && *mbe == '1') || (nranks > 1 && !(mbe && *mbe == '0'));
     if (mb_want && nranks <= kMbRanks) {
-        // per rank: 64-byte IPC handle + 32-byte PCI bus id of its device
-        constexpr size_t kRec = 96;
+        // per rank: 64-byte IPC handle of the device region, 32-byte PCI bus id of its device, 64-byte
+        // record of the host region (the fallback when a peer's device is not visible here)
+        constexpr size_t kRec = 160;
         std::vector<char> all(kRec * nranks, 0);
         // the exchange buffer is the context's reduction scratch (allocated at nk_ctx_create), so no
         // rank can fail an allocation here and leave the others alone in the collectives below
         static_assert(kRec * kMbRanks <= sizeof(double) * kRedCap, "handle records fit one reduction slot");
         char* dbuf = reinterpret_cast<char*>(c->red);
-        int rc = nk_dist_mailbox_handle(c, all.data() + kRec * (size_t)rank);
+        const bool force_host = mb_force_host();
+        int rc = NK_OK;
+        if (!force_host) rc = nk_dist_mailbox_handle(c, all.data() + kRec * (size_t)rank);  // (device region)
         if (rc == NK_OK && hipDeviceGetPCIBusId(all.data() + kRec * (size_t)rank + 64, 32, c->device) != hipSuccess)
             rc = NK_E_HIP;
+        int rch = mb_alloc_host(c);
+        if (rch == NK_OK) {
+            HostHandle hh{};
+            std::memcpy(hh.magic, kHostMagic, 8);
+            std::memcpy(hh.name, c->mb_host_name, sizeof(hh.name));
+            hh.bytes = c->mb_host_bytes;
+            std::memcpy(all.data() + kRec * (size_t)rank + 96, &hh, sizeof(hh));
+        }
         // allgather the IPC handles: collective, every rank takes part whatever its local state
         (void)hipMemcpy(dbuf + kRec * (size_t)rank, all.data() + kRec * (size_t)rank, kRec, hipMemcpyHostToDevice);
         const ncclResult_t ag = ncclAllGather(dbuf + kRec * (size_t)rank, dbuf, kRec, ncclChar, cm->comm, c->stream);
@@ -291,28 +446,47 @@ int nk_dist_init(nk_ctx* c, int32_t rank, int32_t nranks, const char id[128]) {
             (void)mb_verdict(c, false);
             return rccl_fail(c, ag, "ncclAllGather (mailbox handles)");
         }
-        if (rc == NK_OK) {
-            std::vector<char> handles(64 * (size_t)nranks), busids(32 * (size_t)nranks);
-            for (int r = 0; r < nranks; ++r) {
-                std::memcpy(handles.data() + 64 * (size_t)r, all.data() + kRec * (size_t)r, 64);
-                std::memcpy(busids.data() + 32 * (size_t)r, all.data() + kRec * (size_t)r + 64, 32);
-            }
-            rc = mb_open_peers(c, rank, nranks, handles.data(), busids.data());
+        std::vector<char> handles(64 * (size_t)nranks), hhandles(64 * (size_t)nranks), busids(32 * (size_t)nranks);
+        for (int r = 0; r < nranks; ++r) {
+            std::memcpy(handles.data() + 64 * (size_t)r, all.data() + kRec * (size_t)r, 64);
+            std::memcpy(busids.data() + 32 * (size_t)r, all.data() + kRec * (size_t)r + 64, 32);
+            std::memcpy(hhandles.data() + 64 * (size_t)r, all.data() + kRec * (size_t)r + 96, 64);
+        }
+        // the device regions over xGMI when every rank can map every peer's; else (all ranks together)
+        // the host regions
+        if (!force_host && rc == NK_OK) rc = mb_open_peers(c, rank, nranks, handles.data(), busids.data());
+        if (force_host || !all_ranks_ok(c, rc == NK_OK)) {
+            if (!force_host)
+                std::fprintf(stderr, "[nkhip] rank %d: device mailboxes not reachable by every rank (%s); host mailbox\n",
+                             rank, c->err.c_str());
+            c->err.clear();
+            mb_disable(c);
+            rc = rch == NK_OK ? mb_open_peers(c, rank, nranks, hhandles.data(), busids.data()) : rch;
         }
         if (mb_verdict(c, rc == NK_OK) != NK_OK) {
             std::fprintf(stderr, "[nkhip] rank %d: peer mailbox off (%s); reductions use ncclAllReduce\n", rank,
                          c->err.c_str());
             c->err.clear();
         }
+        mb_host_unlink(c);  // every rank has mapped it (or gave up) by the verdict
     }
     return NK_OK;
 }
 
 int nk_dist_mailbox_handle(nk_ctx* c, char out[64]) {
     if (!c || !out) return NK_E_ARG;
+    if (mb_force_host() && !c->comm) {  // the mailbox-only transport in host memory (NK_DIST_MAILBOX=host)
+        NK_TRY(mb_alloc_host(c));
+        HostHandle hh{};
+        std::memcpy(hh.magic, kHostMagic, 8);
+        std::memcpy(hh.name, c->mb_host_name, sizeof(hh.name));
+        hh.bytes = c->mb_host_bytes;
+        std::memcpy(out, &hh, sizeof(hh));
+        return NK_OK;
+    }
     NK_TRY(mb_alloc(c));
     hipIpcMemHandle_t h;
-    NK_HIP(c, hipIpcGetMemHandle(&h, c->mb_self));
+    NK_HIP(c, hipIpcGetMemHandle(&h, c->mb_dev));
     static_assert(sizeof(h) == 64, "hipIpcMemHandle_t size");
     std::memcpy(out, &h, 64);
     return NK_OK;
@@ -324,7 +498,9 @@ int nk_dist_mailbox_open(nk_ctx* c, int32_t rank, int32_t nranks, const char* ha
     c->rank = rank;  // mailbox-only (no RCCL communicator): reductions across ranks, no halo exchange
     c->nranks = nranks;
     const int rc = mb_open_peers(c, rank, nranks, handles);
-    return mb_verdict(c, rc == NK_OK);
+    const int v = mb_verdict(c, rc == NK_OK);
+    mb_host_unlink(c);  // (host mode) every rank has mapped it by the self-test's end
+    return v;
 }
 
 int nk_dist_mailbox_active(nk_ctx* c) { return (c && c->mb_on) ? 1 : 0; }
@@ -337,11 +513,15 @@ int nk_dist_path(nk_ctx* c, nk_path_info* out) {
     out->device = c->device;
     out->ranks_on_device = c->res_share;
     out->rccl = c->comm ? 1 : 0;
-    out->mailbox = c->mb_on ? 1 : 0;
-    // the resident sweep also needs the mailbox when ranks cross (RCCL reductions need the host between passes)
-    out->resident_sweep = (c->res_ok && (!c->comm || c->mb_on)) ? 1 : 0;
+    out->mailbox = c->mb_on ? (c->mb_host ? 2 : 1) : 0;
+    // what RAN, from the launches the context counted (not what the configuration would allow)
+    out->resident_sweep = c->n_sweep_resident > 0 ? 1 : 0;
     out->resident_blocks = c->res_gran ? c->res_blocks : 0;
-    out->halo_in_launch = (halo_fuse_knob() && c->mb_on && c->nranks > 1 && c->halo_cap > 0) ? 1 : 0;
+    out->halo_in_launch = (c->n_jv_halo_fused > 0 && c->n_jv_halo_separate == 0) ? 1 : 0;
+    out->jv_halo_fused = c->n_jv_halo_fused;
+    out->jv_halo_separate = c->n_jv_halo_separate;
+    out->sweeps_resident = c->n_sweep_resident;
+    out->mgs_passes = c->n_mgs_pass;
     out->mailbox_error = (c->mb_err && *(volatile int*)c->mb_err) ? 1 : 0;
     out->halo_cap = c->halo_cap;
     if (hipDeviceGetPCIBusId(out->pci_bus_id, (int)sizeof(out->pci_bus_id), c->device) != hipSuccess) {

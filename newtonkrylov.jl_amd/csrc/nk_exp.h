@@ -14,8 +14,9 @@
  *         double-double); expm1(r) = r + r^2/2 + r^3 P(r) with r^2 exact (fma) and the
  *         cubic tail in doubles; 2^(j/128) from a 128-entry double-double table; the result
  *         zh + zl carries a relative error below 2^-76 (bound in DESIGN.md; measured max
- *         ~2^-79 over 10^6 inputs, tests/test_exp.py).  If every value within
- *         2^-72 * zh of zh + zl rounds to zh, zh is the correctly rounded result.
+ *         ~2^-79 over 10^6 inputs, tests/test_exp.py).  A one-fma rounding test (nkx_exp_fast)
+ *         shows whether every value within 2^-73 zh of zh + zl rounds to zh; then zh is the
+ *         correctly rounded result.
  *   slow  (about 2^-18 of inputs, plus the subnormal and overflow bands): exact fixed-point
  *         arithmetic on 192-bit integers (Q2.190): x converted exactly, r = x - k ln2 with ln2
  *         to 2^-190, exp(r/256) by a 17-term Horner series with 1/i! to 2^-190, eight
@@ -258,7 +259,11 @@ NKX_FN int nkx_any_below(const nkx_u64 y[3], int pos) {
 /* round-to-nearest-even of y / 2^sh, sh in [1, 192]; the quotient fits 54 bits */
 NKX_FN nkx_u64 nkx_round_shift(const nkx_u64 y[3], int sh) {
     nkx_u64 q = 0;
-    for (int b = 63; b >= 0; --b) q = (q << 1) | nkx_bit(y, sh + b);
+    if (sh < 192) {
+        const int li = sh >> 6, bi = sh & 63;
+        q = y[li] >> bi;
+        if (bi && li < 2) q |= y[li + 1] << (64 - bi);
+    }
     const nkx_u64 rb = nkx_bit(y, sh - 1);
     if (rb && (nkx_any_below(y, sh - 1) || (q & 1))) q += 1;
     return q;
@@ -411,22 +416,34 @@ NKX_SLOW_FN double nkx_exp_rare(double x) {
     return nkx_exp_slow(x);
 }
 
-/* correctly rounded exp(x); `tab` as for nkx_exp_dd.  Branch-free up to one test: the fast phase runs
-   on x clamped into its range (so every conversion stays defined), and one combined condition --
-   inside the fast range and the Ziv test passed (false for NaN) -- decides whether its result stands. */
-NKX_FN double nk_exp_t(double x, const double* tab) {
+/* The fast phase with its rounding test: returns 1 and *y = exp(x) correctly rounded when it settles x,
+   else 0 (then nkx_exp_rare(x) does).  Branch-free: the fast phase runs on x clamped into its range
+   (every conversion stays defined) and one combined condition decides.  The Ziv test (CRlibm's form):
+   zh = RN(zh + zl) already; if also RN(zh + zl (1 + 2^-18)) == zh (one fma), every value within
+   eps zh of zh + zl rounds to zh for any eps < 2^-73 -- the rounding boundary on zl's side sits
+   ulp_b / 2 from zh with ulp_b >= 2^-53 zh (the smaller ulp below a power of two included): where
+   |zl| >= ulp_b / 4 the test leaves a margin 2^-18 |zl| >= 2^-73 zh, elsewhere the boundary is more
+   than ulp_b / 4 >= 2^-55 zh away.  The fast phase's bound is eps = 2^-76 (measured 2^-79.2).  The
+   test fails for about 2^-18 of inputs, and for NaN. */
+NKX_FN int nkx_exp_fast(double x, const double* tab, double* y) {
     const double xc = fmin(fmax(x, -708.3), 709.78); /* == x inside the fast range */
     double zl;
     int m;
     const double zh = nkx_exp_dd(xc, tab, &zl, &m);
-    const double err = zh * 0x1p-72;
-    const double lo = zh + (zl - err), hi = zh + (zl + err);
-    const int ok = (lo == zh) & (hi == zh) & (x < 709.78) & (x > -708.3);
-    if (ok) return ldexp(zh, m);
+    *y = ldexp(zh, m);
+    return (fma(zl, 0x1.00004p0, zh) == zh) & (x < 709.78) & (x > -708.3);
+}
+
+#ifndef NKX_OWN_EXP_T /* (the device header defines its own: one wave-uniform pass over the rare lanes) */
+/* correctly rounded exp(x); `tab` as for nkx_exp_dd */
+NKX_FN double nk_exp_t(double x, const double* tab) {
+    double y;
+    if (nkx_exp_fast(x, tab, &y)) return y;
     return nkx_exp_rare(x);
 }
 
 /* correctly rounded exp(x), table from NKX_T */
 NKX_FN double nk_exp(double x) { return nk_exp_t(x, &NKX_T[0][0]); }
+#endif
 
 #endif /* NK_EXP_H */

@@ -1,15 +1,39 @@
 // nk_exp_dev.hpp -- the correctly rounded exp (nk_exp.h) instantiated for device code.  nk_exp.h is
 // the same source the CPU oracle compiles, so every Bratu residual / JVP / FD value is bit-identical
-// to the oracle's (bratu.jl:21's lam * exp(u)).  The fast phase inlines into the stencils; the rare
-// exact phase (~2^-18 of inputs, plus the subnormal / overflow bands) is one call.
+// to the oracle's (bratu.jl:21's lam * exp(u)).
+//
+// Device form: every lane runs the branch-free fast phase (nkx_exp_fast, table in LDS for the
+// stencils).  The lanes it does not settle -- about 2^-18 of inputs, plus non-finite / out-of-range
+// ones -- are taken ONE AT A TIME by the whole wave: the lane's x is read into scalar registers
+// (readlane) and nkx_exp_rare runs on wave-uniform values, i.e. as scalar (SALU) code.  No call and
+// no per-lane divergent copy of the 192-bit fixed-point phase: the stencils' VGPR count is the fast
+// phase's alone (a called rare path cost them 24 VGPRs, a per-lane inlined one as many).
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 
 #define NKX_FN __device__ __forceinline__
-#ifndef NKX_SLOW_FN
-#define NKX_SLOW_FN __device__ __attribute__((noinline))
-#endif
+#define NKX_SLOW_FN __device__ __forceinline__
 #define NKX_CONST static __device__ const
+#define NKX_OWN_EXP_T 1
 #include "nk_exp.h"
+
+// correctly rounded exp(x); `tab` = NKX_T as 256 doubles (an LDS copy in the stencils)
+__device__ __forceinline__ double nk_exp_t(double x, const double* tab) {
+    double y;
+    const int ok = nkx_exp_fast(x, tab, &y);
+    unsigned long long rare = __ballot(!ok);
+    while (rare) {  // wave-uniform
+        const int l = __ffsll(rare) - 1;
+        const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+        const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+        const double ys = nkx_exp_rare(__hiloint2double(hi, lo));
+        if ((int)(threadIdx.x & 63) == l) y = ys;
+        rare &= rare - 1;
+    }
+    return y;
+}
+
+// correctly rounded exp(x), table from device memory
+__device__ __forceinline__ double nk_exp(double x) { return nk_exp_t(x, &NKX_T[0][0]); }

@@ -77,6 +77,17 @@ struct nk_ctx {
     uint64_t* mb_self = nullptr;           // my mailbox (kMbSlots x kMbRanks x 2 granules)
     uint64_t** mb_peers_dev = nullptr;     // device table: rank -> that rank's mailbox (IPC-mapped)
     std::vector<void*> mb_opened;          // IPC mappings to close
+    // host mailbox (NK_DIST_MAILBOX=host, or a peer's device invisible to this process): every rank's
+    // region lives in a POSIX shared-memory segment, mapped and hipHostRegister-ed by every rank
+    bool mb_host = false;                  // the active region (mb_self) is the host one
+    uint64_t* mb_dev = nullptr;            // my device region (fine-grained device memory, IPC-shared)
+    int64_t halo_cap_dev = 0;
+    void* mb_host_base = nullptr;          // my host region: its mapping here,
+    uint64_t* mb_host_dev = nullptr;       //   its device address,
+    size_t mb_host_bytes = 0;
+    int64_t halo_cap_host = 0;
+    char mb_host_name[48] = {0};           //   its shared-memory name (unlinked once every peer mapped it)
+    std::vector<std::pair<void*, size_t>> mb_host_maps;  // peers' segments mapped here
     int* mb_err = nullptr;                 // pinned host flag: a consumer timed out waiting for a peer
     int* mb_err_dev = nullptr;             // its device address
     unsigned mb_epoch = 1;
@@ -84,6 +95,9 @@ struct nk_ctx {
     uint64_t halo_epoch = 0;
     // resident MGS sweep (launch_mgs_sweep): one block per CU, q held in registers + LDS
     bool res_ok = true;                    // false when another rank shares this GPU (co-residency)
+    // what actually ran (nk_dist_path): Krylov Jv launches whose v ghost planes travelled inside the
+    // stencil launch / were exchanged by a separate launch first, resident sweeps, per-pass MGS launches
+    int64_t n_jv_halo_fused = 0, n_jv_halo_separate = 0, n_sweep_resident = 0, n_mgs_pass = 0;
     uint64_t* res_gran = nullptr;          // partial-sum granules: 2 parities x res_blocks x 2
     int* res_err = nullptr;                // pinned host flag: a granule poll timed out
     int* res_err_dev = nullptr;

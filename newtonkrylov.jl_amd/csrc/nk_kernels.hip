@@ -849,11 +849,13 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         const bool fuse = fuse_env && c->mb_on && (c->nranks > 1 || self) && !per && in.mode != MODE_RES &&
                           (g.dim == 2 || (g.dim == 3 && A.lds3)) && g.plane <= c->halo_cap && tiles_pl <= kHaloTileFlags;
         if (fuse) {
+            ++c->n_jv_halo_fused;
             A.hx_lo = c->rank > 0 || self;
             A.hx_hi = c->rank + 1 < c->nranks || self;
             A.hx_epoch = ++c->halo_epoch;
             A.hx_cap = c->halo_cap;
         } else {
+            if (c->nranks > 1 || per) ++c->n_jv_halo_separate;
             NK_TRY(halo_exchange(c, p, in.v));
         }
     }
@@ -988,6 +990,7 @@ int launch_mgs_pass(nk_ctx* c, int64_t n, double* q, const double* vi, const dou
     const int g = red_blocks(n);
     int fin;
     double* part = red_out(c, g, out, &fin);
+    ++c->n_mgs_pass;
     if (vnext)
         // unique-DRAM model: V_{i+1} is the next pass's V_i (counted there), so q in + q out + V_i
         return launch(c, "mgs_pass", 32.0 * n, [&] {

@@ -690,6 +690,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
     // serves the second read at best): np + 2 doubles per resident point (q in, V_1..V_np, q / V_{k+1}
     // out), 3 np for a streamed point (q read and written every pass, each V once)
     const double dram = 8.0 * (double)n * (f * ((jin ? 5.0 : 2.0) + np) + (1.0 - f) * (3.0 * np));
+    ++c->n_sweep_resident;
     return launch(c, jin ? "arnoldi_step" : "mgs_sweep", bytes, [&] {
         const dim3 g(c->res_blocks), b(kResThreads);
         switch (rv) {

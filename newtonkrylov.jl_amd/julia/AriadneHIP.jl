@@ -51,6 +51,10 @@ struct NkPathInfo
     mailbox_error::Int32
     halo_cap::Int64
     pci_bus_id::NTuple{32, UInt8}
+    jv_halo_fused::Int64
+    jv_halo_separate::Int64
+    sweeps_resident::Int64
+    mgs_passes::Int64
 end
 function path_info(ctx::HipContext)
     r = Ref{NkPathInfo}()
@@ -59,7 +63,8 @@ function path_info(ctx::HipContext)
     (rank = p.rank, nranks = p.nranks, device = p.device, ranks_on_device = p.ranks_on_device, rccl = p.rccl != 0,
      mailbox = p.mailbox != 0, resident_sweep = p.resident_sweep != 0, resident_blocks = p.resident_blocks,
      halo_in_launch = p.halo_in_launch != 0, mailbox_error = p.mailbox_error != 0, halo_cap = p.halo_cap,
-     pci_bus_id = String(UInt8[c for c in p.pci_bus_id if c != 0x00]))
+     pci_bus_id = String(UInt8[c for c in p.pci_bus_id if c != 0x00]), jv_halo_fused = p.jv_halo_fused,
+     jv_halo_separate = p.jv_halo_separate, sweeps_resident = p.sweeps_resident, mgs_passes = p.mgs_passes)
 end
 
 # --------------------------------------------------------------------------- nk_problem (C layout)

@@ -132,6 +132,8 @@ F_(res, u, p)
 ah.mul_(out, ah.JacobianOperator(F_, res, u, p, jv=args.jv), vd)
 jv_loc = out.to_numpy()
 F_loc = res.to_numpy()
+ah.mul_(out, ah.JacobianOperator(F_, res, u, p, jv="fd"), vd, eps=1e-7)  # a given eps: bit-comparable
+jvfd_loc = out.to_numpy()
 dot = ah.kdot(len(u), u, vd)
 if args.fault_rank >= 0:
     import time
@@ -160,23 +162,24 @@ if args.krylov_itmax > 0:
     sweeps = ctx.prof_read().get("mgs_sweep", {}).get("launches", 0)  # resident sweeps that ran
     ctx.prof_enable(0)
     parts = [None] * world
-    dist.all_gather_object(parts, dict(y0=y0, x=ws.x.to_numpy()))
+    dist.all_gather_object(parts, dict(y0=y0, x=ws.x.to_numpy(), F=F_loc, jvfd=jvfd_loc))
     if rank == 0:
         parts.sort(key=lambda d: d["y0"])
-        np.savez(args.out + ".npz", x=np.concatenate([d["x"] for d in parts]), h=np.array(ws.stats.residuals))
-        json.dump(dict(niter=ws.stats.niter, n_matvec=ws.stats.n_matvec, world=world, sweeps=sweeps),
-                  open(args.out + ".json", "w"))
+        cat = lambda key: np.concatenate([d[key] for d in parts])  # noqa: E731
+        np.savez(args.out + ".npz", x=cat("x"), F=cat("F"), jvfd=cat("jvfd"), v=v_glob, h=np.array(ws.stats.residuals))
+        json.dump(dict(niter=ws.stats.niter, n_matvec=ws.stats.n_matvec, world=world, sweeps=sweeps,
+                       path=ctx.path_info()), open(args.out + ".json", "w"))
     dist.barrier()
     ctx.sync()
     sys.exit(0)
 u, r = ah.newton_krylov_(F_, u, p, res, jv=args.jv, **kw)
 parts = [None] * world
-dist.all_gather_object(parts, dict(y0=y0, u=u.to_numpy(), jv=jv_loc, F=F_loc))
+dist.all_gather_object(parts, dict(y0=y0, u=u.to_numpy(), jv=jv_loc, F=F_loc, jvfd=jvfd_loc))
 if rank == 0:
     parts.sort(key=lambda d: d["y0"])
     np.savez(args.out + ".npz", u=np.concatenate([d["u"] for d in parts]), jv=np.concatenate([d["jv"] for d in parts]),
-             F=np.concatenate([d["F"] for d in parts]), v=v_glob)
+             F=np.concatenate([d["F"] for d in parts]), jvfd=np.concatenate([d["jvfd"] for d in parts]), v=v_glob)
     json.dump(dict(solved=bool(r.solved), outer=r.stats.outer_iterations, inner=r.stats.inner_iterations,
-                   n_res=r.stats.n_res, dot=dot, world=world), open(args.out + ".json", "w"))
+                   n_res=r.stats.n_res, dot=dot, world=world, path=ctx.path_info()), open(args.out + ".json", "w"))
 dist.barrier()
 ctx.sync()

@@ -108,7 +108,7 @@ def test_ziv_cases_take_the_exact_phase():
 
 def test_fast_phase_error_bound():
     """The fast phase's double-double result is within 2^-76 (relative) of exp(x) -- the Ziv test uses
-    2^-72, so a correct rounding decision never rests on the bound's last bits (measured ~2^-79)."""
+    test is valid up to 2^-73 (measured ~2^-79)."""
     rng = np.random.default_rng(9)
     x = np.concatenate([rng.uniform(-1.0, 3.0, 4000), rng.uniform(-708.0, 709.7, 4000)])
     zh, zl, m, _ = oc.exp_dd(x)

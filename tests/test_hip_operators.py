@@ -2,9 +2,10 @@
 form (:59-85), collect(J) (:140-162) -- pinned by the reference's own known answers
 (test/runtests.jl:4-54, run through a user residual on the device) and by the oracle.
 
-Tolerances: heat entries bit-identical (no transcendental); Bratu entries identical up to exp
-(torch / ocml vs glibc, <= 1 ulp of lambda e^u); colour-probed and unit-probed collect(J) are
-bit-identical (every probe entry is one Jacobian entry computed from the same operands).
+Tolerances: every entry bit-identical -- heat has no transcendental, and the Bratu kernels and the
+Kelley user residual take exp from the correctly rounded nk_exp (csrc/nk_exp.h, shared with the
+oracle); colour-probed and unit-probed collect(J) are bit-identical (every probe entry is one
+Jacobian entry computed from the same operands).
 """
 import json
 import os
@@ -67,13 +68,7 @@ def test_collect_matches_oracle_and_unit_probing(ctx, kind):
     np.testing.assert_array_equal(A, B)
     ref = oracle_dense_jacobian(P, u0)
     assert np.array_equal(A != 0, ref != 0)  # the stencil pattern
-    if kind.startswith("heat"):
-        np.testing.assert_array_equal(A, ref)
-    else:
-        lam_e = P.lam * np.exp(u0.reshape(-1))
-        np.testing.assert_allclose(np.diag(A), np.diag(ref), rtol=0, atol=0 + (4 * ULP * lam_e + 2 * np.spacing(np.abs(np.diag(ref)))).max())
-        off = ~np.eye(P.n, dtype=bool)
-        np.testing.assert_array_equal(A[off], ref[off])
+    np.testing.assert_array_equal(A, ref)
     # transpose: collect(transpose(J)) == transpose(collect(J))  (runtests.jl:54)
     np.testing.assert_array_equal(ah.collect(ah.transpose(J)).toarray(), A.T)
 
@@ -98,25 +93,40 @@ def test_transpose_and_batched_mul(ctx):
     assert J.T.size == tuple(reversed(J.size))
 
 
-def _kelley_user():
-    """runtests.jl's 2x2 problem, F(x) = [x1^2 + x2^2 - 2, exp(x1 - 1) + x2^2 - 2], as a device user
-    residual (torch), with its tangent and transpose tangent."""
+def _exp1m(X):
+    """exp(x1 - 1) through the library's correctly rounded exp (ah.exp_, nk_vexp), a 1-element tensor"""
     import torch
+
+    t = (X[0:1] - 1).contiguous()
+    return ah.exp_(torch.empty_like(t), t)
+
+
+def kelley_oop(x, p):
+    """runtests.jl:10-14's out-of-place F(x, p) (a new array; x is a torch view of the device vector)"""
+    import torch
+
+    return torch.cat([x[0:1] ** 2 + x[1:2] ** 2 - 2, _exp1m(x) + x[1:2] ** 2 - 2])
+
+
+def _kelley_user():
+    """runtests.jl's 2x2 problem, F(x) = [x1^2 + x2^2 - 2, exp(x1 - 1) + x2^2 - 2] (runtests.jl:4-7), as a
+    device user residual (torch) with exp from ah.exp_, its tangent -- Enzyme's forward mode of F!, term
+    by term -- and transpose tangent."""
 
     def F(res, x, p):
         X = x.torch()
         r = res.torch()
         r[0] = X[0] ** 2 + X[1] ** 2 - 2
-        r[1] = torch.exp(X[0] - 1) + X[1] ** 2 - 2
+        r[1] = _exp1m(X)[0] + X[1] ** 2 - 2
 
     def J(out, x, v, p):
         X, V, o = x.torch(), v.torch(), out.torch()
         o[0] = 2 * X[0] * V[0] + 2 * X[1] * V[1]
-        o[1] = torch.exp(X[0] - 1) * V[0] + 2 * X[1] * V[1]
+        o[1] = _exp1m(X)[0] * V[0] + 2 * X[1] * V[1]
 
     def JT(out, x, w, p):
         X, W, o = x.torch(), w.torch(), out.torch()
-        o[0] = 2 * X[0] * W[0] + torch.exp(X[0] - 1) * W[1]
+        o[0] = 2 * X[0] * W[0] + _exp1m(X)[0] * W[1]
         o[1] = 2 * X[1] * W[0] + 2 * X[1] * W[1]
 
     return ah.UserResidual(F, J, name="kelley!", JT=JT)
@@ -131,17 +141,31 @@ def test_reference_known_answers_through_the_device(ctx, golden_dir):
     J = ah.JacobianOperator(K, res, x, None)
     out = x.zero()
     ah.mul_(out, J, ah.DeviceArray.from_numpy(np.array([1.0, 0.0])))  # runtests.jl:36-38
-    np.testing.assert_allclose(out.to_numpy(), ka["jvp_e1"], rtol=ULP, atol=0)
+    assert out.to_numpy().tolist() == ka["jvp_e1"] == [6.0, 7.38905609893065]  # exactly: exp(2.0), rounded once
     ah.mul_(out, J.T, ah.DeviceArray.from_numpy(np.array([1.0, 0.0])))  # runtests.jl:40-42
-    np.testing.assert_array_equal(out.to_numpy(), ka["vjp_e1"])
-    A = ah.collect(J).toarray()  # runtests.jl:44-46
-    np.testing.assert_allclose(A, np.array(ka["jacobian"]), rtol=ULP, atol=0)
+    assert out.to_numpy().tolist() == ka["vjp_e1"]
+    A = ah.collect(J).toarray()  # runtests.jl:44-46: collect(J) == J_Enz
+    assert A.tolist() == ka["jacobian"]
     np.testing.assert_array_equal(ah.collect(J.T).toarray(), A.T)  # runtests.jl:54
+    # runtests.jl:57-66 (batched): mul!(Out, J, I) == J_Enz, mul!(Out, transpose(J), I) == collect(transpose(J))
+    cols = [ah.DeviceArray.from_numpy(np.array(c)) for c in ([1.0, 0.0], [0.0, 1.0])]
+    outs = [x.zero(), x.zero()]
+    ah.mul_(outs, J, cols)
+    assert np.column_stack([o.to_numpy() for o in outs]).tolist() == ka["jacobian"]
+    ah.mul_(outs, J.T, cols)
+    np.testing.assert_array_equal(np.column_stack([o.to_numpy() for o in outs]), ah.collect(J.T).toarray())
     for x0 in ka["starts_inplace"]:  # runtests.jl:15-18: newton_krylov! from (2, 0.5) is solved
         u, r = ah.newton_krylov_(K, ah.DeviceArray.from_numpy(np.array(x0)), None)
         assert r.solved
         np.testing.assert_allclose(u.to_numpy(), ka["root"], atol=1e-5)
         u, r = ah.newton_krylov_(K, ah.DeviceArray.from_numpy(np.array(x0)), None, jv="fd")
+        assert r.solved
+    for x0 in ka["starts_outofplace"]:  # runtests.jl:20-23: newton_krylov(F, (3, 5)) -- out of place -- is solved
+        x0d = ah.DeviceArray.from_numpy(np.array(x0))
+        u, r = ah.newton_krylov(kelley_oop, x0d, None, jv="fd")
+        assert r.solved and x0d.to_numpy().tolist() == x0  # u0 untouched
+        np.testing.assert_allclose(u.to_numpy(), ka["root"], atol=1e-5)
+        u, r = ah.newton_krylov(K, x0d, None)  # the same start with the exact tangent
         assert r.solved
 
 

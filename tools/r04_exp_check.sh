@@ -21,6 +21,6 @@ step probe 300 python -u tools/bratu_parity_probe.py
 step bench 300 python -u bench.py --steps 20 --warmup 5
 tail -n 1 $OUT/bench.log > $OUT/bench.json
 if [ "${AB:-1}" = 1 ]; then
-    VARIANTS="NK_EXP_OCML=0|NK_EXP_OCML=1" WL="${AB_WL:-bratu2d}" ROUNDS=${AB_ROUNDS:-2} step ab_exp 900 bash tools/ab_env.sh
+    VARIANTS="${AB_VARIANTS:-NK_EXP_OCML=0|NK_EXP_OCML=1}" WL="${AB_WL:-bratu2d}" ROUNDS=${AB_ROUNDS:-2} step ab_exp 900 bash tools/ab_env.sh
 fi
 echo "[r04] done"
