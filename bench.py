@@ -151,27 +151,33 @@ def cpu_thread_probe(affinity, share):
 def copy_calibration(device, n=1 << 27, reps=5):
     """Achievable HBM streaming rate on this GPU: a plain copy over two 1 GiB vectors (nkb_copy, one 16-B
     element per thread, non-temporal), run after the timed region (GB/s on 16 B per element).  The copy
-    is a timing hook of the kernel-variant bench build (lib/libnkhip_kbench.so, its own context): the
-    product library carries no timing hooks."""
-    import ctypes as C
-
+    is a timing hook of the kernel-variant bench build (lib/libnkhip_kbench.so): the product library
+    carries no timing hooks.  It runs in a short child process that loads only that build, so the two
+    copies of the library (same kernels, same device globals) never share a process."""
     from ariadne_hip import _lib
 
     if not os.path.exists(_lib.KBENCH_LIB):
         return None
-    kb = C.CDLL(_lib.KBENCH_LIB)
-    kb.nk_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
-    kb.nk_ctx_destroy.argtypes = [C.c_void_p]
-    kb.nkb_copy.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.POINTER(C.c_double)]
-    h = C.c_void_p()
-    if kb.nk_ctx_create(device, C.byref(h)) != 0:
+    code = (
+        "import ctypes as C, sys\n"
+        f"kb = C.CDLL({_lib.KBENCH_LIB!r})\n"
+        "kb.nk_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]\n"
+        "kb.nk_ctx_destroy.argtypes = [C.c_void_p]\n"
+        "kb.nkb_copy.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.POINTER(C.c_double)]\n"
+        "h = C.c_void_p()\n"
+        f"if kb.nk_ctx_create({int(device)}, C.byref(h)) != 0: sys.exit(1)\n"
+        "us = C.c_double()\n"
+        f"rc = kb.nkb_copy(h, {int(n)}, {int(reps)}, C.byref(us))\n"
+        "kb.nk_ctx_destroy(h)\n"
+        "print(us.value if rc == 0 else -1.0)\n")
+    try:
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180)
+        us = float(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 and r.stdout.strip() else -1.0
+    except (subprocess.TimeoutExpired, ValueError, IndexError):
         return None
-    us = C.c_double()
-    rc = kb.nkb_copy(h, n, reps, C.byref(us))
-    kb.nk_ctx_destroy(h)
-    if rc != 0 or us.value <= 0:
+    if us <= 0:
         return None
-    return 16.0 * n / (us.value * 1e-6) / 1e9
+    return 16.0 * n / (us * 1e-6) / 1e9
 
 
 def free_port() -> int:

@@ -84,6 +84,7 @@ int mb_check(nk_ctx* c) {
     if (c->ilu_err && *(volatile int*)c->ilu_err) {  // a strip of the pipelined ILU(0) sweep never advanced
         *c->ilu_err = 0;
         c->ilu_pipe_ok = false;  // later sweeps use the one-work-group level sweep
+        c->ilu_redo = true;      // nk_krylov_solve / nk_precond_apply redo their work once on it
         return fail(c, NK_E_HIP, "pipelined ILU(0) sweep: a strip's progress never arrived (timeout); pipelined sweep disabled");
     }
     return NK_OK;

@@ -109,6 +109,7 @@ struct nk_ctx {
     int64_t* ilu_prog = nullptr;
     int64_t ilu_prog_cap = 0;
     int* ilu_err = nullptr;
+    bool ilu_redo = false;                 // a pipelined ILU(0) sweep timed out: the caller redoes its work (level sweep)
     int* ilu_err_dev = nullptr;
     bool ilu_pipe_ok = true;               // false after a progress poll timed out: the one-work-group sweep
     // distribution

@@ -652,7 +652,14 @@ int nk_precond_apply(nk_ctx* c, const nk_problem* p, const nk_precond* N, const 
     }
     double dummy = 0.0;
     NK_TRY(apply_precond(c, p, N, A, g.n, z, v, false, &dummy));
-    return nk_sync(c);
+    int rc = nk_sync(c);
+    if (rc != NK_OK && c->ilu_redo) {  // a pipelined ILU(0) sweep timed out: once more on the level sweep
+        c->ilu_redo = false;
+        c->err.clear();
+        NK_TRY(apply_precond(c, p, N, A, g.n, z, v, false, &dummy));
+        rc = nk_sync(c);
+    }
+    return rc;
 }
 
 int nk_workspace_create(nk_ctx* c, int32_t algo, const nk_problem* p, int32_t memory, nk_workspace** out) {
@@ -745,6 +752,19 @@ int nk_krylov_solve(nk_workspace* ws, const nk_problem* p, const double* u, cons
         return fail(c, NK_E_ARG, "the device CG takes no right preconditioner (use GMRES / FGMRES)");
     int rc = (ws->algo == NK_ALGO_CG) ? cg(ws, A, b, o, st, hist, hist_cap, hist_len)
                                       : gmres(ws, p, A, b, o, st, hist, hist_cap, hist_len);
+    if (rc != NK_OK && c->ilu_redo && !ws->u_fused) {
+        // a pipelined ILU(0) sweep timed out (reported at the step's sync, not by a sync per apply):
+        // the whole solve once more, every ILU(0) apply now on the level sweep (u is still untouched)
+        c->ilu_redo = false;
+        c->err.clear();
+        (void)hipStreamSynchronize(c->stream);
+        *st = nk_krylov_stats{};
+        if (hist_len) *hist_len = 0;
+        A.n_matvec = 0;
+        rc = (ws->algo == NK_ALGO_CG) ? cg(ws, A, b, o, st, hist, hist_cap, hist_len)
+                                      : gmres(ws, p, A, b, o, st, hist, hist_cap, hist_len);
+    }
+    c->ilu_redo = false;
     st->n_matvec = A.n_matvec;
     if (rc == NK_OK && o->u_update && !ws->u_fused) {  // not fused (CG, early exits): u .-= x, ||u||
         Red ru{};

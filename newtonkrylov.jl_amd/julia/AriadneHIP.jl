@@ -95,20 +95,24 @@ mutable struct HipVector <: AbstractVector{Float64}
     ctx::HipContext
     ptr::Ptr{Float64}
     grid::NTuple{3, Int}
-    gen::Int     # bumped by every write this shim makes (touch!)
+    gen::Int     # a stamp from the process-wide counter GEN, renewed by every write this shim makes (touch!)
     f0of::Any    # set by a built-in residual F!(res, u, p): (u, u.gen, p) it was evaluated at; `nothing` once rewritten
     function HipVector(ctx::HipContext, grid::NTuple{3, Int})
         r = Ref{Ptr{Float64}}(C_NULL)
         p = geometry(grid)
         check(ccall((:nk_vec_alloc, libnkhip), Cint, (Ptr{Cvoid}, Ref{NkProblem}, Ref{Ptr{Float64}}), ctx.ptr, p, r),
               ctx, "nk_vec_alloc")
-        v = new(ctx, r[], grid, 0, nothing)
+        v = new(ctx, r[], grid, next_gen(), nothing)
         finalizer(x -> ccall((:nk_vec_free, libnkhip), Cint, (Ptr{Cvoid}, Ptr{Float64}), x.ctx.ptr, x.ptr), v)
     end
     # non-owning view of library-owned storage (e.g. the Krylov workspace's x)
-    HipVector(ctx::HipContext, ptr::Ptr{Float64}, grid::NTuple{3, Int}) = new(ctx, ptr, grid, 0, nothing)
+    HipVector(ctx::HipContext, ptr::Ptr{Float64}, grid::NTuple{3, Int}) = new(ctx, ptr, grid, next_gen(), nothing)
 end
-touch!(v::HipVector) = (v.gen += 1; v.f0of = nothing; v)
+# One monotonically increasing counter for every vector and every write: a (objectid, gen) stamp can
+# never repeat, even when a collected vector's objectid is reused by a new one (whose gen is fresh).
+const GEN = Threads.Atomic{Int}(0)
+next_gen() = Threads.atomic_add!(GEN, 1) + 1
+touch!(v::HipVector) = (v.gen = next_gen(); v.f0of = nothing; v)
 # the state a residual was evaluated at: u and every device vector in p (u_n of the heat problems) by
 # identity and write generation, the scalars by value
 stampof(x::HipVector) = (objectid(x), x.gen)
