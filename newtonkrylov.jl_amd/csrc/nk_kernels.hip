@@ -734,7 +734,7 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     A.nx = p->nx; A.ny = p->ny; A.nz = p->nz;
     A.hx2 = p->hx * p->hx; A.hy2 = p->hy * p->hy; A.hz2 = p->hz * p->hz;
     A.lam = p->lambda; A.a = p->a; A.dt = p->dt; A.eps = in.eps;
-    A.fast = fast | (NK_TUNE("NK_EXP_OCML", 0) ? 4 : 0);  // kbench A/B: the platform exp
+    A.fast = fast | (NK_TUNE("NK_EXP_OCML", 0) ? (1 << 20) : 0);  // kbench A/B (bit 2^20): the platform exp
     A.vdiv = in.vdiv;
     A.vout = in.vout;
     A.ihx2 = 1.0 / A.hx2; A.ihy2 = 1.0 / A.hy2; A.ihz2 = 1.0 / A.hz2; A.ieps = in.eps != 0.0 ? 1.0 / in.eps : 0.0;
@@ -819,6 +819,17 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         // plane-major order, upward marches (0, the product) -- profiles/r03/ab_zalt*.log
         static const int zalt_env = NK_TUNE("NK_ST3_ZALT", 0);
         A.zalt = (A.lds3 && !(fast & 65536)) ? zalt_env : 0;  // kbench fast bit 65536: the plane-major order
+        // the y-march (k_st3y, kbench NK_ST3_YMARCH=1: slabs short along z; NK_ST3Y_ROWS rows per chunk):
+        // tiles of nw planes x 64 vec columns marching a chunk of rows
+        static const int ym_env = NK_TUNE("NK_ST3_YMARCH", 0);
+        static const int ym_rows = NK_TUNE("NK_ST3Y_ROWS", 64);
+        A.ym = (A.lds3 && (ym_env || (fast & 524288)) && rows_override <= 0 && !A.zalt) ? 1 : 0;  // (bit 2^19: the y-march)
+        if (A.ym) {
+            const int64_t r = std::min<int64_t>(std::max(1, ym_rows), p->ny);
+            A.rows = (int)r;
+            A.tiles_y = (int)((p->ny + r - 1) / r);
+            grid = A.tiles_x * A.tiles_y * (int)((p->nz + A.nw - 1) / A.nw);
+        }
     }
     // FD with F0 recomputed from u (2D, VEC <= 2: k_st2d<..., F0R>; 3D heat: k_st3l<..., F0R>, not
     // with NK_F0R=3 (A/B)); never with the `fast` reciprocals,

@@ -31,6 +31,7 @@ struct KArgs {
     double alpha;        // G_Midpoint! α
     int nw;              // 3D: rows (waves) per tile
     int lds3;            // 3D: y-neighbour rows through LDS (k_st3l) instead of per-wave loads (k_st3d)
+    int ym;              // 3D: the y-march (k_st3y: NW planes per tile, rows marched, z-neighbours through LDS)
     int lin;             // tiles in dispatch (= address) order instead of XCD-contiguous bands
     int zalt;            // 3D: z-chunks of one tile column dispatched together, odd chunks marching down
     int tile2;           // 2D one-shot LDS tiles of tile2 rows (k_st2t) instead of the row march (0: march)
@@ -166,7 +167,7 @@ __device__ __forceinline__ double point_value(const KArgs& A, double c, double l
                                               double xc, double lsumg, const double* et) {
     if constexpr (KIND == NK_BRATU1D || KIND == NK_BRATU2D) {
 #ifdef NK_KBENCH
-        if (A.fast & 4) {  // kbench A/B only: the platform (ocml) exp, <= 1 ulp off the correctly rounded one
+        if (A.fast & (1 << 20)) {  // kbench A/B only: the platform (ocml) exp, <= 1 ulp off the correctly rounded one
             if (MODE == MODE_JEXACT) return lsum + A.lam * (exp(uc) * c);
             const double r = lsum + A.lam * exp(c);
             return MODE == MODE_JFD ? fdq(A, r, f0c) : r;
@@ -1278,6 +1279,236 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
     if constexpr (EPI != EPI_NONE) publish<64 * NW>(acc, A.part, A.fin, sh, tz * A.tiles_x * A.tiles_y + txy);
 }
 
+// ------------------------------------------------------------------------------ 3D stencil, y-march
+// For slabs that are short along z (config 5: 512^2 x 64 per rank): the tile is NW consecutive PLANES
+// (one wave each) x 64*VEC columns, and it marches along y over a chunk of A.rows rows.  The roles of
+// k_st3l's axes swap: the z-neighbours of row j come from the adjacent waves through LDS (the tile's
+// edge waves load the halo planes' row -- the slab's ghost planes from memory, or from the inbox when
+// they travel in this launch), the y-neighbours are the march's registers, x-neighbours shuffles.  The
+// march re-reads (rows + 2) / rows of each field instead of the z-march's (16 + 2) / 16.  Arithmetic and
+// association order are k_st3l's: ((x-Laplacian + y-Laplacian) + z-Laplacian), so every output is
+// bit-identical to it.  Rows -1 / ny are not in memory (the ghost layer lives along z only): the zero
+// boundary there, or the wrapped row under bc_periodic!.
+template <int KIND, int MODE, int EPI, int VEC, bool PER = false, int NW = 4, bool F0R = false>
+__global__ __launch_bounds__(64 * NW) void k_st3y(KArgs A0) {
+    __shared__ double sh[kShN];
+    const double* const et = nullptr;  // heat kinds: no exp
+    KArgs A = A0;
+    A.hd = A.vdiv ? *A.vdiv : 1.0;
+    constexpr int SCH = scheme_of<KIND>();
+    constexpr bool kG = SCH != 0 && MODE != MODE_JEXACT;
+    constexpr bool kTG = SCH == 2 && kG;
+    constexpr bool kR = MODE == MODE_JFD && F0R;
+    __shared__ double lz[2][kTG ? 2 : 1][NW][64 * VEC];
+    __shared__ double lzu[2][kR ? NW : 1][kR ? 64 * VEC : 1];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int64_t nx = A.nx, ny = A.ny, nz = A.nz, pl = nx * ny;
+    int tz, txy;
+    tile3_of(b, nb, A.tiles_x, A.tiles_y, (int)((nz + NW - 1) / NW), A.hx_lo, A.hx_hi, 0, tz, txy);
+    const int ty = txy / A.tiles_x, tx = txy % A.tiles_x;
+    const int64_t x0 = (int64_t)tx * (64 * VEC) + (int64_t)lane * VEC;
+    const int64_t k = (int64_t)tz * NW + wv;  // my plane
+    const bool act = x0 < nx && k < nz;
+    const int64_t ok0 = act ? k * pl + x0 : 0;  // row 0 of my plane at my columns
+    // z-neighbours: the adjacent wave's LDS row when it is in this tile, else the halo plane's row (the
+    // ghost planes -1 / nz exist in memory: zero, or the neighbour slab's / the ring's plane)
+    const bool lds_u = wv + 1 < NW && k + 1 < nz;
+    const bool lds_d = wv >= 1;
+    const bool ld_u = !lds_u && act, ld_d = !lds_d && act;  // wave-uniform
+    const XEdge xe = x_edge<VEC, PER>(lane, act, x0, nx);
+    const int64_t de = xe.de, de2 = xe.de2;
+    const bool edge_ok = xe.ok, edge_ok2 = xe.ok2;
+    const int64_t y0 = (int64_t)ty * A.rows;
+    const int64_t y1 = y0 + A.rows < ny ? y0 + A.rows : ny;
+    constexpr bool kUn = SCH == 0 && MODE != MODE_JEXACT;
+    constexpr bool kF0 = MODE == MODE_JFD && !kR;
+    constexpr bool kAx = EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID;
+    constexpr bool vout = MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS);
+    // ghost planes of v fetched in this launch: the z-tiles at the slab's ends exchange the patch rows
+    // [y0, y1) x their columns of my first / last plane
+    const uint64_t* ib_lo = nullptr;
+    const uint64_t* ib_hi = nullptr;
+    if constexpr (MODE != MODE_RES && !PER) {
+        const int nzt = (int)((nz + NW - 1) / NW);
+        const HaloTile ht{A.hx_lo && tz == 0 && y0 < ny, A.hx_hi && tz == nzt - 1 && y0 < ny};
+        if (ht.lo || ht.hi) {  // block-uniform
+            const int64_t ca = (int64_t)tx * (64 * VEC), cb = ca + 64 * VEC < nx ? ca + 64 * VEC : nx;
+            if (halo_tile_exchange(A.v, pl, nz, nx, y0, y1, ca, cb, txy, ht, A.hx_epoch, A.hx_cap, 64 * NW)) {
+                const int par = (int)(A.hx_epoch & 1);
+                if (ht.lo) ib_lo = halo_inbox(g_mb.self, par, 0, A.hx_cap);
+                if (ht.hi) ib_hi = halo_inbox(g_mb.self, par, 1, A.hx_cap);
+            }
+        }
+    }
+    // the inbox holding my halo plane's row, if any (wave-uniform)
+    const uint64_t* ibu = (ib_hi && k + 1 == nz) ? ib_hi : nullptr;
+    const uint64_t* ibd = (ib_lo && k == 0) ? ib_lo : nullptr;
+    // row r of my plane (r in [-1, ny]): in range, or wrapped (PER); rows -1 / ny are zero otherwise
+    auto row_ok = [&](int64_t r) { return PER || (r >= 0 && r < ny); };
+    auto row_off = [&](int64_t r) {
+        const int64_t rr = PER ? (r < 0 ? r + ny : (r >= ny ? r - ny : r)) : (r < 0 ? 0 : (r >= ny ? ny - 1 : r));
+        return ok0 + rr * nx;
+    };
+    auto centre_row = [&](int64_t r) {
+        const int64_t o = row_off(r);
+        return load_raw<MODE, VEC, true, kG, PER>(A, o, o + de, o + de2);
+    };
+    auto halo_row = [&](int64_t r, bool up) {  // plane k +- 1, row r (r in [0, ny))
+        const int64_t o = row_off(r) + (up ? pl : -pl);
+        const uint64_t* ib = up ? ibu : ibd;
+        return ib ? load_raw_ib<MODE, VEC, kG>(A, ib, o, o - (up ? (k + 1) : (k - 1)) * pl)
+                  : load_raw<MODE, VEC, false, kG, PER>(A, o, 0);
+    };
+    double acc = 0.0;
+    if (y0 < ny && tz * (int64_t)NW < nz) {
+        // rows y0-1 and y0 cooked up front; row y0+1 raw in flight
+        const RawRow<MODE, VEC> rm0 = centre_row(y0 - 1);
+        const RawRow<MODE, VEC> rc0 = centre_row(y0);
+        Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(A, rm0, act && row_ok(y0 - 1), edge_ok && row_ok(y0 - 1),
+                                                      edge_ok2 && row_ok(y0 - 1));
+        Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, rc0, act, edge_ok, edge_ok2);
+        Field<VEC> um{}, uc_{};
+        if constexpr (kR) {
+            um = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rm0), act && row_ok(y0 - 1),
+                                                   edge_ok && row_ok(y0 - 1), edge_ok2 && row_ok(y0 - 1));
+            uc_ = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rc0), act, edge_ok, edge_ok2);
+        }
+        RawRow<MODE, VEC> rp = centre_row(y0 + 1);
+        RawRow<MODE, VEC> ru{}, rd{};
+        if (ld_u) ru = halo_row(y0, true);
+        if (ld_d) rd = halo_row(y0, false);
+        Row<VEC> unc{}, f0c{}, ax{};
+        {
+            const int64_t o = row_off(y0);
+            if constexpr (kUn) unc = data_row<VEC, NK_ST_NTN>(A.un, o, true);
+            if constexpr (kF0) f0c = data_row<VEC, NK_ST_NT>(A.F0, o, true);
+            if constexpr (kAx) ax = data_row<VEC>(A.aux, o, true);
+        }
+        const int cnt = (int)(y1 - y0);
+        for (int it = 0; it < cnt; ++it) {
+            const int64_t j = y0 + it;
+            const int64_t o = row_off(j);
+            const int par = it & 1;
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) {
+                lz[par][0][wv][lane * VEC + q] = fc.c[q];
+                if constexpr (kTG) lz[par][kTG ? 1 : 0][wv][lane * VEC + q] = fc.g[q];
+                if constexpr (kR) lzu[par][kR ? wv : 0][kR ? lane * VEC + q : 0] = uc_.c[q];
+            }
+            // ---- issue: row j+2, the halo rows and centre data of row j+1
+            const bool more = it + 1 < cnt;
+            const int64_t j2 = more ? j + 2 : j + 1, j1 = more ? j + 1 : j;
+            const RawRow<MODE, VEC> rpp = centre_row(j2);
+            RawRow<MODE, VEC> ruu{}, rdd{};
+            if (ld_u) ruu = halo_row(j1, true);
+            if (ld_d) rdd = halo_row(j1, false);
+            Row<VEC> uncn{}, f0cn{}, axn{};
+            const int64_t o1 = row_off(j1);
+            if constexpr (kUn) uncn = data_row<VEC, NK_ST_NTN>(A.un, o1, true);
+            if constexpr (kF0) f0cn = data_row<VEC, NK_ST_NT>(A.F0, o1, true);
+            if constexpr (kAx) axn = data_row<VEC>(A.aux, o1, true);
+            // ---- cook what was issued one iteration ago
+            const bool pok = row_ok(j + 1);
+            const Field<VEC> fp = cook<MODE, VEC, SCH, kG, PER>(A, rp, act && pok, edge_ok && pok, edge_ok2 && pok);
+            Field<VEC> fu{}, fd{};
+            if (ld_u) fu = cook<MODE, VEC, SCH, kG, PER>(A, ru, act, false);
+            if (ld_d) fd = cook<MODE, VEC, SCH, kG, PER>(A, rd, act, false);
+            Field<VEC> up{}, fuu{}, fdu{};
+            if constexpr (kR) {
+                up = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rp), act && pok, edge_ok && pok, edge_ok2 && pok);
+                if (ld_u) fuu = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(ru), act, false);
+                if (ld_d) fdu = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rd), act, false);
+            }
+            __syncthreads();  // row j of every plane of the tile is in LDS
+            double cu[VEC], cd[VEC], gu[VEC], gd[VEC];
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) {
+                cu[q] = lds_u ? lz[par][0][wv + (lds_u ? 1 : 0)][lane * VEC + q] : fu.c[q];
+                cd[q] = lds_d ? lz[par][0][wv - (lds_d ? 1 : 0)][lane * VEC + q] : fd.c[q];
+                if constexpr (kTG) {
+                    gu[q] = lds_u ? lz[par][1][wv + (lds_u ? 1 : 0)][lane * VEC + q] : fu.g[q];
+                    gd[q] = lds_d ? lz[par][1][wv - (lds_d ? 1 : 0)][lane * VEC + q] : fd.g[q];
+                } else {
+                    gu[q] = gd[q] = 0.0;
+                }
+            }
+            double cuu[VEC], cdu[VEC];
+            LR xu{};
+            if constexpr (kR) {
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) {
+                    cuu[q] = lds_u ? lzu[par][kR ? wv + (lds_u ? 1 : 0) : 0][kR ? lane * VEC + q : 0] : fuu.c[q];
+                    cdu[q] = lds_d ? lzu[par][kR ? wv - (lds_d ? 1 : 0) : 0][kR ? lane * VEC + q : 0] : fdu.c[q];
+                }
+                xu = x_nbrs<PER>(uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
+            }
+            // ---- compute row j of my plane
+            const LR xn = x_nbrs<PER>(fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
+            const double lft = xn.l, rgt = xn.r;
+            double glft = 0.0, grgt = 0.0;
+            if constexpr (SCH == 2 && kG) {
+                const LR g2 = x_nbrs<PER>(fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
+                glft = g2.l;
+                grgt = g2.r;
+            }
+            if (act) {
+                Row<VEC> val;
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) {
+                    const double w = (q == 0) ? lft : fc.c[q == 0 ? 0 : q - 1];
+                    const double e = (q == VEC - 1) ? rgt : fc.c[q == VEC - 1 ? q : q + 1];
+                    const double c = fc.c[q];
+                    const double lsum = (lapk(A, c, e, w, A.hx2, A.ihx2) + lapk(A, c, fp.c[q], fm.c[q], A.hy2, A.ihy2)) +
+                                        lapk(A, c, cu[q], cd[q], A.hz2, A.ihz2);
+                    double lsumg = 0.0;
+                    if constexpr (SCH == 2 && kG) {
+                        const double g = fc.g[q];
+                        const double gw = (q == 0) ? glft : fc.g[q == 0 ? 0 : q - 1];
+                        const double ge = (q == VEC - 1) ? grgt : fc.g[q == VEC - 1 ? q : q + 1];
+                        lsumg = (lapk(A, g, ge, gw, A.hx2, A.ihx2) + lapk(A, g, fp.g[q], fm.g[q], A.hy2, A.ihy2)) +
+                                lapk(A, g, gu[q], gd[q], A.hz2, A.ihz2);
+                    }
+                    const double unq = kG ? fc.g[q] : unc.v[q];
+                    double f0 = f0c.v[q];
+                    if constexpr (kR) {
+                        const double uw = (q == 0) ? xu.l : uc_.c[q == 0 ? 0 : q - 1];
+                        const double ue = (q == VEC - 1) ? xu.r : uc_.c[q == VEC - 1 ? q : q + 1];
+                        const double ucc = uc_.c[q];
+                        const double lsu = (lapk(A, ucc, ue, uw, A.hx2, A.ihx2) + lapk(A, ucc, up.c[q], um.c[q], A.hy2, A.ihy2)) +
+                                           lapk(A, ucc, cuu[q], cdu[q], A.hz2, A.ihz2);
+                        f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unq, 0.0, SCH == 1 ? uc_.x[q] : ucc, lsumg, et);
+                    }
+                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0, SCH == 1 ? fc.x[q] : c, lsumg, et);
+                    acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[q] : ax.v[q], acc);
+                    val.v[q] = r;
+                }
+                store_row<VEC>(A.out, o, val);
+                if (vout) {
+                    Row<VEC> vn;
+#pragma unroll
+                    for (int q = 0; q < VEC; ++q) vn.v[q] = fc.vn[q];
+                    store_row<VEC, NK_ST_NT>(A.vout, o, vn);
+                }
+            }
+            fm = fc;
+            fc = fp;
+            if constexpr (kR) {
+                um = uc_;
+                uc_ = up;
+            }
+            rp = rpp;
+            ru = ruu;
+            rd = rdd;
+            unc = uncn;
+            f0c = f0cn;
+            ax = axn;
+        }
+    }
+    if constexpr (EPI != EPI_NONE) publish<64 * NW>(acc, A.part, A.fin, sh, tz * A.tiles_x * A.tiles_y + txy);
+}
+
 // ------------------------------------------------------------------------------ stencil dispatch
 template <int KIND, int MODE, int EPI, int NW>
 void go_st3l(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
@@ -1305,6 +1536,30 @@ void go_st3l(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
     }
     if (vec == 2) hipLaunchKernelGGL((k_st3l<KIND, MODE, EPI, 2, false, NW>), dim3(grid), dim3(64 * NW), 0, s, A);
     else hipLaunchKernelGGL((k_st3l<KIND, MODE, EPI, 1, false, NW>), dim3(grid), dim3(64 * NW), 0, s, A);
+}
+
+template <int KIND, int MODE, int EPI, int NW>
+void go_st3y(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
+    constexpr bool kF0R = MODE == MODE_JFD && KIND == NK_HEAT3D_EULER;
+    if constexpr (kF0R) {
+        if (A.f0r) {
+            if (per) {
+                if (vec == 2) hipLaunchKernelGGL((k_st3y<KIND, MODE, EPI, 2, true, NW, true>), dim3(grid), dim3(64 * NW), 0, s, A);
+                else hipLaunchKernelGGL((k_st3y<KIND, MODE, EPI, 1, true, NW, true>), dim3(grid), dim3(64 * NW), 0, s, A);
+                return;
+            }
+            if (vec == 2) hipLaunchKernelGGL((k_st3y<KIND, MODE, EPI, 2, false, NW, true>), dim3(grid), dim3(64 * NW), 0, s, A);
+            else hipLaunchKernelGGL((k_st3y<KIND, MODE, EPI, 1, false, NW, true>), dim3(grid), dim3(64 * NW), 0, s, A);
+            return;
+        }
+    }
+    if (per) {
+        if (vec == 2) hipLaunchKernelGGL((k_st3y<KIND, MODE, EPI, 2, true, NW>), dim3(grid), dim3(64 * NW), 0, s, A);
+        else hipLaunchKernelGGL((k_st3y<KIND, MODE, EPI, 1, true, NW>), dim3(grid), dim3(64 * NW), 0, s, A);
+        return;
+    }
+    if (vec == 2) hipLaunchKernelGGL((k_st3y<KIND, MODE, EPI, 2, false, NW>), dim3(grid), dim3(64 * NW), 0, s, A);
+    else hipLaunchKernelGGL((k_st3y<KIND, MODE, EPI, 1, false, NW>), dim3(grid), dim3(64 * NW), 0, s, A);
 }
 
 template <int KIND, int MODE, int EPI, int NW>
@@ -1387,6 +1642,11 @@ void go_stencil(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
         // k_st3d: 4-row tiles, every wave loads its y-neighbour rows (8- and 16-row tiles measured 2-9 %
         // slower, profiles/r01/kbench_stencil3d.log); k_st3l: y-neighbours through LDS, 4- or 8-row tiles
 #ifdef NK_KBENCH
+        if (A.ym) {  // the y-march (kernel-variant build: NK_ST3_YMARCH)
+            if (A.nw == 8) go_st3y<KIND, MODE, EPI, 8>(A, vec, grid, s, per);
+            else go_st3y<KIND, MODE, EPI, 4>(A, vec, grid, s, per);
+            return;
+        }
         if (!A.lds3) go_st3d<KIND, MODE, EPI, 4>(A, vec, grid, s, per);
         else if (A.nw == 8) go_st3l<KIND, MODE, EPI, 8>(A, vec, grid, s, per);
         else
