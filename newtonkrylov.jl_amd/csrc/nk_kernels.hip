@@ -480,7 +480,8 @@ __global__ __launch_bounds__(kBlock) void k_jdiag(KArgs A, double* __restrict__ 
         if (DIM >= 2) lsum = lsum + lapk(A, c, 0.0, 0.0, A.hy2, A.ihy2);
         if (DIM == 3) lsum = lsum + lapk(A, c, 0.0, 0.0, A.hz2, A.ihz2);
         const double uc = (KIND == NK_BRATU1D || KIND == NK_BRATU2D) ? A.u[i] : 0.0;
-        const double d = point_value<KIND, MODE_JEXACT>(A, c, lsum, uc, 0.0, 0.0, 1.0, 0.0, &NKX_T[0][0]);
+        bool rare_ = false;
+        const double d = point_value<KIND, MODE_JEXACT>(A, c, lsum, uc, 0.0, 0.0, 1.0, 0.0, &NKX_T[0][0], rare_);
         out[i] = recip ? 1.0 / d : d;
     }
 }

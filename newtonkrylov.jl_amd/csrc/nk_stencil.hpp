@@ -162,9 +162,11 @@ constexpr bool kind_bratu(int k) { return k == NK_BRATU1D || k == NK_BRATU2D; }
 //   Midpoint   (u_n + Δt du(α u_n + (1-α) w)) - w        tangent  Δt (a lap((1-α) v)) - v
 //   Trapezoid  (u_n + (Δt/2) (du(u_n) + du(w))) - w      tangent  (Δt/2) (a lap(v)) - v
 // et: the exp table (nk_exp.h's NKX_T) in LDS for the Bratu kinds (NK_EXP_LDS), unused otherwise.
-template <int KIND, int MODE>
+// XM = 1: the exp's fast phase only -- a lane it does not settle sets `rare` (its value is then not the
+// correctly rounded one, and the caller recomputes: k_st2d's two-pass march); XM = 0: nk_exp_t itself.
+template <int KIND, int MODE, int XM = 0>
 __device__ __forceinline__ double point_value(const KArgs& A, double c, double lsum, double uc, double unc, double f0c,
-                                              double xc, double lsumg, const double* et) {
+                                              double xc, double lsumg, const double* et, bool& rare) {
     if constexpr (KIND == NK_BRATU1D || KIND == NK_BRATU2D) {
 #ifdef NK_KBENCH
         if (A.fast & (1 << 20)) {  // kbench A/B only: the platform (ocml) exp, <= 1 ulp off the correctly rounded one
@@ -173,8 +175,17 @@ __device__ __forceinline__ double point_value(const KArgs& A, double c, double l
             return MODE == MODE_JFD ? fdq(A, r, f0c) : r;
         }
 #endif
-        if (MODE == MODE_JEXACT) return lsum + A.lam * (nk_exp_t(uc, et) * c);  // Enzyme tangent of λ exp(u)
-        const double r = lsum + A.lam * nk_exp_t(c, et);
+        auto ex = [&](double x) {
+            if constexpr (XM == 1) {
+                double y;
+                if (!nkx_exp_fast(x, et, &y)) rare = true;
+                return y;
+            } else {
+                return nk_exp_t(x, et);
+            }
+        };
+        if (MODE == MODE_JEXACT) return lsum + A.lam * (ex(uc) * c);  // Enzyme tangent of λ exp(u)
+        const double r = lsum + A.lam * ex(c);
         return MODE == MODE_JFD ? fdq(A, r, f0c) : r;
     } else {  // implicit.jl:8-37
         constexpr int SCH = scheme_of<KIND>();
@@ -210,7 +221,8 @@ __global__ __launch_bounds__(kBlock) void k_st1d(KArgs A0) {
         const double c = fieldval<MODE>(A, i), l = fieldval<MODE>(A, i - 1), r = fieldval<MODE>(A, i + 1);
         const double uc = (MODE == MODE_JEXACT) ? A.u[i] : 0.0;
         const double f0 = (MODE == MODE_JFD) ? A.F0[i] : 0.0;
-        double val = point_value<NK_BRATU1D, MODE>(A, c, lap(c, r, l, A.hx2), uc, 0.0, f0, c, 0.0, et);
+        bool rare_ = false;
+        double val = point_value<NK_BRATU1D, MODE>(A, c, lap(c, r, l, A.hx2), uc, 0.0, f0, c, 0.0, et, rare_);
         const double ax = (EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID) ? A.aux[i]
                           : (EPI == EPI_DOTVS ? A.v[i] / A.hd : 0.0);
         acc = epilogue<EPI>(val, ax, acc);
@@ -646,6 +658,14 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
     auto as_res = [](const RawRow<MODE, VEC>& r) { return as_res_row<MODE, VEC>(r); };
     constexpr bool vout = MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS);  // fused kdivcopy!: V_k stored
     double acc = 0.0;
+    // The march as a lambda over XM: the Bratu kinds run it first with the exp's fast phase alone (XM = 1,
+    // no exact phase in the loop: its scalar registers would otherwise spill the loop's invariants); a
+    // wave any of whose lanes the rounding test did not settle (about one wave-tile in 60) runs its tile
+    // again with the full exp (XM = 0), overwriting the same outputs and its partial sum -- so every
+    // stored value and partial is the one a single exact pass computes.
+    auto march = [&](auto xm_) -> bool {
+    constexpr int XM = decltype(xm_)::value;
+    bool rare = false;
     if (y0 < ny) {
         // rows y0-1 (ghost plane when y0 = 0) and y0 cooked up front; row y0+1 raw in flight
         const RawRow<MODE, VEC> rm0 =
@@ -723,9 +743,9 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
                         const double ue = (k == VEC - 1) ? un_.r : uc_.c[k == VEC - 1 ? k : k + 1];
                         const double ucc = uc_.c[k];
                         const double lsu = lapk(A, ucc, ue, uw, A.hx2, A.ihx2) + lapk(A, ucc, up.c[k], um.c[k], A.hy2, A.ihy2);
-                        f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unk, 0.0, SCH == 1 ? uc_.x[k] : ucc, lsumg, et);
+                        f0 = point_value<KIND, MODE_RES, XM>(A, ucc, lsu, 0.0, unk, 0.0, SCH == 1 ? uc_.x[k] : ucc, lsumg, et, rare);
                     }
-                    double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unk, f0, SCH == 1 ? fc.x[k] : c, lsumg, et);
+                    double r = point_value<KIND, MODE, XM>(A, c, lsum, uc.v[k], unk, f0, SCH == 1 ? fc.x[k] : c, lsumg, et, rare);
                     acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[k] : ax.v[k], acc);
                     val.v[k] = r;
                 }
@@ -750,6 +770,16 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
             ax = axn;
         }
     }
+    return rare;
+    };
+    if constexpr (kind_bratu(KIND)) {
+        if (__ballot(march(std::integral_constant<int, 1>{}))) {  // wave-uniform
+            acc = 0.0;
+            (void)march(std::integral_constant<int, 0>{});
+        }
+    } else {
+        (void)march(std::integral_constant<int, 0>{});
+    }
     if constexpr (EPI != EPI_NONE) publish(acc, A.part, A.fin, sh, t);
 }
 
@@ -763,6 +793,7 @@ template <int KIND, int MODE, int EPI, int VEC, bool PER = false, bool F0R = fal
 __global__ __launch_bounds__(64 * NW) void k_st2t(KArgs A0) {
     __shared__ double sh[kShN];
     NK_EXP_LDS(KIND)
+    bool rare_ = false;
     KArgs A = A0;
     A.hd = A.vdiv ? *A.vdiv : 1.0;
     constexpr int SCH = scheme_of<KIND>();
@@ -883,9 +914,9 @@ __global__ __launch_bounds__(64 * NW) void k_st2t(KArgs A0) {
                 const double ucc = uc_.c[k];
                 const double lsu = lapk(A, ucc, ue, uw, A.hx2, A.ihx2) +
                                    lapk(A, ucc, lu[kR ? wv + 2 : 0][kR ? q : 0], lu[kR ? wv : 0][kR ? q : 0], A.hy2, A.ihy2);
-                f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unk, 0.0, SCH == 1 ? uc_.x[k] : ucc, lsumg, et);
+                f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unk, 0.0, SCH == 1 ? uc_.x[k] : ucc, lsumg, et, rare_);
             }
-            double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unk, f0, SCH == 1 ? fc.x[k] : c, lsumg, et);
+            double r = point_value<KIND, MODE>(A, c, lsum, uc.v[k], unk, f0, SCH == 1 ? fc.x[k] : c, lsumg, et, rare_);
             acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[k] : ax.v[k], acc);
             val.v[k] = r;
         }
@@ -920,6 +951,7 @@ template <int KIND, int MODE, int EPI, int VEC, bool PER = false, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
     __shared__ double sh[kShN];
     const double* const et = nullptr;  // heat kinds: no exp
+    bool rare_ = false;
     KArgs A = A0;
     A.hd = A.vdiv ? *A.vdiv : 1.0;
     constexpr int SCH = scheme_of<KIND>();
@@ -1015,7 +1047,7 @@ __global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
                                 lapk(A, g, fp.g[q], fm.g[q], A.hz2, A.ihz2);
                     }
                     const double unq = kG ? fc.g[q] : unc.v[q];
-                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0c.v[q], SCH == 1 ? fc.x[q] : c, lsumg, et);
+                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0c.v[q], SCH == 1 ? fc.x[q] : c, lsumg, et, rare_);
                     acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[q] : ax.v[q], acc);
                     val.v[q] = r;
                 }
@@ -1053,6 +1085,7 @@ template <int KIND, int MODE, int EPI, int VEC, bool PER = false, int NW = 8, bo
 __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
     __shared__ double sh[kShN];
     const double* const et = nullptr;  // heat kinds: no exp
+    bool rare_ = false;
     KArgs A = A0;
     A.hd = A.vdiv ? *A.vdiv : 1.0;
     constexpr int SCH = scheme_of<KIND>();
@@ -1248,9 +1281,9 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
                         const double ucc = uc_.c[q];
                         const double lsu = (lapk(A, ucc, ue, uw, A.hx2, A.ihx2) + lapk(A, ucc, cnu[q], csu[q], A.hy2, A.ihy2)) +
                                            lapk(A, ucc, dn ? um.c[q] : up.c[q], dn ? up.c[q] : um.c[q], A.hz2, A.ihz2);
-                        f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unq, 0.0, SCH == 1 ? uc_.x[q] : ucc, lsumg, et);
+                        f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unq, 0.0, SCH == 1 ? uc_.x[q] : ucc, lsumg, et, rare_);
                     }
-                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0, SCH == 1 ? fc.x[q] : c, lsumg, et);
+                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0, SCH == 1 ? fc.x[q] : c, lsumg, et, rare_);
                     acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[q] : ax.v[q], acc);
                     val.v[q] = r;
                 }
@@ -1293,6 +1326,7 @@ template <int KIND, int MODE, int EPI, int VEC, bool PER = false, int NW = 4, bo
 __global__ __launch_bounds__(64 * NW) void k_st3y(KArgs A0) {
     __shared__ double sh[kShN];
     const double* const et = nullptr;  // heat kinds: no exp
+    bool rare_ = false;
     KArgs A = A0;
     A.hd = A.vdiv ? *A.vdiv : 1.0;
     constexpr int SCH = scheme_of<KIND>();
@@ -1478,9 +1512,9 @@ __global__ __launch_bounds__(64 * NW) void k_st3y(KArgs A0) {
                         const double ucc = uc_.c[q];
                         const double lsu = (lapk(A, ucc, ue, uw, A.hx2, A.ihx2) + lapk(A, ucc, up.c[q], um.c[q], A.hy2, A.ihy2)) +
                                            lapk(A, ucc, cuu[q], cdu[q], A.hz2, A.ihz2);
-                        f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unq, 0.0, SCH == 1 ? uc_.x[q] : ucc, lsumg, et);
+                        f0 = point_value<KIND, MODE_RES>(A, ucc, lsu, 0.0, unq, 0.0, SCH == 1 ? uc_.x[q] : ucc, lsumg, et, rare_);
                     }
-                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0, SCH == 1 ? fc.x[q] : c, lsumg, et);
+                    double r = point_value<KIND, MODE>(A, c, lsum, 0.0, unq, f0, SCH == 1 ? fc.x[q] : c, lsumg, et, rare_);
                     acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[q] : ax.v[q], acc);
                     val.v[q] = r;
                 }
