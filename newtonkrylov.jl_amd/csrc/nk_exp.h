@@ -10,7 +10,7 @@
  * wherever Base.exp rounds correctly, e.g. exp(2.0) == 7.38905609893065 of test/runtests.jl:38).
  *
  * Algorithm (Ziv's strategy, two phases):
- *   fast  x = k ln2/128 + r, |r| <= ln2/256 (Cody-Waite, ln2/128 in three parts, r as a
+ *   fast  x = k ln2/128 + r, |r| <= 1.125 ln2/256 (Cody-Waite, ln2/128 in three parts, r as a
  *         double-double); expm1(r) = r + r^2/2 + r^3 P(r) with r^2 exact (fma) and the
  *         cubic tail in doubles; 2^(j/128) from a 128-entry double-double table; the result
  *         zh + zl carries a relative error below 2^-76 (bound in DESIGN.md; measured max
@@ -40,16 +40,17 @@
 typedef unsigned long long nkx_u64;
 typedef unsigned __int128 nkx_u128;
 
-#define NKX_INVLN2N 0x1.71547652b82fep+7
-#define NKX_L2N_H 0x1.62e42fef00000p-8
-#define NKX_L2N_M 0x1.473de6af278edp-41
-#define NKX_L2N_L -0x1.9ff0342542fc3p-97
-/* Taylor coefficients of the cubic tail r^3 (1/6 + r/24 + r^2/120 + r^3/720 + r^4/5040) */
+#define NKX_INVLN2N 0x1.7154700000000p+7
+#define NKX_L2N_H 0x1.62e4200000000p-8
+#define NKX_L2N_M 0x1.fdf473de6af28p-29
+#define NKX_L2N_L -0x1.c4c67fc0d0951p-83
+/* Taylor coefficients of the cubic tail r^3 (1/6 + r/24 + r^2/120 + r^3/720 + r^4/5040); 1/720 and 1/5040
+   to 21 bits, like INVLN2N and L2N_H (gfx950 takes such doubles as 32-bit literals: fewer scalar registers) */
 #define NKX_C3 0x1.5555555555555p-3
 #define NKX_C4 0x1.5555555555555p-5
 #define NKX_C5 0x1.1111111111111p-7
-#define NKX_C6 0x1.6c16c16c16c17p-10
-#define NKX_C7 0x1.a01a01a01a01ap-13
+#define NKX_C6 0x1.6c16c00000000p-10
+#define NKX_C7 0x1.a01a000000000p-13
 #define NKX_INVLN2 0x1.71547652b82fep+0
 
 /* 2^(j/128) = hi + lo */
@@ -377,7 +378,7 @@ NKX_SLOW_FN double nkx_exp_slow(double x) {
 NKX_FN double nkx_exp_dd(double x, const double* tab, double* zl_out, int* m_out) {
     const double kd = rint(x * NKX_INVLN2N);
     const int k = (int)kd;
-    const double rh = fma(-kd, NKX_L2N_H, x); /* exact: kd * H has <= 51 bits, Sterbenz */
+    const double rh = fma(kd, -NKX_L2N_H, x); /* exact: kd * H has <= 39 bits, Sterbenz */
     const double ph = kd * NKX_L2N_M;
     const double pl = fma(kd, NKX_L2N_M, -ph);
     const double r1 = rh - ph; /* TwoSum(rh, -ph) */

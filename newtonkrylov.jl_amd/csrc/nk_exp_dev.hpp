@@ -35,5 +35,13 @@ __device__ __forceinline__ double nk_exp_t(double x, const double* tab) {
     return y;
 }
 
+// correctly rounded exp(x) per lane: the exact phase runs divergently (vector registers) in the lanes
+// that need it -- for code where little else is live (k_st2d's fixup of the points its march marked)
+__device__ __forceinline__ double nk_exp_lane(double x, const double* tab) {
+    double y;
+    if (nkx_exp_fast(x, tab, &y)) return y;
+    return nkx_exp_rare(x);
+}
+
 // correctly rounded exp(x), table from device memory
 __device__ __forceinline__ double nk_exp(double x) { return nk_exp_t(x, &NKX_T[0][0]); }

@@ -56,7 +56,9 @@ def test_constants_match_generator():
     """Every constant in nk_exp.h is what tools/gen_exp_consts.py derives with mpmath."""
     src = open(HDR).read()
     h, m, l = gen.ln2n_split()
-    for name, v in (("NKX_INVLN2N", gen.invln2n()), ("NKX_L2N_H", h), ("NKX_L2N_M", m), ("NKX_L2N_L", l)):
+    c3, c4, c5, c6, c7 = gen.coeffs()
+    for name, v in (("NKX_INVLN2N", gen.invln2n()), ("NKX_L2N_H", h), ("NKX_L2N_M", m), ("NKX_L2N_L", l),
+                    ("NKX_C3", c3), ("NKX_C4", c4), ("NKX_C5", c5), ("NKX_C6", c6), ("NKX_C7", c7)):
         got = re.search(rf"#define {name} (\S+)", src).group(1)
         assert float.fromhex(got) == v, name
     tab = re.findall(r"\{(-?0x[0-9a-fp.+-]+), (-?0x[0-9a-fp.+-]+)\},\s+/\* (\d+) \*/", src)

@@ -4,8 +4,11 @@ Prints C initialisers (hex-float doubles and 64-bit limbs); nk_exp.h holds their
 tests/test_exp.py re-derives every constant from this script's functions and compares.
 
   NKX_T[j] = (hi, lo)  2^(j/128) = hi + lo to ~107 bits, j = 0..127 (the fast path's table)
-  L2N_H/M/L            ln2/128 = H + M + L, H with 33 significant bits (kd * H exact for |kd| < 2^20)
-  INVLN2N              128/ln2 rounded
+  L2N_H/M/L            ln2/128 = H + M + L, H with 21 significant bits (kd * H exact for |kd| < 2^32; a
+                       double whose low 32 bits are zero, which gfx950's VOP2 fmac takes as a literal)
+  INVLN2N              128/ln2 to 21 significant bits (k may then be off the nearest integer by one only
+                       near a half: |r| <= 1.125 ln2/256, inside the fast phase's error analysis)
+  C6, C7               1/720, 1/5040 to 21 significant bits (their terms are below 2^-60 and 2^-72)
   LN2_FX               round(ln2 * 2^190) as three 64-bit limbs (the slow path's fixed point, Q2.190)
   INVFACT_FX[i]        round(2^190 / i!), i = 0..17
 """
@@ -33,7 +36,7 @@ def table():
 def ln2n_split():
     c = mpmath.log(2) / N
     m, e = mpmath.frexp(c)  # c = m 2^e, 0.5 <= m < 1
-    hi = mpmath.ldexp(mpmath.floor(mpmath.ldexp(m, 33)), e - 33)  # 33 significant bits
+    hi = mpmath.ldexp(mpmath.floor(mpmath.ldexp(m, 21)), e - 21)  # 21 significant bits
     h = float(hi)
     assert mpmath.mpf(h) == hi
     mid = dbl(c - hi)
@@ -41,8 +44,20 @@ def ln2n_split():
     return h, mid, low
 
 
+def short21(v):
+    """v rounded to 21 significant bits (the high 32-bit word of a double, the low word zero)"""
+    m, e = mpmath.frexp(mpmath.mpf(v))
+    return float(mpmath.ldexp(mpmath.nint(mpmath.ldexp(m, 21)), e - 21))
+
+
 def invln2n():
-    return dbl(N / mpmath.log(2))
+    return short21(N / mpmath.log(2))
+
+
+def coeffs():
+    """C3 .. C7 of the cubic tail r^3 (C3 + r (C4 + r (C5 + r (C6 + r C7))))"""
+    return [dbl(1 / mpmath.factorial(3)), dbl(1 / mpmath.factorial(4)), dbl(1 / mpmath.factorial(5)),
+            short21(1 / mpmath.factorial(6)), short21(1 / mpmath.factorial(7))]
 
 
 def fx(v):
@@ -64,6 +79,8 @@ def invfact_fx():
 def main():
     h, m, l = ln2n_split()
     print(f"#define NKX_INVLN2N {invln2n().hex()}")
+    for i, c in enumerate(coeffs()):
+        print(f"#define NKX_C{i + 3} {c.hex()}")
     print(f"#define NKX_L2N_H {h.hex()}\n#define NKX_L2N_M {m.hex()}\n#define NKX_L2N_L {l.hex()}")
     print("/* 2^(j/128) = hi + lo */")
     for j, (a, b) in enumerate(table()):
