@@ -590,15 +590,39 @@ __device__ __forceinline__ void tile3_of(int b, int nb, int tiles_x, int tiles_y
     txy = (col % tiles_y) * tiles_x + col / tiles_y;
 }
 
-// west / east neighbours of the VEC points of a lane: lane shuffles, the wave-edge lanes' edge values
+// one-lane shifts across the whole wave as DPP moves (gfx9's wave_shr:1 / wave_shl:1): a VALU op per
+// 32-bit half, where __shfl_up / __shfl_down go through the LDS crossbar (ds_bpermute) and an lgkmcnt
+// wait.  The lane with no source (0 resp. 63) keeps 0; x_nbrs overrides it with its edge value.
+__device__ __forceinline__ double wave_shr1(double x) {  // lane i <- lane i - 1
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x138, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_shl1(double x) {  // lane i <- lane i + 1
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x130, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x130, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+
+// west / east neighbours of the VEC points of a lane: lane shifts, the wave-edge lanes' edge values
 struct LR {
     double l, r;
 };
 template <bool PER>
-__device__ __forceinline__ LR x_nbrs(double cfirst, double clast, double e, double e2, int lane, bool rwrap) {
+__device__ __forceinline__ LR x_nbrs(const KArgs& A, double cfirst, double clast, double e, double e2, int lane,
+                                     bool rwrap) {
     LR o;
-    o.l = __shfl_up(clast, 1, 64);
-    o.r = __shfl_down(cfirst, 1, 64);
+#ifdef NK_KBENCH
+    if (A.fast & (1 << 21)) {  // kbench A/B only: the LDS-crossbar shuffles
+        o.l = __shfl_up(clast, 1, 64);
+        o.r = __shfl_down(cfirst, 1, 64);
+    } else
+#endif
+    {
+        (void)A;
+        o.l = wave_shr1(clast);
+        o.r = wave_shl1(cfirst);
+    }
     if (lane == 0) o.l = e;
     if constexpr (PER) {
         if (lane == 63 || rwrap) o.r = e2;
@@ -711,14 +735,14 @@ __global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
             LR un_{};
             if constexpr (kR) {
                 up = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res(rp), act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
-                un_ = x_nbrs<PER>(uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
+                un_ = x_nbrs<PER>(A, uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
             }
             // ---- compute row j from registers
-            const LR xn = x_nbrs<PER>(fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
+            const LR xn = x_nbrs<PER>(A, fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
             const double lft = xn.l, rgt = xn.r;
             double glft = 0.0, grgt = 0.0;
             if constexpr (SCH == 2 && kG) {
-                const LR gn = x_nbrs<PER>(fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
+                const LR gn = x_nbrs<PER>(A, fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
                 glft = gn.l;
                 grgt = gn.r;
             }
@@ -887,10 +911,10 @@ __global__ __launch_bounds__(64 * NW) void k_st2t(KArgs A0) {
     __syncthreads();
     double acc = 0.0;
     if (comp && act) {
-        const LR xn = x_nbrs<PER>(fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
+        const LR xn = x_nbrs<PER>(A, fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
         LR gn{}, un_{};
-        if constexpr (kTG) gn = x_nbrs<PER>(fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
-        if constexpr (kR) un_ = x_nbrs<PER>(uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
+        if constexpr (kTG) gn = x_nbrs<PER>(A, fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
+        if constexpr (kR) un_ = x_nbrs<PER>(A, uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
         Row<VEC> val;
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
@@ -1021,11 +1045,11 @@ __global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
             const Field<VEC> fn = cook<MODE, VEC, SCH, kG, PER>(A, rn, has_n, false);
             const Field<VEC> fs = cook<MODE, VEC, SCH, kG, PER>(A, rs, has_s, false);
             // ---- compute plane k
-            const LR xn = x_nbrs<PER>(fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
+            const LR xn = x_nbrs<PER>(A, fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
             const double lft = xn.l, rgt = xn.r;
             double glft = 0.0, grgt = 0.0;
             if constexpr (SCH == 2 && kG) {
-                const LR gn = x_nbrs<PER>(fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
+                const LR gn = x_nbrs<PER>(A, fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
                 glft = gn.l;
                 grgt = gn.r;
             }
@@ -1245,14 +1269,14 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
                     if (!has_n) cnu[q] = 0.0;
                     if (!has_s) csu[q] = 0.0;
                 }
-                xu = x_nbrs<PER>(uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
+                xu = x_nbrs<PER>(A, uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
             }
             // ---- compute plane k
-            const LR xn = x_nbrs<PER>(fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
+            const LR xn = x_nbrs<PER>(A, fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
             const double lft = xn.l, rgt = xn.r;
             double glft = 0.0, grgt = 0.0;
             if constexpr (SCH == 2 && kG) {
-                const LR g2 = x_nbrs<PER>(fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
+                const LR g2 = x_nbrs<PER>(A, fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
                 glft = g2.l;
                 grgt = g2.r;
             }
@@ -1476,14 +1500,14 @@ __global__ __launch_bounds__(64 * NW) void k_st3y(KArgs A0) {
                     cuu[q] = lds_u ? lzu[par][kR ? wv + (lds_u ? 1 : 0) : 0][kR ? lane * VEC + q : 0] : fuu.c[q];
                     cdu[q] = lds_d ? lzu[par][kR ? wv - (lds_d ? 1 : 0) : 0][kR ? lane * VEC + q : 0] : fdu.c[q];
                 }
-                xu = x_nbrs<PER>(uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
+                xu = x_nbrs<PER>(A, uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
             }
             // ---- compute row j of my plane
-            const LR xn = x_nbrs<PER>(fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
+            const LR xn = x_nbrs<PER>(A, fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
             const double lft = xn.l, rgt = xn.r;
             double glft = 0.0, grgt = 0.0;
             if constexpr (SCH == 2 && kG) {
-                const LR g2 = x_nbrs<PER>(fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
+                const LR g2 = x_nbrs<PER>(A, fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
                 glft = g2.l;
                 grgt = g2.r;
             }
