@@ -595,6 +595,8 @@ def main():
         if not v or v["ms"] <= 0:
             return None
         ach = v["bytes"] / (v["ms"] * 1e-3) / 1e9
+        if ach <= 0:
+            return None
         tb = traffic(name)
         # mean algorithmic bytes over ALL launches (a sweep's size varies with the Arnoldi step; the
         # timed launches are every 64th one).  PMC traffic comes from a separate run with the same
@@ -618,7 +620,9 @@ def main():
                 "bytes_per_launch": bpl, "avg_us": round(1e6 * bpl / (ach * 1e9), 3),
                 "avg_us_timed": 1e3 * v["ms"] / v["timed"], "timed_launches": v["timed"]}
 
-    dominant = next(iter(kernels), None)
+    # the kernel with the largest share of the time among those that move operand bytes (with ranks sharing
+    # one GPU, the one-block cross-rank waits -- k_finalize, no bytes -- can carry the largest share)
+    dominant = next((k for k, v in kernels.items() if v["gbs"]), None)
     # the Jv of the Arnoldi steps: fused with V_k = q / h (jv_*_dot_norm), or reading V_k as stored
     # by the previous resident sweep (jv_*_dot) -- whichever carries more of the time
     jv_kernel = max((W.jv_kernel, W.jv_kernel.replace("_dot_norm", "_dot")),

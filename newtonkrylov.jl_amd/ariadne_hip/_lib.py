@@ -16,6 +16,9 @@ PRODUCT_LIB = os.path.join(PKG_DIR, "lib", "libnkhip.so")
 # NK_KBENCH_LIB=1 loads it instead -- tools/ and the variant-equivalence tests only
 KBENCH_LIB = os.path.join(PKG_DIR, "lib", "libnkhip_kbench.so")
 LIB_PATH = KBENCH_LIB if os.environ.get("NK_KBENCH_LIB") == "1" else PRODUCT_LIB
+# A/B tools only: a product build with extra defines (`make variant TAG=...` -> lib/libnkhip_v_TAG.so)
+if os.environ.get("NK_LIB_VARIANT"):
+    LIB_PATH = os.path.join(PKG_DIR, "lib", f"libnkhip_v_{os.environ['NK_LIB_VARIANT']}.so")
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "nkhip.h")
 
 NK_OK = 0

@@ -142,6 +142,12 @@ __device__ __forceinline__ void storevec(double* __restrict__ p, int64_t o, cons
 }
 
 constexpr bool kind_bratu(int k) { return k == NK_BRATU1D || k == NK_BRATU2D; }
+// waves per SIMD the Bratu k_st2d kernels are register-allocated for (unconstrained, the exp's double-double
+// fast phase takes them to 97-109 VGPRs: 4 waves).  5: FD Jv + dot 177 us, 4: 182 us, 6 (80 VGPRs, spills):
+// 198 us (profiles/r04/ab_lib_wpe.log)
+#ifndef NK_ST2D_BRATU_WPE
+#define NK_ST2D_BRATU_WPE 5
+#endif
 
 // The exp table (NKX_T: 128 double-double entries, 2 KB) copied into LDS once per block for the Bratu
 // kinds, where every point evaluates exp: read with ds_read, its lookups never wait behind the rows the
@@ -176,6 +182,13 @@ __device__ __forceinline__ double point_value(const KArgs& A, double c, double l
         }
 #endif
         auto ex = [&](double x) {
+#ifdef NK_KBENCH
+            if (A.fast & (1 << 22)) {  // kbench diagnosis only: the fast phase's value, no rounding test acted on
+                double y;
+                (void)nkx_exp_fast(x, et, &y);
+                return y;
+            }
+#endif
             if constexpr (XM == 1) {
                 double y;
                 if (!nkx_exp_fast(x, et, &y)) rare = true;
@@ -640,7 +653,8 @@ __device__ __forceinline__ LR x_nbrs(const KArgs& A, double cfirst, double clast
 // point_value), so (F(w) - F(u)) / eps is bit-identical to loading the F0 that kernel stored, and
 // 8 B/pt less is read.  Valid only when F0 IS that residual of this u (the Newton loop's res).
 template <int KIND, int MODE, int EPI, int VEC, bool PER = false, bool F0R = false>
-__global__ __launch_bounds__(kBlock) void k_st2d(KArgs A0) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kind_bratu(KIND) ? NK_ST2D_BRATU_WPE : 1)))
+void k_st2d(KArgs A0) {
     __shared__ double sh[kShN];
     NK_EXP_LDS(KIND)
     KArgs A = A0;

@@ -115,9 +115,12 @@ def test_config4_slab_gmres_first_steps(ctx):
     x = ws.x.to_numpy()
     xo, sto, ho = oc.krylov_solve(P, ui, F0d, jv="fd", F0=F0d, memory=30, **kw)
     assert ws.stats.niter == sto["niter"] == 12
-    # the operator is bit-identical: only the summation order of the reductions differs
+    # the operator is bit-identical: only the summation order of the reductions differs.  The residual
+    # histories follow it to 1e-11; x, to the FD operator's own noise: a one-ulp change in a basis vector
+    # moves F(u + eps v)'s roundings, |F| / |Jv| ~ 1e3 here, so Jv moves by ~1e-16 |F| / eps ~ 1e-9 |Jv|,
+    # and x, made of the V_k, follows (measured 9.9e-9 relative on the GPU, r04)
     assert np.allclose(np.array(ws.stats.residuals), ho, rtol=1e-11)
-    assert np.max(np.abs(x - xo)) <= 1e-11 * np.max(np.abs(xo))
+    assert np.max(np.abs(x - xo)) <= 5e-8 * np.max(np.abs(xo))
     ws.free()
 
 

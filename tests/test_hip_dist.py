@@ -179,9 +179,21 @@ def check_meta(meta, world):
 
 
 def free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    """A free port BELOW the ephemeral range (Linux: 32768-60999).  A port the kernel hands out for bind(0)
+    comes from the range every outgoing connection draws from -- the previous test's gloo / RCCL mesh
+    sockets included -- and was taken again before rank 0's store could listen on it (EADDRINUSE, r04)."""
+    import random
+
+    rng = random.Random(os.getpid() ^ time.time_ns())
+    for _ in range(200):
+        port = rng.randrange(20000, 32000)
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", port))
+            except OSError:
+                continue
+            return port
+    raise RuntimeError("no free port in 20000-32000")
 
 
 @pytest.mark.parametrize("transport,world", [("mailbox", 2), ("rccl", 2), ("mailbox", 3), ("rccl", 3), ("mailbox", 4),
