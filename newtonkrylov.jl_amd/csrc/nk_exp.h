@@ -33,9 +33,14 @@
  *   NKX_FN       qualifiers of the fast path (device: __device__ __forceinline__; C: static inline)
  *   NKX_SLOW_FN  qualifiers of the rare path (device: __device__ __attribute__((noinline)))
  *   NKX_CONST    storage qualifier of the tables (device: static __device__ const; C: static const)
+ *   NKX_NOUNROLL (optional) a loop pragma for the exact phase's two long loops (device: unroll 1)
  */
 #ifndef NK_EXP_H
 #define NK_EXP_H
+
+#ifndef NKX_NOUNROLL
+#define NKX_NOUNROLL
+#endif
 
 typedef unsigned long long nkx_u64;
 typedef unsigned __int128 nkx_u128;
@@ -336,6 +341,7 @@ NKX_SLOW_FN double nkx_exp_slow(double x) {
     rr[2] = (R[2] >> 8) | (R[3] << 56);
     /* exp(r') = sum_{i <= 17} r'^i / i!  (Horner) */
     nkx_u64 y[3] = {NKX_INVFACT_FX[17][0], NKX_INVFACT_FX[17][1], NKX_INVFACT_FX[17][2]};
+    NKX_NOUNROLL
     for (int i = 16; i >= 0; --i) {
         nkx_u64 t[3];
         nkx_mul(t, y, rr);
@@ -346,6 +352,7 @@ NKX_SLOW_FN double nkx_exp_slow(double x) {
             c = (nkx_u64)(s2 >> 64);
         }
     }
+    NKX_NOUNROLL
     for (int i = 0; i < 8; ++i) { /* exp(r) = exp(r')^256 */
         nkx_u64 t[3];
         nkx_mul(t, y, y);

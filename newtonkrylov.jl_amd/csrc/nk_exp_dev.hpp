@@ -17,6 +17,7 @@
 #define NKX_SLOW_FN __device__ __forceinline__
 #define NKX_CONST static __device__ const
 #define NKX_OWN_EXP_T 1
+#define NKX_NOUNROLL _Pragma("unroll 1")
 #include "nk_exp.h"
 
 // correctly rounded exp(x); `tab` = NKX_T as 256 doubles (an LDS copy in the stencils)
@@ -39,7 +40,7 @@ __device__ __forceinline__ double nk_exp_t(double x, const double* tab) {
 // that need it -- for code where little else is live (k_st2d's fixup of the points its march marked)
 __device__ __forceinline__ double nk_exp_lane(double x, const double* tab) {
     double y;
-    if (nkx_exp_fast(x, tab, &y)) return y;
+    if (__builtin_expect(nkx_exp_fast(x, tab, &y), 1)) return y;
     return nkx_exp_rare(x);
 }
 

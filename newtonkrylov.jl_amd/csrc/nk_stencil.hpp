@@ -142,11 +142,18 @@ __device__ __forceinline__ void storevec(double* __restrict__ p, int64_t o, cons
 }
 
 constexpr bool kind_bratu(int k) { return k == NK_BRATU1D || k == NK_BRATU2D; }
-// waves per SIMD the Bratu k_st2d kernels are register-allocated for (unconstrained, the exp's double-double
-// fast phase takes them to 97-109 VGPRs: 4 waves).  5: FD Jv + dot 177 us, 4: 182 us, 6 (80 VGPRs, spills):
-// 198 us (profiles/r04/ab_lib_wpe.log)
+// The Bratu k_st2d march evaluates the exp per lane in one pass (XM = 2: the fast phase, and in the rare
+// lanes it does not settle the exact phase, divergently, in vector registers); XM = 1 is round 4's first
+// form: the fast phase alone, and a wave with an unsettled lane re-running its whole tile with the full
+// exp -- about 64 re-runs per 4096^2 launch, and whichever lands in the last round of waves stretches the
+// launch by a whole wave lifetime (FD Jv + dot 176 us against 127 us, profiles/r04/ab_lib_single_pass.log).
+#ifndef NK_ST2D_BRATU_XM
+#define NK_ST2D_BRATU_XM 2
+#endif
+// Waves per SIMD the Bratu k_st2d kernels are register-allocated for: 4 (<= 128 VGPRs; the cold exact
+// phase's registers stay off the hot path).  5 forces spills the march pays for: 147 us against 127 us.
 #ifndef NK_ST2D_BRATU_WPE
-#define NK_ST2D_BRATU_WPE 5
+#define NK_ST2D_BRATU_WPE 4
 #endif
 
 // The exp table (NKX_T: 128 double-double entries, 2 KB) copied into LDS once per block for the Bratu
@@ -193,6 +200,8 @@ __device__ __forceinline__ double point_value(const KArgs& A, double c, double l
                 double y;
                 if (!nkx_exp_fast(x, et, &y)) rare = true;
                 return y;
+            } else if constexpr (XM == 2) {
+                return nk_exp_lane(x, et);
             } else {
                 return nk_exp_t(x, et);
             }
@@ -811,10 +820,14 @@ void k_st2d(KArgs A0) {
     return rare;
     };
     if constexpr (kind_bratu(KIND)) {
+#if NK_ST2D_BRATU_XM == 2
+        (void)march(std::integral_constant<int, 2>{});
+#else
         if (__ballot(march(std::integral_constant<int, 1>{}))) {  // wave-uniform
             acc = 0.0;
             (void)march(std::integral_constant<int, 0>{});
         }
+#endif
     } else {
         (void)march(std::integral_constant<int, 0>{});
     }
