@@ -2,12 +2,13 @@
 // the same source the CPU oracle compiles, so every Bratu residual / JVP / FD value is bit-identical
 // to the oracle's (bratu.jl:21's lam * exp(u)).
 //
-// Device form: every lane runs the branch-free fast phase (nkx_exp_fast, table in LDS for the
-// stencils).  The lanes it does not settle -- about 2^-18 of inputs, plus non-finite / out-of-range
-// ones -- are taken ONE AT A TIME by the whole wave: the lane's x is read into scalar registers
-// (readlane) and nkx_exp_rare runs on wave-uniform values, i.e. as scalar (SALU) code.  No call and
-// no per-lane divergent copy of the 192-bit fixed-point phase: the stencils' VGPR count is the fast
-// phase's alone (a called rare path cost them 24 VGPRs, a per-lane inlined one as many).
+// Device forms: every lane runs the branch-free fast phase (nkx_exp_fast; the stencils pass the table
+// as an LDS copy).  The lanes it does not settle -- about 2^-18 of inputs, plus non-finite / out-of-range
+// ones -- take the exact phase either
+//   nk_exp_lane  per lane, divergently, in vector registers: the stencil marches (k_st2d), allocated so
+//                this cold code's registers never displace the hot loop's, or
+//   nk_exp_t     one lane at a time for the whole wave: the lane's x read into scalar registers
+//                (readlane), the exact phase run as wave-uniform scalar code (k_exp, batched JVPs, 1D).
 #pragma once
 #include <hip/hip_runtime.h>
 

@@ -27,6 +27,7 @@ struct KArgs {
     const double* vdiv;
     double* vout;
     double hd;           // *vdiv, loaded once per block
+    double ihd;          // RN(1 / hd), for div_rn
     int fin;             // fold the partials in-kernel (publish)
     double alpha;        // G_Midpoint! α
     int nw;              // 3D: rows (waves) per tile
@@ -73,26 +74,42 @@ constexpr bool heat_kind() {
     return KIND >= NK_HEAT2D_EULER && KIND <= NK_HEAT3D_TRAPEZOID;
 }
 
-__device__ __forceinline__ double vin(const KArgs& A, int64_t o) {
-    const double v = A.v[o];
-    return A.vdiv ? v / A.hd : v;
+// RN(a / b), the IEEE quotient, from yb = RN(1 / b) (computed once: host or kernel prologue): q0 = a yb is
+// within an ulp of a / b, the remainder a - b q0 is exact (fma), and one correction q0 + r yb rounds to
+// RN(a / b) (Markstein's theorem; round to nearest, no under/overflow -- the operands outside
+// 2^-900 <= |a|, |q0| <= 2^1000, zeros included, take the division itself).  3 VALU operations instead of
+// the ~10 of a division; bit-identical (also checked on 2.2e8 quotients by tests/test_div_rn.py).
+__device__ __forceinline__ double div_rn(double a, double b, double yb) {
+    const double q0 = a * yb;
+    const double r = fma(-q0, b, a);
+    const double q1 = fma(r, yb, q0);
+    const double aa = fabs(a), aq = fabs(q0);
+    if (__builtin_expect(aa >= 0x1p-900 && aq >= 0x1p-900 && aq <= 0x1p1000, 1)) return q1;
+    return a / b;
 }
 
-// ((p - 2c) + m) / h^2 exactly as the reference writes it; the kbench build's `fast` variant multiplies
-// by 1/h^2 instead (not bit-faithful; < 2 % faster)
+__device__ __forceinline__ double vin(const KArgs& A, int64_t o) {
+    const double v = A.v[o];
+    return A.vdiv ? div_rn(v, A.hd, A.ihd) : v;
+}
+
+// ((p - 2c) + m) / h^2 exactly as the reference writes it (div_rn: the same double); the kbench build's
+// `fast` variant multiplies by 1/h^2 instead (not bit-faithful)
 __device__ __forceinline__ double lapk(const KArgs& A, double c, double p, double m, double h2, double ih2) {
     const double s = (p - 2.0 * c) + m;
 #ifdef NK_KBENCH
     if (A.fast & 1) return s * ih2;
+    if (A.fast & (1 << 23)) return s / h2;  // A/B: the division instruction sequence
 #endif
-    return s / h2;
+    return div_rn(s, h2, ih2);
 }
 // (r - F0) / eps, the FD quotient (kbench `fast`: times 1/eps)
 __device__ __forceinline__ double fdq(const KArgs& A, double r, double f0c) {
 #ifdef NK_KBENCH
     if (A.fast & 1) return (r - f0c) * A.ieps;
+    if (A.fast & (1 << 23)) return (r - f0c) / A.eps;
 #endif
-    return (r - f0c) / A.eps;
+    return div_rn(r - f0c, A.eps, A.ieps);
 }
 
 template <int MODE>
@@ -142,6 +159,13 @@ __device__ __forceinline__ void storevec(double* __restrict__ p, int64_t o, cons
 }
 
 constexpr bool kind_bratu(int k) { return k == NK_BRATU1D || k == NK_BRATU2D; }
+// A/B only (-DNK_ST_KEEP_VDIV): keep the runtime v / h test in every instantiation (round 3's form, where
+// the instances without the fused normalisation evaluated the division and discarded it)
+#ifdef NK_ST_KEEP_VDIV
+constexpr bool kKeepVdiv = true;
+#else
+constexpr bool kKeepVdiv = false;
+#endif
 // The Bratu k_st2d march evaluates the exp per lane in one pass (XM = 2: the fast phase, and in the rare
 // lanes it does not settle the exact phase, divergently, in vector registers); XM = 1 is round 4's first
 // form: the fast phase alone, and a wave with an unsettled lane re-running its whole tile with the full
@@ -235,7 +259,9 @@ __global__ __launch_bounds__(kBlock) void k_st1d(KArgs A0) {
     __shared__ double sh[kShN];
     NK_EXP_LDS(NK_BRATU1D)
     KArgs A = A0;
+    if constexpr (!kKeepVdiv && EPI != EPI_DOTV && EPI != EPI_DOTVS) A.vdiv = nullptr;  // v / h only with V_k stored
     A.hd = A.vdiv ? *A.vdiv : 1.0;
+    A.ihd = 1.0 / A.hd;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     double acc = 0.0;
     if (i < A.nx) {
@@ -246,10 +272,10 @@ __global__ __launch_bounds__(kBlock) void k_st1d(KArgs A0) {
         bool rare_ = false;
         double val = point_value<NK_BRATU1D, MODE>(A, c, lap(c, r, l, A.hx2), uc, 0.0, f0, c, 0.0, et, rare_);
         const double ax = (EPI == EPI_DOT || EPI == EPI_DOTV || EPI == EPI_RESID) ? A.aux[i]
-                          : (EPI == EPI_DOTVS ? A.v[i] / A.hd : 0.0);
+                          : (EPI == EPI_DOTVS ? div_rn(A.v[i], A.hd, A.ihd) : 0.0);
         acc = epilogue<EPI>(val, ax, acc);
         A.out[i] = val;
-        if constexpr (MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS)) A.vout[i] = A.v[i] / A.hd;
+        if constexpr (MODE != MODE_RES && (EPI == EPI_DOTV || EPI == EPI_DOTVS)) A.vout[i] = div_rn(A.v[i], A.hd, A.ihd);
     }
     if (EPI != EPI_NONE) publish(acc, A.part, A.fin, sh);
 }
@@ -273,12 +299,12 @@ __device__ __forceinline__ Row<VEC> field_row(const KArgs& A, int64_t o, bool ok
                     r.v[h] = q.x; r.v[h + 1] = q.y;
                 } else if constexpr (MODE == MODE_JEXACT) {
                     double2 q = *reinterpret_cast<const double2*>(A.v + o + h);
-                    if (A.vdiv) { q.x = q.x / A.hd; q.y = q.y / A.hd; }
+                    if (A.vdiv) { q.x = div_rn(q.x, A.hd, A.ihd); q.y = div_rn(q.y, A.hd, A.ihd); }
                     r.v[h] = q.x; r.v[h + 1] = q.y;
                 } else {
                     const double2 qu = *reinterpret_cast<const double2*>(A.u + o + h);
                     double2 qv = *reinterpret_cast<const double2*>(A.v + o + h);
-                    if (A.vdiv) { qv.x = qv.x / A.hd; qv.y = qv.y / A.hd; }
+                    if (A.vdiv) { qv.x = div_rn(qv.x, A.hd, A.ihd); qv.y = div_rn(qv.y, A.hd, A.ihd); }
                     r.v[h] = qu.x + A.eps * qv.x;  // w = u + eps v
                     r.v[h + 1] = qu.y + A.eps * qv.y;
                 }
@@ -470,10 +496,10 @@ __device__ __forceinline__ WV cook_w(const KArgs& A, double ra, double rb, bool 
         r.v = 0.0;
         r.w = ra;
     } else if constexpr (MODE == MODE_JEXACT) {
-        r.v = div ? ra / A.hd : ra;
+        r.v = div ? div_rn(ra, A.hd, A.ihd) : ra;
         r.w = r.v;
     } else {
-        r.v = div ? rb / A.hd : rb;
+        r.v = div ? div_rn(rb, A.hd, A.ihd) : rb;
         r.w = ra + A.eps * r.v;  // w = u + eps v
     }
     return r;
@@ -667,7 +693,9 @@ void k_st2d(KArgs A0) {
     __shared__ double sh[kShN];
     NK_EXP_LDS(KIND)
     KArgs A = A0;
+    if constexpr (!kKeepVdiv && EPI != EPI_DOTV && EPI != EPI_DOTVS) A.vdiv = nullptr;  // v / h only with V_k stored
     A.hd = A.vdiv ? *A.vdiv : 1.0;
+    A.ihd = 1.0 / A.hd;
     constexpr int SCH = scheme_of<KIND>();
     constexpr bool kG = SCH != 0 && MODE != MODE_JEXACT;  // u_n rows with the stencil field
     const int lane = threadIdx.x & 63;
@@ -846,7 +874,9 @@ __global__ __launch_bounds__(64 * NW) void k_st2t(KArgs A0) {
     NK_EXP_LDS(KIND)
     bool rare_ = false;
     KArgs A = A0;
+    if constexpr (!kKeepVdiv && EPI != EPI_DOTV && EPI != EPI_DOTVS) A.vdiv = nullptr;  // v / h only with V_k stored
     A.hd = A.vdiv ? *A.vdiv : 1.0;
+    A.ihd = 1.0 / A.hd;
     constexpr int SCH = scheme_of<KIND>();
     constexpr bool kG = SCH != 0 && MODE != MODE_JEXACT;
     constexpr bool kTG = SCH == 2 && kG;              // G_Trapezoid!: u_n's Laplacian
@@ -1004,7 +1034,9 @@ __global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
     const double* const et = nullptr;  // heat kinds: no exp
     bool rare_ = false;
     KArgs A = A0;
+    if constexpr (!kKeepVdiv && EPI != EPI_DOTV && EPI != EPI_DOTVS) A.vdiv = nullptr;  // v / h only with V_k stored
     A.hd = A.vdiv ? *A.vdiv : 1.0;
+    A.ihd = 1.0 / A.hd;
     constexpr int SCH = scheme_of<KIND>();
     constexpr bool kG = SCH != 0 && MODE != MODE_JEXACT;
     const int lane = threadIdx.x & 63;
@@ -1138,7 +1170,9 @@ __global__ __launch_bounds__(64 * NW) void k_st3l(KArgs A0) {
     const double* const et = nullptr;  // heat kinds: no exp
     bool rare_ = false;
     KArgs A = A0;
+    if constexpr (!kKeepVdiv && EPI != EPI_DOTV && EPI != EPI_DOTVS) A.vdiv = nullptr;  // v / h only with V_k stored
     A.hd = A.vdiv ? *A.vdiv : 1.0;
+    A.ihd = 1.0 / A.hd;
     constexpr int SCH = scheme_of<KIND>();
     constexpr bool kG = SCH != 0 && MODE != MODE_JEXACT;
     constexpr bool kTG = SCH == 2 && kG;  // G_Trapezoid!: u_n's y-neighbours too
@@ -1379,7 +1413,9 @@ __global__ __launch_bounds__(64 * NW) void k_st3y(KArgs A0) {
     const double* const et = nullptr;  // heat kinds: no exp
     bool rare_ = false;
     KArgs A = A0;
+    if constexpr (!kKeepVdiv && EPI != EPI_DOTV && EPI != EPI_DOTVS) A.vdiv = nullptr;  // v / h only with V_k stored
     A.hd = A.vdiv ? *A.vdiv : 1.0;
+    A.ihd = 1.0 / A.hd;
     constexpr int SCH = scheme_of<KIND>();
     constexpr bool kG = SCH != 0 && MODE != MODE_JEXACT;
     constexpr bool kTG = SCH == 2 && kG;

@@ -163,7 +163,9 @@ def test_newton_preconditioned_bratu1d_config1(ctx, N, algo):
     """examples/bratu.jl's preconditioned solves at BASELINE config 1 size (1D Bratu N = 1000).
     Hundreds of Arnoldi steps per Newton step on cond(J) ~ 1.75e8 make the inner counts chaotic in
     the last bits (as for CG, test_hip.py), so: equal Newton steps, inner counts within 5 %, and the
-    same root to the precision fp64 determines it (~1e-8 relative)."""
+    same root to the precision the solve determines it: the oracle's own root moves by 1.4-1.8e-6
+    (relative) when u0 is perturbed by 1e-15 relative with N = inner GMRES(5) + FGMRES, 1.2e-7 with
+    Jacobi (measured, r04) -- hence 5e-6."""
     P = oc.bratu1d(1000)
     u0 = oc.sin_ic(P)
     ref, so = oc.newton_krylov(P, u0, algo=algo, N=N)
@@ -172,7 +174,7 @@ def test_newton_preconditioned_bratu1d_config1(ctx, N, algo):
     assert r.solved and so["solved"]
     assert r.stats.outer_iterations == so["outer_iterations"]
     assert abs(r.stats.inner_iterations - so["inner_iterations"]) <= 0.05 * so["inner_iterations"]
-    np.testing.assert_allclose(u.to_numpy(), ref, rtol=0, atol=1e-6 * np.abs(ref).max())
+    np.testing.assert_allclose(u.to_numpy(), ref, rtol=0, atol=5e-6 * np.abs(ref).max())
 
 
 # ----------------------------------------------------------------------------- ILU(0)
