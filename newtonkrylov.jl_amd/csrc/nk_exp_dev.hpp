@@ -39,10 +39,20 @@ __device__ __forceinline__ double nk_exp_t(double x, const double* tab) {
 
 // correctly rounded exp(x) per lane: the exact phase runs divergently (vector registers) in the lanes
 // that need it -- for code where little else is live (k_st2d's fixup of the points its march marked)
+#ifndef NK_EXP_RARE_CALL
+#define NK_EXP_RARE_CALL 1
+#endif
+// the exact phase as a real call: its registers are the callee's; the caller saves what it keeps in
+// the clobbered ones around the call -- in the cold block, never in the loop that contains it
+__device__ __attribute__((noinline)) double nk_exp_rare_fn(double x) { return nkx_exp_rare(x); }
 __device__ __forceinline__ double nk_exp_lane(double x, const double* tab) {
     double y;
     if (__builtin_expect(nkx_exp_fast(x, tab, &y), 1)) return y;
+#if NK_EXP_RARE_CALL
+    return nk_exp_rare_fn(x);
+#else
     return nkx_exp_rare(x);
+#endif
 }
 
 // correctly rounded exp(x), table from device memory
