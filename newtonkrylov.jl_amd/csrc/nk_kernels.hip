@@ -735,11 +735,10 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     A.nx = p->nx; A.ny = p->ny; A.nz = p->nz;
     A.hx2 = p->hx * p->hx; A.hy2 = p->hy * p->hy; A.hz2 = p->hz * p->hz;
     A.lam = p->lambda; A.a = p->a; A.dt = p->dt; A.eps = in.eps;
-    // kbench A/B bits: 2^20 the platform exp, 2^21 x-neighbours through ds_bpermute instead of DPP shifts,
-    // 2^22 the exp's fast phase alone (diagnosis: not correctly rounded), 2^23 the stencils' divisions as
-    // division instruction sequences instead of div_rn
-    A.fast = fast | (NK_TUNE("NK_EXP_OCML", 0) ? (1 << 20) : 0) | (NK_TUNE("NK_XNBR_SHFL", 0) ? (1 << 21) : 0) |
-             (NK_TUNE("NK_EXP_FASTONLY", 0) ? (1 << 22) : 0) | (NK_TUNE("NK_DIV_INSN", 0) ? (1 << 23) : 0);
+    // kbench A/B bits: 2^20 the platform exp, 2^22 the exp's fast phase alone (diagnosis: not correctly
+    // rounded), 2^23 the Bratu stencils' divisions as division instruction sequences instead of div_rn
+    A.fast = fast | (NK_TUNE("NK_EXP_OCML", 0) ? (1 << 20) : 0) | (NK_TUNE("NK_EXP_FASTONLY", 0) ? (1 << 22) : 0) |
+             (NK_TUNE("NK_DIV_INSN", 0) ? (1 << 23) : 0);
     A.vdiv = in.vdiv;
     A.vout = in.vout;
     A.ihx2 = 1.0 / A.hx2; A.ihy2 = 1.0 / A.hy2; A.ihz2 = 1.0 / A.hz2; A.ieps = in.eps != 0.0 ? 1.0 / in.eps : 0.0;

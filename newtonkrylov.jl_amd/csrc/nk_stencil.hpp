@@ -74,12 +74,24 @@ constexpr bool heat_kind() {
     return KIND >= NK_HEAT2D_EULER && KIND <= NK_HEAT3D_TRAPEZOID;
 }
 
+// div_rn is used in the Bratu stencil objects only (nk_stencil_inst.hip with NK_ST_KIND 1 / 2: their FD Jv
+// 130 -> 126 us, profiles/r04/ab_div_rn.log); elsewhere its guard's compares and exec-mask branches cost
+// more than the division sequence they replace (the heat2d FD Jv loop: 304 -> 471 instructions).
+#if defined(NK_ST_KIND) && (NK_ST_KIND == NK_BRATU1D || NK_ST_KIND == NK_BRATU2D)
+#define NK_ST_DIV_RN 1
+#else
+#define NK_ST_DIV_RN 0
+#endif
 // RN(a / b), the IEEE quotient, from yb = RN(1 / b) (computed once: host or kernel prologue): q0 = a yb is
 // within an ulp of a / b, the remainder a - b q0 is exact (fma), and one correction q0 + r yb rounds to
 // RN(a / b) (Markstein's theorem; round to nearest, no under/overflow -- the operands outside
 // 2^-900 <= |a|, |q0| <= 2^1000, zeros included, take the division itself).  3 VALU operations instead of
 // the ~10 of a division; bit-identical (also checked on 2.2e8 quotients by tests/test_div_rn.py).
 __device__ __forceinline__ double div_rn(double a, double b, double yb) {
+#if !NK_ST_DIV_RN
+    (void)yb;
+    return a / b;
+#endif
     const double q0 = a * yb;
     const double r = fma(-q0, b, a);
     const double q1 = fma(r, yb, q0);
@@ -641,6 +653,12 @@ __device__ __forceinline__ void tile3_of(int b, int nb, int tiles_x, int tiles_y
 // one-lane shifts across the whole wave as DPP moves (gfx9's wave_shr:1 / wave_shl:1): a VALU op per
 // 32-bit half, where __shfl_up / __shfl_down go through the LDS crossbar (ds_bpermute) and an lgkmcnt
 // wait.  The lane with no source (0 resp. 63) keeps 0; x_nbrs overrides it with its edge value.
+// Opt-in (-DNK_XNBR_DPP=1): bitwise, but in the heat2d FD Jv the compiler then waits for ALL loads in
+// flight mid-loop (vmcnt(0) where the ds_bpermute form keeps the next rows' two loads outstanding,
+// vmcnt(2)) -- 550 -> 607 us (profiles/r04/README.md)
+#ifndef NK_XNBR_DPP
+#define NK_XNBR_DPP 0
+#endif
 __device__ __forceinline__ double wave_shr1(double x) {  // lane i <- lane i - 1
     const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x138, 0xf, 0xf, false);
     const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x138, 0xf, 0xf, false);
@@ -660,17 +678,14 @@ template <bool PER>
 __device__ __forceinline__ LR x_nbrs(const KArgs& A, double cfirst, double clast, double e, double e2, int lane,
                                      bool rwrap) {
     LR o;
-#ifdef NK_KBENCH
-    if (A.fast & (1 << 21)) {  // kbench A/B only: the LDS-crossbar shuffles
-        o.l = __shfl_up(clast, 1, 64);
-        o.r = __shfl_down(cfirst, 1, 64);
-    } else
+    (void)A;
+#if NK_XNBR_DPP
+    o.l = wave_shr1(clast);
+    o.r = wave_shl1(cfirst);
+#else
+    o.l = __shfl_up(clast, 1, 64);
+    o.r = __shfl_down(cfirst, 1, 64);
 #endif
-    {
-        (void)A;
-        o.l = wave_shr1(clast);
-        o.r = wave_shl1(cfirst);
-    }
     if (lane == 0) o.l = e;
     if constexpr (PER) {
         if (lane == 63 || rwrap) o.r = e2;
