@@ -653,9 +653,7 @@ __device__ __forceinline__ void tile3_of(int b, int nb, int tiles_x, int tiles_y
 // one-lane shifts across the whole wave as DPP moves (gfx9's wave_shr:1 / wave_shl:1): a VALU op per
 // 32-bit half, where __shfl_up / __shfl_down go through the LDS crossbar (ds_bpermute) and an lgkmcnt
 // wait.  The lane with no source (0 resp. 63) keeps 0; x_nbrs overrides it with its edge value.
-// Opt-in (-DNK_XNBR_DPP=1): bitwise, but in the heat2d FD Jv the compiler then waits for ALL loads in
-// flight mid-loop (vmcnt(0) where the ds_bpermute form keeps the next rows' two loads outstanding,
-// vmcnt(2)) -- 550 -> 607 us (profiles/r04/README.md)
+// Opt-in (-DNK_XNBR_DPP=1): bitwise and neutral on every workload measured (profiles/r04/README.md).
 #ifndef NK_XNBR_DPP
 #define NK_XNBR_DPP 0
 #endif
