@@ -1177,7 +1177,6 @@ __global__ __launch_bounds__(64 * NW) void k_st3d(KArgs A0) {
 // cost no extra load issue and re-fetch (NW + 2) / NW of a plane instead of 1.5x.
 // F0R: as k_st2d's -- F(u) recomputed from the u rows (and a second LDS row for the u field's
 // y-neighbours) with the residual kernel's arithmetic instead of loading F0
-template <int KIND, int MODE, int EPI, int VEC, bool PER = false, int NW = 8, bool F0R = false>
 // Waves per SIMD the 3D z-march is allocated for: 4 (<= 128 VGPRs instead of 132) for G_Euler!'s FD Jv + dot
 // with F(u) recomputed -- the config-5 slab's Jv, 147 -> 141 us; every other instance unconstrained (the
 // same cap on all of them: 512^3 Euler FD Jv 1160 -> 1257 us, midpoint 1303 -> 2900 us with spills,
@@ -1185,6 +1184,7 @@ template <int KIND, int MODE, int EPI, int VEC, bool PER = false, int NW = 8, bo
 #ifndef NK_ST3L_WPE
 #define NK_ST3L_WPE(KIND, EPI, F0R) ((KIND == NK_HEAT3D_EULER && EPI == EPI_DOT && F0R) ? 4 : 1)
 #endif
+template <int KIND, int MODE, int EPI, int VEC, bool PER = false, int NW = 8, bool F0R = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L_WPE(KIND, EPI, F0R)))) void k_st3l(KArgs A0) {
     __shared__ double sh[kShN];
     const double* const et = nullptr;  // heat kinds: no exp
