@@ -191,6 +191,15 @@ constexpr bool kKeepVdiv = false;
 #ifndef NK_ST2D_BRATU_WPE
 #define NK_ST2D_BRATU_WPE 4
 #endif
+#ifndef NK_ST2D_HEAT_CAP  // A/B: occupancy caps for the trapezoid kernels just above a wave threshold
+#define NK_ST2D_HEAT_CAP 0
+#endif
+constexpr int st2d_wpe(int kind, int mode, bool f0r) {
+    return kind_bratu(kind) ? NK_ST2D_BRATU_WPE
+                            : ((NK_ST2D_HEAT_CAP && kind == NK_HEAT2D_TRAPEZOID)
+                                   ? (mode == MODE_RES ? 6 : (f0r ? 4 : 1))
+                                   : 1);
+}
 
 // The exp table (NKX_T: 128 double-double entries, 2 KB) copied into LDS once per block for the Bratu
 // kinds, where every point evaluates exp: read with ds_read, its lookups never wait behind the rows the
@@ -701,7 +710,7 @@ __device__ __forceinline__ LR x_nbrs(const KArgs& A, double cfirst, double clast
 // point_value), so (F(w) - F(u)) / eps is bit-identical to loading the F0 that kernel stored, and
 // 8 B/pt less is read.  Valid only when F0 IS that residual of this u (the Newton loop's res).
 template <int KIND, int MODE, int EPI, int VEC, bool PER = false, bool F0R = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kind_bratu(KIND) ? NK_ST2D_BRATU_WPE : 1)))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(st2d_wpe(KIND, MODE, F0R))))
 void k_st2d(KArgs A0) {
     __shared__ double sh[kShN];
     NK_EXP_LDS(KIND)
