@@ -191,7 +191,7 @@ constexpr bool kKeepVdiv = false;
 #ifndef NK_ST2D_BRATU_WPE
 #define NK_ST2D_BRATU_WPE 4
 #endif
-#ifndef NK_ST2D_HEAT_CAP  // A/B: occupancy caps for the trapezoid kernels just above a wave threshold
+#ifndef NK_ST2D_HEAT_CAP  // A/B: occupancy caps for the trapezoid kernels (no gain: profiles/r04/ab_trapezoid_caps.log)
 #define NK_ST2D_HEAT_CAP 0
 #endif
 constexpr int st2d_wpe(int kind, int mode, bool f0r) {
