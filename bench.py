@@ -48,9 +48,10 @@ KIND = {("heat2d", "euler"): 3, ("heat3d", "euler"): 4, ("heat2d", "midpoint"): 
 
 
 def stencil_prefix(workload, scheme="euler"):
+    """Fallback when a profile entry names no instantiation: the product's 2D march / 3D z-march (k_st3l)."""
     if workload == "bratu2d":
         return "nk::k_st2d<2, "
-    return f"nk::k_st{workload[-2:]}<{KIND[workload, scheme]}, "
+    return f"nk::k_st{'2d' if workload == 'heat2d' else '3l'}<{KIND[workload, scheme]}, "
 
 
 def pmc_name(workload, kernel, scheme="euler"):
@@ -196,6 +197,69 @@ def launch_ranks(n: int, argv: list) -> int:
     return subprocess.run(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")).returncode
 
 
+def exchange_cost(p0, p1, steps, elapsed):
+    """What the exchange cost this rank over the timed steps, from the device's own peer-wait clocks
+    (nk_path_info): ghost-plane waits of the slab-end tiles (or exchange blocks) and cross-rank reduction
+    waits (block 0 of every mailbox all-reduce consumer).  The end tiles of one launch wait side by side,
+    so a launch's ghost-plane delay is about their MEAN wait; a reduction's is block 0's wait.
+    exchange_share = (launches with an in-launch / separate exchange x mean tile wait + reduction waits)
+    / elapsed: an upper bound on the time the exchange kept off the critical path (waits can overlap work)."""
+    d = {k: p1[k] - p0[k] for k in ("halo_waits", "reduce_waits", "halo_wait_us", "reduce_wait_us",
+                                     "jv_halo_fused", "jv_halo_separate")}
+    launches = d["jv_halo_fused"] + d["jv_halo_separate"]
+    halo_mean = d["halo_wait_us"] / d["halo_waits"] if d["halo_waits"] else 0.0
+    red_mean = d["reduce_wait_us"] / d["reduce_waits"] if d["reduce_waits"] else 0.0
+    per_step = (launches * halo_mean + d["reduce_wait_us"]) / max(1, steps)
+    return {"halo_waits": d["halo_waits"], "halo_wait_us_mean": round(halo_mean, 3),
+            "halo_launches": launches, "reduce_waits": d["reduce_waits"], "reduce_wait_us_mean": round(red_mean, 3),
+            "exchange_us_per_step": round(per_step, 1),
+            "exchange_share": round(per_step * steps * 1e-6 / elapsed, 4) if elapsed > 0 else None}
+
+
+def config2_reference():
+    """The single-GPU config-2 line to compare a slab line's per-DoF rate with: the newest driver record
+    (BENCH_rNN.json at the repo root) of the default 2D Bratu 4096^2 bench, in DoF x matvecs / s."""
+    import glob
+
+    for f in sorted(glob.glob(os.path.join(ROOT, "BENCH_r*.json")), reverse=True):
+        try:
+            with open(f) as fh:
+                rec = json.load(fh)
+            line = json.loads(rec["run"]["stdout_tail"].strip().splitlines()[-1])
+        except (OSError, KeyError, ValueError, IndexError):
+            continue
+        if line.get("n_gpus") == 1 and "4096x4096 (4096x4096 per GPU)" in line.get("config", {}).get("workload", ""):
+            return {"value": line["value"] * 4096 ** 2, "source": f"{os.path.basename(f)}: {line['value']} matvecs/s "
+                    "x 4096^2 (2D Bratu 4096^2, one GPU)"}
+    return None
+
+
+def scaling_fields(value, dof_per_unit, paths, workload, slab_of, world, global_n, ref=None):
+    """The multi-GPU part of the JSON line (a pure function: tests/test_bench_launcher.py checks an 8-rank
+    assembly on CPU).  dof_rate: the north star's >= 6x at 8 GPUs as a per-DoF rate -- DoF x matvecs / s of
+    this line against the single-GPU config-2 line (a one-rank slab line has no exchange: its ratio is the
+    ceiling the exchange can only lower).  ranks: every rank's path report with its exchange cost;
+    exchange: the worst rank's share of the timed region spent waiting for peers."""
+    out = {}
+    if world > 1 or global_n:
+        dof = value * dof_per_unit
+        if ref is None and workload == "bratu2d":
+            ref = config2_reference()
+        out["dof_rate"] = {"dof_matvecs_per_s": round(dof, 1),
+                           "vs_config2_single_gpu": round(dof / ref["value"], 3) if ref else None,
+                           "config2_reference": ref["source"] if ref else None,
+                           "exchange": "none (one rank's slab alone)" if slab_of else "included"}
+    if world > 1:
+        out["ranks"] = paths  # per rank: transport, resident sweep, in-launch ghost planes, launch counts, cost
+        ex = [q.get("exchange") or {} for q in paths]
+        shares = [e.get("exchange_share") for e in ex if e.get("exchange_share") is not None]
+        out["exchange"] = {"max_share": max(shares) if shares else None,
+                           "max_halo_wait_us_mean": max((e.get("halo_wait_us_mean", 0.0) for e in ex), default=None),
+                           "max_reduce_wait_us_mean": max((e.get("reduce_wait_us_mean", 0.0) for e in ex), default=None),
+                           "what": "per rank: device wall-clock peer waits over the timed steps (ranks[].exchange)"}
+    return out
+
+
 def noisy(shape_rows, nx, seed_rows):
     """0.1 U(-1, 1) noise whose every row is seeded by its GLOBAL index, so a slab sees the same field."""
     return np.stack([0.1 * np.random.default_rng([0, int(r)]).uniform(-1.0, 1.0, nx) for r in seed_rows]).reshape(
@@ -233,6 +297,9 @@ class Bratu2D:
         self.jv_kernel = "jv_fd_dot_norm" if args.jv == "fd" else "jv_exact_dot_norm"
         self.scaling = "strong" if args.global_n else "weak"
         self.units_per_matvec = 1 if args.global_n else world  # matvecs counted over the whole problem
+        # grid points one counted matvec covers: the global grid (strong scaling / one rank's slab of it
+        # alone: `value` counts global matvecs), else one rank's slab (weak scaling: slab matvecs)
+        self.dof_per_unit = n * ny_glob if args.global_n else n * rows
         slab = (f"; rank {rank}'s slab of the {parts}-way split ALONE on one GPU (ghost planes zero, no exchange): "
                 f"value = slab matvecs/s = the global matvec rate {parts} GPUs would reach without exchange cost"
                 if args.slab_of else "")
@@ -348,6 +415,7 @@ class HeatEuler:
             u0 = base + noisy((planes, n), n, range(rows0 * n, (rows0 + planes) * n))
         self.scaling = "strong" if args.global_n else "weak"
         self.units_per_matvec = 1 if args.global_n else world
+        self.dof_per_unit = int(np.prod(glob)) if args.global_n else n ** (dim - 1) * planes
         self.u0 = np.ascontiguousarray(u0)
         self.un = ah.DeviceArray.from_numpy(self.u0, grid, ctx)
         self.u = self.un.copy()
@@ -517,6 +585,7 @@ def main():
     # NK_E_* error and the whole launch exit non-zero instead of hanging
     fault_rank = int(os.environ.get("NK_BENCH_FAULT_RANK", "-1"))
     barrier()
+    path0 = ctx.path_info()  # the peer-wait counters before the timed region
     t0 = time.perf_counter()
     matvecs = 0
     last = None
@@ -543,6 +612,7 @@ def main():
     # the launch counts that prove it: a multi-GPU line names its own path
     path = ctx.path_info()
     path["host"] = socket.gethostname()
+    path["exchange"] = exchange_cost(path0, path, args.steps, elapsed)
     path["launches"] = {k: prof.get(k, {}).get("launches", 0)
                         for k in ("mgs_sweep", "mgs_pass", "mgs_pass_last", "halo_ipc", "halo_rccl", "allreduce")}
     paths = [path]
@@ -585,7 +655,11 @@ def main():
             pmc = json.load(f)
 
     def traffic(name):
-        """PMC HBM bytes per launch of this kernel class as a rate over the same launch duration."""
+        """PMC HBM bytes per launch of this kernel class: the entry of exactly the instantiation this run
+        launched (nk_prof_entry.kernel, stencil classes), else the class's kernel-name prefix."""
+        inst = prof.get(name, {}).get("kernel")
+        if inst:
+            return pmc[inst]["traffic_bytes"] if inst in pmc else None
         pre = pmc_name(args.workload, name, args.scheme)
         hit = [v for k, v in pmc.items() if pre and k.startswith(pre)]
         return hit[0]["traffic_bytes"] if hit else None
@@ -606,7 +680,8 @@ def main():
         # avg_us: the mean launch duration over ALL launches at the measured rate (the timed launches
         # of a kernel whose size varies per launch are not a uniform sample of the sizes);
         # avg_us_timed: the plain mean of the timed launches
-        return {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        return {"kernel": name, "instantiation": v.get("kernel") or None, "bound": "hbm", "achieved": round(ach, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4),
                 "bytes_basis": "l2_egress: every operand byte the kernel loads / stores (any cache level; "
                                "PMC FETCH/WRITE_SIZE count the same, Infinity-Cache hits included)",
@@ -670,8 +745,7 @@ def main():
                                     "thread, non-temporal load + store (the fastest copy of tools/stream_probe.py), "
                                     "mean of 5 launches, after the timed region"},
         }
-        if world > 1:
-            out["ranks"] = paths  # per rank: transport, resident sweep, in-launch ghost planes, launch counts
+        out.update(scaling_fields(value, W.dof_per_unit, paths, args.workload, args.slab_of, world, args.global_n))
         if world == 1 and not args.no_cpu_baseline and not args.global_n:
             # the node's host cores: the fastest thread count the process's affinity mask offers (the
             # headline figure), and the per-GPU share the box gives one GPU (OMP_NUM_THREADS, 16 there)

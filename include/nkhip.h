@@ -322,6 +322,18 @@ typedef struct nk_path_info {
     int64_t jv_halo_separate; /* Jv launches that exchanged them with a separate launch first        */
     int64_t sweeps_resident;  /* resident MGS sweeps (one launch per Arnoldi step)                     */
     int64_t mgs_passes;       /* per-pass MGS launches (the chain)                                     */
+    /* FD operator launches of the built-in stencils, by the instantiation that ran: F(u) recomputed from
+       the u rows (F0R: nk_krylov_opts.f0_is_residual) / F0 loaded */
+    int64_t jv_fd_f0r;
+    int64_t jv_fd_f0_read;
+    /* what the exchange costs this rank, measured on the device (wall clock) since the context was created:
+       the ghost-plane waits of the slab-end stencil tiles (in-launch) or exchange blocks (separate launch),
+       one per tile / block and launch; and the cross-rank reduction waits, one per mailbox all-reduce
+       (its consumer's block 0).  Zero without a peer mailbox. */
+    int64_t halo_waits;
+    int64_t reduce_waits;
+    double halo_wait_us;
+    double reduce_wait_us;
 } nk_path_info;
 int nk_dist_path(nk_ctx* ctx, nk_path_info* out);
 
@@ -336,6 +348,9 @@ typedef struct nk_prof_entry {
     double bytes_all;      /* algorithmic bytes of ALL launches (per-launch sizes may vary)   */
     double dram_bytes_all; /* the unique-DRAM model of ALL launches: each distinct operand byte once
                               (re-reads counted as Infinity-Cache hits -- a lower bound on DRAM traffic) */
+    char kernel[64];       /* stencil classes: the instantiation the last launch ran, as rocprofv3 names it
+                              without the namespace / argument list (e.g. "nk::k_st2d<7, 2, 4, 2, true, true>");
+                              empty for the other classes */
 } nk_prof_entry;
 /* every = 0: off; every = k > 0: time every k-th launch of each kernel class with a pair of HIP
  * events on the context stream (k > 1 keeps the event overhead out of the timed region). */

@@ -94,12 +94,15 @@ class nk_path_info(C.Structure):
                 ("rccl", C.c_int32), ("mailbox", C.c_int32), ("resident_sweep", C.c_int32),
                 ("resident_blocks", C.c_int32), ("halo_in_launch", C.c_int32), ("mailbox_error", C.c_int32),
                 ("halo_cap", C.c_int64), ("pci_bus_id", C.c_char * 32), ("jv_halo_fused", C.c_int64),
-                ("jv_halo_separate", C.c_int64), ("sweeps_resident", C.c_int64), ("mgs_passes", C.c_int64)]
+                ("jv_halo_separate", C.c_int64), ("sweeps_resident", C.c_int64), ("mgs_passes", C.c_int64),
+                ("jv_fd_f0r", C.c_int64), ("jv_fd_f0_read", C.c_int64), ("halo_waits", C.c_int64),
+                ("reduce_waits", C.c_int64), ("halo_wait_us", C.c_double), ("reduce_wait_us", C.c_double)]
 
 
 class nk_prof_entry(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("timed", C.c_int64), ("total_ms", C.c_double),
-                ("bytes", C.c_double), ("bytes_all", C.c_double), ("dram_bytes_all", C.c_double)]
+                ("bytes", C.c_double), ("bytes_all", C.c_double), ("dram_bytes_all", C.c_double),
+                ("kernel", C.c_char * 64)]
 
 
 # name -> (restype, argtypes); mirrors include/nkhip.h one to one

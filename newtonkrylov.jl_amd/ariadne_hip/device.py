@@ -115,7 +115,7 @@ class Context:
         self.check(load().nk_prof_read(self.handle, buf, cap, C.byref(cnt)), "nk_prof_read")
         return {buf[i].name.decode(): dict(launches=buf[i].launches, timed=buf[i].timed, ms=buf[i].total_ms,
                                            bytes=buf[i].bytes, bytes_all=buf[i].bytes_all,
-                                           dram_all=buf[i].dram_bytes_all)
+                                           dram_all=buf[i].dram_bytes_all, kernel=buf[i].kernel.decode())
                 for i in range(min(cnt.value, cap))}
 
 

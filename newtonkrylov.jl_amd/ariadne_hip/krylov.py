@@ -34,17 +34,26 @@ def exp_(y, x, ctx=None):
     tensors on the context's device (enqueued on the library stream, where user callbacks run)."""
     from .device import default_context
 
-    def ptr_len(a):
+    ctx = ctx or (y.ctx if isinstance(y, DeviceArray) else x.ctx if isinstance(x, DeviceArray) else default_context())
+
+    def ptr_len(a, what):
+        # every operand must live on THIS context's GPU: a host tensor's (or another device's) address
+        # handed to the kernel would fault the GPU instead of raising
         if isinstance(a, DeviceArray):
+            if a.ctx is not ctx:
+                raise ValueError(f"exp_: {what} belongs to another context")
             return a.ptr, a.n
+        if not hasattr(a, "data_ptr"):
+            raise ValueError(f"exp_: {what} must be a DeviceArray or a torch tensor")
         if a.dtype != __import__("torch").float64 or not a.is_contiguous():
             raise ValueError("exp_: contiguous float64 tensors only")
+        if not a.is_cuda or a.device.index != ctx.device:
+            raise ValueError(f"exp_: {what} must be on the context's GPU (cuda:{ctx.device}), not {a.device}")
         return a.data_ptr(), a.numel()
 
-    (py, ny), (px, nx) = ptr_len(y), ptr_len(x)
+    (py, ny), (px, nx) = ptr_len(y, "y"), ptr_len(x, "x")
     if ny != nx:
         raise ValueError(f"exp_: lengths differ ({ny} vs {nx})")
-    ctx = ctx or (y.ctx if isinstance(y, DeviceArray) else x.ctx if isinstance(x, DeviceArray) else default_context())
     ctx.check(load().nk_vexp(ctx.handle, nx, py, px), "nk_vexp")
     return y
 

@@ -497,6 +497,8 @@ int nk_prof_read(nk_ctx* c, nk_prof_entry* out, int32_t cap, int32_t* count) {
             out[m].bytes = c->acc[k].bytes;
             out[m].bytes_all = c->acc[k].bytes_all;
             out[m].dram_bytes_all = c->acc[k].dram_all;
+            std::memset(out[m].kernel, 0, sizeof(out[m].kernel));
+            std::strncpy(out[m].kernel, c->acc[k].kernel.c_str(), sizeof(out[m].kernel) - 1);
         }
         ++m;
     }

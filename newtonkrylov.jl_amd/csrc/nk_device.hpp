@@ -21,6 +21,8 @@ struct MbInfo {
     int rank, nranks;
     int* err;            // pinned host flag
     unsigned spin_limit;
+    unsigned long long* wacc;  // peer-wait accounting (nk_path_info): [2w] ticks, [2w + 1] waits; w = 0 ghost
+                               // planes, 1 cross-rank reductions (null: not counted)
 };
 hipError_t resident_bind_mb(const MbInfo& m);  // nk_resident.hip's copy of g_mb
 
@@ -68,6 +70,15 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
 // one copy of g_mb per translation unit (internal linkage): mailbox_bind sets every copy
 __device__ MbInfo g_mb;
 
+// one peer wait's device wall-clock time (ticks since t0) into the context's counters
+constexpr int kWaitHalo = 0, kWaitReduce = 1;
+__device__ __forceinline__ void wait_note(int which, uint64_t t0) {
+    if (!g_mb.wacc) return;
+    const unsigned long long dt = (unsigned long long)(wall_clock64() - t0);
+    __hip_atomic_fetch_add(g_mb.wacc + 2 * which, dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(g_mb.wacc + 2 * which + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ uint64_t* mb_cell(uint64_t* base, unsigned epoch, int rank) {
     return base + ((size_t)(epoch % kMbSlots) * kMbRanks + rank) * 2;
 }
@@ -88,6 +99,7 @@ __device__ __forceinline__ void mb_send(double t, unsigned epoch) {
 __device__ double mb_recv(unsigned epoch, double* sh) {
     if (threadIdx.x < 64) {
         const int l = threadIdx.x, nr = g_mb.nranks;
+        const uint64_t t0 = (blockIdx.x == 0 && l == 0) ? wall_clock64() : 0;
         uint32_t half = 0;
         if (l < 2 * nr) {
             const uint64_t* g = mb_cell(g_mb.self, epoch, l >> 1) + (l & 1);
@@ -113,6 +125,7 @@ __device__ double mb_recv(unsigned epoch, double* sh) {
         double t = 0.0;
         for (int r = 0; r < nr; ++r) t += __shfl(v, 2 * r, 64);  // fixed rank order
         if (l == 0) sh[kShB] = t;
+        if (blockIdx.x == 0 && l == 0) wait_note(kWaitReduce, t0);  // (every lane's poll has ended here)
     }
     __syncthreads();
     return sh[kShB];
@@ -248,6 +261,7 @@ __device__ __forceinline__ bool halo_tile_exchange(const double* __restrict__ v,
         if (t.lo) __hip_atomic_store(halo_tile_flags(g_mb.peers[(rank + nr - 1) % nr], par, 1) + tile, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (t.hi) __hip_atomic_store(halo_tile_flags(g_mb.peers[(rank + 1) % nr], par, 0) + tile, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         hx_ok = 1;
+        const uint64_t t0 = wall_clock64();
         for (int side = 0; side < 2; ++side) {
             if ((side == 0 && !t.lo) || (side == 1 && !t.hi)) continue;
             const uint64_t* f = halo_tile_flags(g_mb.self, par, side) + tile;
@@ -262,6 +276,7 @@ __device__ __forceinline__ bool halo_tile_exchange(const double* __restrict__ v,
                 __builtin_amdgcn_s_sleep(2);
             }
         }
+        wait_note(kWaitHalo, t0);
     }
     __syncthreads();
     return hx_ok != 0;

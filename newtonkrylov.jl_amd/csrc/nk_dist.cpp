@@ -120,7 +120,8 @@ static int mb_alloc(nk_ctx* c) {
 // resident MGS sweep's per-pass cross-rank stage -- stays on the mailbox.
 struct HostHandle {  // the 64-byte record that stands in for a hipIpcMemHandle_t
     char magic[8];
-    char name[48];
+    char name[40];      // the POSIX shared-memory name (pid, sequence, device and a random nonce)
+    uint64_t host;      // the host that owns it (host_identity): a record from another host is refused
     uint64_t bytes;
 };
 static_assert(sizeof(HostHandle) == 64, "host mailbox handle record");
@@ -131,6 +132,51 @@ static bool mb_force_host() {
     return e && std::strcmp(e, "host") == 0;
 }
 
+// this host: FNV-1a of the host name and the kernel's boot id (a segment name is only meaningful on the
+// host -- and the boot -- that created it)
+static uint64_t host_identity() {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&h](const char* t, size_t n) {
+        for (size_t i = 0; i < n && t[i]; ++i) h = (h ^ (unsigned char)t[i]) * 1099511628211ull;
+    };
+    char buf[256] = {0};
+    if (gethostname(buf, sizeof(buf) - 1) == 0) mix(buf, sizeof(buf));
+    std::memset(buf, 0, sizeof(buf));
+    if (FILE* f = std::fopen("/proc/sys/kernel/random/boot_id", "r")) {
+        if (std::fgets(buf, sizeof(buf), f)) mix(buf, sizeof(buf));
+        std::fclose(f);
+    }
+    return h;
+}
+
+static uint64_t random_nonce() {
+    uint64_t v = 0;
+    if (FILE* f = std::fopen("/dev/urandom", "rb")) {
+        if (std::fread(&v, sizeof(v), 1, f) != 1) v = 0;
+        std::fclose(f);
+    }
+    return v ^ ((uint64_t)getpid() << 32) ^ (uint64_t)(uintptr_t)&v;
+}
+
+static HostHandle host_record(const nk_ctx* c) {
+    HostHandle hh{};
+    std::memcpy(hh.magic, kHostMagic, 8);
+    std::strncpy(hh.name, c->mb_host_name, sizeof(hh.name) - 1);
+    hh.host = host_identity();
+    hh.bytes = c->mb_host_bytes;
+    return hh;
+}
+
+// the 64-byte IPC handle of my device region
+static int mb_device_record(nk_ctx* c, char out[64]) {
+    NK_TRY(mb_alloc(c));
+    hipIpcMemHandle_t h;
+    NK_HIP(c, hipIpcGetMemHandle(&h, c->mb_dev));
+    static_assert(sizeof(h) == 64, "hipIpcMemHandle_t size");
+    std::memcpy(out, &h, 64);
+    return NK_OK;
+}
+
 static int mb_alloc_host(nk_ctx* c) {
     if (c->mb_host_base) return NK_OK;
     NK_HIP(c, hipSetDevice(c->device));
@@ -138,7 +184,9 @@ static int mb_alloc_host(nk_ctx* c) {
     c->halo_cap_host = (hc && *hc) ? atoll(hc) : ((int64_t)1 << 16);
     const size_t bytes = mb_region_bytes(c->halo_cap_host);
     static unsigned seq = 0;
-    std::snprintf(c->mb_host_name, sizeof(c->mb_host_name), "/nk_mb_%d_%u_%d", (int)getpid(), seq++, c->device);
+    static_assert(sizeof(HostHandle::name) <= sizeof(c->mb_host_name), "host mailbox name");
+    std::snprintf(c->mb_host_name, sizeof(HostHandle::name), "/nk_mb_%d_%u_%d_%012llx", (int)getpid(), seq++ % 1000,
+                  c->device, (unsigned long long)(random_nonce() & 0xffffffffffffull));
     const int fd = shm_open(c->mb_host_name, O_CREAT | O_EXCL | O_RDWR, 0600);
     if (fd < 0) return fail(c, NK_E_NOMEM, std::string("host mailbox: shm_open failed for ") + c->mb_host_name);
     void* p = MAP_FAILED;
@@ -204,6 +252,8 @@ void mb_free(nk_ctx* c) {
     if (c->mb_err) (void)hipHostFree(c->mb_err);
     c->mb_err = nullptr;
     c->mb_err_dev = nullptr;
+    if (c->mb_wacc) (void)hipFree(c->mb_wacc);
+    c->mb_wacc = nullptr;
 }
 
 // map a peer's host segment: its device address for my kernels
@@ -211,6 +261,8 @@ static int mb_map_host_peer(nk_ctx* c, int r, const char* rec, uint64_t** out) {
     HostHandle h;
     std::memcpy(&h, rec, sizeof(h));
     h.name[sizeof(h.name) - 1] = 0;
+    if (h.host != host_identity())  // another host's (or boot's) segment name: never open it here
+        return fail(c, NK_E_ARG, "host mailbox: rank " + std::to_string(r) + " runs on another host");
     const int fd = shm_open(h.name, O_RDWR, 0600);
     if (fd < 0) return fail(c, NK_E_HIP, "host mailbox: rank " + std::to_string(r) + "'s segment cannot be opened");
     void* p = mmap(nullptr, h.bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
@@ -335,16 +387,21 @@ static bool halo_selftest(nk_ctx* c) {
     return ok;
 }
 
-// min over ranks of a local success flag (RCCL; a context without a communicator decides alone)
+// min over ranks of a local success flag (RCCL; a context without a communicator decides alone).  Every
+// rank always enters the all-reduce -- a local failure contributes 0 -- so no peer is left in it alone.
 static bool all_ranks_ok(nk_ctx* c, bool local_ok) {
     if (!c->comm) return local_ok;
     double v = local_ok ? 1.0 : 0.0;
-    if (hipMemcpy(c->scal, &v, sizeof(double), hipMemcpyHostToDevice) != hipSuccess) return false;
+    bool wrote = hipMemcpy(c->scal, &v, sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
+    if (!wrote) {
+        (void)hipGetLastError();
+        (void)hipMemsetAsync(c->scal, 0, sizeof(double), c->stream);  // 0.0: this rank is not ok
+    }
     if (ncclAllReduce(c->scal, c->scal, 1, ncclFloat64, ncclMin, c->comm->comm, c->stream) != ncclSuccess) return false;
     if (hipMemcpyAsync(c->hpin, c->scal, sizeof(double), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
         return false;
-    return c->hpin[0] == 1.0;
+    return wrote && c->hpin[0] == 1.0;
 }
 
 static int mb_verdict(nk_ctx* c, bool local_ok) {
@@ -415,26 +472,27 @@ int nk_dist_init(nk_ctx* c, int32_t rank, int32_t nranks, const char id[128]) {
     const bool mb_want = (mbe && *mbe == '1') || (nranks > 1 && !(mbe && *mbe == '0'));
     if (mb_want && nranks <= kMbRanks) {
         // per rank: 64-byte IPC handle of the device region, 32-byte PCI bus id of its device, 64-byte
-        // record of the host region (the fallback when a peer's device is not visible here)
-        constexpr size_t kRec = 160;
+        // record of the host region (the fallback when a peer's device is not visible here), and this
+        // rank's NK_DIST_MAILBOX=host vote (one rank asking for the host mailbox moves all of them: the
+        // choice is agreed through this allgather, never taken from one rank's environment alone)
+        constexpr size_t kRec = 168;
         std::vector<char> all(kRec * nranks, 0);
         // the exchange buffer is the context's reduction scratch (allocated at nk_ctx_create), so no
         // rank can fail an allocation here and leave the others alone in the collectives below
         static_assert(kRec * kMbRanks <= sizeof(double) * kRedCap, "handle records fit one reduction slot");
         char* dbuf = reinterpret_cast<char*>(c->red);
-        const bool force_host = mb_force_host();
+        const bool force_host_here = mb_force_host();
         int rc = NK_OK;
-        if (!force_host) rc = nk_dist_mailbox_handle(c, all.data() + kRec * (size_t)rank);  // (device region)
+        // (the device handle is always produced: whether to use it is decided after the allgather)
+        rc = mb_device_record(c, all.data() + kRec * (size_t)rank);  // (device region)
         if (rc == NK_OK && hipDeviceGetPCIBusId(all.data() + kRec * (size_t)rank + 64, 32, c->device) != hipSuccess)
             rc = NK_E_HIP;
         int rch = mb_alloc_host(c);
         if (rch == NK_OK) {
-            HostHandle hh{};
-            std::memcpy(hh.magic, kHostMagic, 8);
-            std::memcpy(hh.name, c->mb_host_name, sizeof(hh.name));
-            hh.bytes = c->mb_host_bytes;
+            const HostHandle hh = host_record(c);
             std::memcpy(all.data() + kRec * (size_t)rank + 96, &hh, sizeof(hh));
         }
+        all[kRec * (size_t)rank + 160] = force_host_here ? 1 : 0;
         // allgather the IPC handles: collective, every rank takes part whatever its local state
         (void)hipMemcpy(dbuf + kRec * (size_t)rank, all.data() + kRec * (size_t)rank, kRec, hipMemcpyHostToDevice);
         const ncclResult_t ag = ncclAllGather(dbuf + kRec * (size_t)rank, dbuf, kRec, ncclChar, cm->comm, c->stream);
@@ -444,8 +502,11 @@ int nk_dist_init(nk_ctx* c, int32_t rank, int32_t nranks, const char id[128]) {
         if (ag != ncclSuccess) {
             // still join the verdict's all-reduce (the other ranks are in it), then report the failure
             (void)mb_verdict(c, false);
+            mb_host_unlink(c);
             return rccl_fail(c, ag, "ncclAllGather (mailbox handles)");
         }
+        bool force_host = false;
+        for (int r = 0; r < nranks; ++r) force_host = force_host || all[kRec * (size_t)r + 160] != 0;
         std::vector<char> handles(64 * (size_t)nranks), hhandles(64 * (size_t)nranks), busids(32 * (size_t)nranks);
         for (int r = 0; r < nranks; ++r) {
             std::memcpy(handles.data() + 64 * (size_t)r, all.data() + kRec * (size_t)r, 64);
@@ -455,6 +516,7 @@ int nk_dist_init(nk_ctx* c, int32_t rank, int32_t nranks, const char id[128]) {
         // the device regions over xGMI when every rank can map every peer's; else (all ranks together)
         // the host regions
         if (!force_host && rc == NK_OK) rc = mb_open_peers(c, rank, nranks, handles.data(), busids.data());
+        // (all_ranks_ok is entered by every rank unless the agreed vote skips it on every rank alike)
         if (force_host || !all_ranks_ok(c, rc == NK_OK)) {
             if (!force_host)
                 std::fprintf(stderr, "[nkhip] rank %d: device mailboxes not reachable by every rank (%s); host mailbox\n",
@@ -477,19 +539,11 @@ int nk_dist_mailbox_handle(nk_ctx* c, char out[64]) {
     if (!c || !out) return NK_E_ARG;
     if (mb_force_host() && !c->comm) {  // the mailbox-only transport in host memory (NK_DIST_MAILBOX=host)
         NK_TRY(mb_alloc_host(c));
-        HostHandle hh{};
-        std::memcpy(hh.magic, kHostMagic, 8);
-        std::memcpy(hh.name, c->mb_host_name, sizeof(hh.name));
-        hh.bytes = c->mb_host_bytes;
+        const HostHandle hh = host_record(c);
         std::memcpy(out, &hh, sizeof(hh));
         return NK_OK;
     }
-    NK_TRY(mb_alloc(c));
-    hipIpcMemHandle_t h;
-    NK_HIP(c, hipIpcGetMemHandle(&h, c->mb_dev));
-    static_assert(sizeof(h) == 64, "hipIpcMemHandle_t size");
-    std::memcpy(out, &h, 64);
-    return NK_OK;
+    return mb_device_record(c, out);
 }
 
 int nk_dist_mailbox_open(nk_ctx* c, int32_t rank, int32_t nranks, const char* handles) {
@@ -523,6 +577,22 @@ int nk_dist_path(nk_ctx* c, nk_path_info* out) {
     out->sweeps_resident = c->n_sweep_resident;
     out->mgs_passes = c->n_mgs_pass;
     out->mailbox_error = (c->mb_err && *(volatile int*)c->mb_err) ? 1 : 0;
+    out->jv_fd_f0r = c->n_fd_f0r;
+    out->jv_fd_f0_read = c->n_fd_f0_read;
+    if (c->mb_wacc) {  // the device's peer-wait counters (after the work enqueued so far)
+        unsigned long long w[4] = {0, 0, 0, 0};
+        NK_HIP(c, hipStreamSynchronize(c->stream));
+        NK_HIP(c, hipMemcpy(w, c->mb_wacc, sizeof(w), hipMemcpyDeviceToHost));
+        int khz = 0;  // the device wall clock's rate
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0) {
+            (void)hipGetLastError();
+            khz = 100000;  // 100 MHz, the gfx9 constant
+        }
+        out->halo_waits = (int64_t)w[1];
+        out->reduce_waits = (int64_t)w[3];
+        out->halo_wait_us = 1e3 * (double)w[0] / khz;
+        out->reduce_wait_us = 1e3 * (double)w[2] / khz;
+    }
     out->halo_cap = c->halo_cap;
     if (hipDeviceGetPCIBusId(out->pci_bus_id, (int)sizeof(out->pci_bus_id), c->device) != hipSuccess) {
         (void)hipGetLastError();

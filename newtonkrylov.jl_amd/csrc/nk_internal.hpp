@@ -43,6 +43,7 @@ struct ProfPending {
 struct ProfAcc {
     int64_t launches = 0, timed = 0;
     double ms = 0.0, bytes = 0.0, bytes_all = 0.0, dram_all = 0.0;
+    std::string kernel;  // the instantiation the class's last launch ran (stencils: StInst::name)
 };
 
 struct Comm;  // RCCL state (nk_dist.cpp)
@@ -89,6 +90,8 @@ struct nk_ctx {
     char mb_host_name[48] = {0};           //   its shared-memory name (unlinked once every peer mapped it)
     std::vector<std::pair<void*, size_t>> mb_host_maps;  // peers' segments mapped here
     int* mb_err = nullptr;                 // pinned host flag: a consumer timed out waiting for a peer
+    unsigned long long* mb_wacc = nullptr; // device counters of the peer waits (nk_path_info): halo ticks, halo
+                                           // waits, reduction ticks, reduction waits (device wall clock)
     int* mb_err_dev = nullptr;             // its device address
     unsigned mb_epoch = 1;
     int64_t halo_cap = 0;                  // doubles per inbox plane (0: no IPC halo exchange)
@@ -98,6 +101,8 @@ struct nk_ctx {
     // what actually ran (nk_dist_path): Krylov Jv launches whose v ghost planes travelled inside the
     // stencil launch / were exchanged by a separate launch first, resident sweeps, per-pass MGS launches
     int64_t n_jv_halo_fused = 0, n_jv_halo_separate = 0, n_sweep_resident = 0, n_mgs_pass = 0;
+    // FD operator launches of the built-in stencils by instantiation: F(u) recomputed (F0R) / F0 loaded
+    int64_t n_fd_f0r = 0, n_fd_f0_read = 0;
     uint64_t* res_gran = nullptr;          // partial-sum granules: 2 parities x res_blocks x 2
     int* res_err = nullptr;                // pinned host flag: a granule poll timed out
     int* res_err_dev = nullptr;
@@ -165,26 +170,35 @@ int prof_begin(nk_ctx* c, hipEvent_t* a);
 int prof_end(nk_ctx* c, int k, hipEvent_t a, double bytes);
 void prof_drain(nk_ctx* c, bool blocking);
 
-// run `launch()` (which enqueues one kernel on c->stream) under optional event timing.  bytes: the
-// kernel's algorithmic operand bytes (every load / store it must issue, served by any cache level);
-// dram: the unique-DRAM model of the same launch (each distinct operand byte once; < 0: = bytes)
+// run `f()` (which enqueues one kernel on c->stream and returns that launch's algorithmic operand bytes
+// -- every load / store it must issue, served by any cache level -- for the instantiation it actually
+// dispatched) under optional event timing.  dram: the unique-DRAM model of the same launch (each
+// distinct operand byte once; < 0: = bytes); kernel (optional): the instantiation's name for the profile
 template <typename F>
-int launch(nk_ctx* c, const char* name, double bytes, F&& f, double dram = -1.0) {
+int launch_dyn(nk_ctx* c, const char* name, F&& f, double dram = -1.0, const char* const* kernel = nullptr) {
     hipEvent_t a = nullptr;
     int k = -1;
     bool timed = false;
     if (c->prof) {
         k = kid(c, name);
-        c->acc[k].bytes_all += bytes;
-        c->acc[k].dram_all += dram < 0.0 ? bytes : dram;
         timed = (c->acc[k].launches++ % c->prof_every) == 0;
         if (timed) NK_TRY(prof_begin(c, &a));
     }
-    f();
+    const double bytes = f();
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(c, NK_E_HIP, std::string("launch ") + name + ": " + hipGetErrorString(e));
+    if (c->prof) {
+        c->acc[k].bytes_all += bytes;
+        c->acc[k].dram_all += dram < 0.0 ? bytes : dram;
+        if (kernel && *kernel) c->acc[k].kernel = *kernel;
+    }
     if (timed) NK_TRY(prof_end(c, k, a, bytes));
     return NK_OK;
+}
+// the same for a kernel whose bytes do not depend on the dispatch
+template <typename F>
+int launch(nk_ctx* c, const char* name, double bytes, F&& f, double dram = -1.0) {
+    return launch_dyn(c, name, [&] { f(); return bytes; }, dram);
 }
 
 // ---------------------------------------------------------------- reductions

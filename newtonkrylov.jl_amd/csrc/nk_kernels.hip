@@ -532,6 +532,11 @@ int mailbox_bind(nk_ctx* c) {
         // NK_MB_SPIN_LIMIT shortens it for the failure-path tests)
         const char* e = getenv("NK_MB_SPIN_LIMIT");
         m.spin_limit = (e && *e) ? (unsigned)atoll(e) : (1u << 26);
+        if (!c->mb_wacc) {  // the peer-wait counters (nk_path_info), zeroed once per context
+            NK_HIP(c, hipMalloc(reinterpret_cast<void**>(&c->mb_wacc), 4 * sizeof(unsigned long long)));
+            NK_HIP(c, hipMemset(c->mb_wacc, 0, 4 * sizeof(unsigned long long)));
+        }
+        m.wacc = c->mb_wacc;
     }
     NK_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(g_mb), &m, sizeof(m)));
     // and the copy in every stencil instantiation unit
@@ -587,6 +592,7 @@ __global__ __launch_bounds__(kBlock) void k_halo_ipc(double* __restrict__ v, int
         if (hi) __hip_atomic_store(halo_flags(g_mb.peers[rhi]) + (par * 2 + 0) * kHaloBlocks + b, epoch,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         ready = 1;
+        const uint64_t t0 = wall_clock64();
         for (int side = 0; side < 2; ++side) {
             if ((side == 0 && !lo) || (side == 1 && !hi)) continue;
             const uint64_t* f = halo_flags(g_mb.self) + (par * 2 + side) * kHaloBlocks + b;
@@ -601,6 +607,7 @@ __global__ __launch_bounds__(kBlock) void k_halo_ipc(double* __restrict__ v, int
                 __builtin_amdgcn_s_sleep(2);
             }
         }
+        wait_note(kWaitHalo, t0);
     }
     __syncthreads();
     if (!ready) return;
@@ -888,15 +895,18 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         if (nparts > kRedCap - 2) return fail(c, NK_E_ARG, "stencil grid exceeds reduction capacity");
         A.part = red_out(c, nparts, red, &A.fin);
     }
-    // algorithmic (compulsory) bytes per launch
+    // algorithmic (compulsory) bytes per launch, for the instantiation the dispatch launched (StInst: an
+    // F0R kernel reads no F0)
     const bool heat = nk_is_heat(p->kind);
-    int words = 1;  // out
-    if (in.mode == MODE_RES) words += 1 + (heat ? 1 : 0);
-    else if (in.mode == MODE_JEXACT) words += 1 + (heat ? 0 : 1);
-    else words += 3 + (heat ? 1 : 0) - (f0r ? 1 : 0);
-    if (in.epi == EPI_RESID || (in.epi == EPI_DOT && in.aux)) words += 1;
-    if (in.vout) words += 1;  // fused kdivcopy!: V_k is written
-    const double bytes = 8.0 * words * (double)g.n;
+    auto bytes_of = [&](const StInst& st) {
+        int words = 1;  // out
+        if (in.mode == MODE_RES) words += 1 + (heat ? 1 : 0);
+        else if (in.mode == MODE_JEXACT) words += 1 + (heat ? 0 : 1);
+        else words += 3 + (heat ? 1 : 0) - (st.f0r ? 1 : 0);
+        if (in.epi == EPI_RESID || (in.epi == EPI_DOT && in.aux)) words += 1;
+        if (in.vout) words += 1;  // fused kdivcopy!: V_k is written
+        return 8.0 * words * (double)g.n;
+    };
     static const char* names[3][4] = {
         {"residual", "residual_norm", "residual_dot", "residual_resid"},
         {"jv_exact", "jv_exact_sumsq", "jv_exact_dot", "jv_exact_resid"},
@@ -913,22 +923,27 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     if (in.epi == EPI_DOT && !in.aux && !in.vout) return fail(c, NK_E_ARG, "dot epilogue needs its partner");
     hipStream_t s = c->stream;
     const char* kname = epi == EPI_DOTV ? fused_names[mode] : (epi == EPI_DOTVS ? v1_names[mode] : names[mode][epi]);
-    return launch(c, kname, bytes, [&] {
+    StInst st{};
+    const char* stname = st.name;
+    const int rc = launch_dyn(c, kname, [&] {
         switch (kind) {  // one translation unit per kind (nk_stencil_inst.hip)
-        case NK_BRATU1D: stencil_kind_1(A, mode, epi, vec, grid, s, false); break;
-        case NK_BRATU2D: stencil_kind_2(A, mode, epi, vec, grid, s, false); break;
-        case NK_HEAT2D_EULER: stencil_kind_3(A, mode, epi, vec, grid, s, per); break;
-        case NK_HEAT3D_EULER: stencil_kind_4(A, mode, epi, vec, grid, s, per); break;
-        case NK_HEAT2D_MIDPOINT: stencil_kind_5(A, mode, epi, vec, grid, s, per); break;
-        case NK_HEAT3D_MIDPOINT: stencil_kind_6(A, mode, epi, vec, grid, s, per); break;
-        case NK_HEAT2D_TRAPEZOID: stencil_kind_7(A, mode, epi, vec, grid, s, per); break;
-        default: stencil_kind_8(A, mode, epi, vec, grid, s, per); break;
+        case NK_BRATU1D: st = stencil_kind_1(A, mode, epi, vec, grid, s, false); break;
+        case NK_BRATU2D: st = stencil_kind_2(A, mode, epi, vec, grid, s, false); break;
+        case NK_HEAT2D_EULER: st = stencil_kind_3(A, mode, epi, vec, grid, s, per); break;
+        case NK_HEAT3D_EULER: st = stencil_kind_4(A, mode, epi, vec, grid, s, per); break;
+        case NK_HEAT2D_MIDPOINT: st = stencil_kind_5(A, mode, epi, vec, grid, s, per); break;
+        case NK_HEAT3D_MIDPOINT: st = stencil_kind_6(A, mode, epi, vec, grid, s, per); break;
+        case NK_HEAT2D_TRAPEZOID: st = stencil_kind_7(A, mode, epi, vec, grid, s, per); break;
+        default: st = stencil_kind_8(A, mode, epi, vec, grid, s, per); break;
         }
         if (A.group > 1) {  // one-shot tiles: the group sums in tile order, as the next kernel's partials
             const int ng = (grid + A.group - 1) / A.group;
             hipLaunchKernelGGL(k_tile_fold, dim3(ng), dim3(64), 0, s, A.tpart, A.group, grid, A.part, A.fin);
         }
-    });
+        return bytes_of(st);
+    }, -1.0, &stname);
+    if (rc == NK_OK && mode == MODE_JFD) ++(st.f0r ? c->n_fd_f0r : c->n_fd_f0_read);
+    return rc;
 }
 }  // namespace
 
@@ -1393,7 +1408,7 @@ static int ilu_pipe_setup(nk_ctx* c, const nk_problem* p, int dim, IluPipe* P, i
     }
     P->prog = c->ilu_prog;
     P->err = c->ilu_err_dev;
-    P->spin = 1u << 22;
+    P->spin = 1u << 22;  // polls before a strip gives up
     int dev = 0, cus = 0;
     NK_HIP(c, hipGetDevice(&dev));
     NK_HIP(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
@@ -1446,11 +1461,22 @@ int launch_ilu0_solve(nk_ctx* c, const nk_problem* p, int dim, const double* d, 
         P.d = const_cast<double*>(d);
         P.z = z;
         P.v = v;
+        // the solve sweeps' poll limit (operational timeout): NK_ILU_SPIN_LIMIT shortens it for the
+        // failure-path tests, which must see the solve sweeps -- not the factor -- time out
+        static const unsigned spin = (unsigned)env_cfg("NK_ILU_SPIN_LIMIT", 1 << 22);
+        P.spin = spin;
         // no host sync here (it would stall every Arnoldi step that applies the preconditioner): a
         // strip that timed out sets ilu_err, the next existing sync (mb_check) reports it, and the
         // Krylov solve / nk_precond_apply redoes its work once on the level sweep (ilu_redo)
         NK_TRY(ilu_pipe_launch<1>(c, P, grid, "ilu0_forward", 24.0 * n));  // v, d in; y out
-        return ilu_pipe_launch<2>(c, P, grid, "ilu0_backward", 24.0 * n);  // y, d in; z out
+        NK_TRY(ilu_pipe_launch<2>(c, P, grid, "ilu0_backward", 24.0 * n));  // y, d in; z out
+        if (c->nranks == 1) return NK_OK;
+        // Several ranks: the recovery must stay rank-local.  Redoing the whole Krylov solve on this rank
+        // alone would re-enter reductions its peers have already moved past (the mailbox pairs them by
+        // epoch): wrong scalars or a hang.  So check now (a host sync per apply, distributed ILU(0) only)
+        // and redo this apply on the level sweep -- block Jacobi: the apply itself has no collective.
+        const int bad = ilu_pipe_failed(c);
+        if (bad <= 0) return bad;
     }
     const IluArgs I = ilu_args(p, dim);
     return launch(c, "ilu0_solve_levels", 48.0 * n, [&] {

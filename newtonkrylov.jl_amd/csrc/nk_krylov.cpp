@@ -653,7 +653,9 @@ int nk_precond_apply(nk_ctx* c, const nk_problem* p, const nk_precond* N, const 
     double dummy = 0.0;
     NK_TRY(apply_precond(c, p, N, A, g.n, z, v, false, &dummy));
     int rc = nk_sync(c);
-    if (rc != NK_OK && c->ilu_redo) {  // a pipelined ILU(0) sweep timed out: once more on the level sweep
+    // a pipelined ILU(0) sweep timed out: once more on the level sweep (one rank only -- with several, the
+    // apply recovers by itself, launch_ilu0_solve)
+    if (rc != NK_OK && c->ilu_redo && c->nranks == 1) {
         c->ilu_redo = false;
         c->err.clear();
         NK_TRY(apply_precond(c, p, N, A, g.n, z, v, false, &dummy));
@@ -752,9 +754,11 @@ int nk_krylov_solve(nk_workspace* ws, const nk_problem* p, const double* u, cons
         return fail(c, NK_E_ARG, "the device CG takes no right preconditioner (use GMRES / FGMRES)");
     int rc = (ws->algo == NK_ALGO_CG) ? cg(ws, A, b, o, st, hist, hist_cap, hist_len)
                                       : gmres(ws, p, A, b, o, st, hist, hist_cap, hist_len);
-    if (rc != NK_OK && c->ilu_redo && !ws->u_fused) {
+    if (rc != NK_OK && c->ilu_redo && !ws->u_fused && c->nranks == 1) {
         // a pipelined ILU(0) sweep timed out (reported at the step's sync, not by a sync per apply):
-        // the whole solve once more, every ILU(0) apply now on the level sweep (u is still untouched)
+        // the whole solve once more, every ILU(0) apply now on the level sweep (u is still untouched).
+        // One rank only: a redo on one rank would pair its reductions with its peers' later ones, so a
+        // distributed solve checks each apply instead (launch_ilu0_solve)
         c->ilu_redo = false;
         c->err.clear();
         (void)hipStreamSynchronize(c->stream);

@@ -10,8 +10,8 @@
 
 namespace nk {
 
-void NK_CAT(stencil_kind_, NK_ST_KIND)(const KArgs& A, int mode, int epi, int vec, int grid, hipStream_t s, bool per) {
-    go_stencil_mode<NK_ST_KIND>(A, mode, epi, vec, grid, s, per);
+StInst NK_CAT(stencil_kind_, NK_ST_KIND)(const KArgs& A, int mode, int epi, int vec, int grid, hipStream_t s, bool per) {
+    return go_stencil_mode<NK_ST_KIND>(A, mode, epi, vec, grid, s, per);
 }
 
 hipError_t NK_CAT(stencil_bind_mb_, NK_ST_KIND)(const MbInfo& m) {

@@ -55,6 +55,12 @@ struct NkPathInfo
     jv_halo_separate::Int64
     sweeps_resident::Int64
     mgs_passes::Int64
+    jv_fd_f0r::Int64
+    jv_fd_f0_read::Int64
+    halo_waits::Int64
+    reduce_waits::Int64
+    halo_wait_us::Float64
+    reduce_wait_us::Float64
 end
 function path_info(ctx::HipContext)
     r = Ref{NkPathInfo}()
@@ -64,7 +70,9 @@ function path_info(ctx::HipContext)
      mailbox = p.mailbox != 0, resident_sweep = p.resident_sweep != 0, resident_blocks = p.resident_blocks,
      halo_in_launch = p.halo_in_launch != 0, mailbox_error = p.mailbox_error != 0, halo_cap = p.halo_cap,
      pci_bus_id = String(UInt8[c for c in p.pci_bus_id if c != 0x00]), jv_halo_fused = p.jv_halo_fused,
-     jv_halo_separate = p.jv_halo_separate, sweeps_resident = p.sweeps_resident, mgs_passes = p.mgs_passes)
+     jv_halo_separate = p.jv_halo_separate, sweeps_resident = p.sweeps_resident, mgs_passes = p.mgs_passes,
+     jv_fd_f0r = p.jv_fd_f0r, jv_fd_f0_read = p.jv_fd_f0_read, halo_waits = p.halo_waits,
+     reduce_waits = p.reduce_waits, halo_wait_us = p.halo_wait_us, reduce_wait_us = p.reduce_wait_us)
 end
 
 # --------------------------------------------------------------------------- nk_problem (C layout)

@@ -91,7 +91,8 @@ def lib():
     global _lib
     if _lib is None:
         srcs = (os.path.join(HERE, "nk_oracle.c"), EXP_H)
-        if not os.path.exists(LIB_PATH) or any(os.path.getmtime(LIB_PATH) < os.path.getmtime(f) for f in srcs if os.path.exists(f)):
+        if not all(os.path.exists(f) for f in (LIB_PATH, LIBM_PATH)) or any(
+                os.path.getmtime(LIB_PATH) < os.path.getmtime(f) for f in srcs if os.path.exists(f)):
             build()
         L = C.CDLL(LIB_PATH)
         D, I64, P = C.c_double, C.c_int64, C.POINTER(C.c_double)
@@ -126,6 +127,28 @@ def lib():
         L.oc_exp_dd.restype = I64
         _lib = L
     return _lib
+
+
+LIBM_PATH = os.path.join(HERE, "_build", "libnkoracle_libm.so")
+_libm = None
+
+
+def libm_variant():
+    """The oracle built with the platform libm's exp (glibc) instead of nk_exp.h -- a cross-check of the
+    shared correctly rounded exp (tests/test_oracle.py); residual / exact JVP / FD operator only."""
+    global _libm
+    if _libm is None:
+        lib()  # (builds both)
+        if not os.path.exists(LIBM_PATH):
+            build()
+        L = C.CDLL(LIBM_PATH)
+        D, P = C.c_double, C.POINTER(C.c_double)
+        L.oc_residual.argtypes = [C.POINTER(_Problem), P, P]
+        L.oc_jv_exact.argtypes = [C.POINTER(_Problem), P, P, P]
+        L.oc_jv_fd.argtypes = [C.POINTER(_Problem), P, P, P, P, D]
+        L.oc_exp.argtypes = [C.c_int64, P, P]
+        _libm = L
+    return _libm
 
 
 def _p(a: np.ndarray):
@@ -226,20 +249,21 @@ def sin_ic(P: Problem) -> np.ndarray:
 
 
 # -- kernels -------------------------------------------------------------------------------------
-def residual(P: Problem, u: np.ndarray) -> np.ndarray:
+def residual(P: Problem, u: np.ndarray, libm: bool = False) -> np.ndarray:
+    """F!(res, u, p) (libm: with the platform exp instead of the shared correctly rounded one)."""
     u = np.ascontiguousarray(u, dtype=np.float64)
     res = np.empty_like(u)
     cp = P._c()
-    lib().oc_residual(C.byref(cp), _p(res), _p(u))
+    (libm_variant() if libm else lib()).oc_residual(C.byref(cp), _p(res), _p(u))
     return res
 
 
-def jv_exact(P: Problem, u, v) -> np.ndarray:
+def jv_exact(P: Problem, u, v, libm: bool = False) -> np.ndarray:
     u = np.ascontiguousarray(u, dtype=np.float64)
     v = np.ascontiguousarray(v, dtype=np.float64)
     out = np.empty_like(u)
     cp = P._c()
-    lib().oc_jv_exact(C.byref(cp), _p(out), _p(u), _p(v))
+    (libm_variant() if libm else lib()).oc_jv_exact(C.byref(cp), _p(out), _p(u), _p(v))
     return out
 
 
@@ -288,15 +312,15 @@ def fd_eps(unorm: float, vnorm: float) -> float:
     return lib().oc_fd_eps(unorm, vnorm)
 
 
-def jv_fd(P: Problem, u, v, F0=None, eps: float | None = None) -> np.ndarray:
+def jv_fd(P: Problem, u, v, F0=None, eps: float | None = None, libm: bool = False) -> np.ndarray:
     u = np.ascontiguousarray(u, dtype=np.float64)
     v = np.ascontiguousarray(v, dtype=np.float64)
-    F0 = residual(P, u) if F0 is None else np.ascontiguousarray(F0, dtype=np.float64)
+    F0 = residual(P, u, libm=libm) if F0 is None else np.ascontiguousarray(F0, dtype=np.float64)
     if eps is None:
         eps = fd_eps(norm(u), norm(v))
     out = np.empty_like(u)
     cp = P._c()
-    lib().oc_jv_fd(C.byref(cp), _p(out), _p(u), _p(v), _p(F0), eps)
+    (libm_variant() if libm else lib()).oc_jv_fd(C.byref(cp), _p(out), _p(u), _p(v), _p(F0), eps)
     return out
 
 

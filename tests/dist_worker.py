@@ -29,6 +29,8 @@ ap.add_argument("--tol-rel", type=float, default=1e-9, help="Newton tol_rel of t
 ap.add_argument("--krylov-itmax", type=int, default=0,
                 help="> 0: instead of the Newton solve, one restarted GMRES(10) solve J x = F(u0) with this fixed "
                      "budget (atol = rtol = 0); rank 0 saves x and the residual history")
+ap.add_argument("--precond", choices=["none", "ilu0"], default="none",
+                help="with --krylov-itmax: right preconditioner N = ilu0(J) (block Jacobi: each slab factored alone)")
 ap.add_argument("--problem", choices=["bratu", "heat_periodic", "heat3d"], default="bratu",
                 help="heat_periodic: G_Trapezoid! ∘ diffusion! with bc_periodic! -- u_n's ghost planes are "
                      "exchanged too and the slabs form a ring (rank 0 <-> rank world-1)")
@@ -157,8 +159,9 @@ if args.fault_rank >= 0:
 if args.krylov_itmax > 0:
     ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=10))
     ctx.prof_enable(1)
-    ah.krylov_solve_(ws, ah.JacobianOperator(F_, res, u, p, jv=args.jv), res, restart=True, atol=0.0, rtol=0.0,
-                     itmax=args.krylov_itmax, history=True)
+    J = ah.JacobianOperator(F_, res, u, p, jv=args.jv)
+    N = ah.ilu0(J) if args.precond == "ilu0" else None
+    ah.krylov_solve_(ws, J, res, restart=True, atol=0.0, rtol=0.0, itmax=args.krylov_itmax, history=True, N=N)
     sweeps = ctx.prof_read().get("mgs_sweep", {}).get("launches", 0)  # resident sweeps that ran
     ctx.prof_enable(0)
     parts = [None] * world

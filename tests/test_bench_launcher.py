@@ -51,6 +51,69 @@ def test_one_gpu_runs_in_process():
     assert len(got) == 1 and got[0]["world"] == 1
 
 
+def _bench_module():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _path(rank, halo_us, red_us, waits=(160, 1240), launches=10):
+    return {"rank": rank, "nranks": 8, "mailbox": 1, "halo_in_launch": 1, "mailbox_error": 0,
+            "jv_halo_fused": launches, "jv_halo_separate": 0, "halo_waits": waits[0], "reduce_waits": waits[1],
+            "halo_wait_us": halo_us, "reduce_wait_us": red_us, "launches": {"mgs_sweep": 300}}
+
+
+def test_exchange_cost_from_the_wait_counters():
+    """exchange_cost: deltas of the device's peer-wait clocks over the timed region -- launches x mean
+    end-tile wait + block 0's reduction waits, as a share of the elapsed time."""
+    b = _bench_module()
+    p0 = _path(0, 100.0, 50.0, waits=(16, 10), launches=1)
+    p1 = _path(0, 100.0 + 16 * 309 * 2.0, 50.0 + 4650 * 3.0, waits=(16 + 16 * 309, 10 + 4650), launches=1 + 309)
+    e = b.exchange_cost(p0, p1, steps=1, elapsed=0.25)
+    assert e["halo_waits"] == 16 * 309 and e["halo_launches"] == 309 and e["halo_wait_us_mean"] == 2.0
+    assert e["reduce_waits"] == 4650 and e["reduce_wait_us_mean"] == 3.0
+    assert e["exchange_us_per_step"] == round(309 * 2.0 + 4650 * 3.0, 1)
+    assert e["exchange_share"] == round((309 * 2.0 + 4650 * 3.0) * 1e-6 / 0.25, 4)
+    z = b.exchange_cost(p0, p0, steps=3, elapsed=1.0)  # one rank / no mailbox: no waits, no share
+    assert z["exchange_us_per_step"] == 0.0 and z["exchange_share"] == 0.0
+
+
+def test_eight_rank_json_assembly():
+    """The N = 8 line's multi-GPU fields, assembled on CPU from eight synthetic rank reports: the per-DoF
+    rate against config 2's single-GPU line, every rank's exchange cost, the worst rank's share."""
+    b = _bench_module()
+    paths = []
+    for r in range(8):
+        q = _path(r, 0.0, 0.0)
+        q["exchange"] = b.exchange_cost(_path(r, 0.0, 0.0, (0, 0), 0), _path(r, 16 * 309 * (1.0 + r), 4650 * 2.0,
+                                                                            (16 * 309, 4650), 309), 1, 0.3)
+        paths.append(q)
+    ref = {"value": 1264.664 * 4096 ** 2, "source": "BENCH_r04.json"}
+    out = b.scaling_fields(8 * 1000.0, 4096 * 4096, paths, "bratu2d", 0, 8, 0, ref=ref)
+    assert out["dof_rate"]["vs_config2_single_gpu"] == round(8000.0 / 1264.664, 3)
+    assert out["dof_rate"]["exchange"] == "included"
+    assert [q["rank"] for q in out["ranks"]] == list(range(8))
+    assert out["exchange"]["max_halo_wait_us_mean"] == 8.0
+    assert out["exchange"]["max_share"] == max(q["exchange"]["exchange_share"] for q in paths)
+    json.dumps(out)  # serialisable as the bench line
+    # config 4 (strong scaling, --global-n 16384): value counts global matvecs of the 16384^2 grid
+    g = b.scaling_fields(451.6, 16384 ** 2, [], "bratu2d", 8, 1, 16384, ref=ref)
+    assert g["dof_rate"]["vs_config2_single_gpu"] == round(451.6 * 16 / 1264.664, 3)  # the 5.71x ceiling
+    assert g["dof_rate"]["exchange"].startswith("none") and "ranks" not in g
+
+
+def test_config2_reference_reads_the_driver_record(tmp_path, monkeypatch):
+    b = _bench_module()
+    line = {"n_gpus": 1, "value": 1264.664, "config": {"workload": "2D Bratu 4096x4096 (4096x4096 per GPU), ..."}}
+    (tmp_path / "BENCH_r09.json").write_text(json.dumps({"run": {"stdout_tail": "noise\n" + json.dumps(line)}}))
+    monkeypatch.setattr(b, "ROOT", str(tmp_path))
+    ref = b.config2_reference()
+    assert ref["value"] == 1264.664 * 4096 ** 2 and "BENCH_r09.json" in ref["source"]
+
+
 def test_world_size_mismatch_is_an_error():
     p = run(["--gpus", "2", "--launch-probe", "0"], env={"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode == 2
@@ -75,3 +138,11 @@ def test_two_rank_bench_runs_end_to_end():
     d = json.loads(line[0])
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["matvecs_per_step"] == 309
     assert d["config"]["reductions"] in ("peer mailbox (IPC/xGMI)", "ncclAllReduce")
+    # the line judges its own exchange: every rank reports non-zero device peer waits over the timed step
+    assert len(d["ranks"]) == 2 and d["dof_rate"]["dof_matvecs_per_s"] > 0
+    if d["config"]["reductions"] == "peer mailbox (IPC/xGMI)":
+        for q in d["ranks"]:
+            e = q["exchange"]
+            assert e["reduce_waits"] > 0 and e["reduce_wait_us_mean"] > 0, e
+            assert e["halo_waits"] > 0 and e["halo_wait_us_mean"] > 0, e
+            assert 0 < e["exchange_share"] < 1, e

@@ -230,6 +230,29 @@ def test_slabs_match_oracle(tmp_path, world, transport):
         assert meta["path"]["mailbox"] and meta["path"]["mailbox_host"] == (env.get("NK_DIST_MAILBOX") == "host")
 
 
+def test_ilu0_pipeline_timeout_recovers_rank_locally(tmp_path):
+    """a pipelined ILU(0) sweep that times out on one rank of a distributed solve must recover on
+    that rank alone (the apply redone on the level sweep right away) -- a whole-solve redo on one rank would
+    pair its reductions with the peers' later ones.  Two ranks on the mailbox, block-Jacobi ILU(0) GMRES(10)
+    with a fixed budget, once normally and once with every strip poll allowed a single spin
+    (NK_ILU_SPIN_LIMIT=1: the pipelined sweeps time out and the level sweep takes over): the same iterate
+    and history bit for bit (both sweeps are bitwise the oracle's), and the timeout really happened."""
+    res = {}
+    for tag, extra in (("pipe", {}), ("timeout", {"NK_ILU_SPIN_LIMIT": "1"})):
+        out = str(tmp_path / tag)
+        env = worker_env(2, **extra)
+        rc, log = run_ranks(2, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
+                                "--nx", "64", "--ny", "512", "--krylov-itmax", "25", "--precond", "ilu0"], env)
+        assert rc == 0, log[-3000:]
+        res[tag] = (json.load(open(out + ".json")), np.load(out + ".npz"), log)
+    assert "pipelined ILU(0) sweep timed out" in res["timeout"][2]
+    assert "pipelined ILU(0) sweep timed out" not in res["pipe"][2]
+    (m0, d0, _), (m1, d1, _) = res["pipe"], res["timeout"]
+    assert m0["niter"] == m1["niter"] == 25
+    np.testing.assert_array_equal(d0["h"], d1["h"])
+    np.testing.assert_array_equal(d0["x"], d1["x"])
+
+
 @pytest.mark.parametrize("world,nx,ny,tol", [(2, 48, 40, 1e-9), (4, 64, 96, 1e-9), (8, 48, 40, 1e-9)])
 def test_slabs_fd_jv_match_oracle(tmp_path, world, nx, ny, tol):
     """BASELINE config 4's operator on slabs: the finite-difference Jv (the north-star kernel, eps from

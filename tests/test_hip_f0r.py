@@ -73,9 +73,13 @@ def solve(F, p, u0, flag, **kw):
     J = ah.JacobianOperator(F, res, u, p, jv="fd")
     u.ctx.prof_reset()
     u.ctx.prof_enable(1)
+    before = u.ctx.path_info()
     ah.krylov_solve_(ws, J, res, history=True, _f0_is_residual=flag, **kw)
+    after = u.ctx.path_info()
     prof = u.ctx.prof_read()
     u.ctx.prof_enable(0)
+    # the FD stencil launches by the instantiation that ran (nk_path_info launch counters)
+    prof["_ran"] = {k: after[k] - before[k] for k in ("jv_fd_f0r", "jv_fd_f0_read")}
     out = ws.x.to_numpy(), list(ws.stats.residuals), ws.stats.niter, prof
     ws.free()
     return out
@@ -100,20 +104,31 @@ def test_f0_recomputed_is_bitwise(ctx, name, nx, ny, bc, nz, reorth):
     assert n0 == n1 == 35
     assert h0 == h1
     np.testing.assert_array_equal(x0, x1)
-    # the flag reached the stencils the policy picks (2D heat; Bratu's V_k-storing launches; 3D
-    # G_Euler! except the V_1 step): those
-    # FD Jv launches moved 8 B/pt less
+    # the flag reached the stencils the policy picks (2D heat, zero and periodic; Bratu's V_k-storing
+    # launches; 3D G_Euler! except the V_1 step) -- judged by the instantiation that RAN: the profile
+    # names it (the F0R template flag is its last argument) and the library counts FD launches by it;
+    # the byte model follows the same instantiation (8 B/pt less exactly where F0R ran)
     jv = [k for k in p0 if k.startswith("jv_fd")]
     assert jv
-    saved = {k: (p0[k]["bytes"] - p1[k]["bytes"]) / p0[k]["timed"] / (8.0 * nx * ny * max(nz, 1)) for k in jv}
     if nz:
         uses = lambda k: name == "euler" and k != "jv_fd_dot_v1"  # noqa: E731
     elif name == "bratu2d":  # the V_k-storing launches only
         uses = lambda k: k in ("jv_fd_dot_norm", "jv_fd_dot_v1")  # noqa: E731
     else:
         uses = lambda k: True  # noqa: E731
+    stencil = "k_st3l" if nz else "k_st2d"
+    per_pos = -3 if nz else -2  # PER in k_st3l<KIND, MODE, EPI, VEC, PER, NW, F0R> / k_st2d<..., VEC, PER, F0R>
+    n_jv = sum(p0[k]["launches"] for k in jv)
+    assert p0["_ran"] == {"jv_fd_f0r": 0, "jv_fd_f0_read": n_jv}
+    assert p1["_ran"] == {"jv_fd_f0r": sum(p1[k]["launches"] for k in jv if uses(k)),
+                          "jv_fd_f0_read": sum(p1[k]["launches"] for k in jv if not uses(k))}
     for k in jv:
-        assert saved[k] == pytest.approx(1.0 if uses(k) else 0.0, abs=1e-12), (k, saved[k])
+        k0, k1 = p0[k]["kernel"], p1[k]["kernel"]
+        assert k0.startswith(f"nk::{stencil}<") and k0.endswith(", false>"), (k, k0)
+        assert k1.startswith(f"nk::{stencil}<") and k1.endswith(", true>" if uses(k) else ", false>"), (k, k1)
+        assert k1.split(",")[per_pos].strip() == ("true" if bc == "periodic" else "false"), (k, k1)
+        saved = (p0[k]["bytes"] - p1[k]["bytes"]) / p0[k]["timed"] / (8.0 * nx * ny * max(nz, 1))
+        assert saved == pytest.approx(1.0 if uses(k) else 0.0, abs=1e-12), (k, saved)
 
 
 def test_newton_uses_it_and_matches_oracle(ctx):
@@ -143,6 +158,7 @@ for name, nx, ny, bc, nz in [("bratu2d", 200, 150, "zero", 0), ("bratu2d", 201, 
     x0, h0, n0, p0 = t.solve(F, p, u0, False, **kw)
     x1, h1, n1, p1 = t.solve(F, p, u0, True, **kw)
     jv = [k for k in p0 if k.startswith("jv_fd")]
+    assert p1["_ran"]["jv_fd_f0_read"] == 0 and p1["_ran"]["jv_fd_f0r"] == sum(p1[k]["launches"] for k in jv)
     db = sum(p0[k]["bytes"] / p0[k]["timed"] * p0[k]["launches"] - p1[k]["bytes"] / p1[k]["timed"] * p1[k]["launches"] for k in jv)
     out.append(dict(same=bool(h0 == h1 and np.array_equal(x0, x1)), n=int(n1),
                     db=db / (8.0 * nx * ny * max(nz, 1) * sum(p0[k]["launches"] for k in jv))))

@@ -483,3 +483,29 @@ def test_fd_gmres_sensitivity():
     assert 0 < d_order < 1e-7, d_order
     assert d_ulp > 1e-4, d_ulp
     np.testing.assert_allclose(h3[:11], h1[:11], rtol=1e-7)  # the first cycle is still tight
+
+
+def test_bratu_operator_against_the_platform_exp():
+    """The shared correctly rounded exp (nk_exp.h, compiled by the HIP stencils AND the oracle) against the
+    platform libm's exp (glibc; faithful like Julia's Base.exp, not proven correctly rounded) in the same
+    oracle (oracle/_build/libnkoracle_libm.so): a regression in the shared exp cannot hide behind device
+    and oracle results that agree because they share it.  Bratu residual, exact JVP and FD operator within
+    the ulp bounds one faithful exp allows; exp itself at most 1 ulp apart.  Where glibc (or Base.exp)
+    misrounds, the two differ by that ulp: parity against the reference's Base.exp is unpinned there."""
+    rng = np.random.default_rng(11)
+    P = oc.bratu2d(256, 192)
+    u = oc.sin_ic(P) + 0.05 * rng.standard_normal(P.shape)
+    v = rng.standard_normal(P.shape)
+    ulp = lambda a: np.spacing(np.abs(a))  # noqa: E731
+    e_cr, e_lm = oc.exp(u.ravel()), np.exp(u.ravel())  # (numpy's exp: the platform libm too)
+    assert np.all(np.abs(e_cr - e_lm) <= ulp(e_cr))
+    nl = P.lam * np.exp(u)  # the nonlinear term, where the two exps enter
+    F_cr, F_lm = oc.residual(P, u), oc.residual(P, u, libm=True)
+    assert np.all(np.abs(F_cr - F_lm) <= 2 * ulp(nl) + ulp(F_cr))
+    J_cr, J_lm = oc.jv_exact(P, u, v), oc.jv_exact(P, u, v, libm=True)
+    assert np.all(np.abs(J_cr - J_lm) <= 2 * ulp(nl * v) + ulp(J_cr))
+    eps = 1e-7
+    D_cr, D_lm = oc.jv_fd(P, u, v, eps=eps), oc.jv_fd(P, u, v, eps=eps, libm=True)
+    w = u + eps * v
+    bound = (2 * ulp(P.lam * np.exp(w)) + ulp(F_cr + eps * v) + 2 * ulp(nl) + ulp(F_cr)) / eps + 2 * ulp(D_cr)
+    assert np.all(np.abs(D_cr - D_lm) <= bound)

@@ -1,8 +1,7 @@
 #!/bin/bash
 # One GPU-box check of the current build (run from the repo root; results in gpurun_out/check_<tag>/):
-# the -m gpu suite, smoke(), the bench as the driver runs it, then (AB=1) the heat workloads with the
-# vector start offsets off (kbench NK_ALLOC_STAGGER=0) and on.  Each GPU step has its own time limit
-# and the script stops at the first failure.
+# the -m gpu suite, smoke(), the bench as the driver runs it.  Each GPU step has its own time limit and
+# the script stops at the first failure.
 set -e -o pipefail
 T=${1:-check}
 OUT=gpurun_out/check_$T
@@ -16,9 +15,4 @@ echo "[check] bench"
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > "$OUT/bench_driver_style.log" 2>&1
 tail -n 1 "$OUT/bench_driver_style.log" > "$OUT/bench_driver_style.json"
 python3 -c "import json; d=json.load(open('$OUT/bench_driver_style.json')); print(d['value'], d['roofline']['frac'])"
-if [ "${AB:-0}" = 1 ]; then
-  WL="heat2d|heat2d --scheme trapezoid --bc periodic|heat3d|heat3d --scheme midpoint" STAGGERS="0 131072" ROUNDS=1 \
-    bash tools/ab_stagger.sh > "$OUT/ab_stagger_heat.log" 2>&1
-  cat "$OUT/ab_stagger_heat.log"
-fi
 echo "[check] done"
