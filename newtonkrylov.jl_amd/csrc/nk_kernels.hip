@@ -758,7 +758,12 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         static const int vec_pref = NK_TUNE("NK_ST_VEC", 2);
         vec = (p->nx % 2 == 0) ? 2 : 1;
         if (((fast & 4) || vec_pref == 4) && p->nx % 4 == 0 && !per) vec = 4;
-        A.tiles_x = (int)((p->nx + kBlock * vec - 1) / (kBlock * vec));
+        // overlapping wave tiles (k_st2d<..., OVL>): 62 vec output columns per wave, the halo columns in the
+        // rows' own loads instead of per-row edge loads
+        static const int ovl_env = NK_TUNE("NK_ST_OVL", 0);
+        A.ovl = (ovl_env && vec <= 2) ? 1 : 0;
+        const int64_t tw = A.ovl ? 4 * 62 * vec : kBlock * vec;  // output columns per tile
+        A.tiles_x = (int)((p->nx + tw - 1) / tw);
         // rows per tile: about 1024 tiles, between 8 and 32 rows (4096^2: 32-row tiles, FD Jv 121.3 ->
         // 114.8 us and +0.6 % on the bench, profiles/r02/ab_st_blocks.log; 8192^2 heat: 32 rows are
         // as fast as 64 for the FD Jv and 3 % faster for the residual, kbench_st2d_8192.log), and

@@ -8,8 +8,11 @@
 # Only counters `rocprofv3 -L` lists are requested; each pass holds <= 8 SQ counters.
 set -e -o pipefail
 ROOT=$(pwd)
-OUT=$ROOT/gpurun_out/pmc_insts
+OUT=$ROOT/gpurun_out/pmc_insts${PMC_SUFFIX:-}
 mkdir -p "$OUT"
+# PMC_EXPORT="NK_KBENCH_LIB=1 NK_ST_OVL=1": variables exported for the profiled runs (a kernel variant);
+# exported before rocprofv3, never an `env` hop after its `--`
+for kv in ${PMC_EXPORT:-}; do export "$kv"; done
 export TMPDIR=/tmp
 declare -A WARGS=(
     [bratu2d]="--workload bratu2d"
