@@ -758,12 +758,7 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         static const int vec_pref = NK_TUNE("NK_ST_VEC", 2);
         vec = (p->nx % 2 == 0) ? 2 : 1;
         if (((fast & 4) || vec_pref == 4) && p->nx % 4 == 0 && !per) vec = 4;
-        // overlapping wave tiles (k_st2d<..., OVL>): 62 vec output columns per wave, the halo columns in the
-        // rows' own loads instead of per-row edge loads
-        static const int ovl_env = NK_TUNE("NK_ST_OVL", 0);
-        A.ovl = (ovl_env && vec <= 2) ? 1 : 0;
-        const int64_t tw = A.ovl ? 4 * 62 * vec : kBlock * vec;  // output columns per tile
-        A.tiles_x = (int)((p->nx + tw - 1) / tw);
+        A.tiles_x = (int)((p->nx + kBlock * vec - 1) / (kBlock * vec));
         // rows per tile: about 1024 tiles, between 8 and 32 rows (4096^2: 32-row tiles, FD Jv 121.3 ->
         // 114.8 us and +0.6 % on the bench, profiles/r02/ab_st_blocks.log; 8192^2 heat: 32 rows are
         // as fast as 64 for the FD Jv and 3 % faster for the residual, kbench_st2d_8192.log), and
@@ -855,7 +850,10 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
     // second exp per point (config-4 slab Jv 277 -> 246 us, V_1 step 248 -> 227 us, bench +1.2 %),
     // while the plain Jv + dot (116 -> 122 us) and the restart residual (110 -> 126 us) do not
     // (profiles/r02/ab_f0r_bratu.log); 2 for every Bratu launch too; 0 never
-    static const int f0r_env = NK_TUNE("NK_F0R", 1);
+#ifndef NK_F0R_DEFAULT  // (product variant builds for A/B: 0 never, 2 every FD launch, 3 no 3D F0R)
+#define NK_F0R_DEFAULT 1
+#endif
+    static const int f0r_env = NK_TUNE("NK_F0R", NK_F0R_DEFAULT);
     // 3D: the F0R kernel needs 145 VGPRs (3 waves per SIMD instead of 4), which pays only where the
     // field is cheap and the kernel moves the most bytes: G_Euler!'s Jv with a dot partner (512^3
     // FD Jv + V_k store 1400 -> 1198 us), not the V_1 = r0 / beta step, not midpoint / trapezoid

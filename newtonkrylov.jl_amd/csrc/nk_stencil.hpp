@@ -40,7 +40,6 @@ struct KArgs {
     double* tpart;       // one-shot tiles with more tiles than kTileParts: per-tile partials (plain stores),
     int group;           //   folded in groups of `group` tiles by k_tile_fold right after the stencil launch
     int f0r;             // 2D FD: F0 = F(u) recomputed from the u rows already loaded (k_st2d<..., F0R>)
-    int ovl;             // 2D: overlapping wave tiles (k_st2d<..., OVL>: 62 VEC output columns per wave, no edge loads)
     // ghost planes of v through the peers' inboxes inside this launch (halo_tile_exchange): the rank
     // has a lower / upper neighbour whose boundary patch this launch fetches itself
     int hx_lo, hx_hi;
@@ -201,9 +200,6 @@ constexpr bool kKeepVdiv = false;
 #ifndef NK_ST2D_BRATU_WPE
 #define NK_ST2D_BRATU_WPE 4
 #endif
-#ifndef NK_ST2D_SERIAL_EXP
-#define NK_ST2D_SERIAL_EXP 0
-#endif
 #ifndef NK_ST2D_HEAT_CAP  // A/B: occupancy caps for the trapezoid kernels (no gain: profiles/r04/ab_trapezoid_caps.log)
 #define NK_ST2D_HEAT_CAP 0
 #endif
@@ -254,7 +250,9 @@ __device__ __forceinline__ double point_value(const KArgs& A, double c, double l
                 return y;
             }
 #endif
-#if defined(NK_ST_EXP_DIAG) && NK_ST_EXP_DIAG == 1  // A/B diagnosis builds only (wrong answers): the platform exp
+// NK_ST_EXP_DIAG (product variant builds for diagnosis only -- wrong answers): 1 the platform exp, 2 no exp,
+// the march's floor without the correctly rounded exp (profiles/r05/ab_expdiag.log)
+#if defined(NK_ST_EXP_DIAG) && NK_ST_EXP_DIAG == 1
             return exp(x);
 #elif defined(NK_ST_EXP_DIAG) && NK_ST_EXP_DIAG == 2  // no exp at all: the march's cost without it
             return x;
@@ -727,10 +725,7 @@ __device__ __forceinline__ LR x_nbrs(const KArgs& A, double cfirst, double clast
 // exactly the residual kernel's arithmetic (the u field cooked as MODE_RES, the same Laplacian and
 // point_value), so (F(w) - F(u)) / eps is bit-identical to loading the F0 that kernel stored, and
 // 8 B/pt less is read.  Valid only when F0 IS that residual of this u (the Newton loop's res).
-// OVL: overlapping wave tiles -- wave w of tile tx outputs the 62 VEC columns [c0, c0 + 62 VEC) and loads
-// [c0 - VEC, c0 + 63 VEC): lanes 0 and 63 hold the halo columns in the row's own loads, so no lane issues
-// per-row edge loads (bc_periodic!: the halo lanes' columns wrap); only lanes 1..62 store and sum.
-template <int KIND, int MODE, int EPI, int VEC, bool PER = false, bool F0R = false, bool OVL = false>
+template <int KIND, int MODE, int EPI, int VEC, bool PER = false, bool F0R = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(st2d_wpe(KIND, MODE, F0R))))
 void k_st2d(KArgs A0) {
     __shared__ double sh[kShN];
@@ -746,16 +741,10 @@ void k_st2d(KArgs A0) {
     const int t = tile_of(b, nb, A.tiles_x, A.tiles_y, A.hx_lo, A.hx_hi, A.lin);  // (lin: address order)
     const int tx = t % A.tiles_x, ty = t / A.tiles_x;
     const int64_t nx = A.nx, ny = A.ny;
-    constexpr bool kPE = PER && !OVL;  // the per-row edge slots of bc_periodic! (not with overlapping tiles)
-    constexpr int64_t kTW = OVL ? 4 * 62 * VEC : kBlock * VEC;  // output columns per tile
-    const int64_t x0 = OVL ? (int64_t)tx * kTW + (int64_t)(threadIdx.x >> 6) * (62 * VEC) - VEC + (int64_t)lane * VEC
-                           : (int64_t)tx * (kBlock * VEC) + (int64_t)threadIdx.x * VEC;
-    // act: the lane's columns hold grid values (else the zero boundary); out: the lane computes them
-    const bool act = OVL ? (PER ? x0 < nx + VEC : (x0 >= 0 && x0 < nx)) : x0 < nx;
-    const bool out = OVL ? (lane >= 1 && lane <= 62 && x0 < nx) : act;
-    // clamped (OVL + periodic: wrapped) column: every load stays inside the allocation
-    const int64_t xc = !act ? 0 : (OVL && PER ? (x0 < 0 ? x0 + nx : (x0 >= nx ? x0 - nx : x0)) : x0);
-    const XEdge xe = OVL ? XEdge{} : x_edge<VEC, PER>(lane, act, x0, nx);
+    const int64_t x0 = (int64_t)tx * (kBlock * VEC) + (int64_t)threadIdx.x * VEC;
+    const bool act = x0 < nx;
+    const int64_t xc = act ? x0 : 0;  // clamped column: every load stays inside the allocation
+    const XEdge xe = x_edge<VEC, PER>(lane, act, x0, nx);
     const int64_t de = xe.de, de2 = xe.de2;
     const bool edge_ok = xe.ok, edge_ok2 = xe.ok2;
     const int64_t y0 = (int64_t)ty * A.rows;
@@ -766,7 +755,7 @@ void k_st2d(KArgs A0) {
     if constexpr (MODE != MODE_RES && !PER) {
         const HaloTile ht{A.hx_lo && y0 == 0 && y0 < ny, A.hx_hi && y1 == ny && y0 < ny};
         if (ht.lo || ht.hi) {  // block-uniform
-            const int64_t ca = (int64_t)tx * kTW, cb = ca + kTW < nx ? ca + kTW : nx;
+            const int64_t ca = (int64_t)tx * (kBlock * VEC), cb = ca + kBlock * VEC < nx ? ca + kBlock * VEC : nx;
             if (halo_tile_exchange(A.v, nx, ny, nx, 0, 1, ca, cb, tx, ht, A.hx_epoch, A.hx_cap, kBlock)) {
                 const int par = (int)(A.hx_epoch & 1);
                 if (ht.lo) ib_lo = halo_inbox(g_mb.self, par, 0, A.hx_cap);
@@ -794,19 +783,19 @@ void k_st2d(KArgs A0) {
         // rows y0-1 (ghost plane when y0 = 0) and y0 cooked up front; row y0+1 raw in flight
         const RawRow<MODE, VEC> rm0 =
             ib_lo ? load_raw_ib<MODE, VEC, kG>(A, ib_lo, (y0 - 1) * nx + xc, xc)
-                  : load_raw<MODE, VEC, !OVL, kG, kPE, NK_ST_NTU>(A, (y0 - 1) * nx + xc, (y0 - 1) * nx + xc + de, (y0 - 1) * nx + xc + de2);
+                  : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 - 1) * nx + xc, (y0 - 1) * nx + xc + de, (y0 - 1) * nx + xc + de2);
         const RawRow<MODE, VEC> rc0 =
-            load_raw<MODE, VEC, !OVL, kG, kPE, NK_ST_NTU>(A, y0 * nx + xc, y0 * nx + xc + de, y0 * nx + xc + de2);
-        Field<VEC> fm = cook<MODE, VEC, SCH, kG, kPE>(A, rm0, act, false, false);
-        Field<VEC> fc = cook<MODE, VEC, SCH, kG, kPE>(A, rc0, act, edge_ok, edge_ok2);
+            load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, y0 * nx + xc, y0 * nx + xc + de, y0 * nx + xc + de2);
+        Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(A, rm0, act, false, false);
+        Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, rc0, act, edge_ok, edge_ok2);
         Field<VEC> um{}, uc_{};  // F0R: the u field of rows j-1, j
         if constexpr (kR) {
-            um = cook<MODE_RES, VEC, SCH, kG, kPE>(A, as_res(rm0), act, false, false);
-            uc_ = cook<MODE_RES, VEC, SCH, kG, kPE>(A, as_res(rc0), act, edge_ok, edge_ok2);
+            um = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res(rm0), act, false, false);
+            uc_ = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res(rc0), act, edge_ok, edge_ok2);
         }
         RawRow<MODE, VEC> rp =
             (ib_hi && y0 + 1 == ny) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, (y0 + 1) * nx + xc, xc)
-                                    : load_raw<MODE, VEC, !OVL, kG, kPE, NK_ST_NTU>(A, (y0 + 1) * nx + xc, (y0 + 1) * nx + xc + de, (y0 + 1) * nx + xc + de2);
+                                    : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, (y0 + 1) * nx + xc, (y0 + 1) * nx + xc + de, (y0 + 1) * nx + xc + de2);
         Row<VEC> uc{}, unc{}, f0c{}, ax{};
         {
             const int64_t o = y0 * nx + xc;
@@ -822,7 +811,7 @@ void k_st2d(KArgs A0) {
             const int64_t r2 = (j + 1 < y1) ? j + 2 : j + 1;  // (ny: the upper ghost row)
             const int64_t o2 = r2 * nx + xc;
             const RawRow<MODE, VEC> rpp = (ib_hi && r2 == ny) ? load_raw_ib<MODE, VEC, kG>(A, ib_hi, o2, xc)
-                                                              : load_raw<MODE, VEC, !OVL, kG, kPE, NK_ST_NTU>(A, o2, o2 + de, o2 + de2);
+                                                              : load_raw<MODE, VEC, true, kG, PER, NK_ST_NTU>(A, o2, o2 + de, o2 + de2);
             Row<VEC> ucn{}, uncn{}, f0cn{}, axn{};
             const int64_t o1 = (j + 1 < y1) ? o + nx : o;
             if constexpr (kU) ucn = data_row<VEC>(A.u, o1, true);
@@ -830,23 +819,23 @@ void k_st2d(KArgs A0) {
             if constexpr (kF0) f0cn = data_row<VEC, NK_ST_NT>(A.F0, o1, true);
             if constexpr (kAx) axn = data_row<VEC>(A.aux, o1, true);
             // ---- cook row j+1 (its loads were issued one iteration ago)
-            const Field<VEC> fp = cook<MODE, VEC, SCH, kG, kPE>(A, rp, act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
+            const Field<VEC> fp = cook<MODE, VEC, SCH, kG, PER>(A, rp, act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
             Field<VEC> up{};
             LR un_{};
             if constexpr (kR) {
-                up = cook<MODE_RES, VEC, SCH, kG, kPE>(A, as_res(rp), act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
-                un_ = x_nbrs<kPE>(A, uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
+                up = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res(rp), act, edge_ok && j + 1 < ny, edge_ok2 && j + 1 < ny);
+                un_ = x_nbrs<PER>(A, uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
             }
             // ---- compute row j from registers
-            const LR xn = x_nbrs<kPE>(A, fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
+            const LR xn = x_nbrs<PER>(A, fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
             const double lft = xn.l, rgt = xn.r;
             double glft = 0.0, grgt = 0.0;
             if constexpr (SCH == 2 && kG) {
-                const LR gn = x_nbrs<kPE>(A, fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
+                const LR gn = x_nbrs<PER>(A, fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
                 glft = gn.l;
                 grgt = gn.r;
             }
-            if (out) {
+            if (act) {
                 Row<VEC> val;
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) {
@@ -872,11 +861,6 @@ void k_st2d(KArgs A0) {
                     double r = point_value<KIND, MODE, XM>(A, c, lsum, uc.v[k], unk, f0, SCH == 1 ? fc.x[k] : c, lsumg, et, rare);
                     acc = epilogue<EPI>(r, EPI == EPI_DOTVS ? fc.vn[k] : ax.v[k], acc);
                     val.v[k] = r;
-#if NK_ST2D_SERIAL_EXP
-                    // A/B: the VEC points' exps one after the other (no interleaving: half the exp's live
-                    // registers, for a higher occupancy target)
-                    if constexpr (kind_bratu(KIND)) __builtin_amdgcn_sched_barrier(0);
-#endif
                 }
                 store_row<VEC>(A.out, o, val);
                 if (vout) {
@@ -1178,22 +1162,13 @@ StInst go_st1d(const KArgs& A, int grid, hipStream_t s) {
     return r;
 }
 
-template <int KIND, int MODE, int EPI, int VEC, bool PER = false, bool F0R = false, bool OVL = false>
-StInst go_st2d_i(const KArgs& A, int grid, hipStream_t s) {
-    hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, VEC, PER, F0R, OVL>), dim3(grid), dim3(kBlock), 0, s, A);
-    StInst r{};
-    snprintf(r.name, sizeof r.name, "nk::k_st2d<%d, %d, %d, %d, %s, %s, %s>", KIND, MODE, EPI, VEC, st_tf(PER),
-             st_tf(F0R), st_tf(OVL));
-    r.f0r = F0R;
-    return r;
-}
-// the row march with per-row edge loads, or (A.ovl) with overlapping wave tiles
 template <int KIND, int MODE, int EPI, int VEC, bool PER = false, bool F0R = false>
 StInst go_st2d(const KArgs& A, int grid, hipStream_t s) {
-    if constexpr (VEC <= 2) {
-        if (A.ovl) return go_st2d_i<KIND, MODE, EPI, VEC, PER, F0R, true>(A, grid, s);
-    }
-    return go_st2d_i<KIND, MODE, EPI, VEC, PER, F0R, false>(A, grid, s);
+    hipLaunchKernelGGL((k_st2d<KIND, MODE, EPI, VEC, PER, F0R>), dim3(grid), dim3(kBlock), 0, s, A);
+    StInst r{};
+    snprintf(r.name, sizeof r.name, "nk::k_st2d<%d, %d, %d, %d, %s, %s>", KIND, MODE, EPI, VEC, st_tf(PER), st_tf(F0R));
+    r.f0r = F0R;
+    return r;
 }
 
 template <int KIND, int MODE, int EPI, int VEC, bool PER, int NW, bool F0R>

@@ -117,7 +117,7 @@ def test_f0_recomputed_is_bitwise(ctx, name, nx, ny, bc, nz, reorth):
     else:
         uses = lambda k: True  # noqa: E731
     stencil = "k_st3l" if nz else "k_st2d"
-    # template arguments: k_st2d<KIND, MODE, EPI, VEC, PER, F0R, OVL> / k_st3l<KIND, MODE, EPI, VEC, PER, NW, F0R>
+    # template arguments: k_st2d<KIND, MODE, EPI, VEC, PER, F0R> / k_st3l<KIND, MODE, EPI, VEC, PER, NW, F0R>
     f0r_pos = 6 if nz else 5
 
     def targs(name):
