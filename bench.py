@@ -225,8 +225,17 @@ def config2_reference():
         try:
             with open(f) as fh:
                 rec = json.load(fh)
-            line = json.loads(rec["run"]["stdout_tail"].strip().splitlines()[-1])
-        except (OSError, KeyError, ValueError, IndexError):
+        except (OSError, ValueError):
+            continue
+        line = rec.get("parsed") if isinstance(rec.get("parsed"), dict) else None
+        if line is None:  # else the JSON line among the captured output (stderr lines may follow it)
+            tail = (rec.get("run") or {}).get("stdout_tail") or ""
+            lines = [ln for ln in tail.splitlines() if ln.startswith('{"metric"')]
+            try:
+                line = json.loads(lines[-1]) if lines else None
+            except ValueError:
+                line = None
+        if not line or "value" not in line:
             continue
         if line.get("n_gpus") == 1 and "4096x4096 (4096x4096 per GPU)" in line.get("config", {}).get("workload", ""):
             return {"value": line["value"] * 4096 ** 2, "source": f"{os.path.basename(f)}: {line['value']} matvecs/s "

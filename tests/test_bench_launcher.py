@@ -107,11 +107,18 @@ def test_eight_rank_json_assembly():
 
 def test_config2_reference_reads_the_driver_record(tmp_path, monkeypatch):
     b = _bench_module()
-    line = {"n_gpus": 1, "value": 1264.664, "config": {"workload": "2D Bratu 4096x4096 (4096x4096 per GPU), ..."}}
-    (tmp_path / "BENCH_r09.json").write_text(json.dumps({"run": {"stdout_tail": "noise\n" + json.dumps(line)}}))
+    line = {"metric": "Krylov matvecs/sec", "n_gpus": 1, "value": 1264.664,
+            "config": {"workload": "2D Bratu 4096x4096 (4096x4096 per GPU), ..."}}
+    # the driver's record: the parsed line, or the JSON line among the captured output (stderr may follow)
+    (tmp_path / "BENCH_r09.json").write_text(json.dumps({"run": {"stdout_tail": "noise\n" + json.dumps(line) +
+                                                                  "\nbench.py: cpu/gpu agreement\n"}}))
     monkeypatch.setattr(b, "ROOT", str(tmp_path))
     ref = b.config2_reference()
     assert ref["value"] == 1264.664 * 4096 ** 2 and "BENCH_r09.json" in ref["source"]
+    (tmp_path / "BENCH_r10.json").write_text(json.dumps({"parsed": dict(line, value=1300.0), "run": {}}))
+    assert b.config2_reference()["value"] == 1300.0 * 4096 ** 2
+    monkeypatch.setattr(b, "ROOT", os.path.dirname(BENCH))  # the repo's own driver records parse too
+    assert b.config2_reference() is not None
 
 
 def test_world_size_mismatch_is_an_error():
