@@ -300,6 +300,14 @@ int nk_halo_exchange(nk_ctx* ctx, const nk_problem* p, double* v);
 int nk_dist_mailbox_handle(nk_ctx* ctx, char out[64]);
 int nk_dist_mailbox_open(nk_ctx* ctx, int32_t rank, int32_t nranks, const char* handles /* nranks x 64 */);
 int nk_dist_mailbox_active(nk_ctx* ctx);  /* 1: reductions use the peer mailbox, 0: RCCL / single rank */
+/* The process grid of 3D problems (BASELINE config 5: 2 x 2 x 2 blocks): px * py * pz = nranks, rank =
+ * (iz py + iy) px + ix, every rank owning an nx x ny x nz block (global spacings, as for slabs).  The
+ * default px = py = 1 is the slab decomposition along z.  With px * py > 1 every 3D grid function carries
+ * x / y ghost faces besides its z ghost planes, exchanged with the six neighbours through the peer mailbox
+ * (packed faces, one launch); call it before allocating vectors.  bc_zero!, built-in residuals; 2D / 1D
+ * problems keep slabs.  The reference has no distributed path (examples/halovector.jl:1-45's ghost layer,
+ * on every side). */
+int nk_dist_grid(nk_ctx* ctx, int32_t px, int32_t py, int32_t pz);
 /* Which distributed path this context runs (diagnostics: bench.py prints it for every rank, so a
  * multi-GPU run names the transport it actually used).  No reference counterpart: the reference
  * has no distributed path (its ghost-cell pattern is examples/halovector.jl:1-45). */

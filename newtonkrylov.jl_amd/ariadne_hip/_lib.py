@@ -159,6 +159,7 @@ SIGNATURES = {
     "nk_dist_mailbox_open": (C.c_int, [_VP, _I32, _I32, C.c_char_p]),
     "nk_dist_mailbox_active": (C.c_int, [_VP]),
     "nk_dist_path": (C.c_int, [_VP, C.POINTER(nk_path_info)]),
+    "nk_dist_grid": (C.c_int, [_VP, _I32, _I32, _I32]),
     "nk_prof_enable": (C.c_int, [_VP, _I32]),
     "nk_prof_reset": (C.c_int, [_VP]),
     "nk_prof_read": (C.c_int, [_VP, C.POINTER(nk_prof_entry), _I32, C.POINTER(_I32)]),

@@ -96,6 +96,13 @@ class Context:
         self.check(load().nk_dist_mailbox_open(self.handle, rank, nranks, handles), "nk_dist_mailbox_open")
         self.rank, self.nranks = rank, nranks
 
+    def set_process_grid(self, px: int, py: int, pz: int):
+        """3D blocks instead of z-slabs (nk_dist_grid): px x py x pz ranks, rank = (iz py + iy) px + ix.
+        Call after the ranks are connected and before allocating any vector: a 3D grid function then
+        carries its x / y ghost faces too, exchanged with its z planes through the peer mailbox."""
+        self.check(load().nk_dist_grid(self.handle, int(px), int(py), int(pz)), "nk_dist_grid")
+        self.pgrid = (int(px), int(py), int(pz))
+
     def init_distributed(self, rank: int, nranks: int, unique_id: bytes):
         self.check(load().nk_dist_init(self.handle, rank, nranks, unique_id), "nk_dist_init")
         self.rank, self.nranks = rank, nranks
@@ -140,6 +147,7 @@ class Grid:
     shape_xyz: tuple          # local (nx,) / (nx, ny) / (nx, ny, nz)
     global_xyz: tuple         # global extents
     offset: int = 0           # first global index of this slab along the slowest axis
+    origin: tuple = None      # 3D blocks: first global (x, y, z) index of this block (None: (0, 0, offset))
 
     @staticmethod
     def full(*dims) -> "Grid":

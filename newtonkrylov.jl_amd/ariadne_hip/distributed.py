@@ -1,4 +1,5 @@
-"""Multi-GPU setup: one process per GPU, slab decomposition along the slowest axis (nk_dist.cpp).
+"""Multi-GPU setup: one process per GPU, slab decomposition along the slowest axis (nk_dist.cpp), or
+3D blocks for the 3D kinds (`block` + Context.set_process_grid: x / y ghost faces as well).
 
 torch.distributed (gloo) is only the control plane here: it broadcasts RCCL's unique id from rank 0.
 RCCL then bootstraps the data path: at nk_dist_init the ranks allgather the IPC handles of each
@@ -34,6 +35,33 @@ def slab(global_xyz, rank: int, nranks: int) -> Grid:
     sizes = [base + (1 if r < extra else 0) for r in range(nranks)]
     off = sum(sizes[:rank])
     return Grid(g[:-1] + (sizes[rank],), g, off)
+
+
+def _split(n: int, parts: int):
+    if n < parts:
+        raise ValueError("fewer points than ranks along an axis")
+    base, extra = divmod(n, parts)
+    sizes = [base + (1 if r < extra else 0) for r in range(parts)]
+    return sizes, [sum(sizes[:r]) for r in range(parts)]
+
+
+def block(global_xyz, rank: int, pgrid) -> Grid:
+    """The 3D block of `rank` in a px x py x pz process grid (Context.set_process_grid; rank =
+    (iz py + iy) px + ix): every axis split like `slab` splits z, so the blocks sharing a face share its
+    extents.  pgrid (1, 1, nranks) is `slab`."""
+    g = tuple(int(d) for d in global_xyz)
+    px, py, pz = (int(d) for d in pgrid)
+    if len(g) != 3:
+        raise ValueError("blocks are 3D")
+    if not 0 <= rank < px * py * pz:
+        raise ValueError("rank outside the process grid")
+    idx = (rank % px, (rank // px) % py, rank // (px * py))
+    shape, origin = [], []
+    for d, parts in enumerate((px, py, pz)):
+        sizes, offs = _split(g[d], parts)
+        shape.append(sizes[idx[d]])
+        origin.append(offs[idx[d]])
+    return Grid(tuple(shape), g, origin[2], tuple(origin))
 
 
 def init_distributed(ctx: Context, rank: int, nranks: int, broadcast_object) -> None:

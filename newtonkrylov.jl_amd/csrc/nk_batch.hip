@@ -447,12 +447,14 @@ int nk_jv_batched(nk_ctx* c, const nk_problem* p, int32_t k, double* const* out,
     if (k == 0) return NK_OK;
     for (int b = 0; b < k; ++b)
         if (!out[b] || !v[b]) return NK_E_ARG;
-    if (nk_is_user(p->kind)) {  // a user residual has no batched kernel: one product per column
+    Geo g{};
+    if (!nk_is_user(p->kind)) NK_TRY(geometry(c, p, &g));
+    // a user residual has no batched kernel, and 3D blocks take their x / y ghost layers from faces the
+    // batched kernel does not read: one product per column (each bit-identical to the batched form)
+    if (nk_is_user(p->kind) || blocks3d(c, g)) {
         for (int b = 0; b < k; ++b) NK_TRY(nk_jv(c, p, out[b], u, v[b], F0, mode, eps));
         return NK_OK;
     }
-    Geo g;
-    NK_TRY(geometry(c, p, &g));
     if (mode == NK_JV_FD && !F0) return fail(c, NK_E_ARG, "FD Jv needs F0 = F(u)");
     std::vector<double> e((size_t)k, eps);
     std::vector<char> zero((size_t)k, 0);

@@ -62,6 +62,10 @@ int geometry(nk_ctx* c, const nk_problem* p, Geo* g) {
         return fail(c, NK_E_ARG, "unknown boundary condition");
     }
     if (nk_is_heat(p->kind) && !p->un) return fail(c, NK_E_ARG, "heat problem needs u_n");
+    if (g->dim == 3 && c && c->px * c->py > 1) {  // 3D blocks (nk_dist_grid)
+        if (p->bc == NK_BC_PERIODIC) return fail(c, NK_E_ARG, "3D blocks: bc_zero! only (periodic problems use z-slabs)");
+        if (nk_is_user(p->kind)) return fail(c, NK_E_ARG, "3D blocks: built-in residuals only (user residuals use z-slabs)");
+    }
     g->n = p->nx * p->ny * p->nz;
     g->front = (g->plane + 31) / 32 * 32;
     return NK_OK;
@@ -270,13 +274,15 @@ int nk_vec_alloc(nk_ctx* c, const nk_problem* p, double** out) {
     // (vectors under 2 MB live in sub-allocated pools: no offset, no wasted room)
     const bool big = (size_t)g.n * sizeof(double) >= ((size_t)2 << 20);
     const size_t shift = stagger > 0 && big ? (size_t)(c->alloc_seq++ % smod) * ((size_t)stagger / 256 * 32) : 0;  // doubles
-    const size_t total = (size_t)(g.front + g.n + g.plane + 32) + shift;
+    const int64_t faces = face_words(c, p, g);  // 3D blocks: the x / y ghost faces after the trailing plane
+    const size_t total = (size_t)(g.front + g.n + g.plane + faces + 32) + shift;
     void* base = nullptr;
     if (hipMalloc(&base, total * sizeof(double)) != hipSuccess) return fail(c, NK_E_NOMEM, "hipMalloc failed (vector)");
     NK_HIP(c, hipMemsetAsync(base, 0, total * sizeof(double), c->stream));
     NK_HIP(c, hipStreamSynchronize(c->stream));
     double* interior = static_cast<double*>(base) + g.front + shift;
     c->allocs[interior] = base;
+    if (faces) c->faced.insert(interior);
     *out = interior;
     return NK_OK;
 }
@@ -287,6 +293,7 @@ int nk_vec_free(nk_ctx* c, double* v) {
     if (it == c->allocs.end()) return fail(c, NK_E_ARG, "nk_vec_free: not a vector of this context");
     NK_HIP(c, hipStreamSynchronize(c->stream));
     NK_HIP(c, hipFree(it->second));
+    c->faced.erase(v);
     c->allocs.erase(it);
     return NK_OK;
 }

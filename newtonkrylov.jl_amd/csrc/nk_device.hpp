@@ -220,10 +220,10 @@ __device__ __forceinline__ double lap(double c, double p, double m, double h2) {
 // ------------------------------------------------------------------------------ peer ghost planes
 __device__ __forceinline__ uint64_t* halo_flags(uint64_t* base) { return base + kMbWords; }
 __device__ __forceinline__ uint64_t* halo_tile_flags(uint64_t* base, int par, int side) {
-    return base + kMbWords + (size_t)2 * 2 * kHaloBlocks + (size_t)(par * 2 + side) * kHaloTileFlags;
+    return base + kMbWords + (size_t)2 * kHaloSides * kHaloBlocks + (size_t)(par * 2 + side) * kHaloTileFlags;
 }
 __device__ __forceinline__ uint64_t* halo_inbox(uint64_t* base, int par, int side, int64_t cap) {
-    return base + kMbWords + kHaloFlagWords + (size_t)(par * 2 + side) * (size_t)cap;
+    return base + kMbWords + kHaloFlagWords + (size_t)(par * kHaloSides + side) * (size_t)cap;
 }
 __device__ __forceinline__ double ld_inbox(const uint64_t* p) {
     return __longlong_as_double((long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));

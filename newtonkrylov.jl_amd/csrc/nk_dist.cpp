@@ -10,6 +10,7 @@
 #include <sys/mman.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -26,6 +27,18 @@ static int rccl_fail(nk_ctx* c, ncclResult_t r, const char* what) {
     return fail(c, NK_E_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
+// 3D blocks: rank = (iz py + iy) px + ix; side s = 2 a + hi of axis a = z, y, x (kHaloSides numbering)
+int block_nbr(const nk_ctx* c, int side) {
+    const int px = c->px, py = c->py, r = c->rank;
+    const int ix = r % px, iy = (r / px) % py, iz = r / (px * py), pz = c->nranks / (px * py);
+    const int hi = side & 1;
+    switch (side >> 1) {
+    case 0: return hi ? (iz + 1 < pz ? r + px * py : -1) : (iz > 0 ? r - px * py : -1);
+    case 1: return hi ? (iy + 1 < py ? r + px : -1) : (iy > 0 ? r - px : -1);
+    default: return hi ? (ix + 1 < px ? r + 1 : -1) : (ix > 0 ? r - 1 : -1);
+    }
+}
+
 // bc_periodic! (heat_2D.jl:15-26) along the slab axis makes the slabs a ring: the lone slab wraps
 // onto itself (a local copy), rank 0's lower neighbour is rank nranks-1 and vice versa.
 int halo_exchange(nk_ctx* c, const nk_problem* p, const double* v) {
@@ -34,6 +47,13 @@ int halo_exchange(nk_ctx* c, const nk_problem* p, const double* v) {
     Geo g;
     NK_TRY(geometry(c, p, &g));
     double* vv = const_cast<double*>(v);  // only the ghost planes are written
+    if (blocks3d(c, g)) {  // 3D blocks: all six ghost layers, through the peer mailbox
+        if (!c->faced.count(vv)) return fail(c, NK_E_STATE, "3D blocks: a vector allocated before nk_dist_grid has no ghost faces");
+        if (!c->mb_on) return fail(c, NK_E_STATE, "3D blocks exchange their ghost faces through the peer mailbox (it is off)");
+        const int64_t big = std::max({p->nx * p->ny, p->nx * p->nz, p->ny * p->nz});
+        if (big > c->halo_cap) return fail(c, NK_E_ARG, "3D blocks: a ghost face is larger than the IPC inbox (NK_HALO_CAP)");
+        return launch_faces_ipc(c, vv, p);
+    }
     if (ring && c->nranks <= 1) return launch_periodic_fill(c, vv, g.plane, g.nplanes);
     if (!c->comm && !c->mb_on) return NK_OK;
     if (c->mb_on && g.plane <= c->halo_cap) return launch_halo_ipc(c, vv, g.plane, g.nplanes, ring);
@@ -84,7 +104,7 @@ int allreduce_scalar(nk_ctx* c, double* dev, int64_t count) {
 // nk_dist_init, verified by a self-test whose verdict all ranks agree on; any failure falls back
 // to the RCCL all-reduce.
 static size_t mb_region_bytes(int64_t cap) {
-    return sizeof(uint64_t) * (kMbWords + kHaloFlagWords) + sizeof(double) * 4 * (size_t)cap;
+    return sizeof(uint64_t) * (kMbWords + kHaloFlagWords) + sizeof(double) * 2 * kHaloSides * (size_t)cap;
 }
 
 static int mb_alloc_err(nk_ctx* c) {
@@ -558,6 +578,17 @@ int nk_dist_mailbox_open(nk_ctx* c, int32_t rank, int32_t nranks, const char* ha
 }
 
 int nk_dist_mailbox_active(nk_ctx* c) { return (c && c->mb_on) ? 1 : 0; }
+
+int nk_dist_grid(nk_ctx* c, int32_t px, int32_t py, int32_t pz) {
+    if (!c || px < 1 || py < 1 || pz < 1) return NK_E_ARG;
+    if ((int64_t)px * py * pz != c->nranks)
+        return fail(c, NK_E_ARG, "nk_dist_grid: px * py * pz must equal the number of ranks");
+    if (!c->allocs.empty() && (px * py > 1) != (c->px * c->py > 1))
+        return fail(c, NK_E_STATE, "nk_dist_grid: set the process grid before allocating vectors");
+    c->px = px;
+    c->py = py;
+    return NK_OK;
+}
 
 int nk_dist_path(nk_ctx* c, nk_path_info* out) {
     if (!c || !out) return NK_E_ARG;

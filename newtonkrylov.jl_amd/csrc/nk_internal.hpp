@@ -10,6 +10,7 @@
 #include <map>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "nkhip.h"
@@ -55,6 +56,7 @@ struct nk_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     std::unordered_map<double*, void*> allocs;  // interior pointer -> allocation base
+    std::unordered_set<double*> faced;          // 3D blocks: the vectors that carry x / y ghost faces
     unsigned alloc_seq = 0;                     // vectors allocated so far (their start offsets, §3)
     double* red = nullptr;                      // kRedSlots * kRedCap partial sums
     double* scal = nullptr;                     // kScalCap device scalars
@@ -117,8 +119,10 @@ struct nk_ctx {
     bool ilu_redo = false;                 // a pipelined ILU(0) sweep timed out: the caller redoes its work (level sweep)
     int* ilu_err_dev = nullptr;
     bool ilu_pipe_ok = true;               // false after a progress poll timed out: the one-work-group sweep
-    // distribution
+    // distribution: nranks = px * py * pz ranks; px = py = 1 (the default) is the slab decomposition along the
+    // slowest axis, otherwise 3D problems are split into blocks (rank = (iz py + iy) px + ix, nk_dist_grid)
     int rank = 0, nranks = 1;
+    int px = 1, py = 1;
     nk::Comm* comm = nullptr;
 };
 
@@ -234,18 +238,22 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
 constexpr int kMbSlots = 256;                // mailbox ring (epoch % kMbSlots)
 constexpr int kMbRanks = 32;                 // max ranks of the mailbox all-reduce (2 granules each: one wave polls them all)
 constexpr int kHaloBlocks = 64;              // blocks (= flags per side) of the IPC ghost-plane exchange
+constexpr int kHaloSides = 6;                // ghost layers by the side they come from: 0 / 1 the slowest axis's lower /
+                                             // upper neighbour (slabs; z of 3D blocks), 2 / 3 y, 4 / 5 x (3D blocks)
 constexpr int kHaloTileFlags = 4096;         // stencil tiles per plane whose ghost patch travels in the stencil itself
 // one fine-grained region per rank, IPC-mapped by every other rank:
-//   [mailbox: kMbSlots x kMbRanks x 2 u64][halo flags: 2 parity x 2 sides x kHaloBlocks u64]
+//   [mailbox: kMbSlots x kMbRanks x 2 u64][halo flags: 2 parity x kHaloSides x kHaloBlocks u64]
 //   [tile flags: 2 parity x 2 sides x kHaloTileFlags u64]
-//   [halo inbox: 2 parity x 2 sides x halo_cap doubles]   (side 0: from the lower rank, 1: from the upper)
+//   [halo inbox: 2 parity x kHaloSides x halo_cap doubles]   (side 0: from the lower rank, 1: from the upper, ...)
 constexpr size_t kMbWords = (size_t)2 * kMbSlots * kMbRanks;
-constexpr size_t kHaloFlagWords = (size_t)2 * 2 * (kHaloBlocks + kHaloTileFlags);
+constexpr size_t kHaloFlagWords = (size_t)2 * kHaloSides * kHaloBlocks + (size_t)2 * 2 * kHaloTileFlags;
 int mailbox_bind(nk_ctx* c);                 // make c's mailbox the one the kernels use (nk_kernels.hip)
 int mailbox_selftest(nk_ctx* c, bool* ok);   // a few epochs through the mailbox vs the expected sums
 // ghost planes of v (interior pointer, `plane` doubles per plane, `nplanes` planes) through the peer
 // inboxes: push my boundary planes into the neighbours' inboxes, pull theirs into my ghost planes
 int launch_halo_ipc(nk_ctx* c, double* v, int64_t plane, int64_t nplanes, bool ring);
+// 3D blocks: the six ghost layers of v (z planes in the allocation, x / y faces after it) through the inboxes
+int launch_faces_ipc(nk_ctx* c, double* v, const nk_problem* p);
 int launch_periodic_fill(nk_ctx* c, double* v, int64_t plane, int64_t nplanes);
 
 // ---------------------------------------------------------------- kernel launchers (nk_kernels.hip)
@@ -327,6 +335,15 @@ inline int nk_scheme(int kind) {
 }
 
 // ---------------------------------------------------------------- distribution (nk_dist.cpp)
+// 3D blocks (nk_dist_grid with px * py > 1): a 3D grid function's allocation carries, after its trailing
+// z ghost plane, the four x / y ghost faces the neighbours' boundary layers are exchanged into:
+//   [y-lo: nx nz][y-hi: nx nz][x-lo: ny nz][x-hi: ny nz]   (y faces indexed k nx + i, x faces k ny + j)
+inline bool blocks3d(const nk_ctx* c, const Geo& g) { return g.dim == 3 && c->px * c->py > 1; }
+inline int64_t face_words(const nk_ctx* c, const nk_problem* p, const Geo& g) {
+    return blocks3d(c, g) ? 2 * (p->nx + p->ny) * p->nz : 0;
+}
+// the neighbour rank on side s (kHaloSides numbering) of a 3D block, -1 at a physical boundary
+int block_nbr(const nk_ctx* c, int side);
 int halo_exchange(nk_ctx* c, const nk_problem* p, const double* v);
 // ghost planes of u_n when the residual reads its neighbours (G_Midpoint!, G_Trapezoid!)
 int exchange_un(nk_ctx* c, const nk_problem* p);

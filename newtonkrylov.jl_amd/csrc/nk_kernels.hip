@@ -587,15 +587,15 @@ __global__ __launch_bounds__(kBlock) void k_halo_ipc(double* __restrict__ v, int
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every thread drains its stores before the flag
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (lo) __hip_atomic_store(halo_flags(g_mb.peers[rlo]) + (par * 2 + 1) * kHaloBlocks + b, epoch,
+        if (lo) __hip_atomic_store(halo_flags(g_mb.peers[rlo]) + (par * kHaloSides + 1) * kHaloBlocks + b, epoch,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (hi) __hip_atomic_store(halo_flags(g_mb.peers[rhi]) + (par * 2 + 0) * kHaloBlocks + b, epoch,
+        if (hi) __hip_atomic_store(halo_flags(g_mb.peers[rhi]) + (par * kHaloSides + 0) * kHaloBlocks + b, epoch,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         ready = 1;
         const uint64_t t0 = wall_clock64();
         for (int side = 0; side < 2; ++side) {
             if ((side == 0 && !lo) || (side == 1 && !hi)) continue;
-            const uint64_t* f = halo_flags(g_mb.self) + (par * 2 + side) * kHaloBlocks + b;
+            const uint64_t* f = halo_flags(g_mb.self) + (par * kHaloSides + side) * kHaloBlocks + b;
             unsigned spins = 0;
             while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
                 if (++spins > g_mb.spin_limit ||
@@ -621,6 +621,88 @@ __global__ __launch_bounds__(kBlock) void k_halo_ipc(double* __restrict__ v, int
         for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
             v[nplanes * plane + i] =
                 __longlong_as_double((long long)__hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    }
+}
+
+// 3D blocks (nk_dist_grid): the six ghost layers of v through the peers' inboxes in ONE launch (packed
+// faces).  Block b owns chunk b of every face: it pushes my boundary layer on each side s that has a
+// neighbour into that neighbour's inbox for side s ^ 1 (system-scope stores), drains, raises its flag
+// there, waits for the neighbours' block-b flags in my region and unpacks their layers -- the z ones into
+// my ghost planes, the x / y ones into the faces after the allocation's trailing plane.  Neighbours share
+// the face's extents, and the grid is always kHaloBlocks blocks, so both sides cut a face alike.  At a
+// physical boundary the layer stays zero (zero-filled allocation, never written there).
+struct FaceArgs {
+    int64_t nx, ny, nz;
+    int64_t fy, fx;  // offsets of the y-lo / x-lo faces from the interior pointer
+    int nbr[kHaloSides];
+};
+__device__ __forceinline__ int64_t face_len(const FaceArgs& F, int s) {
+    return s < 2 ? F.nx * F.ny : (s < 4 ? F.nx * F.nz : F.ny * F.nz);
+}
+// element i of my boundary layer on side s: planes (k fastest-y-x order of a plane), y faces k nx + x,
+// x faces k ny + j
+__device__ __forceinline__ int64_t face_src(const FaceArgs& F, int s, int64_t i) {
+    const int64_t pl = F.nx * F.ny;
+    if (s == 0) return i;
+    if (s == 1) return (F.nz - 1) * pl + i;
+    if (s < 4) return (i / F.nx) * pl + (s == 2 ? 0 : F.ny - 1) * F.nx + i % F.nx;
+    return (i / F.ny) * pl + (i % F.ny) * F.nx + (s == 4 ? 0 : F.nx - 1);
+}
+// where element i of the layer from side s lands in my allocation
+__device__ __forceinline__ int64_t face_dst(const FaceArgs& F, int s, int64_t i) {
+    const int64_t pl = F.nx * F.ny;
+    if (s == 0) return i - pl;
+    if (s == 1) return F.nz * pl + i;
+    if (s < 4) return F.fy + (s == 3 ? F.nx * F.nz : 0) + i;
+    return F.fx + (s == 5 ? F.ny * F.nz : 0) + i;
+}
+__global__ __launch_bounds__(kBlock) void k_faces_ipc(double* __restrict__ v, FaceArgs F, uint64_t epoch, int64_t cap) {
+    __shared__ int ready;
+    const int b = blockIdx.x, G = gridDim.x;
+    const int par = (int)(epoch & 1);
+    for (int s = 0; s < kHaloSides; ++s) {
+        if (F.nbr[s] < 0) continue;
+        const int64_t len = face_len(F, s), per = (len + G - 1) / G;
+        const int64_t c0 = (int64_t)b * per, c1 = c0 + per < len ? c0 + per : len;
+        uint64_t* dst = halo_inbox(g_mb.peers[F.nbr[s]], par, s ^ 1, cap);
+        for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
+            __hip_atomic_store(dst + i, (uint64_t)__double_as_longlong(v[face_src(F, s, i)]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every thread drains its stores before the flags
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int s = 0; s < kHaloSides; ++s)
+            if (F.nbr[s] >= 0)
+                __hip_atomic_store(halo_flags(g_mb.peers[F.nbr[s]]) + (par * kHaloSides + (s ^ 1)) * kHaloBlocks + b, epoch,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ready = 1;
+        const uint64_t t0 = wall_clock64();
+        for (int s = 0; s < kHaloSides; ++s) {
+            if (F.nbr[s] < 0) continue;
+            const uint64_t* f = halo_flags(g_mb.self) + (par * kHaloSides + s) * kHaloBlocks + b;
+            unsigned spins = 0;
+            while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+                if (++spins > g_mb.spin_limit ||
+                    ((spins & 255) == 0 && __hip_atomic_load(g_mb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
+                    __hip_atomic_store(g_mb.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    ready = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        wait_note(kWaitHalo, t0);
+    }
+    __syncthreads();
+    if (!ready) return;
+    for (int s = 0; s < kHaloSides; ++s) {
+        if (F.nbr[s] < 0) continue;
+        const int64_t len = face_len(F, s), per = (len + G - 1) / G;
+        const int64_t c0 = (int64_t)b * per, c1 = c0 + per < len ? c0 + per : len;
+        const uint64_t* src = halo_inbox(g_mb.self, par, s, cap);
+        for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
+            v[face_dst(F, s, i)] = __longlong_as_double((long long)__hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     }
 }
 
@@ -659,6 +741,27 @@ int launch_halo_ipc(nk_ctx* c, double* v, int64_t plane, int64_t nplanes, bool r
     return launch(c, "halo_ipc", 16.0 * plane * nbrs, [&] {
         hipLaunchKernelGGL(k_halo_ipc, dim3(nb), dim3(kBlock), 0, c->stream, v, plane, nplanes, epoch, c->halo_cap,
                            ring ? 1 : 0);
+    });
+}
+
+int launch_faces_ipc(nk_ctx* c, double* v, const nk_problem* p) {
+    Geo g;
+    NK_TRY(geometry(c, p, &g));
+    FaceArgs F{};
+    F.nx = p->nx;
+    F.ny = p->ny;
+    F.nz = p->nz;
+    F.fy = g.n + g.plane;
+    F.fx = F.fy + 2 * p->nx * p->nz;
+    double bytes = 0.0;
+    for (int s = 0; s < kHaloSides; ++s) {
+        F.nbr[s] = block_nbr(c, s);
+        if (F.nbr[s] >= 0) bytes += 16.0 * (double)(s < 2 ? p->nx * p->ny : (s < 4 ? p->nx * p->nz : p->ny * p->nz));
+    }
+    if (bytes == 0.0) return NK_OK;
+    const uint64_t epoch = ++c->halo_epoch;
+    return launch(c, "halo_faces", bytes, [&] {
+        hipLaunchKernelGGL(k_faces_ipc, dim3(kHaloBlocks), dim3(kBlock), 0, c->stream, v, F, epoch, c->halo_cap);
     });
 }
 
@@ -807,6 +910,13 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         }
     } else {
         vec = (p->nx % 2 == 0) ? 2 : 1;
+        if (blocks3d(c, g)) {  // 3D blocks: x / y ghost layers from the faces after the trailing plane
+            A.blk = 1;
+            A.fy = g.n + g.plane;
+            A.fx = A.fy + 2 * p->nx * p->nz;
+            for (int sd = 2; sd < kHaloSides; ++sd)
+                if (block_nbr(c, sd) >= 0) A.nbm |= 1 << sd;
+        }
         // rows per 3D tile and the y-neighbour path (k_st3d loads, k_st3l LDS); fast bits 8 / 16 select
         // k_st3l with 4 / 8 rows (kernel-variant bench), NK_ST3_LDS / NK_ST3_NW likewise
         // k_st3l with 4-row tiles is the default: +6-16 % over k_st3d on every 3D kind / mode at 512^3
@@ -815,6 +925,10 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         static const int nw_env = NK_TUNE("NK_ST3_NW", 4);
         A.lds3 = (fast & 24) ? 1 : lds_env;
         A.nw = A.lds3 ? ((fast & 8) ? 4 : ((fast & 16) ? 8 : (nw_env == 4 ? 4 : 8))) : 4;
+        if (A.blk) {  // 3D blocks: k_st3l with 4-row tiles (the kernel-variant build's other forms have no faces)
+            A.lds3 = 1;
+            A.nw = 4;
+        }
         A.tiles_x = (int)((p->nx + 64 * vec - 1) / (64 * vec));
         A.tiles_y = (int)((p->ny + A.nw - 1) / A.nw);
         static const int target = NK_TUNE("NK_ST3_BLOCKS", 8192);  // shorter z-marches keep y-adjacent tiles in step (L2 reuse of the halo rows)
@@ -829,12 +943,12 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         // odd z-chunks marching down, 2 plane-major + odd chunks down, 3 chunk pairs): within +-3 % of the
         // plane-major order, upward marches (0, the product) -- profiles/r03/ab_zalt*.log
         static const int zalt_env = NK_TUNE("NK_ST3_ZALT", 0);
-        A.zalt = (A.lds3 && !(fast & 65536)) ? zalt_env : 0;  // kbench fast bit 65536: the plane-major order
+        A.zalt = (A.lds3 && !(fast & 65536) && !A.blk) ? zalt_env : 0;  // kbench fast bit 65536: the plane-major order
         // the y-march (k_st3y, kbench NK_ST3_YMARCH=1: slabs short along z; NK_ST3Y_ROWS rows per chunk):
         // tiles of nw planes x 64 vec columns marching a chunk of rows
         static const int ym_env = NK_TUNE("NK_ST3_YMARCH", 0);
         static const int ym_rows = NK_TUNE("NK_ST3Y_ROWS", 64);
-        A.ym = (A.lds3 && (ym_env || (fast & 524288)) && rows_override <= 0 && !A.zalt) ? 1 : 0;  // (bit 2^19: the y-march)
+        A.ym = (A.lds3 && (ym_env || (fast & 524288)) && rows_override <= 0 && !A.zalt && !A.blk) ? 1 : 0;  // (bit 2^19: the y-march)
         if (A.ym) {
             const int64_t r = std::min<int64_t>(std::max(1, ym_rows), p->ny);
             A.rows = (int)r;
@@ -871,7 +985,7 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         const int fuse_env = halo_fuse_knob();
         const int64_t tiles_pl = g.dim == 2 ? A.tiles_x : (int64_t)A.tiles_x * A.tiles_y;
         const bool self = halo_self_ring(c);
-        const bool fuse = fuse_env && c->mb_on && (c->nranks > 1 || self) && !per && in.mode != MODE_RES &&
+        const bool fuse = fuse_env && c->mb_on && (c->nranks > 1 || self) && !per && !A.blk && in.mode != MODE_RES &&
                           (g.dim == 2 || (g.dim == 3 && A.lds3)) && g.plane <= c->halo_cap && tiles_pl <= kHaloTileFlags;
         if (fuse) {
             ++c->n_jv_halo_fused;

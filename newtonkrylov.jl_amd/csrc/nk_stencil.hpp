@@ -40,6 +40,9 @@ struct KArgs {
     double* tpart;       // one-shot tiles with more tiles than kTileParts: per-tile partials (plain stores),
     int group;           //   folded in groups of `group` tiles by k_tile_fold right after the stencil launch
     int f0r;             // 2D FD: F0 = F(u) recomputed from the u rows already loaded (k_st2d<..., F0R>)
+    int blk;             // 3D blocks (k_st3l<..., BLK>): x / y ghost layers from the faces at fy / fx
+    int nbm;             //   bit s: side s (kHaloSides numbering) has a neighbour
+    int64_t fy, fx;      //   offsets of the y-lo / x-lo faces from the interior pointer
     // ghost planes of v through the peers' inboxes inside this launch (halo_tile_exchange): the rank
     // has a lower / upper neighbour whose boundary patch this launch fetches itself
     int hx_lo, hx_hi;
@@ -916,7 +919,11 @@ void k_st2d(KArgs A0) {
 #ifndef NK_ST3L_WPE
 #define NK_ST3L_WPE(KIND, EPI, F0R) ((KIND == NK_HEAT3D_EULER && EPI == EPI_DOT && F0R) ? 4 : 1)
 #endif
-template <int KIND, int MODE, int EPI, int VEC, bool PER = false, int NW = 8, bool F0R = false>
+// BLK (3D blocks, nk_dist_grid): the x / y ghost layers come from the faces after the allocation's trailing
+// plane (KArgs::fy / fx, sides with a neighbour in KArgs::nbm) -- the left / right x-edges of the block's
+// first / last column through the edge slots (the right one as the periodic wrap's second slot), the halo
+// rows beyond the block's first / last row from the y faces; z keeps the ghost planes.
+template <int KIND, int MODE, int EPI, int VEC, bool PER = false, int NW = 8, bool F0R = false, bool BLK = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L_WPE(KIND, EPI, F0R)))) void k_st3l(KArgs A0) {
     __shared__ double sh[kShN];
     const double* const et = nullptr;  // heat kinds: no exp
@@ -942,6 +949,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L
     const int64_t j = (int64_t)ty * NW + wv;
     const bool act = x0 < nx && j < ny;
     const int64_t oj = (act ? j * nx + x0 : 0);
+    constexpr bool kE2 = PER || BLK;  // the second x-edge slot: the periodic wrap, or a block's x-hi face
+    // BLK: this lane's x-edges / this wave's halo rows from the faces (a neighbour on that side)
+    const bool fxl = BLK && (A.nbm & 16) && lane == 0 && act && x0 == 0;
+    const bool fxr = BLK && (A.nbm & 32) && act && x0 + VEC == nx;
+    const bool fyn = BLK && (A.nbm & 8) && act && j + 1 == ny;
+    const bool fys = BLK && (A.nbm & 4) && act && j == 0;
     // y-neighbours: from the adjacent wave's LDS row when it is in this tile, else a halo-row load
     const bool lds_n = wv + 1 < NW && j + 1 < ny;
     const bool lds_s = wv >= 1;
@@ -953,13 +966,23 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L
         dn_ = !act ? 0 : (j + 1 < ny ? nx : -(ny - 1) * nx);
         ds = !act ? 0 : (j >= 1 ? -nx : (ny - 1) * nx);
     } else {
-        has_n = act && j + 1 < ny;
-        has_s = act && j >= 1;
-        dn_ = has_n ? nx : 0;
-        ds = has_s ? -nx : 0;
+        has_n = act && (j + 1 < ny || fyn);
+        has_s = act && (j >= 1 || fys);
+        dn_ = has_n && !fyn ? nx : 0;
+        ds = has_s && !fys ? -nx : 0;
     }
     const bool ld_n = !lds_n && has_n, ld_s = !lds_s && has_s;  // wave-uniform
-    const XEdge xe = x_edge<VEC, PER>(lane, act, x0, nx);
+    XEdge xe{};
+    if constexpr (BLK) {  // in-array edges inside the block, faces at its x-ends
+        const bool lin = lane == 0 && act && x0 >= 1, rin = lane == 63 && act && x0 + VEC < nx;
+        xe.de = lin ? -1 : 0;
+        xe.ok = lin || fxl;
+        xe.de2 = rin ? VEC : 0;
+        xe.ok2 = rin || fxr;
+        xe.rwrap = fxr;
+    } else {
+        xe = x_edge<VEC, PER>(lane, act, x0, nx);
+    }
     const int64_t de = xe.de, de2 = xe.de2;
     const bool edge_ok = xe.ok, edge_ok2 = xe.ok2;
     const int64_t z0 = (int64_t)tz * A.rows;
@@ -980,7 +1003,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L
     // ghost planes of v from the neighbours' patches, fetched by this launch (z-tiles at the slab's ends)
     const uint64_t* ib_lo = nullptr;
     const uint64_t* ib_hi = nullptr;
-    if constexpr (MODE != MODE_RES && !PER) {
+    if constexpr (MODE != MODE_RES && !PER && !BLK) {
         const HaloTile ht{A.hx_lo && z0 == 0 && z0 < nz, A.hx_hi && z1 == nz && z0 < nz};
         if (ht.lo || ht.hi) {  // block-uniform
             const int64_t ra = (int64_t)ty * NW, rb = ra + NW < ny ? ra + NW : ny;
@@ -995,28 +1018,34 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L
     double acc = 0.0;
     // a plane ahead of the march (plane kk at offset o): the neighbour's patch from the inbox for a
     // ghost plane fetched in this launch, else memory
+    // the x-edge offsets of plane kk (BLK: the faces for the block's end columns of an interior plane)
+    auto eo1 = [&](int64_t kk, int64_t o) { return (fxl && kk >= 0 && kk < nz) ? A.fx + kk * ny + j : o + de; };
+    auto eo2 = [&](int64_t kk, int64_t o) { return (fxr && kk >= 0 && kk < nz) ? A.fx + ny * nz + kk * ny + j : o + de2; };
+    // the halo rows of plane kk beyond the tile (BLK: the y faces beyond the block's first / last row)
+    auto nrow = [&](int64_t kk, int64_t o) { return fyn ? A.fy + nx * nz + kk * nx + x0 : o + dn_; };
+    auto srow = [&](int64_t kk, int64_t o) { return fys ? A.fy + kk * nx + x0 : o + ds; };
     auto ahead = [&](int64_t kk, int64_t o) {
         const uint64_t* ib = (ib_hi && kk == nz) ? ib_hi : ((ib_lo && kk == -1) ? ib_lo : nullptr);
-        return ib ? load_raw_ib<MODE, VEC, kG>(A, ib, o, oj) : load_raw<MODE, VEC, true, kG, PER>(A, o, o + de, o + de2);
+        return ib ? load_raw_ib<MODE, VEC, kG>(A, ib, o, oj) : load_raw<MODE, VEC, true, kG, kE2>(A, o, eo1(kk, o), eo2(kk, o));
     };
     if (z0 < nz) {
         const int64_t o0 = zs * pl + oj;
         const int64_t kb = zs - dz;  // the plane behind the first
         const uint64_t* ibb = (ib_lo && kb == -1) ? ib_lo : ((ib_hi && kb == nz) ? ib_hi : nullptr);
         const RawRow<MODE, VEC> rm0 =
-            ibb ? load_raw_ib<MODE, VEC, kG>(A, ibb, o0 - st, oj) : load_raw<MODE, VEC, false, kG, PER>(A, o0 - st, 0);
-        const RawRow<MODE, VEC> rc0 = load_raw<MODE, VEC, true, kG, PER>(A, o0, o0 + de, o0 + de2);
-        Field<VEC> fm = cook<MODE, VEC, SCH, kG, PER>(A, rm0, act, false);
-        Field<VEC> fc = cook<MODE, VEC, SCH, kG, PER>(A, rc0, act, edge_ok, edge_ok2);
+            ibb ? load_raw_ib<MODE, VEC, kG>(A, ibb, o0 - st, oj) : load_raw<MODE, VEC, false, kG, kE2>(A, o0 - st, 0);
+        const RawRow<MODE, VEC> rc0 = load_raw<MODE, VEC, true, kG, kE2>(A, o0, eo1(zs, o0), eo2(zs, o0));
+        Field<VEC> fm = cook<MODE, VEC, SCH, kG, kE2>(A, rm0, act, false);
+        Field<VEC> fc = cook<MODE, VEC, SCH, kG, kE2>(A, rc0, act, edge_ok, edge_ok2);
         Field<VEC> um{}, uc_{};  // F0R: the u field of planes k-1, k
         if constexpr (kR) {
-            um = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rm0), act, false);
-            uc_ = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rc0), act, edge_ok, edge_ok2);
+            um = cook<MODE_RES, VEC, SCH, kG, kE2>(A, as_res_row<MODE, VEC>(rm0), act, false);
+            uc_ = cook<MODE_RES, VEC, SCH, kG, kE2>(A, as_res_row<MODE, VEC>(rc0), act, edge_ok, edge_ok2);
         }
         RawRow<MODE, VEC> rp = ahead(zs + dz, o0 + st);
         RawRow<MODE, VEC> rn{}, rs{};
-        if (ld_n) rn = load_raw<MODE, VEC, false, kG, PER>(A, o0 + dn_, 0);
-        if (ld_s) rs = load_raw<MODE, VEC, false, kG, PER>(A, o0 + ds, 0);
+        if (ld_n) rn = load_raw<MODE, VEC, false, kG, kE2>(A, nrow(zs, o0), 0);
+        if (ld_s) rs = load_raw<MODE, VEC, false, kG, kE2>(A, srow(zs, o0), 0);
         Row<VEC> unc{}, f0c{}, ax{};
         if constexpr (kUn) unc = data_row<VEC, NK_ST_NTN>(A.un, o0, true);
         if constexpr (kF0) f0c = data_row<VEC, NK_ST_NT>(A.F0, o0, true);
@@ -1040,22 +1069,23 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L
             const int64_t k2 = more ? k + 2 * dz : k + dz;  // the plane o2 is in (-1 / nz: a ghost plane)
             const RawRow<MODE, VEC> rpp = ahead(k2, o2);
             RawRow<MODE, VEC> rnn{}, rss{};
-            if (ld_n) rnn = load_raw<MODE, VEC, false, kG, PER>(A, o1 + dn_, 0);
-            if (ld_s) rss = load_raw<MODE, VEC, false, kG, PER>(A, o1 + ds, 0);
+            const int64_t k1 = more ? k + dz : k;  // the plane o1 is in
+            if (ld_n) rnn = load_raw<MODE, VEC, false, kG, kE2>(A, nrow(k1, o1), 0);
+            if (ld_s) rss = load_raw<MODE, VEC, false, kG, kE2>(A, srow(k1, o1), 0);
             Row<VEC> uncn{}, f0cn{}, axn{};
             if constexpr (kUn) uncn = data_row<VEC, NK_ST_NTN>(A.un, o1, true);
             if constexpr (kF0) f0cn = data_row<VEC, NK_ST_NT>(A.F0, o1, true);
             if constexpr (kAx) axn = data_row<VEC>(A.aux, o1, true);
             // ---- cook what was issued one iteration ago
-            const Field<VEC> fp = cook<MODE, VEC, SCH, kG, PER>(A, rp, act, edge_ok, edge_ok2);
+            const Field<VEC> fp = cook<MODE, VEC, SCH, kG, kE2>(A, rp, act, edge_ok, edge_ok2);
             Field<VEC> fn{}, fs{};
-            if (ld_n) fn = cook<MODE, VEC, SCH, kG, PER>(A, rn, has_n, false);
-            if (ld_s) fs = cook<MODE, VEC, SCH, kG, PER>(A, rs, has_s, false);
+            if (ld_n) fn = cook<MODE, VEC, SCH, kG, kE2>(A, rn, has_n, false);
+            if (ld_s) fs = cook<MODE, VEC, SCH, kG, kE2>(A, rs, has_s, false);
             Field<VEC> up{}, fnu{}, fsu{};
             if constexpr (kR) {
-                up = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rp), act, edge_ok, edge_ok2);
-                if (ld_n) fnu = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rn), has_n, false);
-                if (ld_s) fsu = cook<MODE_RES, VEC, SCH, kG, PER>(A, as_res_row<MODE, VEC>(rs), has_s, false);
+                up = cook<MODE_RES, VEC, SCH, kG, kE2>(A, as_res_row<MODE, VEC>(rp), act, edge_ok, edge_ok2);
+                if (ld_n) fnu = cook<MODE_RES, VEC, SCH, kG, kE2>(A, as_res_row<MODE, VEC>(rn), has_n, false);
+                if (ld_s) fsu = cook<MODE_RES, VEC, SCH, kG, kE2>(A, as_res_row<MODE, VEC>(rs), has_s, false);
             }
             __syncthreads();  // plane k's rows are in LDS (parity: the next plane's writes go to the other buffer)
             double cn[VEC], cs[VEC], gn[VEC], gs[VEC];
@@ -1082,14 +1112,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L
                     if (!has_n) cnu[q] = 0.0;
                     if (!has_s) csu[q] = 0.0;
                 }
-                xu = x_nbrs<PER>(A, uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
+                xu = x_nbrs<kE2>(A, uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
             }
             // ---- compute plane k
-            const LR xn = x_nbrs<PER>(A, fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
+            const LR xn = x_nbrs<kE2>(A, fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
             const double lft = xn.l, rgt = xn.r;
             double glft = 0.0, grgt = 0.0;
             if constexpr (SCH == 2 && kG) {
-                const LR g2 = x_nbrs<PER>(A, fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
+                const LR g2 = x_nbrs<kE2>(A, fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
                 glft = g2.l;
                 grgt = g2.r;
             }
@@ -1171,12 +1201,12 @@ StInst go_st2d(const KArgs& A, int grid, hipStream_t s) {
     return r;
 }
 
-template <int KIND, int MODE, int EPI, int VEC, bool PER, int NW, bool F0R>
+template <int KIND, int MODE, int EPI, int VEC, bool PER, int NW, bool F0R, bool BLK = false>
 StInst go_st3l_i(const KArgs& A, int grid, hipStream_t s) {
-    hipLaunchKernelGGL((k_st3l<KIND, MODE, EPI, VEC, PER, NW, F0R>), dim3(grid), dim3(64 * NW), 0, s, A);
+    hipLaunchKernelGGL((k_st3l<KIND, MODE, EPI, VEC, PER, NW, F0R, BLK>), dim3(grid), dim3(64 * NW), 0, s, A);
     StInst r{};
-    snprintf(r.name, sizeof r.name, "nk::k_st3l<%d, %d, %d, %d, %s, %d, %s>", KIND, MODE, EPI, VEC, st_tf(PER), NW,
-             st_tf(F0R));
+    snprintf(r.name, sizeof r.name, "nk::k_st3l<%d, %d, %d, %d, %s, %d, %s, %s>", KIND, MODE, EPI, VEC, st_tf(PER), NW,
+             st_tf(F0R), st_tf(BLK));
     r.f0r = F0R;
     return r;
 }
@@ -1188,6 +1218,14 @@ StInst go_st3l(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
 #else
     constexpr bool kF0R = MODE == MODE_JFD && KIND == NK_HEAT3D_EULER;  // the only 3D F0R kind the launcher picks
 #endif
+    if (A.blk) {  // 3D blocks: bc_zero! only
+        if constexpr (kF0R) {
+            if (A.f0r) return vec == 2 ? go_st3l_i<KIND, MODE, EPI, 2, false, NW, true, true>(A, grid, s)
+                                       : go_st3l_i<KIND, MODE, EPI, 1, false, NW, true, true>(A, grid, s);
+        }
+        return vec == 2 ? go_st3l_i<KIND, MODE, EPI, 2, false, NW, false, true>(A, grid, s)
+                        : go_st3l_i<KIND, MODE, EPI, 1, false, NW, false, true>(A, grid, s);
+    }
     if constexpr (kF0R) {  // F0 recomputed from u (KArgs::f0r)
         if (A.f0r) {
             if (per) return vec == 2 ? go_st3l_i<KIND, MODE, EPI, 2, true, NW, true>(A, grid, s)
@@ -1245,10 +1283,12 @@ StInst go_stencil(const KArgs& A, int vec, int grid, hipStream_t s, bool per) {
         // k_st3l: y-neighbours through LDS, 4-row tiles (the kernel-variant build: 8-row tiles, the
         // per-wave y-row loads of k_st3d, the y-march k_st3y)
 #ifdef NK_KBENCH
-        if (A.ym) return A.nw == 8 ? go_st3y<KIND, MODE, EPI, 8>(A, vec, grid, s, per)
-                                   : go_st3y<KIND, MODE, EPI, 4>(A, vec, grid, s, per);
-        if (!A.lds3) return go_st3d<KIND, MODE, EPI, 4>(A, vec, grid, s, per);
-        if (A.nw == 8) return go_st3l<KIND, MODE, EPI, 8>(A, vec, grid, s, per);
+        if (!A.blk) {  // (3D blocks: k_st3l with 4-row tiles only)
+            if (A.ym) return A.nw == 8 ? go_st3y<KIND, MODE, EPI, 8>(A, vec, grid, s, per)
+                                       : go_st3y<KIND, MODE, EPI, 4>(A, vec, grid, s, per);
+            if (!A.lds3) return go_st3d<KIND, MODE, EPI, 4>(A, vec, grid, s, per);
+            if (A.nw == 8) return go_st3l<KIND, MODE, EPI, 8>(A, vec, grid, s, per);
+        }
 #endif
         return go_st3l<KIND, MODE, EPI, 4>(A, vec, grid, s, per);
     }

@@ -75,6 +75,12 @@ function path_info(ctx::HipContext)
      reduce_waits = p.reduce_waits, halo_wait_us = p.halo_wait_us, reduce_wait_us = p.reduce_wait_us)
 end
 
+"""3D blocks instead of z-slabs (nk_dist_grid): px × py × pz ranks, rank = (iz py + iy) px + ix.  Call after
+the ranks are connected and before allocating any vector (each 3D vector then carries x / y ghost faces)."""
+process_grid!(ctx::HipContext, px::Integer, py::Integer, pz::Integer) =
+    check(ccall((:nk_dist_grid, libnkhip), Cint, (Ptr{Cvoid}, Int32, Int32, Int32), ctx.ptr, px, py, pz), ctx,
+          "nk_dist_grid")
+
 # --------------------------------------------------------------------------- nk_problem (C layout)
 struct NkProblem
     kind::Int32

@@ -38,6 +38,8 @@ ap.add_argument("--fault-rank", type=int, default=-1,
                 help=">= 0: failure path -- after the first reductions this rank stops taking part (it waits at a "
                      "gloo barrier, its context alive), the others reduce again and must get an NK_E_* error in "
                      "bounded time; rank 0 records each rank's outcome")
+ap.add_argument("--pgrid", default="",
+                help="heat3d: px,py,pz -- 3D blocks (nk_dist_grid) instead of z-slabs; x / y ghost faces exchanged too")
 ap.add_argument("--transport", choices=["rccl", "mailbox"], default="rccl",
                 help="rccl: nk_dist_init (RCCL bootstrap, then the peer mailbox / RCCL fallback); mailbox: "
                      "IPC handles exchanged over gloo, no RCCL at all (works with every rank on one GPU)")
@@ -73,19 +75,26 @@ else:
 nx, ny = args.nx, args.ny
 if args.problem == "heat3d":  # 3D heat, implicit midpoint, z-slabs (k_st3l: the ghost planes travel in the stencil)
     nz = args.nz
-    grid = ah.slab((nx, ny, nz), rank, world)
-    z0, nzl = grid.offset, grid.shape_xyz[2]
+    if args.pgrid:  # 3D blocks: every vector allocated after the process grid carries its x / y faces
+        pg = tuple(int(t) for t in args.pgrid.split(","))
+        ctx.set_process_grid(*pg)
+        grid = ah.block((nx, ny, nz), rank, pg)
+    else:
+        grid = ah.slab((nx, ny, nz), rank, world)
+    x0, y0, z0 = grid.origin or (0, 0, grid.offset)
+    nxl, nyl, nzl = grid.shape_xyz
+    sl = (slice(z0, z0 + nzl), slice(y0, y0 + nyl), slice(x0, x0 + nxl))
     rng = np.random.default_rng(9)
     un_glob = rng.standard_normal((nz, ny, nx))
     u_glob = un_glob + 0.01 * rng.standard_normal((nz, ny, nx))
     v_glob = rng.standard_normal((nz, ny, nx))
     hx, hy, hz, a = 1.0 / (nx + 1), 1.0 / (ny + 1), 1.0 / (nz + 1), 0.01
     dt = 1.0 / (2.0 * a * (1 / hx ** 2 + 1 / hy ** 2 + 1 / hz ** 2))
-    und = ah.DeviceArray.from_numpy(np.ascontiguousarray(un_glob[z0:z0 + nzl]), grid, ctx)
+    und = ah.DeviceArray.from_numpy(np.ascontiguousarray(un_glob[sl]), grid, ctx)
     F_, p = ah.G_Midpoint_(alpha=0.3).bind(ah.diffusion3d_), (und, dt, None, (a, hx, hy, hz, ah.bc_zero_), 0.0)
-    u = ah.DeviceArray.from_numpy(np.ascontiguousarray(u_glob[z0:z0 + nzl]), grid, ctx)
+    u = ah.DeviceArray.from_numpy(np.ascontiguousarray(u_glob[sl]), grid, ctx)
     res = u.zero()
-    vd = ah.DeviceArray.from_numpy(np.ascontiguousarray(v_glob[z0:z0 + nzl]), grid, ctx)
+    vd = ah.DeviceArray.from_numpy(np.ascontiguousarray(v_glob[sl]), grid, ctx)
     out = u.zero()
     F_(res, u, p)
     ah.mul_(out, ah.JacobianOperator(F_, res, u, p, jv="exact"), vd)
@@ -95,13 +104,16 @@ if args.problem == "heat3d":  # 3D heat, implicit midpoint, z-slabs (k_st3l: the
     F_loc = res.to_numpy()
     u, r = ah.newton_krylov_(F_, u, p, res, tol_abs=6e-6, jv="fd")
     parts = [None] * world
-    dist.all_gather_object(parts, dict(z0=z0, u=u.to_numpy(), jv=jv_ex, jvfd=jv_fd, F=F_loc))
+    dist.all_gather_object(parts, dict(sl=sl, u=u.to_numpy(), jv=jv_ex, jvfd=jv_fd, F=F_loc))
     if rank == 0:
-        parts.sort(key=lambda d: d["z0"])
-        cat = lambda key: np.concatenate([d[key] for d in parts])  # noqa: E731
-        np.savez(args.out + ".npz", u=cat("u"), jv=cat("jv"), jvfd=cat("jvfd"), F=cat("F"))
+        full = {}
+        for key in ("u", "jv", "jvfd", "F"):
+            full[key] = np.full((nz, ny, nx), np.nan)
+            for d in parts:
+                full[key][d["sl"]] = d[key]
+        np.savez(args.out + ".npz", **full)
         json.dump(dict(solved=bool(r.solved), outer=r.stats.outer_iterations, inner=r.stats.inner_iterations,
-                       world=world, mailbox=ctx.mailbox_active), open(args.out + ".json", "w"))
+                       world=world, mailbox=ctx.mailbox_active, path=ctx.path_info()), open(args.out + ".json", "w"))
     dist.barrier()
     ctx.sync()
     sys.exit(0)

@@ -132,6 +132,34 @@ def test_slab_partition():
         ah.slab((4, 2), 0, 3)
 
 
+def test_block_partition():
+    """3D blocks tile the global grid exactly once; rank = (iz py + iy) px + ix; blocks sharing a face
+    share its extents (what k_faces_ipc relies on); pgrid (1, 1, n) is the slab split."""
+    for gx, pg in [((40, 20, 24), (2, 2, 2)), ((33, 20, 17), (1, 3, 1)), ((130, 18, 20), (4, 2, 1)), ((9, 8, 7), (3, 2, 1))]:
+        n = int(np.prod(pg))
+        blocks = [ah.block(gx, r, pg) for r in range(n)]
+        cover = np.zeros(gx[::-1], dtype=int)
+        for b in blocks:
+            (x0, y0, z0), (nx, ny, nz) = b.origin, b.shape_xyz
+            cover[z0:z0 + nz, y0:y0 + ny, x0:x0 + nx] += 1
+            assert b.offset == z0 and b.global_xyz == gx
+        assert (cover == 1).all()
+        px, py, _ = pg
+        for r, b in enumerate(blocks):
+            if r % px + 1 < px:  # x neighbour: same ny, nz
+                assert blocks[r + 1].shape_xyz[1:] == b.shape_xyz[1:]
+            if (r // px) % py + 1 < py:  # y neighbour: same nx, nz
+                o = blocks[r + px].shape_xyz
+                assert (o[0], o[2]) == (b.shape_xyz[0], b.shape_xyz[2])
+    for r in range(3):
+        s, b = ah.slab((8, 8, 9), r, 3), ah.block((8, 8, 9), r, (1, 1, 3))
+        assert (s.shape_xyz, s.offset) == (b.shape_xyz, b.offset)
+    with pytest.raises(ValueError):
+        ah.block((4, 8, 8), 0, (5, 1, 1))
+    with pytest.raises(ValueError):
+        ah.block((8, 8), 0, (2, 1, 1))
+
+
 def test_grid_shapes():
     g = ah.Grid.full(7, 5)
     assert g.np_shape == (5, 7) and g.n == 35 and g.nxyz == (7, 5, 1)
