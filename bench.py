@@ -90,6 +90,10 @@ def parse():
                     help="with --global-n on ONE GPU: run the slab one rank of a --slab-of-way decomposition owns "
                          "(rank slab_of // 2, ghost planes zero, no exchange) -- the per-GPU compute of configs 4 / 5 "
                          "before an 8-GPU node is available (--global-n 16384 --slab-of 8)")
+    ap.add_argument("--pgrid", default="",
+                    help="heat3d --global-n with N > 1 ranks: 3D blocks px,py,pz (nk_dist_grid; 'auto': the most "
+                         "cubic factorisation of N -- 2,2,2 at N = 8, BASELINE config 5's 256^3 blocks) instead of "
+                         "z-slabs; every vector's six ghost layers travel in one packed-face launch")
     ap.add_argument("--memory", type=int, default=0, help="Krylov memory (default 30 for bratu2d, 20 for heat)")
     ap.add_argument("--itmax", type=int, default=300)
     ap.add_argument("--jv", choices=["fd", "exact"], default="fd")
@@ -269,6 +273,25 @@ def scaling_fields(value, dof_per_unit, paths, workload, slab_of, world, global_
     return out
 
 
+def pgrid_of(spec, world):
+    """--pgrid: 'px,py,pz' (product = world) or 'auto' (the most cubic factorisation, x fastest)."""
+    if spec == "auto":
+        best = None
+        for px in range(1, world + 1):
+            for py in range(1, world // px + 1):
+                if world % (px * py):
+                    continue
+                pz = world // (px * py)
+                key = (max(px, py, pz) - min(px, py, pz), -pz, -py)
+                if best is None or key < best[0]:
+                    best = (key, (px, py, pz))
+        return best[1]
+    pg = tuple(int(t) for t in spec.split(","))
+    if len(pg) != 3 or int(np.prod(pg)) != world:
+        raise SystemExit(f"--pgrid {spec}: three factors whose product is the number of ranks ({world})")
+    return pg
+
+
 def noisy(shape_rows, nx, seed_rows):
     """0.1 U(-1, 1) noise whose every row is seeded by its GLOBAL index, so a slab sees the same field."""
     return np.stack([0.1 * np.random.default_rng([0, int(r)]).uniform(-1.0, 1.0, nx) for r in seed_rows]).reshape(
@@ -393,9 +416,14 @@ class HeatEuler:
         parts = args.slab_of or world
         if args.slab_of:
             rank = parts // 2
+        self.pgrid = None
+        if args.pgrid and dim == 3 and world > 1:
+            if not args.global_n:
+                raise SystemExit("--pgrid splits one --global-n problem into blocks")
+            self.pgrid = pgrid_of(args.pgrid, world)
         if args.global_n:  # strong scaling: one global G^dim problem, G / world slab planes per rank
             n = args.global_n
-            if n % parts:
+            if n % parts and not self.pgrid:
                 raise SystemExit(f"--global-n {n} must be divisible by the number of slabs {parts}")
             planes = n // parts
             glob = (n,) * dim
@@ -414,7 +442,17 @@ class HeatEuler:
         grid = ah.Grid((n,) * (dim - 1) + (planes,), glob, rank * planes)
         sines = [np.sin(np.pi * np.arange(1, n + 1) * hs[0])]
         rows0 = rank * planes
-        if dim == 2:
+        if self.pgrid:  # 3D blocks: the process grid first (every vector then carries its x / y faces)
+            ctx.set_process_grid(*self.pgrid)
+            grid = ah.block(glob, rank, self.pgrid)
+            (x0, y0, z0), (nxl, nyl, nzl) = grid.origin, grid.shape_xyz
+            zs = np.sin(np.pi * np.arange(z0 + 1, z0 + nzl + 1) * hs[2])
+            ys = np.sin(np.pi * np.arange(y0 + 1, y0 + nyl + 1) * hs[1])
+            base = zs[:, None, None] * ys[None, :, None] * sines[0][None, None, x0:x0 + nxl]
+            rows = [z * n + y for z in range(z0, z0 + nzl) for y in range(y0, y0 + nyl)]
+            u0 = base + noisy((nzl, nyl), n, rows)[:, :, x0:x0 + nxl]  # the same field as the slabs see
+            planes = nzl
+        elif dim == 2:
             ys = np.sin(np.pi * np.arange(rows0 + 1, rows0 + planes + 1) * hs[1])
             u0 = ys[:, None] * sines[0][None, :] + noisy((planes,), n, range(rows0, rows0 + planes))
         else:
@@ -439,6 +477,9 @@ class HeatEuler:
         self.jv_kernel = "jv_fd_dot_norm" if args.jv == "fd" else "jv_exact_dot_norm"
         shape = "x".join(str(m) for m in glob)
         per_gpu = f"{n}^{dim - 1}x{planes} slab per GPU" if args.global_n else f"{n}^{dim} per GPU"
+        if self.pgrid:
+            per_gpu = ("x".join(str(m) for m in grid.shape_xyz) + " block per GPU, "
+                       + "x".join(str(m) for m in self.pgrid) + " blocks")
         sname = {"euler": "implicit Euler", "midpoint": "implicit midpoint", "trapezoid": "implicit trapezoid"}[args.scheme]
         bcname = "" if args.bc == "zero" else ", bc_periodic!"
         slab = (f"; rank {rank}'s slab of the {parts}-way split ALONE on one GPU (ghost planes zero, no exchange)"
@@ -448,6 +489,8 @@ class HeatEuler:
                          f"reorthogonalization={'true' if self.reorth else 'false'}), "
                          f"{args.jv.upper()} Jv, IC sin*sin + 0.1 U(-1,1){slab}")
         self.side = str(n) if planes == n else f"{n}x{planes}"
+        if self.pgrid:
+            self.side = "block" + "x".join(str(m) for m in grid.shape_xyz)
         self.metric = f"Krylov matvecs/sec + achieved HBM GB/s, {dim}D heat {sname}{bcname} {n}^{dim}"
 
     def step(self):
@@ -728,7 +771,8 @@ def main():
             "dtype": "f64",
             "data": "synthetic (see config.workload)",
             "config": {"workload": W.workload, "matvecs_per_step": matvecs // max(1, args.steps),
-                       "parallelism": f"slab{world}" if not args.slab_of else f"slab 1 of {args.slab_of} (one GPU)",
+                       "parallelism": (("blocks" + "x".join(str(m) for m in W.pgrid)) if getattr(W, "pgrid", None)
+                                       else (f"slab{world}" if not args.slab_of else f"slab 1 of {args.slab_of} (one GPU)")),
                        "reorthogonalization": bool(getattr(W, "reorth", args.reorth == "on")),
                        "devices": (f"{min(world, ndev)} GPU(s) for {world} rank(s) (shared: rehearsal)" if shared
                                    else f"{world} GPU(s), one per rank"),

@@ -29,6 +29,7 @@ static int rccl_fail(nk_ctx* c, ncclResult_t r, const char* what) {
 
 // 3D blocks: rank = (iz py + iy) px + ix; side s = 2 a + hi of axis a = z, y, x (kHaloSides numbering)
 int block_nbr(const nk_ctx* c, int side) {
+    if (block_self(c)) return c->rank;  // kbench self blocks
     const int px = c->px, py = c->py, r = c->rank;
     const int ix = r % px, iy = (r / px) % py, iz = r / (px * py), pz = c->nranks / (px * py);
     const int hi = side & 1;

@@ -237,7 +237,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
                      double* colh, int rv, double** vout, const ResJv* jin = nullptr);
 constexpr int kMbSlots = 256;                // mailbox ring (epoch % kMbSlots)
 constexpr int kMbRanks = 32;                 // max ranks of the mailbox all-reduce (2 granules each: one wave polls them all)
-constexpr int kHaloBlocks = 64;              // blocks (= flags per side) of the IPC ghost-plane exchange
+constexpr int kHaloBlocks = 256;              // blocks (= flags per side) of the IPC ghost-plane exchange
 constexpr int kHaloSides = 6;                // ghost layers by the side they come from: 0 / 1 the slowest axis's lower /
                                              // upper neighbour (slabs; z of 3D blocks), 2 / 3 y, 4 / 5 x (3D blocks)
 constexpr int kHaloTileFlags = 4096;         // stencil tiles per plane whose ghost patch travels in the stencil itself
@@ -338,7 +338,8 @@ inline int nk_scheme(int kind) {
 // 3D blocks (nk_dist_grid with px * py > 1): a 3D grid function's allocation carries, after its trailing
 // z ghost plane, the four x / y ghost faces the neighbours' boundary layers are exchanged into:
 //   [y-lo: nx nz][y-hi: nx nz][x-lo: ny nz][x-hi: ny nz]   (y faces indexed k nx + i, x faces k ny + j)
-inline bool blocks3d(const nk_ctx* c, const Geo& g) { return g.dim == 3 && c->px * c->py > 1; }
+bool block_self(const nk_ctx* c);  // kbench (NK_HALO_SELF=2): a one-rank mailbox is its own neighbour on all six sides
+inline bool blocks3d(const nk_ctx* c, const Geo& g) { return g.dim == 3 && (c->px * c->py > 1 || block_self(c)); }
 inline int64_t face_words(const nk_ctx* c, const nk_problem* p, const Geo& g) {
     return blocks3d(c, g) ? 2 * (p->nx + p->ny) * p->nz : 0;
 }

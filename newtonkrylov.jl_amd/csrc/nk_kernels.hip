@@ -629,7 +629,7 @@ __global__ __launch_bounds__(kBlock) void k_halo_ipc(double* __restrict__ v, int
 // neighbour into that neighbour's inbox for side s ^ 1 (system-scope stores), drains, raises its flag
 // there, waits for the neighbours' block-b flags in my region and unpacks their layers -- the z ones into
 // my ghost planes, the x / y ones into the faces after the allocation's trailing plane.  Neighbours share
-// the face's extents, and the grid is always kHaloBlocks blocks, so both sides cut a face alike.  At a
+// the face's extents, and the grid size is a constant, so both sides cut a face alike.  At a
 // physical boundary the layer stays zero (zero-filled allocation, never written there).
 struct FaceArgs {
     int64_t nx, ny, nz;
@@ -734,8 +734,9 @@ int launch_halo_ipc(nk_ctx* c, double* v, int64_t plane, int64_t nplanes, bool r
     if (halo_self_ring(c)) ring = true;
     else if (c->nranks < 2) return NK_OK;
     const uint64_t epoch = ++c->halo_epoch;
+    static const int nb_max = std::max(1, std::min(kHaloBlocks, NK_TUNE("NK_HALO_NB", kHaloBlocks)));  // (kbench A/B)
     int nb = (int)((plane + 1023) / 1024);
-    if (nb > kHaloBlocks) nb = kHaloBlocks;
+    if (nb > nb_max) nb = nb_max;
     if (nb < 1) nb = 1;
     const int nbrs = ring ? 2 : (c->rank > 0) + (c->rank + 1 < c->nranks);
     return launch(c, "halo_ipc", 16.0 * plane * nbrs, [&] {
@@ -760,8 +761,10 @@ int launch_faces_ipc(nk_ctx* c, double* v, const nk_problem* p) {
     }
     if (bytes == 0.0) return NK_OK;
     const uint64_t epoch = ++c->halo_epoch;
+    // every rank cuts a face into the same nb chunks (the grid size is a constant, never the face's size)
+    static const int nb = std::max(1, std::min(kHaloBlocks, NK_TUNE("NK_FACE_NB", kHaloBlocks)));  // (kbench A/B)
     return launch(c, "halo_faces", bytes, [&] {
-        hipLaunchKernelGGL(k_faces_ipc, dim3(kHaloBlocks), dim3(kBlock), 0, c->stream, v, F, epoch, c->halo_cap);
+        hipLaunchKernelGGL(k_faces_ipc, dim3(nb), dim3(kBlock), 0, c->stream, v, F, epoch, c->halo_cap);
     });
 }
 
@@ -799,6 +802,12 @@ int halo_fuse_knob() {
 bool halo_self_ring(const nk_ctx* c) {
     static const int self = NK_TUNE("NK_HALO_SELF", 0);
     return self && c->mb_on && c->nranks == 1;
+}
+// kbench only (NK_HALO_SELF=2): the lone rank is its own neighbour on all six sides of a 3D block -- the
+// packed-face exchange and k_st3l's face reads of config 5's blocks, timed on one GPU (tools/halo_self.py)
+bool block_self(const nk_ctx* c) {
+    static const int self = NK_TUNE("NK_HALO_SELF", 0);
+    return self == 2 && c->mb_on && c->nranks == 1;
 }
 
 int red_blocks(int64_t n) {

@@ -153,3 +153,45 @@ def test_two_rank_bench_runs_end_to_end():
             assert e["reduce_waits"] > 0 and e["reduce_wait_us_mean"] > 0, e
             assert e["halo_waits"] > 0 and e["halo_wait_us_mean"] > 0, e
             assert 0 < e["exchange_share"] < 1, e
+
+
+def test_pgrid_factorisation():
+    """--pgrid auto: the most cubic px x py x pz of N (BASELINE config 5: 2 x 2 x 2 at N = 8); an explicit
+    grid must multiply to N."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    assert b.pgrid_of("auto", 8) == (2, 2, 2)
+    assert b.pgrid_of("auto", 4) == (1, 2, 2) and b.pgrid_of("auto", 2) == (1, 1, 2)
+    assert b.pgrid_of("auto", 27) == (3, 3, 3)
+    assert b.pgrid_of("2,1,4", 8) == (2, 1, 4)
+    with pytest.raises(SystemExit):
+        b.pgrid_of("2,2,1", 8)
+
+
+@pytest.mark.gpu
+def test_eight_rank_block_bench_rehearsal():
+    """BASELINE config 5's decomposition end to end through bench.py: --workload heat3d --global-n 64
+    --pgrid auto on 8 ranks (2 x 2 x 2 blocks of 32^3; sharing the box's GPU over the mailbox when it has
+    fewer): one JSON line naming the blocks, every rank's ghost faces exchanged (non-zero peer waits)."""
+    import _nkpath  # noqa: F401
+    import ariadne_hip as ah
+
+    args = ["--gpus", "8", "--workload", "heat3d", "--global-n", "64", "--pgrid", "auto", "--steps", "1",
+            "--warmup", "1", "--no-prof", "--no-cpu-baseline"]
+    env = {}
+    if ah.device_count() < 8:
+        args += ["--transport", "mailbox"]
+        env["GPU_MAX_HW_QUEUES"] = "1"  # 8 ranks x 4 queues would time-slice the one GPU
+    p = run(args, env=env, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(line) == 1
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 8 and d["value"] > 0 and d["config"]["parallelism"] == "blocks2x2x2"
+    assert "32x32x32 block per GPU" in d["config"]["workload"]
+    assert len(d["ranks"]) == 8
+    for q in d["ranks"]:
+        assert q["exchange"]["halo_waits"] > 0, q

@@ -8,6 +8,9 @@ for the GPU.  Modes, each in its own process:
   mbox    forced one-rank mailbox, no exchange (every reduction scalar through the mailbox)
   fused   + self ring, v's ghost planes inside the Jv launch (halo_tile_exchange, the product default)
   kernel  + self ring, a separate exchange kernel before every Jv (NK_HALO_FUSE=0)
+  blocks  3D only: the rank is its own neighbour on all SIX sides (NK_HALO_SELF=2) -- config 5's 3D-block
+          path: one packed-face exchange launch per Jv (k_faces_ipc) and k_st3l reading the x / y faces
+          at the block's edges (the operator differs: every axis wraps; the cost is what is measured)
 
 fused - mbox and kernel - mbox are the exchange's cost per Arnoldi step.  fused and kernel apply the same
 operator (the same ghost planes, the same per-point arithmetic) but the fused launch dispatches the
@@ -43,6 +46,7 @@ ENV = {
     "mbox": {"NK_DIST_FORCE": "1", "NK_DIST_MAILBOX": "1"},
     "fused": {"NK_DIST_FORCE": "1", "NK_DIST_MAILBOX": "1", "NK_HALO_SELF": "1"},
     "kernel": {"NK_DIST_FORCE": "1", "NK_DIST_MAILBOX": "1", "NK_HALO_SELF": "1", "NK_HALO_FUSE": "0"},
+    "blocks": {"NK_DIST_FORCE": "1", "NK_DIST_MAILBOX": "1", "NK_HALO_SELF": "2"},
 }
 
 
@@ -106,7 +110,7 @@ print(f"halo self ring: one process, {what}, FD Jv, GMRES(20) restarted, {args.i
 rows = []
 for mode in args.modes.split(","):
     env = dict(os.environ, NK_KBENCH_LIB="1", **ENV[mode])
-    for k in ("NK_HALO_SELF", "NK_HALO_FUSE", "NK_DIST_FORCE", "NK_DIST_MAILBOX"):
+    for k in ("NK_HALO_SELF", "NK_HALO_FUSE", "NK_DIST_FORCE", "NK_DIST_MAILBOX"):  # (NK_HALO_SELF=2: blocks)
         if k not in ENV[mode]:
             env.pop(k, None)
     p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", mode, "--nx", str(args.nx), "--ny",
@@ -120,15 +124,18 @@ for mode in args.modes.split(","):
     r = json.loads(lines[-1][7:])
     rows.append(r)
     print(json.dumps(r), flush=True)
-print("\nmode     us/step  jv_fd_dot us  halo_ipc us (launches)  x sha")
+print("\nmode     us/step  jv_fd_dot us  halo_ipc / halo_faces us (launches)  x sha")
 for r in rows:
     c = r["classes"]
     jv = c.get("jv_fd_dot", {}).get("avg_us", 0.0)
-    h = c.get("halo_ipc", {})
+    h = c.get("halo_ipc") or c.get("halo_faces") or {}
     print(f"{r['mode']:8s} {r['us_per_step']:7.1f}  {jv:11.1f}  {h.get('avg_us', 0.0):8.1f} ({h.get('launches', 0):3d})"
           f"            {r['x_sha']}")
 import numpy as np  # noqa: E402
 
+modes = {r["mode"] for r in rows}
+if not {"fused", "kernel", "plain", "mbox"} <= modes:
+    sys.exit(0)
 xf, xk = (np.load(os.path.join(args.xdir, f"x_{m}.npy")) for m in ("fused", "kernel"))
 xp, xm = (np.load(os.path.join(args.xdir, f"x_{m}.npy")) for m in ("plain", "mbox"))
 print(f"fused vs kernel: max |dx| / max |x| = {np.max(np.abs(xf - xk)) / np.max(np.abs(xk)):.2e} "
