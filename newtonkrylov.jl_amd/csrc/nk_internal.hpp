@@ -241,6 +241,7 @@ constexpr int kHaloBlocks = 256;              // blocks (= flags per side) of th
 constexpr int kHaloSides = 6;                // ghost layers by the side they come from: 0 / 1 the slowest axis's lower /
                                              // upper neighbour (slabs; z of 3D blocks), 2 / 3 y, 4 / 5 x (3D blocks)
 constexpr int kHaloTileFlags = 4096;         // stencil tiles per plane whose ghost patch travels in the stencil itself
+constexpr int64_t kSharedFuseMax = (int64_t)1 << 20;  // ranks sharing a GPU: in-launch ghost planes up to this many points
 // one fine-grained region per rank, IPC-mapped by every other rank:
 //   [mailbox: kMbSlots x kMbRanks x 2 u64][halo flags: 2 parity x kHaloSides x kHaloBlocks u64]
 //   [tile flags: 2 parity x 2 sides x kHaloTileFlags u64]

@@ -994,7 +994,11 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         const int fuse_env = halo_fuse_knob();
         const int64_t tiles_pl = g.dim == 2 ? A.tiles_x : (int64_t)A.tiles_x * A.tiles_y;
         const bool self = halo_self_ring(c);
-        const bool fuse = fuse_env && c->mb_on && (c->nranks > 1 || self) && !per && !A.blk && in.mode != MODE_RES &&
+        // ranks sharing one GPU (rehearsals): in-launch only for small slabs -- a big slab's end tiles spin
+        // on CUs the peer's producing tiles need (r05: 8 ranks x 256^2 x 32 planes, 30 s per step fused
+        // against 27 ms with the exchange kernel, profiles/r05/rehearsal8_heat3d_256_*.json)
+        const bool share_ok = c->res_share <= 1 || g.n <= kSharedFuseMax;
+        const bool fuse = fuse_env && c->mb_on && (c->nranks > 1 || self) && share_ok && !per && !A.blk && in.mode != MODE_RES &&
                           (g.dim == 2 || (g.dim == 3 && A.lds3)) && g.plane <= c->halo_cap && tiles_pl <= kHaloTileFlags;
         if (fuse) {
             ++c->n_jv_halo_fused;
