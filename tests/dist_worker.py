@@ -97,6 +97,24 @@ if args.problem == "heat3d":  # 3D heat, implicit midpoint, z-slabs (k_st3l: the
     vd = ah.DeviceArray.from_numpy(np.ascontiguousarray(v_glob[sl]), grid, ctx)
     out = u.zero()
     F_(res, u, p)
+    if args.krylov_itmax > 0:  # one restarted FD-GMRES(20) solve J x = F(u0), fixed budget
+        ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=20))
+        J = ah.JacobianOperator(F_, res, u, p, jv="fd")
+        ah.krylov_solve_(ws, J, res, restart=True, atol=0.0, rtol=0.0, itmax=args.krylov_itmax, history=True)
+        parts = [None] * world
+        dist.all_gather_object(parts, dict(sl=sl, x=ws.x.to_numpy(), F=res.to_numpy()))
+        if rank == 0:
+            full = {}
+            for key in ("x", "F"):
+                full[key] = np.full((nz, ny, nx), np.nan)
+                for d in parts:
+                    full[key][d["sl"]] = d[key]
+            np.savez(args.out + ".npz", h=np.array(ws.stats.residuals), **full)
+            json.dump(dict(niter=ws.stats.niter, n_matvec=ws.stats.n_matvec, world=world, path=ctx.path_info()),
+                      open(args.out + ".json", "w"))
+        dist.barrier()
+        ctx.sync()
+        sys.exit(0)
     ah.mul_(out, ah.JacobianOperator(F_, res, u, p, jv="exact"), vd)
     jv_ex = out.to_numpy()
     ah.mul_(out, ah.JacobianOperator(F_, res, u, p, jv="fd"), vd, eps=1e-6)

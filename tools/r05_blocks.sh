@@ -6,7 +6,7 @@ set -e -o pipefail
 OUT=gpurun_out/r05_blocks${1:+_$1}
 mkdir -p "$OUT"
 [ -n "$NO_TESTS" ] || timeout -k 10 600 python -u -m pytest tests/test_hip_dist.py tests/test_bench_launcher.py -x -v --timeout 300 \
-    --timeout-method thread -k "blocks or block_bench or two_rank_bench" > "$OUT/tests.log" 2>&1
+    --timeout-method thread -k "${TEST_K:-blocks or block_bench or two_rank_bench}" > "$OUT/tests.log" 2>&1
 export GPU_MAX_HW_QUEUES=1
 # time-shared ranks: a rank's reduction partner may be descheduled for seconds -- a long poll limit
 export NK_MB_SPIN_LIMIT=${NK_MB_SPIN_LIMIT:-1073741824}
