@@ -124,6 +124,7 @@ static int mb_alloc(nk_ctx* c) {
     NK_HIP(c, hipSetDevice(c->device));
     const char* hc = getenv("NK_HALO_CAP");  // doubles per inbox plane (default 1M: a 1024^2 3D plane)
     c->halo_cap_dev = (hc && *hc) ? atoll(hc) : ((int64_t)1 << 20);
+    c->halo_cap_dev = std::max<int64_t>(0, std::min<int64_t>(c->halo_cap_dev, INT32_MAX));  // 32-bit face indexing
     const size_t bytes = mb_region_bytes(c->halo_cap_dev);
     void* p = nullptr;
     if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) != hipSuccess)
@@ -203,6 +204,7 @@ static int mb_alloc_host(nk_ctx* c) {
     NK_HIP(c, hipSetDevice(c->device));
     const char* hc = getenv("NK_HALO_CAP_HOST");
     c->halo_cap_host = (hc && *hc) ? atoll(hc) : ((int64_t)1 << 16);
+    c->halo_cap_host = std::max<int64_t>(0, std::min<int64_t>(c->halo_cap_host, INT32_MAX));
     const size_t bytes = mb_region_bytes(c->halo_cap_host);
     static unsigned seq = 0;
     static_assert(sizeof(HostHandle::name) <= sizeof(c->mb_host_name), "host mailbox name");
@@ -377,6 +379,16 @@ static int mb_open_peers(nk_ctx* c, int rank, int nranks, const char* handles, c
     }
     c->res_share = share;
     c->res_ok = share < 2 || shared_ok;
+    // the most ranks on any one GPU, from the same gathered bus ids on every rank (all ranks, no bus ids:
+    // assume they share): ranks sharing a GPU spin in their exchange kernels together, and all of those
+    // grids must be resident at once -- at 256 blocks x 4 waves, 8 sharing ranks would fill the GPU
+    int most = busids ? 1 : nranks;
+    for (int r = 0; busids && r < nranks; ++r) {
+        int cnt = 0;
+        for (int q = 0; q < nranks; ++q) cnt += std::memcmp(busids + 32 * (size_t)r, busids + 32 * (size_t)q, 32) == 0;
+        most = std::max(most, cnt);
+    }
+    c->xchg_nb = std::max(16, kHaloBlocks / std::max(1, most));
     NK_HIP(c, hipMalloc(reinterpret_cast<void**>(&c->mb_peers_dev), sizeof(uint64_t*) * nranks));
     NK_HIP(c, hipMemcpy(c->mb_peers_dev, peers.data(), sizeof(uint64_t*) * nranks, hipMemcpyHostToDevice));
     *c->mb_err = 0;

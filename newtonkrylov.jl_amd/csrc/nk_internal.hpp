@@ -111,6 +111,8 @@ struct nk_ctx {
     unsigned res_tag = 0;                  // granule tags handed out so far
     int res_blocks = 0, res_rl = 0;        // grid (= CUs) and LDS double2 slots per thread
     int res_share = 1;                     // ranks on this GPU (NK_RES_SHARED: each sweep grid gets CUs / res_share)
+    int xchg_nb = 256;                     // exchange-kernel grid (<= kHaloBlocks), the same on every rank: kHaloBlocks / the most
+                                           // ranks sharing one GPU, so every sharing rank's spinning exchange grid fits at once
     uint64_t* res_tstamp = nullptr;        // kernel-variant bench only (nkb_mgs_res, NK_RES_TSTAMP)
     // pipelined ILU(0) sweeps (launch_ilu0_*): per-strip progress counters + a pinned timeout flag
     int64_t* ilu_prog = nullptr;

@@ -734,7 +734,8 @@ int launch_halo_ipc(nk_ctx* c, double* v, int64_t plane, int64_t nplanes, bool r
     if (halo_self_ring(c)) ring = true;
     else if (c->nranks < 2) return NK_OK;
     const uint64_t epoch = ++c->halo_epoch;
-    static const int nb_max = std::max(1, std::min(kHaloBlocks, NK_TUNE("NK_HALO_NB", kHaloBlocks)));  // (kbench A/B)
+    static const int nb_env = std::max(1, std::min(kHaloBlocks, NK_TUNE("NK_HALO_NB", kHaloBlocks)));  // (kbench A/B)
+    const int nb_max = std::min(nb_env, c->xchg_nb);
     int nb = (int)((plane + 1023) / 1024);
     if (nb > nb_max) nb = nb_max;
     if (nb < 1) nb = 1;
@@ -761,8 +762,9 @@ int launch_faces_ipc(nk_ctx* c, double* v, const nk_problem* p) {
     }
     if (bytes == 0.0) return NK_OK;
     const uint64_t epoch = ++c->halo_epoch;
-    // every rank cuts a face into the same nb chunks (the grid size is a constant, never the face's size)
-    static const int nb = std::max(1, std::min(kHaloBlocks, NK_TUNE("NK_FACE_NB", kHaloBlocks)));  // (kbench A/B)
+    // every rank cuts a face into the same nb chunks (xchg_nb is agreed at mailbox set-up, never the face's size)
+    static const int nb_env = std::max(1, std::min(kHaloBlocks, NK_TUNE("NK_FACE_NB", kHaloBlocks)));  // (kbench A/B)
+    const int nb = std::min(nb_env, c->xchg_nb);
     return launch(c, "halo_faces", bytes, [&] {
         hipLaunchKernelGGL(k_faces_ipc, dim3(nb), dim3(kBlock), 0, c->stream, v, F, epoch, c->halo_cap);
     });
