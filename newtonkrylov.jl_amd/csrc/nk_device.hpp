@@ -225,6 +225,20 @@ __device__ __forceinline__ uint64_t* halo_tile_flags(uint64_t* base, int par, in
 __device__ __forceinline__ uint64_t* halo_inbox(uint64_t* base, int par, int side, int64_t cap) {
     return base + kMbWords + kHaloFlagWords + (size_t)(par * kHaloSides + side) * (size_t)cap;
 }
+// one lane's wait for a peer's flag to reach `epoch` (bounded: an error at the next host sync, never a hang).
+// Exchanges poll their flags in parallel, one lane each: every poll is a system-scope round trip.
+__device__ __forceinline__ bool flag_wait(const uint64_t* f, uint64_t epoch) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+        if (++spins > g_mb.spin_limit ||
+            ((spins & 255) == 0 && __hip_atomic_load(g_mb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
+            __hip_atomic_store(g_mb.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return true;
+}
 __device__ __forceinline__ double ld_inbox(const uint64_t* p) {
     return __longlong_as_double((long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
 }
@@ -257,26 +271,19 @@ __device__ __forceinline__ bool halo_tile_exchange(const double* __restrict__ v,
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every thread drains its stores before the flag
     __syncthreads();
-    if (threadIdx.x == 0) {
-        if (t.lo) __hip_atomic_store(halo_tile_flags(g_mb.peers[(rank + nr - 1) % nr], par, 1) + tile, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (t.hi) __hip_atomic_store(halo_tile_flags(g_mb.peers[(rank + 1) % nr], par, 0) + tile, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        hx_ok = 1;
+    if (threadIdx.x < 64) {  // lane 0 the lower side, lane 1 the upper: flags raised and polled in parallel
+        const int side = (int)threadIdx.x;
+        const bool mine = (side == 0 && t.lo) || (side == 1 && t.hi);
+        if (mine)
+            __hip_atomic_store(halo_tile_flags(g_mb.peers[side == 0 ? (rank + nr - 1) % nr : (rank + 1) % nr], par, side ^ 1) + tile,
+                               epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint64_t t0 = wall_clock64();
-        for (int side = 0; side < 2; ++side) {
-            if ((side == 0 && !t.lo) || (side == 1 && !t.hi)) continue;
-            const uint64_t* f = halo_tile_flags(g_mb.self, par, side) + tile;
-            unsigned spins = 0;
-            while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
-                if (++spins > g_mb.spin_limit ||
-                    ((spins & 255) == 0 && __hip_atomic_load(g_mb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
-                    __hip_atomic_store(g_mb.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    hx_ok = 0;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
+        const bool ok = !mine || flag_wait(halo_tile_flags(g_mb.self, par, side) + tile, epoch);
+        const bool all = __all(ok);
+        if (side == 0) {
+            hx_ok = all ? 1 : 0;
+            wait_note(kWaitHalo, t0);
         }
-        wait_note(kWaitHalo, t0);
     }
     __syncthreads();
     return hx_ok != 0;

@@ -586,28 +586,19 @@ __global__ __launch_bounds__(kBlock) void k_halo_ipc(double* __restrict__ v, int
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every thread drains its stores before the flag
     __syncthreads();
-    if (threadIdx.x == 0) {
-        if (lo) __hip_atomic_store(halo_flags(g_mb.peers[rlo]) + (par * kHaloSides + 1) * kHaloBlocks + b, epoch,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (hi) __hip_atomic_store(halo_flags(g_mb.peers[rhi]) + (par * kHaloSides + 0) * kHaloBlocks + b, epoch,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        ready = 1;
+    if (threadIdx.x < 64) {  // lane 0 the lower side, lane 1 the upper: flags raised and polled in parallel
+        const int side = (int)threadIdx.x;
+        const bool mine = (side == 0 && lo) || (side == 1 && hi);
+        if (mine)
+            __hip_atomic_store(halo_flags(g_mb.peers[side == 0 ? rlo : rhi]) + (par * kHaloSides + (side ^ 1)) * kHaloBlocks + b,
+                               epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint64_t t0 = wall_clock64();
-        for (int side = 0; side < 2; ++side) {
-            if ((side == 0 && !lo) || (side == 1 && !hi)) continue;
-            const uint64_t* f = halo_flags(g_mb.self) + (par * kHaloSides + side) * kHaloBlocks + b;
-            unsigned spins = 0;
-            while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
-                if (++spins > g_mb.spin_limit ||
-                    ((spins & 255) == 0 && __hip_atomic_load(g_mb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
-                    __hip_atomic_store(g_mb.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    ready = 0;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
+        const bool ok = !mine || flag_wait(halo_flags(g_mb.self) + (par * kHaloSides + side) * kHaloBlocks + b, epoch);
+        const bool all = __all(ok);
+        if (side == 0) {
+            ready = all ? 1 : 0;
+            wait_note(kWaitHalo, t0);
         }
-        wait_note(kWaitHalo, t0);
     }
     __syncthreads();
     if (!ready) return;
@@ -671,28 +662,22 @@ __global__ __launch_bounds__(kBlock) void k_faces_ipc(double* __restrict__ v, Fa
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every thread drains its stores before the flags
     __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int s = 0; s < kHaloSides; ++s)
-            if (F.nbr[s] >= 0)
-                __hip_atomic_store(halo_flags(g_mb.peers[F.nbr[s]]) + (par * kHaloSides + (s ^ 1)) * kHaloBlocks + b, epoch,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        ready = 1;
+    if (threadIdx.x < 64) {  // lane s raises side s's flag and polls its own: six round trips in parallel
+        const int s = (int)threadIdx.x;
+        int nbr = -1;
+#pragma unroll
+        for (int q = 0; q < kHaloSides; ++q)
+            if (q == s) nbr = F.nbr[q];
+        if (nbr >= 0)
+            __hip_atomic_store(halo_flags(g_mb.peers[nbr]) + (par * kHaloSides + (s ^ 1)) * kHaloBlocks + b, epoch,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint64_t t0 = wall_clock64();
-        for (int s = 0; s < kHaloSides; ++s) {
-            if (F.nbr[s] < 0) continue;
-            const uint64_t* f = halo_flags(g_mb.self) + (par * kHaloSides + s) * kHaloBlocks + b;
-            unsigned spins = 0;
-            while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
-                if (++spins > g_mb.spin_limit ||
-                    ((spins & 255) == 0 && __hip_atomic_load(g_mb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
-                    __hip_atomic_store(g_mb.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    ready = 0;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
+        const bool ok = nbr < 0 || flag_wait(halo_flags(g_mb.self) + (par * kHaloSides + s) * kHaloBlocks + b, epoch);
+        const bool all = __all(ok);
+        if (s == 0) {
+            ready = all ? 1 : 0;
+            wait_note(kWaitHalo, t0);
         }
-        wait_note(kWaitHalo, t0);
     }
     __syncthreads();
     if (!ready) return;
