@@ -2076,4 +2076,98 @@ extern "C" int nkb_stream(nk_ctx* c, int64_t n, int variant, int grid, int reps,
     (void)hipFree(w);
     return NK_OK;
 }
+
+// The FD Jv's stream pattern without its arithmetic (the 2D march's floor): four reads (u, v,
+// F0, V_1) and one write per point, a dot kept live -- what the memory system gives 4R + 1W at all,
+// against the copy's 1R + 1W.  ORD 0 grid-stride, 1 block-contiguous chunks; U 16-B loads per stream.
+namespace nk {
+namespace {
+template <int U, int ORD>
+__global__ __launch_bounds__(kBlock) void k_stream_jv(int64_t n2, dx2* __restrict__ out, const dx2* __restrict__ a,
+                                                     const dx2* __restrict__ b, const dx2* __restrict__ f,
+                                                     const dx2* __restrict__ w, double* __restrict__ part) {
+    const int64_t nthr = (int64_t)gridDim.x * kBlock;
+    int64_t i, st, ust, end;
+    if constexpr (ORD == 1) {
+        const int64_t per = (n2 + gridDim.x - 1) / gridDim.x;
+        i = (int64_t)blockIdx.x * per + threadIdx.x;
+        end = (int64_t)(blockIdx.x + 1) * per < n2 ? (int64_t)(blockIdx.x + 1) * per : n2;
+        st = kBlock;
+        ust = (int64_t)U * kBlock;
+    } else {
+        i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+        end = n2;
+        st = nthr;
+        ust = nthr * U;
+    }
+    double acc = 0.0;
+    for (; i + (U - 1) * st < end; i += ust) {
+        dx2 x[U], y[U], z[U], t[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            x[u] = ld2<false>(a + i + u * st);
+            y[u] = ld2<false>(b + i + u * st);
+            z[u] = ld2<false>(f + i + u * st);
+            t[u] = ld2<false>(w + i + u * st);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            dx2 r;
+            r.x = fma(1e-7, y[u].x, x[u].x) - z[u].x;
+            r.y = fma(1e-7, y[u].y, x[u].y) - z[u].y;
+            acc = fma(t[u].x, r.x, acc);
+            acc = fma(t[u].y, r.y, acc);
+            st2<false>(out + i + u * st, r);
+        }
+    }
+    for (; i < end; i += st) {  // the remainder (fewer than U strides left)
+        const dx2 x = ld2<false>(a + i), y = ld2<false>(b + i), z = ld2<false>(f + i), t = ld2<false>(w + i);
+        dx2 r;
+        r.x = fma(1e-7, y.x, x.x) - z.x;
+        r.y = fma(1e-7, y.y, x.y) - z.y;
+        acc = fma(t.x, r.x, acc);
+        acc = fma(t.y, r.y, acc);
+        st2<false>(out + i, r);
+    }
+    if (acc == 12345.0) part[0] = acc;  // keeps the dot live
+}
+}  // namespace
+}  // namespace nk
+
+extern "C" int nkb_stream_jv(nk_ctx* c, int64_t n, int variant, int grid, int reps, double* us_out) {
+    using namespace nk;
+    if (!c || n < 2 || reps < 1 || !us_out) return NK_E_ARG;
+    double* buf[5] = {};
+    for (auto& x : buf) {
+        NK_HIP(c, hipMalloc(&x, sizeof(double) * n));
+        NK_TRY(launch_fill(c, n, x, 1.0));
+    }
+    const int g = grid > 0 ? grid : red_blocks(n);
+    const int64_t n2 = n / 2;
+    auto d = [&](int k) { return reinterpret_cast<dx2*>(buf[k]); };
+    double* part = red_slot(c);
+    auto go = [&] {
+        switch (variant) {
+        case 0: hipLaunchKernelGGL((k_stream_jv<1, 0>), dim3(g), dim3(kBlock), 0, c->stream, n2, d(0), d(1), d(2), d(3), d(4), part); break;
+        case 1: hipLaunchKernelGGL((k_stream_jv<2, 0>), dim3(g), dim3(kBlock), 0, c->stream, n2, d(0), d(1), d(2), d(3), d(4), part); break;
+        case 2: hipLaunchKernelGGL((k_stream_jv<2, 1>), dim3(g), dim3(kBlock), 0, c->stream, n2, d(0), d(1), d(2), d(3), d(4), part); break;
+        default: hipLaunchKernelGGL((k_stream_jv<4, 1>), dim3(g), dim3(kBlock), 0, c->stream, n2, d(0), d(1), d(2), d(3), d(4), part); break;
+        }
+    };
+    hipEvent_t a, b;
+    NK_HIP(c, hipEventCreate(&a));
+    NK_HIP(c, hipEventCreate(&b));
+    go();
+    NK_HIP(c, hipEventRecord(a, c->stream));
+    for (int r = 0; r < reps; ++r) go();
+    NK_HIP(c, hipEventRecord(b, c->stream));
+    NK_HIP(c, hipEventSynchronize(b));
+    float ms = 0.f;
+    NK_HIP(c, hipEventElapsedTime(&ms, a, b));
+    *us_out = 1e3 * ms / reps;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    for (auto x : buf) (void)hipFree(x);
+    return NK_OK;
+}
 #endif  // NK_KBENCH

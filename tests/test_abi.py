@@ -36,7 +36,7 @@ def test_product_library_has_no_kbench_hooks_or_knobs():
     build only, lib/libnkhip_kbench.so, which exports the nkb_* hooks and reads the knobs."""
     prod = open(_lib.PRODUCT_LIB, "rb").read()
     kb = open(_lib.KBENCH_LIB, "rb").read()
-    for sym in (b"nkb_copy", b"nkb_stencil_kind", b"nkb_mgs_res", b"nkb_update_x"):
+    for sym in (b"nkb_copy", b"nkb_stencil_kind", b"nkb_mgs_res", b"nkb_update_x", b"nkb_stream_jv"):
         assert sym not in prod, sym
         assert sym in kb, sym
     for k in KNOBS:
