@@ -40,6 +40,8 @@ ap.add_argument("--fault-rank", type=int, default=-1,
                      "bounded time; rank 0 records each rank's outcome")
 ap.add_argument("--pgrid", default="",
                 help="heat3d: px,py,pz -- 3D blocks (nk_dist_grid) instead of z-slabs; x / y ghost faces exchanged too")
+ap.add_argument("--check-errors", action="store_true",
+                help="with --pgrid: the process grid's refusals (a wrong grid, a grid after allocation, bc_periodic!)")
 ap.add_argument("--transport", choices=["rccl", "mailbox"], default="rccl",
                 help="rccl: nk_dist_init (RCCL bootstrap, then the peer mailbox / RCCL fallback); mailbox: "
                      "IPC handles exchanged over gloo, no RCCL at all (works with every rank on one GPU)")
@@ -77,8 +79,37 @@ if args.problem == "heat3d":  # 3D heat, implicit midpoint, z-slabs (k_st3l: the
     nz = args.nz
     if args.pgrid:  # 3D blocks: every vector allocated after the process grid carries its x / y faces
         pg = tuple(int(t) for t in args.pgrid.split(","))
+        early = None
+        if args.check_errors:  # a vector allocated BEFORE the process grid (no faces), and a wrong grid
+            early = ah.DeviceArray(ah.block((nx, ny, nz), rank, pg), ctx)
+            errs = {}
+            try:
+                ctx.set_process_grid(world + 1, 1, 1)
+            except ah.NKError as e:
+                errs["wrong_grid"] = str(e)
+            try:
+                ctx.set_process_grid(*pg)  # vectors exist: switching to blocks now is refused
+            except ah.NKError as e:
+                errs["after_alloc"] = str(e)
+            early.free()
         ctx.set_process_grid(*pg)
         grid = ah.block((nx, ny, nz), rank, pg)
+        if args.check_errors:
+            hx, hy, hz, a = 1.0 / (nx + 1), 1.0 / (ny + 1), 1.0 / (nz + 1), 0.01
+            un0 = ah.DeviceArray(grid, ctx)
+            r0 = un0.zero()
+            try:  # bc_periodic! keeps z-slabs
+                ah.G_Euler_.bind(ah.diffusion3d_)(r0, un0, (un0, 1e-3, None, (a, hx, hy, hz, ah.bc_periodic_), 0.0))
+                ctx.sync()
+            except ah.NKError as e:
+                errs["periodic"] = str(e)
+            outs = [None] * world
+            dist.all_gather_object(outs, errs)
+            if rank == 0:
+                json.dump(dict(errors=outs, world=world), open(args.out + ".json", "w"))
+            dist.barrier()
+            ctx.sync()
+            sys.exit(0)
     else:
         grid = ah.slab((nx, ny, nz), rank, world)
     x0, y0, z0 = grid.origin or (0, 0, grid.offset)

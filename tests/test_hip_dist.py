@@ -428,6 +428,24 @@ def test_heat3d_midpoint_blocks_match_oracle(tmp_path, pgrid, nxyz):
     assert np.max(np.abs(d["u"] - uo)) <= 1e-10
 
 
+def test_block_grid_refusals():
+    """nk_dist_grid's error behaviour on 2 ranks (1 x 2 x 1): a grid whose size is not the rank count and
+    a switch to blocks after a vector exists are NK_E_* errors (the context stays usable), and a
+    bc_periodic! residual on blocks is refused (periodic problems keep z-slabs) -- never wrong numbers."""
+    import tempfile as _tf
+
+    out = os.path.join(_tf.mkdtemp(), "err")
+    rc, log = run_ranks(2, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
+                            "--problem", "heat3d", "--nx", "16", "--ny", "12", "--nz", "10", "--pgrid", "1,2,1",
+                            "--check-errors"], worker_env(2))
+    assert rc == 0, log[-3000:]
+    meta = json.load(open(out + ".json"))
+    for errs in meta["errors"]:
+        assert "px * py * pz must equal the number of ranks" in errs["wrong_grid"], errs
+        assert "before allocating vectors" in errs["after_alloc"], errs
+        assert "bc_zero! only" in errs["periodic"], errs
+
+
 @pytest.mark.parametrize("pgrid", ["2,2,2", "4,2,1", "1,1,8"])
 def test_heat3d_blocks_fd_gmres_budget_matches_oracle(tmp_path, pgrid):
     """8 blocks of a 128 x 96 x 80 grid (64 x 48 x 40 or 32 x 48 x 80 per rank; 1,1,8: z-slabs as the
