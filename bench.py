@@ -599,18 +599,39 @@ def main():
         keys = [None] * world
         dist.all_gather_object(keys, (socket.gethostname(), ctx.path_info()["pci_bus_id"]))
         shared = len(set(keys)) < world
-    if shared and args.transport == "rccl":
+    # NK_BENCH_RCCL_FAIL=1 (test of the fallback below): every rank's RCCL bootstrap "fails" before it starts
+    fake_fail = os.environ.get("NK_BENCH_RCCL_FAIL") == "1"
+    if shared and args.transport == "rccl" and not fake_fail:
         raise SystemExit(f"bench.py: {world} ranks on {ndev} GPU(s): RCCL needs one GPU per rank "
                          "(use --transport mailbox with a small --side to rehearse on fewer GPUs)")
+    rccl_error = None
+    if world > 1 and args.transport == "rccl":
+        obj = [ah.dist_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        try:
+            if fake_fail:
+                raise ah.NKError("NK_BENCH_RCCL_FAIL")
+            ctx.init_distributed(rank, world, obj[0])
+        except ah.NKError as e:  # every rank learns below whether any rank failed
+            rccl_error = str(e)
+        errs = [None] * world
+        dist.all_gather_object(errs, rccl_error)
+        failed = [(r, e) for r, e in enumerate(errs) if e]
+        if failed:
+            # the RCCL bootstrap failed somewhere: every rank starts over on a fresh context with the
+            # mailbox alone (IPC handles over gloo) -- the line records it (config.transport)
+            rccl_error = f"rank {failed[0][0]}: {failed[0][1]}"
+            print(f"bench.py: rank {rank}: RCCL bootstrap failed ({rccl_error}); falling back to the peer mailbox over "
+                  "gloo", file=sys.stderr, flush=True)
+            ctx.close()
+            ctx = ah.Context(device)
+            ah.set_default_context(ctx)
+            args.transport = "mailbox"
     if world > 1 and args.transport == "mailbox":
         handles = [None] * world
         dist.all_gather_object(handles, ctx.mailbox_handle())
         ctx.mailbox_open(rank, world, b"".join(handles))
-    elif world > 1:
-        obj = [ah.dist_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        ctx.init_distributed(rank, world, obj[0])
-    elif os.environ.get("NK_DIST_FORCE") == "1":  # diagnostic: a 1-rank RCCL communicator (every reduction
+    elif world == 1 and os.environ.get("NK_DIST_FORCE") == "1":  # diagnostic: a 1-rank RCCL communicator (every reduction
         ctx.init_distributed(0, 1, ah.dist_unique_id())  # pays the all-reduce path on one GPU)
 
     if args.workload == "bratu2d":
@@ -776,6 +797,8 @@ def main():
                        "reorthogonalization": bool(getattr(W, "reorth", args.reorth == "on")),
                        "devices": (f"{min(world, ndev)} GPU(s) for {world} rank(s) (shared: rehearsal)" if shared
                                    else f"{world} GPU(s), one per rank"),
+                       "transport": (args.transport if world > 1 else "local")
+                                    + (f" (RCCL bootstrap failed: {rccl_error})" if rccl_error else ""),
                        "reductions": ("peer mailbox (IPC/xGMI)" if ctx.mailbox_active else
                                       ("ncclAllReduce" if world > 1 else "local")),
                        "path": {"mailbox_all_ranks": all(q["mailbox"] for q in paths),

@@ -172,6 +172,23 @@ def test_pgrid_factorisation():
 
 
 @pytest.mark.gpu
+def test_rccl_bootstrap_failure_falls_back_to_the_mailbox():
+    """A multi-GPU line must not be lost to an RCCL bootstrap failure: with NK_BENCH_RCCL_FAIL=1 every
+    rank's bootstrap "fails", all ranks agree over gloo, start over on fresh contexts with the peer mailbox
+    alone, and the line says so (config.transport) -- two ranks on the box's GPU(s)."""
+    args = ["--gpus", "2", "--side", "512", "--steps", "1", "--warmup", "1", "--no-prof", "--no-cpu-baseline"]
+    p = run(args, env={"NK_BENCH_RCCL_FAIL": "1"}, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(line) == 1
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert d["config"]["transport"].startswith("mailbox (RCCL bootstrap failed")
+    assert d["config"]["reductions"] == "peer mailbox (IPC/xGMI)"
+    assert "falling back to the peer mailbox" in p.stderr
+
+
+@pytest.mark.gpu
 def test_eight_rank_block_bench_rehearsal():
     """BASELINE config 5's decomposition end to end through bench.py: --workload heat3d --global-n 64
     --pgrid auto on 8 ranks (2 x 2 x 2 blocks of 32^3; sharing the box's GPU over the mailbox when it has
