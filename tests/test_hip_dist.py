@@ -393,12 +393,14 @@ def test_heat3d_midpoint_zslabs_match_oracle(tmp_path, world, nz):
     assert np.max(np.abs(d["u"] - uo)) <= 1e-10
 
 
-@pytest.mark.parametrize("pgrid,nxyz", [("2,2,2", (40, 20, 24)), ("2,1,1", (40, 20, 24)), ("1,2,1", (40, 20, 24)),
-                                         ("1,3,1", (33, 20, 17)), ("2,2,1", (38, 22, 64)), ("1,2,4", (16, 40, 72)),
-                                         ("4,2,1", (130, 18, 20))])
-def test_heat3d_midpoint_blocks_match_oracle(tmp_path, pgrid, nxyz):
+@pytest.mark.parametrize("pgrid,nxyz,scheme", [("2,2,2", (40, 20, 24), "midpoint"), ("2,1,1", (40, 20, 24), "midpoint"),
+                                                ("1,2,1", (40, 20, 24), "midpoint"), ("1,3,1", (33, 20, 17), "midpoint"),
+                                                ("2,2,1", (38, 22, 64), "midpoint"), ("1,2,4", (16, 40, 72), "midpoint"),
+                                                ("4,2,1", (130, 18, 20), "midpoint"), ("2,2,2", (48, 40, 36), "euler"),
+                                                ("4,2,1", (130, 18, 20), "euler")])
+def test_heat3d_midpoint_blocks_match_oracle(tmp_path, pgrid, nxyz, scheme):
     """BASELINE config 5's decomposition: 3D blocks (px x py x pz process grid, nk_dist_grid) of the 3D
-    heat operator (G_Midpoint!, alpha 0.3), mailbox transport with every rank on the box's GPU.  Each
+    heat operator (G_Midpoint!, alpha 0.3; G_Euler!, whose Krylov FD Jv recomputes F(u)), mailbox transport with every rank on the box's GPU.  Each
     vector's six ghost layers travel in one packed-face launch (k_faces_ipc: z planes into the ghost
     planes, x / y layers into the faces after the trailing plane, which k_st3l reads at the block's x / y
     edges).  Residual, exact and FD JVP bit-identical to the oracle on the whole grid, uneven splits
@@ -409,16 +411,19 @@ def test_heat3d_midpoint_blocks_match_oracle(tmp_path, pgrid, nxyz):
     out = str(tmp_path / "blk")
     rc, log = run_ranks(world, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
                                 "--problem", "heat3d", "--nx", str(nx), "--ny", str(ny), "--nz", str(nz),
-                                "--pgrid", pgrid], worker_env(world))
+                                "--pgrid", pgrid, "--scheme", scheme], worker_env(world))
     assert rc == 0, log[-3000:]
     meta = json.load(open(out + ".json"))
     assert meta["mailbox"] and meta["path"]["halo_waits"] > 0
+    if scheme == "euler":  # G_Euler!'s FD Jv in the Krylov solve recomputes F(u) -- faces of u included
+        assert meta["path"]["jv_fd_f0r"] > 0
     d = np.load(out + ".npz")
     rng = np.random.default_rng(9)
     un = rng.standard_normal((nz, ny, nx))
     u0 = un + 0.01 * rng.standard_normal((nz, ny, nx))
     v = rng.standard_normal((nz, ny, nx))
-    P = oc.heat3d_euler(nx, ny, nz, un=un, scheme="midpoint", alpha=0.3)
+    P = (oc.heat3d_euler(nx, ny, nz, un=un, scheme="midpoint", alpha=0.3) if scheme == "midpoint"
+         else oc.heat3d_euler(nx, ny, nz, un=un))
     np.testing.assert_array_equal(d["F"], oc.residual(P, u0))
     np.testing.assert_array_equal(d["jv"], oc.jv_exact(P, u0, v))
     np.testing.assert_array_equal(d["jvfd"], oc.jv_fd(P, u0, v, F0=d["F"], eps=1e-6))
