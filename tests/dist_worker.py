@@ -40,7 +40,7 @@ ap.add_argument("--fault-rank", type=int, default=-1,
                      "bounded time; rank 0 records each rank's outcome")
 ap.add_argument("--pgrid", default="",
                 help="heat3d: px,py,pz -- 3D blocks (nk_dist_grid) instead of z-slabs; x / y ghost faces exchanged too")
-ap.add_argument("--scheme", choices=["midpoint", "euler"], default="midpoint",
+ap.add_argument("--scheme", choices=["midpoint", "euler", "trapezoid"], default="midpoint",
                 help="heat3d: G_Midpoint!(alpha 0.3) or G_Euler! (whose FD Jv recomputes F(u): the F0R kernels)")
 ap.add_argument("--check-errors", action="store_true",
                 help="with --pgrid: the process grid's refusals (a wrong grid, a grid after allocation, bc_periodic!)")
@@ -124,7 +124,7 @@ if args.problem == "heat3d":  # 3D heat, implicit midpoint, z-slabs (k_st3l: the
     hx, hy, hz, a = 1.0 / (nx + 1), 1.0 / (ny + 1), 1.0 / (nz + 1), 0.01
     dt = 1.0 / (2.0 * a * (1 / hx ** 2 + 1 / hy ** 2 + 1 / hz ** 2))
     und = ah.DeviceArray.from_numpy(np.ascontiguousarray(un_glob[sl]), grid, ctx)
-    G = ah.G_Euler_ if args.scheme == "euler" else ah.G_Midpoint_(alpha=0.3)
+    G = {"euler": ah.G_Euler_, "trapezoid": ah.G_Trapezoid_}.get(args.scheme) or ah.G_Midpoint_(alpha=0.3)
     F_, p = G.bind(ah.diffusion3d_), (und, dt, None, (a, hx, hy, hz, ah.bc_zero_), 0.0)
     u = ah.DeviceArray.from_numpy(np.ascontiguousarray(u_glob[sl]), grid, ctx)
     res = u.zero()

@@ -397,10 +397,11 @@ def test_heat3d_midpoint_zslabs_match_oracle(tmp_path, world, nz):
                                                 ("1,2,1", (40, 20, 24), "midpoint"), ("1,3,1", (33, 20, 17), "midpoint"),
                                                 ("2,2,1", (38, 22, 64), "midpoint"), ("1,2,4", (16, 40, 72), "midpoint"),
                                                 ("4,2,1", (130, 18, 20), "midpoint"), ("2,2,2", (48, 40, 36), "euler"),
-                                                ("4,2,1", (130, 18, 20), "euler")])
+                                                ("4,2,1", (130, 18, 20), "euler"), ("2,2,2", (40, 20, 24), "trapezoid")])
 def test_heat3d_midpoint_blocks_match_oracle(tmp_path, pgrid, nxyz, scheme):
     """BASELINE config 5's decomposition: 3D blocks (px x py x pz process grid, nk_dist_grid) of the 3D
-    heat operator (G_Midpoint!, alpha 0.3; G_Euler!, whose Krylov FD Jv recomputes F(u)), mailbox transport with every rank on the box's GPU.  Each
+    heat operator (G_Midpoint!, alpha 0.3; G_Euler!, whose Krylov FD Jv recomputes F(u); G_Trapezoid!, whose
+    stencil reads u_n's faces too), mailbox transport with every rank on the box's GPU.  Each
     vector's six ghost layers travel in one packed-face launch (k_faces_ipc: z planes into the ghost
     planes, x / y layers into the faces after the trailing plane, which k_st3l reads at the block's x / y
     edges).  Residual, exact and FD JVP bit-identical to the oracle on the whole grid, uneven splits
@@ -423,7 +424,7 @@ def test_heat3d_midpoint_blocks_match_oracle(tmp_path, pgrid, nxyz, scheme):
     u0 = un + 0.01 * rng.standard_normal((nz, ny, nx))
     v = rng.standard_normal((nz, ny, nx))
     P = (oc.heat3d_euler(nx, ny, nz, un=un, scheme="midpoint", alpha=0.3) if scheme == "midpoint"
-         else oc.heat3d_euler(nx, ny, nz, un=un))
+         else oc.heat3d_euler(nx, ny, nz, un=un, scheme=scheme))
     np.testing.assert_array_equal(d["F"], oc.residual(P, u0))
     np.testing.assert_array_equal(d["jv"], oc.jv_exact(P, u0, v))
     np.testing.assert_array_equal(d["jvfd"], oc.jv_fd(P, u0, v, F0=d["F"], eps=1e-6))
