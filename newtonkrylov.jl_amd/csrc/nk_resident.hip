@@ -492,6 +492,20 @@ __global__ __launch_bounds__(kResThreads, 1) void k_mgs_res(ResArgs A) {
     for (int s = 0; s < A.rl; ++s) qw[(RV + s) * ss] = lq[s * kResThreads + tid];
 }
 
+// launch one instantiation and name it as rocprofv3 does (the profile entry's kernel: bench.py's PMC lookup)
+template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false, bool ALT = false,
+          int NTM = 0, bool NTS = false, int LB = 4>
+const char* go_res(dim3 g, dim3 b, size_t lds, hipStream_t s, const ResArgs& A) {
+    hipLaunchKernelGGL((k_mgs_res<RV, B, PRE, JV, ALT, NTM, NTS, LB>), g, b, lds, s, A);
+    static char name[80] = {};
+    if (!name[0]) {
+        auto tf = [](bool x) { return x ? "true" : "false"; };
+        std::snprintf(name, sizeof name, "nk::k_mgs_res<%d, %d, %s, %s, %s, %d, %s, %d>", RV, B, tf(PRE), tf(JV), tf(ALT), NTM,
+                      tf(NTS), LB);
+    }
+    return name;
+}
+
 template <int RV, int B = (RV > 80 ? 6 : RV > 64 ? 4 : 8), bool PRE = false, bool JV = false, bool ALT = false,
           int NTM = 0, bool NTS = false, int LB = 4>
 bool res_attr(size_t lds) {
@@ -691,49 +705,51 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
     // out), 3 np for a streamed point (q read and written every pass, each V once)
     const double dram = 8.0 * (double)n * (f * ((jin ? 5.0 : 2.0) + np) + (1.0 - f) * (3.0 * np));
     ++c->n_sweep_resident;
-    return launch(c, jin ? "arnoldi_step" : "mgs_sweep", bytes, [&] {
+    const char* kn = nullptr;
+    return launch_dyn(c, jin ? "arnoldi_step" : "mgs_sweep", [&] {
         const dim3 g(c->res_blocks), b(kResThreads);
         switch (rv) {
         case 0:
 #ifdef NK_KBENCH
-            if (jin) hipLaunchKernelGGL((k_mgs_res<0, 8, false, true>), g, b, lds, c->stream, A);
+            if (jin) kn = go_res<0, 8, false, true>(g, b, lds, c->stream, A);
             else
 #endif
-                hipLaunchKernelGGL(k_mgs_res<0>, g, b, lds, c->stream, A);
+                kn = go_res<0>(g, b, lds, c->stream, A);
             break;
-        case 16: hipLaunchKernelGGL(k_mgs_res<16>, g, b, lds, c->stream, A); break;
-        case 25: hipLaunchKernelGGL(k_mgs_res<25>, g, b, lds, c->stream, A); break;
-        case 48: hipLaunchKernelGGL(k_mgs_res<48>, g, b, lds, c->stream, A); break;
-        case 64: hipLaunchKernelGGL(k_mgs_res<64>, g, b, lds, c->stream, A); break;
+        case 16: kn = go_res<16>(g, b, lds, c->stream, A); break;
+        case 25: kn = go_res<25>(g, b, lds, c->stream, A); break;
+        case 48: kn = go_res<48>(g, b, lds, c->stream, A); break;
+        case 64: kn = go_res<64>(g, b, lds, c->stream, A); break;
         case 89:
 #ifdef NK_KBENCH
-            if (jin) hipLaunchKernelGGL((k_mgs_res<89, 6, false, true>), g, b, lds, c->stream, A);
-            else if (xv == 0) hipLaunchKernelGGL((k_mgs_res<89, 4, true>), g, b, lds, c->stream, A);
-            else if (xv == 1) hipLaunchKernelGGL((k_mgs_res<89, 4>), g, b, lds, c->stream, A);
-            else if (xv == 2) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, true>), g, b, lds, c->stream, A);
-            else if (xv == 3) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, false, 1>), g, b, lds, c->stream, A);
-            else if (xv == 4) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, false, 2>), g, b, lds, c->stream, A);
-            else if (xv == 5) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, false, 0, true>), g, b, lds, c->stream, A);
-            else if (xv == 6) hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, false, 0, true>), g, b, lds, c->stream, A);
-            else if (xv == 8) hipLaunchKernelGGL((k_mgs_res<89, 2, true>), g, b, lds, c->stream, A);
-            else if (xv == 9) hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, false, 0, false, 8>), g, b, lds, c->stream, A);
-            else if (xv == 10) hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, false, 0, false, 6>), g, b, lds, c->stream, A);
-            else if (xv == 11) hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, true>), g, b, lds, c->stream, A);
+            if (jin) kn = go_res<89, 6, false, true>(g, b, lds, c->stream, A);
+            else if (xv == 0) kn = go_res<89, 4, true>(g, b, lds, c->stream, A);
+            else if (xv == 1) kn = go_res<89, 4>(g, b, lds, c->stream, A);
+            else if (xv == 2) kn = go_res<89, 6, false, false, true>(g, b, lds, c->stream, A);
+            else if (xv == 3) kn = go_res<89, 6, false, false, false, 1>(g, b, lds, c->stream, A);
+            else if (xv == 4) kn = go_res<89, 6, false, false, false, 2>(g, b, lds, c->stream, A);
+            else if (xv == 5) kn = go_res<89, 6, false, false, false, 0, true>(g, b, lds, c->stream, A);
+            else if (xv == 6) kn = go_res<89, 4, true, false, false, 0, true>(g, b, lds, c->stream, A);
+            else if (xv == 8) kn = go_res<89, 2, true>(g, b, lds, c->stream, A);
+            else if (xv == 9) kn = go_res<89, 4, true, false, false, 0, false, 8>(g, b, lds, c->stream, A);
+            else if (xv == 10) kn = go_res<89, 4, true, false, false, 0, false, 6>(g, b, lds, c->stream, A);
+            else if (xv == 11) kn = go_res<89, 4, true, false, true>(g, b, lds, c->stream, A);
             else if (streamed && nts_env && pre_env)
-                hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, false, 0, true>), g, b, lds, c->stream, A);
-            else if (streamed && nts_env) hipLaunchKernelGGL((k_mgs_res<89, 6, false, false, false, 0, true>), g, b, lds, c->stream, A);
-            else if (pre_env) hipLaunchKernelGGL((k_mgs_res<89, 4, true>), g, b, lds, c->stream, A);
-            else hipLaunchKernelGGL(k_mgs_res<89>, g, b, lds, c->stream, A);
+                kn = go_res<89, 4, true, false, false, 0, true>(g, b, lds, c->stream, A);
+            else if (streamed && nts_env) kn = go_res<89, 6, false, false, false, 0, true>(g, b, lds, c->stream, A);
+            else if (pre_env) kn = go_res<89, 4, true>(g, b, lds, c->stream, A);
+            else kn = go_res<89>(g, b, lds, c->stream, A);
 #else
             (void)xv;
             (void)pre_env;
-            if (streamed) hipLaunchKernelGGL((k_mgs_res<89, 4, true, false, false, 0, true>), g, b, lds, c->stream, A);
-            else hipLaunchKernelGGL((k_mgs_res<89, 4, true>), g, b, lds, c->stream, A);
+            if (streamed) kn = go_res<89, 4, true, false, false, 0, true>(g, b, lds, c->stream, A);
+            else kn = go_res<89, 4, true>(g, b, lds, c->stream, A);
 #endif
             break;
-        default: hipLaunchKernelGGL(k_mgs_res<32>, g, b, lds, c->stream, A); break;
+        default: kn = go_res<32>(g, b, lds, c->stream, A); break;
         }
-    }, dram);
+        return bytes;
+    }, dram, &kn);
 }
 
 }  // namespace nk

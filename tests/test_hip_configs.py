@@ -109,9 +109,12 @@ def test_config4_slab_gmres_first_steps(ctx):
     ctx.prof_enable(1 << 20)
     kw = dict(restart=True, atol=0.0, rtol=0.0, itmax=12)
     ah.krylov_solve_(ws, ah.JacobianOperator(ah.bratu2d_, res, u, p, jv="fd"), res, history=True, **kw)
-    sweeps = ctx.prof_read().get("mgs_sweep", {}).get("launches", 0)
+    sweep = ctx.prof_read().get("mgs_sweep", {})
+    sweeps = sweep.get("launches", 0)
     ctx.prof_enable(0)
     assert sweeps > 0, "the (half-resident) MGS sweep did not run"
+    # the profile names the instantiation that ran, as rocprofv3 does: half of q streams, non-temporally
+    assert sweep["kernel"] == "nk::k_mgs_res<89, 4, true, false, false, 0, true, 4>", sweep["kernel"]
     x = ws.x.to_numpy()
     xo, sto, ho = oc.krylov_solve(P, ui, F0d, jv="fd", F0=F0d, memory=30, **kw)
     assert ws.stats.niter == sto["niter"] == 12
