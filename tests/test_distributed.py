@@ -1,4 +1,4 @@
-"""Multi-rank protocol of the slab decomposition, on CPU with gloo (world_size 2, 3 and 8: the driver's node size).
+"""Multi-rank protocol of the slab and 3D-block decompositions, on CPU with gloo (world_size 2, 3 and 8: the driver's node size).
 
 libnkhip.so's distributed path (nk_dist.cpp) does exactly two things beyond the single-GPU code:
 before every stencil application it fills the two ghost planes of the input vector with the
@@ -192,3 +192,86 @@ def test_periodic_ring_protocol(tmp_path, world):
     u = un + 0.01 * rng.standard_normal((NY, NX))
     P = oc.heat2d_euler(NX, NY, un=un, scheme="trapezoid", bc=oc.BC_PERIODIC)
     assert np.array_equal(np.load(out)["G"], oc.residual(P, u))
+
+
+# ----------------------------------------------------------------------------- 3D blocks (config 5)
+NB = (13, 10, 9)  # global nx, ny, nz: uneven splits on every axis
+
+
+def block_padded(a, pg, rank):
+    """One rank's block + one ghost layer on every side, exchanged like nk_dist.cpp's k_faces_ipc: the six
+    boundary layers (x faces gathered) to the neighbours of the px x py x pz grid, rank = (iz py + iy) px
+    + ix as block_nbr numbers them; zero on the physical boundary."""
+    px, py, pz = pg
+    ix, iy, iz = rank % px, (rank // px) % py, rank // (px * py)
+    nz, ny, nx = a.shape
+    pad = np.zeros((nz + 2, ny + 2, nx + 2))
+    pad[1:-1, 1:-1, 1:-1] = a
+    # (numpy axis, lower / upper side, neighbour or None): z, y, x
+    sides = [(0, 0, rank - px * py if iz > 0 else None), (0, 1, rank + px * py if iz + 1 < pz else None),
+             (1, 0, rank - px if iy > 0 else None), (1, 1, rank + px if iy + 1 < py else None),
+             (2, 0, rank - 1 if ix > 0 else None), (2, 1, rank + 1 if ix + 1 < px else None)]
+    reqs, got = [], []
+    for ax, hi, nbr in sides:
+        if nbr is None:
+            continue
+        layer = np.ascontiguousarray(np.take(a, -1 if hi else 0, axis=ax))
+        recv = torch.zeros(layer.shape, dtype=torch.float64)
+        reqs.append(dist.isend(torch.from_numpy(layer), nbr))
+        reqs.append(dist.irecv(recv, nbr))
+        got.append((ax, hi, recv))
+    for r in reqs:
+        r.wait()
+    for ax, hi, recv in got:
+        idx = [slice(1, -1)] * 3
+        idx[ax] = -1 if hi else 0
+        pad[tuple(idx)] = recv.numpy()
+    return pad
+
+
+def _block_worker(rank, world, port, out, pg):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = ah.block(NB, rank, pg)
+    (x0, y0, z0), (nxl, nyl, nzl) = g.origin, g.shape_xyz
+    sl = (slice(z0, z0 + nzl), slice(y0, y0 + nyl), slice(x0, x0 + nxl))
+    rng = np.random.default_rng(4)
+    un, u, v = (rng.standard_normal(NB[::-1]) for _ in range(3))
+    G = oc.heat3d_euler(*NB, un=un, scheme="midpoint", alpha=0.3)  # the global spacing and time step
+    # the stencil stand-in: the oracle on the padded block, its inner points kept (the ring holds the
+    # neighbours' layers, or the Dirichlet zeros)
+    upad, unpad, vpad = (block_padded(np.ascontiguousarray(w[sl]), pg, rank) for w in (u, un, v))
+    P = oc.Problem(G.kind, nxl + 2, nyl + 2, nzl + 2, hx=G.hx, hy=G.hy, hz=G.hz, a=G.a, dt=G.dt, un=unpad,
+                   alpha=G.alpha)
+    F = oc.residual(P, upad)[1:-1, 1:-1, 1:-1]
+    Jv = oc.jv_exact(P, upad, vpad)[1:-1, 1:-1, 1:-1]
+    t = torch.tensor([float(np.sum(F * F))], dtype=torch.float64)
+    dist.all_reduce(t)
+    parts = [None] * world
+    dist.all_gather_object(parts, dict(sl=sl, F=F, Jv=Jv))
+    if rank == 0:
+        full = {k: np.full(NB[::-1], np.nan) for k in ("F", "Jv")}
+        for d in parts:
+            for k in full:
+                full[k][d["sl"]] = d[k]
+        np.savez(out, nrm2=float(t.item()), **full)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("pg", [(2, 1, 1), (1, 2, 2), (2, 2, 2), (3, 1, 2)])
+def test_block_protocol_matches_single_domain(tmp_path, pg):
+    """The 3D-block protocol (ah.block's partition, block_nbr's rank numbering, six faces per exchange)
+    around the oracle's heat stencil (G_Midpoint!, alpha 0.3): residual and exact JVP of every block,
+    assembled, bit for bit the single-domain oracle's; the all-reduced ||F||^2 to rounding."""
+    world = int(np.prod(pg))
+    out = str(tmp_path / "blk.npz")
+    mp.spawn(_block_worker, args=(world, _free_port(), out, pg), nprocs=world, join=True)
+    d = np.load(out)
+    rng = np.random.default_rng(4)
+    un, u, v = (rng.standard_normal(NB[::-1]) for _ in range(3))
+    P = oc.heat3d_euler(*NB, un=un, scheme="midpoint", alpha=0.3)
+    F = oc.residual(P, u)
+    np.testing.assert_array_equal(d["F"], F)
+    np.testing.assert_array_equal(d["Jv"], oc.jv_exact(P, u, v))
+    assert abs(float(d["nrm2"]) - float(np.sum(F * F))) <= 1e-12 * float(np.sum(F * F))
