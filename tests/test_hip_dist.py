@@ -397,7 +397,8 @@ def test_heat3d_midpoint_zslabs_match_oracle(tmp_path, world, nz):
                                                 ("1,2,1", (40, 20, 24), "midpoint"), ("1,3,1", (33, 20, 17), "midpoint"),
                                                 ("2,2,1", (38, 22, 64), "midpoint"), ("1,2,4", (16, 40, 72), "midpoint"),
                                                 ("4,2,1", (130, 18, 20), "midpoint"), ("2,2,2", (48, 40, 36), "euler"),
-                                                ("4,2,1", (130, 18, 20), "euler"), ("2,2,2", (40, 20, 24), "trapezoid")])
+                                                ("4,2,1", (130, 18, 20), "euler"), ("2,2,2", (40, 20, 24), "trapezoid"),
+                                                ("2,2,2", (40, 20, 24), "midpoint-host")])
 def test_heat3d_midpoint_blocks_match_oracle(tmp_path, pgrid, nxyz, scheme):
     """BASELINE config 5's decomposition: 3D blocks (px x py x pz process grid, nk_dist_grid) of the 3D
     heat operator (G_Midpoint!, alpha 0.3; G_Euler!, whose Krylov FD Jv recomputes F(u); G_Trapezoid!, whose
@@ -409,13 +410,17 @@ def test_heat3d_midpoint_blocks_match_oracle(tmp_path, pgrid, nxyz, scheme):
     Newton / Krylov counts, so every inner product and Jv of the solve crossed the blocks correctly."""
     world = int(np.prod([int(t) for t in pgrid.split(",")]))
     nx, ny, nz = nxyz
+    host = scheme.endswith("-host")  # the mailbox (faces included) in host shared memory
+    scheme = scheme.replace("-host", "")
     out = str(tmp_path / "blk")
+    env = worker_env(world, **({"NK_DIST_MAILBOX": "host"} if host else {}))
     rc, log = run_ranks(world, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
                                 "--problem", "heat3d", "--nx", str(nx), "--ny", str(ny), "--nz", str(nz),
-                                "--pgrid", pgrid, "--scheme", scheme], worker_env(world))
+                                "--pgrid", pgrid, "--scheme", scheme], env)
     assert rc == 0, log[-3000:]
     meta = json.load(open(out + ".json"))
     assert meta["mailbox"] and meta["path"]["halo_waits"] > 0
+    assert meta["path"]["mailbox_host"] == host
     if scheme == "euler":  # G_Euler!'s FD Jv in the Krylov solve recomputes F(u) -- faces of u included
         assert meta["path"]["jv_fd_f0r"] > 0
     d = np.load(out + ".npz")
