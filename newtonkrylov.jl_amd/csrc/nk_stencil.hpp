@@ -917,14 +917,17 @@ void k_st2d(KArgs A0) {
 // same cap on all of them: 512^3 Euler FD Jv 1160 -> 1257 us, midpoint 1303 -> 2900 us with spills,
 // profiles/r04/ab_st3l_wpe.log)
 #ifndef NK_ST3L_WPE
-#define NK_ST3L_WPE(KIND, EPI, F0R) ((KIND == NK_HEAT3D_EULER && EPI == EPI_DOT && F0R) ? 4 : 1)
+#define NK_ST3L_WPE(KIND, EPI, F0R, BLK) ((KIND == NK_HEAT3D_EULER && EPI == EPI_DOT && F0R && NK_ST3L_WPE_BLK(BLK)) ? 4 : 1)
+#endif
+#ifndef NK_ST3L_WPE_BLK  // (A/B: 1 = the 4-wave cap for the BLK instance too)
+#define NK_ST3L_WPE_BLK(BLK) (!(BLK))
 #endif
 // BLK (3D blocks, nk_dist_grid): the x / y ghost layers come from the faces after the allocation's trailing
 // plane (KArgs::fy / fx, sides with a neighbour in KArgs::nbm) -- the left / right x-edges of the block's
 // first / last column through the edge slots (the right one as the periodic wrap's second slot), the halo
 // rows beyond the block's first / last row from the y faces; z keeps the ghost planes.
 template <int KIND, int MODE, int EPI, int VEC, bool PER = false, int NW = 8, bool F0R = false, bool BLK = false>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L_WPE(KIND, EPI, F0R)))) void k_st3l(KArgs A0) {
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L_WPE(KIND, EPI, F0R, BLK)))) void k_st3l(KArgs A0) {
     __shared__ double sh[kShN];
     const double* const et = nullptr;  // heat kinds: no exp
     bool rare_ = false;
