@@ -79,7 +79,7 @@ double* red_slot(nk_ctx* c) {
 
 int mb_check(nk_ctx* c) {
     if (c->mb_err && *(volatile int*)c->mb_err)
-        return fail(c, NK_E_RCCL, "peer all-reduce: a rank's value never arrived (timeout)");
+        return fail(c, NK_E_RCCL, "peer mailbox: a rank's reduction value or ghost layer never arrived (timeout)");
     if (c->res_err && *(volatile int*)c->res_err) {  // the resident sweep's grid was not co-resident
         *c->res_err = 0;
         c->res_ok = false;  // later solves use one launch per MGS pass

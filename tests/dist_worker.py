@@ -131,6 +131,26 @@ if args.problem == "heat3d":  # 3D heat, implicit midpoint, z-slabs (k_st3l: the
     vd = ah.DeviceArray.from_numpy(np.ascontiguousarray(v_glob[sl]), grid, ctx)
     out = u.zero()
     F_(res, u, p)
+    if args.fault_rank >= 0:  # a rank that stops exchanging: the others' next ghost-face exchange must fail
+        import time
+
+        outcome = dict(rank=rank, skipped=rank == args.fault_rank)
+        if rank != args.fault_rank:
+            t0 = time.perf_counter()
+            try:
+                F_(res, u, p)  # its exchange waits for the faulty rank's faces
+                ctx.sync()
+                outcome["error"] = None
+            except ah.NKError as e:
+                outcome["error"] = str(e)
+            outcome["seconds"] = time.perf_counter() - t0
+            outcome["path"] = ctx.path_info()
+        outs = [None] * world
+        dist.all_gather_object(outs, outcome)
+        if rank == 0:
+            json.dump(dict(fault=outs, world=world), open(args.out + ".json", "w"))
+        dist.barrier()
+        sys.exit(0)  # no ctx.sync(): the mailbox error is sticky on the ranks that timed out
     if args.krylov_itmax > 0:  # one restarted FD-GMRES(20) solve J x = F(u0), fixed budget
         ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=20))
         J = ah.JacobianOperator(F_, res, u, p, jv="fd")

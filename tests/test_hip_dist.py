@@ -516,6 +516,31 @@ def test_dead_rank_reduction_errors_in_bounded_time(tmp_path, world):
         assert o["path"]["mailbox"] and o["path"]["mailbox_error"], o
 
 
+def test_dead_rank_block_faces_error_in_bounded_time(tmp_path):
+    """3D blocks (2 x 2 x 2): rank 7 stops after the first residual and never pushes its faces again.  The
+    next residual (two packed-face exchanges, u and u_n; no reduction) of its three face neighbours (3,
+    5, 6) must end in an NK_E_* error within the spin limit, never a hang.  The others exchange only with
+    those neighbours or healthy ones: each completes, or -- when a neighbour's second exchange comes only
+    after that neighbour's own timeout -- errs in bounded time as well."""
+    out = str(tmp_path / "bfault")
+    env = worker_env(8, NK_MB_SPIN_LIMIT=str(1 << 18))
+    rc, log = run_ranks(8, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
+                            "--problem", "heat3d", "--nx", "24", "--ny", "20", "--nz", "16", "--pgrid", "2,2,2",
+                            "--fault-rank", "7"], env)
+    assert rc == 0, log[-3000:]
+    meta = json.load(open(out + ".json"))
+    for o in meta["fault"]:
+        if o["rank"] == 7:
+            assert o["skipped"]
+            continue
+        assert o["seconds"] < 60.0, o
+        if o["rank"] in (3, 5, 6):
+            assert o["error"] and "never arrived" in o["error"], o
+            assert o["path"]["mailbox_error"], o
+        else:
+            assert o["error"] is None or "never arrived" in o["error"], o
+
+
 def test_bench_exits_nonzero_on_a_stuck_rank(tmp_path):
     """`bench.py --gpus 2` whose rank 1 hangs before its first timed step (NK_BENCH_FAULT_RANK=1): rank 0's
     mailbox waits time out into an error, it exits non-zero, the launcher tears the job down -- the bench
