@@ -919,9 +919,10 @@ void k_st2d(KArgs A0) {
 #ifndef NK_ST3L_WPE
 #define NK_ST3L_WPE(KIND, EPI, F0R, BLK) ((KIND == NK_HEAT3D_EULER && EPI == EPI_DOT && F0R && NK_ST3L_WPE_BLK(BLK)) ? 4 : 1)
 #endif
-#ifndef NK_ST3L_WPE_BLK  // (A/B: 1 = the 4-wave cap for the BLK instance too)
-#define NK_ST3L_WPE_BLK(BLK) (!(BLK))
+#ifndef NK_ST3L_BLK_CAP  // (product variant build for A/B: 1 = the 4-wave cap for the BLK instance too)
+#define NK_ST3L_BLK_CAP 0
 #endif
+#define NK_ST3L_WPE_BLK(BLK) (NK_ST3L_BLK_CAP || !(BLK))
 // BLK (3D blocks, nk_dist_grid): the x / y ghost layers come from the faces after the allocation's trailing
 // plane (KArgs::fy / fx, sides with a neighbour in KArgs::nbm) -- the left / right x-edges of the block's
 // first / last column through the edge slots (the right one as the periodic wrap's second slot), the halo
