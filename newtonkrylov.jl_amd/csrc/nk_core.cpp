@@ -282,7 +282,7 @@ int nk_vec_alloc(nk_ctx* c, const nk_problem* p, double** out) {
     NK_HIP(c, hipStreamSynchronize(c->stream));
     double* interior = static_cast<double*>(base) + g.front + shift;
     c->allocs[interior] = base;
-    if (faces) c->faced.insert(interior);
+    if (faces) c->faced[interior] = faces;
     *out = interior;
     return NK_OK;
 }

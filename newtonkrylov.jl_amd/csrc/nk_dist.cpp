@@ -49,7 +49,10 @@ int halo_exchange(nk_ctx* c, const nk_problem* p, const double* v) {
     NK_TRY(geometry(c, p, &g));
     double* vv = const_cast<double*>(v);  // only the ghost planes are written
     if (blocks3d(c, g)) {  // 3D blocks: all six ghost layers, through the peer mailbox
-        if (!c->faced.count(vv)) return fail(c, NK_E_STATE, "3D blocks: a vector allocated before nk_dist_grid has no ghost faces");
+        const auto fit = c->faced.find(vv);
+        if (fit == c->faced.end()) return fail(c, NK_E_STATE, "3D blocks: a vector allocated before nk_dist_grid has no ghost faces");
+        if (face_words(c, p, g) > fit->second)
+            return fail(c, NK_E_ARG, "3D blocks: the vector's ghost faces are smaller than this problem's (allocated for another grid)");
         if (!c->mb_on) return fail(c, NK_E_STATE, "3D blocks exchange their ghost faces through the peer mailbox (it is off)");
         const int64_t big = std::max({p->nx * p->ny, p->nx * p->nz, p->ny * p->nz});
         if (big > c->halo_cap) return fail(c, NK_E_ARG, "3D blocks: a ghost face is larger than the IPC inbox (NK_HALO_CAP)");

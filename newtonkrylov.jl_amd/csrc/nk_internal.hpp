@@ -56,7 +56,7 @@ struct nk_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     std::unordered_map<double*, void*> allocs;  // interior pointer -> allocation base
-    std::unordered_set<double*> faced;          // 3D blocks: the vectors that carry x / y ghost faces
+    std::unordered_map<double*, int64_t> faced;  // 3D blocks: the vectors that carry x / y ghost faces (-> their size)
     unsigned alloc_seq = 0;                     // vectors allocated so far (their start offsets, §3)
     double* red = nullptr;                      // kRedSlots * kRedCap partial sums
     double* scal = nullptr;                     // kScalCap device scalars
