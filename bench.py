@@ -90,6 +90,12 @@ def parse():
                     help="with --global-n on ONE GPU: run the slab one rank of a --slab-of-way decomposition owns "
                          "(rank slab_of // 2, ghost planes zero, no exchange) -- the per-GPU compute of configs 4 / 5 "
                          "before an 8-GPU node is available (--global-n 16384 --slab-of 8)")
+    ap.add_argument("--block-of", type=int, default=0,
+                    help="heat3d with --global-n G: run ONE rank's block of the N-way 3D-block split (--pgrid auto of N; "
+                         "BASELINE config 5: 2x2x2 of 256^3 at G = 512) alone on one GPU, through the block path: the "
+                         "BLK stencil instances read x / y ghost faces, and one packed six-face exchange per Jv runs "
+                         "over a forced one-rank mailbox whose rank is its own neighbour on every side (NK_HALO_SELF=2 "
+                         "rig: every axis wraps onto the block itself -- the cost is what is measured)")
     ap.add_argument("--pgrid", default="",
                     help="heat3d --global-n with N > 1 ranks: 3D blocks px,py,pz (nk_dist_grid; 'auto': the most "
                          "cubic factorisation of N -- 2,2,2 at N = 8, BASELINE config 5's 256^3 blocks) instead of "
@@ -247,7 +253,7 @@ def config2_reference():
     return None
 
 
-def scaling_fields(value, dof_per_unit, paths, workload, slab_of, world, global_n, ref=None):
+def scaling_fields(value, dof_per_unit, paths, workload, slab_of, world, global_n, ref=None, block_of=0):
     """The multi-GPU part of the JSON line (a pure function: tests/test_bench_launcher.py checks an 8-rank
     assembly on CPU).  dof_rate: the north star's >= 6x at 8 GPUs as a per-DoF rate -- DoF x matvecs / s of
     this line against the single-GPU config-2 line (a one-rank slab line has no exchange: its ratio is the
@@ -261,7 +267,8 @@ def scaling_fields(value, dof_per_unit, paths, workload, slab_of, world, global_
         out["dof_rate"] = {"dof_matvecs_per_s": round(dof, 1),
                            "vs_config2_single_gpu": round(dof / ref["value"], 3) if ref else None,
                            "config2_reference": ref["source"] if ref else None,
-                           "exchange": "none (one rank's slab alone)" if slab_of else "included"}
+                           "exchange": ("none (one rank's slab alone)" if slab_of else
+                                        "self faces on one GPU (no xGMI)" if block_of else "included")}
     if world > 1:
         out["ranks"] = paths  # per rank: transport, resident sweep, in-launch ghost planes, launch counts, cost
         ex = [q.get("exchange") or {} for q in paths]
@@ -413,7 +420,7 @@ class HeatEuler:
     --scheme / --bc: the same loop with G_Midpoint! / G_Trapezoid! and bc_periodic!."""
 
     def __init__(self, args, ctx, rank, world, dim):
-        parts = args.slab_of or world
+        parts = args.slab_of or args.block_of or world
         if args.slab_of:
             rank = parts // 2
         self.pgrid = None
@@ -421,6 +428,9 @@ class HeatEuler:
             if not args.global_n:
                 raise SystemExit("--pgrid splits one --global-n problem into blocks")
             self.pgrid = pgrid_of(args.pgrid, world)
+        if args.block_of:  # rank 0's block of the most cubic split (no process grid: the rig's one rank)
+            self.pgrid = pgrid_of(args.pgrid or "auto", args.block_of)
+            rank = 0
         if args.global_n:  # strong scaling: one global G^dim problem, G / world slab planes per rank
             n = args.global_n
             if n % parts and not self.pgrid:
@@ -443,7 +453,8 @@ class HeatEuler:
         sines = [np.sin(np.pi * np.arange(1, n + 1) * hs[0])]
         rows0 = rank * planes
         if self.pgrid:  # 3D blocks: the process grid first (every vector then carries its x / y faces)
-            ctx.set_process_grid(*self.pgrid)
+            if not args.block_of:  # (--block-of: the NK_HALO_SELF=2 rig gives the lone rank's vectors faces)
+                ctx.set_process_grid(*self.pgrid)
             grid = ah.block(glob, rank, self.pgrid)
             (x0, y0, z0), (nxl, nyl, nzl) = grid.origin, grid.shape_xyz
             zs = np.sin(np.pi * np.arange(z0 + 1, z0 + nzl + 1) * hs[2])
@@ -484,6 +495,10 @@ class HeatEuler:
         bcname = "" if args.bc == "zero" else ", bc_periodic!"
         slab = (f"; rank {rank}'s slab of the {parts}-way split ALONE on one GPU (ghost planes zero, no exchange)"
                 if args.slab_of else "")
+        if args.block_of:
+            slab = (f"; rank 0's block of the {parts}-way block split ALONE on one GPU, its six ghost faces exchanged "
+                    "every Jv with itself over a forced one-rank mailbox (NK_HALO_SELF=2: the operator wraps every "
+                    "axis onto the block; value = the global matvec rate with this exchange form, without xGMI)")
         self.workload = (f"{dim}D heat {sname}{bcname} {shape} ({per_gpu}), one time step per step: "
                          f"newton_krylov! tol_abs=6e-6, GMRES memory {args.memory or 20} (unrestarted, "
                          f"reorthogonalization={'true' if self.reorth else 'false'}), "
@@ -571,6 +586,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.slab_of and (world > 1 or not args.global_n):
         raise SystemExit("--slab-of runs one rank's slab of a --global-n problem on ONE GPU (--gpus 1)")
+    if args.block_of:
+        if world > 1 or not args.global_n or args.workload != "heat3d" or args.slab_of:
+            raise SystemExit("--block-of runs one rank's 3D block of a --global-n heat3d problem on ONE GPU (--gpus 1)")
+        # the rig (read by the library at its first use): a forced one-rank mailbox, the rank its own
+        # neighbour on all six sides
+        os.environ.update(NK_DIST_FORCE="1", NK_DIST_MAILBOX="1", NK_HALO_SELF="2")
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)", file=sys.stderr)
         sys.exit(2)
@@ -599,24 +620,40 @@ def main():
         keys = [None] * world
         dist.all_gather_object(keys, (socket.gethostname(), ctx.path_info()["pci_bus_id"]))
         shared = len(set(keys)) < world
-    # NK_BENCH_RCCL_FAIL=1 (test of the fallback below): every rank's RCCL bootstrap "fails" before it starts
-    fake_fail = os.environ.get("NK_BENCH_RCCL_FAIL") == "1"
-    if shared and args.transport == "rccl" and not fake_fail:
+    # NK_BENCH_RCCL_FAIL (tests of the fallback below): "1" -- every rank's RCCL bootstrap "fails" before it
+    # starts; "rank:K" -- only rank K's local pre-check fails
+    fake = os.environ.get("NK_BENCH_RCCL_FAIL", "")
+    fake_fail = fake == "1" or (fake.startswith("rank:") and fake[5:] == str(rank))
+    if shared and args.transport == "rccl" and not fake:
         raise SystemExit(f"bench.py: {world} ranks on {ndev} GPU(s): RCCL needs one GPU per rank "
                          "(use --transport mailbox with a small --side to rehearse on fewer GPUs)")
     rccl_error = None
     if world > 1 and args.transport == "rccl":
-        obj = [ah.dist_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
+        # ncclCommInitRank is collective: a rank that fails before entering it would leave the others
+        # blocked inside it.  So every rank first probes RCCL locally (its library answers a unique-id
+        # request on this rank's device) and the ranks vote over gloo; only a unanimous vote enters the
+        # collective init.  A failure INSIDE the init that not every rank sees can still block the
+        # others there -- the launcher's time limit is then what ends the job.
+        obj = [None]
         try:
             if fake_fail:
                 raise ah.NKError("NK_BENCH_RCCL_FAIL")
-            ctx.init_distributed(rank, world, obj[0])
-        except ah.NKError as e:  # every rank learns below whether any rank failed
+            uid = ah.dist_unique_id()
+            obj = [uid if rank == 0 else None]
+        except ah.NKError as e:
             rccl_error = str(e)
-        errs = [None] * world
-        dist.all_gather_object(errs, rccl_error)
-        failed = [(r, e) for r, e in enumerate(errs) if e]
+        pre = [None] * world
+        dist.all_gather_object(pre, rccl_error)
+        failed = [(r, e) for r, e in enumerate(pre) if e]
+        if not failed:
+            dist.broadcast_object_list(obj, src=0)
+            try:
+                ctx.init_distributed(rank, world, obj[0])
+            except ah.NKError as e:  # (an error every rank returns from: each learns below)
+                rccl_error = str(e)
+            errs = [None] * world
+            dist.all_gather_object(errs, rccl_error)
+            failed = [(r, e) for r, e in enumerate(errs) if e]
         if failed:
             # the RCCL bootstrap failed somewhere: every rank starts over on a fresh context with the
             # mailbox alone (IPC handles over gloo) -- the line records it (config.transport)
@@ -687,7 +724,8 @@ def main():
     path["host"] = socket.gethostname()
     path["exchange"] = exchange_cost(path0, path, args.steps, elapsed)
     path["launches"] = {k: prof.get(k, {}).get("launches", 0)
-                        for k in ("mgs_sweep", "mgs_pass", "mgs_pass_last", "halo_ipc", "halo_rccl", "allreduce")}
+                        for k in ("mgs_sweep", "mgs_pass", "mgs_pass_last", "halo_ipc", "halo_faces", "halo_rccl",
+                                  "allreduce")}
     paths = [path]
     if dist is not None:
         paths = [None] * world
@@ -792,7 +830,8 @@ def main():
             "dtype": "f64",
             "data": "synthetic (see config.workload)",
             "config": {"workload": W.workload, "matvecs_per_step": matvecs // max(1, args.steps),
-                       "parallelism": (("blocks" + "x".join(str(m) for m in W.pgrid)) if getattr(W, "pgrid", None)
+                       "parallelism": ((f"block 1 of {args.block_of} (one GPU, self faces)") if args.block_of else
+                                       ("blocks" + "x".join(str(m) for m in W.pgrid)) if getattr(W, "pgrid", None)
                                        else (f"slab{world}" if not args.slab_of else f"slab 1 of {args.slab_of} (one GPU)")),
                        "reorthogonalization": bool(getattr(W, "reorth", args.reorth == "on")),
                        "devices": (f"{min(world, ndev)} GPU(s) for {world} rank(s) (shared: rehearsal)" if shared
@@ -821,7 +860,10 @@ def main():
                                     "thread, non-temporal load + store (the fastest copy of tools/stream_probe.py), "
                                     "mean of 5 launches, after the timed region"},
         }
-        out.update(scaling_fields(value, W.dof_per_unit, paths, args.workload, args.slab_of, world, args.global_n))
+        out.update(scaling_fields(value, W.dof_per_unit, paths, args.workload, args.slab_of, world, args.global_n,
+                                  block_of=args.block_of))
+        if args.block_of:
+            out["ranks"] = paths  # the rig's path report: faces exchanged, BLK instances, peer waits
         if world == 1 and not args.no_cpu_baseline and not args.global_n:
             # the node's host cores: the fastest thread count the process's affinity mask offers (the
             # headline figure), and the per-GPU share the box gives one GPU (OMP_NUM_THREADS, 16 there)

@@ -25,10 +25,48 @@ struct MbInfo {
                                // planes, 1 cross-rank reductions (null: not counted)
 };
 hipError_t resident_bind_mb(const MbInfo& m);  // nk_resident.hip's copy of g_mb
+hipError_t kernels_bind_mb(const MbInfo& m);   // nk_kernels.hip's copy
+// the stencil instantiation units' copies (nk_stencil_inst.hip, one per problem kind)
+hipError_t stencil_bind_mb_1(const MbInfo& m);
+hipError_t stencil_bind_mb_2(const MbInfo& m);
+hipError_t stencil_bind_mb_3(const MbInfo& m);
+hipError_t stencil_bind_mb_4(const MbInfo& m);
+hipError_t stencil_bind_mb_5(const MbInfo& m);
+hipError_t stencil_bind_mb_6(const MbInfo& m);
+hipError_t stencil_bind_mb_7(const MbInfo& m);
+hipError_t stencil_bind_mb_8(const MbInfo& m);
 
 typedef double dx2 __attribute__((ext_vector_type(2)));  // 16-B streaming element
 
 namespace {
+
+// ------------------------------------------------------------------------------ streaming order
+// Block-contiguous chunks of `len` elements (a multiple of the block size), threads interleaved
+// inside the chunk: each block streams one address range -- fewer DRAM page switches than the
+// grid-stride order once the vectors outgrow the Infinity Cache (tools/stream_probe.py).
+struct Chunk {
+    int64_t lo, hi;
+};
+__device__ __forceinline__ Chunk block_chunk(int64_t len) {
+    const int64_t per = ((len + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
+    const int64_t lo = (int64_t)blockIdx.x * per;
+    return Chunk{lo, lo + per < len ? lo + per : len};
+}
+#define NK_CHUNKED(i, len)                    \
+    const Chunk ck_ = block_chunk(len);       \
+    for (int64_t i = ck_.lo + threadIdx.x; i < ck_.hi; i += kBlock)
+
+// 16-B loads / stores, non-temporal (NT: streamed past the caches' retention) or plain
+template <bool NT>
+__device__ __forceinline__ dx2 ld2(const dx2* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st2(dx2* p, dx2 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 
 // ------------------------------------------------------------------------------ reductions
 __device__ __forceinline__ double wave_sum(double v) {

@@ -157,20 +157,26 @@ static bool mb_force_host() {
     return e && std::strcmp(e, "host") == 0;
 }
 
-// this host: FNV-1a of the host name and the kernel's boot id (a segment name is only meaningful on the
-// host -- and the boot -- that created it)
+// this host: FNV-1a of the kernel's boot id (a segment name is only meaningful on the kernel -- and the
+// boot -- that created it).  The boot id alone: containers of one machine that share /dev/shm
+// (--ipc=host) carry different host names but one kernel.  Only where no boot id can be
+// read does the host name stand in.
 static uint64_t host_identity() {
     uint64_t h = 1469598103934665603ull;
     auto mix = [&h](const char* t, size_t n) {
         for (size_t i = 0; i < n && t[i]; ++i) h = (h ^ (unsigned char)t[i]) * 1099511628211ull;
     };
     char buf[256] = {0};
-    if (gethostname(buf, sizeof(buf) - 1) == 0) mix(buf, sizeof(buf));
-    std::memset(buf, 0, sizeof(buf));
+    bool boot = false;
     if (FILE* f = std::fopen("/proc/sys/kernel/random/boot_id", "r")) {
-        if (std::fgets(buf, sizeof(buf), f)) mix(buf, sizeof(buf));
+        boot = std::fgets(buf, sizeof(buf), f) != nullptr && buf[0];
         std::fclose(f);
     }
+    if (!boot) {
+        std::memset(buf, 0, sizeof(buf));
+        if (gethostname(buf, sizeof(buf) - 1) != 0) buf[0] = 0;
+    }
+    mix(buf, sizeof(buf));
     return h;
 }
 
@@ -282,6 +288,21 @@ void mb_free(nk_ctx* c) {
     c->mb_wacc = nullptr;
 }
 
+// the region of the two that the agreed mailbox does not use (both when the mailbox is off)
+static void mb_free_unused(nk_ctx* c) {
+    if ((!c->mb_on || c->mb_host) && c->mb_dev) {
+        (void)hipFree(c->mb_dev);
+        c->mb_dev = nullptr;
+    }
+    if ((!c->mb_on || !c->mb_host) && c->mb_host_base) {
+        (void)hipHostUnregister(c->mb_host_base);
+        munmap(c->mb_host_base, c->mb_host_bytes);
+        mb_host_unlink(c);
+        c->mb_host_base = nullptr;
+        c->mb_host_dev = nullptr;
+    }
+}
+
 // map a peer's host segment: its device address for my kernels
 static int mb_map_host_peer(nk_ctx* c, int r, const char* rec, uint64_t** out) {
     HostHandle h;
@@ -391,6 +412,7 @@ static int mb_open_peers(nk_ctx* c, int rank, int nranks, const char* handles, c
         for (int q = 0; q < nranks; ++q) cnt += std::memcmp(busids + 32 * (size_t)r, busids + 32 * (size_t)q, 32) == 0;
         most = std::max(most, cnt);
     }
+    c->share_most = most;
     c->xchg_nb = std::max(16, kHaloBlocks / std::max(1, most));
     NK_HIP(c, hipMalloc(reinterpret_cast<void**>(&c->mb_peers_dev), sizeof(uint64_t*) * nranks));
     NK_HIP(c, hipMemcpy(c->mb_peers_dev, peers.data(), sizeof(uint64_t*) * nranks, hipMemcpyHostToDevice));
@@ -567,6 +589,9 @@ int nk_dist_init(nk_ctx* c, int32_t rank, int32_t nranks, const char id[128]) {
             c->err.clear();
         }
         mb_host_unlink(c);  // every rank has mapped it (or gave up) by the verdict
+        // past the verdict no peer maps the region this rank does not use (device mappings are closed
+        // before any rank opens the host ones): free it (96 MiB of fine-grained memory)
+        mb_free_unused(c);
     }
     return NK_OK;
 }

@@ -111,6 +111,7 @@ struct nk_ctx {
     unsigned res_tag = 0;                  // granule tags handed out so far
     int res_blocks = 0, res_rl = 0;        // grid (= CUs) and LDS double2 slots per thread
     int res_share = 1;                     // ranks on this GPU (NK_RES_SHARED: each sweep grid gets CUs / res_share)
+    int share_most = 1;                    // the most ranks on any one GPU -- the same on every rank (mailbox set-up)
     int xchg_nb = 256;                     // exchange-kernel grid (<= kHaloBlocks), the same on every rank: kHaloBlocks / the most
                                            // ranks sharing one GPU, so every sharing rank's spinning exchange grid fits at once
     uint64_t* res_tstamp = nullptr;        // kernel-variant bench only (nkb_mgs_res, NK_RES_TSTAMP)
@@ -218,6 +219,7 @@ struct Red {
     unsigned epoch = 0;     // mailbox epoch the producing kernel published under (0: none)
 };
 double* red_slot(nk_ctx* c);                 // next partial-sum slot of the ring
+unsigned next_mb_epoch(nk_ctx* c);           // the next peer-mailbox epoch (1 .. 65535)
 double* red_out(nk_ctx* c, int len, Red* r, int* fin);  // slot for a reduction launch (+ fold flag)
 int finish_reduction(nk_ctx* c, Red* r);     // multi-rank: collapse + RCCL all-reduce
 int mb_check(nk_ctx* c);                     // after a host sync: did a mailbox wait time out?
@@ -244,6 +246,8 @@ constexpr int kHaloSides = 6;                // ghost layers by the side they co
                                              // upper neighbour (slabs; z of 3D blocks), 2 / 3 y, 4 / 5 x (3D blocks)
 constexpr int kHaloTileFlags = 4096;         // stencil tiles per plane whose ghost patch travels in the stencil itself
 constexpr int64_t kSharedFuseMax = (int64_t)1 << 20;  // ranks sharing a GPU: in-launch ghost planes up to this many points
+// per slab (rank-uniform estimate: shared_slab_points); NK_SHARED_FUSE_MAX overrides it (test rigs)
+int64_t shared_slab_points(const nk_ctx* c, const nk_problem* p, const Geo& g);
 // one fine-grained region per rank, IPC-mapped by every other rank:
 //   [mailbox: kMbSlots x kMbRanks x 2 u64][halo flags: 2 parity x kHaloSides x kHaloBlocks u64]
 //   [tile flags: 2 parity x 2 sides x kHaloTileFlags u64]
@@ -279,6 +283,9 @@ struct StencilIn {
 };
 // returns the partial sums (when epi != EPI_NONE) in *red
 int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red);
+// the same with the kernel-variant bench's overrides (rows / planes per tile, variant bits; 0, 0: the product)
+int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_override, int fast);
+int wide_blocks(int64_t n);                  // grid of the streaming kernels whose partials only a finaliser reads
 
 int launch_dot(nk_ctx* c, int64_t n, const double* x, const double* y, Red* red);
 int launch_sumsq(nk_ctx* c, int64_t n, const double* x, Red* red);

@@ -156,7 +156,7 @@ if args.problem == "heat3d":  # 3D heat, implicit midpoint, z-slabs (k_st3l: the
         J = ah.JacobianOperator(F_, res, u, p, jv="fd")
         ah.krylov_solve_(ws, J, res, restart=True, atol=0.0, rtol=0.0, itmax=args.krylov_itmax, history=True)
         parts = [None] * world
-        dist.all_gather_object(parts, dict(sl=sl, x=ws.x.to_numpy(), F=res.to_numpy()))
+        dist.all_gather_object(parts, dict(sl=sl, x=ws.x.to_numpy(), F=res.to_numpy(), path=ctx.path_info()))
         if rank == 0:
             full = {}
             for key in ("x", "F"):
@@ -164,7 +164,8 @@ if args.problem == "heat3d":  # 3D heat, implicit midpoint, z-slabs (k_st3l: the
                 for d in parts:
                     full[key][d["sl"]] = d[key]
             np.savez(args.out + ".npz", h=np.array(ws.stats.residuals), **full)
-            json.dump(dict(niter=ws.stats.niter, n_matvec=ws.stats.n_matvec, world=world, path=ctx.path_info()),
+            json.dump(dict(niter=ws.stats.niter, n_matvec=ws.stats.n_matvec, world=world, path=ctx.path_info(),
+                           paths=[d["path"] for d in parts], planes=[d["sl"][0].stop - d["sl"][0].start for d in parts]),
                       open(args.out + ".json", "w"))
         dist.barrier()
         ctx.sync()

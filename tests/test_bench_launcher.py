@@ -172,18 +172,23 @@ def test_pgrid_factorisation():
 
 
 @pytest.mark.gpu
-def test_rccl_bootstrap_failure_falls_back_to_the_mailbox():
+@pytest.mark.parametrize("fail", ["1", "rank:1"])
+def test_rccl_bootstrap_failure_falls_back_to_the_mailbox(fail):
     """A multi-GPU line must not be lost to an RCCL bootstrap failure: with NK_BENCH_RCCL_FAIL=1 every
-    rank's bootstrap "fails", all ranks agree over gloo, start over on fresh contexts with the peer mailbox
-    alone, and the line says so (config.transport) -- two ranks on the box's GPU(s)."""
+    rank's bootstrap "fails"; with rank:1 only rank 1's local pre-check does (the other rank
+    must not be left alone inside the collective init).  All ranks agree over gloo, start over on fresh
+    contexts with the peer mailbox alone, and the line says so (config.transport) -- two ranks on the
+    box's GPU(s)."""
     args = ["--gpus", "2", "--side", "512", "--steps", "1", "--warmup", "1", "--no-prof", "--no-cpu-baseline"]
-    p = run(args, env={"NK_BENCH_RCCL_FAIL": "1"}, timeout=240)
+    p = run(args, env={"NK_BENCH_RCCL_FAIL": fail}, timeout=240)
     assert p.returncode == 0, p.stderr[-2000:]
     line = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
     assert len(line) == 1
     d = json.loads(line[0])
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["config"]["transport"].startswith("mailbox (RCCL bootstrap failed")
+    if fail == "rank:1":
+        assert "rank 1: NK_BENCH_RCCL_FAIL" in d["config"]["transport"]
     assert d["config"]["reductions"] == "peer mailbox (IPC/xGMI)"
     assert "falling back to the peer mailbox" in p.stderr
 

@@ -393,6 +393,43 @@ def test_heat3d_midpoint_zslabs_match_oracle(tmp_path, world, nz):
     assert np.max(np.abs(d["u"] - uo)) <= 1e-10
 
 
+@pytest.mark.parametrize("fuse_max,form", [(20000, "fused"), (10000, "separate"), (5000, "separate")])
+def test_shared_gpu_ghost_plane_form_is_rank_uniform(tmp_path, fuse_max, form):
+    """Ranks sharing one GPU carry a Krylov Jv's ghost planes inside the stencil launch only for slabs up
+    to kSharedFuseMax points (a big slab's end tiles spin on CUs the peer's producing tiles need: the r05
+    30 s/step stall), else through the exchange kernel.  The two forms use different flags, so neighbours
+    must agree: the test takes rank-uniform values only -- the most ranks on one GPU and the
+    largest slab of an even split from the global spacing.  Two ranks, 3D heat 40 x 20 x 25 split 13 / 12
+    planes of 800 points (10400 / 9600), the limit set with NK_SHARED_FUSE_MAX: 10000 lies BETWEEN the two
+    local slab sizes (rank-local tests disagreed there and both ranks timed out).  Every rank takes the
+    same form: in-launch above both sizes, the exchange kernel otherwise -- and 20 FD-GMRES(20) steps give
+    the same bits either way (the form moves no arithmetic)."""
+    out = str(tmp_path / "form")
+    env = worker_env(2, NK_SHARED_FUSE_MAX=str(fuse_max))
+    rc, log = run_ranks(2, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
+                            "--problem", "heat3d", "--scheme", "euler", "--nx", "40", "--ny", "20", "--nz", "25",
+                            "--krylov-itmax", "20"], env)
+    assert rc == 0, log[-3000:]
+    meta = json.load(open(out + ".json"))
+    assert sorted(meta["planes"]) == [12, 13]
+    for q in meta["paths"]:
+        assert q["ranks_on_device"] == 2 or ah.device_count() >= 2, q
+        assert not q["mailbox_error"], q
+        if form == "fused":
+            assert q["jv_halo_fused"] > 0 and q["jv_halo_separate"] == 0, q
+        else:
+            assert q["jv_halo_separate"] > 0 and q["jv_halo_fused"] == 0, q
+    d = np.load(out + ".npz")
+    ref = str(tmp_path / "ref")
+    rc, log = run_ranks(2, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", ref, "--transport", "mailbox",
+                            "--problem", "heat3d", "--scheme", "euler", "--nx", "40", "--ny", "20", "--nz", "25",
+                            "--krylov-itmax", "20"], worker_env(2, NK_SHARED_FUSE_MAX=str(1 if form == "fused" else 1 << 30)))
+    assert rc == 0, log[-3000:]
+    r = np.load(ref + ".npz")
+    np.testing.assert_array_equal(d["x"], r["x"])
+    np.testing.assert_array_equal(d["h"], r["h"])
+
+
 @pytest.mark.parametrize("pgrid,nxyz,scheme", [("2,2,2", (40, 20, 24), "midpoint"), ("2,1,1", (40, 20, 24), "midpoint"),
                                                 ("1,2,1", (40, 20, 24), "midpoint"), ("1,3,1", (33, 20, 17), "midpoint"),
                                                 ("2,2,1", (38, 22, 64), "midpoint"), ("1,2,4", (16, 40, 72), "midpoint"),

@@ -37,11 +37,12 @@ declare -A WARGS=(
     [heat3d_midpoint]="--workload heat3d --scheme midpoint"
     [bratu2d_slab]="--workload bratu2d --global-n 16384 --slab-of 8"
     [heat3d_slab]="--workload heat3d --global-n 512 --slab-of 8"
+    [heat3d_block]="--workload heat3d --global-n 512 --block-of 8"
 )
 declare -A WFILE=(
     [bratu2d]="bratu2d_4096" [heat2d]="heat2d_8192" [heat3d]="heat3d_512"
     [heat2d_trapezoid_periodic]="heat2d_trapezoid_periodic_8192" [heat3d_midpoint]="heat3d_midpoint_512"
-    [bratu2d_slab]="bratu2d_16384x2048" [heat3d_slab]="heat3d_512x64"
+    [bratu2d_slab]="bratu2d_16384x2048" [heat3d_slab]="heat3d_512x64" [heat3d_block]="heat3d_block256x256x256"
 )
 TAGS=${PROFILE_TAGS:-bratu2d heat2d heat3d heat2d_trapezoid_periodic heat3d_midpoint bratu2d_slab heat3d_slab}
 
