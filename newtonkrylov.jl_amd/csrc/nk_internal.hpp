@@ -224,7 +224,7 @@ double* red_out(nk_ctx* c, int len, Red* r, int* fin);  // slot for a reduction 
 int finish_reduction(nk_ctx* c, Red* r);     // multi-rank: collapse + RCCL all-reduce
 int mb_check(nk_ctx* c);                     // after a host sync: did a mailbox wait time out?
 int red_blocks(int64_t n);                   // grid size of streaming reductions
-bool halo_self_ring(const nk_ctx* c);        // kbench: a one-rank mailbox exchanges ghost planes with itself
+bool halo_self_ring(const nk_ctx* c);        // rig (NK_HALO_SELF=1): a forced one-rank mailbox exchanges ghost planes with itself
 int halo_fuse_knob();                        // 1: a Krylov Jv's ghost planes travel in the stencil launch (mailbox up)
 // One Arnoldi step's MGS sweep in one launch (np passes over V[t % k], then ||q||) with q resident
 // on chip; returns 1 (nothing enqueued) when the resident path does not apply.
@@ -348,7 +348,7 @@ inline int nk_scheme(int kind) {
 // 3D blocks (nk_dist_grid with px * py > 1): a 3D grid function's allocation carries, after its trailing
 // z ghost plane, the four x / y ghost faces the neighbours' boundary layers are exchanged into:
 //   [y-lo: nx nz][y-hi: nx nz][x-lo: ny nz][x-hi: ny nz]   (y faces indexed k nx + i, x faces k ny + j)
-bool block_self(const nk_ctx* c);  // kbench (NK_HALO_SELF=2): a one-rank mailbox is its own neighbour on all six sides
+bool block_self(const nk_ctx* c);  // rig (NK_HALO_SELF=2): a forced one-rank mailbox is its own neighbour on all six sides
 inline bool blocks3d(const nk_ctx* c, const Geo& g) { return g.dim == 3 && (c->px * c->py > 1 || block_self(c)); }
 inline int64_t face_words(const nk_ctx* c, const nk_problem* p, const Geo& g) {
     return blocks3d(c, g) ? 2 * (p->nx + p->ny) * p->nz : 0;

@@ -636,8 +636,9 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         const int64_t tiles_pl = g.dim == 2 ? A.tiles_x : (int64_t)A.tiles_x * A.tiles_y;
         const bool self = halo_self_ring(c);
         // ranks sharing one GPU (rehearsals): in-launch only for small slabs -- a big slab's end tiles spin
-        // on CUs the peer's producing tiles need (r05: 8 ranks x 256^2 x 32 planes, 30 s per step fused,
-        // profiles/r05/rehearsal8_heat3d_256_*.json).  Neighbours must agree on the form (tile flags vs
+        // on CUs the peer's producing tiles need (r05: 8 ranks x 256^2 x 32 planes, 30.5 s per step fused;
+        // 26.7 ms with the exchange kernel, profiles/r06/rehearsal8_heat3d_256_slabs.json, the default
+        // spin limit).  Neighbours must agree on the form (tile flags vs
         // the exchange kernel's block flags), so the test uses rank-uniform values only: the most ranks on
         // one GPU and the slab size estimated from the global spacing, never this rank's slab
         static const int64_t fuse_max = env_cfg("NK_SHARED_FUSE_MAX", 0) > 0 ? env_cfg("NK_SHARED_FUSE_MAX", 0) : kSharedFuseMax;
@@ -651,7 +652,7 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
             A.hx_epoch = ++c->halo_epoch;
             A.hx_cap = c->halo_cap;
         } else {
-            if (c->nranks > 1 || per) ++c->n_jv_halo_separate;
+            if (c->nranks > 1 || per || self || block_self(c)) ++c->n_jv_halo_separate;
             NK_TRY(halo_exchange(c, p, in.v));
         }
     }

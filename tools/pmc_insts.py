@@ -14,7 +14,8 @@ import sys
 
 # points per launch of each workload (interior points of the grid the bench solves)
 POINTS = {"bratu2d": 4096 ** 2, "heat2d": 8192 ** 2, "heat2d_trapezoid_periodic": 8192 ** 2,
-          "heat3d_midpoint": 512 ** 3, "heat3d_slab": 512 * 512 * 64}
+          "heat3d_midpoint": 512 ** 3, "heat3d_slab": 512 * 512 * 64,
+          "heat3d_block": 256 ** 3}
 
 
 def short(name):

@@ -20,6 +20,7 @@ declare -A WARGS=(
     [heat2d_trapezoid_periodic]="--workload heat2d --scheme trapezoid --bc periodic"
     [heat3d_midpoint]="--workload heat3d --scheme midpoint"
     [heat3d_slab]="--workload heat3d --global-n 512 --slab-of 8"
+    [heat3d_block]="--workload heat3d --global-n 512 --block-of 8"
 )
 TAGS=${*:-bratu2d heat2d_trapezoid_periodic heat2d heat3d_midpoint heat3d_slab}
 (cd /tmp && timeout -k 10 120 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1) || true
