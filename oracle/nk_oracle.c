@@ -28,7 +28,9 @@
  * written (the reference's evaluation order, Julia does not contract).  BLAS-1 axpy uses fma()
  * explicitly (OpenBLAS daxpy, which Krylov.jl calls for dense vectors, is FMA based); the device
  * kernels use the same convention, so elementwise ops agree bit for bit.  Reductions are
- * deterministic (fixed chunking, independent of the thread count).
+ * deterministic (fixed chunking, independent of the thread count); OC_DEVRED (oc_set_devred) sums
+ * the one-rank 2D GMRES reductions in exactly the device kernels' order instead, so whole restarted
+ * histories compare bit for bit (tests/test_hip_devred.py).
  */
 #include <math.h>
 #include <stdint.h>
@@ -359,6 +361,181 @@ static void op_apply(oc_op* A, double* out, const double* v, double vnorm) {
     }
 }
 
+/* ------------------------------------------------------------------ the device's summation order (OC_DEVRED)
+ * Test infrastructure for VERDICT r05 item 5: the GMRES reductions summed in EXACTLY the order the
+ * product's kernels sum them (one rank, 2D kinds), so restarted FD-GMRES histories compare bit for bit at
+ * any length instead of drifting apart by reduction order.  Every tree below restates one device
+ * reduction (newtonkrylov.jl_amd/csrc/, file named at each); the per-element products are the same fma()
+ * the default mode uses.  Hardware parameters: the CU count (the resident sweep's grid, 256 on MI355X)
+ * and the sweep's LDS slots per thread (39) -- the test asserts the device reports the same grid.
+ *   wave:  wave_sum, a 64-lane butterfly (v += shfl_xor(v, o), o = 32 .. 1; lane 0)   nk_device.hpp
+ *   block: block_sum<256>, four wave sums added in wave order                        nk_device.hpp
+ *   RI:    reduce_input / k_finalize: thread t sums in[t], in[t + 256], ... then block nk_device.hpp
+ *   chunk: k_dot / k_sumsq / k_mgs_pass / k_update_x: block b owns a 256-multiple chunk of the
+ *          double2 elements, thread t its elements t, t + 256, ... (x then y component) nk_kernels.hip
+ *   tiles: k_st2d: tile (tx, ty) = 256 VEC columns x `rows` rows, thread t its VEC columns row by
+ *          row; partial index = tile index                                             nk_stencil.hpp
+ *   sweep: k_mgs_res: block b owns slots [b S / G, (b + 1) S / G) of 256 double2; partials summed by
+ *          one polling wave (lane l: blocks l, 64 + l, 128 + l, 192 + l, then a wave sum) nk_resident.hip */
+static int OC_DEVRED = 0, OC_DEV_CUS = 256, OC_DEV_RL = 39;
+void oc_set_devred(int on, int cus, int rl) {
+    OC_DEVRED = on;
+    OC_DEV_CUS = cus > 0 && cus <= 256 ? cus : 256;
+    OC_DEV_RL = rl >= 0 ? rl : 39;
+}
+int oc_get_devred(void) { return OC_DEVRED; }
+
+static double dr_wave(const double* v) {
+    double a[64], b[64];
+    memcpy(a, v, sizeof a);
+    for (int o = 32; o > 0; o >>= 1) {
+        for (int l = 0; l < 64; ++l) b[l] = a[l] + a[l ^ o];
+        memcpy(a, b, sizeof a);
+    }
+    return a[0];
+}
+static double dr_block(const double* acc) {
+    double r = dr_wave(acc);
+    for (int w = 1; w < 4; ++w) r += dr_wave(acc + 64 * w);
+    return r;
+}
+double oc_dr_ri(const double* in, int64_t len) {
+    double acc[256];
+    for (int t = 0; t < 256; ++t) {
+        double s = 0.0;
+        for (int64_t m = t; m < len; m += 256) s += in[m];
+        acc[t] = s;
+    }
+    return dr_block(acc);
+}
+static int64_t dr_red_blocks(int64_t n) {  /* red_blocks: >= 4 double2 per thread, at most 2048 */
+    int64_t g = (n + 2LL * 256 * 4 - 1) / (2LL * 256 * 4);
+    return g < 1 ? 1 : (g > 2048 ? 2048 : g);
+}
+static int64_t dr_wide_blocks(int64_t n) {  /* wide_blocks: >= 2 double2 per thread, at most kRedCap - 2 */
+    int64_t g = (n + 2LL * 256 * 2 - 1) / (2LL * 256 * 2);
+    return g < 1 ? 1 : (g > 16382 ? 16382 : g);
+}
+/* the chunked streaming kernels' partials of sum x_i y_i over G blocks (y == NULL: x_i^2) */
+void oc_dr_chunk_parts(int64_t n, const double* x, const double* y, int64_t G, double* parts) {
+    if (!y) y = x;
+    const int64_t n2 = n >> 1, per = ((n2 + G - 1) / G + 255) / 256 * 256;
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < G; ++b) {
+        double acc[256] = {0.0};
+        const int64_t lo = b * per, hi = lo + per < n2 ? lo + per : n2;
+        for (int64_t i = lo; i < hi; ++i) {
+            const int t = (int)((i - lo) & 255);
+            acc[t] = fma(x[2 * i], y[2 * i], acc[t]);
+            acc[t] = fma(x[2 * i + 1], y[2 * i + 1], acc[t]);
+        }
+        if ((n & 1) && b == 0) acc[0] = fma(x[n - 1], y[n - 1], acc[0]);
+        parts[b] = dr_block(acc);
+    }
+}
+static double dr_chunk(int64_t n, const double* x, const double* y, int64_t G) {
+    double* parts = (double*)malloc(sizeof(double) * (size_t)G);
+    oc_dr_chunk_parts(n, x, y, G, parts);
+    const double r = oc_dr_ri(parts, G);
+    free(parts);
+    return r;
+}
+/* k_st2d's tile geometry (launch_stencil_ex, nk_kernels.hip: about 1024 tiles of 8 .. 32 rows) */
+static void dr_tiles2d(int64_t nx, int64_t ny, int* vec, int64_t* tiles_x, int64_t* rows, int64_t* tiles_y) {
+    *vec = nx % 2 == 0 ? 2 : 1;
+    *tiles_x = (nx + 256 * *vec - 1) / (256 * *vec);
+    int64_t r = (ny * *tiles_x + 1023) / 1024;
+    if (r > 32) r = 32;
+    if (r < 8) r = 8;
+    const int64_t cap_rows = (ny * *tiles_x + (16384 - 3)) / (16384 - 2);
+    if (r < cap_rows) r = cap_rows;
+    if (r > ny) r = ny;
+    *rows = r;
+    *tiles_y = (ny + r - 1) / r;
+}
+int64_t oc_dr_tile_parts2d(int64_t nx, int64_t ny, const double* x, const double* y, double* parts) {
+    if (!y) y = x;
+    int vec;
+    int64_t tx_n, rows, ty_n;
+    dr_tiles2d(nx, ny, &vec, &tx_n, &rows, &ty_n);
+    if (!parts) return tx_n * ty_n;
+#pragma omp parallel for schedule(static)
+    for (int64_t tl = 0; tl < tx_n * ty_n; ++tl) {
+        const int64_t tx = tl % tx_n, ty = tl / tx_n;
+        const int64_t y0 = ty * rows, y1 = y0 + rows < ny ? y0 + rows : ny;
+        double acc[256] = {0.0};
+        for (int t = 0; t < 256; ++t) {
+            const int64_t x0 = tx * 256 * vec + (int64_t)t * vec;
+            if (x0 >= nx) continue;
+            double a = 0.0;
+            for (int64_t j = y0; j < y1; ++j)
+                for (int k = 0; k < vec; ++k) a = fma(x[j * nx + x0 + k], y[j * nx + x0 + k], a);
+            acc[t] = a;
+        }
+        parts[tl] = dr_block(acc);
+    }
+    return tx_n * ty_n;
+}
+static double dr_tiles(const oc_problem* P, const double* x, const double* y) {
+    const int64_t nt = oc_dr_tile_parts2d(P->nx, P->ny, x, y, NULL);
+    double* parts = (double*)malloc(sizeof(double) * (size_t)nt);
+    oc_dr_tile_parts2d(P->nx, P->ny, x, y, parts);
+    const double r = oc_dr_ri(parts, nt);
+    free(parts);
+    return r;
+}
+/* the resident sweep (launch_mgs_sweep, nk_resident.hip): does it run for np passes over n points? */
+static int dr_sweep_applies(int64_t n, int np) {
+    if (np < 2 || np > 64 || (n & 1)) return 0;
+    const int64_t G = OC_DEV_CUS, n2 = n >> 1, ns = (n2 + 255) / 256;
+    const int64_t whole = ns / G - (n2 % 256 != 0 ? 1 : 0);
+    if (whole < 1) return 0;
+    const int64_t slots = whole < (1 << 20) ? whole : (1 << 20);
+    int64_t rl = slots < OC_DEV_RL ? slots : OC_DEV_RL, rv = slots - rl, pick = 0;
+    static const int kRv[] = {89, 64, 48, 32, 25, 16, 0};
+    for (int i = 0; i < 7; ++i)
+        if (kRv[i] <= rv && kRv[i] <= slots) { pick = kRv[i]; break; }
+    rv = pick;
+    if (rl > slots - rv) rl = slots - rv;
+    const int64_t chunk = ns / G > 1 ? ns / G : 1;
+    return (double)(rv + rl) / (double)chunk >= 0.1;
+}
+void oc_dr_sweep_parts(int64_t n, const double* x, const double* y, int64_t G, double* parts) {
+    if (!y) y = x;
+    const int64_t n2 = n >> 1, ns = (n2 + 255) / 256;
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < G; ++b) {
+        double acc[256] = {0.0};
+        const int64_t lo = b * ns / G * 256, hi0 = (b + 1) * ns / G * 256, hi = hi0 < n2 ? hi0 : n2;
+        for (int64_t i = lo; i < hi; ++i) {
+            const int t = (int)((i - lo) & 255);
+            acc[t] = fma(x[2 * i], y[2 * i], acc[t]);
+            acc[t] = fma(x[2 * i + 1], y[2 * i + 1], acc[t]);
+        }
+        parts[b] = dr_block(acc);
+    }
+}
+double oc_dr_poll1(const double* parts, int64_t G) {
+    double v[64];
+    for (int l = 0; l < 64; ++l) {
+        double p = 0.0;
+        for (int j = 0; j < 4; ++j) p += (64 * j + l < G) ? parts[64 * j + l] : 0.0;
+        v[l] = p;
+    }
+    return dr_wave(v);
+}
+static double dr_sweep(int64_t n, const double* x, const double* y) {
+    const int64_t G = OC_DEV_CUS;
+    double parts[256];
+    oc_dr_sweep_parts(n, x, y, G, parts);
+    return oc_dr_poll1(parts, G);
+}
+/* devred applies to one-rank 2D GMRES / FGMRES without preconditioners (the path the tests compare) */
+static int dr_on(const oc_problem* P) {
+    return OC_DEVRED && (P->kind == OC_BRATU2D || P->kind == OC_HEAT2D_EULER || P->kind == OC_HEAT2D_MIDPOINT ||
+                         P->kind == OC_HEAT2D_TRAPEZOID);
+}
+
 /* ------------------------------------------------------------------ Krylov.jl sym_givens (real) */
 static inline double sgn(double x) { return (x > 0) - (x < 0); }
 void oc_sym_givens(double a, double b, double* c, double* s, double* rho) {
@@ -517,10 +694,13 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
     double* z = (double*)calloc((size_t)cap, sizeof(double));
     double* R = (double*)calloc((size_t)cap * (cap + 1) / 2, sizeof(double));
 
+    /* OC_DEVRED: every reduction in the device's order (nk_krylov.cpp gmres, one rank, no preconditioner) */
+    const int dev = dr_on(A->P) && !N && !M;
+    double xnorm_dev = 0.0; /* ||x|| of the last cycle's update (k_update_x partials), the restart's FD step */
     oc_fill(n, x, 0.0);
     oc_copy(n, w, b); /* w = b - A*0 */
     if (M) prec_apply(A, M, r0, w); /* r0 = M w */
-    double beta = oc_norm(n, r0);
+    double beta = dev ? sqrt(dr_chunk(n, r0, NULL, dr_red_blocks(n))) : oc_norm(n, r0); /* (k_sumsq + k_finalize) */
     double rNorm = beta;
     PUSH_HIST(rNorm);
     const double eps_ = o->atol + o->rtol * rNorm;
@@ -545,12 +725,14 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
             if (restart) {
                 oc_fill(n, xr, 0.0);
                 if (npass >= 1) {
-                    op_apply(A, w, x, -1.0);
+                    op_apply(A, w, x, dev ? xnorm_dev : -1.0);
                     oc_axpby(n, 1.0, b, -1.0, w);
                     if (M) prec_apply(A, M, r0, w);
                 }
             }
-            beta = oc_norm(n, r0);
+            /* device: the first cycle keeps beta; a restart's ||b - A x|| is the fused EPI_RESID stencil's */
+            if (!dev) beta = oc_norm(n, r0);
+            else if (restart && npass >= 1) beta = sqrt(dr_tiles(A->P, r0, NULL));
             z[0] = beta;
             /* kdivcopy!(n, V[1], r0, rNorm): Krylov.jl divides by rNorm -- beta on the first pass, after a
              * restart the previous cycle's estimate |zeta|, not the beta just computed */
@@ -581,18 +763,37 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
                     op_apply(A, w, V[k - 1], k == 1 ? beta / rNorm : 1.0);
                 }
                 if (M) prec_apply(A, M, q, w);
-                for (int i = 1; i <= k; ++i) {
-                    R[nr + i - 1] = oc_dot(n, V[i - 1], q);
-                    oc_axpy(n, -R[nr + i - 1], V[i - 1], q);
-                }
-                if (reorth) {
-                    for (int i = 1; i <= k; ++i) {
-                        double htmp = oc_dot(n, V[i - 1], q);
-                        R[nr + i - 1] += htmp;
-                        oc_axpy(n, -htmp, V[i - 1], q);
+                double Hbis;
+                if (dev) {
+                    /* h_1 = <V_1, J V_k> from the Jv stencil's tile partials; then np passes, each handing on
+                     * the partials of <V_next, q> (<q, q> after the last): the resident sweep's slot partition
+                     * and polling wave, or (one pass, or not resident) k_mgs_pass's chunks + reduce_input */
+                    const int np = reorth ? 2 * k : k;
+                    const int sweep = dr_sweep_applies(n, np);
+                    double h = dr_tiles(A->P, V[0], q);
+                    for (int t = 0; t < np; ++t) {
+                        const int i = t % k;
+                        if (t < k) R[nr + i] = h;
+                        else R[nr + i] += h;
+                        oc_axpy(n, -h, V[i], q);
+                        const double* nxt = t + 1 < np ? V[(t + 1) % k] : q;
+                        h = sweep ? dr_sweep(n, nxt, q) : dr_chunk(n, nxt, q, dr_red_blocks(n));
                     }
+                    Hbis = sqrt(h);
+                } else {
+                    for (int i = 1; i <= k; ++i) {
+                        R[nr + i - 1] = oc_dot(n, V[i - 1], q);
+                        oc_axpy(n, -R[nr + i - 1], V[i - 1], q);
+                    }
+                    if (reorth) {
+                        for (int i = 1; i <= k; ++i) {
+                            double htmp = oc_dot(n, V[i - 1], q);
+                            R[nr + i - 1] += htmp;
+                            oc_axpy(n, -htmp, V[i - 1], q);
+                        }
+                    }
+                    Hbis = oc_norm(n, q);
                 }
-                double Hbis = oc_norm(n, q);
                 for (int i = 1; i <= k - 1; ++i) {
                     double Rtmp = c[i - 1] * R[nr + i - 1] + s[i - 1] * R[nr + i];
                     R[nr + i] = s[i - 1] * R[nr + i - 1] - c[i - 1] * R[nr + i];
@@ -640,6 +841,8 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
                 prec_apply(A, N, xr, pv);
             }
             if (restart) oc_axpy(n, 1.0, xr, x);
+            /* device: ||x|| from the x update's partials (k_update_x over wide_blocks, k_finalize) */
+            if (dev && restart && A->mode == OC_JV_FD) xnorm_dev = sqrt(dr_chunk(n, x, NULL, dr_wide_blocks(n)));
             iter += inner_iter;
             inner_itmax = itmax - iter;
             tired = iter >= itmax;
@@ -829,7 +1032,8 @@ int oc_krylov_solve(const oc_problem* P, int jv_mode, int algo, const double* u,
                     const double* b, double* x, const oc_krylov_opts* o, oc_krylov_stats* st,
                     double* hist, int64_t hist_cap, int64_t* hist_len) {
     oc_op A = {P, jv_mode, u, F0, 0.0, 0};
-    if (jv_mode == OC_JV_FD) A.unorm = oc_norm(oc_n(P), u);
+    if (jv_mode == OC_JV_FD)  /* device: k_sumsq + k_finalize (nk_krylov_solve without a known ||u||) */
+        A.unorm = dr_on(P) ? sqrt(dr_chunk(oc_n(P), u, NULL, dr_red_blocks(oc_n(P)))) : oc_norm(oc_n(P), u);
     if (algo == OC_ALGO_CG) return oc_cg(&A, b, x, o, st, hist, hist_cap, hist_len);
     oc_krylov_opts oo = *o;
     oo.flexible = algo == OC_ALGO_FGMRES;

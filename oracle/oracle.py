@@ -117,6 +117,16 @@ def lib():
         L.oc_ilu0_solve.argtypes = [C.POINTER(_Problem), P, P, P]
         L.oc_set_threads.argtypes = [C.c_int]
         L.oc_set_chunk.argtypes = [C.c_int64]
+        L.oc_set_devred.argtypes = [C.c_int, C.c_int, C.c_int]
+        L.oc_get_devred.restype = C.c_int
+        L.oc_dr_ri.argtypes = [P, I64]
+        L.oc_dr_ri.restype = D
+        L.oc_dr_poll1.argtypes = [P, I64]
+        L.oc_dr_poll1.restype = D
+        L.oc_dr_chunk_parts.argtypes = [I64, P, P, I64, P]
+        L.oc_dr_sweep_parts.argtypes = [I64, P, P, I64, P]
+        L.oc_dr_tile_parts2d.argtypes = [I64, I64, P, P, P]
+        L.oc_dr_tile_parts2d.restype = I64
         L.oc_get_threads.restype = C.c_int
         for name in ("oc_axpy",):
             getattr(L, name).argtypes = [I64, D, P, P]
@@ -348,6 +358,36 @@ def ew_forcing(eta, tol, n_res, n_res_prior, eta_max=0.999, gamma=0.9):
 def set_chunk(c: int):
     """Reduction chunk of the oracle's dot / norm (default 8192): another summation order."""
     lib().oc_set_chunk(int(c))
+
+
+def set_devred(on: bool, cus: int = 256, rl: int = 39):
+    """Sum the one-rank 2D GMRES reductions in exactly the device's order (nk_oracle.c OC_DEVRED): the
+    kernels' trees -- wave butterflies, block sums, reduce_input, the chunked streaming kernels, k_st2d's
+    tiles and the resident sweep's slot partition over `cus` blocks (the GPU's CU count) -- so that
+    restarted FD-GMRES histories compare bit for bit at any length."""
+    lib().oc_set_devred(int(bool(on)), int(cus), int(rl))
+
+
+def get_devred() -> bool:
+    return bool(lib().oc_get_devred())
+
+
+def dr_trees(n: int, x, y=None, *, G: int = 256, nx: int = 0, ny: int = 0):
+    """The device-order trees as separate pieces (CPU tests pin them against a Python restatement):
+    chunk / sweep partials over G blocks, their reduce_input / polling-wave sums, k_st2d tile partials."""
+    x = np.ascontiguousarray(x, dtype=np.float64).ravel()
+    y = x if y is None else np.ascontiguousarray(y, dtype=np.float64).ravel()
+    chunk = np.zeros(G)
+    sweep = np.zeros(G)
+    lib().oc_dr_chunk_parts(n, _p(x), _p(y), G, _p(chunk))
+    lib().oc_dr_sweep_parts(n, _p(x), _p(y), G, _p(sweep))
+    out = dict(chunk=chunk, sweep=sweep, ri_chunk=lib().oc_dr_ri(_p(chunk), G), poll1=lib().oc_dr_poll1(_p(sweep), G))
+    if nx:
+        nt = lib().oc_dr_tile_parts2d(nx, ny, _p(x), _p(y), None)
+        tiles = np.zeros(nt)
+        lib().oc_dr_tile_parts2d(nx, ny, _p(x), _p(y), _p(tiles))
+        out.update(tiles=tiles, ri_tiles=lib().oc_dr_ri(_p(tiles), nt))
+    return out
 
 
 def set_threads(t: int):

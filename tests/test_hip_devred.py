@@ -1,0 +1,83 @@
+"""GMRES parity at any length: the oracle in its device-order mode (oracle.set_devred,
+nk_oracle.c OC_DEVRED) sums every reduction of a one-rank 2D GMRES solve in exactly the tree the product's
+kernels use -- k_st2d's tile partials for <V_1, J V_k> and the restart residual, the resident sweep's slot
+partition and polling wave for the MGS passes (k_mgs_pass's chunks where the sweep does not run),
+k_sumsq / k_update_x for ||b||, ||u||, ||x||, reduce_input / k_finalize for every consumer.  With the
+operator already bit-identical (shared exp, same association order), the whole restarted FD-GMRES
+history and the iterate then agree BIT FOR BIT with the device, however many restarts -- instead of
+drifting apart by summation order (1e-8 over 15 restarts in the default mode).
+
+Tolerance: none (np.array_equal).  Hardware parameter: the sweep grid is the GPU's CU count, read from
+the device's own path report and handed to the oracle."""
+import numpy as np
+import pytest
+
+import _nkpath  # noqa: F401
+import ariadne_hip as ah
+from oracle import oracle as oc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = ah.Context(0)
+    ah.set_default_context(c)
+    yield c
+    c.sync()
+
+
+def problem(kind, nx, ny):
+    if kind == "bratu":
+        P = oc.bratu2d(nx, ny)
+        u = oc.sin_ic(P)
+        return P, u, ah.bratu2d_, (1.0 / (nx + 1), 1.0 / (ny + 1), P.lam)
+    rng = np.random.default_rng(3)
+    un = oc.sin_ic(oc.bratu2d(nx, ny)) + 0.1 * rng.standard_normal((ny, nx))
+    P = oc.heat2d_euler(nx, ny, un=un)
+    u = un + 0.01 * rng.standard_normal((ny, nx))
+    return P, u, None, un
+
+
+def device_solve(ctx, kind, P, u, F_, p, un, memory, itmax, jv, reorth):
+    grid = ah.Grid.full(P.nx, P.ny)
+    ud = ah.DeviceArray.from_numpy(u, grid, ctx)
+    if kind != "bratu":
+        und = ah.DeviceArray.from_numpy(un, grid, ctx)
+        F_ = ah.G_Euler_.bind(ah.diffusion_)
+        p = (und, P.dt, None, (P.a, P.hx, P.hy, ah.bc_zero_), 0.0)
+    res = ud.zero()
+    F_(res, ud, p)
+    ws = ah.krylov_workspace("gmres", ah.KrylovConstructor(res, memory=memory))
+    J = ah.JacobianOperator(F_, res, ud, p, jv=jv)
+    ah.krylov_solve_(ws, J, res, restart=True, atol=0.0, rtol=0.0, itmax=itmax, history=True,
+                     reorthogonalization=reorth)
+    return ws.x.to_numpy(), ws.stats, res.to_numpy(), ctx.path_info()
+
+
+@pytest.mark.parametrize("kind,nx,ny,memory,itmax,jv,reorth", [
+    ("bratu", 1024, 1024, 30, 90, "fd", False),   # 3 restarted GMRES(30) cycles, resident sweep, 128 tiles x 2
+    ("bratu", 512, 384, 20, 60, "fd", False),     # uneven slot partition: some sweep blocks own 2 slots, some 1
+    ("heat", 1024, 512, 20, 60, "fd", True),      # reorthogonalisation: 2k passes per sweep
+    ("bratu", 256, 256, 10, 60, "exact", False),  # below one slot per CU: the k_mgs_pass chain every step
+])
+def test_restarted_gmres_bitwise_in_device_order(ctx, kind, nx, ny, memory, itmax, jv, reorth):
+    P, u, F_, p = problem(kind, nx, ny)
+    x, st, F0, path = device_solve(ctx, kind, P, u, F_, p, p, memory, itmax, jv, reorth)
+    if kind == "heat":
+        np.testing.assert_array_equal(F0, oc.residual(P, u))
+    cus = path["resident_blocks"] or 256
+    oc.set_devred(True, cus=cus)
+    try:
+        xo, so, ho = oc.krylov_solve(P, u, F0, jv=jv, F0=F0, memory=memory, restart=True, atol=0.0, rtol=0.0,
+                                     itmax=itmax, reorthogonalization=reorth)
+    finally:
+        oc.set_devred(False)
+    assert st.niter == so["niter"] == itmax and st.n_matvec == so["n_matvec"]
+    h = np.array(st.residuals)
+    np.testing.assert_array_equal(h, ho)
+    np.testing.assert_array_equal(x, xo)
+    # and the default (chunked) oracle order is NOT the device's: the bits above come from the emulation
+    xd, _, hd = oc.krylov_solve(P, u, F0, jv=jv, F0=F0, memory=memory, restart=True, atol=0.0, rtol=0.0,
+                                itmax=itmax, reorthogonalization=reorth)
+    assert not np.array_equal(hd, h)

@@ -509,3 +509,119 @@ def test_bratu_operator_against_the_platform_exp():
     w = u + eps * v
     bound = (2 * ulp(P.lam * np.exp(w)) + ulp(F_cr + eps * v) + 2 * ulp(nl) + ulp(F_cr)) / eps + 2 * ulp(D_cr)
     assert np.all(np.abs(D_cr - D_lm) <= bound)
+
+
+# ----------------------------------------------------------------------------- device-order reduction trees
+def _fma(a, b, c):
+    from fractions import Fraction
+    return float(Fraction(a) * Fraction(b) + Fraction(c))  # one rounding (int / int true division is exact-rounded)
+
+
+def _wave(v):
+    a = list(v)
+    o = 32
+    while o:
+        a = [a[l] + a[l ^ o] for l in range(64)]
+        o >>= 1
+    return a[0]
+
+
+def _block(acc):
+    r = _wave(acc[0:64])
+    for w in range(1, 4):
+        r += _wave(acc[64 * w:64 * w + 64])
+    return r
+
+
+def _ri(parts):
+    acc = []
+    for t in range(256):
+        s = 0.0
+        for m in range(t, len(parts), 256):
+            s += parts[m]
+        acc.append(s)
+    return _block(acc)
+
+
+def test_device_order_trees_match_their_restatement():
+    """The oracle's device-order trees (nk_oracle.c OC_DEVRED, the GPU parity checker of
+    tests/test_hip_devred.py) against an independent Python restatement of the kernels' summation order:
+    64-lane butterfly wave sums, block sums in wave order, reduce_input's thread-strided sums, the chunked
+    streaming kernels (k_sumsq / k_mgs_pass / k_update_x), the resident sweep's balanced slot partition and
+    polling wave, k_st2d's tiles (256 VEC columns x rows).  Exact equality."""
+    rng = np.random.default_rng(11)
+    n = 6002  # odd double2 count and a tail-free even n; 3001 double2 elements
+    x = rng.standard_normal(n)
+    y = rng.standard_normal(n)
+    G = 5
+    d = oc.dr_trees(n, x, y, G=G, nx=600, ny=10)
+    n2 = n // 2
+    # chunked: block b owns [b per, (b + 1) per) of the double2 elements, per a multiple of 256
+    per = ((n2 + G - 1) // G + 255) // 256 * 256
+    chunk = []
+    for b in range(G):
+        acc = [0.0] * 256
+        for i in range(b * per, min((b + 1) * per, n2)):
+            t = (i - b * per) % 256
+            acc[t] = _fma(x[2 * i], y[2 * i], acc[t])
+            acc[t] = _fma(x[2 * i + 1], y[2 * i + 1], acc[t])
+        chunk.append(_block(acc))
+    assert list(d["chunk"]) == chunk
+    assert d["ri_chunk"] == _ri(chunk)
+    # the sweep: ceil(n2 / 256) slots, block b owns slots [b S / G, (b + 1) S / G)
+    S = (n2 + 255) // 256
+    sweep = []
+    for b in range(G):
+        lo, hi = b * S // G * 256, min((b + 1) * S // G * 256, n2)
+        acc = [0.0] * 256
+        for i in range(lo, hi):
+            t = (i - lo) % 256
+            acc[t] = _fma(x[2 * i], y[2 * i], acc[t])
+            acc[t] = _fma(x[2 * i + 1], y[2 * i + 1], acc[t])
+        sweep.append(_block(acc))
+    assert list(d["sweep"]) == sweep
+    lanes = []
+    for l in range(64):
+        p = 0.0
+        for j in range(4):
+            p += sweep[64 * j + l] if 64 * j + l < G else 0.0
+        lanes.append(p)
+    assert d["poll1"] == _wave(lanes)
+    # k_st2d tiles: 600 x 10 -> 2 tiles of 512 columns, 8-row tiles (the 8-row minimum): 2 x 2 tiles
+    nx, ny, rows = 600, 10, 8
+    X, Y = x[:nx * ny], y[:nx * ny]
+    tiles = []
+    for ty in range(2):
+        for tx in range(2):
+            acc = [0.0] * 256
+            for t in range(256):
+                x0 = tx * 512 + 2 * t
+                if x0 >= nx:
+                    continue
+                a = 0.0
+                for j in range(ty * rows, min(ty * rows + rows, ny)):
+                    for k in range(2):
+                        a = _fma(X[j * nx + x0 + k], Y[j * nx + x0 + k], a)
+                acc[t] = a
+            tiles.append(_block(acc))
+    assert list(d["tiles"]) == tiles
+    assert d["ri_tiles"] == _ri(tiles)
+
+
+def test_device_order_gmres_is_a_reordering_only():
+    """Device-order mode changes only the summation order: a restarted FD-GMRES(20) history agrees with the
+    default mode to rounding-order differences (and is itself deterministic)."""
+    P = oc.bratu2d(128, 96)
+    u0 = oc.sin_ic(P)
+    F = oc.residual(P, u0)
+    kw = dict(jv="fd", F0=F, memory=20, restart=True, atol=0.0, rtol=0.0, itmax=60)
+    x0, _, h0 = oc.krylov_solve(P, u0, F, **kw)
+    oc.set_devred(True)
+    try:
+        x1, _, h1 = oc.krylov_solve(P, u0, F, **kw)
+        x2, _, h2 = oc.krylov_solve(P, u0, F, **kw)
+    finally:
+        oc.set_devred(False)
+    assert np.array_equal(h1, h2) and np.array_equal(x1, x2)
+    assert np.allclose(h1, h0, rtol=1e-7, atol=0)
+    assert np.max(np.abs(x1 - x0)) <= 1e-7 * np.max(np.abs(x0))
