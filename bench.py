@@ -94,8 +94,9 @@ def parse():
                     help="heat3d with --global-n G: run ONE rank's block of the N-way 3D-block split (--pgrid auto of N; "
                          "BASELINE config 5: 2x2x2 of 256^3 at G = 512) alone on one GPU, through the block path: the "
                          "BLK stencil instances read x / y ghost faces, and one packed six-face exchange per Jv runs "
-                         "over a forced one-rank mailbox whose rank is its own neighbour on every side (NK_HALO_SELF=2 "
-                         "rig: every axis wraps onto the block itself -- the cost is what is measured)")
+                         "over a forced one-rank mailbox whose rank is its own neighbour on both sides of every split "
+                         "axis (NK_HALO_SELF=2 rig: those axes wrap onto the block itself -- the cost is what is "
+                         "measured; --pgrid px,py,pz picks another split)")
     ap.add_argument("--pgrid", default="",
                     help="heat3d --global-n with N > 1 ranks: 3D blocks px,py,pz (nk_dist_grid; 'auto': the most "
                          "cubic factorisation of N -- 2,2,2 at N = 8, BASELINE config 5's 256^3 blocks) instead of "
@@ -496,9 +497,9 @@ class HeatEuler:
         slab = (f"; rank {rank}'s slab of the {parts}-way split ALONE on one GPU (ghost planes zero, no exchange)"
                 if args.slab_of else "")
         if args.block_of:
-            slab = (f"; rank 0's block of the {parts}-way block split ALONE on one GPU, its six ghost faces exchanged "
-                    "every Jv with itself over a forced one-rank mailbox (NK_HALO_SELF=2: the operator wraps every "
-                    "axis onto the block; value = the global matvec rate with this exchange form, without xGMI)")
+            slab = (f"; rank 0's block of the {parts}-way block split ALONE on one GPU, the ghost faces of every split "
+                    "axis exchanged every Jv with itself over a forced one-rank mailbox (NK_HALO_SELF=2: those axes "
+                    "wrap onto the block; value = the global matvec rate with this exchange form, without xGMI)")
         self.workload = (f"{dim}D heat {sname}{bcname} {shape} ({per_gpu}), one time step per step: "
                          f"newton_krylov! tol_abs=6e-6, GMRES memory {args.memory or 20} (unrestarted, "
                          f"reorthogonalization={'true' if self.reorth else 'false'}), "
@@ -592,6 +593,8 @@ def main():
         # the rig (read by the library at its first use): a forced one-rank mailbox, the rank its own
         # neighbour on all six sides
         os.environ.update(NK_DIST_FORCE="1", NK_DIST_MAILBOX="1", NK_HALO_SELF="2")
+        pg = pgrid_of(args.pgrid or "auto", args.block_of)  # both sides of every split axis (bit 0 z, 1 y, 2 x)
+        os.environ["NK_HALO_SELF_AXES"] = str((pg[2] > 1) | (pg[1] > 1) << 1 | (pg[0] > 1) << 2)
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)", file=sys.stderr)
         sys.exit(2)

@@ -240,6 +240,7 @@ int nk_ctx_destroy(nk_ctx* c) {
     if (c->tpart) (void)hipFree(c->tpart);
     (void)hipHostFree(c->hpin);
     if (c->res_gran) (void)hipFree(c->res_gran);
+    if (c->blk_order) (void)hipFree(c->blk_order);
     if (c->res_err) (void)hipHostFree(c->res_err);
     if (c->ilu_prog) (void)hipFree(c->ilu_prog);
     if (c->ilu_err) (void)hipHostFree(c->ilu_err);

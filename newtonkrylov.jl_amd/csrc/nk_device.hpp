@@ -258,7 +258,7 @@ __device__ __forceinline__ double lap(double c, double p, double m, double h2) {
 // ------------------------------------------------------------------------------ peer ghost planes
 __device__ __forceinline__ uint64_t* halo_flags(uint64_t* base) { return base + kMbWords; }
 __device__ __forceinline__ uint64_t* halo_tile_flags(uint64_t* base, int par, int side) {
-    return base + kMbWords + (size_t)2 * kHaloSides * kHaloBlocks + (size_t)(par * 2 + side) * kHaloTileFlags;
+    return base + kMbWords + (size_t)2 * kHaloSides * kHaloBlocks + (size_t)(par * kHaloSides + side) * kHaloTileFlags;
 }
 __device__ __forceinline__ uint64_t* halo_inbox(uint64_t* base, int par, int side, int64_t cap) {
     return base + kMbWords + kHaloFlagWords + (size_t)(par * kHaloSides + side) * (size_t)cap;

@@ -29,7 +29,11 @@ static int rccl_fail(nk_ctx* c, ncclResult_t r, const char* what) {
 
 // 3D blocks: rank = (iz py + iy) px + ix; side s = 2 a + hi of axis a = z, y, x (kHaloSides numbering)
 int block_nbr(const nk_ctx* c, int side) {
-    if (block_self(c)) return c->rank;  // kbench self blocks
+    if (block_self(c)) {  // the self-block rig (NK_HALO_SELF=2): its own neighbour on both sides of every
+        // axis in NK_HALO_SELF_AXES (bit 0 z, 1 y, 2 x; default all) -- bench.py --block-of passes the split axes
+        static const int axes = env_cfg("NK_HALO_SELF_AXES", 7);
+        return (axes >> (side >> 1)) & 1 ? c->rank : -1;
+    }
     const int px = c->px, py = c->py, r = c->rank;
     const int ix = r % px, iy = (r / px) % py, iz = r / (px * py), pz = c->nranks / (px * py);
     const int hi = side & 1;

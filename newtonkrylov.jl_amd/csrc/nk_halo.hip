@@ -267,10 +267,10 @@ int mailbox_selftest(nk_ctx* c, bool* ok) {
     return NK_OK;
 }
 
-// ghost planes of a Krylov Jv inside the stencil launch when the peer mailbox is up (kbench: NK_HALO_FUSE=0
-// forces the separate exchange kernel)
+// ghost planes / faces of a Krylov Jv inside the stencil launch when the peer mailbox is up (NK_HALO_FUSE=0, a
+// rig like NK_HALO_SELF: the separate exchange kernels -- the same values, for A/B and the form tests)
 int halo_fuse_knob() {
-    static const int fuse = NK_TUNE("NK_HALO_FUSE", 1);
+    static const int fuse = env_cfg("NK_HALO_FUSE", 1);
     return fuse;
 }
 

@@ -112,6 +112,10 @@ struct nk_ctx {
     int res_blocks = 0, res_rl = 0;        // grid (= CUs) and LDS double2 slots per thread
     int res_share = 1;                     // ranks on this GPU (NK_RES_SHARED: each sweep grid gets CUs / res_share)
     int share_most = 1;                    // the most ranks on any one GPU -- the same on every rank (mailbox set-up)
+    int n_cus = 0;                         // the device's CU count (0: not queried yet)
+    int* blk_order = nullptr;              // 3D blocks, in-launch exchange: the tile dispatch order (device), its
+    int blk_order_cap = 0;                 //   capacity and the geometry it was built for
+    uint64_t blk_order_key = 0;
     int xchg_nb = 256;                     // exchange-kernel grid (<= kHaloBlocks), the same on every rank: kHaloBlocks / the most
                                            // ranks sharing one GPU, so every sharing rank's spinning exchange grid fits at once
     uint64_t* res_tstamp = nullptr;        // kernel-variant bench only (nkb_mgs_res, NK_RES_TSTAMP)
@@ -250,10 +254,10 @@ constexpr int64_t kSharedFuseMax = (int64_t)1 << 20;  // ranks sharing a GPU: in
 int64_t shared_slab_points(const nk_ctx* c, const nk_problem* p, const Geo& g);
 // one fine-grained region per rank, IPC-mapped by every other rank:
 //   [mailbox: kMbSlots x kMbRanks x 2 u64][halo flags: 2 parity x kHaloSides x kHaloBlocks u64]
-//   [tile flags: 2 parity x 2 sides x kHaloTileFlags u64]
+//   [tile flags: 2 parity x kHaloSides sides x kHaloTileFlags u64]  (slab ends: sides 0 / 1; 3D blocks: all six)
 //   [halo inbox: 2 parity x kHaloSides x halo_cap doubles]   (side 0: from the lower rank, 1: from the upper, ...)
 constexpr size_t kMbWords = (size_t)2 * kMbSlots * kMbRanks;
-constexpr size_t kHaloFlagWords = (size_t)2 * kHaloSides * kHaloBlocks + (size_t)2 * 2 * kHaloTileFlags;
+constexpr size_t kHaloFlagWords = (size_t)2 * kHaloSides * kHaloBlocks + (size_t)2 * kHaloSides * kHaloTileFlags;
 int mailbox_bind(nk_ctx* c);                 // make c's mailbox the one the kernels use (nk_kernels.hip)
 int mailbox_selftest(nk_ctx* c, bool* ok);   // a few epochs through the mailbox vs the expected sums
 // ghost planes of v (interior pointer, `plane` doubles per plane, `nplanes` planes) through the peer

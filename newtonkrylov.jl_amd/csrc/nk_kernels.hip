@@ -477,6 +477,85 @@ int wide_blocks(int64_t n) {
 
 
 
+namespace {
+// 3D blocks: may a Jv launch carry its ghost layers itself (blk_tile_exchange)?  Every rank must decide alike
+// (tile flags vs k_faces_ipc's block flags), so from values every rank holds alike: the largest block of the
+// grid from the global spacings (one rank: its own), the most ranks on one GPU.  Each face's patches need a
+// flag each; a z-partner pair sits tiles_x x tiles_y dispatch positions apart, which must stay within one
+// tile per CU so that every waiting tile's partner is resident; ranks sharing a GPU only for small blocks.
+bool blk_inlaunch_ok(nk_ctx* c, const nk_problem* p, int64_t fuse_max) {
+    int64_t bx = p->nx, by = p->ny, bz = p->nz;
+    if (c->nranks > 1) {
+        auto glob = [](double h) { return (h > 0.0 && 1.0 / h < 1e15) ? std::max<int64_t>(1, std::llround(1.0 / h) - 1) : -1; };
+        const int64_t NX = glob(p->hx), NY = glob(p->hy), NZ = glob(p->hz);
+        const int pz = c->nranks / (c->px * c->py);
+        if (NX < 0 || NY < 0 || NZ < 0) return false;
+        bx = (NX + c->px - 1) / c->px;
+        by = (NY + c->py - 1) / c->py;
+        bz = (NZ + pz - 1) / pz;
+    }
+    if (!c->n_cus && (hipDeviceGetAttribute(&c->n_cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->n_cus < 1)) {
+        (void)hipGetLastError();
+        c->n_cus = 0;
+        return false;
+    }
+    const int64_t vec = bx % 2 == 0 ? 2 : 1;
+    const int64_t tx = (bx + 64 * vec - 1) / (64 * vec), ty = (by + 3) / 4, nzc = (bz + 15) / 16;
+    if (tx * ty > kHaloTileFlags || tx * nzc > kHaloTileFlags || ty * nzc > kHaloTileFlags) return false;
+    if (tx * ty > c->n_cus) return false;
+    if (std::max({bx * by, bx * bz, by * bz}) > c->halo_cap) return false;
+    return c->share_most <= 1 || bx * by * bz <= fuse_max;
+}
+
+// the dispatch order of an in-launch block exchange: the exchanging tiles first, in pair order -- z-chunks
+// 0, last, 1, last - 1, ..., rows of tiles likewise, columns innermost -- so each tile's x / y / z partner
+// is at most 1 / tiles_x / tiles_x tiles_y positions away; then the other tiles in XCD bands (plane-major)
+int blk_order(nk_ctx* c, const KArgs& A, int nzc, const int** out) {
+    const int tx_n = A.tiles_x, ty_n = A.tiles_y, tpl = tx_n * ty_n, n = tpl * nzc;
+    int mask = 0;
+    for (int s = 0; s < kHaloSides; ++s) mask |= (A.bnbr[s] >= 0) << s;
+    const uint64_t key = ((uint64_t)tx_n << 44) ^ ((uint64_t)ty_n << 24) ^ ((uint64_t)nzc << 6) ^ (uint64_t)mask;
+    if (c->blk_order && c->blk_order_key == key) {
+        *out = c->blk_order;
+        return NK_OK;
+    }
+    auto ord = [](int i, int m) { return (i & 1) ? m - 1 - (i >> 1) : (i >> 1); };
+    auto exch = [&](int tz, int ty, int tx) {
+        return ((mask & 1) && tz == 0) || ((mask & 2) && tz == nzc - 1) || ((mask & 4) && ty == 0) ||
+               ((mask & 8) && ty == ty_n - 1) || ((mask & 16) && tx == 0) || ((mask & 32) && tx == tx_n - 1);
+    };
+    std::vector<int> order, rest;
+    order.reserve(n);
+    std::vector<char> seen((size_t)n, 0);
+    for (int zi = 0; zi < nzc; ++zi)
+        for (int yi = 0; yi < ty_n; ++yi)
+            for (int tx = 0; tx < tx_n; ++tx) {
+                const int tz = ord(zi, nzc), ty = ord(yi, ty_n);
+                if (exch(tz, ty, tx)) {
+                    order.push_back(tz * tpl + ty * tx_n + tx);
+                    seen[(size_t)(tz * tpl + ty * tx_n + tx)] = 1;
+                }
+            }
+    for (int t = 0; t < n; ++t)
+        if (!seen[(size_t)t]) rest.push_back(t);
+    const int m = (int)rest.size(), m8 = m & ~7;
+    for (int i = 0; i < m; ++i)  // block i of the rest lands on XCD i % 8 and takes that XCD's band's (i / 8)-th tile
+        order.push_back(rest[(size_t)(i < m8 ? (i & 7) * (m8 >> 3) + (i >> 3) : i)]);
+    if (c->blk_order_cap < n) {
+        if (c->blk_order) (void)hipFree(c->blk_order);
+        c->blk_order = nullptr;
+        c->blk_order_cap = 0;
+        NK_HIP(c, hipMalloc(reinterpret_cast<void**>(&c->blk_order), sizeof(int) * (size_t)n));
+        c->blk_order_cap = n;
+    }
+    NK_HIP(c, hipMemcpyAsync(c->blk_order, order.data(), sizeof(int) * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    NK_HIP(c, hipStreamSynchronize(c->stream));  // (the host vector goes out of scope; once per geometry)
+    c->blk_order_key = key;
+    *out = c->blk_order;
+    return NK_OK;
+}
+}  // namespace
+
 int launch_stencil(nk_ctx* c, const StencilIn& in, Red* red) {
     if (in.p && nk_is_user(in.p->kind)) {
         if (in.xchg_v) NK_TRY(halo_exchange(c, in.p, in.v));
@@ -584,7 +663,8 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         static const int target = NK_TUNE("NK_ST3_BLOCKS", 8192);  // shorter z-marches keep y-adjacent tiles in step (L2 reuse of the halo rows)
         int64_t planes = ((int64_t)p->nz * A.tiles_x * A.tiles_y + target - 1) / target;
         static const int min_planes = NK_TUNE("NK_ST_MINPLANES", 16);  // 16: (16 + 2) / 16 z-halo re-reads
-        if (planes < min_planes) planes = min_planes;
+        if (planes < min_planes || A.blk) planes = min_planes;  // (blocks: one chunk size on every rank -- the
+                                                                 //  in-launch exchange numbers x / y patches by chunk)
         if (rows_override > 0) planes = rows_override;
         if (planes > p->nz) planes = p->nz;
         A.rows = (int)planes;
@@ -645,7 +725,20 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         const bool share_ok = c->share_most <= 1 || shared_slab_points(c, p, g) <= fuse_max;
         const bool fuse = fuse_env && c->mb_on && (c->nranks > 1 || self) && share_ok && !per && !A.blk && in.mode != MODE_RES &&
                           (g.dim == 2 || (g.dim == 3 && A.lds3)) && g.plane <= c->halo_cap && tiles_pl <= kHaloTileFlags;
-        if (fuse) {
+        if (A.blk) {  // 3D blocks: every ghost layer inside this launch (blk_tile_exchange) or k_faces_ipc first
+            const bool bfuse = fuse_env && c->mb_on && in.mode != MODE_RES && rows_override <= 0 && blk_inlaunch_ok(c, p, fuse_max);
+            if (bfuse) {
+                ++c->n_jv_halo_fused;
+                A.hx_blk = 1;
+                A.hx_epoch = ++c->halo_epoch;
+                A.hx_cap = c->halo_cap;
+                for (int sd = 0; sd < kHaloSides; ++sd) A.bnbr[sd] = block_nbr(c, sd);
+                NK_TRY(blk_order(c, A, (int)((p->nz + A.rows - 1) / A.rows), &A.torder));
+            } else {
+                ++c->n_jv_halo_separate;
+                NK_TRY(halo_exchange(c, p, in.v));
+            }
+        } else if (fuse) {
             ++c->n_jv_halo_fused;
             A.hx_lo = c->rank > 0 || self;
             A.hx_hi = c->rank + 1 < c->nranks || self;

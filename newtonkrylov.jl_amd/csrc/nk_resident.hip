@@ -41,6 +41,7 @@ struct ResArgs {
     int* err;              // pinned host flag: a poll timed out
     int noxchg;            // kbench build only (NK_RES_NOXCHG=1, timing probe): skip the exchange -- WRONG results
     int ntc;               // NTS: the first ntc streamed slots of a block load V_{i+1} cached (Infinity Cache room)
+    int nwc;               // kernel-variant build: resident slots s >= nwc load V_{i+1} non-temporally (ldw_s)
     int poll1;             // 1: one polling wave (NK_RES_POLL1, default 1), 2: four staggered polling waves, 0: every thread polls one partial
     int strided;           // slots interleaved across blocks (every block exactly full: no streamed remainder)
     int mirror;            // kbench: odd blocks map slot s to the chunk's slot S-1-s (every block exactly full)
@@ -204,6 +205,19 @@ __device__ __forceinline__ dx2 ldw(const dx2* p) {
     if constexpr (NTM == 2) return __builtin_nontemporal_load(p);
     else return *p;
 }
+// V_{i+1} of resident slot `s`: the kernel-variant build's Infinity-Cache retention probe (NK_RES_NWC = w:
+// slots s < w load V_{i+1} with the default policy, the rest non-temporally -- VERDICT r05 item 6); the
+// product loads every slot as ldw does
+template <int NTM>
+__device__ __forceinline__ dx2 ldw_s(const dx2* p, int s, int nwc) {
+#ifdef NK_KBENCH
+    if (NTM != 2 && s >= nwc) return __builtin_nontemporal_load(p);
+#else
+    (void)s;
+    (void)nwc;
+#endif
+    return ldw<NTM>(p);
+}
 
 // the first register batch of a pass, loaded before the previous pass's hand-off completes (its
 // addresses do not depend on h): the load latency hides behind the hand-off
@@ -223,7 +237,7 @@ __device__ __forceinline__ void res_prefetch(const ResArgs& A, ResPre<B>& P, int
 #pragma unroll
         for (int u = 0; u < B; ++u) {
             P.b[u] = ldv<NTM>(vb + u * ss);
-            P.c[u] = ldw<NTM>(wb + u * ss);
+            P.c[u] = ldw_s<NTM>(wb + u * ss, s0 + u, A.nwc);
         }
     }
 }
@@ -267,7 +281,7 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
                 for (int u = 0; u < B; ++u) {
                     if (s0 + u < RV) {
                         bv[u] = ldv<NTM>(vb + (s0 + u) * ss);
-                        cv[u] = ldw<NTM>(wb + (s0 + u) * ss);
+                        cv[u] = ldw_s<NTM>(wb + (s0 + u) * ss, s0 + u, A.nwc);
                     }
                 }
             }
@@ -286,7 +300,7 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 bv[u] = ldv<NTM>(vl + (s + u) * ss);
-                cv[u] = ldw<NTM>(wl + (s + u) * ss);
+                cv[u] = ldw_s<NTM>(wl + (s + u) * ss, RV + s + u, A.nwc);
             }
 #pragma unroll
             for (int u0 = 0; u0 < 4; ++u0) {
@@ -298,7 +312,7 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
         };
         auto one = [&](int s) {
             const dx2 b = ldv<NTM>(vl + s * ss);
-            const dx2 cc = ldw<NTM>(wl + s * ss);
+            const dx2 cc = ldw_s<NTM>(wl + s * ss, RV + s, A.nwc);
             dx2 a = lq[s * kResThreads + tid];
             upd(a, b, cc);
             lq[s * kResThreads + tid] = a;
@@ -308,7 +322,7 @@ __device__ __forceinline__ double res_pass(const ResArgs& A, ResState<RV>& S, dx
 #pragma unroll
             for (int u = 0; u < LB; ++u) {
                 bv[u] = ldv<NTM>(vl + (s + u) * ss);
-                cv[u] = ldw<NTM>(wl + (s + u) * ss);
+                cv[u] = ldw_s<NTM>(wl + (s + u) * ss, RV + s + u, A.nwc);
             }
 #pragma unroll
             for (int u = 0; u < LB; ++u) {
@@ -686,6 +700,7 @@ int launch_mgs_sweep(nk_ctx* c, int64_t n, double* q, const double* const* V, in
         A.ntc = ntc_env >= 0 ? ntc_env : (room > 0 ? (int)(room / slot) : 0);
     }
     A.poll1 = NK_TUNE("NK_RES_POLL1", 1);
+    A.nwc = NK_TUNE("NK_RES_NWC", 1 << 30);
     A.tstamp = c->res_tstamp;
     // cross-rank hand-off: the first `senders` blocks (one per XCD at 8) all send the rank's sum -- the
     // same bits into the same cells -- so the peers see it as soon as the EARLIEST of them has it,

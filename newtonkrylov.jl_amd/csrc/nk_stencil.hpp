@@ -48,6 +48,12 @@ struct KArgs {
     int hx_lo, hx_hi;
     uint64_t hx_epoch;
     int64_t hx_cap;
+    // 3D blocks: all ghost layers of v through the peers' inboxes inside this launch (blk_tile_exchange):
+    // the neighbour rank of each side (-1: a physical boundary) and the host-built tile order (exchanging
+    // tiles first, partners close together)
+    int hx_blk;
+    int bnbr[6];
+    const int* torder;
 };
 
 // What one stencil dispatch launched: the instantiation as rocprofv3 names it (without the anonymous
@@ -903,6 +909,112 @@ void k_st2d(KArgs A0) {
     if constexpr (EPI != EPI_NONE) publish(acc, A.part, A.fin, sh, t);
 }
 
+// 3D blocks: the ghost layers of v through the peers' inboxes INSIDE the Jv launch (KArgs::hx_blk) instead of a
+// separate k_faces_ipc launch before it.  Tile (tx, ty, tz) owns one patch of every block face it touches: its
+// rows x columns of the first / last plane (z), its planes x columns of the first / last row (y), its planes x
+// rows of the first / last column (x).  It pushes each patch into that neighbour's inbox at the face layout
+// k_faces_ipc uses (system-scope stores, drained), raises the patch's flag there, waits for the neighbour's
+// flag of the same patch in its own region, and copies the neighbour's patch into v's ghost plane / face --
+// where the march then reads it exactly as after k_faces_ipc, so the arithmetic and the tile-indexed
+// partials do not change.  Neighbours share the face's extents and the tiling along it (z-chunks of a fixed
+// size, 4-row tiles, 64 VEC columns), so the patch numbers pair up.  Only this tile reads the layers it
+// copies (the x-face slots of its rows / planes, the halo rows of its planes, the ghost plane under its
+// rows and columns).  The host dispatches the exchanging tiles first, partners within one grid's residency.
+template <int NW, int VEC>
+__device__ bool blk_tile_exchange(const KArgs& A, int tx, int ty, int tz, int64_t z0, int64_t z1, int nzc) {
+    __shared__ int bx_ok;
+    const int64_t nx = A.nx, ny = A.ny, nz = A.nz, pl = nx * ny;
+    const int64_t ra = (int64_t)ty * NW, rb = ra + NW < ny ? ra + NW : ny;
+    const int64_t ca = (int64_t)tx * (64 * VEC), cb = ca + 64 * VEC < nx ? ca + 64 * VEC : nx;
+    const int par = (int)(A.hx_epoch & 1);
+    constexpr int nthr = 64 * NW;
+    // (constant indices only: a dynamic index into the KArgs copy would put it in scratch)
+    auto nbr = [&](int s) -> int {
+        switch (s) {
+        case 0: return A.bnbr[0];
+        case 1: return A.bnbr[1];
+        case 2: return A.bnbr[2];
+        case 3: return A.bnbr[3];
+        case 4: return A.bnbr[4];
+        default: return A.bnbr[5];
+        }
+    };
+    auto touches = [&](int s) -> bool {
+        if (nbr(s) < 0) return false;
+        switch (s) {
+        case 0: return tz == 0;
+        case 1: return tz == nzc - 1;
+        case 2: return ty == 0;
+        case 3: return ty == A.tiles_y - 1;
+        case 4: return tx == 0;
+        default: return tx == A.tiles_x - 1;
+        }
+    };
+    auto plen = [&](int s) -> int64_t { return s < 2 ? (rb - ra) * (cb - ca) : (s < 4 ? (z1 - z0) * (cb - ca) : (z1 - z0) * (rb - ra)); };
+    // element q of side s's patch: its index f in the face layout (z: j nx + i, y: k nx + i, x: k ny + j) and
+    // the offset of my own boundary value in v
+    auto at = [&](int s, int64_t q, int64_t& f, int64_t& src) {
+        if (s < 2) {
+            const int64_t w = cb - ca, j = ra + q / w, i = ca + q % w;
+            f = j * nx + i;
+            src = (s == 0 ? 0 : (nz - 1) * pl) + f;
+        } else if (s < 4) {
+            const int64_t w = cb - ca, k = z0 + q / w, i = ca + q % w;
+            f = k * nx + i;
+            src = k * pl + (s == 2 ? 0 : ny - 1) * nx + i;
+        } else {
+            const int64_t w = rb - ra, k = z0 + q / w, j = ra + q % w;
+            f = k * ny + j;
+            src = k * pl + j * nx + (s == 4 ? 0 : nx - 1);
+        }
+    };
+    auto flag_of = [&](int s) -> int { return s < 2 ? ty * A.tiles_x + tx : (s < 4 ? tz * A.tiles_x + tx : tz * A.tiles_y + ty); };
+    double* v = const_cast<double*>(A.v);
+#pragma unroll
+    for (int s = 0; s < kHaloSides; ++s) {  // block-uniform
+        if (!touches(s)) continue;
+        uint64_t* dst = halo_inbox(g_mb.peers[nbr(s)], par, s ^ 1, A.hx_cap);
+        const int64_t len = plen(s);
+        for (int64_t q = threadIdx.x; q < len; q += nthr) {
+            int64_t f, src;
+            at(s, q, f, src);
+            __hip_atomic_store(dst + f, (uint64_t)__double_as_longlong(v[src]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every thread drains its stores before the flags
+    __syncthreads();
+    if (threadIdx.x < 64) {  // lane s raises side s's flag and polls its own: the sides' round trips in parallel
+        const int s = (int)threadIdx.x;
+        const bool mine = s < kHaloSides && touches(s);
+        if (mine)
+            __hip_atomic_store(halo_tile_flags(g_mb.peers[nbr(s)], par, s ^ 1) + flag_of(s), A.hx_epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t t0 = wall_clock64();
+        const bool ok = !mine || flag_wait(halo_tile_flags(g_mb.self, par, s) + flag_of(s), A.hx_epoch);
+        const bool all = __all(ok);
+        if (s == 0) {
+            bx_ok = all ? 1 : 0;
+            wait_note(kWaitHalo, t0);
+        }
+    }
+    __syncthreads();
+    if (!bx_ok) return false;
+#pragma unroll
+    for (int s = 0; s < kHaloSides; ++s) {
+        if (!touches(s)) continue;
+        const uint64_t* src = halo_inbox(g_mb.self, par, s, A.hx_cap);
+        const int64_t base = s == 0 ? -pl : s == 1 ? nz * pl : s == 2 ? A.fy : s == 3 ? A.fy + nx * nz : s == 4 ? A.fx : A.fx + ny * nz;
+        const int64_t len = plen(s);
+        for (int64_t q = threadIdx.x; q < len; q += nthr) {
+            int64_t f, unused;
+            at(s, q, f, unused);
+            v[base + f] = ld_inbox(src + f);
+        }
+    }
+    __syncthreads();  // the march's loads of these layers follow (same workgroup)
+    return true;
+}
+
 // ------------------------------------------------------------------------------ 3D stencil, LDS rows
 // The same tile and z-march as k_st3d, but the y-neighbour rows come from the adjacent waves of the
 // block through LDS: every wave cooks its own centre row of plane k (it already holds it for the z
@@ -946,7 +1058,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L
     const int wv = threadIdx.x >> 6;
     const int nb = gridDim.x, b = blockIdx.x;
     int tz, txy;
-    tile3_of(b, nb, A.tiles_x, A.tiles_y, (int)((A.nz + A.rows - 1) / A.rows), A.hx_lo, A.hx_hi, A.zalt, tz, txy);
+    const int nzc = (int)((A.nz + A.rows - 1) / A.rows);
+    if (BLK && A.torder) {  // the in-launch block exchange's order (host-built: exchanging tiles first)
+        const int t = A.torder[b], tpl = A.tiles_x * A.tiles_y;
+        tz = t / tpl;
+        txy = t % tpl;
+    } else {
+        tile3_of(b, nb, A.tiles_x, A.tiles_y, nzc, A.hx_lo, A.hx_hi, A.zalt, tz, txy);
+    }
     const int ty = txy / A.tiles_x, tx = txy % A.tiles_x;
     const int64_t nx = A.nx, ny = A.ny, nz = A.nz, pl = nx * ny;
     const int64_t x0 = (int64_t)tx * (64 * VEC) + (int64_t)lane * VEC;
@@ -1018,6 +1137,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L
                 if (ht.hi) ib_hi = halo_inbox(g_mb.self, par, 1, A.hx_cap);
             }
         }
+    }
+    if constexpr (MODE != MODE_RES && BLK) {
+        if (A.hx_blk) (void)blk_tile_exchange<NW, VEC>(A, tx, ty, tz, z0, z1, nzc);  // (a time-out is flagged)
     }
     double acc = 0.0;
     // a plane ahead of the march (plane kk at offset o): the neighbour's patch from the inbox for a

@@ -26,7 +26,7 @@ def test_library_built_in_tree():
 
 
 KNOBS = ["NK_RES_NOXCHG", "NK_RES_JV", "NK_RES_STRIDED", "NK_RES_NTC", "NK_RES_PRE", "NK_F0R",
-         "NK_ST_BLOCKS", "NK_MGS_VARIANT", "NK_HALO_FUSE", "NK_RED_BLOCKS", "NK_UPD_U",
+         "NK_ST_BLOCKS", "NK_MGS_VARIANT", "NK_RED_BLOCKS", "NK_UPD_U", "NK_RES_NWC",
          "NK_ALLOC_STAGGER", "NK_ALLOC_STAGGER_MOD"]
 
 
@@ -44,9 +44,10 @@ def test_product_library_has_no_kbench_hooks_or_knobs():
         assert k.encode() in kb, k
     # the product is the smaller build: variant instantiations pruned
     assert len(prod) < 0.7 * len(kb)
-    # operational configuration stays readable in the product (transport, timeouts, shared-GPU rigs)
+    # operational configuration stays readable in the product (transport, timeouts, shared-GPU rigs, the
+    # one-GPU exchange rigs of bench.py --block-of / tools/halo_self.py and the exchange-form switch)
     for k in (b"NK_DIST_MAILBOX", b"NK_MB_SPIN_LIMIT", b"NK_RES_SHARED", b"NK_MGS_RESIDENT", b"NK_HALO_CAP",
-              b"NK_DIST_FORCE"):
+              b"NK_DIST_FORCE", b"NK_HALO_SELF", b"NK_HALO_SELF_AXES", b"NK_HALO_FUSE", b"NK_SHARED_FUSE_MAX"):
         assert k in prod, k
 
 

@@ -626,6 +626,26 @@ def test_bench_reports_every_ranks_path(tmp_path):
     assert line["config"]["path"]["mailbox_all_ranks"]
 
 
+def test_self_block_exchange_forms_are_bitwise():
+    """3D blocks on one GPU (NK_HALO_SELF=2 rig: the lone rank is its own neighbour on all six sides): a
+    restarted FD-GMRES solve with every ghost layer of v exchanged INSIDE the Jv launch (blk_tile_exchange:
+    exchanging tiles first, patches through the tile flags) gives bit for bit the solution of the separate
+    k_faces_ipc launch (NK_HALO_FUSE=0) -- the layers hold the same values and the partials stay tile-indexed
+    -- and the path report says which form ran."""
+    wait_gpu_released()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "halo_self.py"), "--nx", "200", "--ny", "72",
+                        "--nz", "40", "--itmax", "25", "--modes", "blocks,blockk"], capture_output=True, text=True,
+                       timeout=240, env=dict(os.environ))
+    assert p.returncode == 0, (p.stdout + p.stderr)[-3000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("blocks vs blockk")][-1]
+    assert "(bitwise: True)" in line, p.stdout[-3000:]
+    rec = {r["mode"]: r for r in (json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith('{"mode"'))}
+    assert rec["blocks"]["path"]["jv_halo_fused"] > 0 and rec["blocks"]["path"]["jv_halo_separate"] == 0
+    assert rec["blockk"]["path"]["jv_halo_separate"] > 0 and rec["blockk"]["path"]["jv_halo_fused"] == 0
+    assert "halo_faces" in rec["blockk"]["classes"]
+    assert rec["blocks"]["classes"].get("halo_faces", {}).get("launches", 0) <= 2  # u's layers only (once per solve)
+
+
 @pytest.mark.parametrize("dims", [("64", "48", "40"), ("96", "70", "0")])
 def test_self_ring_exchange_forms_are_bitwise(dims):
     """One process, a forced one-rank mailbox whose rank is its own lower and upper neighbour (kernel-variant
