@@ -360,6 +360,9 @@ class Bratu2D:
         from oracle import oracle as oc
 
         oc.set_threads(threads)
+        # the oracle sums in the device's order (oracle.set_devred, the GPU's CU count as its sweep grid), so
+        # the agreement below compares the iterates bit for bit; the arithmetic work is the same either way
+        oc.set_devred(True, cus=getattr(self, "dev_cus", 0) or 256)
         P = oc.bratu2d(self.n)
         u0 = oc.sin_ic(P)
         F0 = oc.residual(P, u0)
@@ -379,6 +382,7 @@ class Bratu2D:
             itmax = max(m, min(itmax, int(20.0 / per_step) // m * m))
         log(f"cpu baseline: {threads} threads, {dt1:.1f} s per restart cycle -> itmax {itmax}")
         x, st, dt = solve(itmax)
+        oc.set_devred(False)
         self.x_cpu, self.cpu_itmax = x, itmax
         return dict(value=st["n_matvec"] / dt, unit="matvecs/s", cores=oc.get_threads(), kind="port",
                     sample=f"oracle/nk_oracle.c: the Krylov solve of one bench step -- GMRES({self.args.memory}) with "
@@ -409,7 +413,8 @@ class Bratu2D:
         return {"quantity": f"||F(u0 - x)|| after one Newton step (GMRES({self.args.memory}), "
                             f"{self.cpu_itmax} Arnoldi steps), GPU vs CPU, relative",
                 "value": d, "tolerance": 1e-10, "ok": d <= 1e-10, "n_res_gpu": n_gpu, "n_res_cpu": n_cpu,
-                "x_rel_diff": dx}
+                "x_rel_diff": dx, "x_bitwise": bool(np.array_equal(x, self.x_cpu)),
+                "cpu_reduction_order": "the device's (oracle.set_devred)"}
 
     def free(self):
         self.ws.free()
@@ -879,6 +884,7 @@ def main():
             else:  # the fastest thread count the affinity mask offers (on a shared host, more is not faster)
                 threads, probe = cpu_thread_probe(affinity, share)
             log(f"cpu baseline on {threads} threads (affinity mask {affinity}, probe {probe})")
+            W.dev_cus = paths[0].get("resident_blocks") or 0  # the sweep grid the oracle's device order follows
             cb = W.cpu_baseline(threads)
             cb["value"] = round(cb["value"], 4)
             cb["host_cpus"] = {"nproc": os.cpu_count(), "affinity": affinity,

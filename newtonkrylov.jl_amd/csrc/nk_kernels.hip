@@ -725,8 +725,15 @@ int launch_stencil_ex(nk_ctx* c, const StencilIn& in, Red* red, int rows_overrid
         const bool share_ok = c->share_most <= 1 || shared_slab_points(c, p, g) <= fuse_max;
         const bool fuse = fuse_env && c->mb_on && (c->nranks > 1 || self) && share_ok && !per && !A.blk && in.mode != MODE_RES &&
                           (g.dim == 2 || (g.dim == 3 && A.lds3)) && g.plane <= c->halo_cap && tiles_pl <= kHaloTileFlags;
-        if (A.blk) {  // 3D blocks: every ghost layer inside this launch (blk_tile_exchange) or k_faces_ipc first
-            const bool bfuse = fuse_env && c->mb_on && in.mode != MODE_RES && rows_override <= 0 && blk_inlaunch_ok(c, p, fuse_max);
+        if (A.blk) {  // 3D blocks: k_faces_ipc first, or (opt-in) every ghost layer inside this launch
+            // In-launch (blk_tile_exchange) is bitwise the same but SLOWER on one GPU, the only place it can be
+            // measured here: the self-block 256^3 Jv 145 + 22 us (faces kernel) -> 187 us in-launch (2x2x2, every
+            // tile exchanges x patches and waits a round trip), 145 + 21 -> 172 us at 1x2x4 (profiles/r06/
+            // ab_blk_*.json).  NK_BLK_INLAUNCH=1 keeps it reachable for xGMI, where the separate kernel's
+            // transfer -- not a round trip -- would dominate (unmeasured)
+            static const int blk_in_env = env_cfg("NK_BLK_INLAUNCH", 0);
+            const bool bfuse = blk_in_env && fuse_env && c->mb_on && in.mode != MODE_RES && rows_override <= 0 &&
+                               blk_inlaunch_ok(c, p, fuse_max);
             if (bfuse) {
                 ++c->n_jv_halo_fused;
                 A.hx_blk = 1;

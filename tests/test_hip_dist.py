@@ -435,7 +435,9 @@ def test_shared_gpu_ghost_plane_form_is_rank_uniform(tmp_path, fuse_max, form):
                                                 ("2,2,1", (38, 22, 64), "midpoint"), ("1,2,4", (16, 40, 72), "midpoint"),
                                                 ("4,2,1", (130, 18, 20), "midpoint"), ("2,2,2", (48, 40, 36), "euler"),
                                                 ("4,2,1", (130, 18, 20), "euler"), ("2,2,2", (40, 20, 24), "trapezoid"),
-                                                ("2,2,2", (40, 20, 24), "midpoint-host")])
+                                                ("2,2,2", (40, 20, 24), "midpoint-host"),
+                                                ("2,2,2", (48, 40, 36), "euler-inlaunch"),
+                                                ("1,2,4", (16, 40, 72), "midpoint-inlaunch")])
 def test_heat3d_midpoint_blocks_match_oracle(tmp_path, pgrid, nxyz, scheme):
     """BASELINE config 5's decomposition: 3D blocks (px x py x pz process grid, nk_dist_grid) of the 3D
     heat operator (G_Midpoint!, alpha 0.3; G_Euler!, whose Krylov FD Jv recomputes F(u); G_Trapezoid!, whose
@@ -448,9 +450,10 @@ def test_heat3d_midpoint_blocks_match_oracle(tmp_path, pgrid, nxyz, scheme):
     world = int(np.prod([int(t) for t in pgrid.split(",")]))
     nx, ny, nz = nxyz
     host = scheme.endswith("-host")  # the mailbox (faces included) in host shared memory
-    scheme = scheme.replace("-host", "")
+    inl = scheme.endswith("-inlaunch")  # every ghost layer of a Krylov Jv inside its launch (NK_BLK_INLAUNCH=1)
+    scheme = scheme.replace("-host", "").replace("-inlaunch", "")
     out = str(tmp_path / "blk")
-    env = worker_env(world, **({"NK_DIST_MAILBOX": "host"} if host else {}))
+    env = worker_env(world, **({"NK_DIST_MAILBOX": "host"} if host else {}), **({"NK_BLK_INLAUNCH": "1"} if inl else {}))
     rc, log = run_ranks(world, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
                                 "--problem", "heat3d", "--nx", str(nx), "--ny", str(ny), "--nz", str(nz),
                                 "--pgrid", pgrid, "--scheme", scheme], env)
@@ -458,6 +461,7 @@ def test_heat3d_midpoint_blocks_match_oracle(tmp_path, pgrid, nxyz, scheme):
     meta = json.load(open(out + ".json"))
     assert meta["mailbox"] and meta["path"]["halo_waits"] > 0
     assert meta["path"]["mailbox_host"] == host
+    assert (meta["path"]["jv_halo_fused"] > 0) == inl and (meta["path"]["jv_halo_separate"] > 0) == (not inl)
     if scheme == "euler":  # G_Euler!'s FD Jv in the Krylov solve recomputes F(u) -- faces of u included
         assert meta["path"]["jv_fd_f0r"] > 0
     d = np.load(out + ".npz")
@@ -628,22 +632,22 @@ def test_bench_reports_every_ranks_path(tmp_path):
 
 def test_self_block_exchange_forms_are_bitwise():
     """3D blocks on one GPU (NK_HALO_SELF=2 rig: the lone rank is its own neighbour on all six sides): a
-    restarted FD-GMRES solve with every ghost layer of v exchanged INSIDE the Jv launch (blk_tile_exchange:
-    exchanging tiles first, patches through the tile flags) gives bit for bit the solution of the separate
-    k_faces_ipc launch (NK_HALO_FUSE=0) -- the layers hold the same values and the partials stay tile-indexed
-    -- and the path report says which form ran."""
+    restarted FD-GMRES solve with every ghost layer of v exchanged INSIDE the Jv launch (NK_BLK_INLAUNCH=1,
+    blk_tile_exchange: exchanging tiles first, patches through the tile flags) gives bit for bit the solution
+    of the separate k_faces_ipc launch (the default) -- the layers hold the same values and the partials stay
+    tile-indexed -- and the path report says which form ran."""
     wait_gpu_released()
     p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "halo_self.py"), "--nx", "200", "--ny", "72",
-                        "--nz", "40", "--itmax", "25", "--modes", "blocks,blockk"], capture_output=True, text=True,
+                        "--nz", "40", "--itmax", "25", "--modes", "blocks,blocki"], capture_output=True, text=True,
                        timeout=240, env=dict(os.environ))
     assert p.returncode == 0, (p.stdout + p.stderr)[-3000:]
-    line = [ln for ln in p.stdout.splitlines() if ln.startswith("blocks vs blockk")][-1]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("blocki vs blocks")][-1]
     assert "(bitwise: True)" in line, p.stdout[-3000:]
     rec = {r["mode"]: r for r in (json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith('{"mode"'))}
-    assert rec["blocks"]["path"]["jv_halo_fused"] > 0 and rec["blocks"]["path"]["jv_halo_separate"] == 0
-    assert rec["blockk"]["path"]["jv_halo_separate"] > 0 and rec["blockk"]["path"]["jv_halo_fused"] == 0
-    assert "halo_faces" in rec["blockk"]["classes"]
-    assert rec["blocks"]["classes"].get("halo_faces", {}).get("launches", 0) <= 2  # u's layers only (once per solve)
+    assert rec["blocki"]["path"]["jv_halo_fused"] > 0 and rec["blocki"]["path"]["jv_halo_separate"] == 0
+    assert rec["blocks"]["path"]["jv_halo_separate"] > 0 and rec["blocks"]["path"]["jv_halo_fused"] == 0
+    assert "halo_faces" in rec["blocks"]["classes"]
+    assert rec["blocki"]["classes"].get("halo_faces", {}).get("launches", 0) <= 2  # u's layers only (once per solve)
 
 
 @pytest.mark.parametrize("dims", [("64", "48", "40"), ("96", "70", "0")])

@@ -9,9 +9,9 @@ for the GPU.  Modes, each in its own process:
   fused   + self ring, v's ghost planes inside the Jv launch (halo_tile_exchange, the product default)
   kernel  + self ring, a separate exchange kernel before every Jv (NK_HALO_FUSE=0)
   blocks  3D only: the rank is its own neighbour on all SIX sides (NK_HALO_SELF=2) -- config 5's 3D-block
-          path: every ghost layer of v inside the Jv launch (blk_tile_exchange), k_st3l reading the x / y
-          faces at the block's edges (the operator differs: every axis wraps; the cost is what is measured)
-  blockk  the same with one packed-face exchange launch per Jv first (k_faces_ipc, NK_HALO_FUSE=0)
+          path: one packed-face exchange launch per Jv (k_faces_ipc) and k_st3l reading the x / y faces
+          at the block's edges (the operator differs: every axis wraps; the cost is what is measured)
+  blocki  the same with every ghost layer of v inside the Jv launch (blk_tile_exchange, NK_BLK_INLAUNCH=1)
 
 fused - mbox and kernel - mbox are the exchange's cost per Arnoldi step.  fused and kernel apply the same
 operator (the same ghost planes, the same per-point arithmetic) but the fused launch dispatches the
@@ -48,7 +48,7 @@ ENV = {
     "fused": {"NK_DIST_FORCE": "1", "NK_DIST_MAILBOX": "1", "NK_HALO_SELF": "1"},
     "kernel": {"NK_DIST_FORCE": "1", "NK_DIST_MAILBOX": "1", "NK_HALO_SELF": "1", "NK_HALO_FUSE": "0"},
     "blocks": {"NK_DIST_FORCE": "1", "NK_DIST_MAILBOX": "1", "NK_HALO_SELF": "2"},
-    "blockk": {"NK_DIST_FORCE": "1", "NK_DIST_MAILBOX": "1", "NK_HALO_SELF": "2", "NK_HALO_FUSE": "0"},
+    "blocki": {"NK_DIST_FORCE": "1", "NK_DIST_MAILBOX": "1", "NK_HALO_SELF": "2", "NK_BLK_INLAUNCH": "1"},
 }
 
 
@@ -113,7 +113,7 @@ rows = []
 for mode in args.modes.split(","):
     env = dict(os.environ, **ENV[mode])  # (the rigs are operational knobs of the product library)
     env.pop("NK_KBENCH_LIB", None)
-    for k in ("NK_HALO_SELF", "NK_HALO_FUSE", "NK_DIST_FORCE", "NK_DIST_MAILBOX"):  # (NK_HALO_SELF=2: blocks)
+    for k in ("NK_HALO_SELF", "NK_HALO_FUSE", "NK_DIST_FORCE", "NK_DIST_MAILBOX", "NK_BLK_INLAUNCH"):
         if k not in ENV[mode]:
             env.pop(k, None)
     p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", mode, "--nx", str(args.nx), "--ny",
@@ -137,9 +137,9 @@ for r in rows:
 import numpy as np  # noqa: E402
 
 modes = {r["mode"] for r in rows}
-if {"blocks", "blockk"} <= modes:
-    xb, xk = (np.load(os.path.join(args.xdir, f"x_{m}.npy")) for m in ("blocks", "blockk"))
-    print(f"blocks vs blockk: max |dx| / max |x| = {np.max(np.abs(xb - xk)) / np.max(np.abs(xk)):.2e} "
+if {"blocks", "blocki"} <= modes:
+    xb, xk = (np.load(os.path.join(args.xdir, f"x_{m}.npy")) for m in ("blocki", "blocks"))
+    print(f"blocki vs blocks: max |dx| / max |x| = {np.max(np.abs(xb - xk)) / np.max(np.abs(xk)):.2e} "
           f"(bitwise: {np.array_equal(xb, xk)})")
 if not {"fused", "kernel", "plain", "mbox"} <= modes:
     sys.exit(0)
