@@ -378,10 +378,22 @@ static void op_apply(oc_op* A, double* out, const double* v, double vnorm) {
  *   sweep: k_mgs_res: block b owns slots [b S / G, (b + 1) S / G) of 256 double2; partials summed by
  *          one polling wave (lane l: blocks l, 64 + l, 128 + l, 192 + l, then a wave sum) nk_resident.hip */
 static int OC_DEVRED = 0, OC_DEV_CUS = 256, OC_DEV_RL = 39;
+/* the ranks' decomposition (px x py x pz blocks, rank = (iz py + iy) px + ix, every axis split as
+ * ariadne_hip.block / slab split it; 2D slabs: 1 x R x 1) and whether their sweeps run resident (ranks
+ * sharing one GPU do not) -- each rank's partials in its own block's order, the ranks' sums added in rank
+ * order as the peer mailbox adds them (mb_recv) */
+static int OC_DEV_PX = 1, OC_DEV_PY = 1, OC_DEV_PZ = 1, OC_DEV_RESIDENT = 1;
 void oc_set_devred(int on, int cus, int rl) {
     OC_DEVRED = on;
     OC_DEV_CUS = cus > 0 && cus <= 256 ? cus : 256;
     OC_DEV_RL = rl >= 0 ? rl : 39;
+    OC_DEV_PX = OC_DEV_PY = OC_DEV_PZ = OC_DEV_RESIDENT = 1;
+}
+void oc_set_devred_ranks(int px, int py, int pz, int resident) {
+    OC_DEV_PX = px > 0 ? px : 1;
+    OC_DEV_PY = py > 0 ? py : 1;
+    OC_DEV_PZ = pz > 0 ? pz : 1;
+    OC_DEV_RESIDENT = resident != 0;
 }
 int oc_get_devred(void) { return OC_DEVRED; }
 
@@ -476,10 +488,41 @@ int64_t oc_dr_tile_parts2d(int64_t nx, int64_t ny, const double* x, const double
     }
     return tx_n * ty_n;
 }
-static double dr_tiles(const oc_problem* P, const double* x, const double* y) {
-    const int64_t nt = oc_dr_tile_parts2d(P->nx, P->ny, x, y, NULL);
+/* k_st3l's tiles (launch_stencil_ex, nk_kernels.hip): 4 rows (one per wave) x 64 VEC columns, z-chunks of
+ * `planes` (blocks: 16; else about 8192 tiles, at least 16), partial index tz tiles_x tiles_y + ty tiles_x + tx;
+ * thread (wave w, lane l) sums its VEC points of row ty 4 + w plane by plane upward */
+int64_t oc_dr_tile_parts3d(int64_t nx, int64_t ny, int64_t nz, int blk, const double* x, const double* y, double* parts) {
+    if (!y) y = x;
+    const int vec = nx % 2 == 0 ? 2 : 1;
+    const int64_t tx_n = (nx + 64 * vec - 1) / (64 * vec), ty_n = (ny + 3) / 4, tpl = tx_n * ty_n;
+    int64_t planes = (nz * tpl + 8191) / 8192;
+    if (planes < 16 || blk) planes = 16;
+    if (planes > nz) planes = nz;
+    const int64_t nzc = (nz + planes - 1) / planes, pl = nx * ny;
+    if (!parts) return tpl * nzc;
+#pragma omp parallel for schedule(static)
+    for (int64_t tl = 0; tl < tpl * nzc; ++tl) {
+        const int64_t tz = tl / tpl, ty = (tl % tpl) / tx_n, tx = tl % tx_n;
+        const int64_t z0 = tz * planes, z1 = z0 + planes < nz ? z0 + planes : nz;
+        double acc[256] = {0.0};
+        for (int t = 0; t < 256; ++t) {
+            const int64_t j = ty * 4 + t / 64, x0 = tx * 64 * vec + (int64_t)(t % 64) * vec;
+            if (x0 >= nx || j >= ny) continue;
+            double a = 0.0;
+            for (int64_t k = z0; k < z1; ++k)
+                for (int q = 0; q < vec; ++q) a = fma(x[k * pl + j * nx + x0 + q], y[k * pl + j * nx + x0 + q], a);
+            acc[t] = a;
+        }
+        parts[tl] = dr_block(acc);
+    }
+    return tpl * nzc;
+}
+/* one rank's sum of its stencil launch's tile partials (reduce_input over the tiles) */
+static double dr_tiles_local(int dim, int64_t nx, int64_t ny, int64_t nz, int blk, const double* x, const double* y) {
+    const int64_t nt = dim == 3 ? oc_dr_tile_parts3d(nx, ny, nz, blk, x, y, NULL) : oc_dr_tile_parts2d(nx, ny, x, y, NULL);
     double* parts = (double*)malloc(sizeof(double) * (size_t)nt);
-    oc_dr_tile_parts2d(P->nx, P->ny, x, y, parts);
+    if (dim == 3) oc_dr_tile_parts3d(nx, ny, nz, blk, x, y, parts);
+    else oc_dr_tile_parts2d(nx, ny, x, y, parts);
     const double r = oc_dr_ri(parts, nt);
     free(parts);
     return r;
@@ -530,10 +573,56 @@ static double dr_sweep(int64_t n, const double* x, const double* y) {
     oc_dr_sweep_parts(n, x, y, G, parts);
     return oc_dr_poll1(parts, G);
 }
-/* devred applies to one-rank 2D GMRES / FGMRES without preconditioners (the path the tests compare) */
+/* devred applies to 2D / 3D GMRES / FGMRES without preconditioners (the paths the tests compare) */
 static int dr_on(const oc_problem* P) {
-    return OC_DEVRED && (P->kind == OC_BRATU2D || P->kind == OC_HEAT2D_EULER || P->kind == OC_HEAT2D_MIDPOINT ||
-                         P->kind == OC_HEAT2D_TRAPEZOID);
+    return OC_DEVRED && P->kind != OC_BRATU1D;
+}
+enum { DR_RED = 0, DR_WIDE = 1, DR_TILES = 2, DR_PASS = 3 };
+/* one reduction of sum x_i y_i (y NULL: x_i^2) over the global grid, as the ranks compute it: each rank its
+ * block's tree (DR_RED: k_sumsq / k_dot over red_blocks; DR_WIDE: k_update_x's wide_blocks; DR_TILES: the
+ * stencil's tiles; DR_PASS: an MGS pass of an np-pass step -- the resident sweep where it runs, else
+ * k_mgs_pass's chunks), then the ranks' values added in rank order from 0.0 (mb_recv) */
+static double dr_reduce(const oc_problem* P, int kind, const double* x, const double* y, int np) {
+    const int dim = P->kind == OC_BRATU2D || oc_heat_dim(P->kind) == 2 ? 2 : 3;
+    const int px = OC_DEV_PX, py = OC_DEV_PY, pz = dim == 3 ? OC_DEV_PZ : 1;
+    const int64_t NX = P->nx, NY = P->ny, NZ = dim == 3 ? P->nz : 1;
+    const int R = px * py * pz, blk = dim == 3 && px * py > 1;
+    double total = 0.0;
+    double *lx = NULL, *ly = NULL;
+    for (int r = 0; r < R; ++r) {
+        const int ix = r % px, iy = (r / px) % py, iz = r / (px * py);
+        int64_t o[3], m[3];
+        const int64_t N[3] = {NX, NY, NZ};
+        const int idx[3] = {ix, iy, iz}, parts_[3] = {px, py, pz};
+        for (int a = 0; a < 3; ++a) {  /* split as ariadne_hip.block / slab: the first N % p parts one larger */
+            const int64_t base = N[a] / parts_[a], extra = N[a] % parts_[a];
+            m[a] = base + (idx[a] < extra ? 1 : 0);
+            o[a] = idx[a] * base + (idx[a] < extra ? idx[a] : extra);
+        }
+        const int64_t nl = m[0] * m[1] * m[2];
+        const double *xs = x, *ys = y;
+        if (R > 1) {  /* this rank's block, x fastest */
+            lx = (double*)realloc(lx, sizeof(double) * (size_t)nl);
+            if (y) ly = (double*)realloc(ly, sizeof(double) * (size_t)nl);
+            for (int64_t k = 0; k < m[2]; ++k)
+                for (int64_t j = 0; j < m[1]; ++j) {
+                    const int64_t g = ((o[2] + k) * NY + o[1] + j) * NX + o[0], l = (k * m[1] + j) * m[0];
+                    memcpy(lx + l, x + g, sizeof(double) * (size_t)m[0]);
+                    if (y) memcpy(ly + l, y + g, sizeof(double) * (size_t)m[0]);
+                }
+            xs = lx;
+            ys = y ? ly : NULL;
+        }
+        double v;
+        if (kind == DR_TILES) v = dr_tiles_local(dim, m[0], m[1], m[2], blk, xs, ys);
+        else if (kind == DR_WIDE) v = dr_chunk(nl, xs, ys, dr_wide_blocks(nl));
+        else if (kind == DR_PASS && OC_DEV_RESIDENT && dr_sweep_applies(nl, np)) v = dr_sweep(nl, xs, ys ? ys : xs);
+        else v = dr_chunk(nl, xs, ys, dr_red_blocks(nl));
+        total = R > 1 ? total + v : v;
+    }
+    free(lx);
+    free(ly);
+    return total;
 }
 
 /* ------------------------------------------------------------------ Krylov.jl sym_givens (real) */
@@ -694,13 +783,13 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
     double* z = (double*)calloc((size_t)cap, sizeof(double));
     double* R = (double*)calloc((size_t)cap * (cap + 1) / 2, sizeof(double));
 
-    /* OC_DEVRED: every reduction in the device's order (nk_krylov.cpp gmres, one rank, no preconditioner) */
+    /* OC_DEVRED: every reduction in the device's order (nk_krylov.cpp gmres, no preconditioner) */
     const int dev = dr_on(A->P) && !N && !M;
     double xnorm_dev = 0.0; /* ||x|| of the last cycle's update (k_update_x partials), the restart's FD step */
     oc_fill(n, x, 0.0);
     oc_copy(n, w, b); /* w = b - A*0 */
     if (M) prec_apply(A, M, r0, w); /* r0 = M w */
-    double beta = dev ? sqrt(dr_chunk(n, r0, NULL, dr_red_blocks(n))) : oc_norm(n, r0); /* (k_sumsq + k_finalize) */
+    double beta = dev ? sqrt(dr_reduce(A->P, DR_RED, r0, NULL, 0)) : oc_norm(n, r0); /* (k_sumsq + k_finalize) */
     double rNorm = beta;
     PUSH_HIST(rNorm);
     const double eps_ = o->atol + o->rtol * rNorm;
@@ -732,7 +821,7 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
             }
             /* device: the first cycle keeps beta; a restart's ||b - A x|| is the fused EPI_RESID stencil's */
             if (!dev) beta = oc_norm(n, r0);
-            else if (restart && npass >= 1) beta = sqrt(dr_tiles(A->P, r0, NULL));
+            else if (restart && npass >= 1) beta = sqrt(dr_reduce(A->P, DR_TILES, r0, NULL, 0));
             z[0] = beta;
             /* kdivcopy!(n, V[1], r0, rNorm): Krylov.jl divides by rNorm -- beta on the first pass, after a
              * restart the previous cycle's estimate |zeta|, not the beta just computed */
@@ -769,15 +858,14 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
                      * the partials of <V_next, q> (<q, q> after the last): the resident sweep's slot partition
                      * and polling wave, or (one pass, or not resident) k_mgs_pass's chunks + reduce_input */
                     const int np = reorth ? 2 * k : k;
-                    const int sweep = dr_sweep_applies(n, np);
-                    double h = dr_tiles(A->P, V[0], q);
+                    double h = dr_reduce(A->P, DR_TILES, V[0], q, 0);
                     for (int t = 0; t < np; ++t) {
                         const int i = t % k;
                         if (t < k) R[nr + i] = h;
                         else R[nr + i] += h;
                         oc_axpy(n, -h, V[i], q);
                         const double* nxt = t + 1 < np ? V[(t + 1) % k] : q;
-                        h = sweep ? dr_sweep(n, nxt, q) : dr_chunk(n, nxt, q, dr_red_blocks(n));
+                        h = dr_reduce(A->P, DR_PASS, nxt, q, np);
                     }
                     Hbis = sqrt(h);
                 } else {
@@ -842,7 +930,7 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
             }
             if (restart) oc_axpy(n, 1.0, xr, x);
             /* device: ||x|| from the x update's partials (k_update_x over wide_blocks, k_finalize) */
-            if (dev && restart && A->mode == OC_JV_FD) xnorm_dev = sqrt(dr_chunk(n, x, NULL, dr_wide_blocks(n)));
+            if (dev && restart && A->mode == OC_JV_FD) xnorm_dev = sqrt(dr_reduce(A->P, DR_WIDE, x, NULL, 0));
             iter += inner_iter;
             inner_itmax = itmax - iter;
             tired = iter >= itmax;
@@ -1033,7 +1121,7 @@ int oc_krylov_solve(const oc_problem* P, int jv_mode, int algo, const double* u,
                     double* hist, int64_t hist_cap, int64_t* hist_len) {
     oc_op A = {P, jv_mode, u, F0, 0.0, 0};
     if (jv_mode == OC_JV_FD)  /* device: k_sumsq + k_finalize (nk_krylov_solve without a known ||u||) */
-        A.unorm = dr_on(P) ? sqrt(dr_chunk(oc_n(P), u, NULL, dr_red_blocks(oc_n(P)))) : oc_norm(oc_n(P), u);
+        A.unorm = dr_on(P) ? sqrt(dr_reduce(P, DR_RED, u, NULL, 0)) : oc_norm(oc_n(P), u);
     if (algo == OC_ALGO_CG) return oc_cg(&A, b, x, o, st, hist, hist_cap, hist_len);
     oc_krylov_opts oo = *o;
     oo.flexible = algo == OC_ALGO_FGMRES;

@@ -606,6 +606,32 @@ def test_device_order_trees_match_their_restatement():
             tiles.append(_block(acc))
     assert list(d["tiles"]) == tiles
     assert d["ri_tiles"] == _ri(tiles)
+    # k_st3l tiles: 4 rows (one per wave) x 64 VEC columns, z-chunks of 16 planes (blocks; the same here for the
+    # single domain: 20 planes x 36 tiles stay under 8192 tiles), thread (wave, lane) upward over its planes
+    import ctypes as C
+    nx, ny, nz = 130, 9, 20
+    X3, Y3 = rng.standard_normal(nx * ny * nz), rng.standard_normal(nx * ny * nz)
+    L = oc.lib()
+    nt = L.oc_dr_tile_parts3d(nx, ny, nz, 1, oc._p(X3), oc._p(Y3), None)
+    got = np.zeros(nt)
+    L.oc_dr_tile_parts3d(nx, ny, nz, 1, oc._p(X3), oc._p(Y3), oc._p(got))
+    tx_n, ty_n, pl = 2, 3, nx * ny  # 130 columns (VEC 2): 2 tiles of 128 (the second 2 wide); 9 rows: 3 tiles of 4
+    want = []
+    for tz in range(2):
+        for ty in range(ty_n):
+            for tx in range(tx_n):
+                acc = [0.0] * 256
+                for t in range(256):
+                    j, x0 = ty * 4 + t // 64, tx * 128 + (t % 64) * 2
+                    if x0 >= nx or j >= ny:
+                        continue
+                    a = 0.0
+                    for k in range(tz * 16, min(tz * 16 + 16, nz)):
+                        for q in range(2):
+                            a = _fma(X3[k * pl + j * nx + x0 + q], Y3[k * pl + j * nx + x0 + q], a)
+                    acc[t] = a
+                want.append(_block(acc))
+    assert nt == len(want) and list(got) == want
 
 
 def test_device_order_gmres_is_a_reordering_only():
