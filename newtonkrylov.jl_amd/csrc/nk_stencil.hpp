@@ -435,8 +435,10 @@ struct RawRow {
     double g[VEC], ge, ge2;  // u_n (G)
 };
 
+// PER (the second edge slot): e2 = false skips its loads (wave-uniform: no VMEM instruction issued) -- a 3D
+// block's x-hi face travels in the first slot except in a one-lane last tile
 template <int MODE, int VEC, bool EDGE = true, bool G = false, bool PER = false, bool NTU = false>
-__device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o, int64_t oe, int64_t oe2 = 0) {
+__device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o, int64_t oe, int64_t oe2 = 0, bool e2 = true) {
     RawRow<MODE, VEC> r;
     const double* __restrict__ pa = (MODE == MODE_JEXACT) ? A.v : A.u;
     if constexpr (VEC % 2 == 0) {
@@ -455,7 +457,7 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o,
     }
     if constexpr (EDGE) r.ae = pa[oe];
     else r.ae = 0.0;
-    if constexpr (EDGE && PER) r.ae2 = pa[oe2];
+    if constexpr (EDGE && PER) r.ae2 = e2 ? pa[oe2] : 0.0;
     if constexpr (MODE == MODE_JFD) {
         if constexpr (VEC % 2 == 0) {
 #pragma unroll
@@ -468,7 +470,7 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o,
         }
         if constexpr (EDGE) r.be = A.v[oe];
         else r.be = 0.0;
-        if constexpr (EDGE && PER) r.be2 = A.v[oe2];
+        if constexpr (EDGE && PER) r.be2 = e2 ? A.v[oe2] : 0.0;
     }
     if constexpr (G) {
         if constexpr (VEC % 2 == 0) {
@@ -482,7 +484,7 @@ __device__ __forceinline__ RawRow<MODE, VEC> load_raw(const KArgs& A, int64_t o,
         }
         if constexpr (EDGE) r.ge = A.un[oe];
         else r.ge = 0.0;
-        if constexpr (EDGE && PER) r.ge2 = A.un[oe2];
+        if constexpr (EDGE && PER) r.ge2 = e2 ? A.un[oe2] : 0.0;
     }
     return r;
 }
@@ -706,7 +708,9 @@ __device__ __forceinline__ double wave_shl1(double x) {  // lane i <- lane i + 1
 struct LR {
     double l, r;
 };
-template <bool PER>
+// BLK (3D blocks): lane 0's first slot is its left neighbour (in-array or the x-lo face), lane 63's and
+// the x-hi face lane's (rwrap) the right one; only a one-lane last tile (lane 0 on both) uses the second
+template <bool PER, bool BLK = false>
 __device__ __forceinline__ LR x_nbrs(const KArgs& A, double cfirst, double clast, double e, double e2, int lane,
                                      bool rwrap) {
     LR o;
@@ -719,7 +723,10 @@ __device__ __forceinline__ LR x_nbrs(const KArgs& A, double cfirst, double clast
     o.r = __shfl_down(cfirst, 1, 64);
 #endif
     if (lane == 0) o.l = e;
-    if constexpr (PER) {
+    if constexpr (BLK) {
+        if (rwrap) o.r = lane == 0 ? e2 : e;
+        else if (lane == 63) o.r = e;
+    } else if constexpr (PER) {
         if (lane == 63 || rwrap) o.r = e2;
     } else {
         if (lane == 63) o.r = e;
@@ -1096,12 +1103,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L
     }
     const bool ld_n = !lds_n && has_n, ld_s = !lds_s && has_s;  // wave-uniform
     XEdge xe{};
-    if constexpr (BLK) {  // in-array edges inside the block, faces at its x-ends
+    if constexpr (BLK) {  // in-array edges inside the block, faces at its x-ends -- one edge slot (one load per
+        // field and row, as a slab's), the second only for a one-lane last tile's x-hi face (e2w, wave-uniform)
         const bool lin = lane == 0 && act && x0 >= 1, rin = lane == 63 && act && x0 + VEC < nx;
-        xe.de = lin ? -1 : 0;
-        xe.ok = lin || fxl;
-        xe.de2 = rin ? VEC : 0;
-        xe.ok2 = rin || fxr;
+        xe.de = lin ? -1 : (rin ? VEC : 0);
+        xe.ok = lin || fxl || rin || (fxr && lane != 0);
+        xe.de2 = 0;
+        xe.ok2 = fxr && lane == 0;
         xe.rwrap = fxr;
     } else {
         xe = x_edge<VEC, PER>(lane, act, x0, nx);
@@ -1145,14 +1153,22 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L
     // a plane ahead of the march (plane kk at offset o): the neighbour's patch from the inbox for a
     // ghost plane fetched in this launch, else memory
     // the x-edge offsets of plane kk (BLK: the faces for the block's end columns of an interior plane)
-    auto eo1 = [&](int64_t kk, int64_t o) { return (fxl && kk >= 0 && kk < nz) ? A.fx + kk * ny + j : o + de; };
+    auto eo1 = [&](int64_t kk, int64_t o) {
+        if (BLK && kk >= 0 && kk < nz) {
+            if (fxl) return A.fx + kk * ny + j;
+            if (fxr && lane != 0) return A.fx + ny * nz + kk * ny + j;
+        }
+        return o + de;
+    };
     auto eo2 = [&](int64_t kk, int64_t o) { return (fxr && kk >= 0 && kk < nz) ? A.fx + ny * nz + kk * ny + j : o + de2; };
+    // BLK: the second edge slot's loads only where lane 0 is the x-hi face lane (a one-lane last tile)
+    const bool e2w = !BLK || ((A.nbm & 32) && j < ny && (int64_t)tx * (64 * VEC) + VEC == nx);
     // the halo rows of plane kk beyond the tile (BLK: the y faces beyond the block's first / last row)
     auto nrow = [&](int64_t kk, int64_t o) { return fyn ? A.fy + nx * nz + kk * nx + x0 : o + dn_; };
     auto srow = [&](int64_t kk, int64_t o) { return fys ? A.fy + kk * nx + x0 : o + ds; };
     auto ahead = [&](int64_t kk, int64_t o) {
         const uint64_t* ib = (ib_hi && kk == nz) ? ib_hi : ((ib_lo && kk == -1) ? ib_lo : nullptr);
-        return ib ? load_raw_ib<MODE, VEC, kG>(A, ib, o, oj) : load_raw<MODE, VEC, true, kG, kE2>(A, o, eo1(kk, o), eo2(kk, o));
+        return ib ? load_raw_ib<MODE, VEC, kG>(A, ib, o, oj) : load_raw<MODE, VEC, true, kG, kE2>(A, o, eo1(kk, o), eo2(kk, o), e2w);
     };
     if (z0 < nz) {
         const int64_t o0 = zs * pl + oj;
@@ -1160,7 +1176,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L
         const uint64_t* ibb = (ib_lo && kb == -1) ? ib_lo : ((ib_hi && kb == nz) ? ib_hi : nullptr);
         const RawRow<MODE, VEC> rm0 =
             ibb ? load_raw_ib<MODE, VEC, kG>(A, ibb, o0 - st, oj) : load_raw<MODE, VEC, false, kG, kE2>(A, o0 - st, 0);
-        const RawRow<MODE, VEC> rc0 = load_raw<MODE, VEC, true, kG, kE2>(A, o0, eo1(zs, o0), eo2(zs, o0));
+        const RawRow<MODE, VEC> rc0 = load_raw<MODE, VEC, true, kG, kE2>(A, o0, eo1(zs, o0), eo2(zs, o0), e2w);
         Field<VEC> fm = cook<MODE, VEC, SCH, kG, kE2>(A, rm0, act, false);
         Field<VEC> fc = cook<MODE, VEC, SCH, kG, kE2>(A, rc0, act, edge_ok, edge_ok2);
         Field<VEC> um{}, uc_{};  // F0R: the u field of planes k-1, k
@@ -1238,14 +1254,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L
                     if (!has_n) cnu[q] = 0.0;
                     if (!has_s) csu[q] = 0.0;
                 }
-                xu = x_nbrs<kE2>(A, uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
+                xu = x_nbrs<kE2, BLK>(A, uc_.c[0], uc_.c[VEC - 1], uc_.e, uc_.e2, lane, xe.rwrap);
             }
             // ---- compute plane k
-            const LR xn = x_nbrs<kE2>(A, fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
+            const LR xn = x_nbrs<kE2, BLK>(A, fc.c[0], fc.c[VEC - 1], fc.e, fc.e2, lane, xe.rwrap);
             const double lft = xn.l, rgt = xn.r;
             double glft = 0.0, grgt = 0.0;
             if constexpr (SCH == 2 && kG) {
-                const LR g2 = x_nbrs<kE2>(A, fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
+                const LR g2 = x_nbrs<kE2, BLK>(A, fc.g[0], fc.g[VEC - 1], fc.ge, fc.ge2, lane, xe.rwrap);
                 glft = g2.l;
                 grgt = g2.r;
             }
