@@ -638,16 +638,16 @@ def main():
     rccl_error = None
     if world > 1 and args.transport == "rccl":
         # ncclCommInitRank is collective: a rank that fails before entering it would leave the others
-        # blocked inside it.  So every rank first probes RCCL locally (its library answers a unique-id
-        # request on this rank's device) and the ranks vote over gloo; only a unanimous vote enters the
-        # collective init.  A failure INSIDE the init that not every rank sees can still block the
-        # others there -- the launcher's time limit is then what ends the job.
+        # blocked inside it.  So everything that can fail before it -- rank 0's unique id, a rank's local
+        # state (NK_BENCH_RCCL_FAIL=rank:K fakes that) -- is voted on over gloo first; only a unanimous
+        # vote enters the collective init.  A failure INSIDE the init that not every rank sees can still
+        # block the others there -- the launcher's time limit is then what ends the job.
         obj = [None]
         try:
             if fake_fail:
                 raise ah.NKError("NK_BENCH_RCCL_FAIL")
-            uid = ah.dist_unique_id()
-            obj = [uid if rank == 0 else None]
+            if rank == 0:
+                obj = [ah.dist_unique_id()]
         except ah.NKError as e:
             rccl_error = str(e)
         pre = [None] * world
