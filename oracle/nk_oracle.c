@@ -383,6 +383,7 @@ static int OC_DEVRED = 0, OC_DEV_CUS = 256, OC_DEV_RL = 39;
  * sharing one GPU do not) -- each rank's partials in its own block's order, the ranks' sums added in rank
  * order as the peer mailbox adds them (mb_recv) */
 static int OC_DEV_PX = 1, OC_DEV_PY = 1, OC_DEV_PZ = 1, OC_DEV_RESIDENT = 1;
+static double OC_DEV_BNORM = 0.0;  /* > 0: the Newton driver's ||F(u)||, which the device solve takes as ||b|| */
 void oc_set_devred(int on, int cus, int rl) {
     OC_DEVRED = on;
     OC_DEV_CUS = cus > 0 && cus <= 256 ? cus : 256;
@@ -789,7 +790,8 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
     oc_fill(n, x, 0.0);
     oc_copy(n, w, b); /* w = b - A*0 */
     if (M) prec_apply(A, M, r0, w); /* r0 = M w */
-    double beta = dev ? sqrt(dr_reduce(A->P, DR_RED, r0, NULL, 0)) : oc_norm(n, r0); /* (k_sumsq + k_finalize) */
+    /* device: the Newton loop hands ||F(u)|| over as ||b|| (nk_krylov_opts.b_norm), else k_sumsq + k_finalize */
+    double beta = dev ? (OC_DEV_BNORM > 0.0 ? OC_DEV_BNORM : sqrt(dr_reduce(A->P, DR_RED, r0, NULL, 0))) : oc_norm(n, r0);
     double rNorm = beta;
     PUSH_HIST(rNorm);
     const double eps_ = o->atol + o->rtol * rNorm;
@@ -1042,9 +1044,14 @@ int oc_newton_krylov(const oc_problem* P, double* u, const oc_newton_opts* o, oc
     double* minv = (o->mprecond == OC_PRECOND_JACOBI || o->mprecond == OC_PRECOND_ILU) ? (double*)malloc(sizeof(double) * n) : NULL;
     oc_op A = {P, o->jv_mode, u, res, 0.0, 0};
     int64_t nres_count = 0;
+    /* OC_DEVRED (GMRES / FGMRES without preconditioners): the device driver's norms in its order --
+     * ||F(u)|| from the residual kernel's tiles (nk_residual_norm), ||u|| from the update fused into the
+     * solve's last x update (k_update_x's wide chunks; k_sumsq before the first solve) */
+    const int dev = dr_on(P) && o->precond == OC_PRECOND_NONE && o->mprecond == OC_PRECOND_NONE && o->algo != OC_ALGO_CG;
+    double unorm_dev = 0.0;
     oc_residual(P, res, u);
     nres_count++;
-    double n_res = oc_norm(n, res);
+    double n_res = dev ? sqrt(dr_reduce(P, DR_TILES, res, NULL, 0)) : oc_norm(n, res);
     int64_t nh = 0;
     if (nres_hist && nh < hist_cap) nres_hist[nh] = n_res;
     nh++;
@@ -1058,7 +1065,8 @@ int oc_newton_krylov(const oc_problem* P, double* u, const oc_newton_opts* o, oc
         if (!o->rtol_user) ko.rtol = (o->forcing != OC_FORCING_NONE) ? eta : sqrt(DBL_EPSILON);
         oc_krylov_stats ks;
         memset(&ks, 0, sizeof ks);
-        if (o->jv_mode == OC_JV_FD) A.unorm = oc_norm(n, u);
+        if (o->jv_mode == OC_JV_FD)
+            A.unorm = !dev ? oc_norm(n, u) : (unorm_dev > 0.0 ? unorm_dev : sqrt(dr_reduce(P, DR_RED, u, NULL, 0)));
         /* N = factory(J) for this step (Ariadne.jl:318-333 passes N through to krylov_solve!) */
         oc_precond Np = {OC_PRECOND_NONE, o->precond_itmax, NULL, P};
         if (o->precond == OC_PRECOND_JACOBI) {
@@ -1089,13 +1097,17 @@ int oc_newton_krylov(const oc_problem* P, double* u, const oc_newton_opts* o, oc
         ko.M = Mp.kind != OC_PRECOND_NONE ? &Mp : NULL;
         ko.flexible = o->algo == OC_ALGO_FGMRES;
         /* b = copy(res) (Ariadne.jl:338): res is not overwritten by our operator, so pass it directly */
+        if (dev) OC_DEV_BNORM = n_res;
         if (o->algo == OC_ALGO_CG) oc_cg(&A, res, d, &ko, &ks, NULL, 0, NULL);
         else oc_gmres(&A, res, d, &ko, &ks, NULL, 0, NULL);
+        OC_DEV_BNORM = 0.0;
         oc_axpy(n, -1.0, d, u); /* u .-= 1 .* d */
+        /* device: fused into the last cycle's x update (wide chunks); no cycle ran: k_axpy_sumsq (red_blocks) */
+        if (dev) unorm_dev = sqrt(dr_reduce(P, ks.niter > 0 ? DR_WIDE : DR_RED, u, NULL, 0));
         double n_prior = n_res;
         oc_residual(P, res, u);
         nres_count++;
-        n_res = oc_norm(n, res);
+        n_res = dev ? sqrt(dr_reduce(P, DR_TILES, res, NULL, 0)) : oc_norm(n, res);
         if (isinf(n_res) || isnan(n_res)) break;
         if (o->forcing == OC_FORCING_EW) eta = oc_ew_forcing(o->eta_max, o->gamma, eta, tol, n_res, n_prior);
         outer += 1;

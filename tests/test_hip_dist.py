@@ -451,8 +451,9 @@ def test_heat3d_midpoint_blocks_match_oracle(tmp_path, pgrid, nxyz, scheme):
     vector's six ghost layers travel in one packed-face launch (k_faces_ipc: z planes into the ghost
     planes, x / y layers into the faces after the trailing plane, which k_st3l reads at the block's x / y
     edges).  Residual, exact and FD JVP bit-identical to the oracle on the whole grid, uneven splits
-    included (33 = 11 x 3, 17 planes, 130 = 4 x 32 + 2); one implicit step with the FD operator: equal
-    Newton / Krylov counts, so every inner product and Jv of the solve crossed the blocks correctly."""
+    included (33 = 11 x 3, 17 planes, 130 = 4 x 32 + 2); one implicit step with the FD operator against the
+    oracle in the device's summation order: equal Newton / Krylov counts and u bit for bit, so every inner
+    product and Jv of the solve crossed the blocks correctly."""
     world = int(np.prod([int(t) for t in pgrid.split(",")]))
     nx, ny, nz = nxyz
     host = scheme.endswith("-host")  # the mailbox (faces included) in host shared memory
@@ -480,10 +481,17 @@ def test_heat3d_midpoint_blocks_match_oracle(tmp_path, pgrid, nxyz, scheme):
     np.testing.assert_array_equal(d["F"], oc.residual(P, u0))
     np.testing.assert_array_equal(d["jv"], oc.jv_exact(P, u0, v))
     np.testing.assert_array_equal(d["jvfd"], oc.jv_fd(P, u0, v, F0=d["F"], eps=1e-6))
-    uo, so = oc.newton_krylov(P, u0, tol_abs=6e-6, jv="fd")
+    # the implicit step in the device's summation order (each rank's trees over its block, the ranks' sums
+    # in rank order, the Newton driver's norms included): counts and u_{n+1} bit for bit
+    oc.set_devred(True, cus=meta["path"]["resident_blocks"] or 256, ranks=tuple(int(t) for t in pgrid.split(",")),
+                  resident=meta["path"]["sweeps_resident"] > 0)
+    try:
+        uo, so = oc.newton_krylov(P, u0, tol_abs=6e-6, jv="fd")
+    finally:
+        oc.set_devred(False)
     assert meta["solved"] and so["solved"]
     assert (meta["outer"], meta["inner"]) == (so["outer_iterations"], so["inner_iterations"])
-    assert np.max(np.abs(d["u"] - uo)) <= 1e-10
+    np.testing.assert_array_equal(d["u"], uo)
 
 
 def test_block_grid_refusals():
