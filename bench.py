@@ -525,6 +525,7 @@ class HeatEuler:
         from oracle import oracle as oc
 
         oc.set_threads(threads)
+        oc.set_devred(True, cus=getattr(self, "dev_cus", 0) or 256)  # the device's summation order (agreement)
         m = self.n  # bounded sample: one time step of the same problem
         bcc = oc.BC_PERIODIC if self.args.bc == "periodic" else oc.BC_ZERO
         P = (oc.heat2d_euler(m, scheme=self.args.scheme, bc=bcc) if self.dim == 2
@@ -545,6 +546,7 @@ class HeatEuler:
                 self.cpu_step = (u0, u.copy(), st)
             P.un = u
             steps, newton, matvecs = steps + 1, newton + st["outer_iterations"], matvecs + st["n_matvec"]
+        oc.set_devred(False)
         return dict(value=matvecs / dt, unit="matvecs/s", cores=oc.get_threads(), kind="port",
                     sample=f"oracle/nk_oracle.c: {steps} {self.args.scheme} time steps (reorthogonalization="
                            f"{self.reorth}; {newton} Newton, {matvecs} matvecs) of the same {self.dim}D heat problem "
@@ -571,6 +573,7 @@ class HeatEuler:
         return {"quantity": f"u after one implicit {self.args.scheme} time step (converged newton_krylov!, "
                             f"tol_abs=6e-6), GPU vs CPU, relative 2-norm",
                 "value": d, "tolerance": 1e-10, "ok": bool(d <= 1e-10 and same),
+                "u_bitwise": bool(np.array_equal(u_gpu, u_cpu)), "cpu_reduction_order": "the device's (oracle.set_devred)",
                 "counts_gpu": [r.stats.outer_iterations, r.stats.inner_iterations],
                 "counts_cpu": [st["outer_iterations"], st["inner_iterations"]],
                 "n_res_gpu": r.stats.n_res, "n_res_cpu": st["n_res"]}

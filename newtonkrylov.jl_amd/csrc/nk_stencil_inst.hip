@@ -1,6 +1,6 @@
 // nk_stencil_inst.hip -- instantiates the stencil kernels of ONE problem kind (NK_ST_KIND, set by
 // the Makefile: one object per kind, compiled in parallel).
-#include "nk_stencil.hpp"
+#include "nk_stencil_kern.hpp"
 
 #ifndef NK_ST_KIND
 #error "compile with -DNK_ST_KIND=<problem kind>"
