@@ -518,12 +518,26 @@ int64_t oc_dr_tile_parts3d(int64_t nx, int64_t ny, int64_t nz, int blk, const do
     }
     return tpl * nzc;
 }
+/* k_st1d: one point per thread, one partial per 256-point block */
+int64_t oc_dr_tile_parts1d(int64_t nx, const double* x, const double* y, double* parts) {
+    if (!y) y = x;
+    const int64_t G = (nx + 255) / 256;
+    if (!parts) return G;
+    for (int64_t b = 0; b < G; ++b) {
+        double acc[256] = {0.0};
+        for (int t = 0; t < 256 && b * 256 + t < nx; ++t) acc[t] = fma(x[b * 256 + t], y[b * 256 + t], 0.0);
+        parts[b] = dr_block(acc);
+    }
+    return G;
+}
 /* one rank's sum of its stencil launch's tile partials (reduce_input over the tiles) */
 static double dr_tiles_local(int dim, int64_t nx, int64_t ny, int64_t nz, int blk, const double* x, const double* y) {
-    const int64_t nt = dim == 3 ? oc_dr_tile_parts3d(nx, ny, nz, blk, x, y, NULL) : oc_dr_tile_parts2d(nx, ny, x, y, NULL);
+    const int64_t nt = dim == 3 ? oc_dr_tile_parts3d(nx, ny, nz, blk, x, y, NULL)
+                       : dim == 2 ? oc_dr_tile_parts2d(nx, ny, x, y, NULL) : oc_dr_tile_parts1d(nx, x, y, NULL);
     double* parts = (double*)malloc(sizeof(double) * (size_t)nt);
     if (dim == 3) oc_dr_tile_parts3d(nx, ny, nz, blk, x, y, parts);
-    else oc_dr_tile_parts2d(nx, ny, x, y, parts);
+    else if (dim == 2) oc_dr_tile_parts2d(nx, ny, x, y, parts);
+    else oc_dr_tile_parts1d(nx, x, y, parts);
     const double r = oc_dr_ri(parts, nt);
     free(parts);
     return r;
@@ -574,9 +588,10 @@ static double dr_sweep(int64_t n, const double* x, const double* y) {
     oc_dr_sweep_parts(n, x, y, G, parts);
     return oc_dr_poll1(parts, G);
 }
-/* devred applies to 2D / 3D GMRES / FGMRES without preconditioners (the paths the tests compare) */
+/* devred applies to GMRES / FGMRES / CG without preconditioners (the paths the tests compare) */
 static int dr_on(const oc_problem* P) {
-    return OC_DEVRED && P->kind != OC_BRATU1D;
+    (void)P;
+    return OC_DEVRED;
 }
 enum { DR_RED = 0, DR_WIDE = 1, DR_TILES = 2, DR_PASS = 3 };
 /* one reduction of sum x_i y_i (y NULL: x_i^2) over the global grid, as the ranks compute it: each rank its
@@ -584,9 +599,9 @@ enum { DR_RED = 0, DR_WIDE = 1, DR_TILES = 2, DR_PASS = 3 };
  * stencil's tiles; DR_PASS: an MGS pass of an np-pass step -- the resident sweep where it runs, else
  * k_mgs_pass's chunks), then the ranks' values added in rank order from 0.0 (mb_recv) */
 static double dr_reduce(const oc_problem* P, int kind, const double* x, const double* y, int np) {
-    const int dim = P->kind == OC_BRATU2D || oc_heat_dim(P->kind) == 2 ? 2 : 3;
-    const int px = OC_DEV_PX, py = OC_DEV_PY, pz = dim == 3 ? OC_DEV_PZ : 1;
-    const int64_t NX = P->nx, NY = P->ny, NZ = dim == 3 ? P->nz : 1;
+    const int dim = P->kind == OC_BRATU1D ? 1 : (P->kind == OC_BRATU2D || oc_heat_dim(P->kind) == 2 ? 2 : 3);
+    const int px = OC_DEV_PX, py = dim >= 2 ? OC_DEV_PY : 1, pz = dim == 3 ? OC_DEV_PZ : 1;
+    const int64_t NX = P->nx, NY = dim >= 2 ? P->ny : 1, NZ = dim == 3 ? P->nz : 1;
     const int R = px * py * pz, blk = dim == 3 && px * py > 1;
     double total = 0.0;
     double *lx = NULL, *ly = NULL;
@@ -977,7 +992,10 @@ int oc_cg(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_kryl
     oc_copy(n, r, b);
     if (M) prec_apply(A, M, zr, r);
     oc_copy(n, p, zr);
-    double gamma = oc_dot(n, r, zr);
+    /* OC_DEVRED (no preconditioner): <r, r> from k_sumsq / k_cg_update's chunks, <p, Ap> from the stencil's
+     * tiles, ||p|| (the FD step) from k_sumsq (nk_krylov.cpp cg) */
+    const int dev = dr_on(A->P) && !M;
+    double gamma = dev ? dr_reduce(A->P, DR_RED, r, NULL, 0) : oc_dot(n, r, zr);
     double rNorm = sqrt(gamma);
     PUSH_HIST(rNorm);
     st->inconsistent = 0; st->breakdown = 0;
@@ -989,8 +1007,8 @@ int oc_cg(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_kryl
         const double eps_ = o->atol + o->rtol * rNorm;
         int solved = rNorm <= eps_, tired = iter >= itmax, zero_curvature = 0, inconsistent = 0;
         while (!(solved || tired || zero_curvature)) {
-            op_apply(A, Ap, p, -1.0);
-            double pAp = oc_dot(n, p, Ap);
+            op_apply(A, Ap, p, dev && A->mode == OC_JV_FD ? sqrt(dr_reduce(A->P, DR_RED, p, NULL, 0)) : -1.0);
+            double pAp = dev ? dr_reduce(A->P, DR_TILES, p, Ap, 0) : oc_dot(n, p, Ap);
             if (pAp <= DBL_EPSILON * pNorm2) {
                 if (fabs(pAp) <= DBL_EPSILON * pNorm2) { zero_curvature = 1; inconsistent = 1; }
             }
@@ -999,7 +1017,7 @@ int oc_cg(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_kryl
             oc_axpy(n, alpha, p, x);
             oc_axpy(n, -alpha, Ap, r);
             if (M) prec_apply(A, M, zr, r);
-            double gamma_next = oc_dot(n, r, zr);
+            double gamma_next = dev ? dr_reduce(A->P, DR_RED, r, NULL, 0) : oc_dot(n, r, zr);
             rNorm = sqrt(gamma_next);
             PUSH_HIST(rNorm);
             int mach = (rNorm + 1.0 <= 1.0);
@@ -1047,7 +1065,7 @@ int oc_newton_krylov(const oc_problem* P, double* u, const oc_newton_opts* o, oc
     /* OC_DEVRED (GMRES / FGMRES without preconditioners): the device driver's norms in its order --
      * ||F(u)|| from the residual kernel's tiles (nk_residual_norm), ||u|| from the update fused into the
      * solve's last x update (k_update_x's wide chunks; k_sumsq before the first solve) */
-    const int dev = dr_on(P) && o->precond == OC_PRECOND_NONE && o->mprecond == OC_PRECOND_NONE && o->algo != OC_ALGO_CG;
+    const int dev = dr_on(P) && o->precond == OC_PRECOND_NONE && o->mprecond == OC_PRECOND_NONE;
     double unorm_dev = 0.0;
     oc_residual(P, res, u);
     nres_count++;
@@ -1103,7 +1121,7 @@ int oc_newton_krylov(const oc_problem* P, double* u, const oc_newton_opts* o, oc
         OC_DEV_BNORM = 0.0;
         oc_axpy(n, -1.0, d, u); /* u .-= 1 .* d */
         /* device: fused into the last cycle's x update (wide chunks); no cycle ran: k_axpy_sumsq (red_blocks) */
-        if (dev) unorm_dev = sqrt(dr_reduce(P, ks.niter > 0 ? DR_WIDE : DR_RED, u, NULL, 0));
+        if (dev) unorm_dev = sqrt(dr_reduce(P, ks.niter > 0 && o->algo != OC_ALGO_CG ? DR_WIDE : DR_RED, u, NULL, 0));
         double n_prior = n_res;
         oc_residual(P, res, u);
         nres_count++;

@@ -9,6 +9,8 @@ drifting apart by summation order (1e-8 over 15 restarts in the default mode).
 
 Tolerance: none (np.array_equal).  Hardware parameter: the sweep grid is the GPU's CU count, read from
 the device's own path report and handed to the oracle."""
+import os
+
 import numpy as np
 import pytest
 
@@ -115,3 +117,27 @@ def test_newton_bitwise_in_device_order(ctx, kind, nx, ny, kw):
     assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
     np.testing.assert_array_equal(np.array(hist), so["n_res_history"])
     np.testing.assert_array_equal(ud.to_numpy(), uo)
+
+
+def test_config1_newton_cg_bitwise_in_device_order(ctx, golden_dir):
+    """BASELINE config 1 (examples/bratu.jl:59-63: 1D Bratu N = 1000, algo = :cg, exact JVP) against the oracle
+    in the device's order (k_st1d's 256-point partials, k_sumsq / k_cg_update's chunks): thousands of CG
+    iterations on cond(J) ~ 1.75e8, whose counts move by ~9 % under a 1-ulp change of u0 in the default
+    order (test_hip.py::test_newton_bratu1d_cg_config1 compares only the outcome there) -- here equal outer /
+    inner counts and u bit for bit."""
+    g = np.load(os.path.join(golden_dir, "bratu1d_n1000.npz"))
+    P = oc.bratu1d(1000)
+    u = ah.DeviceArray.from_numpy(g["u0"], None, ctx)
+    hist = []
+    u, r = ah.newton_krylov_(ah.bratu_, u, (P.hx, P.lam), u.similar(), algo="cg",
+                             callback=lambda u_, res_, n: hist.append(n))
+    oc.set_devred(True)
+    try:
+        uo, so = oc.newton_krylov(P, g["u0"], algo="cg")
+    finally:
+        oc.set_devred(False)
+    assert r.solved and so["solved"]
+    assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
+    np.testing.assert_array_equal(np.array(hist), so["n_res_history"])
+    np.testing.assert_array_equal(u.to_numpy(), uo)
+    assert np.max(np.abs(uo - g["true_sol"])) < 3e-4
