@@ -7,7 +7,7 @@ T=${1:-check}
 OUT=gpurun_out/check_$T
 mkdir -p "$OUT"
 echo "[check] gpu suite"
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/gputest.log" 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/gputest.log" 2>&1
 tail -n 2 "$OUT/gputest.log"
 echo "[check] smoke"
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
