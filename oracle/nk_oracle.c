@@ -446,6 +446,21 @@ void oc_dr_chunk_parts(int64_t n, const double* x, const double* y, int64_t G, d
         parts[b] = dr_block(acc);
     }
 }
+/* k_cg_update's partials: the same chunks over the n SCALAR elements (NK_CHUNKED(i, n), nk_precond.hip) */
+static double dr_chunk1(int64_t n, const double* x, const double* y, int64_t G) {
+    if (!y) y = x;
+    const int64_t per = ((n + G - 1) / G + 255) / 256 * 256;
+    double* parts = (double*)malloc(sizeof(double) * (size_t)G);
+    for (int64_t b = 0; b < G; ++b) {
+        double acc[256] = {0.0};
+        const int64_t lo = b * per, hi = lo + per < n ? lo + per : n;
+        for (int64_t i = lo; i < hi; ++i) acc[(i - lo) & 255] = fma(x[i], y[i], acc[(i - lo) & 255]);
+        parts[b] = dr_block(acc);
+    }
+    const double r = oc_dr_ri(parts, G);
+    free(parts);
+    return r;
+}
 static double dr_chunk(int64_t n, const double* x, const double* y, int64_t G) {
     double* parts = (double*)malloc(sizeof(double) * (size_t)G);
     oc_dr_chunk_parts(n, x, y, G, parts);
@@ -593,7 +608,7 @@ static int dr_on(const oc_problem* P) {
     (void)P;
     return OC_DEVRED;
 }
-enum { DR_RED = 0, DR_WIDE = 1, DR_TILES = 2, DR_PASS = 3 };
+enum { DR_RED = 0, DR_WIDE = 1, DR_TILES = 2, DR_PASS = 3, DR_RED1 = 4 };
 /* one reduction of sum x_i y_i (y NULL: x_i^2) over the global grid, as the ranks compute it: each rank its
  * block's tree (DR_RED: k_sumsq / k_dot over red_blocks; DR_WIDE: k_update_x's wide_blocks; DR_TILES: the
  * stencil's tiles; DR_PASS: an MGS pass of an np-pass step -- the resident sweep where it runs, else
@@ -632,6 +647,7 @@ static double dr_reduce(const oc_problem* P, int kind, const double* x, const do
         double v;
         if (kind == DR_TILES) v = dr_tiles_local(dim, m[0], m[1], m[2], blk, xs, ys);
         else if (kind == DR_WIDE) v = dr_chunk(nl, xs, ys, dr_wide_blocks(nl));
+        else if (kind == DR_RED1) v = dr_chunk1(nl, xs, ys, dr_red_blocks(nl));
         else if (kind == DR_PASS && OC_DEV_RESIDENT && dr_sweep_applies(nl, np)) v = dr_sweep(nl, xs, ys ? ys : xs);
         else v = dr_chunk(nl, xs, ys, dr_red_blocks(nl));
         total = R > 1 ? total + v : v;
@@ -1017,7 +1033,7 @@ int oc_cg(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_kryl
             oc_axpy(n, alpha, p, x);
             oc_axpy(n, -alpha, Ap, r);
             if (M) prec_apply(A, M, zr, r);
-            double gamma_next = dev ? dr_reduce(A->P, DR_RED, r, NULL, 0) : oc_dot(n, r, zr);
+            double gamma_next = dev ? dr_reduce(A->P, DR_RED1, r, NULL, 0) : oc_dot(n, r, zr);  /* (k_cg_update) */
             rNorm = sqrt(gamma_next);
             PUSH_HIST(rNorm);
             int mach = (rNorm + 1.0 <= 1.0);
