@@ -603,12 +603,18 @@ static double dr_sweep(int64_t n, const double* x, const double* y) {
     oc_dr_sweep_parts(n, x, y, G, parts);
     return oc_dr_poll1(parts, G);
 }
-/* devred applies to GMRES / FGMRES / CG without preconditioners (the paths the tests compare) */
+/* devred applies to GMRES / FGMRES / CG, preconditioned or not (Jacobi, ILU(0), the GMRES preconditioner) */
 static int dr_on(const oc_problem* P) {
     (void)P;
     return OC_DEVRED;
 }
 enum { DR_RED = 0, DR_WIDE = 1, DR_TILES = 2, DR_PASS = 3, DR_RED1 = 4 };
+static double dr_reduce(const oc_problem* P, int kind, const double* x, const double* y, int np);
+/* ||z||^2 of z = N v as apply_precond (nk_krylov.cpp) sums it: fused into k_diag_apply's scalar chunks for a
+ * diagonal N, k_sumsq after the ILU(0) solve / the inner GMRES */
+static double dr_prec_norm2(const oc_problem* P, const oc_precond* N, const double* z) {
+    return dr_reduce(P, N->kind == OC_PRECOND_DIAG ? DR_RED1 : DR_RED, z, NULL, 0);
+}
 /* one reduction of sum x_i y_i (y NULL: x_i^2) over the global grid, as the ranks compute it: each rank its
  * block's tree (DR_RED: k_sumsq / k_dot over red_blocks; DR_WIDE: k_update_x's wide_blocks; DR_TILES: the
  * stencil's tiles; DR_PASS: an MGS pass of an np-pass step -- the resident sweep where it runs, else
@@ -815,14 +821,19 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
     double* z = (double*)calloc((size_t)cap, sizeof(double));
     double* R = (double*)calloc((size_t)cap * (cap + 1) / 2, sizeof(double));
 
-    /* OC_DEVRED: every reduction in the device's order (nk_krylov.cpp gmres, no preconditioner) */
-    const int dev = dr_on(A->P) && !N && !M;
+    /* OC_DEVRED: every reduction in the device's order (nk_krylov.cpp gmres) */
+    const int dev = dr_on(A->P);
+    const double bnorm_dev = OC_DEV_BNORM; /* the caller's ||b||, for this solve only (not an inner GMRES's) */
+    OC_DEV_BNORM = 0.0;
     double xnorm_dev = 0.0; /* ||x|| of the last cycle's update (k_update_x partials), the restart's FD step */
     oc_fill(n, x, 0.0);
     oc_copy(n, w, b); /* w = b - A*0 */
     if (M) prec_apply(A, M, r0, w); /* r0 = M w */
-    /* device: the Newton loop hands ||F(u)|| over as ||b|| (nk_krylov_opts.b_norm), else k_sumsq + k_finalize */
-    double beta = dev ? (OC_DEV_BNORM > 0.0 ? OC_DEV_BNORM : sqrt(dr_reduce(A->P, DR_RED, r0, NULL, 0))) : oc_norm(n, r0);
+    /* device: the Newton loop hands ||F(u)|| over as ||b|| (nk_krylov_opts.b_norm), else k_sumsq + k_finalize;
+     * with M, ||M b|| from apply_precond */
+    double beta = !dev ? oc_norm(n, r0)
+                  : M ? sqrt(dr_prec_norm2(A->P, M, r0))
+                  : (bnorm_dev > 0.0 ? bnorm_dev : sqrt(dr_reduce(A->P, DR_RED, r0, NULL, 0)));
     double rNorm = beta;
     PUSH_HIST(rNorm);
     const double eps_ = o->atol + o->rtol * rNorm;
@@ -854,7 +865,8 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
             }
             /* device: the first cycle keeps beta; a restart's ||b - A x|| is the fused EPI_RESID stencil's */
             if (!dev) beta = oc_norm(n, r0);
-            else if (restart && npass >= 1) beta = sqrt(dr_reduce(A->P, DR_TILES, r0, NULL, 0));
+            else if (restart && npass >= 1)
+                beta = M ? sqrt(dr_prec_norm2(A->P, M, r0)) : sqrt(dr_reduce(A->P, DR_TILES, r0, NULL, 0));
             z[0] = beta;
             /* kdivcopy!(n, V[1], r0, rNorm): Krylov.jl divides by rNorm -- beta on the first pass, after a
              * restart the previous cycle's estimate |zeta|, not the beta just computed */
@@ -874,12 +886,10 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
                     R = (double*)xrealloc(R, sizeof(double) * nR); memset(R + oR, 0, sizeof(double) * (nR - oR));
                     cap = ncap;
                 }
-                if (flex) {
-                    prec_apply(A, N, Z[k - 1], V[k - 1]);
-                    op_apply(A, w, Z[k - 1], -1.0);
-                } else if (N) {
-                    prec_apply(A, N, pv, V[k - 1]);
-                    op_apply(A, w, pv, -1.0);
+                if (N) { /* the FD step's ||N V_k||: apply_precond's reduction on the device */
+                    double* zk = flex ? Z[k - 1] : pv;
+                    prec_apply(A, N, zk, V[k - 1]);
+                    op_apply(A, w, zk, dev && A->mode == OC_JV_FD ? sqrt(dr_prec_norm2(A->P, N, zk)) : -1.0);
                 } else {
                     /* ||V_1|| = beta / rNorm (1 on the first cycle, |r0| / |zeta| after a restart) */
                     op_apply(A, w, V[k - 1], k == 1 ? beta / rNorm : 1.0);
@@ -891,7 +901,7 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
                      * the partials of <V_next, q> (<q, q> after the last): the resident sweep's slot partition
                      * and polling wave, or (one pass, or not resident) k_mgs_pass's chunks + reduce_input */
                     const int np = reorth ? 2 * k : k;
-                    double h = dr_reduce(A->P, DR_TILES, V[0], q, 0);
+                    double h = dr_reduce(A->P, M ? DR_RED : DR_TILES, V[0], q, 0);  /* with M: k_dot after M */
                     for (int t = 0; t < np; ++t) {
                         const int i = t % k;
                         if (t < k) R[nr + i] = h;
@@ -963,7 +973,8 @@ int oc_gmres(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_k
             }
             if (restart) oc_axpy(n, 1.0, xr, x);
             /* device: ||x|| from the x update's partials (k_update_x over wide_blocks, k_finalize) */
-            if (dev && restart && A->mode == OC_JV_FD) xnorm_dev = sqrt(dr_reduce(A->P, DR_WIDE, x, NULL, 0));
+            if (dev && restart && A->mode == OC_JV_FD) /* gmres! with N: k_sumsq after x += N (V y) */
+                xnorm_dev = sqrt(dr_reduce(A->P, N && !flex ? DR_RED : DR_WIDE, x, NULL, 0));
             iter += inner_iter;
             inner_itmax = itmax - iter;
             tired = iter >= itmax;
@@ -1008,10 +1019,11 @@ int oc_cg(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_kryl
     oc_copy(n, r, b);
     if (M) prec_apply(A, M, zr, r);
     oc_copy(n, p, zr);
-    /* OC_DEVRED (no preconditioner): <r, r> from k_sumsq / k_cg_update's chunks, <p, Ap> from the stencil's
-     * tiles, ||p|| (the FD step) from k_sumsq (nk_krylov.cpp cg) */
-    const int dev = dr_on(A->P) && !M;
-    double gamma = dev ? dr_reduce(A->P, DR_RED, r, NULL, 0) : oc_dot(n, r, zr);
+    /* OC_DEVRED: <r, r> from k_sumsq / k_cg_update's chunks (<r, z> from k_dot with M), <p, Ap> from the
+     * stencil's tiles, ||p|| (the FD step) from k_sumsq (nk_krylov.cpp cg) */
+    const int dev = dr_on(A->P);
+    OC_DEV_BNORM = 0.0; /* the device CG sums ||b|| itself (and an inner GMRES preconditioner must not take it) */
+    double gamma = dev ? dr_reduce(A->P, DR_RED, r, M ? zr : NULL, 0) : oc_dot(n, r, zr);
     double rNorm = sqrt(gamma);
     PUSH_HIST(rNorm);
     st->inconsistent = 0; st->breakdown = 0;
@@ -1033,7 +1045,9 @@ int oc_cg(oc_op* A, const double* b, double* x, const oc_krylov_opts* o, oc_kryl
             oc_axpy(n, alpha, p, x);
             oc_axpy(n, -alpha, Ap, r);
             if (M) prec_apply(A, M, zr, r);
-            double gamma_next = dev ? dr_reduce(A->P, DR_RED1, r, NULL, 0) : oc_dot(n, r, zr);  /* (k_cg_update) */
+            double gamma_next = !dev ? oc_dot(n, r, zr)
+                                : M ? dr_reduce(A->P, DR_RED, r, zr, 0)  /* k_dot after z = M r */
+                                    : dr_reduce(A->P, DR_RED1, r, NULL, 0);  /* (k_cg_update) */
             rNorm = sqrt(gamma_next);
             PUSH_HIST(rNorm);
             int mach = (rNorm + 1.0 <= 1.0);
@@ -1078,10 +1092,10 @@ int oc_newton_krylov(const oc_problem* P, double* u, const oc_newton_opts* o, oc
     double* minv = (o->mprecond == OC_PRECOND_JACOBI || o->mprecond == OC_PRECOND_ILU) ? (double*)malloc(sizeof(double) * n) : NULL;
     oc_op A = {P, o->jv_mode, u, res, 0.0, 0};
     int64_t nres_count = 0;
-    /* OC_DEVRED (GMRES / FGMRES without preconditioners): the device driver's norms in its order --
-     * ||F(u)|| from the residual kernel's tiles (nk_residual_norm), ||u|| from the update fused into the
-     * solve's last x update (k_update_x's wide chunks; k_sumsq before the first solve) */
-    const int dev = dr_on(P) && o->precond == OC_PRECOND_NONE && o->mprecond == OC_PRECOND_NONE;
+    /* OC_DEVRED: the device driver's norms in its order -- ||F(u)|| from the residual kernel's tiles
+     * (nk_residual_norm), ||u|| from the update fused into the solve's last x update (k_update_x's wide
+     * chunks; k_sumsq before the first solve; k_axpy_sumsq where the update is not fused) */
+    const int dev = dr_on(P);
     double unorm_dev = 0.0;
     oc_residual(P, res, u);
     nres_count++;
@@ -1136,8 +1150,10 @@ int oc_newton_krylov(const oc_problem* P, double* u, const oc_newton_opts* o, oc
         else oc_gmres(&A, res, d, &ko, &ks, NULL, 0, NULL);
         OC_DEV_BNORM = 0.0;
         oc_axpy(n, -1.0, d, u); /* u .-= 1 .* d */
-        /* device: fused into the last cycle's x update (wide chunks); no cycle ran: k_axpy_sumsq (red_blocks) */
-        if (dev) unorm_dev = sqrt(dr_reduce(P, ks.niter > 0 && o->algo != OC_ALGO_CG ? DR_WIDE : DR_RED, u, NULL, 0));
+        /* device: fused into the last cycle's x update (wide chunks); no cycle ran, CG, or gmres! with N
+         * (x = N (V y) after the update): k_axpy_sumsq (red_blocks) */
+        const int fused = ks.niter > 0 && o->algo != OC_ALGO_CG && !(ko.N && o->algo != OC_ALGO_FGMRES);
+        if (dev) unorm_dev = sqrt(dr_reduce(P, fused ? DR_WIDE : DR_RED, u, NULL, 0));
         double n_prior = n_res;
         oc_residual(P, res, u);
         nres_count++;
