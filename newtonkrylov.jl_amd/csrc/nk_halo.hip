@@ -61,12 +61,18 @@ __global__ void k_mb_test(unsigned epoch, double value, double* out) {
 
 namespace {
 
+// One wait for a batch of loads (vmcnt(0) lgkmcnt(0), gfx9 encoding).  Without it the waitcnt pass puts a
+// full vmcnt(0) before EACH of the predicated stores that follow (its count is lost at their join points):
+// six serialised store acknowledgements -- over fine-grained memory about a microsecond each.
+__device__ __forceinline__ void wait_loads() { __builtin_amdgcn_s_waitcnt(0x0070); }
+
 // Ghost planes through the peers' inboxes (IPC-mapped fine-grained memory over xGMI).  Block b
 // owns chunk b of the plane: it pushes my boundary-plane chunks into the lower / upper
 // neighbour's inbox (system-scope stores), drains, raises its epoch flag there, then waits for the
 // neighbours' block b flags in my region and copies their chunks into my ghost planes.  Inboxes
 // alternate by epoch parity: epoch e's push can only start after the neighbour finished epoch e-2.
 // ring = 1 (bc_periodic! along the slab axis): rank 0's lower neighbour is rank nranks-1 and vice versa.
+// Both sides' loads of an element round are issued before its stores (one memory latency per round).
 __global__ __launch_bounds__(kBlock) void k_halo_ipc(double* __restrict__ v, int64_t plane, int64_t nplanes,
                                                     uint64_t epoch, int64_t cap, int ring) {
     __shared__ int ready;
@@ -78,15 +84,14 @@ __global__ __launch_bounds__(kBlock) void k_halo_ipc(double* __restrict__ v, int
     const int64_t c0 = (int64_t)b * per, c1 = c0 + per < plane ? c0 + per : plane;
     const double* first = v;
     const double* last = v + (nplanes - 1) * plane;
-    if (lo) {  // my first interior plane -> the lower rank's "from upper" inbox
-        uint64_t* dst = halo_inbox(g_mb.peers[rlo], par, 1, cap);
-        for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
-            __hip_atomic_store(dst + i, (uint64_t)__double_as_longlong(first[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    if (hi) {  // my last interior plane -> the upper rank's "from lower" inbox
-        uint64_t* dst = halo_inbox(g_mb.peers[rhi], par, 0, cap);
-        for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
-            __hip_atomic_store(dst + i, (uint64_t)__double_as_longlong(last[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // my first interior plane -> the lower rank's "from upper" inbox, my last -> the upper rank's "from lower"
+    uint64_t* dlo = lo ? halo_inbox(g_mb.peers[rlo], par, 1, cap) : nullptr;
+    uint64_t* dhi = hi ? halo_inbox(g_mb.peers[rhi], par, 0, cap) : nullptr;
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock) {
+        const double a = lo ? first[i] : 0.0, z = hi ? last[i] : 0.0;
+        wait_loads();
+        if (lo) __hip_atomic_store(dlo + i, (uint64_t)__double_as_longlong(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (hi) __hip_atomic_store(dhi + i, (uint64_t)__double_as_longlong(z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every thread drains its stores before the flag
     __syncthreads();
@@ -106,16 +111,14 @@ __global__ __launch_bounds__(kBlock) void k_halo_ipc(double* __restrict__ v, int
     }
     __syncthreads();
     if (!ready) return;
-    if (lo) {
-        const uint64_t* src = halo_inbox(g_mb.self, par, 0, cap);
-        for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
-            v[i - plane] = __longlong_as_double((long long)__hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-    }
-    if (hi) {
-        const uint64_t* src = halo_inbox(g_mb.self, par, 1, cap);
-        for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
-            v[nplanes * plane + i] =
-                __longlong_as_double((long long)__hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    const uint64_t* slo = halo_inbox(g_mb.self, par, 0, cap);
+    const uint64_t* shi = halo_inbox(g_mb.self, par, 1, cap);
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock) {
+        const uint64_t a = lo ? __hip_atomic_load(slo + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0;
+        const uint64_t z = hi ? __hip_atomic_load(shi + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0;
+        wait_loads();
+        if (lo) v[i - plane] = __longlong_as_double((long long)a);
+        if (hi) v[nplanes * plane + i] = __longlong_as_double((long long)z);
     }
 }
 
@@ -155,14 +158,28 @@ __global__ __launch_bounds__(kBlock) void k_faces_ipc(double* __restrict__ v, Fa
     __shared__ int ready;
     const int b = blockIdx.x, G = gridDim.x;
     const int par = (int)(epoch & 1);
+    // my chunk [c0, c1) of each face (empty where no neighbour); an element round issues the loads of all six
+    // faces before any store -- one memory latency per round instead of one per face
+    int64_t c0[kHaloSides], c1[kHaloSides], per_max = 0;
+    uint64_t* dst[kHaloSides];
+#pragma unroll
     for (int s = 0; s < kHaloSides; ++s) {
-        if (F.nbr[s] < 0) continue;
-        const int64_t len = face_len(F, s), per = (len + G - 1) / G;
-        const int64_t c0 = (int64_t)b * per, c1 = c0 + per < len ? c0 + per : len;
-        uint64_t* dst = halo_inbox(g_mb.peers[F.nbr[s]], par, s ^ 1, cap);
-        for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
-            __hip_atomic_store(dst + i, (uint64_t)__double_as_longlong(v[face_src(F, s, i)]), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
+        const int64_t len = F.nbr[s] >= 0 ? face_len(F, s) : 0, per = (len + G - 1) / G;
+        c0[s] = (int64_t)b * per;
+        c1[s] = c0[s] + per < len ? c0[s] + per : len;
+        per_max = per > per_max ? per : per_max;
+        dst[s] = F.nbr[s] >= 0 ? halo_inbox(g_mb.peers[F.nbr[s]], par, s ^ 1, cap) : nullptr;
+    }
+    for (int64_t o = threadIdx.x; o < per_max; o += kBlock) {
+        double val[kHaloSides];
+#pragma unroll
+        for (int s = 0; s < kHaloSides; ++s) val[s] = c0[s] + o < c1[s] ? v[face_src(F, s, c0[s] + o)] : 0.0;
+        wait_loads();
+#pragma unroll
+        for (int s = 0; s < kHaloSides; ++s)
+            if (c0[s] + o < c1[s])
+                __hip_atomic_store(dst[s] + c0[s] + o, (uint64_t)__double_as_longlong(val[s]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every thread drains its stores before the flags
     __syncthreads();
@@ -185,13 +202,18 @@ __global__ __launch_bounds__(kBlock) void k_faces_ipc(double* __restrict__ v, Fa
     }
     __syncthreads();
     if (!ready) return;
-    for (int s = 0; s < kHaloSides; ++s) {
-        if (F.nbr[s] < 0) continue;
-        const int64_t len = face_len(F, s), per = (len + G - 1) / G;
-        const int64_t c0 = (int64_t)b * per, c1 = c0 + per < len ? c0 + per : len;
-        const uint64_t* src = halo_inbox(g_mb.self, par, s, cap);
-        for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock)
-            v[face_dst(F, s, i)] = __longlong_as_double((long long)__hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    const uint64_t* src[kHaloSides];  // hoisted: the stores into v below could alias g_mb for the compiler
+#pragma unroll
+    for (int s = 0; s < kHaloSides; ++s) src[s] = halo_inbox(g_mb.self, par, s, cap);
+    for (int64_t o = threadIdx.x; o < per_max; o += kBlock) {
+        uint64_t val[kHaloSides];
+#pragma unroll
+        for (int s = 0; s < kHaloSides; ++s)
+            val[s] = c0[s] + o < c1[s] ? __hip_atomic_load(src[s] + c0[s] + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0;
+        wait_loads();
+#pragma unroll
+        for (int s = 0; s < kHaloSides; ++s)
+            if (c0[s] + o < c1[s]) v[face_dst(F, s, c0[s] + o)] = __longlong_as_double((long long)val[s]);
     }
 }
 
