@@ -256,6 +256,17 @@ __device__ __forceinline__ void publish(double acc, double* part, int fin, doubl
 __device__ __forceinline__ double lap(double c, double p, double m, double h2) { return ((p - 2.0 * c) + m) / h2; }
 
 // ------------------------------------------------------------------------------ peer ghost planes
+// One wait for a batch of loads (vmcnt(0) lgkmcnt(0), gfx9 encoding).  The exchanges load a round of
+// elements, wait once, then store them all: a load issued after a system-scope store can only be waited
+// for together with that store's acknowledgement (one in-order vmcnt), so a load -> store loop pays one
+// store round trip per element -- over fine-grained memory about a microsecond each.  (Without the explicit
+// wait the waitcnt pass also loses the count at the predicated stores' join points and waits before each.)
+__device__ __forceinline__ void wait_loads() { __builtin_amdgcn_s_waitcnt(0x0070); }
+// elements per thread per exchange round: a 2D slab tile's patch (one 512-column row) is 2 per thread; a 3D
+// block tile's y patch 8 (two rounds).  The 3D slab tiles keep one element per round (R = 1): the batch's
+// registers pushed the config-5 slab Jv (k_st3l at its 128-VGPR cap) into a spill reload inside the march.
+constexpr int kXchgRound = 2, kXchgRoundBlk = 4;
+
 __device__ __forceinline__ uint64_t* halo_flags(uint64_t* base) { return base + kMbWords; }
 __device__ __forceinline__ uint64_t* halo_tile_flags(uint64_t* base, int par, int side) {
     return base + kMbWords + (size_t)2 * kHaloSides * kHaloBlocks + (size_t)(par * kHaloSides + side) * kHaloTileFlags;
@@ -290,6 +301,7 @@ __device__ __forceinline__ double ld_inbox(const uint64_t* p) {
 struct HaloTile {
     int lo, hi;          // this tile needs the lower / upper neighbour's patch
 };
+template <int R = kXchgRound>
 __device__ __forceinline__ bool halo_tile_exchange(const double* __restrict__ v, int64_t plane, int64_t nplanes,
                                                    int64_t nx, int64_t ra, int64_t rb, int64_t ca, int64_t cb, int tile,
                                                    HaloTile t, uint64_t epoch, int64_t cap, int nthreads) {
@@ -302,9 +314,28 @@ __device__ __forceinline__ bool halo_tile_exchange(const double* __restrict__ v,
         const int peer = side == 0 ? (rank + nr - 1) % nr : (rank + 1) % nr;  // (modular: a one-rank self ring, kbench)
         const double* src = side == 0 ? v : v + (nplanes - 1) * plane;
         uint64_t* dst = halo_inbox(g_mb.peers[peer], par, side == 0 ? 1 : 0, cap);
-        for (int64_t q = threadIdx.x; q < cnt; q += nthreads) {
-            const int64_t pos = (ra + q / w) * nx + ca + q % w;
-            __hip_atomic_store(dst + pos, (uint64_t)__double_as_longlong(src[pos]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if constexpr (R == 1) {
+            for (int64_t q = threadIdx.x; q < cnt; q += nthreads) {
+                const int64_t pos = (ra + q / w) * nx + ca + q % w;
+                __hip_atomic_store(dst + pos, (uint64_t)__double_as_longlong(src[pos]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        } else {
+            for (int64_t q0 = threadIdx.x; q0 < cnt; q0 += (int64_t)R * nthreads) {  // rounds: loads, one wait, stores
+                double a[R];
+                int64_t pos[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int64_t q = q0 + (int64_t)r * nthreads;
+                    pos[r] = (ra + q / w) * nx + ca + q % w;
+                    a[r] = q < cnt ? src[pos[r]] : 0.0;
+                }
+                wait_loads();
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (q0 + (int64_t)r * nthreads < cnt)
+                        __hip_atomic_store(dst + pos[r], (uint64_t)__double_as_longlong(a[r]), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every thread drains its stores before the flag

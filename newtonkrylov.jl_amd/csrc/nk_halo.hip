@@ -61,11 +61,6 @@ __global__ void k_mb_test(unsigned epoch, double value, double* out) {
 
 namespace {
 
-// One wait for a batch of loads (vmcnt(0) lgkmcnt(0), gfx9 encoding).  Without it the waitcnt pass puts a
-// full vmcnt(0) before EACH of the predicated stores that follow (its count is lost at their join points):
-// six serialised store acknowledgements -- over fine-grained memory about a microsecond each.
-__device__ __forceinline__ void wait_loads() { __builtin_amdgcn_s_waitcnt(0x0070); }
-
 // Ghost planes through the peers' inboxes (IPC-mapped fine-grained memory over xGMI).  Block b
 // owns chunk b of the plane: it pushes my boundary-plane chunks into the lower / upper
 // neighbour's inbox (system-scope stores), drains, raises its epoch flag there, then waits for the

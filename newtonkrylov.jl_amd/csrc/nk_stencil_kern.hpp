@@ -257,10 +257,21 @@ __device__ bool blk_tile_exchange(const KArgs& A, int tx, int ty, int tz, int64_
         if (!touches(s)) continue;
         uint64_t* dst = halo_inbox(g_mb.peers[nbr(s)], par, s ^ 1, A.hx_cap);
         const int64_t len = plen(s);
-        for (int64_t q = threadIdx.x; q < len; q += nthr) {
-            int64_t f, src;
-            at(s, q, f, src);
-            __hip_atomic_store(dst + f, (uint64_t)__double_as_longlong(v[src]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int64_t q0 = threadIdx.x; q0 < len; q0 += (int64_t)kXchgRoundBlk * nthr) {  // rounds: loads, one wait, stores
+            double a[kXchgRoundBlk];
+            int64_t f[kXchgRoundBlk];
+#pragma unroll
+            for (int r = 0; r < kXchgRoundBlk; ++r) {
+                const int64_t q = q0 + (int64_t)r * nthr;
+                int64_t src;
+                at(s, q, f[r], src);
+                a[r] = q < len ? v[src] : 0.0;
+            }
+            wait_loads();
+#pragma unroll
+            for (int r = 0; r < kXchgRoundBlk; ++r)
+                if (q0 + (int64_t)r * nthr < len)
+                    __hip_atomic_store(dst + f[r], (uint64_t)__double_as_longlong(a[r]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every thread drains its stores before the flags
@@ -287,10 +298,20 @@ __device__ bool blk_tile_exchange(const KArgs& A, int tx, int ty, int tz, int64_
         const uint64_t* src = halo_inbox(g_mb.self, par, s, A.hx_cap);
         const int64_t base = s == 0 ? -pl : s == 1 ? nz * pl : s == 2 ? A.fy : s == 3 ? A.fy + nx * nz : s == 4 ? A.fx : A.fx + ny * nz;
         const int64_t len = plen(s);
-        for (int64_t q = threadIdx.x; q < len; q += nthr) {
-            int64_t f, unused;
-            at(s, q, f, unused);
-            v[base + f] = ld_inbox(src + f);
+        for (int64_t q0 = threadIdx.x; q0 < len; q0 += (int64_t)kXchgRoundBlk * nthr) {
+            double a[kXchgRoundBlk];
+            int64_t f[kXchgRoundBlk];
+#pragma unroll
+            for (int r = 0; r < kXchgRoundBlk; ++r) {
+                const int64_t q = q0 + (int64_t)r * nthr;
+                int64_t unused;
+                at(s, q, f[r], unused);
+                a[r] = q < len ? ld_inbox(src + f[r]) : 0.0;
+            }
+            wait_loads();
+#pragma unroll
+            for (int r = 0; r < kXchgRoundBlk; ++r)
+                if (q0 + (int64_t)r * nthr < len) v[base + f[r]] = a[r];
         }
     }
     __syncthreads();  // the march's loads of these layers follow (same workgroup)
@@ -414,7 +435,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NK_ST3L
         if (ht.lo || ht.hi) {  // block-uniform
             const int64_t ra = (int64_t)ty * NW, rb = ra + NW < ny ? ra + NW : ny;
             const int64_t ca = (int64_t)tx * (64 * VEC), cb = ca + 64 * VEC < nx ? ca + 64 * VEC : nx;
-            if (halo_tile_exchange(A.v, pl, nz, nx, ra, rb, ca, cb, txy, ht, A.hx_epoch, A.hx_cap, 64 * NW)) {
+            if (halo_tile_exchange<1>(A.v, pl, nz, nx, ra, rb, ca, cb, txy, ht, A.hx_epoch, A.hx_cap, 64 * NW)) {
                 const int par = (int)(A.hx_epoch & 1);
                 if (ht.lo) ib_lo = halo_inbox(g_mb.self, par, 0, A.hx_cap);
                 if (ht.hi) ib_hi = halo_inbox(g_mb.self, par, 1, A.hx_cap);
