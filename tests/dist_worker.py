@@ -29,8 +29,9 @@ ap.add_argument("--tol-rel", type=float, default=1e-9, help="Newton tol_rel of t
 ap.add_argument("--krylov-itmax", type=int, default=0,
                 help="> 0: instead of the Newton solve, one restarted GMRES(10) solve J x = F(u0) with this fixed "
                      "budget (atol = rtol = 0); rank 0 saves x and the residual history")
-ap.add_argument("--precond", choices=["none", "ilu0"], default="none",
-                help="with --krylov-itmax: right preconditioner N = ilu0(J) (block Jacobi: each slab factored alone)")
+ap.add_argument("--precond", choices=["none", "ilu0", "jacobi"], default="none",
+                help="with --krylov-itmax: right preconditioner N = ilu0(J) (block Jacobi: each slab factored alone); "
+                     "jacobi: the Newton solve's N factory (1 ./ diag(J), pointwise: the global operator)")
 ap.add_argument("--problem", choices=["bratu", "heat_periodic", "heat3d"], default="bratu",
                 help="heat_periodic: G_Trapezoid! ∘ diffusion! with bc_periodic! -- u_n's ghost planes are "
                      "exchanged too and the slabs form a ring (rank 0 <-> rank world-1)")
@@ -200,6 +201,8 @@ if args.problem == "bratu":
     u0 = np.sin(np.pi * ys)[:, None] * np.sin(np.pi * xs)[None, :]
     F_, p = ah.bratu2d_, (hx, hy, lam)
     kw = dict(memory=10, tol_rel=args.tol_rel, krylov_kwargs=dict(restart=True))
+    if args.precond == "jacobi":
+        kw["N"] = ah.jacobi
 else:
     rng = np.random.default_rng(5)
     un_glob = rng.standard_normal((ny, nx))

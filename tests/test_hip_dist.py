@@ -242,6 +242,32 @@ def test_slabs_match_oracle(tmp_path, world, transport):
         assert meta["path"]["mailbox"] and meta["path"]["mailbox_host"] == (env.get("NK_DIST_MAILBOX") == "host")
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_slabs_jacobi_newton_bitwise_in_device_order(tmp_path, world):
+    """The preconditioned Newton solve on slabs through the mailbox (N = 1 ./ diag(J) per Newton step, FD Jv):
+    every rank's ||N V_k|| from k_diag_apply's scalar chunks over its slab, the ranks' sums in rank order --
+    the oracle in the device's order gives counts, and the root, bit for bit."""
+    out = str(tmp_path / "dist")
+    env = worker_env(world)
+    rc, log = run_ranks(world, [os.path.join(ROOT, "tests", "dist_worker.py"), "--out", out, "--transport", "mailbox",
+                                "--tol-rel", "1e-8", "--precond", "jacobi", "--jv", "fd", "--nx", "96", "--ny", "80"], env)
+    assert rc == 0, log[-3000:]
+    meta = json.load(open(out + ".json"))
+    d = np.load(out + ".npz")
+    assert meta["path"]["mailbox"]
+    P = oc.bratu2d(96, 80)
+    u0 = oc.sin_ic(P)
+    oc.set_devred(True, cus=meta["path"]["resident_blocks"] or 256, ranks=(1, world, 1),
+                  resident=meta["path"]["sweeps_resident"] > 0)
+    try:
+        uo, so = oc.newton_krylov(P, u0, memory=10, restart=True, tol_rel=1e-8, N="jacobi", jv="fd")
+    finally:
+        oc.set_devred(False)
+    assert meta["solved"] and so["solved"]
+    assert (meta["outer"], meta["inner"]) == (so["outer_iterations"], so["inner_iterations"])
+    np.testing.assert_array_equal(d["u"], uo)
+
+
 def test_ilu0_pipeline_timeout_recovers_rank_locally(tmp_path):
     """a pipelined ILU(0) sweep that times out on one rank of a distributed solve must recover on
     that rank alone (the apply redone on the level sweep right away) -- a whole-solve redo on one rank would
