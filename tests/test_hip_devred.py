@@ -253,3 +253,45 @@ def test_newton_preconditioned_config1_bitwise_in_device_order(ctx, N, algo):
     assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
     assert r.n_matvec == so["n_matvec"]
     np.testing.assert_array_equal(u.to_numpy(), ref)
+
+
+# ----------------------------------------------------------------------------- implicit.jl schemes, 2D and 3D
+_G = {"euler": ah.G_Euler_, "midpoint": ah.G_Midpoint_, "trapezoid": ah.G_Trapezoid_}
+_BC = {oc.BC_ZERO: ah.bc_zero_, oc.BC_PERIODIC: ah.bc_periodic_}
+
+
+@pytest.mark.parametrize("scheme,alpha,bc,shape", [
+    ("euler", 0.5, oc.BC_ZERO, (256, 192)),
+    ("trapezoid", 0.5, oc.BC_PERIODIC, (256, 256)),     # k_st2d's periodic instance (square: heat_2D.jl:23-24)
+    ("midpoint", 0.3, oc.BC_ZERO, (130, 67)),           # odd width: one-column (VEC 1) tiles
+    ("euler", 0.5, oc.BC_ZERO, (64, 48, 40)),           # k_st3l's tiles, z-chunks
+    ("midpoint", 0.5, oc.BC_PERIODIC, (48, 48, 48)),
+    ("trapezoid", 0.5, oc.BC_ZERO, (66, 33, 20)),
+])
+def test_scheme_newton_bitwise_in_device_order(ctx, scheme, alpha, bc, shape):
+    """One implicit step of each implicit.jl scheme (G_Euler! / G_Midpoint!(α) / G_Trapezoid! over diffusion!,
+    bc_zero! / bc_periodic!) as the config-3 / config-5 benches run it -- newton_krylov!, tol_abs = 6e-6, FD
+    Jv, unrestarted GMRES(20) with reorthogonalisation -- against the oracle in the device's order: equal
+    counts, the ||F|| history and the step bit for bit, 2D and 3D (test_hip_schemes.py: to 1e-10)."""
+    rng = np.random.default_rng(11)
+    un = rng.standard_normal(shape[::-1])
+    mk = oc.heat2d_euler if len(shape) == 2 else oc.heat3d_euler
+    P = mk(*shape, un=un, scheme=scheme, bc=bc, alpha=alpha)
+    G = _G[scheme](alpha=alpha) if scheme == "midpoint" else _G[scheme]
+    F = G.bind(ah.diffusion_ if P.dim == 2 else ah.diffusion3d_)
+    fp = (P.a, P.hx, P.hy, _BC[bc]) if P.dim == 2 else (P.a, P.hx, P.hy, P.hz, _BC[bc])
+    p = (ah.DeviceArray.from_numpy(un), P.dt, None, fp, 0.0)
+    u0 = un + 0.01 * rng.standard_normal(un.shape)
+    hist = []
+    kw = dict(tol_abs=6e-6, jv="fd", krylov_kwargs=dict(reorthogonalization=True))
+    u, r = ah.newton_krylov_(F, ah.DeviceArray.from_numpy(u0), p, callback=lambda u_, res_, n: hist.append(n), **kw)
+    path = ctx.path_info()
+    oc.set_devred(True, cus=path["resident_blocks"] or 256)
+    try:
+        uo, so = oc.newton_krylov(P, u0, tol_abs=6e-6, jv="fd", reorthogonalization=True)
+    finally:
+        oc.set_devred(False)
+    assert r.solved and so["solved"]
+    assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
+    np.testing.assert_array_equal(np.array(hist), so["n_res_history"])
+    np.testing.assert_array_equal(u.to_numpy(), uo)
