@@ -1,7 +1,7 @@
 """GPU tests of nk_newton_krylov (the Newton loop of src/Ariadne.jl:288-372 inside libnkhip.so, the
 entry point for C / C++ callers).  It issues exactly the library calls the Python host mirror issues,
-so every result must be BIT-IDENTICAL to `newton_krylov_`; against the CPU oracle the bar is the one
-of test_hip.py (equal outer/inner counts, the converged root)."""
+so every result must be BIT-IDENTICAL to `newton_krylov_`; against the CPU oracle: equal outer/inner
+counts, and the root bit for bit in the oracle's device-order mode."""
 import numpy as np
 import pytest
 
@@ -44,14 +44,19 @@ def test_native_newton_bit_identical_to_host_loop(ctx, case):
 
 
 def test_native_newton_cg_bratu1d_matches_oracle(ctx):
-    """Config 1 (examples/bratu.jl:59-63): algo = :cg on 1D Bratu N = 1000."""
+    """Config 1 (examples/bratu.jl:59-63): algo = :cg on 1D Bratu N = 1000 -- against the oracle in the
+    device's reduction order (test_hip_devred.py): equal counts and the root bit for bit."""
     P = oc.bratu1d(1000)
     u0 = oc.sin_ic(P)
-    ref, st = oc.newton_krylov(P, u0, algo="cg")
+    oc.set_devred(True)
+    try:
+        ref, st = oc.newton_krylov(P, u0, algo="cg")
+    finally:
+        oc.set_devred(False)
     u, r = ah.newton_krylov_native(ah.bratu_, ah.DeviceArray.from_numpy(u0), (P.hx, P.lam), algo="cg")
-    assert r.solved == st["solved"]
-    assert r.stats.outer_iterations == st["outer_iterations"]
-    assert r.stats.n_res <= st["tol"]
+    assert r.solved and st["solved"]
+    assert (r.stats.outer_iterations, r.stats.inner_iterations) == (st["outer_iterations"], st["inner_iterations"])
+    np.testing.assert_array_equal(u.to_numpy(), ref)
 
 
 def test_native_newton_heat_step_matches_oracle(ctx):
@@ -65,6 +70,12 @@ def test_native_newton_heat_step_matches_oracle(ctx):
     assert r.solved and st["solved"]
     assert (r.stats.outer_iterations, r.stats.inner_iterations) == (st["outer_iterations"], st["inner_iterations"])
     np.testing.assert_allclose(u.to_numpy(), ref, rtol=0, atol=1e-10 * np.abs(ref).max())
+    oc.set_devred(True)  # and in the device's reduction order: bit for bit
+    try:
+        ref_dev, _ = oc.newton_krylov(P, u0, tol_abs=6e-6, memory=20)
+    finally:
+        oc.set_devred(False)
+    np.testing.assert_array_equal(u.to_numpy(), ref_dev)
 
 
 def test_native_newton_user_residual(ctx):
