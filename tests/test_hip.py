@@ -143,6 +143,15 @@ def test_dot_deterministic(ctx):
 
 
 # ----------------------------------------------------------------------------- Krylov solves
+def devred_solve(P, u, b, cus=256, **kw):
+    """The oracle's solve in the device's reduction order (oracle.set_devred, test_hip_devred.py)."""
+    oc.set_devred(True, cus=cus)
+    try:
+        return oc.krylov_solve(P, u, b, **kw)
+    finally:
+        oc.set_devred(False)
+
+
 def device_solve(P, u, b, **kw):
     F, p = params(P)
     ud, bd = dev(u), dev(b)
@@ -183,6 +192,11 @@ def test_gmres_matches_oracle(ctx, restart, memory, reorth, jv):
         k = ho > 1e-6 * ho[0]
         assert np.allclose(h[k], ho[k], rtol=1e-8, atol=0)
         assert np.max(np.abs(x - xo)) <= 1e-10 * np.max(np.abs(xo))
+    # in the device's reduction order the same restatement is bit for bit
+    xr, sr, hr = devred_solve(P, u, b, jv=jv, F0=F0, memory=memory, **kw)
+    assert sr["niter"] == st.niter
+    np.testing.assert_array_equal(h, hr)
+    np.testing.assert_array_equal(x, xr)
 
 
 @pytest.mark.parametrize("restart,memory", [(True, 10), (False, 20)])
@@ -204,6 +218,9 @@ def test_heat_fd_gmres_matches_oracle(ctx, restart, memory):
     k = ho > 1e-6 * ho[0]
     assert np.allclose(h[k], ho[k], rtol=1e-9, atol=0)
     assert np.max(np.abs(x - xo)) <= 1e-11 * np.max(np.abs(xo))
+    xr, _, hr = devred_solve(P, u, b, jv="fd", F0=F0, memory=memory, **kw)
+    np.testing.assert_array_equal(h, hr)
+    np.testing.assert_array_equal(x, xr)
 
 
 def test_cg_matches_oracle(ctx):
@@ -216,6 +233,9 @@ def test_cg_matches_oracle(ctx):
     m = ho > 1e-6 * ho[0]
     assert np.allclose(np.array(st.residuals)[m], ho[m], rtol=1e-6)
     assert np.max(np.abs(x - xo)) <= 1e-6 * np.max(np.abs(xo))
+    xr, _, hr = devred_solve(P, u, b, algo="cg", atol=1e-12, rtol=1e-10)
+    np.testing.assert_array_equal(np.array(st.residuals), hr)
+    np.testing.assert_array_equal(x, xr)
 
 
 def test_gmres_deterministic(ctx):
