@@ -5,7 +5,8 @@ q = M A (N V_k), and their stopping test measures ||M r||; cg! takes M as its SP
 cross-checked in tests/test_oracle.py; Krylov.jl itself is absent: parity against the reference is
 unpinned beyond the known answer that ILU(0) of the 1D Jacobian is its exact LU, so M = J^-1 and every
 left-preconditioned solve takes one step).  The bar: equal iteration and matvec counts, residual
-histories to 1e-8 relative over the first cycle, solutions to the solve's tolerance.
+histories to 1e-8 relative over the first cycle, solutions to the solve's tolerance -- and, against the
+oracle in the device's reduction order, histories and solutions bit for bit.
 """
 import numpy as np
 import pytest
@@ -33,6 +34,15 @@ def bratu(nx=48, ny=40, seed=4):
     p = (P.hx, P.hy, P.lam)
     ah.bratu2d_(res, u, p)
     return P, u0, u, res, p
+
+
+def devred(fn, *a, **k):
+    """An oracle call in the device's reduction order (oracle.set_devred, test_hip_devred.py)."""
+    oc.set_devred(True)
+    try:
+        return fn(*a, **k)
+    finally:
+        oc.set_devred(False)
 
 
 def solve(J, b, algo, **kw):
@@ -71,6 +81,9 @@ def test_jacobi_left_preconditioned_matches_oracle(ctx, algo, jv):
     assert st.residuals[0] == pytest.approx(np.linalg.norm(d * b), rel=1e-13)  # beta = ||M b||
     np.testing.assert_allclose(st.residuals[:26], ho[:26], rtol=1e-8)
     assert np.linalg.norm(x - xo) <= 1e-6 * np.linalg.norm(xo)
+    xr, _, hr = devred(oc.krylov_solve, P, u0, b, algo=algo, jv=jv, M=("diag", d), **kw)  # device order: bitwise
+    np.testing.assert_array_equal(np.array(st.residuals), hr)
+    np.testing.assert_array_equal(x, xr)
 
 
 def test_left_and_right_preconditioners_together(ctx):
@@ -86,6 +99,9 @@ def test_left_and_right_preconditioners_together(ctx):
     assert st.niter == so["niter"] and st.solved == so["solved"]
     np.testing.assert_allclose(st.residuals[:21], ho[:21], rtol=1e-8)
     assert np.linalg.norm(x - xo) <= 1e-6 * np.linalg.norm(xo)
+    xr, _, hr = devred(oc.krylov_solve, P, u0, b, N=("diag", d), M=("ilu0", D), **kw)
+    np.testing.assert_array_equal(np.array(st.residuals), hr)
+    np.testing.assert_array_equal(x, xr)
 
 
 @pytest.mark.parametrize("algo", ["gmres", "fgmres"])
@@ -123,6 +139,9 @@ def test_preconditioned_cg_matches_oracle(ctx):
     assert st.solved and st.niter == so["niter"]
     np.testing.assert_allclose(st.residuals[:20], ho[:20], rtol=1e-8)
     assert np.linalg.norm(x - xo) <= 1e-6 * np.linalg.norm(xo)
+    xr, _, hr = devred(oc.krylov_solve, P, u0, b, algo="cg", atol=1e-12, rtol=1e-10, M=("diag", mo))
+    np.testing.assert_array_equal(np.array(st.residuals), hr)
+    np.testing.assert_array_equal(x, xr)
 
 
 def test_newton_left_default_atol_stagnates_like_the_oracle(ctx):
@@ -136,6 +155,9 @@ def test_newton_left_default_atol_stagnates_like_the_oracle(ctx):
     assert not r.solved and not so["solved"]
     assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
     assert r.stats.n_res == pytest.approx(so["n_res"], rel=1e-4)  # a stalled iterate: rounding is not damped
+    uo, sd = devred(oc.newton_krylov, P, u0, M="jacobi")  # in the device's order: the same bits
+    assert r.stats.n_res == sd["n_res"]
+    np.testing.assert_array_equal(u.to_numpy(), uo)
 
 
 @pytest.mark.parametrize("M", ["jacobi", "ilu"])
@@ -151,6 +173,8 @@ def test_newton_left_preconditioned_bratu2d_matches_oracle(ctx, M):
     assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
     assert r.n_matvec == so["n_matvec"]
     np.testing.assert_allclose(u.to_numpy(), ref, rtol=0, atol=1e-9 * np.abs(ref).max())
+    uo, _ = devred(oc.newton_krylov, P, u0, M=M, atol=0.0)
+    np.testing.assert_array_equal(u.to_numpy(), uo)
 
 
 def test_newton_left_ilu_bratu1d_config1(ctx, golden_dir):
