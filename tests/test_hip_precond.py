@@ -5,7 +5,7 @@ newton_krylov_.  The oracle restates the same Krylov.jl algorithms (third-party:
 reference itself is unpinned), so the bar is: identity-preconditioned == unpreconditioned bit for
 bit, jacobian_diag == diag(collect(J)) bit for bit, and against the oracle equal iteration counts,
 residual histories to 1e-8 relative over the first cycle, solutions / Newton roots to the solve's
-tolerance.
+tolerance -- and bit for bit against the oracle in the device's reduction order.
 """
 import numpy as np
 import pytest
@@ -33,6 +33,15 @@ def bratu(nx=72, ny=56, seed=4):
     p = (P.hx, P.hy, P.lam)
     ah.bratu2d_(res, u, p)
     return P, u0, u, res, p
+
+
+def devred(fn, *a, cus=256, **k):
+    """An oracle call in the device's reduction order (oracle.set_devred, test_hip_devred.py)."""
+    oc.set_devred(True, cus=cus)
+    try:
+        return fn(*a, **k)
+    finally:
+        oc.set_devred(False)
 
 
 def solve(J, b, algo, N=None, **kw):
@@ -125,6 +134,9 @@ def test_jacobi_preconditioned_matches_oracle(ctx, algo, jv):
     assert st.niter == so["niter"] and st.n_matvec == so["n_matvec"]
     np.testing.assert_allclose(st.residuals[:26], ho[:26], rtol=1e-8)
     assert np.linalg.norm(x - xo) <= 1e-6 * np.linalg.norm(xo)
+    xr, _, hr = devred(oc.krylov_solve, P, u0, b, algo=algo, jv=jv, N=("diag", d), **kw)  # device order: bitwise
+    np.testing.assert_array_equal(np.array(st.residuals), hr)
+    np.testing.assert_array_equal(x, xr)
 
 
 @pytest.mark.parametrize("jv", ["exact", "fd"])
@@ -141,6 +153,9 @@ def test_fgmres_gmres_preconditioner_matches_oracle(ctx, jv):
     assert st.niter == so["niter"] and st.n_matvec == so["n_matvec"]
     np.testing.assert_allclose(st.residuals[:4], ho[:4], rtol=1e-8)
     assert np.linalg.norm(x - xo) <= 1e-6 * np.linalg.norm(xo)
+    xr, _, hr = devred(oc.krylov_solve, P, u0, b, algo="fgmres", jv=jv, N=("gmres", 5), **kw)
+    np.testing.assert_array_equal(np.array(st.residuals), hr)
+    np.testing.assert_array_equal(x, xr)
 
 
 @pytest.mark.parametrize("N,algo", [("jacobi", "gmres"), (("gmres", 5), "fgmres")])
@@ -156,6 +171,8 @@ def test_newton_preconditioned_bratu2d_matches_oracle(ctx, N, algo):
     assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
     assert r.n_matvec == so["n_matvec"]
     np.testing.assert_allclose(u.to_numpy(), ref, rtol=0, atol=1e-9 * np.abs(ref).max())
+    uo, _ = devred(oc.newton_krylov, P, u0, algo=algo, N=N)
+    np.testing.assert_array_equal(u.to_numpy(), uo)
 
 
 @pytest.mark.parametrize("N,algo", [("jacobi", "gmres"), (("gmres", 5), "fgmres")])
@@ -234,6 +251,8 @@ def test_newton_ilu_bratu2d_matches_oracle(ctx):
     assert r.solved and so["solved"]
     assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
     np.testing.assert_allclose(u.to_numpy(), ref, rtol=0, atol=1e-9 * np.abs(ref).max())
+    uo, _ = devred(oc.newton_krylov, P, u0, algo="gmres", N="ilu", memory=30, restart=True)
+    np.testing.assert_array_equal(u.to_numpy(), uo)
 
 
 @pytest.mark.parametrize("algo", ["gmres", "fgmres"])
@@ -244,12 +263,16 @@ def test_jacobi_preconditioned_resident_sweep_matches_oracle(ctx, algo):
     J = ah.JacobianOperator(ah.bratu2d_, res, u, p, jv="exact")
     kw = dict(restart=True, itmax=24, atol=0.0, rtol=0.0, memory=10)
     x, st = solve(J, res, algo, N=ah.jacobi(J), **kw)
+    path = ctx.path_info()
     b = oc.residual(P, u0)
     d = oc.jacobian_diag(P, u0, reciprocal=True)
     xo, so, ho = oc.krylov_solve(P, u0, b, algo=algo, jv="exact", N=("diag", d), **kw)
     assert st.niter == so["niter"] == 24 and st.n_matvec == so["n_matvec"]
     np.testing.assert_allclose(st.residuals, ho, rtol=1e-9)
     assert np.linalg.norm(x - xo) <= 1e-9 * np.linalg.norm(xo)
+    xr, _, hr = devred(oc.krylov_solve, P, u0, b, algo=algo, jv="exact", N=("diag", d), cus=path["resident_blocks"] or 256, **kw)
+    np.testing.assert_array_equal(np.array(st.residuals), hr)  # the resident sweep's tree included
+    np.testing.assert_array_equal(x, xr)
 
 
 # ----------------------------------------------------------------------------- pipelined ILU(0)
