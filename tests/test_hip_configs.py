@@ -124,6 +124,13 @@ def test_config4_slab_gmres_first_steps(ctx):
     # and x, made of the V_k, follows (measured 9.9e-9 relative on the GPU, r04)
     assert np.allclose(np.array(ws.stats.residuals), ho, rtol=1e-11)
     assert np.max(np.abs(x - xo)) <= 5e-8 * np.max(np.abs(xo))
+    oc.set_devred(True, cus=ctx.path_info()["resident_blocks"] or 256)  # the half-resident sweep's own order
+    try:
+        xr, _, hr = oc.krylov_solve(P, ui, F0d, jv="fd", F0=F0d, memory=30, **kw)
+    finally:
+        oc.set_devred(False)
+    np.testing.assert_array_equal(np.array(ws.stats.residuals), hr)
+    np.testing.assert_array_equal(x, xr)
     ws.free()
 
 

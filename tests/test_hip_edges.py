@@ -75,6 +75,13 @@ def test_itmax_cap(ctx, algo):
     assert st.n_matvec == so["n_matvec"]
     np.testing.assert_allclose(st.residuals, ho, rtol=1e-9)
     assert np.linalg.norm(x - xo) <= 1e-9 * np.linalg.norm(xo)
+    oc.set_devred(True)
+    try:
+        xr, _, hr = oc.krylov_solve(P, u0, res.to_numpy(), algo=algo, jv="exact", memory=5, **kw)
+    finally:
+        oc.set_devred(False)
+    np.testing.assert_array_equal(np.array(st.residuals), hr)
+    np.testing.assert_array_equal(x, xr)
 
 
 @pytest.mark.parametrize("nx,ny", [(3, 3), (5, 2), (4, 4)])

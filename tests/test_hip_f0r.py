@@ -144,6 +144,12 @@ def test_newton_uses_it_and_matches_oracle(ctx):
     assert r.solved and so["solved"]
     assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
     np.testing.assert_allclose(u.to_numpy(), ref, rtol=0, atol=1e-8 * np.abs(ref).max())
+    oc.set_devred(True)  # F(u) recomputed or read, the same bits: the device-order oracle's root
+    try:
+        ref_dev, _ = oc.newton_krylov(P, u0, jv="fd", memory=20)
+    finally:
+        oc.set_devred(False)
+    np.testing.assert_array_equal(u.to_numpy(), ref_dev)
 
 
 BRATU_CHILD = r"""

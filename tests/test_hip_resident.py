@@ -63,11 +63,20 @@ def test_resident_sweep_matches_oracle(ctx, nx, ny, reorth):
     b = oc.residual(P, u)
     kw = dict(restart=True, reorthogonalization=reorth, atol=0.0, rtol=0.0, itmax=24)
     x, st = solve(P, u, b, memory=10, **kw)
+    cus = ctx.path_info()["resident_blocks"] or 256
     xo, sto, ho = oc.krylov_solve(P, u, b, jv="exact", memory=10, **kw)
     assert st.niter == sto["niter"] == 24 and st.n_matvec == sto["n_matvec"]
     # the same MGS arithmetic per element; only the order of the partial sums differs
     assert np.allclose(np.array(st.residuals), ho, rtol=1e-9, atol=0)
     assert np.max(np.abs(x - xo)) <= 1e-9 * np.max(np.abs(xo))
+    # and in the sweep's own order (slot partition over the CUs, the polling wave): bit for bit
+    oc.set_devred(True, cus=cus)
+    try:
+        xr, _, hr = oc.krylov_solve(P, u, b, jv="exact", memory=10, **kw)
+    finally:
+        oc.set_devred(False)
+    np.testing.assert_array_equal(np.array(st.residuals), hr)
+    np.testing.assert_array_equal(x, xr)
 
 
 def test_resident_sweep_deterministic(ctx):
@@ -173,6 +182,12 @@ def test_heat2d_step_partly_resident_matches_oracle(ctx):
     assert r.solved and so["solved"]
     assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
     assert np.max(np.abs(un.to_numpy() - ref)) <= 1e-10
+    oc.set_devred(True, cus=ctx.path_info()["resident_blocks"] or 256)  # the partly resident sweep's tree
+    try:
+        ref_dev, _ = oc.newton_krylov(Q, u0.copy(), tol_abs=6e-6)
+    finally:
+        oc.set_devred(False)
+    np.testing.assert_array_equal(un.to_numpy(), ref_dev)
 
 
 def test_closing_a_context_keeps_another_ones_mailbox(monkeypatch):
