@@ -172,6 +172,17 @@ def worker_env(world, **extra):
     return env
 
 
+def devred_call(fn, meta, ranks, *a, **k):
+    """An oracle call in the device's reduction order for the decomposition `ranks` = (px, py, pz) the worker
+    ran (its CU count and whether its sweeps ran resident from the worker's path report)."""
+    oc.set_devred(True, cus=meta["path"]["resident_blocks"] or 256, ranks=ranks,
+                  resident=meta["path"]["sweeps_resident"] > 0)
+    try:
+        return fn(*a, **k)
+    finally:
+        oc.set_devred(False)
+
+
 def check_meta(meta, world):
     if "skip" in meta:
         assert ah.device_count() < world, "RCCL failed although every rank had its own GPU"
@@ -320,6 +331,10 @@ def test_slabs_fd_jv_match_oracle(tmp_path, world, nx, ny, tol):
     assert meta["solved"] and so["solved"] and se["solved"]
     assert meta["outer"] == so["outer_iterations"]
     assert np.max(np.abs(d["u"] - ue)) <= 1e-7 * np.max(np.abs(ue))
+    # the FD solve in the device's order (each rank's trees over its slab, ranks summed in rank order): bitwise
+    uo, sd = devred_call(oc.newton_krylov, meta, (1, world, 1), P, u0, memory=10, restart=True, tol_rel=tol, jv="fd")
+    assert (meta["outer"], meta["inner"]) == (sd["outer_iterations"], sd["inner_iterations"])
+    np.testing.assert_array_equal(d["u"], uo)
 
 
 @pytest.mark.parametrize("transport", ["mailbox", "rccl"])
@@ -347,6 +362,9 @@ def test_periodic_trapezoid_ring_matches_oracle(tmp_path, world, transport):
     assert meta["solved"] and so["solved"]
     assert (meta["outer"], meta["inner"]) == (so["outer_iterations"], so["inner_iterations"])
     assert np.max(np.abs(d["u"] - uo)) <= 1e-10
+    if transport == "mailbox" and meta["path"]["mailbox"]:  # the ring's reductions in the device's order: bitwise
+        ud, _ = devred_call(oc.newton_krylov, meta, (1, world, 1), P, u0, tol_abs=6e-6, reorthogonalization=True)
+        np.testing.assert_array_equal(d["u"], ud)
 
 
 @pytest.mark.parametrize("host", [False, True])
@@ -373,6 +391,10 @@ def test_resident_sweep_two_ranks_one_gpu(tmp_path, host):
     assert meta["niter"] == sto["niter"] == 20 and meta["n_matvec"] == sto["n_matvec"]
     assert np.allclose(d["h"], ho, rtol=1e-9, atol=0)
     assert np.max(np.abs(d["x"] - xo)) <= 1e-9 * np.max(np.abs(xo))
+    # each rank's 128-block sweep tree, the pass scalars added in rank order: bit for bit
+    xr, _, hr = devred_call(oc.krylov_solve, meta, (1, 2, 1), P, u0, F, jv="exact", memory=10, **kw)
+    np.testing.assert_array_equal(d["h"], hr)
+    np.testing.assert_array_equal(d["x"], xr)
 
 
 def test_eight_ranks_256x256_slabs_fd_gmres(tmp_path):
@@ -435,6 +457,8 @@ def test_heat3d_midpoint_zslabs_match_oracle(tmp_path, world, nz):
     assert meta["solved"] and so["solved"]
     assert (meta["outer"], meta["inner"]) == (so["outer_iterations"], so["inner_iterations"])
     assert np.max(np.abs(d["u"] - uo)) <= 1e-10
+    ud, _ = devred_call(oc.newton_krylov, meta, (1, 1, world), P, u0, tol_abs=6e-6, jv="fd")  # z-slabs: bitwise
+    np.testing.assert_array_equal(d["u"], ud)
 
 
 @pytest.mark.parametrize("fuse_max,form", [(20000, "fused"), (10000, "separate"), (5000, "separate")])
