@@ -380,6 +380,12 @@ def test_heat3d_newton(ctx, golden_dir):
     uo, so = oc.newton_krylov(P, g["u"], tol_abs=6e-6)
     assert r.solved and (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
     assert np.max(np.abs(u.to_numpy() - uo)) <= 1e-12
+    oc.set_devred(True)
+    try:
+        ud, _ = oc.newton_krylov(P, g["u"], tol_abs=6e-6)
+    finally:
+        oc.set_devred(False)
+    np.testing.assert_array_equal(u.to_numpy(), ud)
 
 
 # ----------------------------------------------------------------------------- BASELINE size (4096^2)
@@ -412,6 +418,9 @@ def test_bratu2d_4096_full_size(ctx):
     assert st.niter == sto["niter"] == 12
     assert np.allclose(np.array(st.residuals), ho, rtol=1e-8)
     assert np.max(np.abs(x - xo)) <= 1e-8 * np.max(np.abs(xo))
+    xr, _, hr = devred_solve(P, u, F0, cus=ctx.path_info()["resident_blocks"] or 256, jv="fd", F0=F0d, memory=30, **kw)
+    np.testing.assert_array_equal(np.array(st.residuals), hr)  # the resident sweep's tree at 4096^2: bitwise
+    np.testing.assert_array_equal(x, xr)
 
 
 def test_errors_are_reported(ctx):

@@ -110,6 +110,12 @@ def test_scheme_newton_matches_oracle(ctx, scheme, alpha, bc, jv):
     assert r.solved and so["solved"]
     assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
     assert np.max(np.abs(u.to_numpy() - uo)) <= 1e-10
+    oc.set_devred(True)  # in the device's reduction order: bit for bit
+    try:
+        ud, _ = oc.newton_krylov(P, un, tol_abs=6e-6, jv=jv)
+    finally:
+        oc.set_devred(False)
+    np.testing.assert_array_equal(u.to_numpy(), ud)
 
 
 @pytest.mark.parametrize("G,scheme", [(ah.G_Midpoint_, "midpoint"), (ah.G_Trapezoid_, "trapezoid"), (ah.G_Euler_, "euler")])
@@ -132,6 +138,15 @@ def test_solve_timestepping_periodic(ctx, G, scheme):
         assert r.solved and so["solved"]
         assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
     assert np.max(np.abs(un.to_numpy() - cur)) <= 1e-10
+    cur = u0.copy()  # the whole time loop in the device's reduction order: bit for bit
+    oc.set_devred(True)
+    try:
+        for _ in results:
+            cur, _ = oc.newton_krylov(oc.heat2d_euler(N, un=cur, scheme=scheme, bc=oc.BC_PERIODIC), cur, tol_abs=6e-6,
+                                      reorthogonalization=True)
+    finally:
+        oc.set_devred(False)
+    np.testing.assert_array_equal(un.to_numpy(), cur)
 
 
 def test_trapezoid_periodic_eigen_decay_3d(ctx):
