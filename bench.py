@@ -160,6 +160,35 @@ def cpu_thread_probe(affinity, share):
     return best, probe
 
 
+def jv_alone_calibration(W, ctx, reps=20):
+    """BASELINE.md's fused FD Jv as defined there (read u, v, F0; write out: 32 B/pt) -- the `mul!` product
+    k_st2d<…, EPI_NONE> -- timed after the timed region on the workload's own u, F(u) and a basis vector
+    (the Krylov step runs the 40 B/pt form with <V_1, Jv> fused, jv_roofline)."""
+    v = W.ws.basis(1) if hasattr(W.ws, "basis") else None
+    if v is None:
+        v = W.u
+    out = W.u.zero()
+    J = ah.JacobianOperator(ah.bratu2d_, W.res, W.u, W.p, jv="fd")
+    ah.mul_(out, J, v, eps=1e-7)  # warm
+    ctx.sync()
+    ctx.prof_reset()
+    ctx.prof_enable(1)
+    for _ in range(reps):
+        ah.mul_(out, J, v, eps=1e-7)
+    ctx.sync()
+    d = ctx.prof_read().get("jv_fd", {})
+    ctx.prof_enable(0)
+    if not d.get("timed"):
+        return None
+    us = 1e3 * d["ms"] / d["timed"]
+    pts = len(W.u)
+    ach = 32.0 * pts / (us * 1e-6) / 1e9
+    return {"kernel": d.get("kernel"), "avg_us": round(us, 2), "bytes_per_pt": 32, "achieved": round(ach, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "launches": d["timed"],
+            "what": "FD Jv alone (read u, v, F0; write out), BASELINE.md's 32 B/pt definition, HIP events, "
+                    "after the timed region"}
+
+
 def copy_calibration(device, n=1 << 27, reps=5):
     """Achievable HBM streaming rate on this GPU: a plain copy over two 1 GiB vectors (nkb_copy, one 16-B
     element per thread, non-temporal), run after the timed region (GB/s on 16 B per element).  The copy
@@ -744,6 +773,8 @@ def main():
     if rank == 0:
         log("timed steps done; copy calibration")
     copy_gbs = copy_calibration(device) if rank == 0 else None
+    jv_alone = jv_alone_calibration(W, ctx) if (rank == 0 and world == 1 and args.workload == "bratu2d"
+                                                  and args.jv == "fd" and not args.no_prof) else None
 
     # Two byte counts per kernel class (nk_prof_entry): `bytes` = the operand bytes the kernel moves
     # through the memory hierarchy (every load / store it issues, served by L2, the Infinity Cache or
@@ -861,6 +892,7 @@ def main():
             "gbs_dram_model_wholejob": round(world * total_dram / elapsed / 1e9, 1) if total_dram else None,
             "roofline": roof(dominant) if dominant else None,
             "jv_roofline": roof(jv_kernel),
+            "jv_alone": jv_alone,
             "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in list(kernels.items())[:8]},
             "newton_n_res": last.stats.n_res if last else None,
