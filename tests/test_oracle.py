@@ -651,3 +651,36 @@ def test_device_order_gmres_is_a_reordering_only():
     assert np.array_equal(h1, h2) and np.array_equal(x1, x2)
     assert np.allclose(h1, h0, rtol=1e-7, atol=0)
     assert np.max(np.abs(x1 - x0)) <= 1e-7 * np.max(np.abs(x0))
+
+
+@pytest.mark.parametrize("algo,side,kind", [("gmres", "N", "diag"), ("fgmres", "N", "diag"), ("gmres", "M", "diag"),
+                                            ("gmres", "N", "ilu0"), ("fgmres", "N", "gmres"), ("cg", "M", "negdiag")])
+def test_device_order_preconditioned_is_a_reordering_only(algo, side, kind):
+    """The preconditioned paths of the device-order mode (||N V_k||, ||M b||, <V_1, M J V_k>, <r, M r> in their
+    kernels' trees): the same solve as the default mode up to summation order, and deterministic.  OC_DEV_BNORM
+    (the Newton driver's ||F||) is consumed by the outer solve only -- an inner GMRES preconditioner sums its own."""
+    P = oc.bratu2d(64, 48)
+    u0 = oc.sin_ic(P) + 0.05 * np.random.default_rng(4).standard_normal(P.shape)
+    F = oc.residual(P, u0)
+    d = oc.jacobian_diag(P, u0, reciprocal=True)
+    prec = {"diag": ("diag", d), "negdiag": ("diag", -d), "ilu0": ("ilu0", oc.ilu0_factor(P, u0)), "gmres": ("gmres", 5)}[kind]
+    kw = dict(algo=algo, jv="fd", F0=F, memory=20, atol=0.0, rtol=0.0, itmax=40, **{side: prec})
+    if algo != "cg":
+        kw["restart"] = algo == "gmres"
+    x0, s0, h0 = oc.krylov_solve(P, u0, F, **kw)
+    oc.set_devred(True)
+    try:
+        x1, s1, h1 = oc.krylov_solve(P, u0, F, **kw)
+        x2, _, h2 = oc.krylov_solve(P, u0, F, **kw)
+        un, sn = oc.newton_krylov(P, oc.sin_ic(P), algo="fgmres", N=("gmres", 5), jv="fd", memory=20)
+    finally:
+        oc.set_devred(False)
+    assert np.array_equal(h1, h2) and np.array_equal(x1, x2)
+    assert s0["niter"] == s1["niter"] and s0["n_matvec"] == s1["n_matvec"]
+    # an inner GMRES is a nonlinear N: FGMRES carries its summation-order differences forward (7e-6 at step 40)
+    tol = 1e-4 if kind == "gmres" else 1e-6
+    assert np.allclose(h1, h0, rtol=tol, atol=0)
+    assert np.max(np.abs(x1 - x0)) <= tol * np.max(np.abs(x0))
+    ud, sd = oc.newton_krylov(P, oc.sin_ic(P), algo="fgmres", N=("gmres", 5), jv="fd", memory=20)
+    assert sn["solved"] and sd["solved"] and sn["outer_iterations"] == sd["outer_iterations"]
+    assert np.max(np.abs(un - ud)) <= 1e-8 * np.max(np.abs(ud))
