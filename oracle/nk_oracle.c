@@ -384,12 +384,17 @@ static int OC_DEVRED = 0, OC_DEV_CUS = 256, OC_DEV_RL = 39;
  * order as the peer mailbox adds them (mb_recv) */
 static int OC_DEV_PX = 1, OC_DEV_PY = 1, OC_DEV_PZ = 1, OC_DEV_RESIDENT = 1;
 static double OC_DEV_BNORM = 0.0;  /* > 0: the Newton driver's ||F(u)||, which the device solve takes as ||b|| */
+/* the device evaluates the residual as a USER problem (NK_USER*, nk_user.cpp): the callback's F, then
+ * k_user_epi's scalar chunks for every reduction a built-in stencil sums over its tiles */
+static int OC_DEV_USER = 0;
 void oc_set_devred(int on, int cus, int rl) {
     OC_DEVRED = on;
     OC_DEV_CUS = cus > 0 && cus <= 256 ? cus : 256;
     OC_DEV_RL = rl >= 0 ? rl : 39;
     OC_DEV_PX = OC_DEV_PY = OC_DEV_PZ = OC_DEV_RESIDENT = 1;
+    OC_DEV_USER = 0;
 }
+void oc_set_devred_user(int user) { OC_DEV_USER = user != 0; }
 void oc_set_devred_ranks(int px, int py, int pz, int resident) {
     OC_DEV_PX = px > 0 ? px : 1;
     OC_DEV_PY = py > 0 ? py : 1;
@@ -651,7 +656,8 @@ static double dr_reduce(const oc_problem* P, int kind, const double* x, const do
             ys = y ? ly : NULL;
         }
         double v;
-        if (kind == DR_TILES) v = dr_tiles_local(dim, m[0], m[1], m[2], blk, xs, ys);
+        if (kind == DR_TILES && OC_DEV_USER) v = dr_chunk1(nl, xs, ys, dr_red_blocks(nl));  /* k_user_epi */
+        else if (kind == DR_TILES) v = dr_tiles_local(dim, m[0], m[1], m[2], blk, xs, ys);
         else if (kind == DR_WIDE) v = dr_chunk(nl, xs, ys, dr_wide_blocks(nl));
         else if (kind == DR_RED1) v = dr_chunk1(nl, xs, ys, dr_red_blocks(nl));
         else if (kind == DR_PASS && OC_DEV_RESIDENT && dr_sweep_applies(nl, np)) v = dr_sweep(nl, xs, ys ? ys : xs);

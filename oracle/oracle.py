@@ -119,6 +119,7 @@ def lib():
         L.oc_set_chunk.argtypes = [C.c_int64]
         L.oc_set_devred.argtypes = [C.c_int, C.c_int, C.c_int]
         L.oc_set_devred_ranks.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int]
+        L.oc_set_devred_user.argtypes = [C.c_int]
         L.oc_dr_tile_parts3d.argtypes = [I64, I64, I64, C.c_int, P, P, P]
         L.oc_dr_tile_parts3d.restype = I64
         L.oc_get_devred.restype = C.c_int
@@ -363,16 +364,18 @@ def set_chunk(c: int):
     lib().oc_set_chunk(int(c))
 
 
-def set_devred(on: bool, cus: int = 256, rl: int = 39, ranks=(1, 1, 1), resident: bool = True):
+def set_devred(on: bool, cus: int = 256, rl: int = 39, ranks=(1, 1, 1), resident: bool = True, user: bool = False):
     """Sum the 2D / 3D GMRES reductions in exactly the device's order (nk_oracle.c OC_DEVRED): the kernels'
     trees -- wave butterflies, block sums, reduce_input, the chunked streaming kernels, k_st2d's / k_st3l's
     tiles and the resident sweep's slot partition over `cus` blocks (the GPU's CU count) -- so that
     restarted FD-GMRES histories compare bit for bit at any length.  ranks = (px, py, pz): the decomposition
     (3D blocks / z-slabs; 2D slabs are (1, R, 1)), each rank's tree over its own block and the ranks' sums
     added in rank order, as the peer mailbox adds them; resident: whether the ranks' MGS sweeps ran resident
-    (ranks sharing one GPU run the per-pass chain)."""
+    (ranks sharing one GPU run the per-pass chain); user: the device evaluated the residual through a user
+    callback (NK_USER*), whose reductions are k_user_epi's scalar chunks instead of the stencil's tiles."""
     lib().oc_set_devred(int(bool(on)), int(cus), int(rl))
     lib().oc_set_devred_ranks(*(int(t) for t in ranks), int(bool(resident)))
+    lib().oc_set_devred_user(int(bool(user)))  # user: the device ran the problem as a user residual (k_user_epi)
 
 
 def get_devred() -> bool:

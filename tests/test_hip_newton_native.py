@@ -101,3 +101,13 @@ def test_native_newton_user_residual(ctx):
     # the reductions are summed in a different (fixed) order on the two paths; a solve to tol_abs = 6e-6
     # leaves that visible at ~1e-11
     np.testing.assert_allclose(ua.to_numpy(), ub.to_numpy(), rtol=0, atol=1e-9 * np.abs(un).max())
+    # each path bit for bit against the oracle in its own device order: the user residual's reductions are
+    # k_user_epi's scalar chunks (oracle.set_devred(user=True)), the built-in stencil's its tiles
+    for u_dev, r_dev, user in ((ua, ra, True), (ub, rb, False)):
+        oc.set_devred(True, user=user)
+        try:
+            uo, so = oc.newton_krylov(P, un, tol_abs=6e-6, jv="fd")
+        finally:
+            oc.set_devred(False)
+        assert (r_dev.stats.outer_iterations, r_dev.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
+        np.testing.assert_array_equal(u_dev.to_numpy(), uo)
