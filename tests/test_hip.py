@@ -273,6 +273,12 @@ def test_newton_bratu2d_gmres30_golden(ctx, golden_dir):
     assert r.stats.outer_iterations == so["outer_iterations"]
     assert r.stats.inner_iterations == so["inner_iterations"]
     assert np.max(np.abs(u.to_numpy() - g["ustar"])) <= 1e-8 * np.max(np.abs(g["ustar"]))
+    oc.set_devred(True)  # the oracle in the device's reduction order: the root bit for bit
+    try:
+        ud, _ = oc.newton_krylov(P, g["u0"], memory=30, restart=True, tol_rel=1e-10)
+    finally:
+        oc.set_devred(False)
+    np.testing.assert_array_equal(u.to_numpy(), ud)
     # same ||F(u)|| as the CPU path on the same final iterate: F itself is bit-identical, only the
     # norm's summation order differs
     uu = u.to_numpy()
@@ -326,6 +332,13 @@ def test_newton_fd_vs_exact(ctx):
     assert re_.solved and rf.solved
     assert rf.stats.outer_iterations == so["outer_iterations"]
     assert np.max(np.abs(uf.to_numpy() - ue.to_numpy())) <= 1e-8 * np.max(np.abs(ue.to_numpy()))
+    oc.set_devred(True)
+    try:
+        for jv, ud in (("fd", uf), ("exact", ue)):  # each operator's solve bit for bit in the device's order
+            uo, _ = oc.newton_krylov(P, u0, memory=30, restart=True, tol_rel=1e-9, jv=jv)
+            np.testing.assert_array_equal(ud.to_numpy(), uo)
+    finally:
+        oc.set_devred(False)
 
 
 def test_newton_forcing_variants_and_outofplace(ctx):
@@ -337,6 +350,13 @@ def test_newton_forcing_variants_and_outofplace(ctx):
         uo, so = oc.newton_krylov(P, u0, memory=30, restart=True, forcing=name)
         assert r.solved and so["solved"]
         assert r.stats.outer_iterations == so["outer_iterations"]
+        oc.set_devred(True)
+        try:
+            ud, sd = oc.newton_krylov(P, u0, memory=30, restart=True, forcing=name)
+        finally:
+            oc.set_devred(False)
+        assert r.stats.inner_iterations == sd["inner_iterations"]
+        np.testing.assert_array_equal(u.to_numpy(), ud)
     ud = dev(u0)
     u2, r2 = ah.newton_krylov(ah.bratu2d_, ud, p, memory=30, krylov_kwargs=dict(restart=True))
     assert r2.solved and np.array_equal(ud.to_numpy(), u0)  # out-of-place leaves u0 alone
@@ -370,6 +390,14 @@ def test_heat2d_solve_timestepping(ctx):
         assert r.solved and so["solved"]
         assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
     assert np.max(np.abs(un.to_numpy() - cur)) <= 1e-10
+    cur = u0.copy()  # the time loop in the device's reduction order: bit for bit
+    oc.set_devred(True)
+    try:
+        for _ in results:
+            cur, _ = oc.newton_krylov(oc.heat2d_euler(N, un=cur), cur, tol_abs=6e-6)
+    finally:
+        oc.set_devred(False)
+    np.testing.assert_array_equal(un.to_numpy(), cur)
 
 
 def test_heat3d_newton(ctx, golden_dir):

@@ -206,3 +206,9 @@ def test_config5_slab_time_step(ctx):
     assert r.solved and so["solved"]
     assert (r.stats.outer_iterations, r.stats.inner_iterations) == (so["outer_iterations"], so["inner_iterations"])
     assert np.max(np.abs(u.to_numpy() - uo)) <= 1e-10
+    oc.set_devred(True, cus=ctx.path_info()["resident_blocks"] or 256)  # the slab's own reduction trees: bitwise
+    try:
+        ud, _ = oc.newton_krylov(P, u0.copy(), tol_abs=6e-6)
+    finally:
+        oc.set_devred(False)
+    np.testing.assert_array_equal(u.to_numpy(), ud)

@@ -176,6 +176,13 @@ def test_user_bratu_newton_matches_oracle(ctx):
         got = u.to_numpy()
         assert np.linalg.norm(got - ref) <= 1e-8 * np.linalg.norm(ref), F
         assert r.stats.n_res <= st["tol"]
+        oc.set_devred(True, user=F is USER_BRATU)  # each path in its own device order: bit for bit
+        try:
+            ud, sd = oc.newton_krylov(P, u0, jv="fd", memory=20)
+        finally:
+            oc.set_devred(False)
+        assert r.stats.inner_iterations == sd["inner_iterations"], F
+        np.testing.assert_array_equal(got, ud)
 
 
 def test_user_cg_runs_on_user_operator(ctx):
