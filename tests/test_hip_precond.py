@@ -335,5 +335,10 @@ def test_ilu0_preconditioned_gmres_4096(ctx):
     _, sto, ho = oc.krylov_solve(P, u0, F0, memory=30, N=("ilu0", d), **kw)
     assert ws.stats.niter == sto["niter"] == 24
     assert np.allclose(h_ilu, ho, rtol=1e-8)
+    x_ilu = ws.x.to_numpy()
+    xr, _, hr = devred(oc.krylov_solve, P, u0, F0, memory=30, N=("ilu0", d), cus=ctx.path_info()["resident_blocks"] or 256,
+                       **kw)
+    np.testing.assert_array_equal(h_ilu, hr)  # the pipelined ILU(0) sweeps and the resident MGS sweep: bitwise
+    np.testing.assert_array_equal(x_ilu, xr)
     ah.krylov_solve_(ws, J, res, history=True, **kw)  # unpreconditioned, same budget
     assert h_ilu[-1] < np.array(ws.stats.residuals)[-1]
